@@ -1,0 +1,155 @@
+"""Seeded synthetic weights for the AutoVC Generator (no checkpoints are reachable offline).
+
+A counter-based splitmix64 stream per tensor gives bit-identical weights on every host and
+numpy version, so fixtures only need to record the seed.  Bounds follow the reference init
+(SURVEY §8a row a1):
+
+* Conv1d weight: xavier_uniform with gain relu=sqrt(2) for encoder/decoder convs
+  (autovc/auto_encoder/encoder.py:41-45, decoder.py:43-47), tanh=5/3 for postnet 0-3 and
+  linear=1 for postnet 4 (postnet.py:21-47); ConvNorm in net_layers.py:44-45.
+* Linear weight (decoder.linear_projection): xavier_uniform gain 1 (net_layers.py:15-17).
+* Conv/Linear bias: PyTorch default U(+-1/sqrt(fan_in)).
+* LSTM weights and biases: PyTorch default U(+-1/sqrt(H)).
+* BatchNorm: the reference starts at gamma=1, beta=0, running (0, 1).  With
+  ``bn_perturb=True`` (the default for tests/bench) gamma, beta and the running statistics are
+  drawn from small ranges instead so that affine/eval-mode bugs cannot hide behind identities.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+
+_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def _mix(z: np.ndarray) -> np.ndarray:
+    z = (z ^ (z >> np.uint64(30))) * _M1
+    z = (z ^ (z >> np.uint64(27))) * _M2
+    return z ^ (z >> np.uint64(31))
+
+
+def uniform01(seed: int, stream: int, n: int) -> np.ndarray:
+    """n float64 values in [0,1) with 24 random bits each, from (seed, stream)."""
+    with np.errstate(over="ignore"):
+        base = _mix(np.array([(seed * 1_000_003 + stream + 1) & 0xFFFFFFFFFFFFFFFF],
+                             dtype=np.uint64) * _GOLDEN)[0]
+        ctr = np.arange(1, n + 1, dtype=np.uint64) * _GOLDEN + base
+        z = _mix(ctr)
+    return (z >> np.uint64(40)).astype(np.float64) * (1.0 / (1 << 24))
+
+
+def _u(seed, stream, shape, lo, hi) -> np.ndarray:
+    n = int(np.prod(shape)) if len(shape) else 1
+    v = lo + (hi - lo) * uniform01(seed, stream, n)
+    return v.astype(np.float32).reshape(shape)
+
+
+def param_specs(dim_neck=32, dim_emb=256, dim_pre=512):
+    """(name, shape, kind, extra) in the reference state_dict order."""
+    specs = []
+    gain_relu, gain_tanh, gain_lin = math.sqrt(2.0), 5.0 / 3.0, 1.0
+
+    def conv(prefix, cin, cout, gain):
+        specs.append((prefix + ".0.conv.weight", (cout, cin, 5), "xavier", (gain, cin * 5, cout * 5)))
+        specs.append((prefix + ".0.conv.bias", (cout,), "fanin", cin * 5))
+        specs.append((prefix + ".1.weight", (cout,), "bn_gamma", None))
+        specs.append((prefix + ".1.bias", (cout,), "bn_beta", None))
+        specs.append((prefix + ".1.running_mean", (cout,), "bn_rmean", None))
+        specs.append((prefix + ".1.running_var", (cout,), "bn_rvar", None))
+        specs.append((prefix + ".1.num_batches_tracked", (), "bn_count", None))
+
+    def lstm(prefix, din, h, layers, bidir):
+        for l in range(layers):
+            for sfx in ([""] + (["_reverse"] if bidir else [])):
+                lin = din if l == 0 else h * (2 if bidir else 1)
+                specs.append((f"{prefix}.weight_ih_l{l}{sfx}", (4 * h, lin), "lstm", h))
+                specs.append((f"{prefix}.weight_hh_l{l}{sfx}", (4 * h, h), "lstm", h))
+                specs.append((f"{prefix}.bias_ih_l{l}{sfx}", (4 * h,), "lstm", h))
+                specs.append((f"{prefix}.bias_hh_l{l}{sfx}", (4 * h,), "lstm", h))
+
+    for i in range(3):
+        conv(f"encoder.convolutions.{i}", 80 + dim_emb if i == 0 else 512, 512, gain_relu)
+    lstm("encoder.lstm", 512, dim_neck, 2, True)
+    lstm("decoder.lstm1", dim_neck * 2 + dim_emb, dim_pre, 1, False)
+    for i in range(3):
+        conv(f"decoder.convolutions.{i}", dim_pre, dim_pre, gain_relu)
+    lstm("decoder.lstm2", dim_pre, 1024, 2, False)
+    specs.append(("decoder.linear_projection.linear_layer.weight", (80, 1024), "xavier", (gain_lin, 1024, 80)))
+    specs.append(("decoder.linear_projection.linear_layer.bias", (80,), "fanin", 1024))
+    conv("postnet.convolutions.0", 80, 512, gain_tanh)
+    for i in range(1, 4):
+        conv(f"postnet.convolutions.{i}", 512, 512, gain_tanh)
+    conv("postnet.convolutions.4", 512, 80, gain_lin)
+    return specs
+
+
+def synthetic_state_dict(seed: int = 0, bn_perturb: bool = True, **dims) -> "OrderedDict[str, np.ndarray]":
+    """Deterministic numpy state dict with the reference's keys, shapes and init bounds."""
+    out = OrderedDict()
+    for idx, (name, shape, kind, extra) in enumerate(param_specs(**dims)):
+        if kind == "xavier":
+            gain, fi, fo = extra
+            a = gain * math.sqrt(6.0 / (fi + fo))
+            out[name] = _u(seed, idx, shape, -a, a)
+        elif kind == "fanin":
+            b = 1.0 / math.sqrt(extra)
+            out[name] = _u(seed, idx, shape, -b, b)
+        elif kind == "lstm":
+            b = 1.0 / math.sqrt(extra)
+            out[name] = _u(seed, idx, shape, -b, b)
+        elif kind == "bn_gamma":
+            out[name] = _u(seed, idx, shape, 0.5, 1.5) if bn_perturb else np.ones(shape, np.float32)
+        elif kind == "bn_beta":
+            out[name] = _u(seed, idx, shape, -0.2, 0.2) if bn_perturb else np.zeros(shape, np.float32)
+        elif kind == "bn_rmean":
+            out[name] = _u(seed, idx, shape, -0.1, 0.1) if bn_perturb else np.zeros(shape, np.float32)
+        elif kind == "bn_rvar":
+            out[name] = _u(seed, idx, shape, 0.5, 1.5) if bn_perturb else np.ones(shape, np.float32)
+        elif kind == "bn_count":
+            out[name] = np.array(0, dtype=np.int64)
+        else:  # pragma: no cover
+            raise AssertionError(kind)
+    return out
+
+
+def torch_state_dict(seed: int = 0, bn_perturb: bool = True, device="cpu", **dims):
+    import torch
+    return OrderedDict((k, torch.from_numpy(v).to(device)) for k, v in
+                       synthetic_state_dict(seed, bn_perturb, **dims).items())
+
+
+def state_checksum(sd) -> float:
+    """Order-sensitive float64 checksum used by fixtures to detect generator drift."""
+    s = 0.0
+    for i, (k, v) in enumerate(sd.items()):
+        a = np.asarray(v.cpu().numpy() if hasattr(v, "cpu") else v, dtype=np.float64).ravel()
+        if a.size:
+            s += (i + 1) * float(a.sum()) + float((a * np.arange(1, a.size + 1) % 7).sum()) * 1e-6
+    return s
+
+
+# ---- synthetic inputs -------------------------------------------------------
+
+def synthetic_mel(seed: int, B: int, T: int, n_mels: int = 80) -> np.ndarray:
+    """U[0,1) mels, shape (B, 80, T): real mels are clipped to [0,1] (spectrogram.py:31)."""
+    return _u(seed, 10_000_001, (B, n_mels, T), 0.0, 1.0)
+
+
+def synthetic_embedding(seed: int, B: int, dim: int = 256) -> np.ndarray:
+    """|N(0,1)| then L2-normalised, mimicking the speaker encoder's ReLU + L2 (model.py:85-88)."""
+    u1 = uniform01(seed, 20_000_003, B * dim)
+    u2 = uniform01(seed, 20_000_005, B * dim)
+    g = np.abs(np.sqrt(-2.0 * np.log1p(-u1)) * np.cos(2 * np.pi * u2)).reshape(B, dim)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    return g.astype(np.float32)
+
+
+def onehot_embedding(B: int, dim: int = 256, offset: int = 0) -> np.ndarray:
+    """One-hot speaker ids c[i, i mod 256] = 1 as in dataloader.py:82-85."""
+    c = np.zeros((B, dim), np.float32)
+    c[np.arange(B), (np.arange(B) + offset) % dim] = 1.0
+    return c

@@ -1,0 +1,180 @@
+"""Generate the golden fixtures from the REFERENCE AutoEncoder (run in the build container only).
+
+The reference has no tests and no golden vectors of its own, so parity is pinned
+here: the reference class autovc/auto_encoder/model.py:27 is imported straight from
+/root/reference with `wandb` and the package __init__ stubbed (SURVEY §8c loader recipe), loaded
+with seeded synthetic weights (autovc_amd.weights, seed 0), and run on seeded inputs.  Only
+small inputs/outputs are written (tests/golden/*.npz); the weights are re-generated from the
+seed and checked against a stored checksum.
+
+    python tests/golden/make_golden.py          # rewrites tests/golden/*.npz
+
+Nothing on the GPU box runs this file (it needs /root/reference).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+from autovc_amd.weights import (onehot_embedding, state_checksum, synthetic_embedding,  # noqa: E402
+                                synthetic_mel, torch_state_dict)
+
+REF = "/root/reference"
+
+
+def load_reference():
+    sys.modules.setdefault("wandb", types.ModuleType("wandb"))
+    for name, path in [("autovc", REF + "/autovc"), ("autovc.auto_encoder", REF + "/autovc/auto_encoder")]:
+        m = types.ModuleType(name)
+        m.__path__ = [path]
+        sys.modules[name] = m
+    model = importlib.import_module("autovc.auto_encoder.model")
+    hp = importlib.import_module("autovc.utils.hparams")
+    return model.AutoEncoder, hp.AutoEncoderParams
+
+
+def make_ae(AE, seed=0):
+    torch.manual_seed(1234)
+    ae = AE(device="cpu", verbose=False)
+    sd = torch_state_dict(seed)
+    ae.load_state_dict(sd)
+    return ae, state_checksum(sd)
+
+
+def bn_buffers(ae):
+    out = {}
+    for k, v in ae.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var") or k.endswith("num_batches_tracked"):
+            out["bn/" + k] = v.detach().numpy().copy()
+    return out
+
+
+def fwd_case(AE, B, T, train, x_seed, lengths=None):
+    ae, ck = make_ae(AE)
+    ae.train(train)
+    x = synthetic_mel(x_seed, B, T)
+    if lengths is not None:  # collate_fn zero-pad semantics (dataloader.py:112-121)
+        for i, L in enumerate(lengths):
+            x[i, :, L:] = 0.0
+    c_org = synthetic_embedding(x_seed + 100, B)
+    c_trg = synthetic_embedding(x_seed + 200, B)
+    with torch.no_grad():
+        mel, mel_post, codes = ae(torch.from_numpy(x), torch.from_numpy(c_org), torch.from_numpy(c_trg))
+    d = dict(x=x, c_org=c_org, c_trg=c_trg, mel=mel.numpy(), mel_post=mel_post.numpy(),
+             codes=codes.numpy(), train=np.array(train), weights_checksum=np.array(ck), seed=np.array(0))
+    if lengths is not None:
+        d["lengths"] = np.array(lengths)
+    d.update(bn_buffers(ae))
+    return d
+
+
+def batch_forward_case(AE):
+    ae, ck = make_ae(AE)
+    ae.train(True)
+    M, N = 5, 128
+    batch = synthetic_mel(7, M, N)
+    c_org = synthetic_embedding(107, 1)
+    c_trg = synthetic_embedding(207, 1)
+    with torch.no_grad():
+        out = ae.batch_forward(torch.from_numpy(batch), torch.from_numpy(c_org), torch.from_numpy(c_trg), overlap=0.5)
+    return dict(batch=batch, c_org=c_org, c_trg=c_trg, out=out.numpy(), overlap=np.array(0.5),
+                weights_checksum=np.array(ck))
+
+
+TRACE_TENSORS = ["encoder.convolutions.0.0.conv.weight", "encoder.lstm.weight_hh_l0_reverse",
+                 "decoder.lstm2.weight_hh_l1", "decoder.linear_projection.linear_layer.bias",
+                 "postnet.convolutions.4.1.weight"]
+
+
+def train_case(AE, hparams, steps=3, B=4, T=128):
+    """Replays model.py:303-321 with the reference's own forward/_loss/Adam/clip/EMA, then checks
+    the same batches through the reference `learn()` give the same parameters."""
+    ae, ck = make_ae(AE)
+    xs = [synthetic_mel(30 + s, B, T) for s in range(steps)]
+    cs = [onehot_embedding(B, offset=4 * s) for s in range(steps)]
+    opt_params = {k: v for k, v in hparams["optimizer"].items() if k not in ("lr_scheduler", "n_warmup_steps")}
+
+    ae.train()
+    ae.criterion1 = torch.nn.MSELoss()
+    ae.criterion2 = torch.nn.L1Loss()
+    ae.optimiser = torch.optim.Adam(ae.parameters(), **opt_params)
+    avg = ae.flatten_params()
+    losses, norms = [], []
+    for s in range(steps):
+        X, c = torch.from_numpy(xs[s]), torch.from_numpy(cs[s])
+        out_dec, out_post, codes = ae(X, c, c)
+        loss = ae._loss(X=X, c_org=c, out_decoder=out_dec, out_postnet=out_post, content_codes=codes)
+        ae.optimiser.zero_grad()
+        loss.backward()
+        norms.append(float(torch.nn.utils.clip_grad_norm_(ae.parameters(), max_norm=1)))
+        ae.optimiser.step()
+        avg = 0.9999 * avg + (1 - 0.9999) * ae.flatten_params()
+        losses.append(float(loss.detach()))
+    sd = ae.state_dict()
+    d = dict(losses=np.array(losses), grad_norms=np.array(norms), weights_checksum=np.array(ck),
+             ema_sum=np.array(float(avg.double().sum())), ema_abs=np.array(float(avg.double().abs().sum())),
+             B=np.array(B), T=np.array(T), steps=np.array(steps))
+    for s in range(steps):
+        d[f"x{s}"] = xs[s]
+        d[f"c{s}"] = cs[s]
+    for k, v in sd.items():
+        a = v.detach().double().numpy()
+        d["sum/" + k] = np.array(a.sum())
+        d["abs/" + k] = np.array(np.abs(a).sum())
+    for k in TRACE_TENSORS:
+        d["val/" + k] = sd[k].detach().numpy().ravel()[:256].copy()
+
+    # Cross-check against the reference training loop itself (model.py:218-361).
+    ae2, _ = make_ae(AE)
+    hp_opt = hparams["optimizer"]
+    saved = dict(hp_opt)
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        os.makedirs("ckpt")
+        try:
+            ae2.learn([(torch.from_numpy(xs[s]), torch.from_numpy(cs[s])) for s in range(steps)],
+                      n_epochs=1, save_dir="ckpt", model_name="m.pt")
+        finally:
+            os.chdir(cwd)
+            hp_opt.clear()
+            hp_opt.update(saved)
+    for k, v in ae2.state_dict().items():
+        assert torch.equal(v, sd[k]), f"learn() diverged from the replayed loop at {k}"
+    return d
+
+
+def main():
+    AE, hparams = load_reference()
+    torch.set_num_threads(8)
+    cases = {
+        "fwd_b2_t128_train": lambda: fwd_case(AE, 2, 128, True, 1),
+        "fwd_b2_t128_eval": lambda: fwd_case(AE, 2, 128, False, 1),
+        "fwd_b2_t100_train": lambda: fwd_case(AE, 2, 100, True, 2),
+        "fwd_b1_t128_train": lambda: fwd_case(AE, 1, 128, True, 3),
+        "fwd_b3_t33_train": lambda: fwd_case(AE, 3, 33, True, 4),
+        "fwd_b2_t1024_ragged": lambda: fwd_case(AE, 2, 1024, True, 5, lengths=[1024, 700]),
+        "batch_forward_m5_n128": lambda: batch_forward_case(AE),
+        "train_b4_t128_3steps": lambda: train_case(AE, hparams),
+    }
+    only = sys.argv[1:]
+    for name, fn in cases.items():
+        if only and name not in only:
+            continue
+        d = fn()
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **d)
+        print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KiB)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,101 @@
+"""The oracle (oracle/autovc_oracle.py, oracle/numpy_ref.py) pinned against the golden vectors
+produced by the reference class itself (tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+import torch
+
+from autovc_amd.weights import state_checksum, torch_state_dict
+from oracle import autovc_oracle as orc
+from oracle import numpy_ref
+from tests.conftest import load_golden
+
+def is_prebn_bias(k):
+    return k.endswith(".0.conv.bias")
+
+
+FWD_CASES = ["fwd_b2_t128_train", "fwd_b2_t128_eval", "fwd_b2_t100_train", "fwd_b1_t128_train",
+             "fwd_b3_t33_train", "fwd_b2_t1024_ragged"]
+
+
+@pytest.fixture(scope="module")
+def sd():
+    return torch_state_dict(0)
+
+
+def test_weight_generator_matches_fixture(sd):
+    g = load_golden("fwd_b2_t128_train")
+    assert state_checksum(sd) == pytest.approx(float(g["weights_checksum"]), rel=0, abs=1e-9)
+    assert sum(v.numel() for k, v in sd.items() if k in orc.param_names(sd)) == 28_422_464
+
+
+@pytest.mark.parametrize("case", FWD_CASES)
+def test_torch_oracle_matches_reference(sd, case):
+    g = load_golden(case)
+    bufs = {k: v.clone() for k, v in sd.items() if "running" in k or "num_batches" in k}
+    with torch.no_grad():
+        mel, post, codes = orc.forward(sd, torch.from_numpy(g["x"]), torch.from_numpy(g["c_org"]),
+                                       torch.from_numpy(g["c_trg"]), bool(g["train"]), bufs)
+    # same aten kernels, same order: agreement to fp32 rounding noise at most
+    np.testing.assert_allclose(mel.numpy(), g["mel"], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(post.numpy(), g["mel_post"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(codes.numpy(), g["codes"], rtol=0, atol=2e-6)
+    for k, v in bufs.items():
+        np.testing.assert_allclose(v.numpy(), g["bn/" + k], rtol=0, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("case", ["fwd_b2_t128_train", "fwd_b2_t128_eval", "fwd_b3_t33_train"])
+def test_numpy_fp64_oracle_matches_reference(sd, case):
+    g = load_golden(case)
+    npsd = {k: v.numpy() for k, v in sd.items()}
+    mel, post, codes, bn = numpy_ref.forward(npsd, g["x"], g["c_org"], g["c_trg"], bool(g["train"]))
+    np.testing.assert_allclose(mel, g["mel"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(post, g["mel_post"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(codes, g["codes"], rtol=0, atol=2e-5)
+    for k, v in bn.items():
+        np.testing.assert_allclose(v, g["bn/" + k], rtol=0, atol=1e-5, err_msg=k)
+
+
+def test_codes_only_path(sd):
+    g = load_golden("fwd_b2_t128_train")
+    with torch.no_grad():
+        codes = orc.forward(sd, torch.from_numpy(g["x"]), torch.from_numpy(g["c_org"]), None, True,
+                            {k: v.clone() for k, v in sd.items() if "running" in k})
+    np.testing.assert_allclose(codes.numpy(), g["codes"], rtol=0, atol=2e-6)
+
+
+def test_batch_forward_oracle(sd):
+    g = load_golden("batch_forward_m5_n128")
+    bufs = {k: v.clone() for k, v in sd.items() if "running" in k}
+    with torch.no_grad():
+        out = orc.batch_forward(sd, torch.from_numpy(g["batch"]), torch.from_numpy(g["c_org"]),
+                                torch.from_numpy(g["c_trg"]), float(g["overlap"]), True, bufs)
+    assert out.shape == (80, 4 * 64 + 128)
+    np.testing.assert_allclose(out.numpy(), g["out"], rtol=0, atol=2e-5)
+
+
+def test_train_trace_oracle(sd):
+    g = load_golden("train_b4_t128_3steps")
+    tr = orc.Trainer(sd)
+    for s in range(int(g["steps"])):
+        loss, norm = tr.step(torch.from_numpy(g[f"x{s}"]), torch.from_numpy(g[f"c{s}"]))
+        assert loss == pytest.approx(float(g["losses"][s]), rel=1e-5)
+        assert norm == pytest.approx(float(g["grad_norms"][s]), rel=1e-4)
+    final = tr.sd()
+    for k in final:
+        if ("sum/" + k) not in g:
+            continue
+        a = final[k].detach().double()
+        if is_prebn_bias(k):
+            # d loss / d bias is exactly 0 in exact arithmetic (train-mode BN subtracts the batch
+            # mean), so Adam normalises rounding noise: only the step bound is reproducible.
+            assert float((a - sd[k].double()).abs().max()) <= 3 * 1e-3 * 1.5, k
+            continue
+        assert float(a.abs().sum()) == pytest.approx(float(g["abs/" + k]), rel=1e-6, abs=1e-7), k
+        assert float(a.sum()) == pytest.approx(float(g["sum/" + k]), rel=0, abs=2e-5 * float(g["abs/" + k])), k
+    assert float(tr.avg.double().sum()) == pytest.approx(float(g["ema_sum"]), rel=1e-6)
+
+
+def test_known_answers():
+    """Code length 32*(floor(T/32)+ceil(T/32)) and ValueError at T<32."""
+    for T, n in [(128, 256), (100, 224), (33, 96), (1024, 2048)]:
+        assert 32 * (T // 32 + -(-T // 32)) == n
