@@ -1,0 +1,27 @@
+# Builds the MI355X (gfx950) HIP library behind the C ABI in include/autovc_hip.h.
+#   make            -> autovc_amd/libautovc_hip.so
+#   make check-abi  -> verifies every symbol declared in the header is exported
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable
+SRC      := $(wildcard autovc_amd/csrc/*.hip)
+HDR      := $(wildcard autovc_amd/csrc/*.h) include/autovc_hip.h
+OBJ      := $(patsubst autovc_amd/csrc/%.hip,build/%.o,$(SRC))
+LIB      := autovc_amd/libautovc_hip.so
+
+all: $(LIB)
+
+build/%.o: autovc_amd/csrc/%.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJ) -o $@
+
+check-abi: $(LIB)
+	python3 -c "import re,ctypes;h=open('include/autovc_hip.h').read();names=re.findall(r'^\w[\w\s\*]*?\b(avc_\w+)\(',h,re.M);lib=ctypes.CDLL('$(LIB)');[getattr(lib,n) for n in names];print(len(names),'symbols ok')"
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean check-abi

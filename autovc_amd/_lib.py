@@ -1,0 +1,156 @@
+"""ctypes binding of the HIP C-ABI library (include/autovc_hip.h -> autovc_amd/libautovc_hip.so).
+
+The library is the only compute path of this package: there is no CPU or pure-PyTorch
+fallback, and every call fails loudly (RuntimeError/ValueError) when the library is missing or a
+kernel launch is rejected.  `torch` is imported first so that the library binds to the HIP
+runtime torch already loaded (both carry SONAME libamdhip64.so.7).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("AUTOVC_HIP_LIB", os.path.join(_HERE, "libautovc_hip.so"))
+
+ACT_NONE, ACT_RELU, ACT_TANH = 0, 1, 2
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_Z = ctypes.c_size_t
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+_SIGS = {
+    "avc_abi_version": [],
+    "avc_last_error": [],
+    "avc_context_create": [_I, ctypes.POINTER(_P)],
+    "avc_context_destroy": [_P],
+    "avc_context_reserve": [_P, _Z],
+    "avc_gemm": [_P, _I, _I, _I, _P, _I, _P, _I, _P, _P, _I, _P],
+    "avc_conv_bn_act_forward": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _I,
+                                _P, _P, _P, _P, _P, _P],
+    "avc_conv_bn_act_backward": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P,
+                                 _P, _P, _P, _P, _I, _P],
+    "avc_lstm_forward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P],
+    "avc_lstm_backward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P,
+                          _P, _P, _P, _I, _I, _P],
+    "avc_linear_forward": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
+    "avc_linear_backward": [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P],
+    "avc_frames_from_mel": [_I, _I, _I, _P, _I, _P, _P, _P],
+    "avc_frames_from_mel_backward": [_I, _I, _I, _I, _P, _I, _P, _P, _I, _P],
+    "avc_mel_from_frames": [_I, _I, _I, _P, _P, _P],
+    "avc_codes_from_encoder": [_I, _I, _P, _P, _P],
+    "avc_codes_from_encoder_backward": [_I, _I, _P, _P, _I, _P],
+    "avc_decoder_input": [_I, _I, _P, _I, _P, _P, _P],
+    "avc_decoder_input_backward": [_I, _I, _I, _P, _P, _I, _P],
+    "avc_overlap_average": [_I, _I, _I, _I, _P, _P, _P],
+    "avc_loss_forward": [_P, _I, _Z, _P, _P, _P, _I, _P],
+    "avc_loss_backward": [_I, _Z, _P, _P, _P, _P, _P, _I, _P],
+    "avc_clip_adam_ema": [_P, _Z, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, _F, _P, _P],
+    "avc_timing_enable": [_I],
+    "avc_timing_reset": [],
+    "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)],
+    "avc_generator_param_count": [],
+    "avc_generator_forward": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P],
+}
+_RESTYPES = {"avc_last_error": ctypes.c_char_p}
+
+_lib = None
+_lock = threading.Lock()
+_contexts = {}
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes library.  Raises if it is absent: no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HipLibraryError(
+                    f"HIP library not found at {LIB_PATH}; build it with `make` (hipcc --offload-arch=gfx950)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, args in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = _RESTYPES.get(name, ctypes.c_int)
+            _lib = lib
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = load().avc_last_error().decode(errors="replace")
+        if status == 1:
+            raise ValueError(f"{what}: {msg}")
+        raise HipLibraryError(f"{what} failed ({status}): {msg}")
+
+
+def call(name: str, *args):
+    check(getattr(load(), name)(*args), name)
+
+
+def context(device: torch.device) -> int:
+    """Per-device library context (owns the scratch arena)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    ctx = _contexts.get(idx)
+    if ctx is None:
+        with _lock:
+            ctx = _contexts.get(idx)
+            if ctx is None:
+                p = ctypes.c_void_p()
+                check(load().avc_context_create(idx, ctypes.byref(p)), "avc_context_create")
+                ctx = p.value
+                _contexts[idx] = ctx
+    return ctx
+
+
+def stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a contiguous fp32 CUDA tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("autovc_amd runs on the GPU only (HIP kernels); got a CPU tensor")
+    if t.dtype != torch.float32:
+        raise TypeError(f"autovc_amd kernels are fp32; got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError("autovc_amd kernels need contiguous tensors")
+    return t.data_ptr()
+
+
+TIMING_CLASSES = {"gemm": 0, "lstm_step_fwd": 1, "lstm_step_bwd": 2, "lstm32": 3}
+
+
+def timing_enable(names):
+    mask = 0
+    for n in names:
+        mask |= 1 << TIMING_CLASSES[n]
+    call("avc_timing_enable", mask)
+
+
+def timing_reset():
+    call("avc_timing_reset")
+
+
+def timing_read(name):
+    ms, fl, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_long()
+    call("avc_timing_read", TIMING_CLASSES[name], ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by),
+         ctypes.byref(n))
+    return {"ms": ms.value, "flops": fl.value, "bytes": by.value, "launches": n.value}

@@ -1,0 +1,379 @@
+"""Drop-in Generator: `AutoEncoder` with the reference's constructor, attributes, state_dict keys
+and methods (autovc/auto_encoder/model.py:27-453), computing on hand-written gfx950 HIP kernels.
+
+Paths:
+  * inference (no autograd needed, c_trg given): ONE call into the library's whole-Generator
+    forward (avc_generator_forward) — the convert() hot path;
+  * everything else (training, codes-only, grad-enabled conversion): the per-layer autograd
+    Functions of autovc_amd.ops, each a C-ABI forward/backward pair.
+Both honour `module.training` per BatchNorm exactly like nn.BatchNorm1d (train mode uses batch
+statistics and updates the running buffers; the reference never calls .eval()).
+"""
+from __future__ import annotations
+
+import ctypes
+import inspect
+import time
+
+import torch
+import torch.nn as nn
+
+from .. import _lib, ops
+from ..hparams import AutoEncoderParams
+from .decoder import Decoder
+from .encoder import Encoder
+from .postnet import Postnet
+
+
+def _default_device():
+    return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam semantics (amsgrad=False) on the flat parameter/gradient buffers of an
+    AutoEncoder, fused with clip_grad_norm_ and the EMA of model.py:314-321 in one HIP pass
+    (avc_clip_adam_ema).  state_dict() has torch Adam's layout (step/exp_avg/exp_avg_sq)."""
+
+    def __init__(self, model: "AutoEncoder", lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 amsgrad=False, **_ignored):
+        if amsgrad:
+            raise NotImplementedError("amsgrad is not used by the reference (hparams.py:33)")
+        model._ensure_flat()
+        params = list(model.parameters())
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None)
+        super().__init__(params, defaults)
+        self.model = model
+        self.exp_avg = torch.zeros_like(model._flat_param)
+        self.exp_avg_sq = torch.zeros_like(model._flat_param)
+        self._step = 0
+        self._step_t = torch.tensor(0.0)
+        for p, (off, n) in zip(params, model._flat_slices):
+            self.state[p] = {"step": self._step_t, "exp_avg": self.exp_avg[off:off + n].view_as(p),
+                             "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p)}
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.model._ensure_flat()
+        self.model._flat_grad.zero_()
+
+    @torch.no_grad()
+    def step(self, closure=None, max_norm: float = 0.0, ema: torch.Tensor | None = None,
+             ema_decay: float = 0.9999):
+        loss = closure() if closure is not None else None
+        m = self.model
+        if not m._flat_valid():
+            raise RuntimeError("parameters were re-allocated after the optimizer was built")
+        g = self.param_groups[0]
+        self._step += 1
+        self._step_t.fill_(float(self._step))
+        norm = torch.empty((), dtype=torch.float32, device=m._flat_param.device)
+        b1, b2 = g["betas"]
+        _lib.call("avc_clip_adam_ema", _lib.context(norm.device), m._flat_param.numel(),
+                  m._flat_param.data_ptr(), m._flat_grad.data_ptr(), self.exp_avg.data_ptr(),
+                  self.exp_avg_sq.data_ptr(), None if ema is None else _lib.ptr(ema), float(g["lr"]),
+                  float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), self._step,
+                  float(max_norm), float(ema_decay), norm.data_ptr(), _lib.stream(norm.device))
+        self.last_grad_norm = norm
+        return loss
+
+    def load_state_dict(self, state_dict):
+        st = state_dict["state"]
+        params = list(self.model.parameters())
+        for i, p in enumerate(params):
+            if i in st:
+                self.state[p]["exp_avg"].copy_(st[i]["exp_avg"])
+                self.state[p]["exp_avg_sq"].copy_(st[i]["exp_avg_sq"])
+                self._step = int(float(st[i]["step"]))
+        self._step_t.fill_(float(self._step))
+        for g, sg in zip(self.param_groups, state_dict["param_groups"]):
+            for k, v in sg.items():
+                if k != "params":
+                    g[k] = v
+
+
+class AutoEncoder(nn.Module):
+    """Generator network (reference model.py:27): Encoder + Decoder + Postnet."""
+
+    def __init__(self, dim_neck=AutoEncoderParams["model"]["dim_neck"],
+                 dim_emb=AutoEncoderParams["model"]["dim_emb"],
+                 dim_pre=AutoEncoderParams["model"]["dim_pre"],
+                 freq=AutoEncoderParams["model"]["freq"], verbose=True, device=None):
+        super().__init__()
+        if dim_emb != 256 or dim_pre != 512:
+            raise NotImplementedError("HIP Generator kernels are built for dim_emb=256, dim_pre=512")
+        self.verbose = verbose
+        device = _default_device() if device is None else device
+        self.device = device if not isinstance(device, str) else torch.device(device)
+        self.logging = {}
+        self.encoder = Encoder(dim_neck, dim_emb, freq)
+        self.decoder = Decoder(dim_neck, dim_emb, dim_pre)
+        self.postnet = Postnet()
+        self._flat_param = None
+        self._flat_grad = None
+        self._flat_slices = []
+        self._gen_cache = None
+
+    # ---- flat parameter storage (one buffer for Adam/EMA/all-reduce) -----------------------
+    def _flat_valid(self):
+        if self._flat_param is None:
+            return False
+        base = self._flat_param.data_ptr()
+        for p, (off, n) in zip(self.parameters(), self._flat_slices):
+            if p.data_ptr() != base + 4 * off or p.grad is None or p.grad.data_ptr() != self._flat_grad.data_ptr() + 4 * off:
+                return False
+        return True
+
+    def _ensure_flat(self):
+        if self._flat_valid():
+            return
+        params = list(self.parameters())
+        dev = params[0].device
+        total = sum(p.numel() for p in params)
+        flat = torch.empty(total, dtype=torch.float32, device=dev)
+        grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        slices, off = [], 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                flat[off:off + n].copy_(p.data.reshape(-1))
+                p.data = flat[off:off + n].view_as(p)
+                p.grad = grad[off:off + n].view_as(p)
+                slices.append((off, n))
+                off += n
+        self._flat_param, self._flat_grad, self._flat_slices = flat, grad, slices
+
+    def flatten_params(self):
+        """model.py:379-383."""
+        return torch.cat([param.data.view(-1) for param in self.parameters()], 0)
+
+    def load_flattened_params(self, flattened_params):
+        """model.py:385-392."""
+        offset = 0
+        for param in self.parameters():
+            param.data.copy_(flattened_params[offset:offset + param.nelement()].view(param.size()))
+            offset += param.nelement()
+
+    # ---- forward ------------------------------------------------------------------------------
+    def _bns(self):
+        return [m for m in self.modules() if isinstance(m, nn.BatchNorm1d)]
+
+    def _fast_path_ok(self, x, c_org, c_trg):
+        if c_trg is None:
+            return False
+        if torch.is_grad_enabled() and (x.requires_grad or c_org.requires_grad or c_trg.requires_grad
+                                        or any(p.requires_grad for p in self.parameters())):
+            return False
+        bns = self._bns()
+        modes = {b.training for b in bns}
+        return len(modes) == 1 and all(b.momentum == 0.1 and b.eps == 1e-5 and b.track_running_stats
+                                       for b in bns)
+
+    def _gen_params(self):
+        tensors = [v for k, v in self.state_dict(keep_vars=True).items()
+                   if not k.endswith("num_batches_tracked")]
+        key = tuple(t.data_ptr() for t in tensors)
+        if self._gen_cache is None or self._gen_cache[0] != key:
+            for t in tensors:
+                _lib.ptr(t)
+            arr = (ctypes.c_void_p * len(tensors))(*key)
+            self._gen_cache = (key, arr)
+        return self._gen_cache[1]
+
+    def _generator_forward(self, x, c_org, c_trg):
+        B, _, T = x.shape
+        training = self._bns()[0].training
+        mel = torch.empty((B, 80, T), dtype=torch.float32, device=x.device)
+        mel_post = torch.empty_like(mel)
+        codes = torch.empty((B, 32 * (T // 32 + (T + 31) // 32)), dtype=torch.float32, device=x.device)
+        params = self._gen_params()
+        if len(params) != _lib.load().avc_generator_param_count():
+            raise RuntimeError("state_dict layout does not match the library's Generator")
+        _lib.call("avc_generator_forward", _lib.context(x.device), T, B, params, _lib.ptr(x),
+                  _lib.ptr(c_org), _lib.ptr(c_trg), int(training), _lib.ptr(mel), _lib.ptr(mel_post),
+                  _lib.ptr(codes), _lib.stream(x.device))
+        if training:
+            for b in self._bns():
+                b.num_batches_tracked.add_(1)
+        return mel, mel_post, codes
+
+    @staticmethod
+    def _check(x, c, name):
+        if not x.is_cuda:
+            raise RuntimeError(f"autovc_amd.AutoEncoder runs on the GPU only; {name} is on {x.device}")
+        if x.dtype != torch.float32:
+            raise TypeError(f"{name} must be float32, got {x.dtype}")
+
+    def forward(self, x, c_org, c_trg):
+        """model.py:68-146.  x (B,80,T) channel-first, c_org/c_trg (B,256).  Returns
+        (mel_outputs, mel_outputs_postnet, content_codes), or content_codes if c_trg is None."""
+        self._check(x, None, "x")
+        if x.dim() != 3 or x.shape[1] != 80:
+            raise ValueError(f"x must be (B, 80, T), got {tuple(x.shape)}")
+        B, _, T = x.shape
+        if T < self.encoder.freq:
+            # the reference fails in torch.cat of an empty code list (model.py:99 / :143)
+            raise ValueError("torch.cat(): expected a non-empty list of Tensors")
+        c_org = c_org.to(torch.float32).contiguous()
+        if c_trg is not None:
+            c_trg = c_trg.to(torch.float32).contiguous()
+        x = x.contiguous()
+        if self._fast_path_ok(x, c_org, c_trg):
+            return self._generator_forward(x, c_org, c_trg)
+        save = torch.is_grad_enabled()
+        enc = self.encoder.frames(x, c_org, save)
+        codes = ops.Codes.apply(enc, T, B)
+        if c_trg is None:
+            return codes
+        din = ops.DecoderInput.apply(enc, c_trg, T, B)
+        melf = self.decoder.frames(din, T, B, save)
+        postf = self.postnet.frames(melf, T, B, residual=melf)
+        return ops.MelFromFrames.apply(melf, T, B), ops.MelFromFrames.apply(postf, T, B), codes
+
+    # ---- checkpoints (model.py:149-181) -------------------------------------------------------
+    def load(self, model_name, model_dir=AutoEncoderParams["model_dir"], device=None):
+        self.device = device if device is not None else self.device
+        model_path = model_dir.strip("/") + "/" + model_name
+        checkpoint = torch.load(model_path, map_location=self.device, weights_only=True)
+        self.load_state_dict(checkpoint["model_state"])
+        self.share_memory()
+        if self.verbose:
+            print("Loaded auto encoder \"%s\" trained to step %d" % (model_path, checkpoint["step"]))
+
+    def save(self, model_name, save_dir=AutoEncoderParams["learn"]["save_dir"], wandb_run=None):
+        model_path = save_dir.strip("/") + "/" + model_name
+        self._sync_bn_buffers()
+        torch.save({
+            "step": self.logging.get("step"),
+            "model_state": {k: v.detach().clone() for k, v in self.state_dict().items()},
+            "optimizer_state": self.optimiser.state_dict(),
+        }, model_path)
+        if wandb_run is not None:
+            import wandb  # only when the caller logs to wandb
+            artifact = wandb.Artifact(model_name, "AutoEncoder")
+            artifact.add_file(model_path)
+            wandb_run.log_artifact(artifact)
+
+    def _sync_bn_buffers(self):
+        """Data-parallel training keeps per-rank BN statistics; rank 0's are the saved ones."""
+        if torch.distributed.is_available() and torch.distributed.is_initialized() \
+                and torch.distributed.get_world_size() > 1:
+            for b in self.buffers():
+                torch.distributed.broadcast(b, 0)
+
+    # ---- training (model.py:184-361) ----------------------------------------------------------
+    def _loss(self, X, c_org, out_decoder, out_postnet, content_codes, mu=1, lambd=1):
+        """MSE(post,X) + mu*MSE(dec,X) + lambd*L1(Enc(post,c_org), codes); nothing detached."""
+        reconstructed_content_codes = self(out_postnet, c_org, None)
+        reconstruction_loss1 = ops.mse_loss(out_postnet, X)
+        reconstruction_loss2 = ops.mse_loss(out_decoder, X)
+        content_loss = ops.l1_loss(reconstructed_content_codes, content_codes)
+        return reconstruction_loss1 + mu * reconstruction_loss2 + lambd * content_loss
+
+    def configure_optimizer(self, **opt):
+        params = {k: v for k, v in AutoEncoderParams["optimizer"].items()
+                  if k not in ("lr_scheduler", "n_warmup_steps")}
+        params.update(opt)
+        self._ensure_flat()
+        self.optimiser = FusedAdam(self, **params)
+        self.avg_params = self._flat_param.detach().clone()
+        return self.optimiser
+
+    def train_step(self, X, c_org, ema_decay=AutoEncoderParams["learn"]["ema_decay"], max_norm=1.0):
+        """One iteration of the reference loop body (model.py:304-321): forward, _loss, backward,
+        [data-parallel gradient all-reduce], clip_grad_norm_(1) + Adam + EMA (one fused pass).
+        Returns (loss, pre-clip total grad norm) as device scalars."""
+        if getattr(self, "optimiser", None) is None or not isinstance(self.optimiser, FusedAdam):
+            self.configure_optimizer()
+        X = X.to(self._flat_param.device, torch.float32).contiguous()
+        c_org = c_org.to(self._flat_param.device, torch.float32).contiguous()
+        out_decoder, out_postnet, content_codes = self(X, c_org, c_org)
+        loss = self._loss(X=X, c_org=c_org, out_decoder=out_decoder, out_postnet=out_postnet,
+                          content_codes=content_codes)
+        self.optimiser.zero_grad()
+        loss.backward()
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            ws = torch.distributed.get_world_size()
+            if ws > 1:
+                torch.distributed.all_reduce(self._flat_grad)
+                self._flat_grad.div_(ws)
+        self.optimiser.step(max_norm=max_norm, ema=self.avg_params, ema_decay=ema_decay)
+        return loss.detach(), self.optimiser.last_grad_norm
+
+    def learn(self, trainloader, n_epochs=AutoEncoderParams["learn"]["n_epochs"],
+              log_freq=AutoEncoderParams["learn"]["log_freq"],
+              save_freq=AutoEncoderParams["learn"]["save_freq"],
+              save_dir=AutoEncoderParams["learn"]["save_dir"],
+              model_name=AutoEncoderParams["learn"]["model_name"],
+              ema_decay=AutoEncoderParams["learn"]["ema_decay"], wandb_run=None, voice_converter=None,
+              source_examples=None, target_examples=None, **opt_params):
+        """Training loop of model.py:218-361 (same arguments, logging keys, save cadence and
+        per-epoch ExponentialLR(0.95)); the optimizer is FusedAdam with the reference's Adam
+        settings (hparams optimizer dict; like the reference, **opt_params are not applied)."""
+        self.logging.update(step=0, running_loss=0.0, log_steps=0, total_time=0.0)
+        N_iterations = n_epochs * len(trainloader)
+        self.train()
+        if wandb_run is not None:
+            wandb_run.watch(self, log_freq=log_freq)
+        self.criterion1 = ops.mse_loss
+        self.criterion2 = ops.l1_loss
+        self.configure_optimizer()
+        self.lr_scheduler = torch.optim.lr_scheduler.ExponentialLR(self.optimiser, gamma=0.95)
+        if self.verbose:
+            print(f"Training Auto Encoder on {torch.cuda.get_device_name()} (cuda)...")
+        for epoch in range(n_epochs):
+            self.logging["step_start_time"] = time.time()
+            self.logging["batch"] = 0
+            for X, c_org in trainloader:
+                loss, _ = self.train_step(X, c_org, ema_decay=ema_decay)
+                self.logging["step"] += 1
+                self.logging["running_loss"] += loss
+                self.logging["log_steps"] += 1
+                self.logging["epoch"] = epoch + 1
+                self.logging["batch"] += 1
+                self.logging["lr"] = self.optimiser.param_groups[0]["lr"]
+                if self.verbose:
+                    self.logging["total_time"] += (time.time() - self.logging["step_start_time"])
+                    print(f"\rstep {self.logging['step']}/{N_iterations} | loss {float(loss):.5f}", end="")
+                if (self.logging["step"] % log_freq == 0 or self.logging["step"] == N_iterations) \
+                        and wandb_run is not None:
+                    self._log(wandb_run, X, None)
+            if self.logging["epoch"] % save_freq == 0 or self.logging["epoch"] == n_epochs:
+                self.save(model_name, save_dir, wandb_run)
+            if voice_converter is not None:
+                assert source_examples is not None and target_examples is not None
+                voice_converter.convert_multiple(
+                    sources=source_examples, targets=target_examples,
+                    save_dir="training_examples" if wandb_run is None or wandb_run.mode == "disabled" else "wandb",
+                    audio_log_dict={"epoch": self.logging["epoch"], "batch": self.logging["batch"],
+                                    "step": self.logging["step"]}, cut=True)
+            self.lr_scheduler.step()
+        if self.verbose:
+            print("\n")
+
+    def _log(self, wandb_run, X, out_postnet):
+        wandb_run.log({"loss": float(self.logging["running_loss"]) / self.logging["log_steps"],
+                       "epoch": self.logging["epoch"], "batch": self.logging["batch"],
+                       "step": self.logging["step"], "learning rate": self.logging["lr"]})
+        self.logging["running_loss"] = 0.0
+        self.logging["log_steps"] = 0
+
+    # ---- long-form conversion (model.py:395-437) ---------------------------------------------
+    def batch_forward(self, batch, c_org, c_trg, overlap=0.5):
+        c_org = c_org.expand(batch.size(0), -1)
+        c_trg = c_trg.expand(batch.size(0), -1)
+        _, output, _ = self(batch, c_org, c_trg)
+        N = batch.size(-1)
+        return ops.overlap_average(output.detach(), int(N * (1 - overlap)))
+
+    def plot_conversion(self, original, converted):
+        import matplotlib.pyplot as plt
+        fig, ax = plt.subplots(ncols=2, figsize=(20, 10))
+        ax[0].matshow(original.detach().cpu().numpy())
+        ax[0].set_title("Original")
+        ax[1].matshow(converted.detach().cpu().numpy())
+        ax[1].set_title("Reconstructed")
+        return fig
+
+
+AutoEncoder.learn.__allowed_args__ = inspect.getfullargspec(AutoEncoder.learn).args
+AutoEncoder.learn.__allowed_kw__ = inspect.getfullargspec(torch.optim.Adam).args

@@ -1,0 +1,371 @@
+// extern "C" entry points (include/autovc_hip.h), the context/arena, and the whole-Generator
+// forward used by VoiceConverter.convert()-style inference (model.py:68-146).
+#include <algorithm>
+#include <mutex>
+
+#include "elementwise.h"
+#include "kernels.h"
+
+namespace avc {
+
+namespace {
+thread_local std::string g_err;
+}
+
+void set_error(const std::string& msg) { g_err = msg; }
+const char* get_error() { return g_err.c_str(); }
+
+int ensure_arena(avc_context* ctx, size_t bytes) {
+  if (ctx->cap >= bytes) return AVC_OK;
+  if (ctx->top != 0) {
+    set_error("arena growth requested while scratch is in use");
+    return AVC_ERR_WORKSPACE;
+  }
+  int prev = 0;
+  AVC_HIP(hipGetDevice(&prev));
+  if (prev != ctx->device) AVC_HIP(hipSetDevice(ctx->device));
+  size_t want = std::max(bytes, ctx->cap * 3 / 2);
+  want = (want + (1u << 20) - 1) & ~size_t((1u << 20) - 1);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, want);
+  if (prev != ctx->device) (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    set_error(std::string("arena hipMalloc of ") + std::to_string(want) + " bytes: " + hipGetErrorString(e));
+    return AVC_ERR_HIP;
+  }
+  // The old block may still be read by kernels queued earlier on the stream: retire it and
+  // free it only when the context is destroyed.
+  if (ctx->base) ctx->retired.push_back(ctx->base);
+  ctx->base = static_cast<char*>(p);
+  ctx->cap = want;
+  return AVC_OK;
+}
+
+namespace {
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- whole-Generator forward --------------------------------------------------------------
+enum : int {
+  P_ENC_CONV = 0,    // 3 x {W, b, gamma, beta, rmean, rvar}
+  P_ENC_LSTM = 18,   // l0, l0_rev, l1, l1_rev x {w_ih, w_hh, b_ih, b_hh}
+  P_DEC_LSTM1 = 34,  // l0
+  P_DEC_CONV = 38,   // 3 x 6
+  P_DEC_LSTM2 = 56,  // l0, l1
+  P_LIN = 64,        // W, b
+  P_POST = 66,       // 5 x 6
+  P_COUNT = 96,
+};
+
+struct GenBufs {
+  size_t total = 0;
+  size_t nested = 0;
+};
+
+size_t gen_scratch(int T, int B) {
+  const size_t TB = (size_t)T * B, f = sizeof(float);
+  size_t own = TB * (336 + 512 + 512 + 64 + 64 + 320 + 1024 + 1024 + 80 + 80) * f + 4 * 512 * f + 64 * 256;
+  size_t nested = 0;
+  nested = std::max(nested, conv_bn_forward_scratch(T, B, 336, 512));
+  nested = std::max(nested, conv_bn_forward_scratch(T, B, 512, 512));
+  nested = std::max(nested, conv_bn_forward_scratch(T, B, 80, 512));
+  nested = std::max(nested, lstm_forward_scratch(T, B, 512, 32, false));
+  nested = std::max(nested, lstm_forward_scratch(T, B, 320, 512, false));
+  nested = std::max(nested, lstm_forward_scratch(T, B, 512, 1024, false));
+  nested = std::max(nested, lstm_forward_scratch(T, B, 1024, 1024, false));
+  GemmDesc lin;
+  lin.M = (int)TB; lin.N = 80; lin.Kc = 1024; lin.b_trans = 1;
+  nested = std::max(nested, gemm_scratch_bytes(lin));
+  return own + nested + (1 << 20);
+}
+
+int generator_forward(avc_context* ctx, int T, int B, const float* const* P, const float* x,
+                      const float* c_org, const float* c_trg, int training, float* mel,
+                      float* mel_post, float* codes, hipStream_t s) {
+  AVC_CHECK_ARG(T >= 32, "T must be >= 32 frames (model.py:99 concatenates an empty code list)");
+  AVC_CHECK_ARG(B >= 1, "batch must be >= 1");
+  const long TB = (long)T * B;
+  Scratch sc(ctx);
+  AVC_TAKE(x0, float, (size_t)TB * 336, sc);
+  AVC_TAKE(ba, float, (size_t)TB * 512, sc);
+  AVC_TAKE(bb, float, (size_t)TB * 512, sc);
+  AVC_TAKE(e1, float, (size_t)TB * 64, sc);
+  AVC_TAKE(e2, float, (size_t)TB * 64, sc);
+  AVC_TAKE(din, float, (size_t)TB * 320, sc);
+  AVC_TAKE(l1, float, (size_t)TB * 1024, sc);
+  AVC_TAKE(l2, float, (size_t)TB * 1024, sc);
+  AVC_TAKE(melf, float, (size_t)TB * 80, sc);
+  AVC_TAKE(postf, float, (size_t)TB * 80, sc);
+  AVC_TAKE(stat, float, 4 * 512, sc);
+  float* mean = stat;
+  float* invstd = stat + 512;
+  const float eps = 1e-5f, mom = 0.1f;
+  auto M = [&](int i) { return const_cast<float*>(P[i]); };
+
+  auto cba = [&](int base, int cin, int cout, const float* in, float* out, int act,
+                 const float* residual) {
+    return conv_bn_act_forward_impl(ctx, T, B, cin, cout, in, P[base], P[base + 1], P[base + 2],
+                                    P[base + 3], M(base + 4), M(base + 5), training, mom, eps, act,
+                                    residual, out, out, mean, invstd, s);
+  };
+
+  // Encoder (encoder.py:53-97)
+  AVC_TRY(frames_from_mel(T, B, 80, x, 256, c_org, x0, s));
+  AVC_TRY(cba(P_ENC_CONV + 0, 336, 512, x0, ba, AVC_ACT_RELU, nullptr));
+  AVC_TRY(cba(P_ENC_CONV + 6, 512, 512, ba, bb, AVC_ACT_RELU, nullptr));
+  AVC_TRY(cba(P_ENC_CONV + 12, 512, 512, bb, ba, AVC_ACT_RELU, nullptr));
+  const int EL = P_ENC_LSTM;
+  AVC_TRY(lstm_forward_impl(ctx, T, B, 512, 32, 0, ba, 512, P[EL], P[EL + 1], P[EL + 2], P[EL + 3],
+                            e1, 64, nullptr, nullptr, s));
+  AVC_TRY(lstm_forward_impl(ctx, T, B, 512, 32, 1, ba, 512, P[EL + 4], P[EL + 5], P[EL + 6],
+                            P[EL + 7], e1 + 32, 64, nullptr, nullptr, s));
+  AVC_TRY(lstm_forward_impl(ctx, T, B, 64, 32, 0, e1, 64, P[EL + 8], P[EL + 9], P[EL + 10],
+                            P[EL + 11], e2, 64, nullptr, nullptr, s));
+  AVC_TRY(lstm_forward_impl(ctx, T, B, 64, 32, 1, e1, 64, P[EL + 12], P[EL + 13], P[EL + 14],
+                            P[EL + 15], e2 + 32, 64, nullptr, nullptr, s));
+  AVC_TRY(codes_from_encoder(T, B, e2, codes, s));
+
+  // Upsample + decoder (model.py:115-127, decoder.py:58-79)
+  AVC_TRY(decoder_input(T, B, e2, 256, c_trg, din, s));
+  const int D1 = P_DEC_LSTM1;
+  AVC_TRY(lstm_forward_impl(ctx, T, B, 320, 512, 0, din, 320, P[D1], P[D1 + 1], P[D1 + 2], P[D1 + 3],
+                            ba, 512, nullptr, nullptr, s));
+  AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr));
+  AVC_TRY(cba(P_DEC_CONV + 6, 512, 512, bb, ba, AVC_ACT_RELU, nullptr));
+  AVC_TRY(cba(P_DEC_CONV + 12, 512, 512, ba, bb, AVC_ACT_RELU, nullptr));
+  const int D2 = P_DEC_LSTM2;
+  AVC_TRY(lstm_forward_impl(ctx, T, B, 512, 1024, 0, bb, 512, P[D2], P[D2 + 1], P[D2 + 2], P[D2 + 3],
+                            l1, 1024, nullptr, nullptr, s));
+  AVC_TRY(lstm_forward_impl(ctx, T, B, 1024, 1024, 0, l1, 1024, P[D2 + 4], P[D2 + 5], P[D2 + 6],
+                            P[D2 + 7], l2, 1024, nullptr, nullptr, s));
+  GemmDesc lin;
+  lin.M = (int)TB; lin.N = 80; lin.Kc = 1024;
+  lin.A = l2; lin.lda = 1024;
+  lin.B = P[P_LIN]; lin.b_trans = 1; lin.ldb = 1024;
+  lin.bias0 = P[P_LIN + 1];
+  lin.C = melf; lin.ldc = 80;
+  AVC_TRY(gemm_run(ctx, lin, s));
+
+  // Postnet + residual (postnet.py:50-63, model.py:131-132)
+  AVC_TRY(cba(P_POST + 0, 80, 512, melf, ba, AVC_ACT_TANH, nullptr));
+  AVC_TRY(cba(P_POST + 6, 512, 512, ba, bb, AVC_ACT_TANH, nullptr));
+  AVC_TRY(cba(P_POST + 12, 512, 512, bb, ba, AVC_ACT_TANH, nullptr));
+  AVC_TRY(cba(P_POST + 18, 512, 512, ba, bb, AVC_ACT_TANH, nullptr));
+  AVC_TRY(cba(P_POST + 24, 512, 80, bb, postf, AVC_ACT_NONE, melf));
+  AVC_TRY(mel_from_frames(T, B, 80, melf, mel, s));
+  AVC_TRY(mel_from_frames(T, B, 80, postf, mel_post, s));
+  return AVC_OK;
+}
+
+}  // namespace
+}  // namespace avc
+
+using namespace avc;
+
+extern "C" {
+
+int avc_abi_version(void) { return 1; }
+const char* avc_last_error(void) { return get_error(); }
+
+int avc_context_create(int device, avc_context** out) {
+  AVC_CHECK_ARG(out != nullptr, "out is NULL");
+  int n = 0;
+  AVC_HIP(hipGetDeviceCount(&n));
+  AVC_CHECK_ARG(device >= 0 && device < n, "device ordinal out of range");
+  auto* c = new avc_context();
+  c->device = device;
+  *out = c;
+  return AVC_OK;
+}
+
+int avc_context_destroy(avc_context* ctx) {
+  if (!ctx) return AVC_OK;
+  AVC_HIP(hipDeviceSynchronize());
+  for (void* p : ctx->retired) (void)hipFree(p);
+  if (ctx->base) (void)hipFree(ctx->base);
+  delete ctx;
+  return AVC_OK;
+}
+
+int avc_context_reserve(avc_context* ctx, size_t bytes) {
+  AVC_CHECK_ARG(ctx != nullptr, "ctx is NULL");
+  return ensure_arena(ctx, bytes);
+}
+
+int avc_gemm(avc_context* ctx, int M, int N, int K, const float* A, int a_trans, const float* B,
+             int b_trans, const float* bias, float* C, int accumulate, void* stream) {
+  AVC_CHECK_ARG(ctx && A && B && C, "NULL pointer");
+  GemmDesc d;
+  d.M = M; d.N = N; d.Kc = K;
+  d.A = A; d.a_trans = a_trans; d.lda = a_trans ? M : K;
+  d.B = B; d.b_trans = b_trans; d.ldb = b_trans ? K : N;
+  d.bias0 = bias; d.C = C; d.ldc = N; d.accumulate = accumulate;
+  AVC_TRY(ensure_arena(ctx, gemm_scratch_bytes(d) + 4096));
+  return gemm_run(ctx, d, S(stream));
+}
+
+int avc_conv_bn_act_forward(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                            const float* weight, const float* bias, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            int training, float momentum, float eps, int act,
+                            const float* residual, float* y_pre, float* out, float* mean,
+                            float* invstd, void* stream) {
+  AVC_CHECK_ARG(ctx && x && weight && gamma && beta && y_pre && out && mean && invstd, "NULL pointer");
+  AVC_TRY(ensure_arena(ctx, conv_bn_forward_scratch(T, B, cin, cout)));
+  return conv_bn_act_forward_impl(ctx, T, B, cin, cout, x, weight, bias, gamma, beta, running_mean,
+                                  running_var, training, momentum, eps, act, residual, y_pre, out,
+                                  mean, invstd, S(stream));
+}
+
+int avc_conv_bn_act_backward(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                             const float* weight, const float* gamma, const float* beta,
+                             const float* y_pre, const float* mean, const float* invstd,
+                             int training, int act, const float* d_out, float* d_x,
+                             float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
+                             int accumulate, void* stream) {
+  AVC_CHECK_ARG(ctx && x && weight && gamma && beta && y_pre && mean && invstd && d_out, "NULL pointer");
+  AVC_TRY(ensure_arena(ctx, conv_bn_backward_scratch(T, B, cin, cout)));
+  return conv_bn_act_backward_impl(ctx, T, B, cin, cout, x, weight, gamma, beta, y_pre, mean, invstd,
+                                   training, act, d_out, d_x, d_weight, d_bias, d_gamma, d_beta,
+                                   accumulate, S(stream));
+}
+
+int avc_lstm_forward(avc_context* ctx, int T, int B, int din, int H, int reverse, const float* x,
+                     int ldx, const float* w_ih, const float* w_hh, const float* b_ih,
+                     const float* b_hh, float* y, int ldy, float* saved_gates, float* saved_c,
+                     void* stream) {
+  AVC_CHECK_ARG(ctx && x && w_ih && w_hh && b_ih && b_hh && y, "NULL pointer");
+  AVC_CHECK_ARG((saved_gates == nullptr) == (saved_c == nullptr), "saved_gates/saved_c must both be set or both NULL");
+  AVC_TRY(ensure_arena(ctx, lstm_forward_scratch(T, B, din, H, saved_c != nullptr)));
+  return lstm_forward_impl(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, b_ih, b_hh, y, ldy,
+                           saved_gates, saved_c, S(stream));
+}
+
+int avc_lstm_backward(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                      const float* x, int ldx, const float* w_ih, const float* w_hh,
+                      const float* y, int ldy, const float* saved_gates, const float* saved_c,
+                      const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh, float* d_b_ih,
+                      float* d_b_hh, int accumulate_dx, int accumulate_dw, void* stream) {
+  AVC_CHECK_ARG(ctx && x && w_ih && w_hh && y && d_y && d_w_ih && d_w_hh && d_b_ih && d_b_hh, "NULL pointer");
+  AVC_TRY(ensure_arena(ctx, lstm_backward_scratch(T, B, din, H)));
+  return lstm_backward_impl(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, y, ldy, saved_gates,
+                            saved_c, d_y, d_x, d_w_ih, d_w_hh, d_b_ih, d_b_hh, accumulate_dx,
+                            accumulate_dw, S(stream));
+}
+
+int avc_linear_forward(avc_context* ctx, int M, int din, int dout, const float* x,
+                       const float* weight, const float* bias, float* y, void* stream) {
+  AVC_CHECK_ARG(ctx && x && weight && y, "NULL pointer");
+  GemmDesc d;
+  d.M = M; d.N = dout; d.Kc = din;
+  d.A = x; d.lda = din;
+  d.B = weight; d.b_trans = 1; d.ldb = din;
+  d.bias0 = bias; d.C = y; d.ldc = dout;
+  AVC_TRY(ensure_arena(ctx, gemm_scratch_bytes(d) + 4096));
+  return gemm_run(ctx, d, S(stream));
+}
+
+int avc_linear_backward(avc_context* ctx, int M, int din, int dout, const float* x,
+                        const float* weight, const float* d_y, float* d_x, float* d_weight,
+                        float* d_bias, int accumulate, void* stream) {
+  AVC_CHECK_ARG(ctx && x && weight && d_y, "NULL pointer");
+  GemmDesc dx;  // d_x = d_y W
+  dx.M = M; dx.N = din; dx.Kc = dout;
+  dx.A = d_y; dx.lda = dout;
+  dx.B = weight; dx.ldb = din;
+  dx.C = d_x; dx.ldc = din; dx.accumulate = accumulate;
+  GemmDesc dw;  // d_W = d_y^T x
+  dw.M = dout; dw.N = din; dw.Kc = M;
+  dw.A = d_y; dw.a_trans = 1; dw.lda = dout;
+  dw.B = x; dw.ldb = din; dw.b_rows = M;
+  dw.C = d_weight; dw.ldc = din; dw.accumulate = accumulate;
+  AVC_TRY(ensure_arena(ctx, std::max(gemm_scratch_bytes(dx), gemm_scratch_bytes(dw)) +
+                                colsum_scratch(M, dout) + 8192));
+  if (d_x) AVC_TRY(gemm_run(ctx, dx, S(stream)));
+  if (d_weight) AVC_TRY(gemm_run(ctx, dw, S(stream)));
+  if (d_bias) AVC_TRY(colsum(ctx, M, dout, d_y, dout, d_bias, accumulate, S(stream)));
+  return AVC_OK;
+}
+
+int avc_frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* emb,
+                        float* out, void* stream) {
+  AVC_CHECK_ARG(x && out && (ce == 0 || emb), "NULL pointer");
+  return frames_from_mel(T, B, cm, x, ce, emb, out, S(stream));
+}
+
+int avc_frames_from_mel_backward(int T, int B, int cm, int ce, const float* d_frames, int ld,
+                                 float* d_x, float* d_emb, int accumulate, void* stream) {
+  AVC_CHECK_ARG(d_frames != nullptr, "NULL pointer");
+  return frames_from_mel_backward(T, B, cm, ce, d_frames, ld, d_x, d_emb, accumulate, S(stream));
+}
+
+int avc_mel_from_frames(int T, int B, int cm, const float* frames, float* mel, void* stream) {
+  AVC_CHECK_ARG(frames && mel, "NULL pointer");
+  return mel_from_frames(T, B, cm, frames, mel, S(stream));
+}
+
+int avc_codes_from_encoder(int T, int B, const float* enc_out, float* codes, void* stream) {
+  AVC_CHECK_ARG(enc_out && codes, "NULL pointer");
+  return codes_from_encoder(T, B, enc_out, codes, S(stream));
+}
+
+int avc_codes_from_encoder_backward(int T, int B, const float* d_codes, float* d_enc_out,
+                                    int accumulate, void* stream) {
+  AVC_CHECK_ARG(d_codes && d_enc_out, "NULL pointer");
+  return codes_from_encoder_backward(T, B, d_codes, d_enc_out, accumulate, S(stream));
+}
+
+int avc_decoder_input(int T, int B, const float* enc_out, int ce, const float* c_trg,
+                      float* dec_in, void* stream) {
+  AVC_CHECK_ARG(enc_out && c_trg && dec_in, "NULL pointer");
+  return decoder_input(T, B, enc_out, ce, c_trg, dec_in, S(stream));
+}
+
+int avc_decoder_input_backward(int T, int B, int ce, const float* d_dec_in, float* d_enc_out,
+                               int accumulate, void* stream) {
+  AVC_CHECK_ARG(d_dec_in && d_enc_out, "NULL pointer");
+  return decoder_input_backward(T, B, ce, d_dec_in, d_enc_out, accumulate, S(stream));
+}
+
+int avc_overlap_average(int M, int C, int N, int step, const float* frames, float* out,
+                        void* stream) {
+  AVC_CHECK_ARG(frames && out, "NULL pointer");
+  return overlap_average(M, C, N, step, frames, out, S(stream));
+}
+
+int avc_loss_forward(avc_context* ctx, int kind, size_t n, const float* a, const float* b,
+                     float* loss_out, int accumulate, void* stream) {
+  AVC_CHECK_ARG(ctx && a && b && loss_out, "NULL pointer");
+  AVC_TRY(ensure_arena(ctx, loss_scratch()));
+  return loss_forward(ctx, kind, n, a, b, loss_out, accumulate, S(stream));
+}
+
+int avc_loss_backward(int kind, size_t n, const float* a, const float* b, const float* dscale,
+                      float* grad_a, float* grad_b, int accumulate, void* stream) {
+  AVC_CHECK_ARG(a && b, "NULL pointer");
+  return loss_backward(kind, n, a, b, dscale, grad_a, grad_b, accumulate, S(stream));
+}
+
+int avc_clip_adam_ema(avc_context* ctx, size_t n, float* param, float* grad, float* exp_avg,
+                      float* exp_avg_sq, float* ema, float lr, float beta1, float beta2,
+                      float eps, float weight_decay, int step, float max_norm, float ema_decay,
+                      float* norm_out, void* stream) {
+  AVC_CHECK_ARG(ctx && param && grad && exp_avg && exp_avg_sq, "NULL pointer");
+  AVC_TRY(ensure_arena(ctx, optimizer_scratch()));
+  return clip_adam_ema(ctx, n, param, grad, exp_avg, exp_avg_sq, ema, lr, beta1, beta2, eps,
+                       weight_decay, step, max_norm, ema_decay, norm_out, S(stream));
+}
+
+int avc_generator_param_count(void) { return P_COUNT; }
+
+int avc_generator_forward(avc_context* ctx, int T, int B, const float* const* params,
+                          const float* x, const float* c_org, const float* c_trg, int training,
+                          float* mel, float* mel_post, float* codes, void* stream) {
+  AVC_CHECK_ARG(ctx && params && x && c_org && c_trg && mel && mel_post && codes, "NULL pointer");
+  for (int i = 0; i < P_COUNT; ++i) AVC_CHECK_ARG(params[i] != nullptr, "NULL parameter pointer");
+  AVC_TRY(ensure_arena(ctx, gen_scratch(T, B)));
+  return generator_forward(ctx, T, B, params, x, c_org, c_trg, training, mel, mel_post, codes,
+                           S(stream));
+}
+
+}  // extern "C"

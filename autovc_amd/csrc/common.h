@@ -1,0 +1,101 @@
+// Shared helpers for the AutoVC HIP library (gfx950 / MI355X only).
+//
+// Conventions used by every kernel in this library:
+//   * activations live in HBM time-major: row r = t*B + b of a [T*B][C] row-major matrix
+//     ("frame rows"), so a Conv1d tap shift is a row shift of +-B and BatchNorm statistics
+//     are plain column reductions;
+//   * every pointer is borrowed from the caller (torch owns all tensors); scratch comes from
+//     the avc_context arena;
+//   * errors are reported through a thread-local message and a non-zero status.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/autovc_hip.h"
+
+namespace avc {
+
+void set_error(const std::string& msg);
+const char* get_error();
+
+#define AVC_CHECK_ARG(cond, msg)                         \
+  do {                                                   \
+    if (!(cond)) {                                       \
+      ::avc::set_error(std::string("invalid argument: ") + (msg)); \
+      return AVC_ERR_INVALID;                            \
+    }                                                    \
+  } while (0)
+
+#define AVC_HIP(expr)                                                            \
+  do {                                                                           \
+    hipError_t _e = (expr);                                                      \
+    if (_e != hipSuccess) {                                                      \
+      ::avc::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));        \
+      return AVC_ERR_HIP;                                                        \
+    }                                                                            \
+  } while (0)
+
+#define AVC_LAUNCH_CHECK()                                                       \
+  do {                                                                           \
+    hipError_t _e = hipGetLastError();                                           \
+    if (_e != hipSuccess) {                                                      \
+      ::avc::set_error(std::string("kernel launch: ") + hipGetErrorString(_e));   \
+      return AVC_ERR_HIP;                                                        \
+    }                                                                            \
+  } while (0)
+
+#define AVC_TRY(expr)                  \
+  do {                                 \
+    int _s = (expr);                   \
+    if (_s != AVC_OK) return _s;       \
+  } while (0)
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace avc
+
+// Device arena owned by a context.  Scratch is handed out stack-like inside one API call
+// (mark/release); every call on a context is stream-ordered on the stream it was given, so a
+// region is never reused while an earlier kernel on that stream could still read it.
+struct avc_context {
+  int device = 0;
+  std::vector<void*> retired;   // grown-out blocks, freed at destroy
+  char* base = nullptr;
+  size_t cap = 0;
+  size_t top = 0;
+};
+
+namespace avc {
+
+struct Scratch {
+  avc_context* ctx;
+  size_t mark;
+  explicit Scratch(avc_context* c) : ctx(c), mark(c->top) {}
+  ~Scratch() { ctx->top = mark; }
+  // returns nullptr (and sets error) when the arena is exhausted
+  template <typename T>
+  T* take(size_t count) {
+    size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
+    if (ctx->top + bytes > ctx->cap) {
+      set_error("context arena exhausted: need " + std::to_string(ctx->top + bytes) +
+                " bytes, have " + std::to_string(ctx->cap) + " (call avc_context_reserve)");
+      return nullptr;
+    }
+    T* p = reinterpret_cast<T*>(ctx->base + ctx->top);
+    ctx->top += bytes;
+    return p;
+  }
+};
+
+#define AVC_TAKE(var, T, n, scratch)                 \
+  T* var = (scratch).template take<T>(n);            \
+  if (var == nullptr) return AVC_ERR_WORKSPACE
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+}  // namespace avc

@@ -1,0 +1,142 @@
+// Conv1d(k=5, pad=2) + BatchNorm1d + activation, forward and backward.
+//
+// Reference composition: ConvNorm (net_layers.py:39-49) -> nn.BatchNorm1d -> relu
+// (encoder.py:69-70, decoder.py:69-70) or tanh (postnet.py:54-55) or nothing (postnet.py:61).
+//
+// Forward  : one implicit-GEMM launch (5 taps accumulated inside the K loop, bias and the
+//            per-channel BN partial sums fused in the epilogue), one tiny statistics kernel,
+//            one normalise+activate pass.
+// Backward : BN backward (reduce + apply), dgrad as the same 5-tap implicit GEMM on the
+//            tap-flipped weights, wgrad as 5 batched GEMMs over all frames (split-K).
+#include <algorithm>
+
+#include "elementwise.h"
+#include "kernels.h"
+
+namespace avc {
+namespace {
+
+// Wt[(tau*cin + ci)*cout + co] = W[(co*cin + ci)*5 + tau]   (forward B operand, [K][N])
+// Wd[(tau*cout + co)*cin + ci] = W[(co*cin + ci)*5 + 4-tau] (dgrad B operand, [K][N])
+__global__ void conv_weight_fwd_kernel(const float* __restrict__ W, float* __restrict__ Wt, int cin,
+                                       int cout) {
+  const long total = 5L * cin * cout;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % cout);
+    const long r = i / cout;
+    const int ci = (int)(r % cin), tau = (int)(r / cin);
+    Wt[i] = W[((long)co * cin + ci) * 5 + tau];
+  }
+}
+
+__global__ void conv_weight_dgrad_kernel(const float* __restrict__ W, float* __restrict__ Wd, int cin,
+                                         int cout) {
+  const long total = 5L * cin * cout;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cin);
+    const long r = i / cin;
+    const int co = (int)(r % cout), tau = (int)(r / cout);
+    Wd[i] = W[((long)co * cin + ci) * 5 + (4 - tau)];
+  }
+}
+
+inline int ew_blocks(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
+
+GemmDesc conv_fwd_desc(int T, int B, int cin, int cout, const float* x, const float* Wt,
+                       const float* bias, float* y) {
+  GemmDesc g;
+  g.M = T * B; g.N = cout; g.Kc = cin; g.ntaps = 5;
+  g.A = x; g.lda = cin; g.a_rows = (long)T * B; g.a_shift0 = -2L * B; g.a_tapshift = B;
+  g.B = Wt; g.ldb = cout; g.b_rows = cin; g.b_tapoff = (long)cin * cout;
+  g.C = y; g.ldc = cout; g.bias0 = bias;
+  return g;
+}
+
+}  // namespace
+
+size_t conv_bn_forward_scratch(int T, int B, int cin, int cout) {
+  const int bm = gemm_stats_rows(T * B, cout);
+  const size_t parts = (size_t)((T * B + bm - 1) / bm) * 2 * cout;
+  return (5UL * cin * cout + parts) * sizeof(float) + 1024;
+}
+
+int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                             const float* weight, const float* bias, const float* gamma,
+                             const float* beta, float* running_mean, float* running_var,
+                             int training, float momentum, float eps, int act,
+                             const float* residual, float* y_pre, float* out, float* mean,
+                             float* invstd, hipStream_t s) {
+  AVC_CHECK_ARG(T > 0 && B > 0, "conv: empty input");
+  AVC_CHECK_ARG(cin % 4 == 0 && cout % 4 == 0, "conv: channel counts must be multiples of 4");
+  AVC_CHECK_ARG(training || (running_mean && running_var), "conv: eval mode needs running stats");
+  AVC_CHECK_ARG(!training || (long)T * B > 1, "BatchNorm in training mode needs more than 1 value per channel");
+  Scratch sc(ctx);
+  AVC_TAKE(wt, float, 5UL * cin * cout, sc);
+  conv_weight_fwd_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wt, cin, cout);
+  AVC_LAUNCH_CHECK();
+  GemmDesc g = conv_fwd_desc(T, B, cin, cout, x, wt, bias, y_pre);
+  float* stats = nullptr;
+  int nparts = 0;
+  if (training) {
+    const int bm = gemm_stats_rows(T * B, cout);
+    nparts = (T * B + bm - 1) / bm;
+    AVC_TAKE(st, float, (size_t)nparts * 2 * cout, sc);
+    stats = st;
+    g.stats = stats;
+  }
+  AVC_TRY(gemm_run(ctx, g, s));
+  AVC_TRY(bn_finalize(cout, nparts, stats, (double)T * B, training, momentum, eps, running_mean,
+                      running_var, mean, invstd, s));
+  AVC_TRY(bn_apply((long)T * B, cout, y_pre, mean, invstd, gamma, beta, act, residual, out, s));
+  return AVC_OK;
+}
+
+size_t conv_bn_backward_scratch(int T, int B, int cin, int cout) {
+  const size_t TB = (size_t)T * B;
+  GemmDesc w;
+  w.M = cout; w.N = cin; w.Kc = (int)TB; w.a_trans = 1; w.nz = 5;
+  GemmDesc dg;
+  dg.M = (int)TB; dg.N = cin; dg.Kc = cout; dg.ntaps = 5;
+  return (TB * cout + 5UL * cin * cout) * sizeof(float) + bn_backward_scratch((int)TB, cout) +
+         colsum_scratch((int)TB, cout) + std::max(gemm_scratch_bytes(w), gemm_scratch_bytes(dg)) + 2048;
+}
+
+int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                              const float* weight, const float* gamma, const float* beta,
+                              const float* y_pre, const float* mean, const float* invstd,
+                              int training, int act, const float* d_out, float* d_x,
+                              float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
+                              int accumulate, hipStream_t s) {
+  AVC_CHECK_ARG(T > 0 && B > 0, "conv_backward: empty input");
+  AVC_CHECK_ARG(cin % 4 == 0 && cout % 4 == 0, "conv_backward: channels must be multiples of 4");
+  const long TB = (long)T * B;
+  Scratch sc(ctx);
+  AVC_TAKE(dy, float, (size_t)TB * cout, sc);
+  AVC_TRY(bn_backward(ctx, (int)TB, cout, d_out, y_pre, mean, invstd, gamma, beta, act, training,
+                      d_gamma, d_beta, accumulate, dy, s));
+  if (d_bias) AVC_TRY(colsum(ctx, (int)TB, cout, dy, cout, d_bias, accumulate, s));
+  if (d_x) {
+    AVC_TAKE(wd, float, 5UL * cin * cout, sc);
+    conv_weight_dgrad_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wd, cin, cout);
+    AVC_LAUNCH_CHECK();
+    GemmDesc g;
+    g.M = (int)TB; g.N = cin; g.Kc = cout; g.ntaps = 5;
+    g.A = dy; g.lda = cout; g.a_rows = TB; g.a_shift0 = -2L * B; g.a_tapshift = B;
+    g.B = wd; g.ldb = cin; g.b_rows = cout; g.b_tapoff = (long)cout * cin;
+    g.C = d_x; g.ldc = cin; g.accumulate = accumulate;
+    AVC_TRY(gemm_run(ctx, g, s));
+  }
+  if (d_weight) {
+    // dW[co][ci][tau] = sum_r dY[r][co] * x[r + (tau-2)B][ci]
+    GemmDesc g;
+    g.M = cout; g.N = cin; g.Kc = (int)TB;
+    g.A = dy; g.a_trans = 1; g.lda = cout;
+    g.B = x; g.ldb = cin; g.b_rows = TB; g.b_shift0 = -2L * B; g.b_zshift = B;
+    g.nz = 5; g.c_zoff = 1;
+    g.C = d_weight; g.ldc = 5L * cin; g.ldc_col = 5; g.accumulate = accumulate;
+    AVC_TRY(gemm_run(ctx, g, s));
+  }
+  return AVC_OK;
+}
+
+}  // namespace avc

@@ -1,0 +1,40 @@
+// Internal declarations of the bandwidth-bound kernels (elementwise.hip).
+#pragma once
+#include "common.h"
+
+namespace avc {
+
+int bn_finalize(int C, int nparts, const float* stats, double count, int training, float momentum,
+                float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s);
+int bn_apply(long M, int C, const float* y, const float* mean, const float* invstd,
+             const float* gamma, const float* beta, int act, const float* residual, float* out,
+             hipStream_t s);
+size_t bn_backward_scratch(int M, int C);
+int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* y,
+                const float* mean, const float* invstd, const float* gamma, const float* beta,
+                int act, int training, float* d_gamma, float* d_beta, int accumulate, float* dy,
+                hipStream_t s);
+int frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* emb, float* out,
+                    hipStream_t s);
+int frames_from_mel_backward(int T, int B, int cm, int ce, const float* df, int ld, float* dx,
+                             float* demb, int accumulate, hipStream_t s);
+int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s);
+int codes_from_encoder(int T, int B, const float* enc, float* codes, hipStream_t s);
+int codes_from_encoder_backward(int T, int B, const float* dcodes, float* denc, int accumulate,
+                                hipStream_t s);
+int decoder_input(int T, int B, const float* enc, int ce, const float* ctrg, float* out,
+                  hipStream_t s);
+int decoder_input_backward(int T, int B, int ce, const float* dd, float* denc, int accumulate,
+                           hipStream_t s);
+int overlap_average(int M, int C, int N, int step, const float* fr, float* out, hipStream_t s);
+size_t loss_scratch();
+int loss_forward(avc_context* ctx, int kind, size_t n, const float* a, const float* b, float* out,
+                 int accumulate, hipStream_t s);
+int loss_backward(int kind, size_t n, const float* a, const float* b, const float* dscale,
+                  float* ga, float* gb, int accumulate, hipStream_t s);
+size_t optimizer_scratch();
+int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, float* v, float* ema,
+                  float lr, float b1, float b2, float eps, float wd, int step, float max_norm,
+                  float ema_decay, float* norm_out, hipStream_t s);
+
+}  // namespace avc

@@ -1,0 +1,588 @@
+// Bandwidth-bound kernels of the Generator: column reductions, BatchNorm statistics /
+// normalisation / backward, the layout glue around the encoder bottleneck (concat, down- and
+// up-sampling of the content codes), the reconstruction losses and the fused
+// clip + Adam + EMA optimizer pass.  All of them stream time-major [T*B][C] rows with
+// consecutive lanes on consecutive channels (coalesced), and every reduction is two-pass with
+// a fixed summation order (deterministic, fp64 final combine).
+#include <algorithm>
+#include <cmath>
+
+#include "kernels.h"
+#include "elementwise.h"
+
+namespace avc {
+namespace {
+
+inline int ew_blocks(long n, int per = 256) { return (int)std::max<long>(1, std::min<long>((n + per - 1) / per, 16384)); }
+
+__device__ __forceinline__ float act_fwd(float a, int act) {
+  if (act == AVC_ACT_RELU) return a > 0.f ? a : 0.f;
+  if (act == AVC_ACT_TANH) return tanhf(a);
+  return a;
+}
+// derivative of act at pre-activation a
+__device__ __forceinline__ float act_bwd(float a, int act) {
+  if (act == AVC_ACT_RELU) return a > 0.f ? 1.f : 0.f;
+  if (act == AVC_ACT_TANH) {
+    const float t = tanhf(a);
+    return 1.f - t * t;
+  }
+  return 1.f;
+}
+
+// ---- column sums -------------------------------------------------------------------------
+__global__ void colsum_partial_kernel(int M, int N, const float* __restrict__ X, long ld,
+                                      int rows_per, float* __restrict__ part) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int m0 = blockIdx.y * rows_per, m1 = min(M, m0 + rows_per);
+  float s = 0.f;
+  for (int m = m0; m < m1; ++m) s += X[(long)m * ld + n];
+  part[(long)blockIdx.y * N + n] = s;
+}
+
+__global__ void colsum_final_kernel(int R, int N, const float* __restrict__ part,
+                                    float* __restrict__ out, int accumulate) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int r = 0; r < R; ++r) s += part[(long)r * N + n];
+  out[n] = accumulate ? out[n] + (float)s : (float)s;
+}
+
+void colsum_geometry(int M, int N, int& R, int& rows_per) {
+  const int cb = (N + 255) / 256;
+  R = std::max(1, std::min(M, std::max(1, 1024 / cb)));
+  rows_per = (M + R - 1) / R;
+  R = (M + rows_per - 1) / rows_per;
+}
+
+// ---- BatchNorm ---------------------------------------------------------------------------
+__global__ void bn_finalize_kernel(int C, int nparts, const float* __restrict__ stats, double count,
+                                   int training, float momentum, float eps,
+                                   float* __restrict__ rmean, float* __restrict__ rvar,
+                                   float* __restrict__ mean_out, float* __restrict__ invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (training) {
+    double s = 0.0, s2 = 0.0;
+    for (int p = 0; p < nparts; ++p) {
+      s += stats[((long)p * 2 + 0) * C + c];
+      s2 += stats[((long)p * 2 + 1) * C + c];
+    }
+    const double mean = s / count;
+    double var = s2 / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    if (rvar) {
+      const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+  } else {
+    mean_out[c] = rmean[c];
+    invstd_out[c] = (float)(1.0 / sqrt((double)rvar[c] + (double)eps));
+  }
+}
+
+__global__ void bn_apply_kernel(long M, int C, const float* __restrict__ y,
+                                const float* __restrict__ mean, const float* __restrict__ invstd,
+                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                int act, const float* __restrict__ residual, float* __restrict__ out) {
+  const long total4 = M * C / 4;
+  for (long i4 = blockIdx.x * (long)blockDim.x + threadIdx.x; i4 < total4;
+       i4 += (long)gridDim.x * blockDim.x) {
+    const int c = (int)((i4 * 4) % C);
+    float4 v = reinterpret_cast<const float4*>(y)[i4];
+    float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = (r[e] - mean[c + e]) * invstd[c + e] * gamma[c + e] + beta[c + e];
+      r[e] = act_fwd(a, act);
+    }
+    if (residual) {
+      const float4 q = reinterpret_cast<const float4*>(residual)[i4];
+      r[0] += q.x; r[1] += q.y; r[2] += q.z; r[3] += q.w;
+    }
+    reinterpret_cast<float4*>(out)[i4] = make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
+// partial sums over a row range of dA = d_out * act'(a) and dA * xhat  -> part[r][2][C]
+__global__ void bn_bwd_reduce_kernel(int M, int C, const float* __restrict__ dout,
+                                     const float* __restrict__ y, const float* __restrict__ mean,
+                                     const float* __restrict__ invstd,
+                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                     int act, int rows_per, float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int m0 = blockIdx.y * rows_per, m1 = min(M, m0 + rows_per);
+  const float mu = mean[c], is = invstd[c], g = gamma[c], bt = beta[c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int m = m0; m < m1; ++m) {
+    const long i = (long)m * C + c;
+    const float xh = (y[i] - mu) * is;
+    const float dA = dout[i] * act_bwd(xh * g + bt, act);
+    s1 += dA;
+    s2 += dA * xh;
+  }
+  part[((long)blockIdx.y * 2 + 0) * C + c] = s1;
+  part[((long)blockIdx.y * 2 + 1) * C + c] = s2;
+}
+
+__global__ void bn_bwd_final_kernel(int R, int C, const float* __restrict__ part,
+                                    float* __restrict__ sums, float* __restrict__ d_gamma,
+                                    float* __restrict__ d_beta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int r = 0; r < R; ++r) {
+    s1 += part[((long)r * 2 + 0) * C + c];
+    s2 += part[((long)r * 2 + 1) * C + c];
+  }
+  sums[c] = (float)s1;
+  sums[C + c] = (float)s2;
+  if (d_beta) d_beta[c] = accumulate ? d_beta[c] + (float)s1 : (float)s1;
+  if (d_gamma) d_gamma[c] = accumulate ? d_gamma[c] + (float)s2 : (float)s2;
+}
+
+__global__ void bn_bwd_apply_kernel(long M, int C, const float* __restrict__ dout,
+                                    const float* __restrict__ y, const float* __restrict__ mean,
+                                    const float* __restrict__ invstd,
+                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    int act, int training, const float* __restrict__ sums,
+                                    float inv_count, float* __restrict__ dy) {
+  const long total = M * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float is = invstd[c], g = gamma[c];
+    const float xh = (y[i] - mean[c]) * is;
+    const float dA = dout[i] * act_bwd(xh * g + beta[c], act);
+    float v;
+    if (training) v = g * is * (dA - sums[c] * inv_count - xh * sums[C + c] * inv_count);
+    else v = g * is * dA;
+    dy[i] = v;
+  }
+}
+
+// ---- layout glue -------------------------------------------------------------------------
+__global__ void frames_from_mel_kernel(int T, int B, int cm, const float* __restrict__ x, int ce,
+                                       const float* __restrict__ emb, float* __restrict__ out) {
+  const int C = cm + ce;
+  const long total = (long)T * B * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long r = i / C;
+    const int b = (int)(r % B), t = (int)(r / B);
+    out[i] = c < cm ? x[((long)b * cm + c) * T + t] : emb[(long)b * ce + (c - cm)];
+  }
+}
+
+// d_x[b][c][t] (+)= d_frames[(t*B+b)*ld + c]
+__global__ void mel_grad_kernel(int T, int B, int cm, const float* __restrict__ df, int ld,
+                                float* __restrict__ dx, int accumulate) {
+  const long total = (long)B * cm * T;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T);
+    const long bc = i / T;
+    const int c = (int)(bc % cm), b = (int)(bc / cm);
+    const float v = df[((long)t * B + b) * ld + c];
+    dx[i] = accumulate ? dx[i] + v : v;
+  }
+}
+
+__global__ void emb_grad_kernel(int T, int B, int cm, int ce, const float* __restrict__ df, int ld,
+                                float* __restrict__ demb, int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * ce) return;
+  const int b = i / ce, c = i % ce;
+  double s = 0.0;
+  for (int t = 0; t < T; ++t) s += df[((long)t * B + b) * ld + cm + c];
+  demb[i] = accumulate ? demb[i] + (float)s : (float)s;
+}
+
+__global__ void mel_from_frames_kernel(int T, int B, int cm, const float* __restrict__ fr,
+                                       float* __restrict__ mel) {
+  const long total = (long)B * cm * T;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(i % T);
+    const long bc = i / T;
+    const int c = (int)(bc % cm), b = (int)(bc / cm);
+    mel[i] = fr[((long)t * B + b) * cm + c];
+  }
+}
+
+// codes[b][32*i + d]: i < nA -> forward half at t = 32i+31; else backward half at t = 32(i-nA)
+__global__ void codes_kernel(int T, int B, const float* __restrict__ enc, float* __restrict__ codes,
+                             int backward, int accumulate, float* __restrict__ denc) {
+  const int nA = T / 32, nB = (T + 31) / 32, L = 32 * (nA + nB);
+  const long total = (long)B * L;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(idx / L), q = (int)(idx % L);
+    const int i = q >> 5, d = q & 31;
+    long src;
+    if (i < nA) src = ((long)(32 * i + 31) * B + b) * 64 + d;
+    else src = ((long)(32 * (i - nA)) * B + b) * 64 + 32 + d;
+    if (!backward) codes[idx] = enc[src];
+    else denc[src] = accumulate ? denc[src] + codes[idx] : codes[idx];
+  }
+}
+
+__global__ void decoder_input_kernel(int T, int B, const float* __restrict__ enc, int ce,
+                                     const float* __restrict__ ctrg, float* __restrict__ out) {
+  const int C = 64 + ce, nA = T / 32;
+  const long total = (long)T * B * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long r = i / C;
+    const int b = (int)(r % B), t = (int)(r / B);
+    float v;
+    if (c < 32) {
+      const int blk = min(t / 32, nA - 1);
+      v = enc[((long)(32 * blk + 31) * B + b) * 64 + c];
+    } else if (c < 64) {
+      v = enc[((long)(32 * (t / 32)) * B + b) * 64 + c];
+    } else {
+      v = ctrg[(long)b * ce + (c - 64)];
+    }
+    out[i] = v;
+  }
+}
+
+// one thread per (b, stream s in {fwd,bwd}, code index i, dim d)
+__global__ void decoder_input_bwd_kernel(int T, int B, int ce, const float* __restrict__ dd,
+                                         float* __restrict__ denc) {
+  const int C = 64 + ce, nA = T / 32, nB = (T + 31) / 32;
+  const long total = (long)B * (nA + nB) * 32;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(idx & 31);
+    const long rest = idx >> 5;
+    const int q = (int)(rest % (nA + nB)), b = (int)(rest / (nA + nB));
+    int t0, t1, col, trow;
+    if (q < nA) {  // forward code q covers [32q, 32q+32) (last one also the tail)
+      t0 = 32 * q;
+      t1 = (q == nA - 1) ? T : 32 * q + 32;
+      col = d;
+      trow = 32 * q + 31;
+    } else {
+      const int j = q - nA;
+      t0 = 32 * j;
+      t1 = min(T, 32 * j + 32);
+      col = 32 + d;
+      trow = 32 * j;
+    }
+    float s = 0.f;
+    for (int t = t0; t < t1; ++t) s += dd[((long)t * B + b) * C + col];
+    denc[((long)trow * B + b) * 64 + col] += s;
+  }
+}
+
+// out[c][tau] = mean over slices i covering tau of frames[i][c][tau - i*step], skipping NaNs
+// (model.py:428-437: NaN padding + nanmean)
+__global__ void overlap_average_kernel(int M, int C, int N, int step, const float* __restrict__ fr,
+                                       float* __restrict__ out) {
+  const int L = (M - 1) * step + N;
+  const long total = (long)C * L;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(idx / L), tau = (int)(idx % L);
+    float s = 0.f;
+    int cnt = 0;
+    for (int i = 0; i < M; ++i) {
+      const int k = tau - i * step;
+      if (k < 0 || k >= N) continue;
+      const float v = fr[((long)i * C + c) * N + k];
+      if (v != v) continue;
+      s += v;
+      ++cnt;
+    }
+    out[idx] = cnt ? s / (float)cnt : __int_as_float(0x7fc00000);
+  }
+}
+
+// ---- losses ------------------------------------------------------------------------------
+__global__ void loss_partial_kernel(int kind, long n, const float* __restrict__ a,
+                                    const float* __restrict__ b, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float d = a[i] - b[i];
+    s += kind == 0 ? (double)(d * d) : (double)fabsf(d);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void loss_final_kernel(int nparts, const double* __restrict__ part, double inv_n,
+                                  float* __restrict__ out, int accumulate) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int p = 0; p < nparts; ++p) s += part[p];
+  const float v = (float)(s * inv_n);
+  out[0] = accumulate ? out[0] + v : v;
+}
+
+__global__ void loss_grad_kernel(int kind, long n, const float* __restrict__ a,
+                                 const float* __restrict__ b, const float* __restrict__ dscale,
+                                 float scale, float* __restrict__ ga, float* __restrict__ gb,
+                                 int accumulate) {
+  const float sc = scale * (dscale ? dscale[0] : 1.f);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float d = a[i] - b[i];
+    float g;
+    if (kind == 0) g = 2.f * d * sc;
+    else g = (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * sc;
+    if (ga) ga[i] = accumulate ? ga[i] + g : g;
+    if (gb) gb[i] = accumulate ? gb[i] - g : -g;
+  }
+}
+
+// ---- optimizer ---------------------------------------------------------------------------
+__global__ void sumsq_partial_kernel(long n, const float* __restrict__ g, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const double v = g[i];
+    s += v * v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void clip_coef_kernel(int nparts, const double* __restrict__ part, float max_norm,
+                                 float* __restrict__ norm_out, float* __restrict__ coef) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int p = 0; p < nparts; ++p) s += part[p];
+  const float norm = (float)sqrt(s);
+  if (norm_out) norm_out[0] = norm;
+  float c = 1.f;
+  if (max_norm > 0.f) {
+    c = max_norm / (norm + 1e-6f);
+    if (c > 1.f) c = 1.f;
+  }
+  coef[0] = c;
+}
+
+__global__ void adam_ema_kernel(long n, float* __restrict__ p, float* __restrict__ g,
+                                float* __restrict__ m, float* __restrict__ v, float* __restrict__ ema,
+                                const float* __restrict__ coef, float lr, float b1, float b2,
+                                float eps, float wd, float step_size, float bc2_sqrt, float ema_decay,
+                                int clip) {
+  const float c = clip ? coef[0] : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    if (clip) {
+      gi *= c;
+      g[i] = gi;
+    }
+    float pi = p[i];
+    if (wd != 0.f) gi += wd * pi;
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // torch foreach Adam: exp_avg.lerp_(g, 1-b1)
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi -= step_size * (mi / denom);
+    p[i] = pi;
+    if (ema) ema[i] = ema_decay * ema[i] + (1.f - ema_decay) * pi;
+  }
+}
+
+}  // namespace
+
+// ---- internal API --------------------------------------------------------------------------
+size_t colsum_scratch(int M, int N) {
+  int R, rp;
+  colsum_geometry(M, N, R, rp);
+  return (size_t)R * N * sizeof(float) + 256;
+}
+
+int colsum(avc_context* ctx, int M, int N, const float* X, long ld, float* out, int accumulate,
+           hipStream_t s) {
+  int R, rp;
+  colsum_geometry(M, N, R, rp);
+  Scratch sc(ctx);
+  AVC_TAKE(part, float, (size_t)R * N, sc);
+  colsum_partial_kernel<<<dim3((N + 255) / 256, R), 256, 0, s>>>(M, N, X, ld, rp, part);
+  colsum_final_kernel<<<(N + 255) / 256, 256, 0, s>>>(R, N, part, out, accumulate);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int bn_finalize(int C, int nparts, const float* stats, double count, int training, float momentum,
+                float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s) {
+  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(C, nparts, stats, count, training, momentum,
+                                                     eps, rmean, rvar, mean, invstd);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int bn_apply(long M, int C, const float* y, const float* mean, const float* invstd,
+             const float* gamma, const float* beta, int act, const float* residual, float* out,
+             hipStream_t s) {
+  AVC_CHECK_ARG(C % 4 == 0, "bn_apply: channels must be a multiple of 4");
+  bn_apply_kernel<<<ew_blocks(M * C / 4), 256, 0, s>>>(M, C, y, mean, invstd, gamma, beta, act,
+                                                       residual, out);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+size_t bn_backward_scratch(int M, int C) {
+  int R, rp;
+  colsum_geometry(M, C, R, rp);
+  return (size_t)R * 2 * C * sizeof(float) + 2 * C * sizeof(float) + 512;
+}
+
+int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* y,
+                const float* mean, const float* invstd, const float* gamma, const float* beta,
+                int act, int training, float* d_gamma, float* d_beta, int accumulate, float* dy,
+                hipStream_t s) {
+  int R, rp;
+  colsum_geometry(M, C, R, rp);
+  Scratch sc(ctx);
+  AVC_TAKE(part, float, (size_t)R * 2 * C, sc);
+  AVC_TAKE(sums, float, (size_t)2 * C, sc);
+  bn_bwd_reduce_kernel<<<dim3((C + 255) / 256, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
+                                                                beta, act, rp, part);
+  bn_bwd_final_kernel<<<(C + 255) / 256, 256, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate);
+  bn_bwd_apply_kernel<<<ew_blocks((long)M * C), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
+                                                              beta, act, training, sums,
+                                                              1.f / (float)M, dy);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* emb, float* out,
+                    hipStream_t s) {
+  frames_from_mel_kernel<<<ew_blocks((long)T * B * (cm + ce)), 256, 0, s>>>(T, B, cm, x, ce, emb, out);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int frames_from_mel_backward(int T, int B, int cm, int ce, const float* df, int ld, float* dx,
+                             float* demb, int accumulate, hipStream_t s) {
+  if (dx) mel_grad_kernel<<<ew_blocks((long)B * cm * T), 256, 0, s>>>(T, B, cm, df, ld, dx, accumulate);
+  if (demb && ce > 0)
+    emb_grad_kernel<<<(B * ce + 255) / 256, 256, 0, s>>>(T, B, cm, ce, df, ld, demb, accumulate);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s) {
+  mel_from_frames_kernel<<<ew_blocks((long)B * cm * T), 256, 0, s>>>(T, B, cm, fr, mel);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int codes_from_encoder(int T, int B, const float* enc, float* codes, hipStream_t s) {
+  AVC_CHECK_ARG(T >= 32, "content codes need T >= 32 frames (model.py:99 cat of an empty list)");
+  const long total = (long)B * 32 * (T / 32 + (T + 31) / 32);
+  codes_kernel<<<ew_blocks(total), 256, 0, s>>>(T, B, enc, codes, 0, 0, nullptr);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int codes_from_encoder_backward(int T, int B, const float* dcodes, float* denc, int accumulate,
+                                hipStream_t s) {
+  AVC_CHECK_ARG(T >= 32, "content codes need T >= 32 frames");
+  if (!accumulate) AVC_HIP(hipMemsetAsync(denc, 0, sizeof(float) * (size_t)T * B * 64, s));
+  const long total = (long)B * 32 * (T / 32 + (T + 31) / 32);
+  codes_kernel<<<ew_blocks(total), 256, 0, s>>>(T, B, nullptr, const_cast<float*>(dcodes), 1, 1, denc);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int decoder_input(int T, int B, const float* enc, int ce, const float* ctrg, float* out,
+                  hipStream_t s) {
+  AVC_CHECK_ARG(T >= 32, "decoder input needs T >= 32 frames (model.py:115-119)");
+  decoder_input_kernel<<<ew_blocks((long)T * B * (64 + ce)), 256, 0, s>>>(T, B, enc, ce, ctrg, out);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int decoder_input_backward(int T, int B, int ce, const float* dd, float* denc, int accumulate,
+                           hipStream_t s) {
+  AVC_CHECK_ARG(T >= 32, "decoder input needs T >= 32 frames");
+  if (!accumulate) AVC_HIP(hipMemsetAsync(denc, 0, sizeof(float) * (size_t)T * B * 64, s));
+  const long total = (long)B * (T / 32 + (T + 31) / 32) * 32;
+  decoder_input_bwd_kernel<<<ew_blocks(total), 256, 0, s>>>(T, B, ce, dd, denc);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int overlap_average(int M, int C, int N, int step, const float* fr, float* out, hipStream_t s) {
+  AVC_CHECK_ARG(M >= 1 && C >= 1 && N >= 1 && step >= 0, "overlap_average: bad shape");
+  const long total = (long)C * ((M - 1) * step + N);
+  overlap_average_kernel<<<ew_blocks(total), 256, 0, s>>>(M, C, N, step, fr, out);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+size_t loss_scratch() { return 1024 * sizeof(double) + 256; }
+
+int loss_forward(avc_context* ctx, int kind, size_t n, const float* a, const float* b,
+                 float* out, int accumulate, hipStream_t s) {
+  AVC_CHECK_ARG(kind == 0 || kind == 1, "loss kind must be 0 (MSE) or 1 (L1)");
+  AVC_CHECK_ARG(n > 0, "loss over an empty tensor");
+  Scratch sc(ctx);
+  const int nb = (int)std::min<size_t>(1024, (n + 255) / 256);
+  AVC_TAKE(part, double, (size_t)nb, sc);
+  loss_partial_kernel<<<nb, 256, 0, s>>>(kind, (long)n, a, b, part);
+  loss_final_kernel<<<1, 64, 0, s>>>(nb, part, 1.0 / (double)n, out, accumulate);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int loss_backward(int kind, size_t n, const float* a, const float* b, const float* dscale,
+                  float* ga, float* gb, int accumulate, hipStream_t s) {
+  AVC_CHECK_ARG(kind == 0 || kind == 1, "loss kind must be 0 (MSE) or 1 (L1)");
+  loss_grad_kernel<<<ew_blocks((long)n), 256, 0, s>>>(kind, (long)n, a, b, dscale,
+                                                      1.0f / (float)n, ga, gb, accumulate);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+size_t optimizer_scratch() { return 2048 * sizeof(double) + 512; }
+
+int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, float* v, float* ema,
+                  float lr, float b1, float b2, float eps, float wd, int step, float max_norm,
+                  float ema_decay, float* norm_out, hipStream_t s) {
+  AVC_CHECK_ARG(step >= 1, "adam step counter starts at 1");
+  Scratch sc(ctx);
+  const int nb = (int)std::min<size_t>(2048, (n + 255) / 256);
+  AVC_TAKE(part, double, (size_t)nb, sc);
+  AVC_TAKE(coef, float, 4, sc);
+  const bool need_norm = max_norm > 0.f || norm_out != nullptr;
+  if (need_norm) {
+    sumsq_partial_kernel<<<nb, 256, 0, s>>>((long)n, g, part);
+    clip_coef_kernel<<<1, 64, 0, s>>>(nb, part, max_norm, norm_out, coef);
+  }
+  const double bc1 = 1.0 - std::pow((double)b1, step);
+  const double bc2 = 1.0 - std::pow((double)b2, step);
+  adam_ema_kernel<<<ew_blocks((long)n), 256, 0, s>>>((long)n, p, g, m, v, ema, coef, lr, b1, b2, eps,
+                                                     wd, (float)(lr / bc1), (float)std::sqrt(bc2),
+                                                     ema_decay, max_norm > 0.f ? 1 : 0);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+}  // namespace avc

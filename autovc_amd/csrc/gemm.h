@@ -1,0 +1,38 @@
+// fp32 MFMA GEMM with implicit Conv1d taps — the contraction engine behind every Conv1d,
+// LSTM input projection, Linear and weight-gradient product of the Generator.
+#pragma once
+#include "common.h"
+
+namespace avc {
+
+// C(m, n) = act( sum_tap sum_k A_tap(m, k) * B_tap(k, n) + bias0[n] + bias1[n] )
+//
+// A (a_trans = 0): element (m, k) of tap tau at A[(m + a_shift0 + tau*a_tapshift) * lda + k];
+//                  rows outside [0, a_rows) read as zero (Conv1d zero padding in time).
+// A (a_trans = 1): element (m, k) at A[k * lda + m]  (operand stored K-major, e.g. dY^T).
+// B (b_trans = 0): element (k, n) at B[(k + b_shift) * ldb + n] + tau*b_tapoff, storage
+//                  rows outside [0, b_rows) read as zero; b_shift = b_shift0 + z*b_zshift.
+// B (b_trans = 1): element (k, n) at B[n * ldb + k] + tau*b_tapoff.
+// Grid z enumerates nz independent products (A += z*a_zoff, C += z*c_zoff, B shifted) times
+// nsplit K-splits; with nsplit > 1 raw partial sums go to `slab` and gemm_run() reduces them.
+struct GemmDesc {
+  int M = 0, N = 0, Kc = 0, ntaps = 1;
+  const float* A = nullptr; long lda = 0; long a_rows = 0; long a_shift0 = 0; long a_tapshift = 0;
+  int a_trans = 0;
+  const float* B = nullptr; long ldb = 0; long b_rows = 0; long b_shift0 = 0; long b_zshift = 0;
+  long b_tapoff = 0; int b_trans = 0;
+  int nz = 1; long a_zoff = 0; long c_zoff = 0;
+  float* C = nullptr; long ldc = 0; long ldc_col = 1; int accumulate = 0;
+  const float* bias0 = nullptr; const float* bias1 = nullptr; int act = AVC_ACT_NONE;
+  float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
+  int stats_bm = 0;         // filled by gemm_run: rows per stats partial
+};
+
+// Launch (with automatic tile and split-K choice).  Uses ctx scratch for split-K slabs.
+int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split = 0);
+// Rows covered by one stats partial for a problem of M rows (so callers can size `stats`).
+int gemm_stats_rows(int M, int N);
+// Scratch bytes gemm_run may take for this problem.
+size_t gemm_scratch_bytes(const GemmDesc& d);
+
+}  // namespace avc

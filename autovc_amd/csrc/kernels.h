@@ -1,0 +1,47 @@
+// Internal (non-ABI) entry points shared between the library's translation units.
+#pragma once
+#include "common.h"
+#include "gemm.h"
+
+namespace avc {
+
+// ---- reductions / elementwise (elementwise.hip) ----
+// out[n] (+)= sum_m X[m*ld + n]   (fixed-order, deterministic)
+int colsum(avc_context* ctx, int M, int N, const float* X, long ld, float* out, int accumulate,
+           hipStream_t s);
+size_t colsum_scratch(int M, int N);
+
+// ---- LSTM (lstm.hip) ----
+int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                      const float* x, int ldx, const float* w_ih, const float* w_hh,
+                      const float* b_ih, const float* b_hh, float* y, int ldy,
+                      float* saved_gates, float* saved_c, hipStream_t s);
+size_t lstm_forward_scratch(int T, int B, int din, int H, bool training);
+int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                       const float* x, int ldx, const float* w_ih, const float* w_hh,
+                       const float* y, int ldy, const float* saved_gates, const float* saved_c,
+                       const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh,
+                       float* d_b_ih, float* d_b_hh, int accumulate_dx, int accumulate_dw,
+                       hipStream_t s);
+size_t lstm_backward_scratch(int T, int B, int din, int H);
+
+// ---- conv + BN (convbn.hip) ----
+int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                             const float* weight, const float* bias, const float* gamma,
+                             const float* beta, float* running_mean, float* running_var,
+                             int training, float momentum, float eps, int act,
+                             const float* residual, float* y_pre, float* out, float* mean,
+                             float* invstd, hipStream_t s);
+size_t conv_bn_forward_scratch(int T, int B, int cin, int cout);
+int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                              const float* weight, const float* gamma, const float* beta,
+                              const float* y_pre, const float* mean, const float* invstd,
+                              int training, int act, const float* d_out, float* d_x,
+                              float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
+                              int accumulate, hipStream_t s);
+size_t conv_bn_backward_scratch(int T, int B, int cin, int cout);
+
+// arena growth (only legal when no scratch is outstanding)
+int ensure_arena(avc_context* ctx, size_t bytes);
+
+}  // namespace avc

@@ -1,0 +1,550 @@
+// LSTM layer forward / backward-through-time for gfx950.
+//
+// Gate math follows nn.LSTM (gates i,f,g,o; c' = f*c + i*g; h' = o*tanh(c'); zero initial
+// state) as used by the reference at encoder.py:51, decoder.py:37 and decoder.py:53.
+//
+// Large H (512, 1024 — decoder lstm1/lstm2):
+//   * the input projection for all T steps is one MFMA GEMM (gemm.hip) into Gx [T*B][4H];
+//   * each time step is ONE fused launch: the recurrent product h_{t-1} . W_hh^T on fp32 MFMA
+//     (16x16x4, the K range split over the block's waves, reduced through LDS) with the gate
+//     nonlinearities and the c/h update in the epilogue.  To let one block own complete gate
+//     quadruples, W_hh/W_ih rows are permuted so that gate-columns of 4 hidden units are
+//     adjacent: permuted p = blk*16 + gate*4 + u  <->  PyTorch row gate*H + blk*4 + u.
+//   * backward: one fused launch per step computes dh_rec = dG_{t+1} . W_hh (MFMA, W_hh^T
+//     permuted copy) and the gate/cell gradients; weight gradients are three GEMMs over all
+//     steps afterwards.
+// Small H (32 — encoder BiLSTM): one single-wave workgroup per (utterance, direction) walks
+//   all T steps with W_hh held in registers and h broadcast through LDS (latency-bound path).
+#include <algorithm>
+
+#include "kernels.h"
+#include "timing.h"
+
+namespace avc {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ __forceinline__ int perm_to_orig(int p, int H) {
+  const int blk = p >> 4, g = (p >> 2) & 3, u = p & 3;
+  return g * H + blk * 4 + u;
+}
+
+__global__ void permute_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, int H,
+                                    int D) {
+  const long total = 4L * H * D;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int p = (int)(idx / D);
+    const int c = (int)(idx - (long)p * D);
+    dst[idx] = src[(long)perm_to_orig(p, H) * D + c];
+  }
+}
+
+__global__ void permute_vec_kernel(const float* __restrict__ src, float* __restrict__ dst, int H) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < 4 * H) dst[p] = src[perm_to_orig(p, H)];
+}
+
+// WT[j][p] = W[orig(p)][j]  (W: [4H][H] PyTorch layout -> [H][4H] permuted, K-contiguous for
+// the backward recurrent product).  32x32 LDS-tiled transpose.
+__global__ void transpose_permute_kernel(const float* __restrict__ W, float* __restrict__ WT, int H) {
+  __shared__ float tile[32][33];
+  const int p0 = blockIdx.x * 32, j0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: ty 0..7
+  for (int r = ty; r < 32; r += 8) {
+    const int p = p0 + r;
+    tile[r][tx] = W[(long)perm_to_orig(p, H) * H + j0 + tx];
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) WT[(long)(j0 + r) * 4 * H + p0 + tx] = tile[tx][r];
+}
+
+// dst[orig(p)][:] (+)= src[p][:]
+__global__ void unpermute_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, int H,
+                                      int D, int accumulate) {
+  const long total = 4L * H * D;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int p = (int)(idx / D);
+    const int c = (int)(idx - (long)p * D);
+    float* o = dst + (long)perm_to_orig(p, H) * D + c;
+    if (accumulate) *o += src[idx]; else *o = src[idx];
+  }
+}
+
+__global__ void unpermute_vec2_kernel(const float* __restrict__ src, float* __restrict__ d0,
+                                      float* __restrict__ d1, int H, int accumulate) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= 4 * H) return;
+  const int o = perm_to_orig(p, H);
+  if (accumulate) {
+    if (d0) d0[o] += src[p];
+    if (d1) d1[o] += src[p];
+  } else {
+    if (d0) d0[o] = src[p];
+    if (d1) d1[o] = src[p];
+  }
+}
+
+struct StepArgs {
+  int B, H, K, kw;
+  const float* A; long lda;  // h_{t-1} (fwd) or dG of the next-processed step (bwd); null => 0
+  const float* W;            // [ncols][K] K-contiguous rows
+  // forward
+  const float* gx; const float* c_prev; float* c_out; float* h_out; long ldh_out; float* gates_out;
+  // backward
+  const float* dy; long lddy; const float* gates; const float* c_cur; const float* c_prv;
+  float* dc; float* dg_out;
+};
+
+constexpr int G = 4;  // 16-deep k-chunks loaded per batch (64 k per wave per batch)
+
+template <int MB, bool BWD>
+__global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
+  constexpr int RT = MB / 16;
+  extern __shared__ float part[];  // [NW][MB][16]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, NW = blockDim.x >> 6;
+  const int cb = blockIdx.x, rb = blockIdx.y;
+  const int l15 = lane & 15, lk = 4 * (lane >> 4);
+
+  f32x4 acc0[RT], acc1[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+    acc0[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc1[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (a.A != nullptr) {
+    const int kbeg = w * a.kw;
+    const float* wrow = a.W + (long)(cb * 16 + l15) * a.K + kbeg + lk;
+    const float* arow[RT];
+    bool aok[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int b = rb * MB + r * 16 + l15;
+      aok[r] = b < a.B;
+      arow[r] = a.A + (long)(aok[r] ? b : 0) * a.lda + kbeg + lk;
+    }
+    for (int c0 = 0; c0 < a.kw; c0 += 16 * G) {
+      float4 wv[G], av[G][RT];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        wv[g] = *reinterpret_cast<const float4*>(wrow + c0 + 16 * g);
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          av[g][r] = aok[r] ? *reinterpret_cast<const float4*>(arow[r] + c0 + 16 * g)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          f32x4& acc = (g & 1) ? acc1[r] : acc0[r];
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r].x, wv[g].x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r].y, wv[g].y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r].z, wv[g].z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r].w, wv[g].w, acc, 0, 0, 0);
+        }
+    }
+  }
+  // 16x16 accumulator layout: column = lane&15, rows 4*(lane>>4) + e
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      part[(w * MB + r * 16 + lk + e) * 16 + l15] = acc0[r][e] + acc1[r][e];
+  __syncthreads();
+
+  const int H = a.H;
+  if (!BWD) {
+    for (int cell = tid; cell < MB * 4; cell += blockDim.x) {
+      const int row = cell >> 2, u = cell & 3;
+      const int b = rb * MB + row;
+      if (b >= a.B) continue;
+      float z[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float s = a.gx[(long)b * 4 * H + cb * 16 + g * 4 + u];
+        for (int ww = 0; ww < NW; ++ww) s += part[(ww * MB + row) * 16 + g * 4 + u];
+        z[g] = s;
+      }
+      const float ig = sigmoidf_(z[0]), fg = sigmoidf_(z[1]), gg = tanhf(z[2]), og = sigmoidf_(z[3]);
+      const int j = cb * 4 + u;
+      const float cp = a.c_prev ? a.c_prev[(long)b * H + j] : 0.f;
+      const float c = fg * cp + ig * gg;
+      const float h = og * tanhf(c);
+      a.c_out[(long)b * H + j] = c;
+      a.h_out[(long)b * a.ldh_out + j] = h;
+      if (a.gates_out) {
+        float* go = a.gates_out + (long)b * 4 * H + cb * 16 + u;
+        go[0] = ig;
+        go[4] = fg;
+        go[8] = gg;
+        go[12] = og;
+      }
+    }
+  } else {
+    for (int cell = tid; cell < MB * 16; cell += blockDim.x) {
+      const int row = cell >> 4, jj = cell & 15;
+      const int b = rb * MB + row;
+      if (b >= a.B) continue;
+      const int j = cb * 16 + jj;
+      float dh = a.dy[(long)b * a.lddy + j];
+      for (int ww = 0; ww < NW; ++ww) dh += part[(ww * MB + row) * 16 + jj];
+      const long pb = (long)b * 4 * H + (j >> 2) * 16 + (j & 3);
+      const float ig = a.gates[pb], fg = a.gates[pb + 4], gg = a.gates[pb + 8], og = a.gates[pb + 12];
+      const float c = a.c_cur[(long)b * H + j];
+      const float cp = a.c_prv ? a.c_prv[(long)b * H + j] : 0.f;
+      const float tc = tanhf(c);
+      const float dct = dh * og * (1.f - tc * tc) + a.dc[(long)b * H + j];
+      a.dc[(long)b * H + j] = dct * fg;
+      a.dg_out[pb] = dct * gg * ig * (1.f - ig);
+      a.dg_out[pb + 4] = dct * cp * fg * (1.f - fg);
+      a.dg_out[pb + 8] = dct * ig * (1.f - gg * gg);
+      a.dg_out[pb + 12] = dh * tc * og * (1.f - og);
+    }
+  }
+}
+
+struct StepCfg {
+  int mb, nw;
+};
+
+StepCfg step_cfg(int B, int ncolblocks, int K) {
+  StepCfg c;
+  if (B <= 16) c.mb = 16;
+  else if ((long)ncolblocks * ((B + 63) / 64) >= 240) c.mb = 64;
+  else if ((long)ncolblocks * ((B + 31) / 32) >= 240) c.mb = 32;
+  else c.mb = 16;
+  c.nw = std::max(1, std::min(16, K / 64));
+  while (K % (c.nw * 64) != 0) --c.nw;
+  return c;
+}
+
+void launch_step(const StepCfg& cfg, bool bwd, dim3 grid, const StepArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)cfg.nw * cfg.mb * 16 * sizeof(float);
+  const int threads = cfg.nw * 64;
+  const int cls = bwd ? TC_LSTM_STEP_BWD : TC_LSTM_STEP_FWD;
+  hipEvent_t ev = timing_begin(cls, s);
+  if (!bwd) {
+    if (cfg.mb == 64) lstm_step_kernel<64, false><<<grid, threads, lds, s>>>(a);
+    else if (cfg.mb == 32) lstm_step_kernel<32, false><<<grid, threads, lds, s>>>(a);
+    else lstm_step_kernel<16, false><<<grid, threads, lds, s>>>(a);
+  } else {
+    if (cfg.mb == 64) lstm_step_kernel<64, true><<<grid, threads, lds, s>>>(a);
+    else if (cfg.mb == 32) lstm_step_kernel<32, true><<<grid, threads, lds, s>>>(a);
+    else lstm_step_kernel<16, true><<<grid, threads, lds, s>>>(a);
+  }
+  if (ev) {
+    // recurrent product B x (4H or H) x K plus the W_hh slice streamed once per step
+    const double flops = a.A ? 2.0 * a.B * (double)a.K * (bwd ? a.H : 4.0 * a.H) : 0.0;
+    const double bytes = 4.0 * 4.0 * (double)a.H * a.H;  // one pass over W_hh (4H x H fp32)
+    timing_end(cls, ev, s, flops, bytes);
+  }
+}
+
+// ---- H = 32 persistent single-wave kernels (encoder BiLSTM) ------------------------------
+
+__global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, int reverse,
+                                                        const float* __restrict__ gx,
+                                                        const float* __restrict__ whh,
+                                                        float* __restrict__ y, long ldy,
+                                                        float* __restrict__ gates_out,
+                                                        float* __restrict__ c_out) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float hs[32];
+  float w0[32], w1[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    w0[k] = whh[lane * 32 + k];
+    w1[k] = whh[(lane + 64) * 32 + k];
+  }
+  if (lane < 32) hs[lane] = 0.f;
+  float c = 0.f;
+  __syncthreads();
+  for (int s = 0; s < T; ++s) {
+    const int t = reverse ? T - 1 - s : s;
+    const long row = (long)t * B + b;
+    float z0 = gx[row * 128 + lane], z1 = gx[row * 128 + lane + 64];
+    float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+    for (int k4 = 0; k4 < 8; ++k4) {
+      const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
+      d0 += w0[4 * k4] * h4.x + w0[4 * k4 + 1] * h4.y + w0[4 * k4 + 2] * h4.z + w0[4 * k4 + 3] * h4.w;
+      d1 += w1[4 * k4] * h4.x + w1[4 * k4 + 1] * h4.y + w1[4 * k4 + 2] * h4.z + w1[4 * k4 + 3] * h4.w;
+    }
+    z0 += d0;
+    z1 += d1;
+    const float a0 = sigmoidf_(z0);                              // i (lane<32) or f
+    const float a1 = lane < 32 ? tanhf(z1) : sigmoidf_(z1);      // g (lane<32) or o
+    const float fg = __shfl(a0, (lane + 32) & 63);
+    const float og = __shfl(a1, (lane + 32) & 63);
+    if (lane < 32) {
+      c = fg * c + a0 * a1;
+      const float h = og * tanhf(c);
+      y[row * ldy + lane] = h;
+      if (c_out) c_out[row * 32 + lane] = c;
+      if (gates_out) {
+        float* g = gates_out + row * 128;
+        g[lane] = a0;
+        g[32 + lane] = fg;
+        g[64 + lane] = a1;
+        g[96 + lane] = og;
+      }
+      hs[lane] = h;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void lstm32_bwd_kernel(int T, int B, int reverse,
+                                                        const float* __restrict__ whh,
+                                                        const float* __restrict__ gates,
+                                                        const float* __restrict__ cs,
+                                                        const float* __restrict__ dy, long lddy,
+                                                        float* __restrict__ dg) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int j = lane & 31, half = lane >> 5;
+  __shared__ __attribute__((aligned(16))) float dgs[128];
+  float wc[64];
+#pragma unroll
+  for (int q = 0; q < 64; ++q) wc[q] = whh[(half * 64 + q) * 32 + j];
+  dgs[lane] = 0.f;
+  dgs[lane + 64] = 0.f;
+  float dc = 0.f;
+  __syncthreads();
+  for (int s = T - 1; s >= 0; --s) {
+    const int t = reverse ? T - 1 - s : s;
+    const long row = (long)t * B + b;
+    float part = 0.f;
+#pragma unroll
+    for (int q4 = 0; q4 < 16; ++q4) {
+      const float4 g4 = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
+      part += wc[4 * q4] * g4.x + wc[4 * q4 + 1] * g4.y + wc[4 * q4 + 2] * g4.z + wc[4 * q4 + 3] * g4.w;
+    }
+    part += __shfl_xor(part, 32);
+    float dzi = 0.f, dzf = 0.f, dzg = 0.f, dzo = 0.f;
+    if (lane < 32) {
+      const float dh = dy[row * lddy + j] + part;
+      const float* g = gates + row * 128;
+      const float ig = g[j], fg = g[32 + j], gg = g[64 + j], og = g[96 + j];
+      const float c = cs[row * 32 + j];
+      const int tp = reverse ? t + 1 : t - 1;
+      const float cp = s > 0 ? cs[((long)tp * B + b) * 32 + j] : 0.f;
+      const float tc = tanhf(c);
+      const float dct = dh * og * (1.f - tc * tc) + dc;
+      dc = dct * fg;
+      dzi = dct * gg * ig * (1.f - ig);
+      dzf = dct * cp * fg * (1.f - fg);
+      dzg = dct * ig * (1.f - gg * gg);
+      dzo = dh * tc * og * (1.f - og);
+      float* o = dg + row * 128;
+      o[j] = dzi;
+      o[32 + j] = dzf;
+      o[64 + j] = dzg;
+      o[96 + j] = dzo;
+    }
+    __syncthreads();
+    if (lane < 32) {
+      dgs[j] = dzi;
+      dgs[32 + j] = dzf;
+      dgs[64 + j] = dzg;
+      dgs[96 + j] = dzo;
+    }
+    __syncthreads();
+  }
+}
+
+inline int ew_blocks(long n) { return (int)std::min<long>((n + 255) / 256, 8192); }
+
+}  // namespace
+
+size_t lstm_forward_scratch(int T, int B, int din, int H, bool training) {
+  const size_t f = sizeof(float);
+  size_t s = (size_t)T * B * 4 * H * f + 1024;
+  if (H != 32) s += (size_t)4 * H * (din + H + 2) * f + (training ? 0 : (size_t)2 * B * H * f) + 2048;
+  GemmDesc d;
+  d.M = T * B; d.N = 4 * H; d.Kc = din;
+  return s + gemm_scratch_bytes(d);
+}
+
+int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                      const float* x, int ldx, const float* w_ih, const float* w_hh,
+                      const float* b_ih, const float* b_hh, float* y, int ldy,
+                      float* saved_gates, float* saved_c, hipStream_t s) {
+  AVC_CHECK_ARG(T > 0 && B > 0 && din > 0, "lstm: empty problem");
+  AVC_CHECK_ARG(H == 32 || (H % 64 == 0), "lstm: H must be 32 or a multiple of 64");
+  AVC_CHECK_ARG(din % 4 == 0 && ldx % 4 == 0, "lstm: din/ldx must be multiples of 4");
+  Scratch sc(ctx);
+  const long TB = (long)T * B;
+  AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
+
+  GemmDesc g;
+  g.M = (int)TB; g.N = 4 * H; g.Kc = din;
+  g.A = x; g.lda = ldx; g.a_rows = TB;
+  g.b_trans = 1; g.ldb = din;
+  g.C = gx; g.ldc = 4 * H;
+
+  if (H == 32) {
+    g.B = w_ih; g.bias0 = b_ih; g.bias1 = b_hh;
+    AVC_TRY(gemm_run(ctx, g, s));
+    hipEvent_t ev = timing_begin(TC_LSTM32, s);
+    lstm32_fwd_kernel<<<B, 64, 0, s>>>(T, B, reverse, gx, w_hh, y, ldy, saved_gates, saved_c);
+    AVC_LAUNCH_CHECK();
+    if (ev) timing_end(TC_LSTM32, ev, s, 2.0 * T * B * 128.0 * 32.0, 4.0 * T * B * (128.0 + 32.0));
+    return AVC_OK;
+  }
+
+  AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
+  AVC_TAKE(whh_p, float, (size_t)4 * H * H, sc);
+  AVC_TAKE(bih_p, float, (size_t)4 * H, sc);
+  AVC_TAKE(bhh_p, float, (size_t)4 * H, sc);
+  permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w_ih, wih_p, H, din);
+  permute_rows_kernel<<<ew_blocks(4L * H * H), 256, 0, s>>>(w_hh, whh_p, H, H);
+  permute_vec_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(b_ih, bih_p, H);
+  permute_vec_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(b_hh, bhh_p, H);
+  AVC_LAUNCH_CHECK();
+  g.B = wih_p; g.bias0 = bih_p; g.bias1 = bhh_p;
+  AVC_TRY(gemm_run(ctx, g, s));
+
+  float* cpp = nullptr;
+  if (!saved_c) {
+    AVC_TAKE(tmp, float, (size_t)2 * B * H, sc);
+    cpp = tmp;
+  }
+  const StepCfg cfg = step_cfg(B, H / 4, H);
+  dim3 grid(H / 4, (B + cfg.mb - 1) / cfg.mb);
+  for (int st = 0; st < T; ++st) {
+    const int t = reverse ? T - 1 - st : st;
+    const int tp = reverse ? t + 1 : t - 1;
+    StepArgs a{};
+    a.B = B; a.H = H; a.K = H; a.kw = H / cfg.nw;
+    a.A = st > 0 ? y + (long)tp * B * ldy : nullptr;
+    a.lda = ldy;
+    a.W = whh_p;
+    a.gx = gx + (long)t * B * 4 * H;
+    if (saved_c) {
+      a.c_prev = st > 0 ? saved_c + (long)tp * B * H : nullptr;
+      a.c_out = saved_c + (long)t * B * H;
+    } else {
+      a.c_prev = st > 0 ? cpp + (long)((st - 1) & 1) * B * H : nullptr;
+      a.c_out = cpp + (long)(st & 1) * B * H;
+    }
+    a.h_out = y + (long)t * B * ldy;
+    a.ldh_out = ldy;
+    a.gates_out = saved_gates ? saved_gates + (long)t * B * 4 * H : nullptr;
+    launch_step(cfg, false, grid, a, s);
+  }
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+size_t lstm_backward_scratch(int T, int B, int din, int H) {
+  const size_t f = sizeof(float);
+  const size_t TB = (size_t)T * B;
+  size_t s = TB * 4 * H * f + (size_t)B * H * f + (size_t)4 * H * (din + H) * 2 * f +
+             (size_t)4 * H * f + 8192;
+  GemmDesc d1;  // dW_ih
+  d1.M = 4 * H; d1.N = din; d1.Kc = (int)TB; d1.a_trans = 1;
+  GemmDesc d2 = d1; d2.N = H;
+  GemmDesc d3; d3.M = (int)TB; d3.N = din; d3.Kc = 4 * H;
+  size_t gs = std::max(gemm_scratch_bytes(d1), std::max(gemm_scratch_bytes(d2), gemm_scratch_bytes(d3)));
+  return s + gs + colsum_scratch((int)TB, 4 * H);
+}
+
+int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                       const float* x, int ldx, const float* w_ih, const float* w_hh,
+                       const float* y, int ldy, const float* saved_gates, const float* saved_c,
+                       const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh,
+                       float* d_b_ih, float* d_b_hh, int accumulate_dx, int accumulate_dw,
+                       hipStream_t s) {
+  AVC_CHECK_ARG(T > 0 && B > 0 && din > 0, "lstm_backward: empty problem");
+  AVC_CHECK_ARG(H == 32 || (H % 64 == 0), "lstm_backward: H must be 32 or a multiple of 64");
+  AVC_CHECK_ARG(saved_gates && saved_c, "lstm_backward: saved gates/cells required");
+  Scratch sc(ctx);
+  const long TB = (long)T * B;
+  AVC_TAKE(dg, float, (size_t)TB * 4 * H, sc);
+  const bool small = H == 32;
+  const float* wih_use = w_ih;
+  float* dwih_dst = d_w_ih;
+  float* dwhh_dst = d_w_hh;
+  int acc_w = accumulate_dw;
+
+  if (small) {
+    lstm32_bwd_kernel<<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
+    AVC_LAUNCH_CHECK();
+  } else {
+    AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
+    AVC_TAKE(whhT_p, float, (size_t)4 * H * H, sc);
+    AVC_TAKE(dc, float, (size_t)B * H, sc);
+    permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w_ih, wih_p, H, din);
+    transpose_permute_kernel<<<dim3(4 * H / 32, H / 32), 256, 0, s>>>(w_hh, whhT_p, H);
+    AVC_HIP(hipMemsetAsync(dc, 0, sizeof(float) * B * H, s));
+    AVC_LAUNCH_CHECK();
+    const StepCfg cfg = step_cfg(B, H / 16, 4 * H);
+    dim3 grid(H / 16, (B + cfg.mb - 1) / cfg.mb);
+    for (int st = T - 1; st >= 0; --st) {
+      const int t = reverse ? T - 1 - st : st;
+      const int tn = reverse ? t - 1 : t + 1;  // time index processed after t in the forward pass
+      const int tp = reverse ? t + 1 : t - 1;
+      StepArgs a{};
+      a.B = B; a.H = H; a.K = 4 * H; a.kw = 4 * H / cfg.nw;
+      a.A = st < T - 1 ? dg + (long)tn * B * 4 * H : nullptr;
+      a.lda = 4 * H;
+      a.W = whhT_p;
+      a.dy = d_y + (long)t * B * ldy;
+      a.lddy = ldy;
+      a.gates = saved_gates + (long)t * B * 4 * H;
+      a.c_cur = saved_c + (long)t * B * H;
+      a.c_prv = st > 0 ? saved_c + (long)tp * B * H : nullptr;
+      a.dc = dc;
+      a.dg_out = dg + (long)t * B * 4 * H;
+      launch_step(cfg, true, grid, a, s);
+    }
+    AVC_LAUNCH_CHECK();
+    wih_use = wih_p;
+    AVC_TAKE(dwih_p, float, (size_t)4 * H * din, sc);
+    AVC_TAKE(dwhh_p, float, (size_t)4 * H * H, sc);
+    dwih_dst = dwih_p;
+    dwhh_dst = dwhh_p;
+    acc_w = 0;
+  }
+
+  // weight gradients: dW_ih = dG^T x ; dW_hh = dG^T h_prev (h_prev = y shifted one step)
+  GemmDesc g1;
+  g1.M = 4 * H; g1.N = din; g1.Kc = (int)TB;
+  g1.A = dg; g1.a_trans = 1; g1.lda = 4 * H;
+  g1.B = x; g1.ldb = ldx; g1.b_rows = TB;
+  g1.C = dwih_dst; g1.ldc = din; g1.accumulate = acc_w;
+  AVC_TRY(gemm_run(ctx, g1, s));
+  GemmDesc g2 = g1;
+  g2.N = H;
+  g2.B = y; g2.ldb = ldy; g2.b_shift0 = reverse ? B : -B;
+  g2.C = dwhh_dst; g2.ldc = H;
+  AVC_TRY(gemm_run(ctx, g2, s));
+
+  if (small) {
+    AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, d_b_ih, accumulate_dw, s));
+    AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, d_b_hh, accumulate_dw, s));
+  } else {
+    AVC_TAKE(db_p, float, (size_t)4 * H, sc);
+    AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, db_p, 0, s));
+    unpermute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(dwih_dst, d_w_ih, H, din, accumulate_dw);
+    unpermute_rows_kernel<<<ew_blocks(4L * H * H), 256, 0, s>>>(dwhh_dst, d_w_hh, H, H, accumulate_dw);
+    unpermute_vec2_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(db_p, d_b_ih, d_b_hh, H, accumulate_dw);
+    AVC_LAUNCH_CHECK();
+  }
+
+  if (d_x) {
+    GemmDesc g3;
+    g3.M = (int)TB; g3.N = din; g3.Kc = 4 * H;
+    g3.A = dg; g3.lda = 4 * H; g3.a_rows = TB;
+    g3.B = wih_use; g3.ldb = din;
+    g3.b_trans = small ? 0 : 0;
+    g3.C = d_x; g3.ldc = din; g3.accumulate = accumulate_dx;
+    AVC_TRY(gemm_run(ctx, g3, s));
+  }
+  return AVC_OK;
+}
+
+}  // namespace avc

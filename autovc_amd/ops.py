@@ -1,0 +1,335 @@
+"""Autograd Functions over the HIP C-ABI: one Function per layer of the Generator.
+
+Activations between layers are time-major frame matrices [T*B][C] (see include/autovc_hip.h);
+only the mels at the boundary keep the reference's (B, 80, T) layout.  Every forward/backward
+is a call into libautovc_hip.so on the caller's current stream; nothing here computes on the
+CPU or through PyTorch kernels except autograd's own gradient bookkeeping.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import ACT_NONE, ACT_RELU, ACT_TANH, call, ptr
+
+F32 = 4  # bytes
+
+
+def _dev(t):
+    return t.device
+
+
+def _ctx(t):
+    return _lib.context(t.device)
+
+
+def _stream(t):
+    return _lib.stream(t.device)
+
+
+def _empty(shape, like):
+    return torch.empty(shape, dtype=torch.float32, device=like.device)
+
+
+def _c(t):
+    return None if t is None else t.contiguous()
+
+
+class FramesFromMel(torch.autograd.Function):
+    """x (B,cm,T) [+ emb (B,ce) broadcast over T] -> frames [T*B][cm+ce]
+    (encoder.py:65-66 concat; model.py:127 transpose)."""
+
+    @staticmethod
+    def forward(ctx, x, emb):
+        x = x.contiguous()
+        B, cm, T = x.shape
+        ce = 0 if emb is None else emb.shape[1]
+        emb = _c(emb)
+        out = _empty((T * B, cm + ce), x)
+        call("avc_frames_from_mel", T, B, cm, ptr(x), ce, ptr(emb), ptr(out), _stream(x))
+        ctx.dims = (T, B, cm, ce)
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        T, B, cm, ce = ctx.dims
+        d = d.contiguous()
+        dx = _empty((B, cm, T), d) if ctx.needs_input_grad[0] else None
+        de = _empty((B, ce), d) if (ce and ctx.needs_input_grad[1]) else None
+        if dx is not None or de is not None:
+            call("avc_frames_from_mel_backward", T, B, cm, ce, ptr(d), cm + ce, ptr(dx), ptr(de), 0,
+                 _stream(d))
+        return dx, de
+
+
+class MelFromFrames(torch.autograd.Function):
+    """frames [T*B][cm] -> (B, cm, T)  (decoder output transpose, model.py:127)."""
+
+    @staticmethod
+    def forward(ctx, fr, T, B):
+        fr = fr.contiguous()
+        cm = fr.shape[1]
+        out = _empty((B, cm, T), fr)
+        call("avc_mel_from_frames", T, B, cm, ptr(fr), ptr(out), _stream(fr))
+        ctx.dims = (T, B, cm)
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        T, B, cm = ctx.dims
+        d = d.contiguous()
+        dfr = _empty((T * B, cm), d)
+        call("avc_frames_from_mel", T, B, cm, ptr(d), 0, None, ptr(dfr), _stream(d))
+        return dfr, None, None
+
+
+class ConvBNAct(torch.autograd.Function):
+    """ConvNorm(k=5,p=2) -> BatchNorm1d -> act [+ residual]  (net_layers.py:39-49,
+    encoder.py:69-70, decoder.py:69-70, postnet.py:54-61, model.py:131-132)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, running_mean, running_var, training, momentum,
+                eps, act, residual, T, B):
+        x = x.contiguous()
+        cout, cin, _ = weight.shape
+        y_pre = _empty((T * B, cout), x)
+        out = _empty((T * B, cout), x)
+        mean = _empty((cout,), x)
+        invstd = _empty((cout,), x)
+        call("avc_conv_bn_act_forward", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
+             ptr(_c(bias)), ptr(gamma), ptr(beta), ptr(running_mean), ptr(running_var),
+             int(training), float(momentum), float(eps), act, ptr(_c(residual)), ptr(y_pre), ptr(out),
+             ptr(mean), ptr(invstd), _stream(x))
+        ctx.save_for_backward(x, weight, gamma, beta, y_pre, mean, invstd)
+        ctx.cfg = (T, B, cin, cout, int(training), act, residual is not None, bias is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        x, weight, gamma, beta, y_pre, mean, invstd = ctx.saved_tensors
+        T, B, cin, cout, training, act, has_res, has_bias = ctx.cfg
+        d_out = d_out.contiguous()
+        ng = ctx.needs_input_grad
+        dx = _empty(x.shape, x) if ng[0] else None
+        dw = _empty(weight.shape, x) if ng[1] else None
+        db = _empty((cout,), x) if (has_bias and ng[2]) else None
+        dg = _empty((cout,), x) if ng[3] else None
+        dbt = _empty((cout,), x) if ng[4] else None
+        call("avc_conv_bn_act_backward", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
+             ptr(gamma), ptr(beta), ptr(y_pre), ptr(mean), ptr(invstd), training, act, ptr(d_out),
+             ptr(dx), ptr(dw), ptr(db), ptr(dg), ptr(dbt), 0, _stream(x))
+        d_res = d_out if (has_res and ng[11]) else None
+        return dx, dw, db, dg, dbt, None, None, None, None, None, None, d_res, None, None
+
+
+def _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, reverse, save, T, B):
+    H = w_hh.shape[1]
+    din = x.shape[1]
+    gates = _empty((T * B, 4 * H), x) if save else None
+    cst = _empty((T * B, H), x) if save else None
+    call("avc_lstm_forward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
+         ptr(w_hh.contiguous()), ptr(b_ih), ptr(b_hh), y.data_ptr() + col * F32, ldy, ptr(gates),
+         ptr(cst), _stream(x))
+    return gates, cst
+
+
+def _lstm_bwd(x, w_ih, w_hh, y, col, ldy, gates, cst, d_y, d_x, reverse, acc, T, B):
+    H = w_hh.shape[1]
+    din = x.shape[1]
+    dwi = torch.empty_like(w_ih)
+    dwh = torch.empty_like(w_hh)
+    dbi = _empty((4 * H,), x)
+    dbh = _empty((4 * H,), x)
+    call("avc_lstm_backward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
+         ptr(w_hh.contiguous()), y.data_ptr() + col * F32, ldy, ptr(gates), ptr(cst),
+         d_y.data_ptr() + col * F32, ptr(d_x), ptr(dwi), ptr(dwh), ptr(dbi), ptr(dbh), int(acc), 0,
+         _stream(x))
+    return dwi, dwh, dbi, dbh
+
+
+class LSTMLayer(torch.autograd.Function):
+    """One unidirectional nn.LSTM layer, zero initial state (decoder.py:37,53)."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, T, B, save):
+        x = x.contiguous()
+        H = w_hh.shape[1]
+        y = _empty((T * B, H), x)
+        gates, cst = _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, 0, H, False, save, T, B)
+        if save:
+            ctx.save_for_backward(x, w_ih, w_hh, y, gates, cst)
+        ctx.dims = (T, B)
+        return y
+
+    @staticmethod
+    def backward(ctx, d_y):
+        x, w_ih, w_hh, y, gates, cst = ctx.saved_tensors
+        T, B = ctx.dims
+        d_y = d_y.contiguous()
+        d_x = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dwi, dwh, dbi, dbh = _lstm_bwd(x, w_ih, w_hh, y, 0, y.shape[1], gates, cst, d_y, d_x, False, 0, T, B)
+        return d_x, dwi, dwh, dbi, dbh, None, None, None
+
+
+class BiLSTMLayer(torch.autograd.Function):
+    """One bidirectional nn.LSTM layer (encoder.py:51): output [T*B][2H] = fwd || reverse."""
+
+    @staticmethod
+    def forward(ctx, x, wi_f, wh_f, bi_f, bh_f, wi_r, wh_r, bi_r, bh_r, T, B, save):
+        x = x.contiguous()
+        H = wh_f.shape[1]
+        y = _empty((T * B, 2 * H), x)
+        g_f, c_f = _lstm_fwd(x, wi_f, wh_f, bi_f, bh_f, y, 0, 2 * H, False, save, T, B)
+        g_r, c_r = _lstm_fwd(x, wi_r, wh_r, bi_r, bh_r, y, H, 2 * H, True, save, T, B)
+        if save:
+            ctx.save_for_backward(x, wi_f, wh_f, wi_r, wh_r, y, g_f, c_f, g_r, c_r)
+        ctx.dims = (T, B, H)
+        return y
+
+    @staticmethod
+    def backward(ctx, d_y):
+        x, wi_f, wh_f, wi_r, wh_r, y, g_f, c_f, g_r, c_r = ctx.saved_tensors
+        T, B, H = ctx.dims
+        d_y = d_y.contiguous()
+        d_x = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        gf = _lstm_bwd(x, wi_f, wh_f, y, 0, 2 * H, g_f, c_f, d_y, d_x, False, 0, T, B)
+        gr = _lstm_bwd(x, wi_r, wh_r, y, H, 2 * H, g_r, c_r, d_y, d_x, True, 1, T, B)
+        return (d_x,) + gf + gr + (None, None, None)
+
+
+class Codes(torch.autograd.Function):
+    """Content codes (encoder.py:94-96, model.py:99/143): enc [T*B][64] -> (B, 32*(T//32+ceil(T/32)))."""
+
+    @staticmethod
+    def forward(ctx, enc, T, B):
+        enc = enc.contiguous()
+        L = 32 * (T // 32 + (T + 31) // 32)
+        out = _empty((B, L), enc)
+        call("avc_codes_from_encoder", T, B, ptr(enc), ptr(out), _stream(enc))
+        ctx.dims = (T, B)
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        T, B = ctx.dims
+        d = d.contiguous()
+        de = _empty((T * B, 64), d)
+        call("avc_codes_from_encoder_backward", T, B, ptr(d), ptr(de), 0, _stream(d))
+        return de, None, None
+
+
+class DecoderInput(torch.autograd.Function):
+    """Upsampled codes ++ c_trg -> [T*B][64+256]  (model.py:115-124)."""
+
+    @staticmethod
+    def forward(ctx, enc, c_trg, T, B):
+        enc = enc.contiguous()
+        c_trg = c_trg.contiguous()
+        ce = c_trg.shape[1]
+        out = _empty((T * B, 64 + ce), enc)
+        call("avc_decoder_input", T, B, ptr(enc), ce, ptr(c_trg), ptr(out), _stream(enc))
+        ctx.dims = (T, B, ce)
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        T, B, ce = ctx.dims
+        d = d.contiguous()
+        de = dc = None
+        if ctx.needs_input_grad[0]:
+            de = _empty((T * B, 64), d)
+            call("avc_decoder_input_backward", T, B, ce, ptr(d), ptr(de), 0, _stream(d))
+        if ctx.needs_input_grad[1]:
+            dc = _empty((B, ce), d)
+            call("avc_frames_from_mel_backward", T, B, 64, ce, ptr(d), 64 + ce, None, ptr(dc), 0, _stream(d))
+        return de, dc, None, None
+
+
+class Linear(torch.autograd.Function):
+    """LinearNorm (net_layers.py:3-20; decoder.py:77): [M][din] -> [M][dout]."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x = x.contiguous()
+        M, din = x.shape
+        dout = weight.shape[0]
+        y = _empty((M, dout), x)
+        call("avc_linear_forward", _ctx(x), M, din, dout, ptr(x), ptr(weight.contiguous()), ptr(_c(bias)),
+             ptr(y), _stream(x))
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, d_y):
+        x, weight = ctx.saved_tensors
+        d_y = d_y.contiguous()
+        M, din = x.shape
+        dout = weight.shape[0]
+        ng = ctx.needs_input_grad
+        dx = torch.empty_like(x) if ng[0] else None
+        dw = torch.empty_like(weight) if ng[1] else None
+        db = _empty((dout,), x) if (ctx.has_bias and ng[2]) else None
+        call("avc_linear_backward", _ctx(x), M, din, dout, ptr(x), ptr(weight.contiguous()), ptr(d_y),
+             ptr(dx), ptr(dw), ptr(db), 0, _stream(x))
+        return dx, dw, db
+
+
+class Loss(torch.autograd.Function):
+    """nn.MSELoss (kind 0) / nn.L1Loss (kind 1), mean reduction (model.py:286-288)."""
+
+    @staticmethod
+    def forward(ctx, a, b, kind):
+        a = a.contiguous()
+        b = b.contiguous()
+        if a.shape != b.shape:
+            raise ValueError(f"loss operands differ in shape: {tuple(a.shape)} vs {tuple(b.shape)}")
+        out = _empty((), a)
+        call("avc_loss_forward", _ctx(a), kind, a.numel(), ptr(a), ptr(b), ptr(out), 0, _stream(a))
+        ctx.save_for_backward(a, b)
+        ctx.kind = kind
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        a, b = ctx.saved_tensors
+        d = d.contiguous()
+        ga = torch.empty_like(a) if ctx.needs_input_grad[0] else None
+        gb = torch.empty_like(b) if ctx.needs_input_grad[1] else None
+        call("avc_loss_backward", ctx.kind, a.numel(), ptr(a), ptr(b), ptr(d), ptr(ga), ptr(gb), 0, _stream(a))
+        return ga, gb, None
+
+
+def mse_loss(a, b):
+    return Loss.apply(a, b, 0)
+
+
+def l1_loss(a, b):
+    return Loss.apply(a, b, 1)
+
+
+def overlap_average(frames: torch.Tensor, step: int) -> torch.Tensor:
+    """(M, C, N) slices -> (C, (M-1)*step + N) NaN-padded nanmean paste (model.py:428-437)."""
+    frames = frames.contiguous()
+    M, C, N = frames.shape
+    out = _empty((C, (M - 1) * step + N), frames)
+    call("avc_overlap_average", M, C, N, step, ptr(frames), ptr(out), _stream(frames))
+    return out
+
+
+def gemm(a, b, bias=None, a_trans=False, b_trans=False):
+    """C = op(A) op(B) (+bias) on the library's fp32 MFMA GEMM (exported for tests)."""
+    a = a.contiguous()
+    b = b.contiguous()
+    M = a.shape[1] if a_trans else a.shape[0]
+    K = a.shape[0] if a_trans else a.shape[1]
+    N = b.shape[0] if b_trans else b.shape[1]
+    c = _empty((M, N), a)
+    call("avc_gemm", _ctx(a), M, N, K, ptr(a), int(a_trans), ptr(b), int(b_trans), ptr(_c(bias)), ptr(c), 0,
+         _stream(a))
+    return c
+
+
+__all__ = ["FramesFromMel", "MelFromFrames", "ConvBNAct", "LSTMLayer", "BiLSTMLayer", "Codes",
+           "DecoderInput", "Linear", "Loss", "mse_loss", "l1_loss", "overlap_average", "gemm",
+           "ACT_NONE", "ACT_RELU", "ACT_TANH"]

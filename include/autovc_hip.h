@@ -1,0 +1,193 @@
+/*
+ * autovc_hip.h — C ABI of the MI355X-native AutoVC Generator hot path.
+ *
+ * The reference (Fagprojekt-Deep-voice-conversion/AutoVC) has no FFI: its replaceable unit is
+ * the Python class exported at autovc/auto_encoder/__init__.py:1 (`AutoEncoder`,
+ * autovc/auto_encoder/model.py:27).  This header is the native boundary that class is rebuilt
+ * on: autovc_amd.auto_encoder.AutoEncoder binds exactly these symbols with ctypes.  Each entry
+ * point names the reference module/lines whose arithmetic it replaces.
+ *
+ * Conventions
+ *   - All tensors are fp32, borrowed device pointers (the caller owns every buffer).
+ *   - Activations are TIME-MAJOR "frame rows": element (t, b, c) of a [T*B][C] row-major matrix
+ *     at ((t*B + b)*C + c).  Mels/codes crossing the Python boundary keep the reference's
+ *     channel-first (B, 80, T) / (B, n_codes) layouts; the glue kernels convert.
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream).  All work of one
+ *     call is enqueued on it; nothing blocks the host.  A context must only be used with one
+ *     stream at a time (its scratch arena is stream-ordered).
+ *   - Return value 0 = success; otherwise an AVC_ERR_* code and avc_last_error() holds a
+ *     thread-local message.  Invalid shapes are rejected before anything is launched.
+ */
+#ifndef AUTOVC_HIP_H_
+#define AUTOVC_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVC_OK 0
+#define AVC_ERR_INVALID 1
+#define AVC_ERR_HIP 2
+#define AVC_ERR_WORKSPACE 3
+
+/* activation codes used by the conv/BN/linear entry points */
+#define AVC_ACT_NONE 0
+#define AVC_ACT_RELU 1 /* encoder.py:70, decoder.py:70 */
+#define AVC_ACT_TANH 2 /* postnet.py:55 */
+
+typedef struct avc_context avc_context;
+
+/* ---- library / context ------------------------------------------------------------------ */
+int avc_abi_version(void);
+const char* avc_last_error(void);
+int avc_context_create(int device, avc_context** out);
+int avc_context_destroy(avc_context* ctx);
+/* grow the scratch arena to at least `bytes` (done automatically by every entry point) */
+int avc_context_reserve(avc_context* ctx, size_t bytes);
+
+/* ---- generic fp32 MFMA GEMM (building block exported for tests) ---------------------------
+ * C[M][N] (+)= A[M][K] * B[K][N] (+ bias[N]) with A row-major (a_trans=0) or stored [K][M]
+ * (a_trans=1), B stored [K][N] (b_trans=0) or [N][K] (b_trans=1). */
+int avc_gemm(avc_context* ctx, int M, int N, int K, const float* A, int a_trans, const float* B,
+             int b_trans, const float* bias, float* C, int accumulate, void* stream);
+
+/* ---- Conv1d(k=5,p=2) + BatchNorm1d + activation -------------------------------------------
+ * Replaces ConvNorm (net_layers.py:39-49) + nn.BatchNorm1d + relu/tanh as composed in
+ * encoder.py:39-48,69-70, decoder.py:41-50,69-70 and postnet.py:18-63.
+ *   x        [T*B][cin]            input frames (time-major)
+ *   weight   [cout][cin][5]        PyTorch Conv1d layout;  bias [cout]
+ *   gamma/beta/running_mean/running_var [cout]  (running stats updated in place when training)
+ *   y_pre    [T*B][cout]           out: conv output before BN (kept for backward)
+ *   out      [T*B][cout]           out: act(BN(y_pre)) (+ residual [T*B][cout] if non-NULL,
+ *                                  added after the activation: model.py:131-132)
+ *   mean/invstd [cout]             out: the statistics used (batch stats when training)
+ */
+int avc_conv_bn_act_forward(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                            const float* weight, const float* bias, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            int training, float momentum, float eps, int act,
+                            const float* residual, float* y_pre, float* out, float* mean,
+                            float* invstd, void* stream);
+
+/* Backward of the above.  d_out [T*B][cout] is the gradient of `out`.  Gradients are written
+ * (accumulate=0) or added (accumulate=1) into d_x [T*B][cin] (may be NULL), d_weight
+ * [cout][cin][5], d_bias, d_gamma, d_beta [cout]. */
+int avc_conv_bn_act_backward(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                             const float* weight, const float* gamma, const float* beta,
+                             const float* y_pre, const float* mean, const float* invstd,
+                             int training, int act, const float* d_out, float* d_x,
+                             float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
+                             int accumulate, void* stream);
+
+/* ---- LSTM layer (one direction) -----------------------------------------------------------
+ * Replaces one layer-direction of nn.LSTM (gates i,f,g,o; zero initial state) as used at
+ * encoder.py:51,75 (H=32, bidirectional), decoder.py:37,65 (H=512) and decoder.py:53,74
+ * (H=1024, 2 layers).
+ *   x      [T*B][din] (row stride ldx)    w_ih [4H][din], w_hh [4H][H], b_ih, b_hh [4H]
+ *   y      [T*B][H]   written at column offset inside rows of stride ldy (bidirectional concat)
+ *   saved_gates [T*B][4H], saved_c [T*B][H]  (needed for backward; may be NULL when not training)
+ * reverse=1 runs t = T-1 .. 0 (the `_reverse` direction). */
+int avc_lstm_forward(avc_context* ctx, int T, int B, int din, int H, int reverse, const float* x,
+                     int ldx, const float* w_ih, const float* w_hh, const float* b_ih,
+                     const float* b_hh, float* y, int ldy, float* saved_gates, float* saved_c,
+                     void* stream);
+
+/* Backward through time.  d_y [T*B] rows of stride ldy (gradient of y).  Writes
+ * (accumulate_dx/accumulate_dw = 0) or adds (= 1) d_x [T*B][din] (may be NULL) and d_w_ih,
+ * d_w_hh, d_b_ih, d_b_hh (PyTorch layout); the two directions of a bidirectional layer share
+ * d_x, hence the separate flags. */
+int avc_lstm_backward(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                      const float* x, int ldx, const float* w_ih, const float* w_hh,
+                      const float* y, int ldy, const float* saved_gates, const float* saved_c,
+                      const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh, float* d_b_ih,
+                      float* d_b_hh, int accumulate_dx, int accumulate_dw, void* stream);
+
+/* ---- Linear (decoder.linear_projection, decoder.py:56,77; net_layers.py:3-20) ------------ */
+int avc_linear_forward(avc_context* ctx, int M, int din, int dout, const float* x,
+                       const float* weight, const float* bias, float* y, void* stream);
+int avc_linear_backward(avc_context* ctx, int M, int din, int dout, const float* x,
+                        const float* weight, const float* d_y, float* d_x, float* d_weight,
+                        float* d_bias, int accumulate, void* stream);
+
+/* ---- layout glue --------------------------------------------------------------------------
+ * frames_from_mel: x (B,cm,T) channel-first + optional per-utterance embedding emb (B,ce)
+ * broadcast over time (encoder.py:65-66, model.py:124) -> out [T*B][cm+ce].  */
+int avc_frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* emb,
+                        float* out, void* stream);
+/* backward: d_x (B,cm,T) (+)= transpose of the first cm columns of d_frames [T*B][ld];
+ * d_emb (B,ce) (+)= time-sum of columns [cm, cm+ce) (d_emb may be NULL). */
+int avc_frames_from_mel_backward(int T, int B, int cm, int ce, const float* d_frames, int ld,
+                                 float* d_x, float* d_emb, int accumulate, void* stream);
+/* mel_from_frames: frames [T*B][cm] -> mel (B,cm,T) (model.py:127 transpose) */
+int avc_mel_from_frames(int T, int B, int cm, const float* frames, float* mel, void* stream);
+
+/* Content codes (encoder.py:94-96, model.py:99/143): enc_out [T*B][64] (fwd||bwd) ->
+ * codes (B, 32*(floor(T/32)+ceil(T/32))).  T must be >= 32. */
+int avc_codes_from_encoder(int T, int B, const float* enc_out, float* codes, void* stream);
+int avc_codes_from_encoder_backward(int T, int B, const float* d_codes, float* d_enc_out,
+                                    int accumulate, void* stream);
+/* Decoder input (model.py:115-124): upsampled codes ++ c_trg -> dec_in [T*B][64+ce]. */
+int avc_decoder_input(int T, int B, const float* enc_out, int ce, const float* c_trg,
+                      float* dec_in, void* stream);
+/* d_enc_out (+)= backward of the upsampling of the first 64 columns of d_dec_in. */
+int avc_decoder_input_backward(int T, int B, int ce, const float* d_dec_in, float* d_enc_out,
+                               int accumulate, void* stream);
+
+/* Long-form paste (AutoEncoder.batch_forward, model.py:428-437): M converted slices
+ * frames (M, C, N), slice i shifted right by i*step frames, NaN-padded and nan-averaged:
+ * out (C, (M-1)*step + N). */
+int avc_overlap_average(int M, int C, int N, int step, const float* frames, float* out,
+                        void* stream);
+
+/* ---- losses (model.py:184-215; criteria at model.py:286-288) -----------------------------
+ * kind 0 = nn.MSELoss (mean of (a-b)^2), kind 1 = nn.L1Loss (mean of |a-b|).
+ * forward : loss_out[0] (+)= loss(a, b)   (fixed-order fp64 reduction)
+ * backward: grad_a (+)= dL/da * dscale[0], grad_b (+)= dL/db * dscale[0]; dscale is a DEVICE
+ *           scalar (the incoming gradient of the loss, 1 when NULL); grad_a/grad_b may be NULL. */
+int avc_loss_forward(avc_context* ctx, int kind, size_t n, const float* a, const float* b,
+                     float* loss_out, int accumulate, void* stream);
+int avc_loss_backward(int kind, size_t n, const float* a, const float* b, const float* dscale,
+                      float* grad_a, float* grad_b, int accumulate, void* stream);
+
+/* ---- optimizer (model.py:312-321) ---------------------------------------------------------
+ * One fused pass over flat buffers of n parameters:
+ *   total_norm = ||grad||_2 (written to norm_out[0]); coef = min(1, max_norm/(norm+1e-6))
+ *   Adam(lr, beta1, beta2, eps, weight_decay, step) with the clipped gradient (torch.optim.Adam
+ *   semantics, amsgrad=False), then ema = ema_decay*ema + (1-ema_decay)*param (ema may be NULL).
+ * max_norm <= 0 disables clipping. */
+int avc_clip_adam_ema(avc_context* ctx, size_t n, float* param, float* grad, float* exp_avg,
+                      float* exp_avg_sq, float* ema, float lr, float beta1, float beta2,
+                      float eps, float weight_decay, int step, float max_norm, float ema_decay,
+                      float* norm_out, void* stream);
+
+/* ---- whole Generator forward (inference / convert(), model.py:68-146) ---------------------
+ * One call runs the full encoder -> upsample -> decoder -> postnet chain on device, with the
+ * same semantics as the layer entry points.  `params` is an array of device pointers in the
+ * reference state_dict order (avc_generator_param_count() entries: every tensor of
+ * AutoEncoder.state_dict() except num_batches_tracked).  training!=0 uses batch statistics
+ * and updates the running buffers in place, exactly like the reference's convert() which
+ * never calls .eval().  x (B,80,T), c_org/c_trg (B,256) -> mel, mel_post (B,80,T),
+ * codes (B, 32*(floor(T/32)+ceil(T/32))). */
+int avc_generator_param_count(void);
+int avc_generator_forward(avc_context* ctx, int T, int B, const float* const* params,
+                          const float* x, const float* c_org, const float* c_trg, int training,
+                          float* mel, float* mel_post, float* codes, void* stream);
+
+/* ---- measurement (bench.py) ---------------------------------------------------------------
+ * When bit `cls` of mask is set, every launch of that kernel class is bracketed by HIP events on
+ * its stream; avc_timing_read sums the event-measured durations and the algorithmic FLOPs/bytes
+ * of the recorded launches.  Classes: 0 GEMM (gemm_kernel), 1 LSTM step forward,
+ * 2 LSTM step backward, 3 H=32 persistent LSTM. */
+int avc_timing_enable(int mask);
+int avc_timing_reset(void);
+int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,
+                    long* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AUTOVC_HIP_H_ */

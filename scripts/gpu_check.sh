@@ -1,0 +1,25 @@
+#!/bin/bash
+# GPU-box check sequence: every step has its own time limit; a test failure (exit 1) lets the
+# sequence continue, anything else (fault, abort, segfault, timeout) ends it immediately.
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+run() {
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    kern)  run kern 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -x ;;
+    model) run model 600 python -m pytest tests/test_gpu_model.py -q -m gpu -s ;;
+    gpu)   run gpu 900 python -m pytest tests -q -m gpu ;;
+    bench) run bench 400 python bench.py --steps 10 --warmup 2 ;;
+    benchtrain) run benchtrain 400 python bench.py --mode train --steps 5 --warmup 2 --no-cpu ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -1,0 +1,199 @@
+"""Kernel-level parity of the HIP library (C-ABI calls) against torch-CPU references.
+
+fp32 tolerances: products are exact-fp32 MFMA with a different summation order than the CPU, so
+errors are a few ulp of the accumulated magnitudes (|err| <= 1e-5 * scale unless stated)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from autovc_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    return torch.as_tensor(a, dtype=torch.float32).to(dev).contiguous()
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 80, 1024), (8192, 512, 336), (4, 4, 4), (333, 12, 100)])
+@pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_modes(cuda_device, M, N, K, at, bt):
+    if at and M % 4:
+        pytest.skip("A^T needs M % 4 == 0")
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(K, N, generator=g, dtype=torch.float64)
+    bias = torch.randn(N, generator=g, dtype=torch.float64)
+    ref = A @ B + bias
+    a = A.t() if at else A
+    b = B.t() if bt else B
+    out = ops.gemm(_t(a.contiguous(), cuda_device), _t(b.contiguous(), cuda_device), _t(bias, cuda_device),
+                   a_trans=bool(at), b_trans=bool(bt)).cpu().double()
+    tol = 2e-6 * np.sqrt(K) * 4
+    assert (out - ref).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("B,T,cin,cout,act,training,res", [
+    (2, 128, 336, 512, ops.ACT_RELU, True, False),
+    (3, 33, 512, 512, ops.ACT_RELU, True, False),
+    (2, 100, 80, 512, ops.ACT_TANH, True, False),
+    (2, 64, 512, 80, ops.ACT_NONE, True, True),
+    (2, 64, 512, 80, ops.ACT_NONE, False, True),
+    (1, 40, 512, 512, ops.ACT_TANH, False, False),
+])
+def test_conv_bn_act_forward_backward(cuda_device, B, T, cin, cout, act, training, res):
+    g = torch.Generator().manual_seed(B * 1000 + T + cin + cout)
+    x = torch.rand(B, cin, T, generator=g)
+    W = (torch.rand(cout, cin, 5, generator=g) - 0.5) * 0.1
+    bias = (torch.rand(cout, generator=g) - 0.5) * 0.1
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = (torch.rand(cout, generator=g) - 0.5) * 0.4
+    rm = (torch.rand(cout, generator=g) - 0.5) * 0.2
+    rv = torch.rand(cout, generator=g) + 0.5
+    resid = torch.randn(B, cout, T, generator=g) if res else None
+    dout = torch.randn(B, cout, T, generator=g)
+
+    # CPU reference (fp64, autograd)
+    params = [t.double().clone().requires_grad_(True) for t in (x, W, bias, gamma, beta)]
+    rm_c, rv_c = rm.double().clone(), rv.double().clone()
+    y = F.batch_norm(F.conv1d(params[0], params[1], params[2], padding=2), rm_c, rv_c, params[3], params[4],
+                     training=training, momentum=0.1, eps=1e-5)
+    y = {ops.ACT_RELU: torch.relu, ops.ACT_TANH: torch.tanh, ops.ACT_NONE: lambda v: v}[act](y)
+    if res:
+        y = y + resid.double()
+    y.backward(dout.double())
+
+    # HIP (time-major frames)
+    fr = x.permute(2, 0, 1).reshape(T * B, cin)
+    rm_g, rv_g = _t(rm, cuda_device), _t(rv, cuda_device)
+    xg = _t(fr, cuda_device).requires_grad_(True)
+    pg = [_t(t, cuda_device).requires_grad_(True) for t in (W, bias, gamma, beta)]
+    rg = _t(resid.permute(2, 0, 1).reshape(T * B, cout), cuda_device) if res else None
+    out = ops.ConvBNAct.apply(xg, *pg, rm_g, rv_g, training, 0.1, 1e-5, act, rg, T, B)
+    out.backward(_t(dout.permute(2, 0, 1).reshape(T * B, cout), cuda_device))
+    out_cf = out.detach().cpu().reshape(T, B, cout).permute(1, 2, 0).double()
+    assert (out_cf - y.detach()).abs().max().item() < 2e-5
+    np.testing.assert_allclose(rm_g.cpu().numpy(), rm_c.numpy(), atol=1e-6)
+    np.testing.assert_allclose(rv_g.cpu().numpy(), rv_c.numpy(), atol=1e-5, rtol=1e-5)
+    dx = xg.grad.cpu().reshape(T, B, cin).permute(1, 2, 0).double()
+    scale = lambda t: max(1.0, t.abs().max().item())
+    assert (dx - params[0].grad).abs().max().item() < 2e-5 * scale(params[0].grad)
+    for gp, rp, name in zip(pg, params[1:], ["W", "bias", "gamma", "beta"]):
+        err = (gp.grad.cpu().double() - rp.grad).abs().max().item()
+        if name == "bias" and training:
+            # exact gradient is 0 (BN removes it); only rounding noise on both sides
+            assert err < 1e-3 * scale(params[4].grad), name
+        else:
+            assert err < 3e-5 * scale(rp.grad), name
+
+
+@pytest.mark.parametrize("B,T,din,H,bidir", [(2, 40, 512, 32, True), (3, 33, 64, 32, True),
+                                             (2, 20, 320, 512, False), (5, 12, 512, 1024, False),
+                                             (20, 8, 64, 64, False), (70, 6, 128, 128, False)])
+def test_lstm_forward_backward(cuda_device, B, T, din, H, bidir):
+    g = torch.Generator().manual_seed(B * 31 + T * 7 + H)
+    x = torch.randn(B, T, din, generator=g) * 0.5
+    k = 1.0 / np.sqrt(H)
+    nd = 2 if bidir else 1
+    ws = [[(torch.rand(*s, generator=g) * 2 - 1) * k for s in [(4 * H, din), (4 * H, H), (4 * H,), (4 * H,)]]
+          for _ in range(nd)]
+    dy = torch.randn(B, T, nd * H, generator=g)
+
+    flat = [w.double().clone().requires_grad_(True) for d in ws for w in d]
+    xr = x.double().clone().requires_grad_(True)
+    h0 = torch.zeros(nd, B, H, dtype=torch.float64)
+    yr, _, _ = torch.lstm(xr, (h0, h0.clone()), flat, True, 1, 0.0, False, bidir, True)
+    yr.backward(dy.double())
+
+    xg = _t(x.transpose(0, 1).reshape(T * B, din), cuda_device).requires_grad_(True)
+    wg = [_t(w, cuda_device).requires_grad_(True) for d in ws for w in d]
+    if bidir:
+        yg = ops.BiLSTMLayer.apply(xg, *wg, T, B, True)
+    else:
+        yg = ops.LSTMLayer.apply(xg, *wg, T, B, True)
+    yg.backward(_t(dy.transpose(0, 1).reshape(T * B, nd * H), cuda_device))
+    y_bt = yg.detach().cpu().reshape(T, B, nd * H).transpose(0, 1).double()
+    assert (y_bt - yr.detach()).abs().max().item() < 2e-5
+    dx = xg.grad.cpu().reshape(T, B, din).transpose(0, 1).double()
+    assert (dx - xr.grad).abs().max().item() < 5e-5 * max(1, xr.grad.abs().max().item())
+    for a, b in zip(wg, flat):
+        assert (a.grad.cpu().double() - b.grad).abs().max().item() < 5e-5 * max(1, b.grad.abs().max().item())
+
+
+def test_glue_roundtrip_and_codes(cuda_device):
+    B, T = 3, 100
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(B, 80, T, generator=g)
+    c = torch.rand(B, 256, generator=g)
+    fr = ops.FramesFromMel.apply(_t(x, cuda_device), _t(c, cuda_device)).cpu()
+    ref = torch.cat([x, c[:, :, None].expand(-1, -1, T)], 1).permute(2, 0, 1).reshape(T * B, 336)
+    assert torch.equal(fr, ref)
+    enc = torch.randn(T * B, 64, generator=g)
+    codes = ops.Codes.apply(_t(enc, cuda_device), T, B).cpu()
+    e = enc.reshape(T, B, 64)
+    ref_codes = torch.cat([e[t, :, :32] for t in range(31, T, 32)] + [e[t, :, 32:] for t in range(0, T, 32)], -1)
+    assert torch.equal(codes, ref_codes)
+    din = ops.DecoderInput.apply(_t(enc, cuda_device), _t(c, cuda_device), T, B).cpu().reshape(T, B, 320)
+    ca = [e[t, :, :32] for t in range(31, T, 32)]
+    cb = [e[t, :, 32:] for t in range(0, T, 32)]
+    for t in range(T):
+        assert torch.equal(din[t, :, :32], ca[min(t // 32, len(ca) - 1)])
+        assert torch.equal(din[t, :, 32:64], cb[t // 32])
+        assert torch.equal(din[t, :, 64:], c)
+
+
+def test_glue_backward_matches_autograd(cuda_device):
+    B, T = 2, 70
+    g = torch.Generator().manual_seed(9)
+    enc = torch.randn(T * B, 64, generator=g)
+    c = torch.rand(B, 256, generator=g)
+    dd = torch.randn(T * B, 320, generator=g)
+    dc = torch.randn(B, 32 * (T // 32 + (T + 31) // 32), generator=g)
+    # CPU autograd of the reference's list-comprehension code path (model.py:115-124)
+    er = enc.clone().double().requires_grad_(True)
+    cr = c.clone().double().requires_grad_(True)
+    e = er.reshape(T, B, 64).permute(1, 2, 0)  # (B,64,T)
+    ca = [e[:, :32, i] for i in range(31, T, 32)]
+    cb = [e[:, 32:, i] for i in range(0, T, 32)]
+    up_a = torch.cat([v.unsqueeze(-1).expand(-1, -1, 32) for v in ca], -1)
+    up_a = torch.cat([up_a, ca[-1].unsqueeze(-1).expand(-1, -1, T - up_a.size(-1))], -1)
+    up_b = torch.cat([v.unsqueeze(-1).expand(-1, -1, 32) for v in cb], -1)[:, :, :T]
+    dref = torch.cat([up_a, up_b, cr.unsqueeze(-1).expand(-1, -1, T)], 1).permute(2, 0, 1).reshape(T * B, 320)
+    codes = torch.cat([torch.cat(ca, -1), torch.cat(cb, -1)], -1)
+    (dref * dd.double()).sum().add((codes * dc.double()).sum()).backward()
+
+    eg = _t(enc, cuda_device).requires_grad_(True)
+    cg = _t(c, cuda_device).requires_grad_(True)
+    out = ops.DecoderInput.apply(eg, cg, T, B)
+    cod = ops.Codes.apply(eg, T, B)
+    ((out * _t(dd, cuda_device)).sum() + (cod * _t(dc, cuda_device)).sum()).backward()
+    assert (eg.grad.cpu().double() - er.grad).abs().max().item() < 1e-4
+    assert (cg.grad.cpu().double() - cr.grad).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_losses(cuda_device, kind):
+    g = torch.Generator().manual_seed(3 + kind)
+    a = torch.randn(4, 80, 128, generator=g)
+    b = torch.randn(4, 80, 128, generator=g)
+    ar = a.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    ref = F.mse_loss(ar, br) if kind == 0 else F.l1_loss(ar, br)
+    (ref * 1.7).backward()
+    ag = _t(a, cuda_device).requires_grad_(True)
+    bg = _t(b, cuda_device).requires_grad_(True)
+    out = ops.Loss.apply(ag, bg, kind)
+    (out * 1.7).backward()
+    assert abs(out.item() - ref.item()) < 1e-6 * max(1, abs(ref.item()))
+    assert (ag.grad.cpu().double() - ar.grad).abs().max().item() < 1e-9 + 1e-6 * ar.grad.abs().max().item()
+    assert (bg.grad.cpu().double() - br.grad).abs().max().item() < 1e-9 + 1e-6 * br.grad.abs().max().item()
+
+
+def test_overlap_average(cuda_device):
+    g = torch.Generator().manual_seed(1)
+    fr = torch.randn(5, 80, 128, generator=g)
+    out = ops.overlap_average(_t(fr, cuda_device), 64).cpu()
+    frames = [F.pad(fr[i], (i * 64, (5 - i - 1) * 64), value=float("nan")) for i in range(5)]
+    ref = torch.stack(frames).nanmean(0)
+    assert (out - ref).abs().max().item() < 1e-6

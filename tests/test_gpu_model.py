@@ -1,0 +1,129 @@
+"""Generator-level parity: the HIP AutoEncoder against the golden vectors produced by the
+reference class (tests/golden/make_golden.py) and against the CPU oracle.
+
+Tolerance (BASELINE.json north_star): max|d mel| <= 1e-4 in fp32.  BN running buffers: 1e-5."""
+import numpy as np
+import pytest
+import torch
+
+from autovc_amd.auto_encoder import AutoEncoder
+from autovc_amd.weights import torch_state_dict
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+TOL_MEL = 1e-4
+FWD_CASES = ["fwd_b2_t128_train", "fwd_b2_t128_eval", "fwd_b2_t100_train", "fwd_b1_t128_train",
+             "fwd_b3_t33_train", "fwd_b2_t1024_ragged"]
+
+
+def make_model(dev, train=True):
+    ae = AutoEncoder(device=dev, verbose=False)
+    ae.load_state_dict(torch_state_dict(0))
+    ae.to(dev)
+    ae.train(train)
+    return ae
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def check_bn(ae, g):
+    for k, v in ae.state_dict().items():
+        if ("bn/" + k) in g:
+            ref = g["bn/" + k]
+            if k.endswith("num_batches_tracked"):
+                assert int(v) == int(ref), k
+            else:
+                np.testing.assert_allclose(v.cpu().numpy(), ref, atol=1e-5, rtol=0, err_msg=k)
+
+
+@pytest.mark.parametrize("case", FWD_CASES)
+@pytest.mark.parametrize("path", ["fused", "autograd"])
+def test_forward_matches_reference(cuda_device, case, path):
+    g = load_golden(case)
+    ae = make_model(cuda_device, bool(g["train"]))
+    x, co, ct = (_t(g[k], cuda_device) for k in ("x", "c_org", "c_trg"))
+    if path == "fused":
+        with torch.no_grad():
+            mel, post, codes = ae(x, co, ct)
+    else:
+        x.requires_grad_(True)
+        mel, post, codes = ae(x, co, ct)
+        assert post.grad_fn is not None
+    torch.cuda.synchronize()
+    assert mel.shape == g["mel"].shape and codes.shape == g["codes"].shape
+    err_mel = np.abs(mel.detach().cpu().numpy() - g["mel"]).max()
+    err_post = np.abs(post.detach().cpu().numpy() - g["mel_post"]).max()
+    err_codes = np.abs(codes.detach().cpu().numpy() - g["codes"]).max()
+    print(f"{case} {path}: max|d mel|={err_mel:.2e} max|d mel_post|={err_post:.2e} max|d codes|={err_codes:.2e}")
+    assert err_mel <= TOL_MEL
+    assert err_post <= TOL_MEL
+    assert err_codes <= TOL_MEL
+    check_bn(ae, g)
+
+
+def test_codes_only_and_short_input(cuda_device):
+    g = load_golden("fwd_b2_t128_train")
+    ae = make_model(cuda_device)
+    with torch.no_grad():
+        codes = ae(_t(g["x"], cuda_device), _t(g["c_org"], cuda_device), None)
+    assert np.abs(codes.cpu().numpy() - g["codes"]).max() <= TOL_MEL
+    with pytest.raises(ValueError):
+        ae(torch.rand(1, 80, 31, device=cuda_device), torch.rand(1, 256, device=cuda_device),
+           torch.rand(1, 256, device=cuda_device))
+
+
+def test_batch_forward_matches_reference(cuda_device):
+    g = load_golden("batch_forward_m5_n128")
+    ae = make_model(cuda_device)
+    with torch.no_grad():
+        out = ae.batch_forward(_t(g["batch"], cuda_device), _t(g["c_org"], cuda_device),
+                               _t(g["c_trg"], cuda_device), overlap=float(g["overlap"]))
+    assert out.shape == g["out"].shape
+    assert np.abs(out.cpu().numpy() - g["out"]).max() <= TOL_MEL
+
+
+def test_train_trace_matches_reference(cuda_device):
+    """3 reference training steps (model.py:303-321): loss, pre-clip grad norm, parameters."""
+    g = load_golden("train_b4_t128_3steps")
+    ae = make_model(cuda_device)
+    ae.configure_optimizer()
+    for s in range(int(g["steps"])):
+        loss, norm = ae.train_step(_t(g[f"x{s}"], cuda_device), _t(g[f"c{s}"], cuda_device))
+        print(f"step {s}: loss {loss.item():.7f} (ref {g['losses'][s]:.7f}) "
+              f"norm {norm.item():.6f} (ref {g['grad_norms'][s]:.6f})")
+        assert loss.item() == pytest.approx(float(g["losses"][s]), rel=2e-5)
+        assert norm.item() == pytest.approx(float(g["grad_norms"][s]), rel=2e-4)
+    sd = ae.state_dict()
+    init = torch_state_dict(0)
+    for k, v in sd.items():
+        if ("abs/" + k) not in g or k.endswith("num_batches_tracked"):
+            continue
+        a = v.detach().double().cpu()
+        if k.endswith(".0.conv.bias"):
+            # exactly-zero true gradient (train-mode BN follows): Adam moves these by rounding noise
+            assert (a - init[k].double()).abs().max().item() <= 3 * 1e-3 * 1.5, k
+            continue
+        assert a.abs().sum().item() == pytest.approx(float(g["abs/" + k]), rel=2e-5, abs=1e-6), k
+    for k in ["decoder.lstm2.weight_hh_l1", "decoder.linear_projection.linear_layer.bias",
+              "postnet.convolutions.4.1.weight", "encoder.lstm.weight_hh_l0_reverse"]:
+        got = sd[k].detach().cpu().numpy().ravel()[:256]
+        np.testing.assert_allclose(got, g["val/" + k], atol=5e-6, rtol=0, err_msg=k)
+    ema = ae.avg_params.double()
+    assert ema.sum().item() == pytest.approx(float(g["ema_sum"]), rel=1e-5)
+
+
+def test_fused_and_autograd_paths_agree(cuda_device):
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(4, 80, 96, generator=g).to(cuda_device)
+    c = torch.rand(4, 256, generator=g).to(cuda_device)
+    a = make_model(cuda_device, True)
+    b = make_model(cuda_device, True)
+    with torch.no_grad():
+        m1, p1, c1 = a(x, c, c)
+    m2, p2, c2 = b(x.clone().requires_grad_(True), c, c)
+    assert (p1 - p2.detach()).abs().max().item() < 1e-5
+    for (k, v), (_, w) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert (v.double() - w.double()).abs().max().item() < 1e-6, k
