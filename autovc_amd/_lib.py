@@ -60,7 +60,7 @@ _SIGS = {
 _RESTYPES = {"avc_last_error": ctypes.c_char_p}
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()
 _contexts = {}
 
 

@@ -2,6 +2,7 @@
 # GPU-box check sequence: every step has its own time limit; a test failure (exit 1) lets the
 # sequence continue, anything else (fault, abort, segfault, timeout) ends it immediately.
 set -u
+export PYTHONUNBUFFERED=1
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 run() {
@@ -15,9 +16,9 @@ run() {
 for step in "$@"; do
   case $step in
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    kern)  run kern 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -x ;;
-    model) run model 600 python -m pytest tests/test_gpu_model.py -q -m gpu -s ;;
-    gpu)   run gpu 900 python -m pytest tests -q -m gpu ;;
+    kern)  run kern 600 python -m pytest tests/test_gpu_kernels.py -v -m gpu -x --timeout 120 -p no:cacheprovider ;;
+    model) run model 600 python -m pytest tests/test_gpu_model.py -v -m gpu -s --timeout 200 -p no:cacheprovider ;;
+    gpu)   run gpu 900 python -m pytest tests -v -m gpu --timeout 300 -p no:cacheprovider ;;
     bench) run bench 400 python bench.py --steps 10 --warmup 2 ;;
     benchtrain) run benchtrain 400 python bench.py --mode train --steps 5 --warmup 2 --no-cpu ;;
     *) echo "unknown step $step"; exit 2 ;;
