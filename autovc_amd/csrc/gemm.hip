@@ -62,13 +62,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int t
   const int kt0 = split * kps;
   const int kt1 = min(ktotal, kt0 + kps);
 
-  f32x16 acc[TM][TN];
+  f32x16 acc[TM][TN], cmp[TM][TN];
+  f32x16 zero16;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) zero16[e] = 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    for (int j = 0; j < TN; ++j) {
+      acc[i][j] = zero16;
+      cmp[i][j] = zero16;
+    }
 
   float4 ra[NA], rb[NB];
 
@@ -148,6 +152,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int t
     if (kt + 1 < kt1) AVC_LOAD_TILE(kt + 1);
     const float* As = lds + buf * BK * (PA + PB);
     const float* Bs = As + BK * PA;
+    // Each K-tile (32 products) is accumulated by a fresh MFMA chain and added to the running
+    // total with Kahan compensation: a single fp32 FMA chain over K = 2560 (Conv1d, 5 taps x 512)
+    // is ~8x less accurate than oneDNN's blocked CPU accumulation, and the train-mode BatchNorms
+    // of the postnet amplify that error into mel_post (DESIGN.md "Numerics").
+    f32x16 part[TM][TN];
 #pragma unroll
     for (int s = 0; s < BK / 2; ++s) {
       const int kr = 2 * s + (lane >> 5);
@@ -160,8 +169,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int t
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], s == 0 ? zero16 : part[i][j], 0, 0, 0);
     }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float y = part[i][j][e] - cmp[i][j][e];
+          const float t = acc[i][j][e] + y;
+          cmp[i][j][e] = (t - acc[i][j][e]) - y;
+          acc[i][j][e] = t;
+        }
   }
 
   // ---- epilogue -------------------------------------------------------------------------

@@ -73,7 +73,8 @@ def test_conv_bn_act_forward_backward(cuda_device, B, T, cin, cout, act, trainin
     out = ops.ConvBNAct.apply(xg, *pg, rm_g, rv_g, training, 0.1, 1e-5, act, rg, T, B)
     out.backward(_t(dout.permute(2, 0, 1).reshape(T * B, cout), cuda_device))
     out_cf = out.detach().cpu().reshape(T, B, cout).permute(1, 2, 0).double()
-    assert (out_cf - y.detach()).abs().max().item() < 2e-5
+    # CPU fp32 (oneDNN) reaches ~2.5e-6 on these layers; the HIP path must be at least as tight
+    assert (out_cf - y.detach()).abs().max().item() < 5e-6
     np.testing.assert_allclose(rm_g.cpu().numpy(), rm_c.numpy(), atol=1e-6)
     np.testing.assert_allclose(rv_g.cpu().numpy(), rv_c.numpy(), atol=1e-5, rtol=1e-5)
     dx = xg.grad.cpu().reshape(T, B, cin).permute(1, 2, 0).double()
