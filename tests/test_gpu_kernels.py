@@ -198,3 +198,38 @@ def test_overlap_average(cuda_device):
     frames = [F.pad(fr[i], (i * 64, (5 - i - 1) * 64), value=float("nan")) for i in range(5)]
     ref = torch.stack(frames).nanmean(0)
     assert (out - ref).abs().max().item() < 1e-6
+
+
+@pytest.mark.parametrize("max_norm", [1.0, 0.0])
+def test_fused_clip_adam_ema_matches_torch(cuda_device, max_norm):
+    """avc_clip_adam_ema == clip_grad_norm_(max_norm) + torch.optim.Adam + EMA (model.py:314-321),
+    over 4 steps with gradients spanning 1e-12..1e2 (including |g| << eps and exact zeros)."""
+    from autovc_amd import _lib
+    torch.manual_seed(0)
+    n = 100_003
+    p_ref = torch.randn(n, dtype=torch.float32)
+    scales = 10.0 ** torch.empty(n).uniform_(-12, 2)
+    p_hip = p_ref.clone().to(cuda_device)
+    m = torch.zeros(n, device=cuda_device)
+    v = torch.zeros(n, device=cuda_device)
+    ema = p_hip.clone()
+    ema_ref = p_ref.clone()
+    pr = torch.nn.Parameter(p_ref.clone())
+    opt = torch.optim.Adam([pr], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0)
+    norm_out = torch.empty((), device=cuda_device)
+    for step in range(1, 5):
+        gr = torch.randn(n) * scales
+        gr[::97] = 0.0
+        pr.grad = gr.clone()
+        ref_norm = torch.nn.utils.clip_grad_norm_([pr], max_norm=max_norm) if max_norm > 0 else None
+        opt.step()
+        ema_ref = 0.9999 * ema_ref + (1 - 0.9999) * pr.detach()
+        gh = gr.to(cuda_device)
+        _lib.call("avc_clip_adam_ema", _lib.context(cuda_device), n, p_hip.data_ptr(), gh.data_ptr(), m.data_ptr(),
+                  v.data_ptr(), ema.data_ptr(), 1e-3, 0.9, 0.999, 1e-8, 0.0, step, float(max_norm), 0.9999,
+                  norm_out.data_ptr(), _lib.stream(cuda_device))
+        torch.cuda.synchronize()
+        if ref_norm is not None:
+            assert norm_out.item() == pytest.approx(ref_norm.item(), rel=1e-6)
+        assert (p_hip.cpu() - pr.detach()).abs().max().item() < 2e-7 * max(1.0, pr.abs().max().item())
+        assert (ema.cpu() - ema_ref).abs().max().item() < 1e-6
