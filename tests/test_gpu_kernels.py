@@ -230,6 +230,7 @@ def test_fused_clip_adam_ema_matches_torch(cuda_device, max_norm):
                   norm_out.data_ptr(), _lib.stream(cuda_device))
         torch.cuda.synchronize()
         if ref_norm is not None:
-            assert norm_out.item() == pytest.approx(ref_norm.item(), rel=1e-6)
+            # ours sums squares in fp64, torch's foreach norm in fp32: agreement to fp32 noise
+            assert norm_out.item() == pytest.approx(ref_norm.item(), rel=5e-6)
         assert (p_hip.cpu() - pr.detach()).abs().max().item() < 2e-7 * max(1.0, pr.abs().max().item())
-        assert (ema.cpu() - ema_ref).abs().max().item() < 1e-6
+        assert (ema.cpu() - ema_ref).abs().max().item() < 4e-7 * max(1.0, ema_ref.abs().max().item())
