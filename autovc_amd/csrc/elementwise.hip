@@ -386,7 +386,7 @@ __global__ void adam_ema_kernel(long n, float* __restrict__ p, float* __restrict
                                 float* __restrict__ m, float* __restrict__ v, float* __restrict__ ema,
                                 const float* __restrict__ coef, float lr, float b1, float b2,
                                 float eps, float wd, float step_size, float bc2_sqrt, float ema_decay,
-                                int clip) {
+                                float ema_keep, int clip) {
   const float c = clip ? coef[0] : 1.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float gi = g[i];
@@ -403,7 +403,9 @@ __global__ void adam_ema_kernel(long n, float* __restrict__ p, float* __restrict
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
     pi -= step_size * (mi / denom);
     p[i] = pi;
-    if (ema) ema[i] = ema_decay * ema[i] + (1.f - ema_decay) * pi;
+    // torch: ema_decay * avg + (1 - ema_decay) * flat  (two rounded products, one rounded sum;
+    // 1 - ema_decay formed in double on the host like the Python scalar)
+    if (ema) ema[i] = __fadd_rn(__fmul_rn(ema_decay, ema[i]), __fmul_rn(ema_keep, pi));
   }
 }
 
@@ -580,7 +582,8 @@ int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, floa
   const double bc2 = 1.0 - std::pow((double)b2, step);
   adam_ema_kernel<<<ew_blocks((long)n), 256, 0, s>>>((long)n, p, g, m, v, ema, coef, lr, b1, b2, eps,
                                                      wd, (float)(lr / bc1), (float)std::sqrt(bc2),
-                                                     ema_decay, max_norm > 0.f ? 1 : 0);
+                                                     ema_decay, (float)(1.0 - (double)ema_decay),
+                                                     max_norm > 0.f ? 1 : 0);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
