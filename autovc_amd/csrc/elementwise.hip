@@ -58,18 +58,31 @@ void colsum_geometry(int M, int N, int& R, int& rows_per) {
 }
 
 // ---- BatchNorm ---------------------------------------------------------------------------
-__global__ void bn_finalize_kernel(int C, int nparts, const float* __restrict__ stats, double count,
-                                   int training, float momentum, float eps,
-                                   float* __restrict__ rmean, float* __restrict__ rvar,
-                                   float* __restrict__ mean_out, float* __restrict__ invstd_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// 64 channels per block; the 4 waves split the partial-sum slabs, combine in fp64 through LDS.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, const float* __restrict__ stats,
+                                                          double count, int training, float momentum,
+                                                          float eps, float* __restrict__ rmean,
+                                                          float* __restrict__ rvar,
+                                                          float* __restrict__ mean_out,
+                                                          float* __restrict__ invstd_out) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   if (training) {
     double s = 0.0, s2 = 0.0;
-    for (int p = 0; p < nparts; ++p) {
-      s += stats[((long)p * 2 + 0) * C + c];
-      s2 += stats[((long)p * 2 + 1) * C + c];
+    if (c < C) {
+#pragma unroll 4
+      for (int p = grp; p < nparts; p += 4) {
+        s += stats[((long)p * 2 + 0) * C + c];
+        s2 += stats[((long)p * 2 + 1) * C + c];
+      }
     }
+    red[0][grp][cl] = s;
+    red[1][grp][cl] = s2;
+    __syncthreads();
+    if (grp != 0 || c >= C) return;
+    s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    s2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
     const double mean = s / count;
     double var = s2 / count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -80,32 +93,46 @@ __global__ void bn_finalize_kernel(int C, int nparts, const float* __restrict__ 
       const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
       rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
     }
-  } else {
+  } else if (grp == 0 && c < C) {
     mean_out[c] = rmean[c];
     invstd_out[c] = (float)(1.0 / sqrt((double)rvar[c] + (double)eps));
   }
 }
 
-__global__ void bn_apply_kernel(long M, int C, const float* __restrict__ y,
-                                const float* __restrict__ mean, const float* __restrict__ invstd,
-                                const float* __restrict__ gamma, const float* __restrict__ beta,
-                                int act, const float* __restrict__ residual, float* __restrict__ out) {
-  const long total4 = M * C / 4;
-  for (long i4 = blockIdx.x * (long)blockDim.x + threadIdx.x; i4 < total4;
-       i4 += (long)gridDim.x * blockDim.x) {
-    const int c = (int)((i4 * 4) % C);
-    float4 v = reinterpret_cast<const float4*>(y)[i4];
-    float r[4] = {v.x, v.y, v.z, v.w};
+// Each thread owns one channel quad (its mean/invstd/gamma/beta stay in registers) and walks
+// rows; consecutive threads cover consecutive quads of a row (coalesced float4 streams).
+__global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const float* __restrict__ y,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, int act,
+                                                       const float* __restrict__ residual,
+                                                       float* __restrict__ out) {
+  const int Q = C / 4;
+  const long nthreads = (long)gridDim.x * blockDim.x;
+  const long gt = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long rows_per_pass = nthreads / Q;
+  const int q = (int)(gt % Q);
+  const long r0 = gt / Q;
+  if (r0 >= rows_per_pass) return;  // leftover threads would revisit rows (out may alias y)
+  float sc[4], sh[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float a = (r[e] - mean[c + e]) * invstd[c + e] * gamma[c + e] + beta[c + e];
-      r[e] = act_fwd(a, act);
-    }
+  for (int e = 0; e < 4; ++e) {
+    const int c = 4 * q + e;
+    sc[e] = invstd[c] * gamma[c];
+    sh[e] = beta[c] - mean[c] * sc[e];
+  }
+  for (long r = r0; r < M; r += rows_per_pass) {
+    const long i4 = r * Q + q;
+    const float4 v = reinterpret_cast<const float4*>(y)[i4];
+    float o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = act_fwd(o[e] * sc[e] + sh[e], act);
     if (residual) {
-      const float4 q = reinterpret_cast<const float4*>(residual)[i4];
-      r[0] += q.x; r[1] += q.y; r[2] += q.z; r[3] += q.w;
+      const float4 rr = reinterpret_cast<const float4*>(residual)[i4];
+      o[0] += rr.x; o[1] += rr.y; o[2] += rr.z; o[3] += rr.w;
     }
-    reinterpret_cast<float4*>(out)[i4] = make_float4(r[0], r[1], r[2], r[3]);
+    reinterpret_cast<float4*>(out)[i4] = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -432,8 +459,8 @@ int colsum(avc_context* ctx, int M, int N, const float* X, long ld, float* out, 
 
 int bn_finalize(int C, int nparts, const float* stats, double count, int training, float momentum,
                 float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s) {
-  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, s>>>(C, nparts, stats, count, training, momentum,
-                                                     eps, rmean, rvar, mean, invstd);
+  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, s>>>(C, nparts, stats, count, training, momentum,
+                                                   eps, rmean, rvar, mean, invstd);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
@@ -442,8 +469,11 @@ int bn_apply(long M, int C, const float* y, const float* mean, const float* invs
              const float* gamma, const float* beta, int act, const float* residual, float* out,
              hipStream_t s) {
   AVC_CHECK_ARG(C % 4 == 0, "bn_apply: channels must be a multiple of 4");
-  bn_apply_kernel<<<ew_blocks(M * C / 4), 256, 0, s>>>(M, C, y, mean, invstd, gamma, beta, act,
-                                                       residual, out);
+  // ~4 float4 per thread; every thread owns one channel quad for the whole launch
+  const long Q = C / 4;
+  const long threads = std::max<long>(256, std::min<long>(M * Q / 4, 2048L * 256));
+  const long blocks = (threads + 255) / 256;
+  bn_apply_kernel<<<(int)blocks, 256, 0, s>>>(M, C, y, mean, invstd, gamma, beta, act, residual, out);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

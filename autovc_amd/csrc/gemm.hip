@@ -30,17 +30,20 @@ __device__ __forceinline__ float act_apply(float v, int act) {
   return v;
 }
 
-template <int BM, int BN, int AT, int BT>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int tilesN,
-                                                   int kt_per_tap, int kps, int nsplit,
-                                                   float* __restrict__ slab) {
-  constexpr int PA = BM + 4, PB = BN + 4;
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int NA = BM / 32, NB = BN / 32;  // float4 loads per thread per operand tile
+template <int BM, int BN, int WM, int WN, int AT, int BT>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tilesM, int tilesN,
+                                                            int kt_per_tap, int kps, int nsplit,
+                                                            float* __restrict__ slab) {
+  constexpr int NT = 64 * WM * WN;            // threads
+  constexpr int PA = BM + 4, PB = BN + 4;     // padded k-major LDS rows (16-B aligned)
+  constexpr int WTM = BM / WM, WTN = BN / WN; // wave tile
+  constexpr int TM = WTM / 32, TN = WTN / 32; // 32x32 MFMA tiles per wave
+  constexpr int NA = BM * BK / 4 / NT, NB = BN * BK / 4 / NT;  // float4 staged per thread
+  static_assert(NA * NT * 4 == BM * BK && NB * NT * 4 == BN * BK, "tile/thread mismatch");
   __shared__ __attribute__((aligned(16))) float lds[2 * BK * (PA + PB)];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WN, wn = w % WN;
 
   // XCD-aware bijective remap: blocks sharing an XCD (bid % 8) get consecutive tiles, i.e.
   // the same A row-panel, so the panel is served from that XCD's L2.
@@ -76,36 +79,41 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int t
 
   float4 ra[NA], rb[NB];
 
+  // Staging maps.  K-contiguous operand (A row-major / B^T): element idx -> (row, k-quad) with
+  // 32 consecutive lanes on 32 consecutive rows (conflict-free ds_write_b32 into the k-major
+  // image).  MN-contiguous operand: idx -> (k-row, quad of 4 consecutive rows/cols), one
+  // ds_write_b128 per float4.
+#define AVC_KC_ROW(IDX) (((IDX) & 31) + 32 * ((IDX) >> 8))
+#define AVC_KC_KQ(IDX) (((IDX) >> 5) & 7)
+
 #define AVC_LOAD_TILE(KT)                                                                       \
   {                                                                                             \
     const int tau = (KT) / kt_per_tap;                                                          \
     const int k0 = ((KT) - tau * kt_per_tap) * BK;                                              \
     _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                            \
+      const int idx = tid + NT * i;                                                             \
       if (AT == 0) {                                                                            \
-        const int row_in = (tid & 31) + 32 * i, kq = tid >> 5;                                  \
-        const int m = tm * BM + row_in, k = k0 + 4 * kq;                                        \
+        const int m = tm * BM + AVC_KC_ROW(idx), k = k0 + 4 * AVC_KC_KQ(idx);                   \
         const long srow = (long)m + a_shift0 + (long)tau * a_tapshift;                          \
         const bool ok = m < M && k < Kc && srow >= 0 && srow < a_rows;                          \
         ra[i] = sel4(ok, *reinterpret_cast<const float4*>(Ab + (ok ? srow * lda + k : 0)));    \
       } else {                                                                                  \
-        constexpr int QPR = BM / 4;                                                             \
-        const int mq = tid % QPR, krow = tid / QPR + (256 / QPR) * i;                           \
+        const int mq = idx % (BM / 4), krow = idx / (BM / 4);                                   \
         const int m = tm * BM + 4 * mq, k = k0 + krow;                                          \
         const bool ok = m < M && k < Kc;                                                        \
         ra[i] = sel4(ok, *reinterpret_cast<const float4*>(Ab + (ok ? (long)k * lda + m : 0))); \
       }                                                                                         \
     }                                                                                           \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
+      const int idx = tid + NT * i;                                                             \
       if (BT == 0) {                                                                            \
-        constexpr int QPR = BN / 4;                                                             \
-        const int nq = tid % QPR, krow = tid / QPR + (256 / QPR) * i;                           \
+        const int nq = idx % (BN / 4), krow = idx / (BN / 4);                                   \
         const int n = tn * BN + 4 * nq, k = k0 + krow;                                          \
         const long srow = (long)k + bshift;                                                     \
         const bool ok = n < N && k < Kc && srow >= 0 && srow < b_rows;                          \
         rb[i] = sel4(ok, *reinterpret_cast<const float4*>(Bb + (ok ? (long)tau * b_tapoff + srow * ldb + n : 0))); \
       } else {                                                                                  \
-        const int col_in = (tid & 31) + 32 * i, kq = tid >> 5;                                  \
-        const int n = tn * BN + col_in, k = k0 + 4 * kq;                                        \
+        const int n = tn * BN + AVC_KC_ROW(idx), k = k0 + 4 * AVC_KC_KQ(idx);                   \
         const bool ok = n < N && k < Kc;                                                        \
         rb[i] = sel4(ok, *reinterpret_cast<const float4*>(Bb + (ok ? (long)tau * b_tapoff + (long)n * ldb + k : 0))); \
       }                                                                                         \
@@ -117,29 +125,29 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int t
     float* As = lds + (BUF) * BK * (PA + PB);                                                   \
     float* Bs = As + BK * PA;                                                                   \
     _Pragma("unroll") for (int i = 0; i < NA; ++i) {                                            \
+      const int idx = tid + NT * i;                                                             \
       if (AT == 0) {                                                                            \
-        const int row_in = (tid & 31) + 32 * i, kq = tid >> 5;                                  \
-        As[(4 * kq + 0) * PA + row_in] = ra[i].x;                                               \
-        As[(4 * kq + 1) * PA + row_in] = ra[i].y;                                               \
-        As[(4 * kq + 2) * PA + row_in] = ra[i].z;                                               \
-        As[(4 * kq + 3) * PA + row_in] = ra[i].w;                                               \
+        const int r = AVC_KC_ROW(idx), kq = AVC_KC_KQ(idx);                                     \
+        As[(4 * kq + 0) * PA + r] = ra[i].x;                                                    \
+        As[(4 * kq + 1) * PA + r] = ra[i].y;                                                    \
+        As[(4 * kq + 2) * PA + r] = ra[i].z;                                                    \
+        As[(4 * kq + 3) * PA + r] = ra[i].w;                                                    \
       } else {                                                                                  \
-        constexpr int QPR = BM / 4;                                                             \
-        const int mq = tid % QPR, krow = tid / QPR + (256 / QPR) * i;                           \
+        const int mq = idx % (BM / 4), krow = idx / (BM / 4);                                   \
         *reinterpret_cast<float4*>(As + krow * PA + 4 * mq) = ra[i];                            \
       }                                                                                         \
     }                                                                                           \
     _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                            \
+      const int idx = tid + NT * i;                                                             \
       if (BT == 0) {                                                                            \
-        constexpr int QPR = BN / 4;                                                             \
-        const int nq = tid % QPR, krow = tid / QPR + (256 / QPR) * i;                           \
+        const int nq = idx % (BN / 4), krow = idx / (BN / 4);                                   \
         *reinterpret_cast<float4*>(Bs + krow * PB + 4 * nq) = rb[i];                            \
       } else {                                                                                  \
-        const int col_in = (tid & 31) + 32 * i, kq = tid >> 5;                                  \
-        Bs[(4 * kq + 0) * PB + col_in] = rb[i].x;                                               \
-        Bs[(4 * kq + 1) * PB + col_in] = rb[i].y;                                               \
-        Bs[(4 * kq + 2) * PB + col_in] = rb[i].z;                                               \
-        Bs[(4 * kq + 3) * PB + col_in] = rb[i].w;                                               \
+        const int c = AVC_KC_ROW(idx), kq = AVC_KC_KQ(idx);                                     \
+        Bs[(4 * kq + 0) * PB + c] = rb[i].x;                                                    \
+        Bs[(4 * kq + 1) * PB + c] = rb[i].y;                                                    \
+        Bs[(4 * kq + 2) * PB + c] = rb[i].z;                                                    \
+        Bs[(4 * kq + 3) * PB + c] = rb[i].w;                                                    \
       }                                                                                         \
     }                                                                                           \
   }
@@ -162,9 +170,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int t
       const int kr = 2 * s + (lane >> 5);
       float a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[kr * PA + wm * (BM / 2) + 32 * i + (lane & 31)];
+      for (int i = 0; i < TM; ++i) a[i] = As[kr * PA + wm * WTM + 32 * i + (lane & 31)];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = Bs[kr * PB + wn * (BN / 2) + 32 * j + (lane & 31)];
+      for (int j = 0; j < TN; ++j) b[j] = Bs[kr * PB + wn * WTN + 32 * j + (lane & 31)];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -183,10 +191,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int t
           acc[i][j][e] = t;
         }
   }
+#undef AVC_LOAD_TILE
+#undef AVC_STORE_TILE
+#undef AVC_KC_ROW
+#undef AVC_KC_KQ
 
   // ---- epilogue -------------------------------------------------------------------------
-  const int row_base = tm * BM + wm * (BM / 2) + 4 * (lane >> 5);
-  const int col_base = tn * BN + wn * (BN / 2) + (lane & 31);
+  const int row_base = tm * BM + wm * WTM + 4 * (lane >> 5);
+  const int col_base = tn * BN + wn * WTN + (lane & 31);
   if (nsplit > 1) {
     float* out = slab + ((long)(split * d.nz + z) * d.M) * d.N;
 #pragma unroll
@@ -233,23 +245,29 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc d, int tilesM, int t
 
   if (d.stats) {
     __syncthreads();  // LDS operand tiles are dead now; reuse them for the column reduction
-    float* red = lds;  // [2 (wm)][2 (sum,sq)][BN]
+    float* red = lds;  // [WM][2 (sum,sq)][BN]
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       float s = csum[j] + __shfl_xor(csum[j], 32);
       float s2 = csq[j] + __shfl_xor(csq[j], 32);
       if (lane < 32) {
-        const int cl = wn * (BN / 2) + 32 * j + lane;
+        const int cl = wn * WTN + 32 * j + lane;
         red[(wm * 2 + 0) * BN + cl] = s;
         red[(wm * 2 + 1) * BN + cl] = s2;
       }
     }
     __syncthreads();
-    for (int cl = tid; cl < BN; cl += 256) {
+    for (int cl = tid; cl < BN; cl += NT) {
       const int col = tn * BN + cl;
       if (col < d.N) {
-        d.stats[((long)tm * 2 + 0) * d.N + col] = red[0 * BN + cl] + red[2 * BN + cl];
-        d.stats[((long)tm * 2 + 1) * d.N + col] = red[1 * BN + cl] + red[3 * BN + cl];
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int r = 0; r < WM; ++r) {
+          s += red[(r * 2 + 0) * BN + cl];
+          s2 += red[(r * 2 + 1) * BN + cl];
+        }
+        d.stats[((long)tm * 2 + 0) * d.N + col] = s;
+        d.stats[((long)tm * 2 + 1) * d.N + col] = s2;
       }
     }
   }
@@ -302,18 +320,19 @@ Plan make_plan(const GemmDesc& d, int force_split) {
   return p;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WM, int WN>
 void launch(const GemmDesc& d, const Plan& p, float* slab, hipStream_t s) {
   dim3 grid(p.tilesM * p.tilesN, d.nz * p.nsplit);
+  constexpr int NT = 64 * WM * WN;
   const int code = d.a_trans * 2 + d.b_trans;
   if (code == 0)
-    gemm_kernel<BM, BN, 0, 0><<<grid, 256, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
+    gemm_kernel<BM, BN, WM, WN, 0, 0><<<grid, NT, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
   else if (code == 1)
-    gemm_kernel<BM, BN, 0, 1><<<grid, 256, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
+    gemm_kernel<BM, BN, WM, WN, 0, 1><<<grid, NT, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
   else if (code == 2)
-    gemm_kernel<BM, BN, 1, 0><<<grid, 256, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
+    gemm_kernel<BM, BN, WM, WN, 1, 0><<<grid, NT, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
   else
-    gemm_kernel<BM, BN, 1, 1><<<grid, 256, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
+    gemm_kernel<BM, BN, WM, WN, 1, 1><<<grid, NT, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
 }
 
 }  // namespace
@@ -353,8 +372,8 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     if (!slab) return AVC_ERR_WORKSPACE;
   }
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
-  if (p.bm == 128) launch<128, 128>(d, p, slab, stream);
-  else launch<64, 64>(d, p, slab, stream);
+  if (p.bm == 128) launch<128, 128, 2, 4>(d, p, slab, stream);
+  else launch<64, 64, 2, 2>(d, p, slab, stream);
   AVC_LAUNCH_CHECK();
   if (ev) {
     const double flops = 2.0 * d.M * d.N * (double)d.Kc * d.ntaps * d.nz;
