@@ -348,7 +348,7 @@ int avc_loss_backward(int kind, size_t n, const float* a, const float* b, const 
 
 int avc_clip_adam_ema(avc_context* ctx, size_t n, float* param, float* grad, float* exp_avg,
                       float* exp_avg_sq, float* ema, float lr, float beta1, float beta2,
-                      float eps, float weight_decay, int step, float max_norm, float ema_decay,
+                      float eps, float weight_decay, int step, float max_norm, double ema_decay,
                       float* norm_out, void* stream) {
   AVC_CHECK_ARG(ctx && param && grad && exp_avg && exp_avg_sq, "NULL pointer");
   AVC_TRY(ensure_arena(ctx, optimizer_scratch()));

@@ -597,7 +597,7 @@ size_t optimizer_scratch() { return 2048 * sizeof(double) + 512; }
 
 int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, float* v, float* ema,
                   float lr, float b1, float b2, float eps, float wd, int step, float max_norm,
-                  float ema_decay, float* norm_out, hipStream_t s) {
+                  double ema_decay, float* norm_out, hipStream_t s) {
   AVC_CHECK_ARG(step >= 1, "adam step counter starts at 1");
   Scratch sc(ctx);
   const int nb = (int)std::min<size_t>(2048, (n + 255) / 256);
@@ -612,7 +612,7 @@ int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, floa
   const double bc2 = 1.0 - std::pow((double)b2, step);
   adam_ema_kernel<<<ew_blocks((long)n), 256, 0, s>>>((long)n, p, g, m, v, ema, coef, lr, b1, b2, eps,
                                                      wd, (float)(lr / bc1), (float)std::sqrt(bc2),
-                                                     ema_decay, (float)(1.0 - (double)ema_decay),
+                                                     (float)ema_decay, (float)(1.0 - ema_decay),
                                                      max_norm > 0.f ? 1 : 0);
   AVC_LAUNCH_CHECK();
   return AVC_OK;

@@ -156,11 +156,12 @@ int avc_loss_backward(int kind, size_t n, const float* a, const float* b, const 
  * One fused pass over flat buffers of n parameters:
  *   total_norm = ||grad||_2 (written to norm_out[0]); coef = min(1, max_norm/(norm+1e-6))
  *   Adam(lr, beta1, beta2, eps, weight_decay, step) with the clipped gradient (torch.optim.Adam
- *   semantics, amsgrad=False), then ema = ema_decay*ema + (1-ema_decay)*param (ema may be NULL).
+ *   semantics, amsgrad=False), then ema = ema_decay*ema + (1-ema_decay)*param (ema may be NULL),
+ *   rounded like the reference's fp32 tensor expression with Python-double scalars.
  * max_norm <= 0 disables clipping. */
 int avc_clip_adam_ema(avc_context* ctx, size_t n, float* param, float* grad, float* exp_avg,
                       float* exp_avg_sq, float* ema, float lr, float beta1, float beta2,
-                      float eps, float weight_decay, int step, float max_norm, float ema_decay,
+                      float eps, float weight_decay, int step, float max_norm, double ema_decay,
                       float* norm_out, void* stream);
 
 /* ---- whole Generator forward (inference / convert(), model.py:68-146) ---------------------
