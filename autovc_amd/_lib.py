@@ -51,6 +51,7 @@ _SIGS = {
     "avc_loss_backward": [_I, _Z, _P, _P, _P, _P, _P, _I, _P],
     "avc_clip_adam_ema": [_P, _Z, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, ctypes.c_double, _P, _P],
     "avc_timing_enable": [_I],
+    "avc_lstm_tune": [_I, _I],
     "avc_timing_reset": [],
     "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)],

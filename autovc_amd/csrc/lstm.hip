@@ -154,6 +154,16 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
     for (int e = 0; e < 4; ++e)
       part[(w * MB + r * 16 + lk + e) * 16 + l15] = acc0[r][e] + acc1[r][e];
   __syncthreads();
+  // cross-wave reduction, one (row, column) per thread, fixed order; result in wave-0's slab
+  // (each element is read and then overwritten by the same thread only)
+  if (NW > 1) {
+    for (int idx = tid; idx < MB * 16; idx += blockDim.x) {
+      float s = part[idx];
+      for (int ww = 1; ww < NW; ++ww) s += part[ww * MB * 16 + idx];
+      part[idx] = s;
+    }
+    __syncthreads();
+  }
 
   const int H = a.H;
   if (!BWD) {
@@ -164,9 +174,7 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
       float z[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        float s = a.gx[(long)b * 4 * H + cb * 16 + g * 4 + u];
-        for (int ww = 0; ww < NW; ++ww) s += part[(ww * MB + row) * 16 + g * 4 + u];
-        z[g] = s;
+        z[g] = a.gx[(long)b * 4 * H + cb * 16 + g * 4 + u] + part[row * 16 + g * 4 + u];
       }
       const float ig = sigmoidf_(z[0]), fg = sigmoidf_(z[1]), gg = tanhf(z[2]), og = sigmoidf_(z[3]);
       const int j = cb * 4 + u;
@@ -189,8 +197,7 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
       const int b = rb * MB + row;
       if (b >= a.B) continue;
       const int j = cb * 16 + jj;
-      float dh = a.dy[(long)b * a.lddy + j];
-      for (int ww = 0; ww < NW; ++ww) dh += part[(ww * MB + row) * 16 + jj];
+      const float dh = a.dy[(long)b * a.lddy + j] + part[row * 16 + jj];
       const long pb = (long)b * 4 * H + (j >> 2) * 16 + (j & 3);
       const float ig = a.gates[pb], fg = a.gates[pb + 4], gg = a.gates[pb + 8], og = a.gates[pb + 12];
       const float c = a.c_cur[(long)b * H + j];
@@ -210,6 +217,8 @@ struct StepCfg {
   int mb, nw;
 };
 
+int g_force_mb = 0, g_force_nw = 0;  // avc_lstm_tune() overrides (0 = automatic)
+
 StepCfg step_cfg(int B, int ncolblocks, int K) {
   StepCfg c;
   if (B <= 16) c.mb = 16;
@@ -217,6 +226,8 @@ StepCfg step_cfg(int B, int ncolblocks, int K) {
   else if ((long)ncolblocks * ((B + 31) / 32) >= 240) c.mb = 32;
   else c.mb = 16;
   c.nw = std::max(1, std::min(16, K / 64));
+  if (g_force_mb) c.mb = g_force_mb;
+  if (g_force_nw) c.nw = std::min(g_force_nw, std::max(1, K / 64));
   while (K % (c.nw * 64) != 0) --c.nw;
   return c;
 }
@@ -548,3 +559,17 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
 }
 
 }  // namespace avc
+
+extern "C" int avc_lstm_tune(int rows_per_block, int waves) {
+  if (!(rows_per_block == 0 || rows_per_block == 16 || rows_per_block == 32 || rows_per_block == 64)) {
+    avc::set_error("avc_lstm_tune: rows_per_block must be 0, 16, 32 or 64");
+    return AVC_ERR_INVALID;
+  }
+  if (waves < 0 || waves > 16) {
+    avc::set_error("avc_lstm_tune: waves must be 0..16");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_force_mb = rows_per_block;
+  avc::g_force_nw = waves;
+  return AVC_OK;
+}
