@@ -98,11 +98,12 @@ struct StepArgs {
   float* dc; float* dg_out;
 };
 
-constexpr int G = 4;  // 16-deep k-chunks loaded per batch (64 k per wave per batch)
 
-template <int MB, bool BWD>
+template <int MB, bool BWD, int CPT>
 __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
   constexpr int RT = MB / 16;
+  // 16-deep k-chunks loaded per batch; fewer for the 64-row tile to stay within 128 VGPRs
+  constexpr int G = MB == 64 ? 2 : 4;
   extern __shared__ float part[];  // [NW][MB][16]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, NW = blockDim.x >> 6;
   const int cb = blockIdx.x, rb = blockIdx.y;
@@ -114,6 +115,43 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
     acc0[r] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc1[r] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+
+  // Epilogue operands do not depend on the recurrence: fetch them before the MFMA phase so
+  // their memory latency overlaps it.  Thread owns cells tid + NT*i (i < CPT).
+  const int H = a.H;
+  const int NT = blockDim.x;
+  const int ncell = BWD ? MB * 16 : MB * 4;
+  float pf[CPT][8];
+  bool cok[CPT];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int cell = tid + NT * i;
+    const int row = BWD ? (cell >> 4) : (cell >> 2);
+    const int b = rb * MB + row;
+    cok[i] = cell < ncell && b < a.B;
+    if (!cok[i]) continue;
+    if (!BWD) {
+      const int u = cell & 3;
+      const float* g = a.gx + (long)b * 4 * H + cb * 16 + u;
+      pf[i][0] = g[0];
+      pf[i][1] = g[4];
+      pf[i][2] = g[8];
+      pf[i][3] = g[12];
+      pf[i][4] = a.c_prev ? a.c_prev[(long)b * H + cb * 4 + u] : 0.f;
+    } else {
+      const int j = cb * 16 + (cell & 15);
+      const long pb = (long)b * 4 * H + (j >> 2) * 16 + (j & 3);
+      pf[i][0] = a.gates[pb];
+      pf[i][1] = a.gates[pb + 4];
+      pf[i][2] = a.gates[pb + 8];
+      pf[i][3] = a.gates[pb + 12];
+      pf[i][4] = a.c_cur[(long)b * H + j];
+      pf[i][5] = a.c_prv ? a.c_prv[(long)b * H + j] : 0.f;
+      pf[i][6] = a.dc[(long)b * H + j];
+      pf[i][7] = a.dy[(long)b * a.lddy + j];
+    }
+  }
+
   if (a.A != nullptr) {
     const int kbeg = w * a.kw;
     const float* wrow = a.W + (long)(cb * 16 + l15) * a.K + kbeg + lk;
@@ -165,21 +203,19 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
     __syncthreads();
   }
 
-  const int H = a.H;
   if (!BWD) {
-    for (int cell = tid; cell < MB * 4; cell += blockDim.x) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      if (!cok[i]) continue;
+      const int cell = tid + NT * i;
       const int row = cell >> 2, u = cell & 3;
       const int b = rb * MB + row;
-      if (b >= a.B) continue;
       float z[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        z[g] = a.gx[(long)b * 4 * H + cb * 16 + g * 4 + u] + part[row * 16 + g * 4 + u];
-      }
+      for (int g = 0; g < 4; ++g) z[g] = pf[i][g] + part[row * 16 + g * 4 + u];
       const float ig = sigmoidf_(z[0]), fg = sigmoidf_(z[1]), gg = tanhf(z[2]), og = sigmoidf_(z[3]);
       const int j = cb * 4 + u;
-      const float cp = a.c_prev ? a.c_prev[(long)b * H + j] : 0.f;
-      const float c = fg * cp + ig * gg;
+      const float c = fg * pf[i][4] + ig * gg;
       const float h = og * tanhf(c);
       a.c_out[(long)b * H + j] = c;
       a.h_out[(long)b * a.ldh_out + j] = h;
@@ -192,18 +228,19 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
       }
     }
   } else {
-    for (int cell = tid; cell < MB * 16; cell += blockDim.x) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      if (!cok[i]) continue;
+      const int cell = tid + NT * i;
       const int row = cell >> 4, jj = cell & 15;
       const int b = rb * MB + row;
-      if (b >= a.B) continue;
       const int j = cb * 16 + jj;
-      const float dh = a.dy[(long)b * a.lddy + j] + part[row * 16 + jj];
+      const float dh = pf[i][7] + part[row * 16 + jj];
       const long pb = (long)b * 4 * H + (j >> 2) * 16 + (j & 3);
-      const float ig = a.gates[pb], fg = a.gates[pb + 4], gg = a.gates[pb + 8], og = a.gates[pb + 12];
-      const float c = a.c_cur[(long)b * H + j];
-      const float cp = a.c_prv ? a.c_prv[(long)b * H + j] : 0.f;
+      const float ig = pf[i][0], fg = pf[i][1], gg = pf[i][2], og = pf[i][3];
+      const float c = pf[i][4], cp = pf[i][5];
       const float tc = tanhf(c);
-      const float dct = dh * og * (1.f - tc * tc) + a.dc[(long)b * H + j];
+      const float dct = dh * og * (1.f - tc * tc) + pf[i][6];
       a.dc[(long)b * H + j] = dct * fg;
       a.dg_out[pb] = dct * gg * ig * (1.f - ig);
       a.dg_out[pb + 4] = dct * cp * fg * (1.f - fg);
@@ -229,7 +266,16 @@ StepCfg step_cfg(int B, int ncolblocks, int K) {
   if (g_force_mb) c.mb = g_force_mb;
   if (g_force_nw) c.nw = std::min(g_force_nw, std::max(1, K / 64));
   while (K % (c.nw * 64) != 0) --c.nw;
+  // the epilogue gives each thread at most 4 cells (16 per row in backward, 4 in forward)
+  while (c.mb * 16 > 4 * 64 * c.nw && c.mb > 16) c.mb /= 2;
   return c;
+}
+
+int cells_per_thread(const StepCfg& c, bool bwd) {
+  const int cells = bwd ? c.mb * 16 : c.mb * 4;
+  const int t = c.nw * 64;
+  const int cpt = (cells + t - 1) / t;
+  return cpt <= 1 ? 1 : (cpt <= 2 ? 2 : 4);
 }
 
 void launch_step(const StepCfg& cfg, bool bwd, dim3 grid, const StepArgs& a, hipStream_t s) {
@@ -237,15 +283,21 @@ void launch_step(const StepCfg& cfg, bool bwd, dim3 grid, const StepArgs& a, hip
   const int threads = cfg.nw * 64;
   const int cls = bwd ? TC_LSTM_STEP_BWD : TC_LSTM_STEP_FWD;
   hipEvent_t ev = timing_begin(cls, s);
+  const int cpt = cells_per_thread(cfg, bwd);
+#define AVC_STEP_LAUNCH(MBV, BW)                                                                  \
+  if (cpt == 1) lstm_step_kernel<MBV, BW, 1><<<grid, threads, lds, s>>>(a);                       \
+  else if (cpt == 2) lstm_step_kernel<MBV, BW, 2><<<grid, threads, lds, s>>>(a);                  \
+  else lstm_step_kernel<MBV, BW, 4><<<grid, threads, lds, s>>>(a);
   if (!bwd) {
-    if (cfg.mb == 64) lstm_step_kernel<64, false><<<grid, threads, lds, s>>>(a);
-    else if (cfg.mb == 32) lstm_step_kernel<32, false><<<grid, threads, lds, s>>>(a);
-    else lstm_step_kernel<16, false><<<grid, threads, lds, s>>>(a);
+    if (cfg.mb == 64) { AVC_STEP_LAUNCH(64, false) }
+    else if (cfg.mb == 32) { AVC_STEP_LAUNCH(32, false) }
+    else { AVC_STEP_LAUNCH(16, false) }
   } else {
-    if (cfg.mb == 64) lstm_step_kernel<64, true><<<grid, threads, lds, s>>>(a);
-    else if (cfg.mb == 32) lstm_step_kernel<32, true><<<grid, threads, lds, s>>>(a);
-    else lstm_step_kernel<16, true><<<grid, threads, lds, s>>>(a);
+    if (cfg.mb == 64) { AVC_STEP_LAUNCH(64, true) }
+    else if (cfg.mb == 32) { AVC_STEP_LAUNCH(32, true) }
+    else { AVC_STEP_LAUNCH(16, true) }
   }
+#undef AVC_STEP_LAUNCH
   if (ev) {
     // recurrent product B x (4H or H) x K plus the W_hh slice streamed once per step
     const double flops = a.A ? 2.0 * a.B * (double)a.K * (bwd ? a.H : 4.0 * a.H) : 0.0;
