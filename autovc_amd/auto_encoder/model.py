@@ -18,7 +18,7 @@ import time
 import torch
 import torch.nn as nn
 
-from .. import _lib, ops
+from .. import _lib, dp, ops
 from ..hparams import AutoEncoderParams
 from .decoder import Decoder
 from .encoder import Encoder
@@ -255,10 +255,7 @@ class AutoEncoder(nn.Module):
 
     def _sync_bn_buffers(self):
         """Data-parallel training keeps per-rank BN statistics; rank 0's are the saved ones."""
-        if torch.distributed.is_available() and torch.distributed.is_initialized() \
-                and torch.distributed.get_world_size() > 1:
-            for b in self.buffers():
-                torch.distributed.broadcast(b, 0)
+        dp.broadcast_buffers(self)
 
     # ---- training (model.py:184-361) ----------------------------------------------------------
     def _loss(self, X, c_org, out_decoder, out_postnet, content_codes, mu=1, lambd=1):
@@ -291,11 +288,7 @@ class AutoEncoder(nn.Module):
                           content_codes=content_codes)
         self.optimiser.zero_grad()
         loss.backward()
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            ws = torch.distributed.get_world_size()
-            if ws > 1:
-                torch.distributed.all_reduce(self._flat_grad)
-                self._flat_grad.div_(ws)
+        dp.average_gradients(self._flat_grad)  # data parallel: one RCCL all-reduce, no-op at N=1
         self.optimiser.step(max_norm=max_norm, ema=self.avg_params, ema_decay=ema_decay)
         return loss.detach(), self.optimiser.last_grad_norm
 
