@@ -72,7 +72,7 @@ size_t gen_scratch(int T, int B) {
   nested = std::max(nested, lstm_forward_scratch(T, B, 512, 32, false));
   nested = std::max(nested, lstm_forward_scratch(T, B, 320, 512, false));
   nested = std::max(nested, lstm_forward_scratch(T, B, 512, 1024, false));
-  nested = std::max(nested, lstm_forward_scratch(T, B, 1024, 1024, false));
+  nested = std::max(nested, lstm2_forward_scratch(T, B, 512, 1024, false));
   GemmDesc lin;
   lin.M = (int)TB; lin.N = 80; lin.Kc = 1024; lin.b_trans = 1;
   nested = std::max(nested, gemm_scratch_bytes(lin));
@@ -134,10 +134,9 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TRY(cba(P_DEC_CONV + 6, 512, 512, bb, ba, AVC_ACT_RELU, nullptr));
   AVC_TRY(cba(P_DEC_CONV + 12, 512, 512, ba, bb, AVC_ACT_RELU, nullptr));
   const int D2 = P_DEC_LSTM2;
-  AVC_TRY(lstm_forward_impl(ctx, T, B, 512, 1024, 0, bb, 512, P[D2], P[D2 + 1], P[D2 + 2], P[D2 + 3],
-                            l1, 1024, nullptr, nullptr, s));
-  AVC_TRY(lstm_forward_impl(ctx, T, B, 1024, 1024, 0, l1, 1024, P[D2 + 4], P[D2 + 5], P[D2 + 6],
-                            P[D2 + 7], l2, 1024, nullptr, nullptr, s));
+  // decoder.lstm2: both layers advanced as one wavefront (lstm.hip: lstm2_forward_impl)
+  AVC_TRY(lstm2_forward_impl(ctx, T, B, 512, 1024, bb, 512, P + D2, P + D2 + 4, l1, l2, nullptr,
+                             nullptr, nullptr, nullptr, s));
   GemmDesc lin;
   lin.M = (int)TB; lin.N = 80; lin.Kc = 1024;
   lin.A = l2; lin.lda = 1024;

@@ -24,6 +24,11 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
                        float* d_b_ih, float* d_b_hh, int accumulate_dx, int accumulate_dw,
                        hipStream_t s);
 size_t lstm_backward_scratch(int T, int B, int din, int H);
+// two stacked layers as a wavefront (w0/w1 = {w_ih, w_hh, b_ih, b_hh}); saved buffers optional
+int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                       const float* const* w0, const float* const* w1, float* y0, float* y1,
+                       float* g0, float* c0, float* g1, float* c1, hipStream_t s);
+size_t lstm2_forward_scratch(int T, int B, int din, int H, bool training);
 
 // ---- conv + BN (convbn.hip) ----
 int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,

@@ -41,6 +41,27 @@ __global__ void permute_rows_kernel(const float* __restrict__ src, float* __rest
   }
 }
 
+// dst[p][0:Da] = A[orig(p)][:], dst[p][Da:Da+Db] = Bm[orig(p)][:]   (4H rows)
+__global__ void permute_concat_kernel(const float* __restrict__ A, int Da, const float* __restrict__ Bm,
+                                      int Db, float* __restrict__ dst, int H) {
+  const int D = Da + Db;
+  const long total = 4L * H * D;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int p = (int)(idx / D);
+    const int c = (int)(idx - (long)p * D);
+    const long o = perm_to_orig(p, H);
+    dst[idx] = c < Da ? A[o * Da + c] : Bm[o * Db + (c - Da)];
+  }
+}
+
+// dst[p] = a[orig(p)] + b[orig(p)]
+__global__ void permute_vec_sum_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                       float* __restrict__ dst, int H) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < 4 * H) dst[p] = a[perm_to_orig(p, H)] + b[perm_to_orig(p, H)];
+}
+
 __global__ void permute_vec_kernel(const float* __restrict__ src, float* __restrict__ dst, int H) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < 4 * H) dst[p] = src[perm_to_orig(p, H)];
@@ -87,17 +108,23 @@ __global__ void unpermute_vec2_kernel(const float* __restrict__ src, float* __re
   }
 }
 
+// Per-launch arguments.  A launch may run two independent recurrences side by side (the two
+// stacked layers of decoder.lstm2, layer 1 one step behind layer 0): blocks [0, nblk0) run
+// layer slot 0, the rest slot 1.  The reduction operand of slot L is the concatenation of A[L]
+// (columns [0, K0[L])) and A1[L] (columns [K0[L], K[L])); a NULL source contributes zero.
 struct StepArgs {
-  int B, H, K, kw;
-  const float* A; long lda;  // h_{t-1} (fwd) or dG of the next-processed step (bwd); null => 0
-  const float* W;            // [ncols][K] K-contiguous rows
+  int B, H, nblk0;
+  int K[2], kw[2], K0[2];
+  const float* A[2]; long lda[2];
+  const float* A1[2]; long lda1[2];
+  const float* W[2];   // [ncols][K] K-contiguous rows (permuted gate order)
   // forward
-  const float* gx; const float* c_prev; float* c_out; float* h_out; long ldh_out; float* gates_out;
-  // backward
+  const float* gx[2]; long ldgx[2];   // per-row input projection (+biases); ldgx 0 = one shared row
+  const float* c_prev[2]; float* c_out[2]; float* h_out[2]; long ldh_out[2]; float* gates_out[2];
+  // backward (slot 0 only)
   const float* dy; long lddy; const float* gates; const float* c_cur; const float* c_prv;
   float* dc; float* dg_out;
 };
-
 
 template <int MB, bool BWD, int CPT>
 __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
@@ -106,7 +133,8 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
   constexpr int G = MB == 64 ? 2 : 4;
   extern __shared__ float part[];  // [NW][MB][16]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, NW = blockDim.x >> 6;
-  const int cb = blockIdx.x, rb = blockIdx.y;
+  const int L = (int)blockIdx.x >= a.nblk0 ? 1 : 0;  // block-uniform layer slot
+  const int cb = blockIdx.x - (L ? a.nblk0 : 0), rb = blockIdx.y;
   const int l15 = lane & 15, lk = 4 * (lane >> 4);
 
   f32x4 acc0[RT], acc1[RT];
@@ -132,12 +160,12 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
     if (!cok[i]) continue;
     if (!BWD) {
       const int u = cell & 3;
-      const float* g = a.gx + (long)b * 4 * H + cb * 16 + u;
+      const float* g = a.gx[L] + (long)b * a.ldgx[L] + cb * 16 + u;
       pf[i][0] = g[0];
       pf[i][1] = g[4];
       pf[i][2] = g[8];
       pf[i][3] = g[12];
-      pf[i][4] = a.c_prev ? a.c_prev[(long)b * H + cb * 4 + u] : 0.f;
+      pf[i][4] = a.c_prev[L] ? a.c_prev[L][(long)b * H + cb * 4 + u] : 0.f;
     } else {
       const int j = cb * 16 + (cell & 15);
       const long pb = (long)b * 4 * H + (j >> 2) * 16 + (j & 3);
@@ -152,18 +180,23 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
     }
   }
 
-  if (a.A != nullptr) {
-    const int kbeg = w * a.kw;
-    const float* wrow = a.W + (long)(cb * 16 + l15) * a.K + kbeg + lk;
+  const int kw = a.kw[L];
+  const int kbeg = w * kw;
+  const bool second = kbeg >= a.K0[L];
+  const float* src = second ? a.A1[L] : a.A[L];
+  if (src != nullptr) {
+    const long lds_ = second ? a.lda1[L] : a.lda[L];
+    const int koff = second ? kbeg - a.K0[L] : kbeg;
+    const float* wrow = a.W[L] + (long)(cb * 16 + l15) * a.K[L] + kbeg + lk;
     const float* arow[RT];
     bool aok[RT];
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       const int b = rb * MB + r * 16 + l15;
       aok[r] = b < a.B;
-      arow[r] = a.A + (long)(aok[r] ? b : 0) * a.lda + kbeg + lk;
+      arow[r] = src + (long)(aok[r] ? b : 0) * lds_ + koff + lk;
     }
-    for (int c0 = 0; c0 < a.kw; c0 += 16 * G) {
+    for (int c0 = 0; c0 < kw; c0 += 16 * G) {
       float4 wv[G], av[G][RT];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -217,10 +250,10 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
       const int j = cb * 4 + u;
       const float c = fg * pf[i][4] + ig * gg;
       const float h = og * tanhf(c);
-      a.c_out[(long)b * H + j] = c;
-      a.h_out[(long)b * a.ldh_out + j] = h;
-      if (a.gates_out) {
-        float* go = a.gates_out + (long)b * 4 * H + cb * 16 + u;
+      a.c_out[L][(long)b * H + j] = c;
+      a.h_out[L][(long)b * a.ldh_out[L] + j] = h;
+      if (a.gates_out[L]) {
+        float* go = a.gates_out[L] + (long)b * 4 * H + cb * 16 + u;
         go[0] = ig;
         go[4] = fg;
         go[8] = gg;
@@ -299,9 +332,14 @@ void launch_step(const StepCfg& cfg, bool bwd, dim3 grid, const StepArgs& a, hip
   }
 #undef AVC_STEP_LAUNCH
   if (ev) {
-    // recurrent product B x (4H or H) x K plus the W_hh slice streamed once per step
-    const double flops = a.A ? 2.0 * a.B * (double)a.K * (bwd ? a.H : 4.0 * a.H) : 0.0;
-    const double bytes = 4.0 * 4.0 * (double)a.H * a.H;  // one pass over W_hh (4H x H fp32)
+    // recurrent (+ in-step input) product per active slot; weights streamed once per step
+    double flops = 0.0, bytes = 0.0;
+    const int nslots = a.nblk0 < (int)grid.x ? 2 : 1;
+    for (int L = (a.nblk0 == 0 ? 1 : 0); L < nslots; ++L) {
+      const double kk = (a.A[L] ? a.K0[L] : 0) + (a.A1[L] ? a.K[L] - a.K0[L] : 0);
+      flops += 2.0 * a.B * kk * (bwd ? a.H : 4.0 * a.H);
+      bytes += 4.0 * 4.0 * (double)a.H * a.K[L];
+    }
     timing_end(cls, ev, s, flops, bytes);
   }
 }
@@ -481,21 +519,126 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
     const int t = reverse ? T - 1 - st : st;
     const int tp = reverse ? t + 1 : t - 1;
     StepArgs a{};
-    a.B = B; a.H = H; a.K = H; a.kw = H / cfg.nw;
-    a.A = st > 0 ? y + (long)tp * B * ldy : nullptr;
-    a.lda = ldy;
-    a.W = whh_p;
-    a.gx = gx + (long)t * B * 4 * H;
+    a.B = B; a.H = H; a.nblk0 = (int)grid.x;
+    a.K[0] = H; a.K0[0] = H; a.kw[0] = H / cfg.nw;
+    a.A[0] = st > 0 ? y + (long)tp * B * ldy : nullptr;
+    a.lda[0] = ldy;
+    a.W[0] = whh_p;
+    a.gx[0] = gx + (long)t * B * 4 * H;
+    a.ldgx[0] = 4L * H;
     if (saved_c) {
-      a.c_prev = st > 0 ? saved_c + (long)tp * B * H : nullptr;
-      a.c_out = saved_c + (long)t * B * H;
+      a.c_prev[0] = st > 0 ? saved_c + (long)tp * B * H : nullptr;
+      a.c_out[0] = saved_c + (long)t * B * H;
     } else {
-      a.c_prev = st > 0 ? cpp + (long)((st - 1) & 1) * B * H : nullptr;
-      a.c_out = cpp + (long)(st & 1) * B * H;
+      a.c_prev[0] = st > 0 ? cpp + (long)((st - 1) & 1) * B * H : nullptr;
+      a.c_out[0] = cpp + (long)(st & 1) * B * H;
     }
-    a.h_out = y + (long)t * B * ldy;
-    a.ldh_out = ldy;
-    a.gates_out = saved_gates ? saved_gates + (long)t * B * 4 * H : nullptr;
+    a.h_out[0] = y + (long)t * B * ldy;
+    a.ldh_out[0] = ldy;
+    a.gates_out[0] = saved_gates ? saved_gates + (long)t * B * 4 * H : nullptr;
+    launch_step(cfg, false, grid, a, s);
+  }
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+size_t lstm2_forward_scratch(int T, int B, int din, int H, bool training) {
+  const size_t f = sizeof(float);
+  size_t s = (size_t)T * B * 4 * H * f + (size_t)4 * H * (din + H + 2 * H + 3) * f + 4096;
+  if (!training) s += (size_t)4 * B * H * f;
+  GemmDesc d;
+  d.M = T * B; d.N = 4 * H; d.Kc = din;
+  return s + gemm_scratch_bytes(d);
+}
+
+// Two stacked LSTM layers (decoder.lstm2, decoder.py:53,74) advanced as a wavefront: launch s
+// runs layer 0 at t = s and layer 1 at t = s-1 side by side, so 2T recurrent steps take T+1
+// launches.  Layer 1's input projection is folded into its recurrent product: its gates are
+// [h0_t | h1_{t-1}] . [W_ih1 | W_hh1]^T + (b_ih1 + b_hh1) with K = 2H.
+int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                       const float* const* w0, const float* const* w1, float* y0, float* y1,
+                       float* g0, float* c0, float* g1, float* c1, hipStream_t s) {
+  AVC_CHECK_ARG(T > 0 && B > 0 && din % 4 == 0 && ldx % 4 == 0, "lstm2: bad shape");
+  AVC_CHECK_ARG(H % 64 == 0, "lstm2: H must be a multiple of 64");
+  AVC_CHECK_ARG((g0 == nullptr) == (c0 == nullptr) && (g1 == nullptr) == (c1 == nullptr) &&
+                    (c0 == nullptr) == (c1 == nullptr), "lstm2: saved buffers all or none");
+  Scratch sc(ctx);
+  const long TB = (long)T * B;
+  AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
+  AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
+  AVC_TAKE(whh_p, float, (size_t)4 * H * H, sc);
+  AVC_TAKE(w1_p, float, (size_t)4 * H * 2 * H, sc);
+  AVC_TAKE(bih_p, float, (size_t)4 * H, sc);
+  AVC_TAKE(bhh_p, float, (size_t)4 * H, sc);
+  AVC_TAKE(b1_p, float, (size_t)4 * H, sc);
+  permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w0[0], wih_p, H, din);
+  permute_rows_kernel<<<ew_blocks(4L * H * H), 256, 0, s>>>(w0[1], whh_p, H, H);
+  permute_vec_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w0[2], bih_p, H);
+  permute_vec_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w0[3], bhh_p, H);
+  permute_concat_kernel<<<ew_blocks(8L * H * H), 256, 0, s>>>(w1[0], H, w1[1], H, w1_p, H);
+  permute_vec_sum_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w1[2], w1[3], b1_p, H);
+  AVC_LAUNCH_CHECK();
+  GemmDesc g;
+  g.M = (int)TB; g.N = 4 * H; g.Kc = din;
+  g.A = x; g.lda = ldx; g.a_rows = TB;
+  g.b_trans = 1; g.ldb = din; g.B = wih_p; g.bias0 = bih_p; g.bias1 = bhh_p;
+  g.C = gx; g.ldc = 4 * H;
+  AVC_TRY(gemm_run(ctx, g, s));
+
+  float* cpp0 = nullptr;
+  float* cpp1 = nullptr;
+  if (!c0) {
+    AVC_TAKE(tmp, float, (size_t)4 * B * H, sc);
+    cpp0 = tmp;
+    cpp1 = tmp + 2L * B * H;
+  }
+  StepCfg cfg = step_cfg(B, H / 4, H);
+  cfg.nw = 4;  // both slots share the block shape; layer 1 waves 0-1 read h0, 2-3 read h1
+  const int nb = H / 4;
+  for (int st = 0; st <= T; ++st) {
+    const bool l0 = st < T, l1 = st >= 1;
+    StepArgs a{};
+    a.B = B; a.H = H;
+    const int t0 = st, t1 = st - 1;
+    // slot 0: layer 0 at t0
+    a.K[0] = H; a.K0[0] = H; a.kw[0] = H / cfg.nw;
+    a.A[0] = (l0 && t0 > 0) ? y0 + (long)(t0 - 1) * B * H : nullptr;
+    a.lda[0] = H;
+    a.W[0] = whh_p;
+    a.gx[0] = gx + (long)(l0 ? t0 : 0) * B * 4 * H;
+    a.ldgx[0] = 4L * H;
+    if (c0) {
+      a.c_prev[0] = (l0 && t0 > 0) ? c0 + (long)(t0 - 1) * B * H : nullptr;
+      a.c_out[0] = c0 + (long)(l0 ? t0 : 0) * B * H;
+    } else {
+      a.c_prev[0] = (l0 && t0 > 0) ? cpp0 + (long)((t0 - 1) & 1) * B * H : nullptr;
+      a.c_out[0] = cpp0 + (long)(t0 & 1) * B * H;
+    }
+    a.h_out[0] = y0 + (long)(l0 ? t0 : 0) * B * H;
+    a.ldh_out[0] = H;
+    a.gates_out[0] = g0 ? g0 + (long)(l0 ? t0 : 0) * B * 4 * H : nullptr;
+    // slot 1: layer 1 at t1 (input h0_{t1} | recurrent h1_{t1-1})
+    a.K[1] = 2 * H; a.K0[1] = H; a.kw[1] = 2 * H / cfg.nw;
+    a.A[1] = l1 ? y0 + (long)t1 * B * H : nullptr;
+    a.lda[1] = H;
+    a.A1[1] = (l1 && t1 > 0) ? y1 + (long)(t1 - 1) * B * H : nullptr;
+    a.lda1[1] = H;
+    a.W[1] = w1_p;
+    a.gx[1] = b1_p;
+    a.ldgx[1] = 0;
+    const int tt1 = l1 ? t1 : 0;
+    if (c1) {
+      a.c_prev[1] = (l1 && t1 > 0) ? c1 + (long)(t1 - 1) * B * H : nullptr;
+      a.c_out[1] = c1 + (long)tt1 * B * H;
+    } else {
+      a.c_prev[1] = (l1 && t1 > 0) ? cpp1 + (long)((t1 - 1) & 1) * B * H : nullptr;
+      a.c_out[1] = cpp1 + (long)(tt1 & 1) * B * H;
+    }
+    a.h_out[1] = y1 + (long)tt1 * B * H;
+    a.ldh_out[1] = H;
+    a.gates_out[1] = g1 ? g1 + (long)tt1 * B * 4 * H : nullptr;
+    a.nblk0 = l0 ? nb : 0;
+    dim3 grid((l0 ? nb : 0) + (l1 ? nb : 0), (B + cfg.mb - 1) / cfg.mb);
     launch_step(cfg, false, grid, a, s);
   }
   AVC_LAUNCH_CHECK();
@@ -551,10 +694,11 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
       const int tn = reverse ? t - 1 : t + 1;  // time index processed after t in the forward pass
       const int tp = reverse ? t + 1 : t - 1;
       StepArgs a{};
-      a.B = B; a.H = H; a.K = 4 * H; a.kw = 4 * H / cfg.nw;
-      a.A = st < T - 1 ? dg + (long)tn * B * 4 * H : nullptr;
-      a.lda = 4 * H;
-      a.W = whhT_p;
+      a.B = B; a.H = H; a.nblk0 = (int)grid.x;
+      a.K[0] = 4 * H; a.K0[0] = 4 * H; a.kw[0] = 4 * H / cfg.nw;
+      a.A[0] = st < T - 1 ? dg + (long)tn * B * 4 * H : nullptr;
+      a.lda[0] = 4 * H;
+      a.W[0] = whhT_p;
       a.dy = d_y + (long)t * B * ldy;
       a.lddy = ldy;
       a.gates = saved_gates + (long)t * B * 4 * H;
