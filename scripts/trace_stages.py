@@ -31,9 +31,9 @@ for k, (c, t) in sorted(stages.items(), key=lambda kv: -kv[1][1]):
 by = {}
 for r in fw:
     if r["Kernel_Name"] == "lstm_step_kernel":
-        g = (r["Grid_Size_X"], r["Workgroup_Size_X"])
+        g = (int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]), r["Grid_Size_Y"], r["Workgroup_Size_X"])
         by.setdefault(g, []).append(r["e"] - r["s"])
-for g, v in by.items():
+for g, v in sorted(by.items()):
     print("lstm_step grid", g, "n", len(v), "avg us", round(sum(v) / len(v) / 1e3, 2), "min", min(v) / 1e3)
 gs = [(r["Grid_Size_X"], r["Grid_Size_Y"], (r["e"] - r["s"]) / 1e3) for r in fw if r["Kernel_Name"] == "gemm_kernel"]
 print("gemm launches (gridX, gridY, us):", gs)
