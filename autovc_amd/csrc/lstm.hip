@@ -127,7 +127,7 @@ struct StepArgs {
 };
 
 template <int MB, bool BWD, int CPT>
-__global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
+__global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
   constexpr int RT = MB / 16;
   // 16-deep k-chunks loaded per batch; fewer for the 64-row tile to stay within 128 VGPRs
   constexpr int G = MB == 64 ? 2 : 4;
@@ -196,27 +196,36 @@ __global__ __launch_bounds__(1024) void lstm_step_kernel(StepArgs a) {
       aok[r] = b < a.B;
       arow[r] = src + (long)(aok[r] ? b : 0) * lds_ + koff + lk;
     }
-    for (int c0 = 0; c0 < kw; c0 += 16 * G) {
-      float4 wv[G], av[G][RT];
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        wv[g] = *reinterpret_cast<const float4*>(wrow + c0 + 16 * g);
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          av[g][r] = aok[r] ? *reinterpret_cast<const float4*>(arow[r] + c0 + 16 * g)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int r = 0; r < RT; ++r) {
-          f32x4& acc = (g & 1) ? acc1[r] : acc0[r];
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r].x, wv[g].x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r].y, wv[g].y, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r].z, wv[g].z, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r].w, wv[g].w, acc, 0, 0, 0);
-        }
+    // Register double-buffering: the loads of group g+1 are in flight while group g's MFMAs
+    // run (named buffers, unrolled by two, so no register array is indexed at run time).
+    float4 wA[G], hA[G][RT], wB[G], hB[G][RT];
+#define AVC_GROUP_LOAD(WV, HV, C0)                                                               \
+  _Pragma("unroll") for (int g = 0; g < G; ++g) {                                               \
+    WV[g] = *reinterpret_cast<const float4*>(wrow + (C0) + 16 * g);                             \
+    _Pragma("unroll") for (int r = 0; r < RT; ++r)                                              \
+      HV[g][r] = aok[r] ? *reinterpret_cast<const float4*>(arow[r] + (C0) + 16 * g)             \
+                        : make_float4(0.f, 0.f, 0.f, 0.f);                                      \
+  }
+#define AVC_GROUP_MFMA(WV, HV)                                                                   \
+  _Pragma("unroll") for (int g = 0; g < G; ++g)                                                 \
+    _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                            \
+      f32x4& acc = (g & 1) ? acc1[r] : acc0[r];                                                 \
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(HV[g][r].x, WV[g].x, acc, 0, 0, 0);           \
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(HV[g][r].y, WV[g].y, acc, 0, 0, 0);           \
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(HV[g][r].z, WV[g].z, acc, 0, 0, 0);           \
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(HV[g][r].w, WV[g].w, acc, 0, 0, 0);           \
     }
+    constexpr int GK = 16 * G;
+    AVC_GROUP_LOAD(wA, hA, 0)
+    for (int c0 = 0; c0 < kw; c0 += 2 * GK) {
+      const bool has_b = c0 + GK < kw;
+      if (has_b) { AVC_GROUP_LOAD(wB, hB, c0 + GK) }
+      AVC_GROUP_MFMA(wA, hA)
+      if (c0 + 2 * GK < kw) { AVC_GROUP_LOAD(wA, hA, c0 + 2 * GK) }
+      if (has_b) { AVC_GROUP_MFMA(wB, hB) }
+    }
+#undef AVC_GROUP_LOAD
+#undef AVC_GROUP_MFMA
   }
   // 16x16 accumulator layout: column = lane&15, rows 4*(lane>>4) + e
 #pragma unroll
@@ -295,9 +304,9 @@ StepCfg step_cfg(int B, int ncolblocks, int K) {
   else if ((long)ncolblocks * ((B + 63) / 64) >= 240) c.mb = 64;
   else if ((long)ncolblocks * ((B + 31) / 32) >= 240) c.mb = 32;
   else c.mb = 16;
-  c.nw = std::max(1, std::min(16, K / 64));
+  c.nw = std::max(1, std::min(8, K / 128));
   if (g_force_mb) c.mb = g_force_mb;
-  if (g_force_nw) c.nw = std::min(g_force_nw, std::max(1, K / 64));
+  if (g_force_nw) c.nw = std::min(std::min(g_force_nw, 8), std::max(1, K / 64));
   while (K % (c.nw * 64) != 0) --c.nw;
   // the epilogue gives each thread at most 4 cells (16 per row in backward, 4 in forward)
   while (c.mb * 16 > 4 * 64 * c.nw && c.mb > 16) c.mb /= 2;
@@ -761,8 +770,8 @@ extern "C" int avc_lstm_tune(int rows_per_block, int waves) {
     avc::set_error("avc_lstm_tune: rows_per_block must be 0, 16, 32 or 64");
     return AVC_ERR_INVALID;
   }
-  if (waves < 0 || waves > 16) {
-    avc::set_error("avc_lstm_tune: waves must be 0..16");
+  if (waves < 0 || waves > 8) {
+    avc::set_error("avc_lstm_tune: waves must be 0..8");
     return AVC_ERR_INVALID;
   }
   avc::g_force_mb = rows_per_block;

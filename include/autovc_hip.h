@@ -184,7 +184,7 @@ int avc_generator_forward(avc_context* ctx, int T, int B, const float* const* pa
  * 2 LSTM step backward, 3 H=32 persistent LSTM. */
 int avc_timing_enable(int mask);
 /* Tuning hook for the per-step LSTM kernel: force the batch rows per workgroup (16/32/64) and the
- * number of waves splitting the reduction (1..16); 0 restores the automatic choice. */
+ * number of waves splitting the reduction (1..8); 0 restores the automatic choice. */
 int avc_lstm_tune(int rows_per_block, int waves);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,

@@ -19,7 +19,7 @@ def run(din, H, B, T, bwd):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = {}
     _lib.timing_enable(["lstm_step_fwd", "lstm_step_bwd"])
-    for mb, nw in itertools.product([16, 32, 64], [4, 8, 16]):
+    for mb, nw in itertools.product([16, 32, 64], [2, 4, 8]):
         _lib.call("avc_lstm_tune", mb, nw)
         for rep in range(3):
             _lib.timing_reset()
