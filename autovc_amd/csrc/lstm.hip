@@ -131,11 +131,16 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
   constexpr int RT = MB / 16;
   // 16-deep k-chunks loaded per batch; fewer for the 64-row tile to stay within 128 VGPRs
   constexpr int G = MB == 64 ? 2 : 4;
+
   extern __shared__ float part[];  // [NW][MB][16]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, NW = blockDim.x >> 6;
   const int L = (int)blockIdx.x >= a.nblk0 ? 1 : 0;  // block-uniform layer slot
   const int cb = blockIdx.x - (L ? a.nblk0 : 0), rb = blockIdx.y;
-  const int l15 = lane & 15, lk = 4 * (lane >> 4);
+  const int l15 = lane & 15, lq = lane >> 4;
+  // K permutation of one 16*G group: lane quarter q owns k = 4Gq .. 4Gq+4G-1 (G float4, one
+  // contiguous 16G-byte run per row, so a wave instruction covers whole cache lines); MFMA
+  // (g, e) of the group consumes element e of float4 g on every lane — A and W alike.
+  const int lk = 4 * G * lq;
 
   f32x4 acc0[RT], acc1[RT];
 #pragma unroll
@@ -201,9 +206,9 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
     float4 wA[G], hA[G][RT], wB[G], hB[G][RT];
 #define AVC_GROUP_LOAD(WV, HV, C0)                                                               \
   _Pragma("unroll") for (int g = 0; g < G; ++g) {                                               \
-    WV[g] = *reinterpret_cast<const float4*>(wrow + (C0) + 16 * g);                             \
+    WV[g] = *reinterpret_cast<const float4*>(wrow + (C0) + 4 * g);                              \
     _Pragma("unroll") for (int r = 0; r < RT; ++r)                                              \
-      HV[g][r] = aok[r] ? *reinterpret_cast<const float4*>(arow[r] + (C0) + 16 * g)             \
+      HV[g][r] = aok[r] ? *reinterpret_cast<const float4*>(arow[r] + (C0) + 4 * g)              \
                         : make_float4(0.f, 0.f, 0.f, 0.f);                                      \
   }
 #define AVC_GROUP_MFMA(WV, HV)                                                                   \
@@ -232,7 +237,7 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
   for (int r = 0; r < RT; ++r)
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      part[(w * MB + r * 16 + lk + e) * 16 + l15] = acc0[r][e] + acc1[r][e];
+      part[(w * MB + r * 16 + 4 * lq + e) * 16 + l15] = acc0[r][e] + acc1[r][e];
   __syncthreads();
   // cross-wave reduction, one (row, column) per thread, fixed order; result in wave-0's slab
   // (each element is read and then overwritten by the same thread only)
