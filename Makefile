@@ -25,3 +25,9 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all clean check-abi
+
+# diagnostic build with in-kernel s_memtime stamps (never shipped): diag/libautovc_hip_stamps.so
+stamps:
+	@mkdir -p diag
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -DAVC_STAMPS -shared $(SRC) -o diag/libautovc_hip_stamps.so
+.PHONY: stamps

@@ -25,6 +25,25 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Diagnostic build only (-DAVC_STAMPS): per-wave s_memtime stamps at phase boundaries of the
+// step kernel, written to a debug buffer nothing else reads.  The shipped build has none.
+#ifdef AVC_STAMPS
+__device__ unsigned long long* g_stamps = nullptr;
+#define AVC_STAMP(slot)                                                                           \
+  do {                                                                                            \
+    unsigned long long _t;                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (g_stamps && lane == 0) {                                                                  \
+      const long wid = ((long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + w;       \
+      if (wid < 65536) g_stamps[wid * 8 + (slot)] = _t;                                           \
+    }                                                                                             \
+  } while (0)
+#else
+#define AVC_STAMP(slot) do { } while (0)
+#endif
+
 __host__ __device__ __forceinline__ int perm_to_orig(int p, int H) {
   const int blk = p >> 4, g = (p >> 2) & 3, u = p & 3;
   return g * H + blk * 4 + u;
@@ -135,6 +154,7 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
   extern __shared__ float part[];  // [NW][MB][16]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, NW = blockDim.x >> 6;
   const int L = (int)blockIdx.x >= a.nblk0 ? 1 : 0;  // block-uniform layer slot
+  AVC_STAMP(0);
   const int cb = blockIdx.x - (L ? a.nblk0 : 0), rb = blockIdx.y;
   const int l15 = lane & 15, lq = lane >> 4;
   // K permutation of one 16*G group: lane quarter q owns k = 4Gq .. 4Gq+4G-1 (G float4, one
@@ -222,6 +242,10 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
     }
     constexpr int GK = 16 * G;
     AVC_GROUP_LOAD(wA, hA, 0)
+#ifdef AVC_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AVC_STAMP(1);
+#endif
     for (int c0 = 0; c0 < kw; c0 += 2 * GK) {
       const bool has_b = c0 + GK < kw;
       if (has_b) { AVC_GROUP_LOAD(wB, hB, c0 + GK) }
@@ -232,6 +256,7 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
 #undef AVC_GROUP_LOAD
 #undef AVC_GROUP_MFMA
   }
+  AVC_STAMP(2);
   // 16x16 accumulator layout: column = lane&15, rows 4*(lane>>4) + e
 #pragma unroll
   for (int r = 0; r < RT; ++r)
@@ -249,6 +274,7 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
     }
     __syncthreads();
   }
+  AVC_STAMP(3);
 
   if (!BWD) {
 #pragma unroll
@@ -295,6 +321,7 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
       a.dg_out[pb + 12] = dh * tc * og * (1.f - og);
     }
   }
+  AVC_STAMP(4);
 }
 
 struct StepCfg {
@@ -325,7 +352,16 @@ int cells_per_thread(const StepCfg& c, bool bwd) {
   return cpt <= 1 ? 1 : (cpt <= 2 ? 2 : 4);
 }
 
+#ifdef AVC_STAMPS
+void* g_stamp_buf = nullptr;
+long g_stamp_target = -1, g_stamp_count = 0;
+#endif
+
 void launch_step(const StepCfg& cfg, bool bwd, dim3 grid, const StepArgs& a, hipStream_t s) {
+#ifdef AVC_STAMPS
+  const bool rec = g_stamp_count++ == g_stamp_target && g_stamp_buf;
+  if (rec) (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_stamps), &g_stamp_buf, sizeof(void*), 0, hipMemcpyHostToDevice, s);
+#endif
   const size_t lds = (size_t)cfg.nw * cfg.mb * 16 * sizeof(float);
   const int threads = cfg.nw * 64;
   const int cls = bwd ? TC_LSTM_STEP_BWD : TC_LSTM_STEP_FWD;
@@ -345,6 +381,13 @@ void launch_step(const StepCfg& cfg, bool bwd, dim3 grid, const StepArgs& a, hip
     else { AVC_STEP_LAUNCH(16, true) }
   }
 #undef AVC_STEP_LAUNCH
+#ifdef AVC_STAMPS
+  if (rec) {
+    static void* null_ptr = nullptr;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_stamps), &null_ptr, sizeof(void*), 0, hipMemcpyHostToDevice, s);
+    (void)hipStreamSynchronize(s);
+  }
+#endif
   if (ev) {
     // recurrent (+ in-step input) product per active slot; weights streamed once per step
     double flops = 0.0, bytes = 0.0;
@@ -769,6 +812,15 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
 }
 
 }  // namespace avc
+
+#ifdef AVC_STAMPS
+extern "C" int avc_debug_stamps(void* buf, long target_launch) {
+  avc::g_stamp_buf = buf;
+  avc::g_stamp_target = target_launch;
+  avc::g_stamp_count = 0;
+  return AVC_OK;
+}
+#endif
 
 extern "C" int avc_lstm_tune(int rows_per_block, int waves) {
   if (!(rows_per_block == 0 || rows_per_block == 16 || rows_per_block == 32 || rows_per_block == 64)) {

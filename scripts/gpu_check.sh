@@ -24,6 +24,7 @@ for step in "$@"; do
     perf)  run perf 400 python scripts/perf_layers.py ;;
     prof)  run prof 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o fwd -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-timing ;;
     sweep) run sweep 600 python scripts/sweep_lstm.py ;;
+    stamps) run stamps 300 python scripts/stamps_lstm.py ;;
     benchtrain) run benchtrain 400 python bench.py --mode train --steps 5 --warmup 2 --no-cpu ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
