@@ -241,18 +241,25 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(HV[g][r].w, WV[g].w, acc, 0, 0, 0);           \
     }
     constexpr int GK = 16 * G;
-    AVC_GROUP_LOAD(wA, hA, 0)
+    // Every workgroup reads the same h rows; if all start at k = 0 the CUs of an XCD request the
+    // same lines at the same time and queue on one L2 channel.  Rotate the starting group by
+    // the workgroup's position within its XCD (block id / 8) so they stream different lines.
+    const int ng = kw / GK;
+    const int rot = (int)((blockIdx.x >> 3) % (unsigned)ng);
+#define AVC_COFS(I) ((((I) + rot) % ng) * GK)
+    AVC_GROUP_LOAD(wA, hA, AVC_COFS(0))
 #ifdef AVC_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     AVC_STAMP(1);
 #endif
-    for (int c0 = 0; c0 < kw; c0 += 2 * GK) {
-      const bool has_b = c0 + GK < kw;
-      if (has_b) { AVC_GROUP_LOAD(wB, hB, c0 + GK) }
+    for (int i = 0; i < ng; i += 2) {
+      const bool has_b = i + 1 < ng;
+      if (has_b) { AVC_GROUP_LOAD(wB, hB, AVC_COFS(i + 1)) }
       AVC_GROUP_MFMA(wA, hA)
-      if (c0 + 2 * GK < kw) { AVC_GROUP_LOAD(wA, hA, c0 + 2 * GK) }
+      if (i + 2 < ng) { AVC_GROUP_LOAD(wA, hA, AVC_COFS(i + 2)) }
       if (has_b) { AVC_GROUP_MFMA(wB, hB) }
     }
+#undef AVC_COFS
 #undef AVC_GROUP_LOAD
 #undef AVC_GROUP_MFMA
   }
