@@ -223,13 +223,15 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
     }
     // Register double-buffering: the loads of group g+1 are in flight while group g's MFMAs
     // run (named buffers, unrolled by two, so no register array is indexed at run time).
+    // Loads are unconditional (rows >= B read row 0 and are never stored): a per-lane
+    // "load or zero" select makes hipcc branch around each load and drain vmcnt to 0,
+    // which would serialise the prefetch.
     float4 wA[G], hA[G][RT], wB[G], hB[G][RT];
 #define AVC_GROUP_LOAD(WV, HV, C0)                                                               \
   _Pragma("unroll") for (int g = 0; g < G; ++g) {                                               \
     WV[g] = *reinterpret_cast<const float4*>(wrow + (C0) + 4 * g);                              \
     _Pragma("unroll") for (int r = 0; r < RT; ++r)                                              \
-      HV[g][r] = aok[r] ? *reinterpret_cast<const float4*>(arow[r] + (C0) + 4 * g)              \
-                        : make_float4(0.f, 0.f, 0.f, 0.f);                                      \
+      HV[g][r] = *reinterpret_cast<const float4*>(arow[r] + (C0) + 4 * g);                     \
   }
 #define AVC_GROUP_MFMA(WV, HV)                                                                   \
   _Pragma("unroll") for (int g = 0; g < G; ++g)                                                 \
@@ -246,20 +248,46 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
     // the workgroup's position within its XCD (block id / 8) so they stream different lines.
     const int ng = kw / GK;
     const int rot = (int)((blockIdx.x >> 3) % (unsigned)ng);
-#define AVC_COFS(I) ((((I) + rot) % ng) * GK)
-    AVC_GROUP_LOAD(wA, hA, AVC_COFS(0))
+    // running K offset of the next group to load, wrapped at kw (no divisions in the loop)
+    int cnext = rot * GK;
+#define AVC_NEXT(C) { C = cnext; cnext += GK; cnext = cnext >= kw ? cnext - kw : cnext; }
+    // sched_barrier pins the program order below: without it the scheduler sinks the next
+    // group's loads under the current MFMAs' consumers and the waitcnt pass drains vmcnt to 0.
+#define AVC_PIN __builtin_amdgcn_sched_barrier(0);
+    int c;
+    AVC_NEXT(c)
+    AVC_GROUP_LOAD(wA, hA, c)
 #ifdef AVC_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     AVC_STAMP(1);
 #endif
-    for (int i = 0; i < ng; i += 2) {
-      const bool has_b = i + 1 < ng;
-      if (has_b) { AVC_GROUP_LOAD(wB, hB, AVC_COFS(i + 1)) }
+    // steady state: one basic block per two groups (no conditional loads, so hipcc can count
+    // vmcnt and keep the next group's loads in flight under the current MFMAs)
+    int i = 0;
+    for (; i + 2 < ng; i += 2) {
+      AVC_NEXT(c)
+      AVC_GROUP_LOAD(wB, hB, c)
+      AVC_PIN
       AVC_GROUP_MFMA(wA, hA)
-      if (i + 2 < ng) { AVC_GROUP_LOAD(wA, hA, AVC_COFS(i + 2)) }
-      if (has_b) { AVC_GROUP_MFMA(wB, hB) }
+      AVC_PIN
+      AVC_NEXT(c)
+      AVC_GROUP_LOAD(wA, hA, c)
+      AVC_PIN
+      AVC_GROUP_MFMA(wB, hB)
+      AVC_PIN
     }
-#undef AVC_COFS
+    if (ng - i == 2) {
+      AVC_NEXT(c)
+      AVC_GROUP_LOAD(wB, hB, c)
+      AVC_PIN
+      AVC_GROUP_MFMA(wA, hA)
+      AVC_PIN
+      AVC_GROUP_MFMA(wB, hB)
+    } else {
+      AVC_GROUP_MFMA(wA, hA)
+    }
+#undef AVC_PIN
+#undef AVC_NEXT
 #undef AVC_GROUP_LOAD
 #undef AVC_GROUP_MFMA
   }
