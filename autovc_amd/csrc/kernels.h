@@ -30,6 +30,19 @@ int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const flo
                        float* g0, float* c0, float* g1, float* c1, hipStream_t s);
 size_t lstm2_forward_scratch(int T, int B, int din, int H, bool training);
 
+// ---- split-fp16 LSTM forward recurrence (lstm_split.hip), used by the two above when supported
+bool lstm_split_supported(int H, int din);
+size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers);
+int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                            const float* x, int ldx, const float* w_ih, const float* w_hh,
+                            const float* b_ih, const float* b_hh, float* y, int ldy,
+                            float* saved_gates, float* saved_c, hipStream_t s);
+int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                             const float* const* w0, const float* const* w1, float* y0, float* y1,
+                             float* g0, float* c0, float* g1, float* c1, hipStream_t s);
+// rows of a [4H][D] gate matrix into the permuted gate order p = blk*16 + gate*4 + u (lstm.hip)
+int permute_rows(const float* src, float* dst, int H, int D, hipStream_t s);
+
 // ---- conv + BN (convbn.hip) ----
 int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
                              const float* weight, const float* bias, const float* gamma,

@@ -558,7 +558,14 @@ size_t lstm_forward_scratch(int T, int B, int din, int H, bool training) {
   if (H != 32) s += (size_t)4 * H * (din + H + 2) * f + (training ? 0 : (size_t)2 * B * H * f) + 2048;
   GemmDesc d;
   d.M = T * B; d.N = 4 * H; d.Kc = din;
-  return s + gemm_scratch_bytes(d);
+  s += gemm_scratch_bytes(d);
+  return lstm_split_supported(H, din) ? std::max(s, lstm_split_forward_scratch(T, B, din, H, 1)) : s;
+}
+
+int permute_rows(const float* src, float* dst, int H, int D, hipStream_t s) {
+  permute_rows_kernel<<<ew_blocks(4L * H * D), 256, 0, s>>>(src, dst, H, D);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
 }
 
 int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
@@ -568,6 +575,9 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
   AVC_CHECK_ARG(T > 0 && B > 0 && din > 0, "lstm: empty problem");
   AVC_CHECK_ARG(H == 32 || (H % 64 == 0), "lstm: H must be 32 or a multiple of 64");
   AVC_CHECK_ARG(din % 4 == 0 && ldx % 4 == 0, "lstm: din/ldx must be multiples of 4");
+  if (lstm_split_supported(H, din))
+    return lstm_split_forward_impl(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, b_ih, b_hh, y, ldy,
+                                   saved_gates, saved_c, s);
   Scratch sc(ctx);
   const long TB = (long)T * B;
   AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
@@ -640,7 +650,8 @@ size_t lstm2_forward_scratch(int T, int B, int din, int H, bool training) {
   if (!training) s += (size_t)4 * B * H * f;
   GemmDesc d;
   d.M = T * B; d.N = 4 * H; d.Kc = din;
-  return s + gemm_scratch_bytes(d);
+  s += gemm_scratch_bytes(d);
+  return lstm_split_supported(H, din) ? std::max(s, lstm_split_forward_scratch(T, B, din, H, 2)) : s;
 }
 
 // Two stacked LSTM layers (decoder.lstm2, decoder.py:53,74) advanced as a wavefront: launch s
@@ -654,6 +665,8 @@ int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const flo
   AVC_CHECK_ARG(H % 64 == 0, "lstm2: H must be a multiple of 64");
   AVC_CHECK_ARG((g0 == nullptr) == (c0 == nullptr) && (g1 == nullptr) == (c1 == nullptr) &&
                     (c0 == nullptr) == (c1 == nullptr), "lstm2: saved buffers all or none");
+  if (lstm_split_supported(H, din))
+    return lstm2_split_forward_impl(ctx, T, B, din, H, x, ldx, w0, w1, y0, y1, g0, c0, g1, c1, s);
   Scratch sc(ctx);
   const long TB = (long)T * B;
   AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);

@@ -1,0 +1,691 @@
+// LSTM forward recurrence on split-fp16 MFMA for gfx950 (decoder lstm1 / lstm2, H >= 64).
+//
+// Why: one time step of decoder.lstm2 (both layers, B = 64) is a [64 x 3072] . [3072 x 4096]
+// product — 1.6 GFLOP against 50 MB of weights.  In fp32 MFMA (64 FLOP/clk/SIMD) that alone is
+// >= 10 us per step; worse, with one 16-column tile per workgroup every workgroup re-reads the
+// whole h operand, so the per-CU load path (~70 GB/s per CU from L2) was the real limit.
+//
+// What:
+//   * "3xf16" products: every operand x (pre-scaled by a power of two) is stored as
+//     hi = f16(x), lo = f16(x - hi) and a dot product is accumulated in fp32 by
+//     v_mfma_f32_16x16x32_f16 as hi.hi + hi.lo + lo.hi (16x the fp32 MFMA rate per product, 3
+//     products).  hi+lo carries 22 significant bits; the dropped lo.lo term is 2^-22 relative;
+//     both are below the fp32 accumulation error of a K = 1024..2048 chain.
+//     Weights are scaled per gate row so |w| < 2^15, h (|h| < 1) by 2^15: no fp16 overflow and no
+//     subnormal lo terms that matter.  Unscaling is one multiply per gate in the epilogue.
+//   * tile = 64 batch rows x 64 gate rows (16 hidden units x 4 gates) per workgroup, so h is
+//     re-read 4H/64 times instead of 4H/16; the K range is split over the workgroup's 4 waves
+//     (LDS reduction) and over `nks` workgroups, whose fp32 slabs the last-arriving workgroup
+//     sums in a fixed order (write-through `sc1` slab stores, agent-scope ticket, `sc1` slab
+//     loads: cdna_hip_programming.md, in-launch split-K reduction) before running the gate
+//     epilogue.  Deterministic: the sum order never depends on arrival order.
+//
+// Split layout ("split rows"): a row of K values (K % 32 == 0) is K/32 chunks of 128 B,
+//   chunk c = [hi(k = 32c .. 32c+31) as f16 | lo(same) as f16].
+// Lane l of an MFMA holds k = 8(l>>4) .. 8(l>>4)+7 of a chunk: bytes 16(l>>4) (hi) and
+//   64 + 16(l>>4) (lo) — one 64-B run per row per load instruction.
+#include <algorithm>
+
+#include "kernels.h"
+#include "timing.h"
+
+namespace avc {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#ifdef AVC_STAMPS
+__device__ unsigned long long* g_sstamps = nullptr;
+#define AVC_STAMP(slot)                                                                           \
+  do {                                                                                            \
+    unsigned long long _t;                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (g_sstamps && lane == 0) {                                                                 \
+      const long wid = ((long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + w;       \
+      if (wid < 65536) g_sstamps[wid * 8 + (slot)] = _t;                                          \
+    }                                                                                             \
+  } while (0)
+#else
+#define AVC_STAMP(slot) do { } while (0)
+#endif
+
+constexpr float kHScale = 32768.0f;           // h is stored as h * 2^15
+constexpr float kHUnscale = 1.0f / 32768.0f;
+
+__host__ __device__ __forceinline__ int perm_to_orig(int p, int H) {
+  const int blk = p >> 4, g = (p >> 2) & 3, u = p & 3;
+  return g * H + blk * 4 + u;
+}
+
+__device__ __forceinline__ void split16(float v, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)v;
+  lo = (_Float16)(v - (float)hi);
+}
+
+// Split rows of a weight matrix: dst row p (of R = 4H, permuted gate order when perm != 0) is
+// [A[src(p)][0:Da] | Bm[src(p)][0:Db]] scaled by 2^(15 - e), e = exponent of the row's max |w|;
+// winv[p] = 2^(e - 15) * 2^-15 undoes both scalings.  One workgroup per row.
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ A, int Da,
+                                                         const float* __restrict__ Bm, int Db,
+                                                         int H, int perm,
+                                                         _Float16* __restrict__ dst,
+                                                         float* __restrict__ winv) {
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int o = perm ? perm_to_orig(p, H) : p;
+  const int K = Da + Db;
+  const float* ra = A + (long)o * Da;
+  const float* rb = Bm ? Bm + (long)o * Db : nullptr;
+  float m = 0.f;
+  for (int k = tid; k < K; k += 256) m = fmaxf(m, fabsf(k < Da ? ra[k] : rb[k - Da]));
+  __shared__ float red[256];
+  red[tid] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] = fmaxf(red[tid], red[tid + s]);
+    __syncthreads();
+  }
+  int e = 0;
+  if (red[0] > 0.f) (void)frexpf(red[0], &e);  // max < 2^e
+  const float sc = ldexpf(1.0f, 15 - e);
+  if (tid == 0) winv[p] = ldexpf(1.0f, e - 15) * kHUnscale;
+  _Float16* d = dst + (long)p * 2 * K;
+  for (int k = tid; k < K; k += 256) {
+    const float v = (k < Da ? ra[k] : rb[k - Da]) * sc;
+    _Float16 hi, lo;
+    split16(v, hi, lo);
+    d[(k >> 5) * 64 + (k & 31)] = hi;
+    d[(k >> 5) * 64 + 32 + (k & 31)] = lo;
+  }
+}
+
+// per-gate-row bias vector in permuted order: dst[p] = a[orig(p)] (+ b[orig(p)])
+__global__ void perm_bias_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                 float* __restrict__ dst, int H) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < 4 * H) dst[p] = a[perm_to_orig(p, H)] + (b ? b[perm_to_orig(p, H)] : 0.f);
+}
+
+struct SplitSlot {
+  int K, K0, kslice, nks, ncb;
+  const unsigned char* A; long lda;    // split rows of the reduction operand, columns [0, K0)
+  const unsigned char* A1; long lda1;  // columns [K0, K); NULL source = zeros
+  const unsigned char* W; long ldw;    // split weight rows [4H][K] (permuted gate order)
+  const float* winv;                   // [4H] unscale per gate row
+  const float* gx; long ldgx;          // input projection (+biases) per batch row; ldgx 0 = shared row
+  const float* c_prev;                 // NULL = zero state
+  float* c_out;
+  float* h_out; long ldh;              // fp32 h (the layer output)
+  _Float16* hs_out; long ldhs;         // split h for the next step (halves per row)
+  float* gates_out;                    // training: [B][4H] activated gates (permuted order)
+  float* slab;                         // [nrb][ncb][nks][64*64] fp32 partials
+  int* cnt;                            // [nrb][ncb] tickets, zero before the launch
+};
+
+struct SplitArgs {
+  int B, H, nblk0;
+  SplitSlot s[2];
+};
+
+constexpr int kRowPad = 68;  // LDS row stride (floats): conflict-free partial writes
+
+template <int NW, int NCH>
+__global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a) {
+  extern __shared__ float part[];  // [NW][64][kRowPad] + flag
+  constexpr int NT = NW * 64;
+  constexpr int PP = 256 / NT;  // (row, 16-column block) pairs per thread in the epilogue
+  // wave index through readfirstlane: the buffer descriptors below must be provably uniform, or
+  // hipcc wraps every buffer load in a waterfall loop
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int L = (int)blockIdx.x >= a.nblk0 ? 1 : 0;
+  const SplitSlot& S = L ? a.s[1] : a.s[0];
+  const int lb = blockIdx.x - (L ? a.nblk0 : 0);
+  const int nks = S.nks;
+  const int cb = lb / nks, ks = lb - cb * nks;
+  const int rb = blockIdx.y;
+  const int B = a.B, H = a.H;
+  const int nrows = min(64, B - rb * 64);
+  AVC_STAMP(0);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int kw = NCH * 32;  // == S.kslice / NW (host-checked)
+  const int k0 = ks * S.kslice + w * kw;
+  const bool second = k0 >= S.K0;
+  const unsigned char* src = second ? S.A1 : S.A;
+  if (src != nullptr) {
+    // buffer loads: lane part of the offset in one VGPR, the row-group / chunk part in SGPRs;
+    // rows >= B fall outside the descriptor's range and read as zero
+    const long lds_ = second ? S.lda1 : S.lda;
+    const int kc0 = (second ? k0 - S.K0 : k0) >> 5;
+    const auto hrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(src) + (long)rb * 64 * lds_ + (long)kc0 * 128, 0,
+        (int)(nrows * lds_ - (long)kc0 * 128), 0x00020000);
+    const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(S.W) + (long)cb * 64 * S.ldw + (long)(k0 >> 5) * 128, 0,
+        (int)(64 * S.ldw - (long)(k0 >> 5) * 128), 0x00020000);
+    const int hvo = l15 * (int)lds_ + lq * 16;
+    const int wvo = l15 * (int)S.ldw + lq * 16;
+    const int hrow16 = 16 * (int)lds_, wrow16 = 16 * (int)S.ldw;
+
+    f16x8 hA[4][2], wA[4][2], hB[4][2], wB[4][2];
+#define AVC_LD(RS, VO, SO) __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(RS, VO, SO, 0))
+#define AVC_LOAD(HV, WV, C)                                                                       \
+  _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                                 \
+    HV[r][0] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 128);                                          \
+    HV[r][1] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 128 + 64);                                     \
+  }                                                                                               \
+  _Pragma("unroll") for (int n = 0; n < 4; ++n) {                                                 \
+    WV[n][0] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 128);                                          \
+    WV[n][1] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 128 + 64);                                     \
+  }
+#define AVC_MFMA(HV, WV)                                                                          \
+  _Pragma("unroll") for (int r = 0; r < 4; ++r)                                                   \
+    _Pragma("unroll") for (int n = 0; n < 4; ++n) {                                               \
+      acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][1], WV[n][0], acc[r][n], 0, 0, 0); \
+      acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], WV[n][1], acc[r][n], 0, 0, 0); \
+      acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], WV[n][0], acc[r][n], 0, 0, 0); \
+    }
+#define AVC_PIN __builtin_amdgcn_sched_barrier(0);
+    // register double buffer, program order pinned (see lstm.hip: the scheduler otherwise sinks
+    // the next chunk's loads under the current MFMAs and the waitcnt pass drains to zero)
+    AVC_LOAD(hA, wA, 0)
+#ifdef AVC_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    AVC_STAMP(1);
+#endif
+    // fully unrolled (NCH is a template parameter): in a runtime loop hipcc's waitcnt pass
+    // merges the two buffers' pending loads at the back edge and waits for the just-issued ones
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (c + 1 < NCH) {
+        if (c & 1) { AVC_LOAD(hA, wA, c + 1) } else { AVC_LOAD(hB, wB, c + 1) }
+      }
+      AVC_PIN
+      if (c & 1) { AVC_MFMA(hB, wB) } else { AVC_MFMA(hA, wA) }
+      AVC_PIN
+    }
+#undef AVC_PIN
+#undef AVC_MFMA
+#undef AVC_LOAD
+#undef AVC_LD
+  }
+  AVC_STAMP(2);
+
+  // Epilogue ownership: thread t handles (row, blk) pairs t + NT*i; a pair's 4 float4 columns
+  // blk*16 + 4g (gate g, units 0..3) hold all four gates of 4 hidden units.  Its operands are
+  // fetched now so that their latency overlaps the reduction below.
+  f32x4 gxv[PP][4], wiv[PP][4], cpv[PP];
+#pragma unroll
+  for (int i = 0; i < PP; ++i) {
+    const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+    const int b = min(rb * 64 + row, B - 1);
+    const int p0 = cb * 64 + blk * 16;
+    const float* gxr = S.gx + (long)b * S.ldgx + p0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      gxv[i][g] = *reinterpret_cast<const f32x4*>(gxr + 4 * g);
+      wiv[i][g] = *reinterpret_cast<const f32x4*>(S.winv + p0 + 4 * g);
+    }
+    cpv[i] = S.c_prev ? *reinterpret_cast<const f32x4*>(S.c_prev + (long)b * H + cb * 16 + blk * 4)
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // wave partials -> LDS; C layout of 16x16: column lane&15, rows 4(lane>>4) + e
+  float* mine = part + w * 64 * kRowPad;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * kRowPad + n * 16 + l15] = acc[r][n][e];
+  __syncthreads();
+
+  f32x4 sum[PP][4];
+#pragma unroll
+  for (int i = 0; i < PP; ++i) {
+    const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int off = row * kRowPad + blk * 16 + 4 * g;
+      f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * 64 * kRowPad + off);
+      sum[i][g] = v;
+    }
+  }
+  AVC_STAMP(3);
+
+  if (nks > 1) {
+    // publish this workgroup's slab (write-through), take a ticket; the last one reduces.
+    // Slab element (row, col) of split s at s*4096 + row*64 + col.
+    const long tile = (long)rb * S.ncb + cb;
+    float* slab0 = S.slab + tile * nks * 4096;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(slab0, 0, nks * 4096 * 4, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < PP; ++i) {
+      const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sum[i][g]), rsrc,
+                                               (ks * 4096 + row * 64 + blk * 16 + 4 * g) * 4, 0, 16 /*sc1*/);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(part + NW * 64 * kRowPad);
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(S.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = old;
+    }
+    __syncthreads();
+    AVC_STAMP(4);
+    if (*flag != nks - 1) return;
+    // fixed order s = 0..nks-1, up to 8 slabs in flight per pass
+#pragma unroll
+    for (int i = 0; i < PP; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) sum[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < nks; s0 += 4) {
+      f32x4 v[4][PP][4];
+#pragma unroll
+      for (int s1 = 0; s1 < 4; ++s1)
+#pragma unroll
+        for (int i = 0; i < PP; ++i) {
+          const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            v[s1][i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rsrc, ((s0 + s1) * 4096 + row * 64 + blk * 16 + 4 * g) * 4, 0, 16 /*sc1*/));
+        }
+#pragma unroll
+      for (int s1 = 0; s1 < 4; ++s1)
+        if (s0 + s1 < nks)
+#pragma unroll
+          for (int i = 0; i < PP; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) sum[i][g] += v[s1][i][g];
+    }
+  }
+  AVC_STAMP(5);
+
+  // gate epilogue, 4 hidden units per (row, blk) pair
+#pragma unroll
+  for (int i = 0; i < PP; ++i) {
+    const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+    const int b = rb * 64 + row;
+    if (b >= B) continue;
+    const int j0 = cb * 16 + blk * 4;
+    const f32x4 zi = sum[i][0] * wiv[i][0] + gxv[i][0];
+    const f32x4 zf = sum[i][1] * wiv[i][1] + gxv[i][1];
+    const f32x4 zg = sum[i][2] * wiv[i][2] + gxv[i][2];
+    const f32x4 zo = sum[i][3] * wiv[i][3] + gxv[i][3];
+    f32x4 cn, hv, ig, fg, gg, og;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      // library tanhf/expf on purpose: hardware exp/rcp forms (~1e-7 absolute) doubled the
+      // end-to-end mel error — the train-mode postnet amplifies it past the 1e-4 bar
+      ig[u] = sigmoidf_(zi[u]);
+      fg[u] = sigmoidf_(zf[u]);
+      gg[u] = tanhf(zg[u]);
+      og[u] = sigmoidf_(zo[u]);
+      cn[u] = fg[u] * cpv[i][u] + ig[u] * gg[u];
+      hv[u] = og[u] * tanhf(cn[u]);
+    }
+    *reinterpret_cast<f32x4*>(S.c_out + (long)b * H + j0) = cn;
+    *reinterpret_cast<f32x4*>(S.h_out + (long)b * S.ldh + j0) = hv;
+    if (S.hs_out) {
+      typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+      f16x4 hi, lo;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        _Float16 h1, l1;
+        split16(hv[u] * kHScale, h1, l1);
+        hi[u] = h1;
+        lo[u] = l1;
+      }
+      _Float16* hs = S.hs_out + (long)b * S.ldhs + (j0 >> 5) * 64 + (j0 & 31);
+      *reinterpret_cast<f16x4*>(hs) = hi;
+      *reinterpret_cast<f16x4*>(hs + 32) = lo;
+    }
+    if (S.gates_out) {
+      float* go = S.gates_out + (long)b * 4 * H + cb * 64 + blk * 16;
+      *reinterpret_cast<f32x4*>(go) = ig;
+      *reinterpret_cast<f32x4*>(go + 4) = fg;
+      *reinterpret_cast<f32x4*>(go + 8) = gg;
+      *reinterpret_cast<f32x4*>(go + 12) = og;
+    }
+  }
+  AVC_STAMP(6);
+}
+
+int g_split_kslice = 0;  // avc_lstm_tune() override (0 = automatic)
+
+// K-slice per workgroup: start at min(K, 1024); halve while the launch has fewer than 128
+// workgroups and each wave keeps >= 2 chunks of 32 (measured: scripts/sweep_split.py; the slab
+// hand-off costs more than the extra per-CU bytes of a longer K range).
+void choose_kslices(int nslots, const int* K, const int* ncb, int nrb, int NW, int* kslice) {
+  for (int L = 0; L < nslots; ++L) kslice[L] = std::min(K[L], 1024);
+  if (g_split_kslice) {
+    for (int L = 0; L < nslots; ++L)
+      kslice[L] = std::max(32 * NW, std::min(K[L], g_split_kslice));
+  } else {
+    for (;;) {
+      long wgs = 0;
+      for (int L = 0; L < nslots; ++L) wgs += (long)ncb[L] * (K[L] / kslice[L]) * nrb;
+      if (wgs >= 128) break;
+      bool changed = false;
+      for (int L = 0; L < nslots; ++L)
+        if (kslice[L] / NW >= 128 && kslice[L] % 2 == 0) { kslice[L] /= 2; changed = true; }
+      if (!changed) break;
+    }
+  }
+  // per-wave range: a power-of-two number of 32-deep chunks (1..8), the same for every slot
+  int kw = 256;
+  for (int L = 0; L < nslots; ++L) kw = std::min(kw, kslice[L] / NW);
+  int p2 = 32;
+  while (p2 * 2 <= kw) p2 *= 2;
+  for (int L = 0; L < nslots; ++L) {
+    kslice[L] = p2 * NW;
+    while (K[L] % kslice[L] != 0) kslice[L] /= 2;  // K % (64 NW) == 0 ends this at >= 32 NW
+  }
+  int m = kslice[0];
+  for (int L = 1; L < nslots; ++L) m = std::min(m, kslice[L]);
+  for (int L = 0; L < nslots; ++L) kslice[L] = m;  // powers of two times 32 NW: m divides every K
+}
+
+int pick_nw(int K) { return K % 128 == 0 ? 4 : 2; }
+
+#ifdef AVC_STAMPS
+void* g_sstamp_buf = nullptr;
+long g_sstamp_target = -1, g_sstamp_count = 0;
+#endif
+
+void launch_split(int NW, dim3 grid, const SplitArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)NW * 64 * kRowPad * sizeof(float) + 16;
+#ifdef AVC_STAMPS
+  const bool rec = g_sstamp_count++ == g_sstamp_target && g_sstamp_buf;
+  if (rec) (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sstamps), &g_sstamp_buf, sizeof(void*), 0, hipMemcpyHostToDevice, s);
+#endif
+  hipEvent_t ev = timing_begin(TC_LSTM_STEP_FWD, s);
+  // every active slot uses the same per-wave K range (choose_kslices keeps kslice/NW equal)
+  const int nch = a.s[a.nblk0 > 0 ? 0 : 1].kslice / NW / 32;
+#define AVC_SPLIT_LAUNCH(NWV)                                                                     \
+  switch (nch) {                                                                                  \
+    case 1: lstm_split_step_kernel<NWV, 1><<<grid, NWV * 64, lds, s>>>(a); break;                 \
+    case 2: lstm_split_step_kernel<NWV, 2><<<grid, NWV * 64, lds, s>>>(a); break;                 \
+    case 4: lstm_split_step_kernel<NWV, 4><<<grid, NWV * 64, lds, s>>>(a); break;                 \
+    default: lstm_split_step_kernel<NWV, 8><<<grid, NWV * 64, lds, s>>>(a); break;                \
+  }
+  if (NW == 4) { AVC_SPLIT_LAUNCH(4) } else { AVC_SPLIT_LAUNCH(2) }
+#undef AVC_SPLIT_LAUNCH
+  if (ev) {
+    double flops = 0.0, bytes = 0.0;
+    const int nslots = a.nblk0 < (int)grid.x ? 2 : 1;
+    for (int L = (a.nblk0 == 0 ? 1 : 0); L < nslots; ++L) {
+      const SplitSlot& S = a.s[L];
+      const double kk = (S.A ? S.K0 : 0) + (S.A1 ? S.K - S.K0 : 0);
+      flops += 2.0 * a.B * kk * 4.0 * a.H;
+      bytes += 4.0 * 4.0 * (double)a.H * S.K;  // split weights: 4 B per element
+    }
+    timing_end(TC_LSTM_STEP_FWD, ev, s, flops, bytes);
+  }
+#ifdef AVC_STAMPS
+  if (rec) {
+    static void* null_ptr = nullptr;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sstamps), &null_ptr, sizeof(void*), 0, hipMemcpyHostToDevice, s);
+    (void)hipStreamSynchronize(s);
+  }
+#endif
+}
+
+inline int ew_blocks(long n) { return (int)std::min<long>((n + 255) / 256, 8192); }
+
+inline size_t al(size_t b) { return (b + 255) & ~size_t(255); }
+
+}  // namespace
+
+bool lstm_split_supported(int H, int din) { return H % 64 == 0 && din % 4 == 0; }
+
+size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
+  const size_t f = sizeof(float);
+  const size_t TB = (size_t)T * B;
+  const int nrb = (B + 63) / 64;
+  size_t s = al(TB * 4 * H * f);                                  // gx
+  s += al((size_t)4 * H * din * f) + 2 * al((size_t)4 * H * f);  // permuted W_ih, biases
+  s += al((size_t)4 * H * H * 2 * 2) + al((size_t)4 * H * f);    // split W_hh + winv
+  if (nlayers == 2) s += al((size_t)4 * H * 2 * H * 2 * 2) + 2 * al((size_t)4 * H * f);
+  s += (size_t)nlayers * (2 * al((size_t)B * H * 2 * 2) + 2 * al((size_t)B * H * f));  // h splits, c
+  // slabs: at most K/128 splits of every 64-column tile, per slot
+  s += (size_t)nlayers * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
+  s += al((size_t)(T + 2) * 2 * nrb * (4 * H / 64) * sizeof(int));
+  GemmDesc d;
+  d.M = (int)TB; d.N = 4 * H; d.Kc = din;
+  return s + gemm_scratch_bytes(d) + 4096;
+}
+
+// One layer (lstm.hip: lstm_forward_impl's contract).  x [T*B][din] (ldx), y [T*B][ldy].
+int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                            const float* x, int ldx, const float* w_ih, const float* w_hh,
+                            const float* b_ih, const float* b_hh, float* y, int ldy,
+                            float* saved_gates, float* saved_c, hipStream_t s) {
+  AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm split path: H must be a multiple of 32, >= 64");
+  Scratch sc(ctx);
+  const long TB = (long)T * B;
+  const int nrb = (B + 63) / 64, ncb = 4 * H / 64;
+  AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
+  AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
+  AVC_TAKE(b_p, float, (size_t)4 * H, sc);
+  AVC_TAKE(whh_s, _Float16, (size_t)4 * H * H * 2, sc);
+  AVC_TAKE(winv, float, (size_t)4 * H, sc);
+  AVC_TAKE(hs, _Float16, (size_t)2 * B * H * 2, sc);
+  float* cpp = nullptr;
+  if (!saved_c) {
+    AVC_TAKE(tmp, float, (size_t)2 * B * H, sc);
+    cpp = tmp;
+  }
+  // W_ih is consumed by the fp32 GEMM in permuted row order: reuse the split kernel's permutation
+  // through a plain gather (lstm.hip's permute_rows_kernel lives in that translation unit).
+  split_rows_kernel<<<4 * H, 256, 0, s>>>(w_hh, H, nullptr, 0, H, 1, whh_s, winv);
+  perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(b_ih, b_hh, b_p, H);
+  AVC_LAUNCH_CHECK();
+  AVC_TRY(permute_rows(w_ih, wih_p, H, din, s));
+  GemmDesc g;
+  g.M = (int)TB; g.N = 4 * H; g.Kc = din;
+  g.A = x; g.lda = ldx; g.a_rows = TB;
+  g.b_trans = 1; g.ldb = din; g.B = wih_p; g.bias0 = b_p;
+  g.C = gx; g.ldc = 4 * H;
+  AVC_TRY(gemm_run(ctx, g, s));
+
+  const int NW = pick_nw(H);
+  int K[1] = {H}, nc[1] = {ncb}, ksl[1];
+  choose_kslices(1, K, nc, nrb, NW, ksl);
+  const int nks = H / ksl[0];
+  float* slab = nullptr;
+  int* cnt = nullptr;
+  if (nks > 1) {
+    AVC_TAKE(sl, float, (size_t)nrb * ncb * nks * 4096, sc);
+    AVC_TAKE(ct, int, (size_t)T * nrb * ncb, sc);
+    AVC_HIP(hipMemsetAsync(ct, 0, sizeof(int) * T * nrb * ncb, s));
+    slab = sl;
+    cnt = ct;
+  }
+  dim3 grid(ncb * nks, nrb);
+  for (int st = 0; st < T; ++st) {
+    const int t = reverse ? T - 1 - st : st;
+    const int tp = reverse ? t + 1 : t - 1;
+    SplitArgs a{};
+    a.B = B; a.H = H; a.nblk0 = (int)grid.x;
+    SplitSlot& S = a.s[0];
+    S.K = H; S.K0 = H; S.kslice = ksl[0]; S.nks = nks; S.ncb = ncb;
+    S.A = st > 0 ? reinterpret_cast<const unsigned char*>(hs + (long)((st - 1) & 1) * B * H * 2) : nullptr;
+    S.lda = 4L * H;
+    S.W = reinterpret_cast<const unsigned char*>(whh_s);
+    S.ldw = 4L * H;
+    S.winv = winv;
+    S.gx = gx + (long)t * B * 4 * H;
+    S.ldgx = 4L * H;
+    if (saved_c) {
+      S.c_prev = st > 0 ? saved_c + (long)tp * B * H : nullptr;
+      S.c_out = saved_c + (long)t * B * H;
+    } else {
+      S.c_prev = st > 0 ? cpp + (long)((st - 1) & 1) * B * H : nullptr;
+      S.c_out = cpp + (long)(st & 1) * B * H;
+    }
+    S.h_out = y + (long)t * B * ldy;
+    S.ldh = ldy;
+    S.hs_out = st < T - 1 ? hs + (long)(st & 1) * B * H * 2 : nullptr;
+    S.ldhs = 2L * H;
+    S.gates_out = saved_gates ? saved_gates + (long)t * B * 4 * H : nullptr;
+    S.slab = slab;
+    S.cnt = cnt ? cnt + (long)st * nrb * ncb : nullptr;
+    launch_split(NW, grid, a, s);
+  }
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+// Two stacked layers as a wavefront (lstm.hip: lstm2_forward_impl's contract): launch st runs
+// layer 0 at t = st and layer 1 at t = st-1; layer 1's input projection is folded into its
+// recurrent product over [h0_t | h1_{t-1}] . [W_ih1 | W_hh1]^T.
+int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                             const float* const* w0, const float* const* w1, float* y0, float* y1,
+                             float* g0, float* c0, float* g1, float* c1, hipStream_t s) {
+  AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm2 split path: H must be a multiple of 32, >= 64");
+  Scratch sc(ctx);
+  const long TB = (long)T * B;
+  const int nrb = (B + 63) / 64, ncb = 4 * H / 64;
+  AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
+  AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
+  AVC_TAKE(b0_p, float, (size_t)4 * H, sc);
+  AVC_TAKE(b1_p, float, (size_t)4 * H, sc);
+  AVC_TAKE(w0_s, _Float16, (size_t)4 * H * H * 2, sc);
+  AVC_TAKE(w1_s, _Float16, (size_t)4 * H * 2 * H * 2, sc);
+  AVC_TAKE(winv0, float, (size_t)4 * H, sc);
+  AVC_TAKE(winv1, float, (size_t)4 * H, sc);
+  AVC_TAKE(hs0, _Float16, (size_t)2 * B * H * 2, sc);
+  AVC_TAKE(hs1, _Float16, (size_t)2 * B * H * 2, sc);
+  split_rows_kernel<<<4 * H, 256, 0, s>>>(w0[1], H, nullptr, 0, H, 1, w0_s, winv0);
+  split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[0], H, w1[1], H, H, 1, w1_s, winv1);
+  perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w0[2], w0[3], b0_p, H);
+  perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w1[2], w1[3], b1_p, H);
+  AVC_LAUNCH_CHECK();
+  AVC_TRY(permute_rows(w0[0], wih_p, H, din, s));
+  GemmDesc g;
+  g.M = (int)TB; g.N = 4 * H; g.Kc = din;
+  g.A = x; g.lda = ldx; g.a_rows = TB;
+  g.b_trans = 1; g.ldb = din; g.B = wih_p; g.bias0 = b0_p;
+  g.C = gx; g.ldc = 4 * H;
+  AVC_TRY(gemm_run(ctx, g, s));
+
+  float* cpp0 = nullptr;
+  float* cpp1 = nullptr;
+  if (!c0) {
+    AVC_TAKE(tmp, float, (size_t)4 * B * H, sc);
+    cpp0 = tmp;
+    cpp1 = tmp + 2L * B * H;
+  }
+  const int NW = pick_nw(H);
+  int K[2] = {H, 2 * H}, nc[2] = {ncb, ncb}, ksl[2];
+  choose_kslices(2, K, nc, nrb, NW, ksl);
+  AVC_CHECK_ARG(H % (ksl[1] / NW) == 0, "lstm2 split path: a wave's K range must not straddle h0|h1");
+  const int nks0 = H / ksl[0], nks1 = 2 * H / ksl[1];
+  AVC_TAKE(slab0, float, (size_t)nrb * ncb * nks0 * 4096, sc);
+  AVC_TAKE(slab1, float, (size_t)nrb * ncb * nks1 * 4096, sc);
+  const long cstride = 2L * nrb * ncb;
+  AVC_TAKE(cnt, int, (size_t)(T + 1) * cstride, sc);
+  AVC_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (T + 1) * cstride, s));
+  const long hsz = (long)B * H * 2;  // halves per split-h buffer
+  auto hs0p = [&](int t) { return reinterpret_cast<const unsigned char*>(hs0 + (long)(t & 1) * hsz); };
+  auto hs1p = [&](int t) { return reinterpret_cast<const unsigned char*>(hs1 + (long)(t & 1) * hsz); };
+
+  for (int st = 0; st <= T; ++st) {
+    const bool l0 = st < T, l1 = st >= 1;
+    const int t0 = st, t1 = st - 1;
+    SplitArgs a{};
+    a.B = B; a.H = H;
+    SplitSlot& S0 = a.s[0];
+    S0.K = H; S0.K0 = H; S0.kslice = ksl[0]; S0.nks = nks0; S0.ncb = ncb;
+    S0.A = (l0 && t0 > 0) ? hs0p(t0 - 1) : nullptr;
+    S0.lda = 4L * H;
+    S0.W = reinterpret_cast<const unsigned char*>(w0_s);
+    S0.ldw = 4L * H;
+    S0.winv = winv0;
+    S0.gx = gx + (long)(l0 ? t0 : 0) * B * 4 * H;
+    S0.ldgx = 4L * H;
+    if (c0) {
+      S0.c_prev = (l0 && t0 > 0) ? c0 + (long)(t0 - 1) * B * H : nullptr;
+      S0.c_out = c0 + (long)(l0 ? t0 : 0) * B * H;
+    } else {
+      S0.c_prev = (l0 && t0 > 0) ? cpp0 + (long)((t0 - 1) & 1) * B * H : nullptr;
+      S0.c_out = cpp0 + (long)(t0 & 1) * B * H;
+    }
+    S0.h_out = y0 + (long)(l0 ? t0 : 0) * B * H;
+    S0.ldh = H;
+    S0.hs_out = l0 ? const_cast<_Float16*>(reinterpret_cast<const _Float16*>(hs0p(t0))) : nullptr;
+    S0.ldhs = 2L * H;
+    S0.gates_out = g0 ? g0 + (long)(l0 ? t0 : 0) * B * 4 * H : nullptr;
+    S0.slab = slab0;
+    S0.cnt = cnt + (long)st * cstride;
+
+    SplitSlot& S1 = a.s[1];
+    S1.K = 2 * H; S1.K0 = H; S1.kslice = ksl[1]; S1.nks = nks1; S1.ncb = ncb;
+    S1.A = l1 ? hs0p(t1) : nullptr;
+    S1.lda = 4L * H;
+    S1.A1 = (l1 && t1 > 0) ? hs1p(t1 - 1) : nullptr;
+    S1.lda1 = 4L * H;
+    S1.W = reinterpret_cast<const unsigned char*>(w1_s);
+    S1.ldw = 8L * H;
+    S1.winv = winv1;
+    S1.gx = b1_p;
+    S1.ldgx = 0;
+    const int tt1 = l1 ? t1 : 0;
+    if (c1) {
+      S1.c_prev = (l1 && t1 > 0) ? c1 + (long)(t1 - 1) * B * H : nullptr;
+      S1.c_out = c1 + (long)tt1 * B * H;
+    } else {
+      S1.c_prev = (l1 && t1 > 0) ? cpp1 + (long)((t1 - 1) & 1) * B * H : nullptr;
+      S1.c_out = cpp1 + (long)(tt1 & 1) * B * H;
+    }
+    S1.h_out = y1 + (long)tt1 * B * H;
+    S1.ldh = H;
+    S1.hs_out = (l1 && t1 < T - 1) ? const_cast<_Float16*>(reinterpret_cast<const _Float16*>(hs1p(t1))) : nullptr;
+    S1.ldhs = 2L * H;
+    S1.gates_out = g1 ? g1 + (long)tt1 * B * 4 * H : nullptr;
+    S1.slab = slab1;
+    S1.cnt = cnt + (long)st * cstride + (long)nrb * ncb;
+
+    const int nb0 = l0 ? ncb * nks0 : 0, nb1 = l1 ? ncb * nks1 : 0;
+    a.nblk0 = nb0;
+    launch_split(NW, dim3(nb0 + nb1, nrb), a, s);
+  }
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+}  // namespace avc
+
+#ifdef AVC_STAMPS
+extern "C" int avc_debug_stamps_split(void* buf, long target_launch) {
+  avc::g_sstamp_buf = buf;
+  avc::g_sstamp_target = target_launch;
+  avc::g_sstamp_count = 0;
+  return AVC_OK;
+}
+#endif
+
+extern "C" int avc_lstm_split_tune(int kslice) {
+  if (kslice < 0 || kslice % 32 != 0) {
+    avc::set_error("avc_lstm_split_tune: kslice must be a non-negative multiple of 32");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_split_kslice = kslice;
+  return AVC_OK;
+}

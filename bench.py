@@ -167,10 +167,15 @@ def main():
             achieved = r["flops"] / (r["ms"] * 1e-3) / 1e12
             result["roofline"] = {
                 "kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_MATRIX_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MATRIX_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MATRIX_TFLOPS, 4),
+                "traffic": None,
                 "avg_launch_us": kern[dom]["avg_us"],
                 "flop_per_launch": round(r["flops"] / r["launches"]),
             }
+            tr = pmc_traffic(dom, args)
+            if tr:
+                result["roofline"]["traffic"] = tr["traffic_bytes"]
+                result["roofline"]["traffic_source"] = tr["source"]
         result["kernels"] = kern
         result["instrumented_ms_per_step"] = round(1000 * inst_elapsed / args.steps, 3)
 
@@ -183,6 +188,24 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def pmc_traffic(cls, args):
+    """HBM bytes per launch of kernel class `cls` (FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)
+    from the newest committed rocprofv3 PMC summary of this same default command
+    (profiles/rNN_pmc_traffic.json, written by scripts/pmc_traffic.py); counters cannot be read
+    from inside the process, so the number is the profiled run's, not this run's."""
+    import glob
+    if args.mode != "fwd" or args.batch not in (None, 64) or args.frames != 128:
+        return None
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        c = json.load(fh)["classes"].get(cls)
+    if not c:
+        return None
+    return {"traffic_bytes": c["traffic_bytes"], "source": os.path.relpath(files[-1], HERE)}
 
 
 def cpu_baseline(args, sd, x_np, gpu_out, B, T, rank):

@@ -186,6 +186,9 @@ int avc_timing_enable(int mask);
 /* Tuning hook for the per-step LSTM kernel: force the batch rows per workgroup (16/32/64) and the
  * number of waves splitting the reduction (1..8); 0 restores the automatic choice. */
 int avc_lstm_tune(int rows_per_block, int waves);
+/* Tuning hook for the split-fp16 forward step (lstm_split.hip): force the K range per workgroup
+ * (a multiple of 32; 0 = automatic). */
+int avc_lstm_split_tune(int kslice);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,
                     long* launches);
