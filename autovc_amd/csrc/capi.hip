@@ -143,6 +143,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   lin.B = P[P_LIN]; lin.b_trans = 1; lin.ldb = 1024;
   lin.bias0 = P[P_LIN + 1];
   lin.C = melf; lin.ldc = 80;
+  lin.prec16 = 1;
   AVC_TRY(gemm_run(ctx, lin, s));
 
   // Postnet + residual (postnet.py:50-63, model.py:131-132)
@@ -260,6 +261,7 @@ int avc_linear_forward(avc_context* ctx, int M, int din, int dout, const float* 
   d.A = x; d.lda = din;
   d.B = weight; d.b_trans = 1; d.ldb = din;
   d.bias0 = bias; d.C = y; d.ldc = dout;
+  d.prec16 = 1;
   AVC_TRY(ensure_arena(ctx, gemm_scratch_bytes(d) + 4096));
   return gemm_run(ctx, d, S(stream));
 }

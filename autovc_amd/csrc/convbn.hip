@@ -49,6 +49,7 @@ GemmDesc conv_fwd_desc(int T, int B, int cin, int cout, const float* x, const fl
   g.A = x; g.lda = cin; g.a_rows = (long)T * B; g.a_shift0 = -2L * B; g.a_tapshift = B;
   g.B = Wt; g.ldb = cout; g.b_rows = cin; g.b_tapoff = (long)cin * cout;
   g.C = y; g.ldc = cout; g.bias0 = bias;
+  g.prec16 = 1;
   return g;
 }
 

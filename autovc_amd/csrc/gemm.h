@@ -24,6 +24,7 @@ struct GemmDesc {
   int nz = 1; long a_zoff = 0; long c_zoff = 0;
   float* C = nullptr; long ldc = 0; long ldc_col = 1; int accumulate = 0;
   const float* bias0 = nullptr; const float* bias1 = nullptr; int act = AVC_ACT_NONE;
+  int prec16 = 0;           // 1: split-fp16 ("3xf16") MFMA kernel; forward operands only (|x| < 65504)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
   int stats_bm = 0;         // filled by gemm_run: rows per stats partial
 };

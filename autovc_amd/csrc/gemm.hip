@@ -273,6 +273,261 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
   }
 }
 
+// ---- split-fp16 ("3xf16") GEMM for forward products ------------------------------------
+//
+// Operands are split while they are staged into LDS: x = hi + lo/2^11 with hi = f16(x) and
+// lo = f16((x - hi) * 2^11) (the pre-scaled low part stays out of the f16 subnormal range for
+// |x| > ~6e-5).  v_mfma_f32_32x32x16_f16 accumulates hi.hi into a per-128-k partial that is
+// Kahan-added into the running sum (the same compensation the fp32 kernel uses), and the two
+// cross terms hi.lo + lo.hi into a separate fp32 accumulator scaled by 2^11.  3 f16 products run
+// 5.3x faster than one fp32 MFMA; the error matches the compensated fp32 kernel.
+// Activations and weights only: |x| must stay below the f16 range (65504) — backward products
+// (tiny gradients) stay on the fp32 kernel.
+//
+// Block: NT = 64*WM*WN threads; each thread stages one octet (8 consecutive k) of A and of B
+// per 32-deep K-tile.  LDS holds MFMA fragment images: [tile32][ksub16][hi|lo][64 lanes][16 B],
+// so every fragment read is one conflict-free ds_read_b128 at lane*16.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split8(const float* v, f16x8& hi, f16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = (_Float16)v[j];
+    hi[j] = h;
+    lo[j] = (_Float16)((v[j] - (float)h) * 2048.0f);
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int BT>
+__global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int tilesM, int tilesN,
+                                                              int kt_per_tap, int kps, int nsplit,
+                                                              float* __restrict__ slab) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(BM * 4 == NT && BN * 4 == NT, "one A octet and one B octet per thread");
+  constexpr int AIMG = (BM / 32) * 2 * 2 * 1024;  // bytes per buffer
+  constexpr int BIMG = (BN / 32) * 2 * 2 * 1024;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * (AIMG + BIMG)];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int nwg = tilesM * tilesN;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+  const int tm = wgid / tilesN, tn = wgid - tm * tilesN;
+  const int z = blockIdx.y % d.nz, split = blockIdx.y / d.nz;
+
+  const int M = d.M, N = d.N, Kc = d.Kc;
+  const float* __restrict__ Ab = d.A + (long)z * d.a_zoff;
+  const float* __restrict__ Bb = d.B;
+  const long lda = d.lda, ldb = d.ldb, a_rows = d.a_rows, b_rows = d.b_rows;
+  const long a_shift0 = d.a_shift0, a_tapshift = d.a_tapshift, b_tapoff = d.b_tapoff;
+  const long bshift = d.b_shift0 + (long)z * d.b_zshift;
+  const int ktotal = d.ntaps * kt_per_tap;
+  const int kt0 = split * kps;
+  const int kt1 = min(ktotal, kt0 + kps);
+
+  // staging coordinates: K-contiguous operand -> (row = t>>2, octet = t&3) (a row's 128 B are
+  // read by 4 neighbouring lanes); MN-contiguous B -> (column = t % BN, octet = t / BN)
+  const int ar = tid >> 2, aoct = tid & 3;
+  const int am = tm * BM + ar;
+  const int bc = BT ? (tid >> 2) : (tid % BN);
+  const int boct = BT ? (tid & 3) : (tid / BN);
+  const int bn_ = tn * BN + bc;
+  // fragment-image slot of this thread's octets (tile, ksub, lane)
+  const int a_slot = ((ar >> 5) * 2 + (aoct >> 1)) * 2048 + ((ar & 31) + 32 * (aoct & 1)) * 16;
+  const int b_slot = ((bc >> 5) * 2 + (boct >> 1)) * 2048 + ((bc & 31) + 32 * (boct & 1)) * 16;
+
+  float va[8], vb[8];
+#define AVC16_LOAD(KT)                                                                           \
+  {                                                                                              \
+    const int tau = (KT) / kt_per_tap;                                                           \
+    const int k0 = ((KT) - tau * kt_per_tap) * BK;                                               \
+    {                                                                                            \
+      const int k = k0 + 8 * aoct;                                                               \
+      const long srow = (long)am + a_shift0 + (long)tau * a_tapshift;                            \
+      const bool rok = am < M && srow >= 0 && srow < a_rows;                                     \
+      const bool ok0 = rok && k < Kc, ok1 = rok && k + 4 < Kc;                                   \
+      const float4 x0 = sel4(ok0, *reinterpret_cast<const float4*>(Ab + (ok0 ? srow * lda + k : 0)));     \
+      const float4 x1 = sel4(ok1, *reinterpret_cast<const float4*>(Ab + (ok1 ? srow * lda + k + 4 : 0))); \
+      va[0] = x0.x; va[1] = x0.y; va[2] = x0.z; va[3] = x0.w;                                    \
+      va[4] = x1.x; va[5] = x1.y; va[6] = x1.z; va[7] = x1.w;                                    \
+    }                                                                                            \
+    if (BT) {                                                                                    \
+      const int k = k0 + 8 * boct;                                                               \
+      const bool ok0 = bn_ < N && k < Kc, ok1 = bn_ < N && k + 4 < Kc;                           \
+      const float* bp = Bb + (long)tau * b_tapoff + (long)bn_ * ldb + k;                         \
+      const float4 x0 = sel4(ok0, *reinterpret_cast<const float4*>(ok0 ? bp : Bb));              \
+      const float4 x1 = sel4(ok1, *reinterpret_cast<const float4*>(ok1 ? bp + 4 : Bb));          \
+      vb[0] = x0.x; vb[1] = x0.y; vb[2] = x0.z; vb[3] = x0.w;                                    \
+      vb[4] = x1.x; vb[5] = x1.y; vb[6] = x1.z; vb[7] = x1.w;                                    \
+    } else {                                                                                     \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                            \
+        const int k = k0 + 8 * boct + j;                                                         \
+        const long srow = (long)k + bshift;                                                      \
+        const bool ok = bn_ < N && k < Kc && srow >= 0 && srow < b_rows;                         \
+        const float x = Bb[ok ? (long)tau * b_tapoff + srow * ldb + bn_ : 0];                    \
+        vb[j] = ok ? x : 0.f;                                                                    \
+      }                                                                                          \
+    }                                                                                            \
+  }
+#define AVC16_STORE(BUF)                                                                         \
+  {                                                                                              \
+    unsigned char* Ai = lds + (BUF) * (AIMG + BIMG);                                             \
+    unsigned char* Bi = Ai + AIMG;                                                               \
+    f16x8 hi, lo;                                                                                \
+    split8(va, hi, lo);                                                                          \
+    *reinterpret_cast<f16x8*>(Ai + a_slot) = hi;                                                 \
+    *reinterpret_cast<f16x8*>(Ai + a_slot + 1024) = lo;                                          \
+    split8(vb, hi, lo);                                                                          \
+    *reinterpret_cast<f16x8*>(Bi + b_slot) = hi;                                                 \
+    *reinterpret_cast<f16x8*>(Bi + b_slot + 1024) = lo;                                          \
+  }
+
+  f32x16 zero16;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) zero16[e] = 0.f;
+  f32x16 acc[TM][TN], cmp[TM][TN], part[TM][TN], crs[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = cmp[i][j] = part[i][j] = crs[i][j] = zero16;
+
+  constexpr int KB = 4;  // K-tiles (128 k) per compensated partial
+  if (kt0 < kt1) AVC16_LOAD(kt0);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    AVC16_STORE(buf);
+    __syncthreads();
+    if (kt + 1 < kt1) AVC16_LOAD(kt + 1);
+    const unsigned char* Ai = lds + buf * (AIMG + BIMG);
+    const unsigned char* Bi = Ai + AIMG;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const unsigned char* p = Ai + ((wm * TM + i) * 2 + s) * 2048 + lane * 16;
+        ah[i] = *reinterpret_cast<const f16x8*>(p);
+        al[i] = *reinterpret_cast<const f16x8*>(p + 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const unsigned char* p = Bi + ((wn * TN + j) * 2 + s) * 2048 + lane * 16;
+        bh[j] = *reinterpret_cast<const f16x8*>(p);
+        bl[j] = *reinterpret_cast<const f16x8*>(p + 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], part[i][j], 0, 0, 0);
+          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], crs[i][j], 0, 0, 0);
+          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], crs[i][j], 0, 0, 0);
+        }
+    }
+    if ((kt - kt0) % KB == KB - 1 || kt + 1 == kt1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float y = part[i][j][e] - cmp[i][j][e];
+            const float t = acc[i][j][e] + y;
+            cmp[i][j][e] = (t - acc[i][j][e]) - y;
+            acc[i][j][e] = t;
+          }
+          part[i][j] = zero16;
+        }
+    }
+  }
+#undef AVC16_LOAD
+#undef AVC16_STORE
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = (acc[i][j][e] - cmp[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
+
+  // ---- epilogue (32x32 C layout: col = lane&31, row = (e&3) + 8(e>>2) + 4(lane>>5)) --------
+  const int row_base = tm * BM + wm * WTM + 4 * (lane >> 5);
+  const int col_base = tn * BN + wn * WTN + (lane & 31);
+  if (nsplit > 1) {
+    float* out = slab + ((long)(split * d.nz + z) * d.M) * d.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col_base + 32 * j;
+        if (col >= d.N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+          if (row < d.M) out[(long)row * d.N + col] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+  float* __restrict__ C = d.C + (long)z * d.c_zoff;
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    csum[j] = 0.f;
+    csq[j] = 0.f;
+    const int col = col_base + 32 * j;
+    const bool colok = col < d.N;
+    float bias = 0.f;
+    if (colok) {
+      if (d.bias0) bias += d.bias0[col];
+      if (d.bias1) bias += d.bias1[col];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+        if (!colok || row >= d.M) continue;
+        const float v = act_apply(acc[i][j][e] + bias, d.act);
+        float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
+        if (d.accumulate) *p += v; else *p = v;
+        csum[j] += v;
+        csq[j] += v * v;
+      }
+  }
+  if (d.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float s = csum[j] + __shfl_xor(csum[j], 32);
+      const float s2 = csq[j] + __shfl_xor(csq[j], 32);
+      if (lane < 32) {
+        const int cl = wn * WTN + 32 * j + lane;
+        red[(wm * 2 + 0) * BN + cl] = s;
+        red[(wm * 2 + 1) * BN + cl] = s2;
+      }
+    }
+    __syncthreads();
+    for (int cl = tid; cl < BN; cl += NT) {
+      const int col = tn * BN + cl;
+      if (col < d.N) {
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int r = 0; r < WM; ++r) {
+          s += red[(r * 2 + 0) * BN + cl];
+          s2 += red[(r * 2 + 1) * BN + cl];
+        }
+        d.stats[((long)tm * 2 + 0) * d.N + col] = s;
+        d.stats[((long)tm * 2 + 1) * d.N + col] = s2;
+      }
+    }
+  }
+}
+
 __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __restrict__ slab) {
   const long total = (long)d.nz * d.M * d.N;
   const long MN = (long)d.M * d.N;
@@ -290,6 +545,8 @@ __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __rest
     if (d.accumulate) *p += s; else *p = s;
   }
 }
+
+int g_gemm16 = 1;  // avc_gemm_tune(): 0 routes prec16 products to the fp32 kernel (A/B runs)
 
 struct Plan {
   int bm, bn, tilesM, tilesN, kt_per_tap, ktotal, nsplit, kps;
@@ -318,6 +575,16 @@ Plan make_plan(const GemmDesc& d, int force_split) {
   p.nsplit = (p.ktotal + p.kps - 1) / p.kps;
   if (p.nsplit < 1) p.nsplit = 1;
   return p;
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch16(const GemmDesc& d, const Plan& p, float* slab, hipStream_t s) {
+  dim3 grid(p.tilesM * p.tilesN, d.nz * p.nsplit);
+  constexpr int NT = 64 * WM * WN;
+  if (d.b_trans)
+    gemm16_kernel<BM, BN, WM, WN, 1><<<grid, NT, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
+  else
+    gemm16_kernel<BM, BN, WM, WN, 0><<<grid, NT, 0, s>>>(d, p.tilesM, p.tilesN, p.kt_per_tap, p.kps, p.nsplit, slab);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -372,8 +639,14 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     if (!slab) return AVC_ERR_WORKSPACE;
   }
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
-  if (p.bm == 128) launch<128, 128, 2, 4>(d, p, slab, stream);
-  else launch<64, 64, 2, 2>(d, p, slab, stream);
+  if (d.prec16 && !d.a_trans && g_gemm16) {
+    if (p.bm == 128) launch16<128, 128, 4, 2>(d, p, slab, stream);
+    else launch16<64, 64, 2, 2>(d, p, slab, stream);
+  } else if (p.bm == 128) {
+    launch<128, 128, 2, 4>(d, p, slab, stream);
+  } else {
+    launch<64, 64, 2, 2>(d, p, slab, stream);
+  }
   AVC_LAUNCH_CHECK();
   if (ev) {
     const double flops = 2.0 * d.M * d.N * (double)d.Kc * d.ntaps * d.nz;
@@ -390,3 +663,8 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
 }
 
 }  // namespace avc
+
+extern "C" int avc_gemm_tune(int prec16) {
+  avc::g_gemm16 = prec16 ? 1 : 0;
+  return AVC_OK;
+}

@@ -587,6 +587,7 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
   g.A = x; g.lda = ldx; g.a_rows = TB;
   g.b_trans = 1; g.ldb = din;
   g.C = gx; g.ldc = 4 * H;
+  g.prec16 = 1;
 
   if (H == 32) {
     g.B = w_ih; g.bias0 = b_ih; g.bias1 = b_hh;
@@ -688,6 +689,7 @@ int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const flo
   g.A = x; g.lda = ldx; g.a_rows = TB;
   g.b_trans = 1; g.ldb = din; g.B = wih_p; g.bias0 = bih_p; g.bias1 = bhh_p;
   g.C = gx; g.ldc = 4 * H;
+  g.prec16 = 1;
   AVC_TRY(gemm_run(ctx, g, s));
 
   float* cpp0 = nullptr;

@@ -502,6 +502,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   g.A = x; g.lda = ldx; g.a_rows = TB;
   g.b_trans = 1; g.ldb = din; g.B = wih_p; g.bias0 = b_p;
   g.C = gx; g.ldc = 4 * H;
+  g.prec16 = 1;
   AVC_TRY(gemm_run(ctx, g, s));
 
   const int NW = pick_nw(H);
@@ -583,6 +584,7 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   g.A = x; g.lda = ldx; g.a_rows = TB;
   g.b_trans = 1; g.ldb = din; g.B = wih_p; g.bias0 = b0_p;
   g.C = gx; g.ldc = 4 * H;
+  g.prec16 = 1;
   AVC_TRY(gemm_run(ctx, g, s));
 
   float* cpp0 = nullptr;

@@ -189,6 +189,9 @@ int avc_lstm_tune(int rows_per_block, int waves);
 /* Tuning hook for the split-fp16 forward step (lstm_split.hip): force the K range per workgroup
  * (a multiple of 32; 0 = automatic). */
 int avc_lstm_split_tune(int kslice);
+/* Tuning hook for forward products: 0 runs them on the fp32 MFMA kernel instead of the
+ * split-fp16 one (default 1). */
+int avc_gemm_tune(int prec16);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,
                     long* launches);
