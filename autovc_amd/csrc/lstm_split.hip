@@ -130,13 +130,17 @@ struct SplitArgs {
   SplitSlot s[2];
 };
 
-constexpr int kRowPad = 68;  // LDS row stride (floats): conflict-free partial writes
-
-template <int NW, int NCH>
+// NC = 16-column gate blocks (4 hidden units x 4 gates) per workgroup tile: 4 for the wide
+// split-K tiles of decoder.lstm2, 1 for the narrow full-K tiles of lstm1 (no slab hand-off).
+template <int NW, int NCH, int NC>
 __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a) {
-  extern __shared__ float part[];  // [NW][64][kRowPad] + flag
+  constexpr int TW = 16 * NC;      // tile width (gate rows)
+  constexpr int RP = TW + 4;       // LDS row stride (floats): conflict-free partial writes
+  constexpr int TSZ = 64 * TW;     // floats per tile partial
+  extern __shared__ float part[];  // [NW][64][RP] + flag
   constexpr int NT = NW * 64;
-  constexpr int PP = 256 / NT;  // (row, 16-column block) pairs per thread in the epilogue
+  constexpr int NPAIR = 64 * NC;   // (row, 16-column block) pairs of the tile
+  constexpr int PP = (NPAIR + NT - 1) / NT;  // pairs per thread in the epilogue
   // wave index through readfirstlane: the buffer descriptors below must be provably uniform, or
   // hipcc wraps every buffer load in a waterfall loop
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -151,11 +155,11 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   const int nrows = min(64, B - rb * 64);
   AVC_STAMP(0);
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][NC];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NC; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   constexpr int kw = NCH * 32;  // == S.kslice / NW (host-checked)
   const int k0 = ks * S.kslice + w * kw;
@@ -170,31 +174,45 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
         const_cast<unsigned char*>(src) + (long)rb * 64 * lds_ + (long)kc0 * 128, 0,
         (int)(nrows * lds_ - (long)kc0 * 128), 0x00020000);
     const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<unsigned char*>(S.W) + (long)cb * 64 * S.ldw + (long)(k0 >> 5) * 128, 0,
-        (int)(64 * S.ldw - (long)(k0 >> 5) * 128), 0x00020000);
+        const_cast<unsigned char*>(S.W) + (long)cb * TW * S.ldw + (long)(k0 >> 5) * 128, 0,
+        (int)(TW * S.ldw - (long)(k0 >> 5) * 128), 0x00020000);
     const int hvo = l15 * (int)lds_ + lq * 16;
     const int wvo = l15 * (int)S.ldw + lq * 16;
     const int hrow16 = 16 * (int)lds_, wrow16 = 16 * (int)S.ldw;
 
-    f16x8 hA[4][2], wA[4][2], hB[4][2], wB[4][2];
+    f16x8 hA[4][2], wA[NC][2], hB[4][2], wB[NC][2];
 #define AVC_LD(RS, VO, SO) __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(RS, VO, SO, 0))
 #define AVC_LOAD(HV, WV, C)                                                                       \
   _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                                 \
     HV[r][0] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 128);                                          \
     HV[r][1] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 128 + 64);                                     \
   }                                                                                               \
-  _Pragma("unroll") for (int n = 0; n < 4; ++n) {                                                 \
+  _Pragma("unroll") for (int n = 0; n < NC; ++n) {                                                \
     WV[n][0] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 128);                                          \
     WV[n][1] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 128 + 64);                                     \
   }
 #define AVC_MFMA(HV, WV)                                                                          \
   _Pragma("unroll") for (int r = 0; r < 4; ++r)                                                   \
-    _Pragma("unroll") for (int n = 0; n < 4; ++n) {                                               \
+    _Pragma("unroll") for (int n = 0; n < NC; ++n) {                                              \
       acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][1], WV[n][0], acc[r][n], 0, 0, 0); \
       acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], WV[n][1], acc[r][n], 0, 0, 0); \
       acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], WV[n][0], acc[r][n], 0, 0, 0); \
     }
 #define AVC_PIN __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NC == 1 && NCH <= 4) {
+      // narrow tile: every chunk of the wave's K range in flight at once (40 VGPRs per chunk),
+      // consumed in issue order under counted waits
+      f16x8 hC[NCH][4][2], wC[NCH][NC][2];
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) { AVC_LOAD(hC[c], wC[c], c) }
+#ifdef AVC_STAMPS
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      AVC_STAMP(1);
+#endif
+      AVC_PIN
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) { AVC_MFMA(hC[c], wC[c]) }
+    } else {
     // register double buffer, program order pinned (see lstm.hip: the scheduler otherwise sinks
     // the next chunk's loads under the current MFMAs and the waitcnt pass drains to zero)
     AVC_LOAD(hA, wA, 0)
@@ -213,6 +231,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
       if (c & 1) { AVC_MFMA(hB, wB) } else { AVC_MFMA(hA, wA) }
       AVC_PIN
     }
+    }
 #undef AVC_PIN
 #undef AVC_MFMA
 #undef AVC_LOAD
@@ -220,45 +239,101 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   }
   AVC_STAMP(2);
 
+  // Narrow tiles (NC = 1, 4 waves): 64 rows x 4 hidden units = 256 cells, one per thread, summed
+  // straight from the wave partials (the host never splits K for them).
+  if constexpr (NC == 1 && NW == 4) {
+    const int row = tid >> 2, u = tid & 3;
+    const int b = rb * 64 + row;
+    const int bc = min(b, B - 1);
+    const int p0 = cb * 16 + u;
+    const float* gxr = S.gx + (long)bc * S.ldgx + p0;
+    float gxs[4], wis[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      gxs[g] = gxr[4 * g];
+      wis[g] = S.winv[p0 + 4 * g];
+    }
+    const int j = cb * 4 + u;
+    const float cp = S.c_prev ? S.c_prev[(long)bc * H + j] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) part[w * 64 * RP + (r * 16 + 4 * lq + e) * RP + l15] = acc[r][0][e];
+    __syncthreads();
+    AVC_STAMP(3);
+    float z[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float v = part[row * RP + 4 * g + u];
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) v += part[ww * 64 * RP + row * RP + 4 * g + u];
+      z[g] = v * wis[g] + gxs[g];
+    }
+    AVC_STAMP(5);
+    if (b < B) {
+      const float ig = sigmoidf_(z[0]), fg = sigmoidf_(z[1]), gg = tanhf(z[2]), og = sigmoidf_(z[3]);
+      const float cn = fg * cp + ig * gg;
+      const float hv = og * tanhf(cn);
+      S.c_out[(long)b * H + j] = cn;
+      S.h_out[(long)b * S.ldh + j] = hv;
+      if (S.hs_out) {
+        _Float16 hi, lo;
+        split16(hv * kHScale, hi, lo);
+        _Float16* hs = S.hs_out + (long)b * S.ldhs + (j >> 5) * 64 + (j & 31);
+        hs[0] = hi;
+        hs[32] = lo;
+      }
+      if (S.gates_out) {
+        float* go = S.gates_out + (long)b * 4 * H + p0;
+        go[0] = ig;
+        go[4] = fg;
+        go[8] = gg;
+        go[12] = og;
+      }
+    }
+    AVC_STAMP(6);
+    return;
+  }
+
   // Epilogue ownership: thread t handles (row, blk) pairs t + NT*i; a pair's 4 float4 columns
   // blk*16 + 4g (gate g, units 0..3) hold all four gates of 4 hidden units.  Its operands are
   // fetched now so that their latency overlaps the reduction below.
   f32x4 gxv[PP][4], wiv[PP][4], cpv[PP];
 #pragma unroll
   for (int i = 0; i < PP; ++i) {
-    const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+    const int pr = min(tid + NT * i, NPAIR - 1), row = pr / NC, blk = pr % NC;
     const int b = min(rb * 64 + row, B - 1);
-    const int p0 = cb * 64 + blk * 16;
+    const int p0 = cb * TW + blk * 16;
     const float* gxr = S.gx + (long)b * S.ldgx + p0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       gxv[i][g] = *reinterpret_cast<const f32x4*>(gxr + 4 * g);
       wiv[i][g] = *reinterpret_cast<const f32x4*>(S.winv + p0 + 4 * g);
     }
-    cpv[i] = S.c_prev ? *reinterpret_cast<const f32x4*>(S.c_prev + (long)b * H + cb * 16 + blk * 4)
+    cpv[i] = S.c_prev ? *reinterpret_cast<const f32x4*>(S.c_prev + (long)b * H + cb * 4 * NC + blk * 4)
                       : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
   // wave partials -> LDS; C layout of 16x16: column lane&15, rows 4(lane>>4) + e
-  float* mine = part + w * 64 * kRowPad;
+  float* mine = part + w * 64 * RP;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NC; ++n)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * kRowPad + n * 16 + l15] = acc[r][n][e];
+      for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e];
   __syncthreads();
 
   f32x4 sum[PP][4];
 #pragma unroll
   for (int i = 0; i < PP; ++i) {
-    const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+    const int pr = min(tid + NT * i, NPAIR - 1), row = pr / NC, blk = pr % NC;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const int off = row * kRowPad + blk * 16 + 4 * g;
+      const int off = row * RP + blk * 16 + 4 * g;
       f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
 #pragma unroll
-      for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * 64 * kRowPad + off);
+      for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * 64 * RP + off);
       sum[i][g] = v;
     }
   }
@@ -266,21 +341,22 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
 
   if (nks > 1) {
     // publish this workgroup's slab (write-through), take a ticket; the last one reduces.
-    // Slab element (row, col) of split s at s*4096 + row*64 + col.
+    // Slab element (row, col) of split s at s*TSZ + row*TW + col.
     const long tile = (long)rb * S.ncb + cb;
-    float* slab0 = S.slab + tile * nks * 4096;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(slab0, 0, nks * 4096 * 4, 0x00020000);
+    float* slab0 = S.slab + tile * nks * TSZ;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(slab0, 0, nks * TSZ * 4, 0x00020000);
 #pragma unroll
     for (int i = 0; i < PP; ++i) {
-      const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+      const int pr = tid + NT * i, row = pr / NC, blk = pr % NC;
+      if (pr >= NPAIR) continue;
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, sum[i][g]), rsrc,
-                                               (ks * 4096 + row * 64 + blk * 16 + 4 * g) * 4, 0, 16 /*sc1*/);
+                                               (ks * TSZ + row * TW + blk * 16 + 4 * g) * 4, 0, 16 /*sc1*/);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int* flag = reinterpret_cast<int*>(part + NW * 64 * kRowPad);
+    int* flag = reinterpret_cast<int*>(part + NW * 64 * RP);
     if (tid == 0) {
       const int old = __hip_atomic_fetch_add(S.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = old;
@@ -299,11 +375,11 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
       for (int s1 = 0; s1 < 4; ++s1)
 #pragma unroll
         for (int i = 0; i < PP; ++i) {
-          const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+          const int pr = min(tid + NT * i, NPAIR - 1), row = pr / NC, blk = pr % NC;
 #pragma unroll
           for (int g = 0; g < 4; ++g)
             v[s1][i][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                rsrc, ((s0 + s1) * 4096 + row * 64 + blk * 16 + 4 * g) * 4, 0, 16 /*sc1*/));
+                rsrc, ((s0 + s1) * TSZ + row * TW + blk * 16 + 4 * g) * 4, 0, 16 /*sc1*/));
         }
 #pragma unroll
       for (int s1 = 0; s1 < 4; ++s1)
@@ -319,10 +395,10 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   // gate epilogue, 4 hidden units per (row, blk) pair
 #pragma unroll
   for (int i = 0; i < PP; ++i) {
-    const int pr = tid + NT * i, row = pr >> 2, blk = pr & 3;
+    const int pr = tid + NT * i, row = pr / NC, blk = pr % NC;
     const int b = rb * 64 + row;
-    if (b >= B) continue;
-    const int j0 = cb * 16 + blk * 4;
+    if (pr >= NPAIR || b >= B) continue;
+    const int j0 = cb * 4 * NC + blk * 4;
     const f32x4 zi = sum[i][0] * wiv[i][0] + gxv[i][0];
     const f32x4 zf = sum[i][1] * wiv[i][1] + gxv[i][1];
     const f32x4 zg = sum[i][2] * wiv[i][2] + gxv[i][2];
@@ -356,7 +432,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
       *reinterpret_cast<f16x4*>(hs + 32) = lo;
     }
     if (S.gates_out) {
-      float* go = S.gates_out + (long)b * 4 * H + cb * 64 + blk * 16;
+      float* go = S.gates_out + (long)b * 4 * H + cb * TW + blk * 16;
       *reinterpret_cast<f32x4*>(go) = ig;
       *reinterpret_cast<f32x4*>(go + 4) = fg;
       *reinterpret_cast<f32x4*>(go + 8) = gg;
@@ -366,7 +442,8 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   AVC_STAMP(6);
 }
 
-int g_split_kslice = 0;  // avc_lstm_tune() override (0 = automatic)
+int g_split_kslice = 0;  // avc_lstm_split_tune() overrides (0 = automatic)
+int g_split_nc = 0;
 
 // K-slice per workgroup: start at min(K, 1024); halve while the launch has fewer than 128
 // workgroups and each wave keeps >= 2 chunks of 32 (measured: scripts/sweep_split.py; the slab
@@ -408,8 +485,8 @@ void* g_sstamp_buf = nullptr;
 long g_sstamp_target = -1, g_sstamp_count = 0;
 #endif
 
-void launch_split(int NW, dim3 grid, const SplitArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)NW * 64 * kRowPad * sizeof(float) + 16;
+void launch_split(int NW, int NC, dim3 grid, const SplitArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)NW * 64 * (16 * NC + 4) * sizeof(float) + 16;
 #ifdef AVC_STAMPS
   const bool rec = g_sstamp_count++ == g_sstamp_target && g_sstamp_buf;
   if (rec) (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sstamps), &g_sstamp_buf, sizeof(void*), 0, hipMemcpyHostToDevice, s);
@@ -417,14 +494,18 @@ void launch_split(int NW, dim3 grid, const SplitArgs& a, hipStream_t s) {
   hipEvent_t ev = timing_begin(TC_LSTM_STEP_FWD, s);
   // every active slot uses the same per-wave K range (choose_kslices keeps kslice/NW equal)
   const int nch = a.s[a.nblk0 > 0 ? 0 : 1].kslice / NW / 32;
-#define AVC_SPLIT_LAUNCH(NWV)                                                                     \
+#define AVC_SPLIT_LAUNCH(NWV, NCV)                                                                \
   switch (nch) {                                                                                  \
-    case 1: lstm_split_step_kernel<NWV, 1><<<grid, NWV * 64, lds, s>>>(a); break;                 \
-    case 2: lstm_split_step_kernel<NWV, 2><<<grid, NWV * 64, lds, s>>>(a); break;                 \
-    case 4: lstm_split_step_kernel<NWV, 4><<<grid, NWV * 64, lds, s>>>(a); break;                 \
-    default: lstm_split_step_kernel<NWV, 8><<<grid, NWV * 64, lds, s>>>(a); break;                \
+    case 1: lstm_split_step_kernel<NWV, 1, NCV><<<grid, NWV * 64, lds, s>>>(a); break;            \
+    case 2: lstm_split_step_kernel<NWV, 2, NCV><<<grid, NWV * 64, lds, s>>>(a); break;            \
+    case 4: lstm_split_step_kernel<NWV, 4, NCV><<<grid, NWV * 64, lds, s>>>(a); break;            \
+    default: lstm_split_step_kernel<NWV, 8, NCV><<<grid, NWV * 64, lds, s>>>(a); break;           \
   }
-  if (NW == 4) { AVC_SPLIT_LAUNCH(4) } else { AVC_SPLIT_LAUNCH(2) }
+  if (NW == 4) {
+    if (NC == 4) { AVC_SPLIT_LAUNCH(4, 4) } else { AVC_SPLIT_LAUNCH(4, 1) }
+  } else {
+    if (NC == 4) { AVC_SPLIT_LAUNCH(2, 4) } else { AVC_SPLIT_LAUNCH(2, 1) }
+  }
 #undef AVC_SPLIT_LAUNCH
   if (ev) {
     double flops = 0.0, bytes = 0.0;
@@ -479,7 +560,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm split path: H must be a multiple of 32, >= 64");
   Scratch sc(ctx);
   const long TB = (long)T * B;
-  const int nrb = (B + 63) / 64, ncb = 4 * H / 64;
+  const int nrb = (B + 63) / 64;
   AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
   AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
   AVC_TAKE(b_p, float, (size_t)4 * H, sc);
@@ -506,13 +587,23 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   AVC_TRY(gemm_run(ctx, g, s));
 
   const int NW = pick_nw(H);
+  // narrow full-K tiles when they alone fill the chip (no slab hand-off: one memory round trip
+  // less per step); otherwise 64-column tiles with the K range split over workgroups
+  int NC = (4 * H / 16) * nrb >= 96 && H <= 512 ? 1 : 4;
+  if (g_split_nc) NC = g_split_nc;
+  const int ncb = 4 * H / (16 * NC);
   int K[1] = {H}, nc[1] = {ncb}, ksl[1];
-  choose_kslices(1, K, nc, nrb, NW, ksl);
+  if (NC == 1) {  // narrow tiles reduce the whole K range in one workgroup
+    ksl[0] = H;
+    while ((ksl[0] / NW) > 256 || (ksl[0] / NW) % 32 != 0 || ((ksl[0] / NW / 32) & (ksl[0] / NW / 32 - 1))) ksl[0] /= 2;
+  } else {
+    choose_kslices(1, K, nc, nrb, NW, ksl);
+  }
   const int nks = H / ksl[0];
   float* slab = nullptr;
   int* cnt = nullptr;
   if (nks > 1) {
-    AVC_TAKE(sl, float, (size_t)nrb * ncb * nks * 4096, sc);
+    AVC_TAKE(sl, float, (size_t)nrb * ncb * nks * 1024 * NC, sc);
     AVC_TAKE(ct, int, (size_t)T * nrb * ncb, sc);
     AVC_HIP(hipMemsetAsync(ct, 0, sizeof(int) * T * nrb * ncb, s));
     slab = sl;
@@ -547,7 +638,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
     S.gates_out = saved_gates ? saved_gates + (long)t * B * 4 * H : nullptr;
     S.slab = slab;
     S.cnt = cnt ? cnt + (long)st * nrb * ncb : nullptr;
-    launch_split(NW, grid, a, s);
+    launch_split(NW, NC, grid, a, s);
   }
   AVC_LAUNCH_CHECK();
   return AVC_OK;
@@ -562,7 +653,8 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm2 split path: H must be a multiple of 32, >= 64");
   Scratch sc(ctx);
   const long TB = (long)T * B;
-  const int nrb = (B + 63) / 64, ncb = 4 * H / 64;
+  const int NC = 4;  // the pair always splits K (narrow tiles would re-read h 4x more)
+  const int nrb = (B + 63) / 64, ncb = 4 * H / (16 * NC);
   AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
   AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
   AVC_TAKE(b0_p, float, (size_t)4 * H, sc);
@@ -599,8 +691,8 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   choose_kslices(2, K, nc, nrb, NW, ksl);
   AVC_CHECK_ARG(H % (ksl[1] / NW) == 0, "lstm2 split path: a wave's K range must not straddle h0|h1");
   const int nks0 = H / ksl[0], nks1 = 2 * H / ksl[1];
-  AVC_TAKE(slab0, float, (size_t)nrb * ncb * nks0 * 4096, sc);
-  AVC_TAKE(slab1, float, (size_t)nrb * ncb * nks1 * 4096, sc);
+  AVC_TAKE(slab0, float, (size_t)nrb * ncb * nks0 * 1024 * NC, sc);
+  AVC_TAKE(slab1, float, (size_t)nrb * ncb * nks1 * 1024 * NC, sc);
   const long cstride = 2L * nrb * ncb;
   AVC_TAKE(cnt, int, (size_t)(T + 1) * cstride, sc);
   AVC_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (T + 1) * cstride, s));
@@ -666,7 +758,7 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
 
     const int nb0 = l0 ? ncb * nks0 : 0, nb1 = l1 ? ncb * nks1 : 0;
     a.nblk0 = nb0;
-    launch_split(NW, dim3(nb0 + nb1, nrb), a, s);
+    launch_split(NW, NC, dim3(nb0 + nb1, nrb), a, s);
   }
   AVC_LAUNCH_CHECK();
   return AVC_OK;
@@ -683,11 +775,16 @@ extern "C" int avc_debug_stamps_split(void* buf, long target_launch) {
 }
 #endif
 
-extern "C" int avc_lstm_split_tune(int kslice) {
+extern "C" int avc_lstm_split_tune(int kslice, int col_blocks) {
   if (kslice < 0 || kslice % 32 != 0) {
     avc::set_error("avc_lstm_split_tune: kslice must be a non-negative multiple of 32");
     return AVC_ERR_INVALID;
   }
+  if (!(col_blocks == 0 || col_blocks == 1 || col_blocks == 4)) {
+    avc::set_error("avc_lstm_split_tune: col_blocks must be 0, 1 or 4");
+    return AVC_ERR_INVALID;
+  }
   avc::g_split_kslice = kslice;
+  avc::g_split_nc = col_blocks;
   return AVC_OK;
 }

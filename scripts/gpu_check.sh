@@ -27,7 +27,7 @@ for step in "$@"; do
     pmcw)  run pmcw 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcW -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
     sweep) run sweep 600 python scripts/sweep_lstm.py ;;
     ssplit) run ssplit 400 python scripts/sweep_split.py ;;
-    sstamps) run sstamps 300 python scripts/stamps_split.py 0 256 1024 ;;
+    sstamps) run sstamps 300 python scripts/stamps_split.py 0:0 0:4 ;;
     probe) run probe 200 python scripts/probe_cache.py ;;
     stamps) run stamps 300 python scripts/stamps_lstm.py ;;
     benchtrain) run benchtrain 400 python bench.py --mode train --steps 5 --warmup 2 --no-cpu ;;

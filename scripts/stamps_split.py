@@ -30,8 +30,9 @@ with torch.no_grad():
 torch.cuda.synchronize()
 buf = torch.zeros(65536 * 8, dtype=torch.int64, device=dev)
 names = ["first chunk", "mfma loop", "lds reduce", "slab+ticket", "slab reduce", "epilogue"]
-for ks in [int(a) for a in sys.argv[1:]] or [0]:
-    _lib.call("avc_lstm_split_tune", ks)
+for arg in sys.argv[1:] or ["0:0"]:
+    ks, nc = (int(v) for v in arg.split(":"))
+    _lib.call("avc_lstm_split_tune", ks, nc)
     for name, idx in [("lstm1 H=512 step 64", 64), ("lstm2 pair step 64", 128 + 64)]:
         buf.zero_()
         lib.avc_debug_stamps_split(ctypes.c_void_p(buf.data_ptr()), idx)
@@ -45,7 +46,7 @@ for ks in [int(a) for a in sys.argv[1:]] or [0]:
             continue
         t0 = st[:, 0].min()
         end = np.where(st[:, 6] > 0, st[:, 6], st[:, 4])
-        print(f"kslice={ks} {name}: waves {len(st)}  span {end.max() - t0} ticks; "
+        print(f"kslice={ks} nc={nc} {name}: waves {len(st)}  span {end.max() - t0} ticks; "
               f"reducer waves {(st[:, 6] > 0).sum()}")
         for i, ph in enumerate(names):
             a, b = st[:, i], st[:, i + 1]
@@ -59,4 +60,4 @@ for ks in [int(a) for a in sys.argv[1:]] or [0]:
             if len(v):
                 print(f"   {ph:14s} median {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}  max {v.max():8.0f}  n {len(v)}")
         print(f"   wave start offset median {np.median(st[:, 0] - t0):8.0f}  max {(st[:, 0] - t0).max():8.0f}")
-_lib.call("avc_lstm_split_tune", 0)
+_lib.call("avc_lstm_split_tune", 0, 0)
