@@ -35,6 +35,7 @@ _SIGS = {
     "avc_conv_bn_act_backward": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P,
                                  _P, _P, _P, _P, _I, _P],
     "avc_lstm_forward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P],
+    "avc_bilstm_forward": [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P],
     "avc_lstm_backward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P,
                           _P, _P, _P, _I, _I, _P],
     "avc_linear_forward": [_P, _I, _I, _I, _P, _P, _P, _P, _P],

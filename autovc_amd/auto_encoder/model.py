@@ -191,9 +191,8 @@ class AutoEncoder(nn.Module):
         _lib.call("avc_generator_forward", _lib.context(x.device), T, B, params, _lib.ptr(x),
                   _lib.ptr(c_org), _lib.ptr(c_trg), int(training), _lib.ptr(mel), _lib.ptr(mel_post),
                   _lib.ptr(codes), _lib.stream(x.device))
-        if training:
-            for b in self._bns():
-                b.num_batches_tracked.add_(1)
+        if training:  # one fused launch for the 11 counters
+            torch._foreach_add_([b.num_batches_tracked for b in self._bns()], 1)
         return mel, mel_post, codes
 
     @staticmethod

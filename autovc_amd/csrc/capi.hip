@@ -69,7 +69,7 @@ size_t gen_scratch(int T, int B) {
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 336, 512));
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 512, 512));
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 80, 512));
-  nested = std::max(nested, lstm_forward_scratch(T, B, 512, 32, false));
+  nested = std::max(nested, bilstm_forward_scratch(T, B, 512, 32, false));
   nested = std::max(nested, lstm_forward_scratch(T, B, 320, 512, false));
   nested = std::max(nested, lstm_forward_scratch(T, B, 512, 1024, false));
   nested = std::max(nested, lstm2_forward_scratch(T, B, 512, 1024, false));
@@ -115,14 +115,10 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TRY(cba(P_ENC_CONV + 6, 512, 512, ba, bb, AVC_ACT_RELU, nullptr));
   AVC_TRY(cba(P_ENC_CONV + 12, 512, 512, bb, ba, AVC_ACT_RELU, nullptr));
   const int EL = P_ENC_LSTM;
-  AVC_TRY(lstm_forward_impl(ctx, T, B, 512, 32, 0, ba, 512, P[EL], P[EL + 1], P[EL + 2], P[EL + 3],
-                            e1, 64, nullptr, nullptr, s));
-  AVC_TRY(lstm_forward_impl(ctx, T, B, 512, 32, 1, ba, 512, P[EL + 4], P[EL + 5], P[EL + 6],
-                            P[EL + 7], e1 + 32, 64, nullptr, nullptr, s));
-  AVC_TRY(lstm_forward_impl(ctx, T, B, 64, 32, 0, e1, 64, P[EL + 8], P[EL + 9], P[EL + 10],
-                            P[EL + 11], e2, 64, nullptr, nullptr, s));
-  AVC_TRY(lstm_forward_impl(ctx, T, B, 64, 32, 1, e1, 64, P[EL + 12], P[EL + 13], P[EL + 14],
-                            P[EL + 15], e2 + 32, 64, nullptr, nullptr, s));
+  AVC_TRY(bilstm_forward_impl(ctx, T, B, 512, 32, ba, 512, P + EL, P + EL + 4, e1, 64, nullptr, nullptr,
+                              nullptr, nullptr, s));
+  AVC_TRY(bilstm_forward_impl(ctx, T, B, 64, 32, e1, 64, P + EL + 8, P + EL + 12, e2, 64, nullptr, nullptr,
+                              nullptr, nullptr, s));
   AVC_TRY(codes_from_encoder(T, B, e2, codes, s));
 
   // Upsample + decoder (model.py:115-127, decoder.py:58-79)
@@ -239,6 +235,21 @@ int avc_lstm_forward(avc_context* ctx, int T, int B, int din, int H, int reverse
   AVC_TRY(ensure_arena(ctx, lstm_forward_scratch(T, B, din, H, saved_c != nullptr)));
   return lstm_forward_impl(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, b_ih, b_hh, y, ldy,
                            saved_gates, saved_c, S(stream));
+}
+
+int avc_bilstm_forward(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                       const float* const* w_f, const float* const* w_r, float* y, int ldy,
+                       float* saved_gates_f, float* saved_c_f, float* saved_gates_r,
+                       float* saved_c_r, void* stream) {
+  AVC_CHECK_ARG(ctx && x && w_f && w_r && y, "NULL pointer");
+  for (int i = 0; i < 4; ++i) AVC_CHECK_ARG(w_f[i] && w_r[i], "NULL weight pointer");
+  AVC_CHECK_ARG((saved_gates_f == nullptr) == (saved_c_f == nullptr) &&
+                    (saved_gates_r == nullptr) == (saved_c_r == nullptr) &&
+                    (saved_c_f == nullptr) == (saved_c_r == nullptr),
+                "saved buffers must all be set or all NULL");
+  AVC_TRY(ensure_arena(ctx, bilstm_forward_scratch(T, B, din, H, saved_c_f != nullptr)));
+  return bilstm_forward_impl(ctx, T, B, din, H, x, ldx, w_f, w_r, y, ldy, saved_gates_f, saved_c_f,
+                             saved_gates_r, saved_c_r, S(stream));
 }
 
 int avc_lstm_backward(avc_context* ctx, int T, int B, int din, int H, int reverse,

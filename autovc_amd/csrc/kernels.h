@@ -30,6 +30,12 @@ int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const flo
                        float* g0, float* c0, float* g1, float* c1, hipStream_t s);
 size_t lstm2_forward_scratch(int T, int B, int din, int H, bool training);
 
+// bidirectional layer (wf/wr = {w_ih, w_hh, b_ih, b_hh}); H = 32 runs both directions in one launch
+int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                        const float* const* wf, const float* const* wr, float* y, int ldy,
+                        float* g_f, float* c_f, float* g_r, float* c_r, hipStream_t s);
+size_t bilstm_forward_scratch(int T, int B, int din, int H, bool training);
+
 // ---- split-fp16 LSTM forward recurrence (lstm_split.hip), used by the two above when supported
 bool lstm_split_supported(int H, int din);
 size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers);

@@ -438,27 +438,49 @@ void launch_step(const StepCfg& cfg, bool bwd, dim3 grid, const StepArgs& a, hip
 
 // ---- H = 32 persistent single-wave kernels (encoder BiLSTM) ------------------------------
 
-__global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, int reverse,
-                                                        const float* __restrict__ gx,
-                                                        const float* __restrict__ whh,
-                                                        float* __restrict__ y, long ldy,
-                                                        float* __restrict__ gates_out,
-                                                        float* __restrict__ c_out) {
-  const int b = blockIdx.x, lane = threadIdx.x;
+// One direction of an H = 32 layer, as seen by lstm32_fwd_kernel.
+struct L32Dir {
+  const float* gx;     // [T*B][ldgx] input projection (+biases), this direction's 128 columns
+  const float* whh;    // [128][32]
+  float* y;            // [T*B][ldy] output, this direction's 32 columns
+  float* gates;        // training: [T*B][128] activated gates (or NULL)
+  float* c;            // training: [T*B][32] cell states (or NULL)
+  int reverse;
+};
+
+// Workgroups [0, B) run direction d0, [B, 2B) direction d1 (both directions of a bidirectional
+// layer in one launch).  The input projection of step s+3 is fetched while step s computes: the
+// per-step chain is then LDS + FMA + gate math only.
+__global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx, long ldy, L32Dir d0,
+                                                        L32Dir d1) {
+  const int dir = blockIdx.x >= B ? 1 : 0;
+  const L32Dir& D = dir ? d1 : d0;
+  const int b = blockIdx.x - dir * B, lane = threadIdx.x;
+  const float* __restrict__ gx = D.gx;
+  const int reverse = D.reverse;
   __shared__ __attribute__((aligned(16))) float hs[32];
   float w0[32], w1[32];
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
-    w0[k] = whh[lane * 32 + k];
-    w1[k] = whh[(lane + 64) * 32 + k];
+    w0[k] = D.whh[lane * 32 + k];
+    w1[k] = D.whh[(lane + 64) * 32 + k];
   }
   if (lane < 32) hs[lane] = 0.f;
   float c = 0.f;
+  auto grow = [&](int st) {
+    const int sc = st < T ? st : T - 1;
+    return ((long)(reverse ? T - 1 - sc : sc) * B + b) * ldgx;
+  };
+  float za0 = gx[grow(0) + lane], za1 = gx[grow(0) + lane + 64];
+  float zb0 = gx[grow(1) + lane], zb1 = gx[grow(1) + lane + 64];
+  float zc0 = gx[grow(2) + lane], zc1 = gx[grow(2) + lane + 64];
   __syncthreads();
   for (int s = 0; s < T; ++s) {
     const int t = reverse ? T - 1 - s : s;
     const long row = (long)t * B + b;
-    float z0 = gx[row * 128 + lane], z1 = gx[row * 128 + lane + 64];
+    const long rn = grow(s + 3);
+    const float zd0 = gx[rn + lane], zd1 = gx[rn + lane + 64];
+    float z0 = za0, z1 = za1;
     float d0 = 0.f, d1 = 0.f;
 #pragma unroll
     for (int k4 = 0; k4 < 8; ++k4) {
@@ -475,10 +497,10 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, int revers
     if (lane < 32) {
       c = fg * c + a0 * a1;
       const float h = og * tanhf(c);
-      y[row * ldy + lane] = h;
-      if (c_out) c_out[row * 32 + lane] = c;
-      if (gates_out) {
-        float* g = gates_out + row * 128;
+      D.y[row * ldy + lane] = h;
+      if (D.c) D.c[row * 32 + lane] = c;
+      if (D.gates) {
+        float* g = D.gates + row * 128;
         g[lane] = a0;
         g[32 + lane] = fg;
         g[64 + lane] = a1;
@@ -487,6 +509,9 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, int revers
       hs[lane] = h;
     }
     __syncthreads();
+    za0 = zb0; za1 = zb1;
+    zb0 = zc0; zb1 = zc1;
+    zc0 = zd0; zc1 = zd1;
   }
 }
 
@@ -593,7 +618,8 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
     g.B = w_ih; g.bias0 = b_ih; g.bias1 = b_hh;
     AVC_TRY(gemm_run(ctx, g, s));
     hipEvent_t ev = timing_begin(TC_LSTM32, s);
-    lstm32_fwd_kernel<<<B, 64, 0, s>>>(T, B, reverse, gx, w_hh, y, ldy, saved_gates, saved_c);
+    L32Dir d{gx, w_hh, y, saved_gates, saved_c, reverse};
+    lstm32_fwd_kernel<<<B, 64, 0, s>>>(T, B, 128, ldy, d, d);
     AVC_LAUNCH_CHECK();
     if (ev) timing_end(TC_LSTM32, ev, s, 2.0 * T * B * 128.0 * 32.0, 4.0 * T * B * (128.0 + 32.0));
     return AVC_OK;
@@ -642,6 +668,45 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
     launch_step(cfg, false, grid, a, s);
   }
   AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+size_t bilstm_forward_scratch(int T, int B, int din, int H, bool training) {
+  if (H != 32) return lstm_forward_scratch(T, B, din, H, training);
+  GemmDesc d;
+  d.M = T * B; d.N = 128; d.Kc = din;
+  return (size_t)T * B * 256 * sizeof(float) + gemm_scratch_bytes(d) + 1024;
+}
+
+// Bidirectional layer (encoder.py:51): y[:, 0:H] forward, y[:, H:2H] reverse.  H = 32: both input
+// projections into one [T*B][256] buffer, then ONE recurrence launch for both directions.
+int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                        const float* const* wf, const float* const* wr, float* y, int ldy,
+                        float* g_f, float* c_f, float* g_r, float* c_r, hipStream_t s) {
+  if (H != 32) {
+    AVC_TRY(lstm_forward_impl(ctx, T, B, din, H, 0, x, ldx, wf[0], wf[1], wf[2], wf[3], y, ldy, g_f, c_f, s));
+    return lstm_forward_impl(ctx, T, B, din, H, 1, x, ldx, wr[0], wr[1], wr[2], wr[3], y + H, ldy, g_r, c_r, s);
+  }
+  AVC_CHECK_ARG(T > 0 && B > 0 && din % 4 == 0 && ldx % 4 == 0, "bilstm: bad shape");
+  Scratch sc(ctx);
+  const long TB = (long)T * B;
+  AVC_TAKE(gx, float, (size_t)TB * 256, sc);
+  for (int dir = 0; dir < 2; ++dir) {
+    const float* const* w = dir ? wr : wf;
+    GemmDesc g;
+    g.M = (int)TB; g.N = 128; g.Kc = din;
+    g.A = x; g.lda = ldx; g.a_rows = TB;
+    g.b_trans = 1; g.ldb = din; g.B = w[0]; g.bias0 = w[2]; g.bias1 = w[3];
+    g.C = gx + dir * 128; g.ldc = 256;
+    g.prec16 = 1;
+    AVC_TRY(gemm_run(ctx, g, s));
+  }
+  hipEvent_t ev = timing_begin(TC_LSTM32, s);
+  L32Dir d0{gx, wf[1], y, g_f, c_f, 0};
+  L32Dir d1{gx + 128, wr[1], y + 32, g_r, c_r, 1};
+  lstm32_fwd_kernel<<<2 * B, 64, 0, s>>>(T, B, 256, ldy, d0, d1);
+  AVC_LAUNCH_CHECK();
+  if (ev) timing_end(TC_LSTM32, ev, s, 2.0 * 2 * T * B * 128.0 * 32.0, 2.0 * 4.0 * T * B * (128.0 + 32.0));
   return AVC_OK;
 }
 

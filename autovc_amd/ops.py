@@ -7,6 +7,8 @@ CPU or through PyTorch kernels except autograd's own gradient bookkeeping.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -179,8 +181,12 @@ class BiLSTMLayer(torch.autograd.Function):
         x = x.contiguous()
         H = wh_f.shape[1]
         y = _empty((T * B, 2 * H), x)
-        g_f, c_f = _lstm_fwd(x, wi_f, wh_f, bi_f, bh_f, y, 0, 2 * H, False, save, T, B)
-        g_r, c_r = _lstm_fwd(x, wi_r, wh_r, bi_r, bh_r, y, H, 2 * H, True, save, T, B)
+        sv = [(_empty((T * B, 4 * H), x), _empty((T * B, H), x)) if save else (None, None) for _ in range(2)]
+        (g_f, c_f), (g_r, c_r) = sv
+        keep = [[t.contiguous() for t in grp] for grp in ((wi_f, wh_f, bi_f, bh_f), (wi_r, wh_r, bi_r, bh_r))]
+        ws = [(ctypes.c_void_p * 4)(*[ptr(t) for t in grp]) for grp in keep]
+        call("avc_bilstm_forward", _ctx(x), T, B, x.shape[1], H, ptr(x), x.shape[1], ws[0], ws[1], ptr(y),
+             2 * H, ptr(g_f), ptr(c_f), ptr(g_r), ptr(c_r), _stream(x))
         if save:
             ctx.save_for_backward(x, wi_f, wh_f, wi_r, wh_r, y, g_f, c_f, g_r, c_r)
         ctx.dims = (T, B, H)

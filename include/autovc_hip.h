@@ -95,6 +95,15 @@ int avc_lstm_forward(avc_context* ctx, int T, int B, int din, int H, int reverse
                      const float* b_hh, float* y, int ldy, float* saved_gates, float* saved_c,
                      void* stream);
 
+/* Bidirectional layer (encoder.py:51,75: nn.LSTM(..., bidirectional=True)): y[:, 0:H] is the
+ * forward direction, y[:, H:2H] the reverse one (rows of stride ldy).  w_f / w_r are the four
+ * tensors {w_ih, w_hh, b_ih, b_hh} of each direction; saved buffers per direction as in
+ * avc_lstm_forward.  For H = 32 both directions run in one launch. */
+int avc_bilstm_forward(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                       const float* const* w_f, const float* const* w_r, float* y, int ldy,
+                       float* saved_gates_f, float* saved_c_f, float* saved_gates_r,
+                       float* saved_c_r, void* stream);
+
 /* Backward through time.  d_y [T*B] rows of stride ldy (gradient of y).  Writes
  * (accumulate_dx/accumulate_dw = 0) or adds (= 1) d_x [T*B][din] (may be NULL) and d_w_ih,
  * d_w_hh, d_b_ih, d_b_hh (PyTorch layout); the two directions of a bidirectional layer share
