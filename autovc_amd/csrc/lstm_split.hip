@@ -20,10 +20,12 @@
 //     loads: cdna_hip_programming.md, in-launch split-K reduction) before running the gate
 //     epilogue.  Deterministic: the sum order never depends on arrival order.
 //
-// Split layout ("split rows"): a row of K values (K % 32 == 0) is K/32 chunks of 128 B,
-//   chunk c = [hi(k = 32c .. 32c+31) as f16 | lo(same) as f16].
-// Lane l of an MFMA holds k = 8(l>>4) .. 8(l>>4)+7 of a chunk: bytes 16(l>>4) (hi) and
-//   64 + 16(l>>4) (lo) — one 64-B run per row per load instruction.
+// Split operands are stored FRAGMENT-MAJOR: for every 16-row tile t and 32-deep chunk c of a
+// [rows][K] matrix, two 1 KiB blocks (hi, then lo) hold exactly what the 64 lanes of a
+// v_mfma_f32_16x16x32_f16 operand load: lane l = r + 16q gets row 16t + r, k = 32c + 8q .. +7
+// (8 halves, 16 B).  Block (t, c, hl) starts at ((t*nck + c)*2 + hl) KiB, nck = K/32.  Every
+// operand load is then one contiguous 1 KiB wave instruction (8 full 128-B lines) instead of a
+// 16-row x 64-B "fragment-shaped" gather, which ran the per-CU load path at ~11 B/cycle.
 #include <algorithm>
 
 #include "kernels.h"
@@ -92,13 +94,15 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
   if (red[0] > 0.f) (void)frexpf(red[0], &e);  // max < 2^e
   const float sc = ldexpf(1.0f, 15 - e);
   if (tid == 0) winv[p] = ldexpf(1.0f, e - 15) * kHUnscale;
-  _Float16* d = dst + (long)p * 2 * K;
+  const int nck = K >> 5;
+  _Float16* d = dst + (long)(p >> 4) * nck * 1024 + (p & 15) * 8;
   for (int k = tid; k < K; k += 256) {
     const float v = (k < Da ? ra[k] : rb[k - Da]) * sc;
     _Float16 hi, lo;
     split16(v, hi, lo);
-    d[(k >> 5) * 64 + (k & 31)] = hi;
-    d[(k >> 5) * 64 + 32 + (k & 31)] = lo;
+    _Float16* q = d + (k >> 5) * 1024 + ((k & 31) >> 3) * 128 + (k & 7);
+    q[0] = hi;
+    q[512] = lo;
   }
 }
 
@@ -111,15 +115,17 @@ __global__ void perm_bias_kernel(const float* __restrict__ a, const float* __res
 
 struct SplitSlot {
   int K, K0, kslice, nks, ncb;
-  const unsigned char* A; long lda;    // split rows of the reduction operand, columns [0, K0)
+  // fragment-major split operands; ld* = 32-deep chunks per 16-row tile of that matrix
+  const unsigned char* A; long lda;    // reduction operand, columns [0, K0); ntile 16-row tiles
   const unsigned char* A1; long lda1;  // columns [K0, K); NULL source = zeros
-  const unsigned char* W; long ldw;    // split weight rows [4H][K] (permuted gate order)
+  int ntile;                           // 16-row tiles present in A / A1 (ceil(B/16))
+  const unsigned char* W; long ldw;    // weights [4H][K] (permuted gate order)
   const float* winv;                   // [4H] unscale per gate row
   const float* gx; long ldgx;          // input projection (+biases) per batch row; ldgx 0 = shared row
   const float* c_prev;                 // NULL = zero state
   float* c_out;
   float* h_out; long ldh;              // fp32 h (the layer output)
-  _Float16* hs_out; long ldhs;         // split h for the next step (halves per row)
+  _Float16* hs_out; long ldhs;         // split h for the next step (fragment-major, H/32 chunks)
   float* gates_out;                    // training: [B][4H] activated gates (permuted order)
   float* slab;                         // [nrb][ncb][nks][64*64] fp32 partials
   int* cnt;                            // [nrb][ncb] tickets, zero before the launch
@@ -152,7 +158,6 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   const int cb = lb / nks, ks = lb - cb * nks;
   const int rb = blockIdx.y;
   const int B = a.B, H = a.H;
-  const int nrows = min(64, B - rb * 64);
   AVC_STAMP(0);
 
   f32x4 acc[4][NC];
@@ -166,30 +171,30 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   const bool second = k0 >= S.K0;
   const unsigned char* src = second ? S.A1 : S.A;
   if (src != nullptr) {
-    // buffer loads: lane part of the offset in one VGPR, the row-group / chunk part in SGPRs;
-    // rows >= B fall outside the descriptor's range and read as zero
-    const long lds_ = second ? S.lda1 : S.lda;
+    // buffer loads, one 1 KiB block per wave instruction: the lane offset (lane*16) is the only
+    // VGPR; tile / chunk offsets are SGPRs.  Row tiles past ntile fall outside the descriptor's
+    // range and read as zero (rows of a partial tile are computed and never stored).
+    const long nck = second ? S.lda1 : S.lda;
     const int kc0 = (second ? k0 - S.K0 : k0) >> 5;
+    const long hbase = ((long)rb * 4 * nck + kc0) * 2048;
     const auto hrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<unsigned char*>(src) + (long)rb * 64 * lds_ + (long)kc0 * 128, 0,
-        (int)(nrows * lds_ - (long)kc0 * 128), 0x00020000);
+        const_cast<unsigned char*>(src) + hbase, 0, (int)((long)S.ntile * nck * 2048 - hbase), 0x00020000);
+    const long wbase = ((long)cb * NC * S.ldw + (k0 >> 5)) * 2048;
     const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<unsigned char*>(S.W) + (long)cb * TW * S.ldw + (long)(k0 >> 5) * 128, 0,
-        (int)(TW * S.ldw - (long)(k0 >> 5) * 128), 0x00020000);
-    const int hvo = l15 * (int)lds_ + lq * 16;
-    const int wvo = l15 * (int)S.ldw + lq * 16;
-    const int hrow16 = 16 * (int)lds_, wrow16 = 16 * (int)S.ldw;
+        const_cast<unsigned char*>(S.W) + wbase, 0, (int)(NC * S.ldw * 2048), 0x00020000);
+    const int hvo = lane * 16, wvo = lane * 16;
+    const int hrow16 = (int)nck * 2048, wrow16 = (int)S.ldw * 2048;
 
     f16x8 hA[4][2], wA[NC][2], hB[4][2], wB[NC][2];
 #define AVC_LD(RS, VO, SO) __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(RS, VO, SO, 0))
 #define AVC_LOAD(HV, WV, C)                                                                       \
   _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                                 \
-    HV[r][0] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 128);                                          \
-    HV[r][1] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 128 + 64);                                     \
+    HV[r][0] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 2048);                                         \
+    HV[r][1] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 2048 + 1024);                                  \
   }                                                                                               \
   _Pragma("unroll") for (int n = 0; n < NC; ++n) {                                                \
-    WV[n][0] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 128);                                          \
-    WV[n][1] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 128 + 64);                                     \
+    WV[n][0] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 2048);                                         \
+    WV[n][1] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 2048 + 1024);                                  \
   }
 #define AVC_MFMA(HV, WV)                                                                          \
   _Pragma("unroll") for (int r = 0; r < 4; ++r)                                                   \
@@ -279,9 +284,10 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
       if (S.hs_out) {
         _Float16 hi, lo;
         split16(hv * kHScale, hi, lo);
-        _Float16* hs = S.hs_out + (long)b * S.ldhs + (j >> 5) * 64 + (j & 31);
+        _Float16* hs = S.hs_out + ((long)(b >> 4) * S.ldhs + (j >> 5)) * 1024 +
+                       ((b & 15) + 16 * ((j & 31) >> 3)) * 8 + (j & 7);
         hs[0] = hi;
-        hs[32] = lo;
+        hs[512] = lo;
       }
       if (S.gates_out) {
         float* go = S.gates_out + (long)b * 4 * H + p0;
@@ -427,9 +433,10 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
         hi[u] = h1;
         lo[u] = l1;
       }
-      _Float16* hs = S.hs_out + (long)b * S.ldhs + (j0 >> 5) * 64 + (j0 & 31);
+      _Float16* hs = S.hs_out + ((long)(b >> 4) * S.ldhs + (j0 >> 5)) * 1024 +
+                     ((b & 15) + 16 * ((j0 & 31) >> 3)) * 8 + (j0 & 7);
       *reinterpret_cast<f16x4*>(hs) = hi;
-      *reinterpret_cast<f16x4*>(hs + 32) = lo;
+      *reinterpret_cast<f16x4*>(hs + 512) = lo;
     }
     if (S.gates_out) {
       float* go = S.gates_out + (long)b * 4 * H + cb * TW + blk * 16;
@@ -543,7 +550,8 @@ size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
   s += al((size_t)4 * H * din * f) + 2 * al((size_t)4 * H * f);  // permuted W_ih, biases
   s += al((size_t)4 * H * H * 2 * 2) + al((size_t)4 * H * f);    // split W_hh + winv
   if (nlayers == 2) s += al((size_t)4 * H * 2 * H * 2 * 2) + 2 * al((size_t)4 * H * f);
-  s += (size_t)nlayers * (2 * al((size_t)B * H * 2 * 2) + 2 * al((size_t)B * H * f));  // h splits, c
+  const size_t Bp = (size_t)(B + 15) / 16 * 16;
+  s += (size_t)nlayers * (2 * al(Bp * H * 2 * 2) + 2 * al((size_t)B * H * f));  // h splits, c
   // slabs: at most K/128 splits of every 64-column tile, per slot
   s += (size_t)nlayers * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
   s += al((size_t)(T + 2) * 2 * nrb * (4 * H / 64) * sizeof(int));
@@ -566,7 +574,9 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   AVC_TAKE(b_p, float, (size_t)4 * H, sc);
   AVC_TAKE(whh_s, _Float16, (size_t)4 * H * H * 2, sc);
   AVC_TAKE(winv, float, (size_t)4 * H, sc);
-  AVC_TAKE(hs, _Float16, (size_t)2 * B * H * 2, sc);
+  const int ntile = (B + 15) / 16;
+  const long hsz = (long)ntile * 16 * H * 2;  // halves per split-h buffer
+  AVC_TAKE(hs, _Float16, (size_t)2 * hsz, sc);
   float* cpp = nullptr;
   if (!saved_c) {
     AVC_TAKE(tmp, float, (size_t)2 * B * H, sc);
@@ -617,10 +627,11 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
     a.B = B; a.H = H; a.nblk0 = (int)grid.x;
     SplitSlot& S = a.s[0];
     S.K = H; S.K0 = H; S.kslice = ksl[0]; S.nks = nks; S.ncb = ncb;
-    S.A = st > 0 ? reinterpret_cast<const unsigned char*>(hs + (long)((st - 1) & 1) * B * H * 2) : nullptr;
-    S.lda = 4L * H;
+    S.A = st > 0 ? reinterpret_cast<const unsigned char*>(hs + (long)((st - 1) & 1) * hsz) : nullptr;
+    S.lda = H / 32;
+    S.ntile = ntile;
     S.W = reinterpret_cast<const unsigned char*>(whh_s);
-    S.ldw = 4L * H;
+    S.ldw = H / 32;
     S.winv = winv;
     S.gx = gx + (long)t * B * 4 * H;
     S.ldgx = 4L * H;
@@ -633,8 +644,8 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
     }
     S.h_out = y + (long)t * B * ldy;
     S.ldh = ldy;
-    S.hs_out = st < T - 1 ? hs + (long)(st & 1) * B * H * 2 : nullptr;
-    S.ldhs = 2L * H;
+    S.hs_out = st < T - 1 ? hs + (long)(st & 1) * hsz : nullptr;
+    S.ldhs = H / 32;
     S.gates_out = saved_gates ? saved_gates + (long)t * B * 4 * H : nullptr;
     S.slab = slab;
     S.cnt = cnt ? cnt + (long)st * nrb * ncb : nullptr;
@@ -663,8 +674,10 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   AVC_TAKE(w1_s, _Float16, (size_t)4 * H * 2 * H * 2, sc);
   AVC_TAKE(winv0, float, (size_t)4 * H, sc);
   AVC_TAKE(winv1, float, (size_t)4 * H, sc);
-  AVC_TAKE(hs0, _Float16, (size_t)2 * B * H * 2, sc);
-  AVC_TAKE(hs1, _Float16, (size_t)2 * B * H * 2, sc);
+  const int ntile = (B + 15) / 16;
+  const long hsz = (long)ntile * 16 * H * 2;  // halves per split-h buffer
+  AVC_TAKE(hs0, _Float16, (size_t)2 * hsz, sc);
+  AVC_TAKE(hs1, _Float16, (size_t)2 * hsz, sc);
   split_rows_kernel<<<4 * H, 256, 0, s>>>(w0[1], H, nullptr, 0, H, 1, w0_s, winv0);
   split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[0], H, w1[1], H, H, 1, w1_s, winv1);
   perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w0[2], w0[3], b0_p, H);
@@ -696,7 +709,6 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   const long cstride = 2L * nrb * ncb;
   AVC_TAKE(cnt, int, (size_t)(T + 1) * cstride, sc);
   AVC_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (T + 1) * cstride, s));
-  const long hsz = (long)B * H * 2;  // halves per split-h buffer
   auto hs0p = [&](int t) { return reinterpret_cast<const unsigned char*>(hs0 + (long)(t & 1) * hsz); };
   auto hs1p = [&](int t) { return reinterpret_cast<const unsigned char*>(hs1 + (long)(t & 1) * hsz); };
 
@@ -708,9 +720,10 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
     SplitSlot& S0 = a.s[0];
     S0.K = H; S0.K0 = H; S0.kslice = ksl[0]; S0.nks = nks0; S0.ncb = ncb;
     S0.A = (l0 && t0 > 0) ? hs0p(t0 - 1) : nullptr;
-    S0.lda = 4L * H;
+    S0.lda = H / 32;
+    S0.ntile = ntile;
     S0.W = reinterpret_cast<const unsigned char*>(w0_s);
-    S0.ldw = 4L * H;
+    S0.ldw = H / 32;
     S0.winv = winv0;
     S0.gx = gx + (long)(l0 ? t0 : 0) * B * 4 * H;
     S0.ldgx = 4L * H;
@@ -724,7 +737,7 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
     S0.h_out = y0 + (long)(l0 ? t0 : 0) * B * H;
     S0.ldh = H;
     S0.hs_out = l0 ? const_cast<_Float16*>(reinterpret_cast<const _Float16*>(hs0p(t0))) : nullptr;
-    S0.ldhs = 2L * H;
+    S0.ldhs = H / 32;
     S0.gates_out = g0 ? g0 + (long)(l0 ? t0 : 0) * B * 4 * H : nullptr;
     S0.slab = slab0;
     S0.cnt = cnt + (long)st * cstride;
@@ -732,11 +745,12 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
     SplitSlot& S1 = a.s[1];
     S1.K = 2 * H; S1.K0 = H; S1.kslice = ksl[1]; S1.nks = nks1; S1.ncb = ncb;
     S1.A = l1 ? hs0p(t1) : nullptr;
-    S1.lda = 4L * H;
+    S1.lda = H / 32;
     S1.A1 = (l1 && t1 > 0) ? hs1p(t1 - 1) : nullptr;
-    S1.lda1 = 4L * H;
+    S1.lda1 = H / 32;
+    S1.ntile = ntile;
     S1.W = reinterpret_cast<const unsigned char*>(w1_s);
-    S1.ldw = 8L * H;
+    S1.ldw = 2 * H / 32;
     S1.winv = winv1;
     S1.gx = b1_p;
     S1.ldgx = 0;
@@ -751,7 +765,7 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
     S1.h_out = y1 + (long)tt1 * B * H;
     S1.ldh = H;
     S1.hs_out = (l1 && t1 < T - 1) ? const_cast<_Float16*>(reinterpret_cast<const _Float16*>(hs1p(t1))) : nullptr;
-    S1.ldhs = 2L * H;
+    S1.ldhs = H / 32;
     S1.gates_out = g1 ? g1 + (long)tt1 * B * 4 * H : nullptr;
     S1.slab = slab1;
     S1.cnt = cnt + (long)st * cstride + (long)nrb * ncb;
