@@ -74,7 +74,7 @@ size_t gen_scratch(int T, int B) {
   nested = std::max(nested, lstm_forward_scratch(T, B, 512, 1024, false));
   nested = std::max(nested, lstm2_forward_scratch(T, B, 512, 1024, false));
   GemmDesc lin;
-  lin.M = (int)TB; lin.N = 80; lin.Kc = 1024; lin.b_trans = 1;
+  lin.M = (int)TB; lin.N = 80; lin.Kc = 1024; lin.b_trans = 1; lin.prec16 = 1;
   nested = std::max(nested, gemm_scratch_bytes(lin));
   return own + nested + (1 << 20);
 }

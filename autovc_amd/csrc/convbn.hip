@@ -58,7 +58,8 @@ GemmDesc conv_fwd_desc(int T, int B, int cin, int cout, const float* x, const fl
 size_t conv_bn_forward_scratch(int T, int B, int cin, int cout) {
   const int bm = gemm_stats_rows(T * B, cout);
   const size_t parts = (size_t)((T * B + bm - 1) / bm) * 2 * cout;
-  return (5UL * cin * cout + parts) * sizeof(float) + 1024;
+  const GemmDesc g = conv_fwd_desc(T, B, cin, cout, nullptr, nullptr, nullptr, nullptr);
+  return (5UL * cin * cout + parts) * sizeof(float) + gemm_scratch_bytes(g) + 2048;
 }
 
 int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,

@@ -528,6 +528,267 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
   }
 }
 
+// ---- split-f16 GEMM on pre-split fragment-major operands ("gemm16f") ---------------------
+//
+// Both operands are first split once into the fragment-major layout of v_mfma_f32_32x32x16_f16
+// (split_frag32_kernel): for every 32-row tile t and 16-deep chunk c, two 1 KiB blocks (hi,
+// lo) hold exactly what the 64 lanes of one operand load: lane l = r + 32q gets row 32t + r,
+// k = 16c + 8q .. +7.  Block (t, c, hl) sits at ((t*nkc + c)*2 + hl) KiB; rows are padded to a
+// multiple of 32 and K to a multiple of 32 with zeros.  The GEMM then streams whole 1 KiB blocks
+// global -> LDS with LDS-DMA (buffer_load ... lds: no VGPRs, no conversion ALU, no bank
+// conflicts), three stages deep with counted vmcnt and raw barriers, and reads every fragment
+// with one conflict-free ds_read_b128 at lane*16.  Row tiles outside the operand (Conv1d zero
+// padding; tap shifts must be multiples of 32 rows) fall outside the buffer descriptor and
+// land as zeros.
+__global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restrict__ src, long rs,
+                                                           long ks, int R, int K, int ntile, int nkc,
+                                                           _Float16* __restrict__ dst) {
+  const int G8 = nkc * 2;  // 8-element groups per row
+  const long total = (long)ntile * 32 * G8;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    long r;
+    int g8;
+    if (ks == 1) {  // row-major source: consecutive threads read consecutive 32-B pieces of a row
+      r = idx / G8;
+      g8 = (int)(idx - r * G8);
+    } else {        // transposed source (column stride 1): consecutive threads take consecutive rows
+      const long rows = (long)ntile * 32;
+      g8 = (int)(idx / rows);
+      r = idx - (long)g8 * rows;
+    }
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * g8 + e;
+      v[e] = (r < R && k < K) ? src[r * rs + (long)k * ks] : 0.f;
+    }
+    f16x8 hi, lo;
+    split8(v, hi, lo);
+    const long blk = ((r >> 5) * nkc + (g8 >> 1)) * 2;
+    const int lane = (int)(r & 31) + 32 * (g8 & 1);
+    *reinterpret_cast<f16x8*>(dst + blk * 512 + lane * 8) = hi;
+    *reinterpret_cast<f16x8*>(dst + (blk + 1) * 512 + lane * 8) = lo;
+  }
+}
+
+struct Frag16Args {
+  const _Float16* As; int a_ntile, a_nkc; long a_shift0, a_tapshift;  // shifts in rows (x32)
+  const _Float16* Bs; int b_ntile, b_nkc; long b_tapstride;            // halves per tap
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag16Args f, int tilesM,
+                                                               int tilesN, int kt_per_tap, int kps,
+                                                               int nsplit, float* __restrict__ slab) {
+  constexpr int NT = 64 * WM * WN, NWAVE = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int ABLK = (BM / 32) * 4, BBLK = (BN / 32) * 4;  // 1 KiB blocks per K-tile (2 kc x hi/lo)
+  constexpr int NBLK = ABLK + BBLK;
+  static_assert(NBLK % NWAVE == 0, "blocks per K-tile must split evenly over the waves");
+  constexpr int DPW = NBLK / NWAVE;  // LDS-DMA instructions per wave per K-tile
+  constexpr int STAGE = NBLK * 1024;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // 3 stages
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int nwg = tilesM * tilesN;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+  const int tm = wgid / tilesN, tn = wgid - tm * tilesN;
+  const int split = blockIdx.y;
+  const int ktotal = d.ntaps * kt_per_tap;
+  const int kt0 = split * kps;
+  const int kt1 = min(ktotal, kt0 + kps);
+
+  const auto ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.As), 0,
+                                                     f.a_ntile * f.a_nkc * 2048, 0x00020000);
+  const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.Bs), 0,
+                                                     (int)(d.ntaps * f.b_tapstride * 2), 0x00020000);
+  // Out-of-range blocks get an offset past the descriptor's num_records: the bounds check (on
+  // the VGPR offset; the SGPR offset is not range-checked) makes the DMA land zeros.
+  constexpr unsigned kOut = 0x7FFFFF00u;
+  const int a_ntile = f.a_ntile, a_nkc = f.a_nkc, b_ntile = f.b_ntile, b_nkc = f.b_nkc;
+  const long a_shift0 = f.a_shift0, a_tapshift = f.a_tapshift, b_tapstride = f.b_tapstride;
+
+  // issue the LDS-DMA of K-tile kt into stage st: this wave's DPW blocks of the NBLK
+#define AVC16F_ISSUE(KT, ST)                                                                      \
+  {                                                                                               \
+    const int tau = (KT) / kt_per_tap;                                                            \
+    const int kc0 = ((KT) - tau * kt_per_tap) * 2;                                                \
+    _Pragma("unroll") for (int i = 0; i < DPW; ++i) {                                             \
+      const int b = w * DPW + i;                                                                  \
+      unsigned char* dst = lds + (ST) * STAGE + b * 1024;                                         \
+      if (b < ABLK) {                                                                             \
+        const int rt = b >> 2, kc = (b >> 1) & 1, hl = b & 1;                                     \
+        const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)tau * a_tapshift) / 32; \
+        const bool ok = src_tile >= 0 && src_tile < a_ntile;                                      \
+        const unsigned off = ok ? (unsigned)(((src_tile * a_nkc + kc0 + kc) * 2 + hl) * 1024) : kOut; \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)dst, 16, \
+                                                 off + lane * 16, 0, 0, 0);                       \
+      } else {                                                                                    \
+        const int bb = b - ABLK;                                                                  \
+        const int ct = bb >> 2, kc = (bb >> 1) & 1, hl = bb & 1;                                  \
+        const int src_tile = tn * (BN / 32) + ct;                                                 \
+        const bool ok = src_tile < b_ntile;                                                       \
+        const unsigned off = ok ? (unsigned)(tau * b_tapstride * 2 +                              \
+                                             ((long)(src_tile * b_nkc + kc0 + kc) * 2 + hl) * 1024) : kOut; \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16, \
+                                                 off + lane * 16, 0, 0, 0);                       \
+      }                                                                                           \
+    }                                                                                             \
+  }
+
+  f32x16 zero16;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) zero16[e] = 0.f;
+  f32x16 acc[TM][TN], cmp[TM][TN], part[TM][TN], crs[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = cmp[i][j] = part[i][j] = crs[i][j] = zero16;
+
+  constexpr int KB = 4;  // K-tiles (128 k) per compensated partial
+  if (kt0 < kt1) AVC16F_ISSUE(kt0, 0);
+  if (kt0 + 1 < kt1) AVC16F_ISSUE(kt0 + 1, 1);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int st = (kt - kt0) % 3;
+    // this wave's blocks of tile kt have landed once at most the next tile's DPW are pending
+    if (kt + 1 < kt1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + 2 < kt1) AVC16F_ISSUE(kt + 2, (kt + 2 - kt0) % 3);
+    const unsigned char* Ai = lds + st * STAGE;
+    const unsigned char* Bi = Ai + ABLK * 1024;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const unsigned char* p = Ai + (((wm * TM + i) * 2 + s) * 2) * 1024 + lane * 16;
+        ah[i] = *reinterpret_cast<const f16x8*>(p);
+        al[i] = *reinterpret_cast<const f16x8*>(p + 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const unsigned char* p = Bi + (((wn * TN + j) * 2 + s) * 2) * 1024 + lane * 16;
+        bh[j] = *reinterpret_cast<const f16x8*>(p);
+        bl[j] = *reinterpret_cast<const f16x8*>(p + 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], part[i][j], 0, 0, 0);
+          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], crs[i][j], 0, 0, 0);
+          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], crs[i][j], 0, 0, 0);
+        }
+    }
+    if ((kt - kt0) % KB == KB - 1 || kt + 1 == kt1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float y = part[i][j][e] - cmp[i][j][e];
+            const float t = acc[i][j][e] + y;
+            cmp[i][j][e] = (t - acc[i][j][e]) - y;
+            acc[i][j][e] = t;
+          }
+          part[i][j] = zero16;
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = (acc[i][j][e] - cmp[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
+#undef AVC16F_ISSUE
+
+  // ---- epilogue (32x32 C layout: col = lane&31, row = (e&3) + 8(e>>2) + 4(lane>>5)) --------
+  const int row_base = tm * BM + wm * WTM + 4 * (lane >> 5);
+  const int col_base = tn * BN + wn * WTN + (lane & 31);
+  if (nsplit > 1) {
+    float* out = slab + (long)split * d.M * d.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col_base + 32 * j;
+        if (col >= d.N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+          if (row < d.M) out[(long)row * d.N + col] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+  float* __restrict__ C = d.C;
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    csum[j] = 0.f;
+    csq[j] = 0.f;
+    const int col = col_base + 32 * j;
+    const bool colok = col < d.N;
+    float bias = 0.f;
+    if (colok) {
+      if (d.bias0) bias += d.bias0[col];
+      if (d.bias1) bias += d.bias1[col];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+        if (!colok || row >= d.M) continue;
+        const float v = act_apply(acc[i][j][e] + bias, d.act);
+        float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
+        if (d.accumulate) *p += v; else *p = v;
+        csum[j] += v;
+        csq[j] += v * v;
+      }
+  }
+  if (d.stats) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float s = csum[j] + __shfl_xor(csum[j], 32);
+      const float s2 = csq[j] + __shfl_xor(csq[j], 32);
+      if (lane < 32) {
+        const int cl = wn * WTN + 32 * j + lane;
+        red[(wm * 2 + 0) * BN + cl] = s;
+        red[(wm * 2 + 1) * BN + cl] = s2;
+      }
+    }
+    __syncthreads();
+    for (int cl = tid; cl < BN; cl += NT) {
+      const int col = tn * BN + cl;
+      if (col < d.N) {
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int r = 0; r < WM; ++r) {
+          s += red[(r * 2 + 0) * BN + cl];
+          s2 += red[(r * 2 + 1) * BN + cl];
+        }
+        d.stats[((long)tm * 2 + 0) * d.N + col] = s;
+        d.stats[((long)tm * 2 + 1) * d.N + col] = s2;
+      }
+    }
+  }
+}
+
 __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __restrict__ slab) {
   const long total = (long)d.nz * d.M * d.N;
   const long MN = (long)d.M * d.N;
@@ -546,7 +807,9 @@ __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __rest
   }
 }
 
-int g_gemm16 = 1;  // avc_gemm_tune(): 0 routes prec16 products to the fp32 kernel (A/B runs)
+// avc_gemm_tune(): forward (prec16) products on 0 = the fp32 kernel, 1 = gemm16 (operands split
+// while staged), 2 = gemm16f on pre-split fragment-major operands where eligible (default)
+int g_gemm16 = 2;
 
 struct Plan {
   int bm, bn, tilesM, tilesN, kt_per_tap, ktotal, nsplit, kps;
@@ -575,6 +838,36 @@ Plan make_plan(const GemmDesc& d, int force_split) {
   p.nsplit = (p.ktotal + p.kps - 1) / p.kps;
   if (p.nsplit < 1) p.nsplit = 1;
   return p;
+}
+
+inline long frag_ntile(long rows) { return (rows + 31) / 32; }
+inline int frag_nkc(int K) { return (K + 31) / 32 * 2; }
+inline size_t frag_bytes(long rows, int K) { return (size_t)frag_ntile(rows) * frag_nkc(K) * 2048; }
+
+bool frag16_eligible(const GemmDesc& d) {
+  return d.prec16 && g_gemm16 == 2 && !d.a_trans && d.nz == 1 && d.b_shift0 == 0 && d.b_zshift == 0 &&
+         d.a_shift0 % 32 == 0 && (d.ntaps == 1 || d.a_tapshift % 32 == 0) &&
+         (d.b_trans || d.b_rows >= d.Kc);
+}
+
+size_t frag16_scratch(const GemmDesc& d) {
+  const long a_rows = d.a_rows ? d.a_rows : d.M;
+  return frag_bytes(a_rows, d.Kc) + (size_t)d.ntaps * frag_bytes(d.N, d.Kc) + 1024;
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch16f(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
+  constexpr int NBLK = (BM / 32) * 4 + (BN / 32) * 4;
+  const size_t lds = 3 * NBLK * 1024;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16f_kernel<BM, BN, WM, WN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  dim3 grid(p.tilesM * p.tilesN, p.nsplit);
+  gemm16f_kernel<BM, BN, WM, WN><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, p.kt_per_tap,
+                                                                p.kps, p.nsplit, slab);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -614,8 +907,9 @@ int gemm_stats_rows(int M, int N) {
 
 size_t gemm_scratch_bytes(const GemmDesc& d) {
   Plan p = make_plan(d, 0);
-  if (p.nsplit <= 1) return 0;
-  return (size_t)p.nsplit * d.nz * d.M * d.N * sizeof(float) + 256;
+  size_t s = p.nsplit <= 1 ? 0 : (size_t)p.nsplit * d.nz * d.M * d.N * sizeof(float) + 256;
+  if (d.prec16 && !d.a_trans) s += frag16_scratch(d);
+  return s;
 }
 
 int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) {
@@ -638,8 +932,35 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     slab = sc.take<float>((size_t)p.nsplit * d.nz * d.M * d.N);
     if (!slab) return AVC_ERR_WORKSPACE;
   }
+  Frag16Args fa{};
+  const bool frag = frag16_eligible(d);
+  if (frag) {
+    // split both operands once into the fragment-major layout gemm16f_kernel streams
+    const long a_ntile = frag_ntile(d.a_rows);
+    const int nkc = frag_nkc(d.Kc);
+    const long b_ntile = frag_ntile(d.N);
+    _Float16* as = sc.take<_Float16>(frag_bytes(d.a_rows, d.Kc) / 2);
+    _Float16* bs = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, d.Kc) / 2);
+    if (!as || !bs) return AVC_ERR_WORKSPACE;
+    const long ta = a_ntile * 32 * nkc * 2;
+    split_frag32_kernel<<<(int)std::min<long>((ta + 255) / 256, 8192), 256, 0, stream>>>(
+        d.A, d.lda, 1, (int)d.a_rows, d.Kc, (int)a_ntile, nkc, as);
+    const long tapstride = b_ntile * nkc * 1024;  // halves
+    const long tb = b_ntile * 32 * nkc * 2;
+    for (int tau = 0; tau < d.ntaps; ++tau)
+      split_frag32_kernel<<<(int)std::min<long>((tb + 255) / 256, 8192), 256, 0, stream>>>(
+          d.B + (long)tau * d.b_tapoff, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N,
+          d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, d.b_rows), (int)b_ntile, nkc, bs + tau * tapstride);
+    AVC_LAUNCH_CHECK();
+    fa.As = as; fa.a_ntile = (int)a_ntile; fa.a_nkc = nkc;
+    fa.a_shift0 = d.a_shift0; fa.a_tapshift = d.a_tapshift;
+    fa.Bs = bs; fa.b_ntile = (int)b_ntile; fa.b_nkc = nkc; fa.b_tapstride = tapstride;
+  }
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
-  if (d.prec16 && !d.a_trans && g_gemm16) {
+  if (frag) {
+    if (p.bm == 128) launch16f<128, 128, 4, 2>(d, fa, p, slab, stream);
+    else launch16f<64, 64, 2, 2>(d, fa, p, slab, stream);
+  } else if (d.prec16 && !d.a_trans && g_gemm16) {
     if (p.bm == 128) launch16<128, 128, 4, 2>(d, p, slab, stream);
     else launch16<64, 64, 2, 2>(d, p, slab, stream);
   } else if (p.bm == 128) {
@@ -664,7 +985,11 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
 
 }  // namespace avc
 
-extern "C" int avc_gemm_tune(int prec16) {
-  avc::g_gemm16 = prec16 ? 1 : 0;
+extern "C" int avc_gemm_tune(int mode) {
+  if (mode < 0 || mode > 2) {
+    avc::set_error("avc_gemm_tune: mode must be 0, 1 or 2");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_gemm16 = mode;
   return AVC_OK;
 }

@@ -582,7 +582,7 @@ size_t lstm_forward_scratch(int T, int B, int din, int H, bool training) {
   size_t s = (size_t)T * B * 4 * H * f + 1024;
   if (H != 32) s += (size_t)4 * H * (din + H + 2) * f + (training ? 0 : (size_t)2 * B * H * f) + 2048;
   GemmDesc d;
-  d.M = T * B; d.N = 4 * H; d.Kc = din;
+  d.M = T * B; d.N = 4 * H; d.Kc = din; d.prec16 = 1;
   s += gemm_scratch_bytes(d);
   return lstm_split_supported(H, din) ? std::max(s, lstm_split_forward_scratch(T, B, din, H, 1)) : s;
 }
@@ -674,7 +674,7 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
 size_t bilstm_forward_scratch(int T, int B, int din, int H, bool training) {
   if (H != 32) return lstm_forward_scratch(T, B, din, H, training);
   GemmDesc d;
-  d.M = T * B; d.N = 128; d.Kc = din;
+  d.M = T * B; d.N = 128; d.Kc = din; d.prec16 = 1;
   return (size_t)T * B * 256 * sizeof(float) + gemm_scratch_bytes(d) + 1024;
 }
 
@@ -715,7 +715,7 @@ size_t lstm2_forward_scratch(int T, int B, int din, int H, bool training) {
   size_t s = (size_t)T * B * 4 * H * f + (size_t)4 * H * (din + H + 2 * H + 3) * f + 4096;
   if (!training) s += (size_t)4 * B * H * f;
   GemmDesc d;
-  d.M = T * B; d.N = 4 * H; d.Kc = din;
+  d.M = T * B; d.N = 4 * H; d.Kc = din; d.prec16 = 1;
   s += gemm_scratch_bytes(d);
   return lstm_split_supported(H, din) ? std::max(s, lstm_split_forward_scratch(T, B, din, H, 2)) : s;
 }

@@ -556,7 +556,7 @@ size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
   s += (size_t)nlayers * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
   s += al((size_t)(T + 2) * 2 * nrb * (4 * H / 64) * sizeof(int));
   GemmDesc d;
-  d.M = (int)TB; d.N = 4 * H; d.Kc = din;
+  d.M = (int)TB; d.N = 4 * H; d.Kc = din; d.prec16 = 1;
   return s + gemm_scratch_bytes(d) + 4096;
 }
 

@@ -247,3 +247,46 @@ def test_fused_clip_adam_ema_matches_torch(cuda_device, max_norm):
             assert norm_out.item() == pytest.approx(ref_norm.item(), rel=5e-6)
         assert (p_hip.cpu() - pr.detach()).abs().max().item() < 2e-7 * max(1.0, pr.abs().max().item())
         assert (ema.cpu() - ema_ref).abs().max().item() < 4e-7 * max(1.0, ema_ref.abs().max().item())
+
+
+@pytest.mark.parametrize("M,din,dout", [(64, 32, 32), (96, 64, 80), (8192, 512, 128), (300, 320, 2048), (128, 1024, 80)])
+def test_forward_gemm_paths(cuda_device, M, din, dout):
+    """Forward products on both split-f16 kernels (operands split while staged / pre-split
+    fragment-major with LDS-DMA) against fp64, through the Linear layer."""
+    g = torch.Generator().manual_seed(M + din + dout)
+    x = torch.randn(M, din, generator=g)
+    w = torch.randn(dout, din, generator=g) / np.sqrt(din)
+    b = torch.randn(dout, generator=g) * 0.1
+    ref = x.double() @ w.double().T + b.double()
+    errs = {}
+    try:
+        for mode in (1, 2):
+            _lib.call("avc_gemm_tune", mode)
+            with torch.no_grad():
+                y = ops.Linear.apply(_t(x, cuda_device), _t(w, cuda_device), _t(b, cuda_device))
+            errs[mode] = (y.cpu().double() - ref).abs().max().item()
+    finally:
+        _lib.call("avc_gemm_tune", 2)
+    scale = ref.abs().max().item()
+    assert errs[1] < 2e-6 * max(1.0, scale) and errs[2] < 2e-6 * max(1.0, scale), errs
+
+
+@pytest.mark.parametrize("B,T,cin,cout", [(32, 16, 64, 96), (64, 8, 512, 512), (32, 40, 80, 512)])
+def test_conv_fragment_path(cuda_device, B, T, cin, cout):
+    """Conv1d k5 + BN with a batch that is a multiple of 32 (tap shifts = whole 32-row tiles),
+    i.e. on the pre-split fragment-major GEMM, against fp64."""
+    g = torch.Generator().manual_seed(B + T + cin + cout)
+    x = torch.rand(B, cin, T, generator=g)
+    W = (torch.rand(cout, cin, 5, generator=g) - 0.5) * 0.1
+    bias = (torch.rand(cout, generator=g) - 0.5) * 0.1
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = (torch.rand(cout, generator=g) - 0.5) * 0.4
+    y = F.batch_norm(F.conv1d(x.double(), W.double(), bias.double(), padding=2), None, None,
+                     gamma.double(), beta.double(), training=True, eps=1e-5)
+    fr = x.permute(2, 0, 1).reshape(T * B, cin)
+    with torch.no_grad():
+        out = ops.ConvBNAct.apply(_t(fr, cuda_device), _t(W, cuda_device), _t(bias, cuda_device),
+                                  _t(gamma, cuda_device), _t(beta, cuda_device), None, None, True, 0.1,
+                                  1e-5, ops.ACT_NONE, None, T, B)
+    out_cf = out.cpu().reshape(T, B, cout).permute(1, 2, 0).double()
+    assert (out_cf - y).abs().max().item() < 1e-5
