@@ -115,6 +115,7 @@ __global__ void perm_bias_kernel(const float* __restrict__ a, const float* __res
 
 struct SplitSlot {
   int K, K0, kslice, nks, ncb;
+  int mode;                            // 0: LSTM step epilogue; 1: projection, h_out[b][p] = acc*winv + gx
   // fragment-major split operands; ld* = 32-deep chunks per 16-row tile of that matrix
   const unsigned char* A; long lda;    // reduction operand, columns [0, K0); ntile 16-row tiles
   const unsigned char* A1; long lda1;  // columns [K0, K); NULL source = zeros
@@ -131,9 +132,12 @@ struct SplitSlot {
   int* cnt;                            // [nrb][ncb] tickets, zero before the launch
 };
 
+// A launch runs up to three independent slots side by side: workgroups [0, nb[0]) slot 0,
+// the next nb[1] slot 1, the last nb[2] slot 2.
 struct SplitArgs {
-  int B, H, nblk0;
-  SplitSlot s[2];
+  int B, H;
+  int nb[3];
+  SplitSlot s[3];
 };
 
 // NC = 16-column gate blocks (4 hidden units x 4 gates) per workgroup tile: 4 for the wide
@@ -151,14 +155,39 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   // hipcc wraps every buffer load in a waterfall loop
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
-  const int L = (int)blockIdx.x >= a.nblk0 ? 1 : 0;
-  const SplitSlot& S = L ? a.s[1] : a.s[0];
-  const int lb = blockIdx.x - (L ? a.nblk0 : 0);
+  const int bx = blockIdx.x;
+  const int L = bx < a.nb[0] ? 0 : (bx < a.nb[0] + a.nb[1] ? 1 : 2);
+  const SplitSlot& S = L == 0 ? a.s[0] : (L == 1 ? a.s[1] : a.s[2]);
+  const int lb = bx - (L >= 1 ? a.nb[0] : 0) - (L == 2 ? a.nb[1] : 0);
   const int nks = S.nks;
   const int cb = lb / nks, ks = lb - cb * nks;
   const int rb = blockIdx.y;
   const int B = a.B, H = a.H;
   AVC_STAMP(0);
+
+  // Epilogue ownership (wide tiles): thread t handles (row, blk) pairs t + NT*i; a pair's 4 float4
+  // columns blk*16 + 4g (gate g, units 0..3) hold all four gates of 4 hidden units.  Its
+  // operands are fetched before the MFMA phase so that their latency hides under it.
+  f32x4 gxv[PP][4], wiv[PP][4], cpv[PP];
+  if constexpr (!(NC == 1 && NW == 4))
+#pragma unroll
+  for (int i = 0; i < PP; ++i) {
+    const int pr = min(tid + NT * i, NPAIR - 1), row = pr / NC, blk = pr % NC;
+    const int b = min(rb * 64 + row, B - 1);
+    const int p0 = cb * TW + blk * 16;
+    const float* gxr = S.gx + (long)b * S.ldgx + p0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      gxv[i][g] = *reinterpret_cast<const f32x4*>(gxr + 4 * g);
+      wiv[i][g] = *reinterpret_cast<const f32x4*>(S.winv + p0 + 4 * g);
+    }
+    // unconditional load (a NULL c_prev reads winv instead and is zeroed after): a conditional
+    // load would make hipcc drain vmcnt to 0 at the join, before the MFMA loads are issued
+    const bool hasc = S.c_prev != nullptr;
+    const float* cpp = hasc ? S.c_prev + (long)b * H + cb * 4 * NC + blk * 4 : S.winv;
+    const f32x4 cv = *reinterpret_cast<const f32x4*>(cpp);
+    cpv[i] = hasc ? cv : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   f32x4 acc[4][NC];
 #pragma unroll
@@ -259,7 +288,9 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
       wis[g] = S.winv[p0 + 4 * g];
     }
     const int j = cb * 4 + u;
-    const float cp = S.c_prev ? S.c_prev[(long)bc * H + j] : 0.f;
+    const bool hasc = S.c_prev != nullptr;
+    const float cpl = *(hasc ? S.c_prev + (long)bc * H + j : S.winv);
+    const float cp = hasc ? cpl : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -299,25 +330,6 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     }
     AVC_STAMP(6);
     return;
-  }
-
-  // Epilogue ownership: thread t handles (row, blk) pairs t + NT*i; a pair's 4 float4 columns
-  // blk*16 + 4g (gate g, units 0..3) hold all four gates of 4 hidden units.  Its operands are
-  // fetched now so that their latency overlaps the reduction below.
-  f32x4 gxv[PP][4], wiv[PP][4], cpv[PP];
-#pragma unroll
-  for (int i = 0; i < PP; ++i) {
-    const int pr = min(tid + NT * i, NPAIR - 1), row = pr / NC, blk = pr % NC;
-    const int b = min(rb * 64 + row, B - 1);
-    const int p0 = cb * TW + blk * 16;
-    const float* gxr = S.gx + (long)b * S.ldgx + p0;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      gxv[i][g] = *reinterpret_cast<const f32x4*>(gxr + 4 * g);
-      wiv[i][g] = *reinterpret_cast<const f32x4*>(S.winv + p0 + 4 * g);
-    }
-    cpv[i] = S.c_prev ? *reinterpret_cast<const f32x4*>(S.c_prev + (long)b * H + cb * 4 * NC + blk * 4)
-                      : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
   // wave partials -> LDS; C layout of 16x16: column lane&15, rows 4(lane>>4) + e
@@ -397,6 +409,21 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     }
   }
   AVC_STAMP(5);
+
+  if (S.mode == 1) {
+    // projection slot: the input product of the next layer, scaled and biased, no gate math
+#pragma unroll
+    for (int i = 0; i < PP; ++i) {
+      const int pr = tid + NT * i, row = pr / NC, blk = pr % NC;
+      const int b = rb * 64 + row;
+      if (pr >= NPAIR || b >= B) continue;
+      float* o = S.h_out + (long)b * S.ldh + cb * TW + blk * 16;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4*>(o + 4 * g) = sum[i][g] * wiv[i][g] + gxv[i][g];
+    }
+    AVC_STAMP(6);
+    return;
+  }
 
   // gate epilogue, 4 hidden units per (row, blk) pair
 #pragma unroll
@@ -500,7 +527,8 @@ void launch_split(int NW, int NC, dim3 grid, const SplitArgs& a, hipStream_t s) 
 #endif
   hipEvent_t ev = timing_begin(TC_LSTM_STEP_FWD, s);
   // every active slot uses the same per-wave K range (choose_kslices keeps kslice/NW equal)
-  const int nch = a.s[a.nblk0 > 0 ? 0 : 1].kslice / NW / 32;
+  const int first = a.nb[0] > 0 ? 0 : (a.nb[1] > 0 ? 1 : 2);
+  const int nch = a.s[first].kslice / NW / 32;
 #define AVC_SPLIT_LAUNCH(NWV, NCV)                                                                \
   switch (nch) {                                                                                  \
     case 1: lstm_split_step_kernel<NWV, 1, NCV><<<grid, NWV * 64, lds, s>>>(a); break;            \
@@ -516,8 +544,8 @@ void launch_split(int NW, int NC, dim3 grid, const SplitArgs& a, hipStream_t s) 
 #undef AVC_SPLIT_LAUNCH
   if (ev) {
     double flops = 0.0, bytes = 0.0;
-    const int nslots = a.nblk0 < (int)grid.x ? 2 : 1;
-    for (int L = (a.nblk0 == 0 ? 1 : 0); L < nslots; ++L) {
+    for (int L = 0; L < 3; ++L) {
+      if (a.nb[L] == 0) continue;
       const SplitSlot& S = a.s[L];
       const double kk = (S.A ? S.K0 : 0) + (S.A1 ? S.K - S.K0 : 0);
       flops += 2.0 * a.B * kk * 4.0 * a.H;
@@ -549,12 +577,12 @@ size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
   size_t s = al(TB * 4 * H * f);                                  // gx
   s += al((size_t)4 * H * din * f) + 2 * al((size_t)4 * H * f);  // permuted W_ih, biases
   s += al((size_t)4 * H * H * 2 * 2) + al((size_t)4 * H * f);    // split W_hh + winv
-  if (nlayers == 2) s += al((size_t)4 * H * 2 * H * 2 * 2) + 2 * al((size_t)4 * H * f);
+  if (nlayers == 2) s += 2 * al((size_t)4 * H * H * 2 * 2) + 3 * al((size_t)4 * H * f) + al((size_t)2 * B * 4 * H * f);
   const size_t Bp = (size_t)(B + 15) / 16 * 16;
   s += (size_t)nlayers * (2 * al(Bp * H * 2 * 2) + 2 * al((size_t)B * H * f));  // h splits, c
   // slabs: at most K/128 splits of every 64-column tile, per slot
-  s += (size_t)nlayers * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
-  s += al((size_t)(T + 2) * 2 * nrb * (4 * H / 64) * sizeof(int));
+  s += (size_t)(nlayers + 1) * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
+  s += al((size_t)(T + 2) * 3 * nrb * (4 * H / 64) * sizeof(int));
   GemmDesc d;
   d.M = (int)TB; d.N = 4 * H; d.Kc = din; d.prec16 = 1;
   return s + gemm_scratch_bytes(d) + 4096;
@@ -624,7 +652,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
     const int t = reverse ? T - 1 - st : st;
     const int tp = reverse ? t + 1 : t - 1;
     SplitArgs a{};
-    a.B = B; a.H = H; a.nblk0 = (int)grid.x;
+    a.B = B; a.H = H; a.nb[0] = (int)grid.x;
     SplitSlot& S = a.s[0];
     S.K = H; S.K0 = H; S.kslice = ksl[0]; S.nks = nks; S.ncb = ncb;
     S.A = st > 0 ? reinterpret_cast<const unsigned char*>(hs + (long)((st - 1) & 1) * hsz) : nullptr;
@@ -655,31 +683,39 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   return AVC_OK;
 }
 
-// Two stacked layers as a wavefront (lstm.hip: lstm2_forward_impl's contract): launch st runs
-// layer 0 at t = st and layer 1 at t = st-1; layer 1's input projection is folded into its
-// recurrent product over [h0_t | h1_{t-1}] . [W_ih1 | W_hh1]^T.
+// Two stacked layers as a three-slot wavefront (lstm.hip: lstm2_forward_impl's contract).  Launch
+// st runs, side by side,
+//   slot 0: layer 0 at t = st            (h0_{st-1} . W_hh0^T + Gx0[st]),
+//   slot 1: layer 1's input product for t = st-1:  Gx1 = h0_{st-1} . W_ih1^T + b_ih1 + b_hh1,
+//   slot 2: layer 1 at t = st-2          (h1_{st-3} . W_hh1^T + Gx1[st-2]),
+// so 2T recurrent steps take T+2 launches and every slot reduces K = H inside one workgroup
+// (no cross-workgroup slab hand-off).
 int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                              const float* const* w0, const float* const* w1, float* y0, float* y1,
                              float* g0, float* c0, float* g1, float* c1, hipStream_t s) {
-  AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm2 split path: H must be a multiple of 32, >= 64");
+  AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm2 split path: H must be a multiple of 64");
   Scratch sc(ctx);
   const long TB = (long)T * B;
-  const int NC = 4;  // the pair always splits K (narrow tiles would re-read h 4x more)
+  const int NC = 4;
   const int nrb = (B + 63) / 64, ncb = 4 * H / (16 * NC);
   AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
   AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
   AVC_TAKE(b0_p, float, (size_t)4 * H, sc);
   AVC_TAKE(b1_p, float, (size_t)4 * H, sc);
   AVC_TAKE(w0_s, _Float16, (size_t)4 * H * H * 2, sc);
-  AVC_TAKE(w1_s, _Float16, (size_t)4 * H * 2 * H * 2, sc);
+  AVC_TAKE(w1i_s, _Float16, (size_t)4 * H * H * 2, sc);
+  AVC_TAKE(w1h_s, _Float16, (size_t)4 * H * H * 2, sc);
   AVC_TAKE(winv0, float, (size_t)4 * H, sc);
-  AVC_TAKE(winv1, float, (size_t)4 * H, sc);
+  AVC_TAKE(winv1i, float, (size_t)4 * H, sc);
+  AVC_TAKE(winv1h, float, (size_t)4 * H, sc);
+  AVC_TAKE(gx1, float, (size_t)2 * B * 4 * H, sc);
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2;  // halves per split-h buffer
   AVC_TAKE(hs0, _Float16, (size_t)2 * hsz, sc);
   AVC_TAKE(hs1, _Float16, (size_t)2 * hsz, sc);
   split_rows_kernel<<<4 * H, 256, 0, s>>>(w0[1], H, nullptr, 0, H, 1, w0_s, winv0);
-  split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[0], H, w1[1], H, H, 1, w1_s, winv1);
+  split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[0], H, nullptr, 0, H, 1, w1i_s, winv1i);
+  split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[1], H, nullptr, 0, H, 1, w1h_s, winv1h);
   perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w0[2], w0[3], b0_p, H);
   perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w1[2], w1[3], b1_p, H);
   AVC_LAUNCH_CHECK();
@@ -700,79 +736,97 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
     cpp1 = tmp + 2L * B * H;
   }
   const int NW = pick_nw(H);
-  int K[2] = {H, 2 * H}, nc[2] = {ncb, ncb}, ksl[2];
-  choose_kslices(2, K, nc, nrb, NW, ksl);
-  AVC_CHECK_ARG(H % (ksl[1] / NW) == 0, "lstm2 split path: a wave's K range must not straddle h0|h1");
-  const int nks0 = H / ksl[0], nks1 = 2 * H / ksl[1];
-  AVC_TAKE(slab0, float, (size_t)nrb * ncb * nks0 * 1024 * NC, sc);
-  AVC_TAKE(slab1, float, (size_t)nrb * ncb * nks1 * 1024 * NC, sc);
-  const long cstride = 2L * nrb * ncb;
-  AVC_TAKE(cnt, int, (size_t)(T + 1) * cstride, sc);
-  AVC_HIP(hipMemsetAsync(cnt, 0, sizeof(int) * (T + 1) * cstride, s));
-  auto hs0p = [&](int t) { return reinterpret_cast<const unsigned char*>(hs0 + (long)(t & 1) * hsz); };
-  auto hs1p = [&](int t) { return reinterpret_cast<const unsigned char*>(hs1 + (long)(t & 1) * hsz); };
-
-  for (int st = 0; st <= T; ++st) {
-    const bool l0 = st < T, l1 = st >= 1;
-    const int t0 = st, t1 = st - 1;
+  int K[1] = {H}, nc[1] = {3 * ncb}, ksl[1];
+  choose_kslices(1, K, nc, nrb, NW, ksl);
+  const int nks = H / ksl[0];
+  float* slab[3] = {nullptr, nullptr, nullptr};
+  int* cnt = nullptr;
+  const long cstride = 3L * nrb * ncb;
+  if (nks > 1) {
+    for (int L = 0; L < 3; ++L) {
+      AVC_TAKE(sl, float, (size_t)nrb * ncb * nks * 1024 * NC, sc);
+      slab[L] = sl;
+    }
+    AVC_TAKE(ct, int, (size_t)(T + 2) * cstride, sc);
+    AVC_HIP(hipMemsetAsync(ct, 0, sizeof(int) * (T + 2) * cstride, s));
+    cnt = ct;
+  }
+  auto hs0p = [&](int t) { return hs0 + (long)(t & 1) * hsz; };
+  auto hs1p = [&](int t) { return hs1 + (long)(t & 1) * hsz; };
+  auto fill = [&](SplitSlot& S, int L, int st) {
+    S.K = H; S.K0 = H; S.kslice = ksl[0]; S.nks = nks; S.ncb = ncb;
+    S.lda = H / 32; S.ntile = ntile; S.ldw = H / 32; S.ldhs = H / 32;
+    S.slab = slab[L];
+    S.cnt = cnt ? cnt + (long)st * cstride + (long)L * nrb * ncb : nullptr;
+  };
+  const int nbl = ncb * nks;
+  for (int st = 0; st <= T + 1; ++st) {
     SplitArgs a{};
     a.B = B; a.H = H;
-    SplitSlot& S0 = a.s[0];
-    S0.K = H; S0.K0 = H; S0.kslice = ksl[0]; S0.nks = nks0; S0.ncb = ncb;
-    S0.A = (l0 && t0 > 0) ? hs0p(t0 - 1) : nullptr;
-    S0.lda = H / 32;
-    S0.ntile = ntile;
-    S0.W = reinterpret_cast<const unsigned char*>(w0_s);
-    S0.ldw = H / 32;
-    S0.winv = winv0;
-    S0.gx = gx + (long)(l0 ? t0 : 0) * B * 4 * H;
-    S0.ldgx = 4L * H;
-    if (c0) {
-      S0.c_prev = (l0 && t0 > 0) ? c0 + (long)(t0 - 1) * B * H : nullptr;
-      S0.c_out = c0 + (long)(l0 ? t0 : 0) * B * H;
-    } else {
-      S0.c_prev = (l0 && t0 > 0) ? cpp0 + (long)((t0 - 1) & 1) * B * H : nullptr;
-      S0.c_out = cpp0 + (long)(t0 & 1) * B * H;
+    // slot 0: layer 0 at t0 = st
+    const int t0 = st;
+    if (t0 < T) {
+      SplitSlot& S = a.s[0];
+      fill(S, 0, st);
+      S.mode = 0;
+      S.A = t0 > 0 ? reinterpret_cast<const unsigned char*>(hs0p(t0 - 1)) : nullptr;
+      S.W = reinterpret_cast<const unsigned char*>(w0_s);
+      S.winv = winv0;
+      S.gx = gx + (long)t0 * B * 4 * H;
+      S.ldgx = 4L * H;
+      if (c0) {
+        S.c_prev = t0 > 0 ? c0 + (long)(t0 - 1) * B * H : nullptr;
+        S.c_out = c0 + (long)t0 * B * H;
+      } else {
+        S.c_prev = t0 > 0 ? cpp0 + (long)((t0 - 1) & 1) * B * H : nullptr;
+        S.c_out = cpp0 + (long)(t0 & 1) * B * H;
+      }
+      S.h_out = y0 + (long)t0 * B * H;
+      S.ldh = H;
+      S.hs_out = hs0p(t0);
+      S.gates_out = g0 ? g0 + (long)t0 * B * 4 * H : nullptr;
+      a.nb[0] = nbl;
     }
-    S0.h_out = y0 + (long)(l0 ? t0 : 0) * B * H;
-    S0.ldh = H;
-    S0.hs_out = l0 ? const_cast<_Float16*>(reinterpret_cast<const _Float16*>(hs0p(t0))) : nullptr;
-    S0.ldhs = H / 32;
-    S0.gates_out = g0 ? g0 + (long)(l0 ? t0 : 0) * B * 4 * H : nullptr;
-    S0.slab = slab0;
-    S0.cnt = cnt + (long)st * cstride;
-
-    SplitSlot& S1 = a.s[1];
-    S1.K = 2 * H; S1.K0 = H; S1.kslice = ksl[1]; S1.nks = nks1; S1.ncb = ncb;
-    S1.A = l1 ? hs0p(t1) : nullptr;
-    S1.lda = H / 32;
-    S1.A1 = (l1 && t1 > 0) ? hs1p(t1 - 1) : nullptr;
-    S1.lda1 = H / 32;
-    S1.ntile = ntile;
-    S1.W = reinterpret_cast<const unsigned char*>(w1_s);
-    S1.ldw = 2 * H / 32;
-    S1.winv = winv1;
-    S1.gx = b1_p;
-    S1.ldgx = 0;
-    const int tt1 = l1 ? t1 : 0;
-    if (c1) {
-      S1.c_prev = (l1 && t1 > 0) ? c1 + (long)(t1 - 1) * B * H : nullptr;
-      S1.c_out = c1 + (long)tt1 * B * H;
-    } else {
-      S1.c_prev = (l1 && t1 > 0) ? cpp1 + (long)((t1 - 1) & 1) * B * H : nullptr;
-      S1.c_out = cpp1 + (long)(tt1 & 1) * B * H;
+    // slot 1: layer-1 input product for tp = st - 1
+    const int tp = st - 1;
+    if (tp >= 0 && tp < T) {
+      SplitSlot& S = a.s[1];
+      fill(S, 1, st);
+      S.mode = 1;
+      S.A = reinterpret_cast<const unsigned char*>(hs0p(tp));
+      S.W = reinterpret_cast<const unsigned char*>(w1i_s);
+      S.winv = winv1i;
+      S.gx = b1_p;
+      S.ldgx = 0;
+      S.h_out = gx1 + (long)(tp & 1) * B * 4 * H;
+      S.ldh = 4L * H;
+      a.nb[1] = nbl;
     }
-    S1.h_out = y1 + (long)tt1 * B * H;
-    S1.ldh = H;
-    S1.hs_out = (l1 && t1 < T - 1) ? const_cast<_Float16*>(reinterpret_cast<const _Float16*>(hs1p(t1))) : nullptr;
-    S1.ldhs = H / 32;
-    S1.gates_out = g1 ? g1 + (long)tt1 * B * 4 * H : nullptr;
-    S1.slab = slab1;
-    S1.cnt = cnt + (long)st * cstride + (long)nrb * ncb;
-
-    const int nb0 = l0 ? ncb * nks0 : 0, nb1 = l1 ? ncb * nks1 : 0;
-    a.nblk0 = nb0;
-    launch_split(NW, NC, dim3(nb0 + nb1, nrb), a, s);
+    // slot 2: layer 1 at t1 = st - 2
+    const int t1 = st - 2;
+    if (t1 >= 0 && t1 < T) {
+      SplitSlot& S = a.s[2];
+      fill(S, 2, st);
+      S.mode = 0;
+      S.A = t1 > 0 ? reinterpret_cast<const unsigned char*>(hs1p(t1 - 1)) : nullptr;
+      S.W = reinterpret_cast<const unsigned char*>(w1h_s);
+      S.winv = winv1h;
+      S.gx = gx1 + (long)(t1 & 1) * B * 4 * H;
+      S.ldgx = 4L * H;
+      if (c1) {
+        S.c_prev = t1 > 0 ? c1 + (long)(t1 - 1) * B * H : nullptr;
+        S.c_out = c1 + (long)t1 * B * H;
+      } else {
+        S.c_prev = t1 > 0 ? cpp1 + (long)((t1 - 1) & 1) * B * H : nullptr;
+        S.c_out = cpp1 + (long)(t1 & 1) * B * H;
+      }
+      S.h_out = y1 + (long)t1 * B * H;
+      S.ldh = H;
+      S.hs_out = t1 < T - 1 ? hs1p(t1) : nullptr;
+      S.gates_out = g1 ? g1 + (long)t1 * B * 4 * H : nullptr;
+      a.nb[2] = nbl;
+    }
+    launch_split(NW, NC, dim3(a.nb[0] + a.nb[1] + a.nb[2], nrb), a, s);
   }
   AVC_LAUNCH_CHECK();
   return AVC_OK;
