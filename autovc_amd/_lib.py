@@ -60,6 +60,8 @@ _SIGS = {
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)],
     "avc_generator_param_count": [],
     "avc_generator_forward": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P],
+    "avc_generator_forward_cached": [_P, _I, _I, _P, ctypes.c_long, _P, _P, _P, _I, _P, _P, _P, _P],
+    "avc_prepared_release": [_P],
 }
 _RESTYPES = {"avc_last_error": ctypes.c_char_p}
 

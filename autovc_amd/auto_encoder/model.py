@@ -12,6 +12,7 @@ statistics and updates the running buffers; the reference never calls .eval(), S
 from __future__ import annotations
 
 import ctypes
+import itertools
 import inspect
 import time
 
@@ -27,6 +28,10 @@ from .postnet import Postnet
 
 def _default_device():
     return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+
+_INSTANCES = itertools.count(1)
+_PREP_OWNER = {}  # device -> uid of the model whose derived weights the library holds
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -73,6 +78,7 @@ class FusedAdam(torch.optim.Optimizer):
                   self.exp_avg_sq.data_ptr(), None if ema is None else _lib.ptr(ema), float(g["lr"]),
                   float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), self._step,
                   float(max_norm), float(ema_decay), norm.data_ptr(), _lib.stream(norm.device))
+        m._param_epoch += 1  # parameters changed outside torch's version counters
         self.last_grad_norm = norm
         return loss
 
@@ -112,6 +118,8 @@ class AutoEncoder(nn.Module):
         self._flat_grad = None
         self._flat_slices = []
         self._gen_cache = None
+        self._param_epoch = 0  # bumped by FusedAdam.step (it writes parameters behind torch's back)
+        self._uid = next(_INSTANCES)
 
     # ---- flat parameter storage (one buffer for Adam/EMA/all-reduce) -----------------------
     def _flat_valid(self):
@@ -152,6 +160,13 @@ class AutoEncoder(nn.Module):
         for param in self.parameters():
             param.data.copy_(flattened_params[offset:offset + param.nelement()].view(param.size()))
             offset += param.nelement()
+        self.weights_changed()
+
+    def weights_changed(self):
+        """Tell the fused forward that parameters were written outside torch's version counters
+        (e.g. through `.data` or a raw pointer): its cached derived-weight layouts are rebuilt on
+        the next call.  In-place torch ops, load_state_dict and FusedAdam need no call."""
+        self._param_epoch += 1
 
     # ---- forward ------------------------------------------------------------------------------
     def _bns(self):
@@ -172,12 +187,21 @@ class AutoEncoder(nn.Module):
         tensors = [v for k, v in self.state_dict(keep_vars=True).items()
                    if not k.endswith("num_batches_tracked")]
         key = tuple(t.data_ptr() for t in tensors)
-        if self._gen_cache is None or self._gen_cache[0] != key:
+        dev = tensors[0].device
+        if self._gen_cache is None or self._gen_cache[0] != key or _PREP_OWNER.get(dev) != self._uid:
             for t in tensors:
                 _lib.ptr(t)
+            # the library caches derived weight layouts per context, keyed by parameter pointers:
+            # another model (whose freed storage torch may hand to this one) or moved parameters
+            # must not find stale entries
+            _lib.call("avc_prepared_release", _lib.context(dev))
+            _PREP_OWNER[dev] = self._uid
             arr = (ctypes.c_void_p * len(tensors))(*key)
             self._gen_cache = (key, arr)
-        return self._gen_cache[1]
+        # weights version for the library's derived-layout cache: any in-place change through
+        # torch bumps a tensor's _version; FusedAdam bumps _param_epoch
+        version = (self._param_epoch << 32) + sum(t._version for t in tensors)
+        return self._gen_cache[1], version
 
     def _generator_forward(self, x, c_org, c_trg):
         B, _, T = x.shape
@@ -185,12 +209,12 @@ class AutoEncoder(nn.Module):
         mel = torch.empty((B, 80, T), dtype=torch.float32, device=x.device)
         mel_post = torch.empty_like(mel)
         codes = torch.empty((B, 32 * (T // 32 + (T + 31) // 32)), dtype=torch.float32, device=x.device)
-        params = self._gen_params()
+        params, version = self._gen_params()
         if len(params) != _lib.load().avc_generator_param_count():
             raise RuntimeError("state_dict layout does not match the library's Generator")
-        _lib.call("avc_generator_forward", _lib.context(x.device), T, B, params, _lib.ptr(x),
-                  _lib.ptr(c_org), _lib.ptr(c_trg), int(training), _lib.ptr(mel), _lib.ptr(mel_post),
-                  _lib.ptr(codes), _lib.stream(x.device))
+        _lib.call("avc_generator_forward_cached", _lib.context(x.device), T, B, params, version,
+                  _lib.ptr(x), _lib.ptr(c_org), _lib.ptr(c_trg), int(training), _lib.ptr(mel),
+                  _lib.ptr(mel_post), _lib.ptr(codes), _lib.stream(x.device))
         if training:  # one fused launch for the 11 counters
             torch._foreach_add_([b.num_batches_tracked for b in self._bns()], 1)
         return mel, mel_post, codes

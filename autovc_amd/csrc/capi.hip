@@ -5,6 +5,7 @@
 
 #include "elementwise.h"
 #include "kernels.h"
+#include "timing.h"
 
 namespace avc {
 
@@ -14,6 +15,27 @@ thread_local std::string g_err;
 
 void set_error(const std::string& msg) { g_err = msg; }
 const char* get_error() { return g_err.c_str(); }
+
+void* prep_buffer(avc_context* ctx, int kind, const void* key0, const void* key1, size_t bytes,
+                  bool* fresh) {
+  *fresh = true;
+  if (ctx->prep_version < 0) return nullptr;
+  for (auto& e : ctx->prep) {
+    if (e.kind == kind && e.key0 == key0 && e.key1 == key1 && e.bytes == bytes) {
+      *fresh = e.version != ctx->prep_version;
+      e.version = ctx->prep_version;
+      return e.buf;
+    }
+  }
+  avc_prep_entry e;
+  e.kind = kind; e.key0 = key0; e.key1 = key1; e.bytes = bytes; e.version = ctx->prep_version;
+  if (hipMalloc(&e.buf, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;  // no room: derive into scratch this call
+  }
+  ctx->prep.push_back(e);
+  return e.buf;
+}
 
 int ensure_arena(avc_context* ctx, size_t bytes) {
   if (ctx->cap >= bytes) return AVC_OK;
@@ -140,6 +162,14 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   lin.bias0 = P[P_LIN + 1];
   lin.C = melf; lin.ldc = 80;
   lin.prec16 = 1;
+  if (ctx->prep_version >= 0) {
+    bool fb = true;
+    auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_GEMM_BFRAG, P[P_LIN], nullptr, gemm_bfrag_bytes(lin), &fb));
+    if (bf) {
+      if (fb) AVC_TRY(gemm_prepare_bfrag(lin, bf, s));
+      lin.b_frag = bf;
+    }
+  }
   AVC_TRY(gemm_run(ctx, lin, s));
 
   // Postnet + residual (postnet.py:50-63, model.py:131-132)
@@ -178,6 +208,11 @@ int avc_context_destroy(avc_context* ctx) {
   if (!ctx) return AVC_OK;
   AVC_HIP(hipDeviceSynchronize());
   for (void* p : ctx->retired) (void)hipFree(p);
+  for (auto& e : ctx->prep) (void)hipFree(e.buf);
+  if (ctx->gen.exec) (void)hipGraphExecDestroy(ctx->gen.exec);
+  if (ctx->gen.graph) (void)hipGraphDestroy(ctx->gen.graph);
+  if (ctx->gen.stage) (void)hipFree(ctx->gen.stage);
+  if (ctx->capture_stream) (void)hipStreamDestroy(ctx->capture_stream);
   if (ctx->base) (void)hipFree(ctx->base);
   delete ctx;
   return AVC_OK;
@@ -378,6 +413,123 @@ int avc_generator_forward(avc_context* ctx, int T, int B, const float* const* pa
   AVC_TRY(ensure_arena(ctx, gen_scratch(T, B)));
   return generator_forward(ctx, T, B, params, x, c_org, c_trg, training, mel, mel_post, codes,
                            S(stream));
+}
+
+namespace avc {
+namespace {
+
+void drop_graph(avc_context* ctx) {
+  avc_gen_graph& g = ctx->gen;
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g.exec = nullptr;
+  g.graph = nullptr;
+}
+
+size_t codes_len(int T) { return (size_t)32 * (T / 32 + (T + 31) / 32); }
+
+// Capture the forward on the context's private stream into g (staging buffers as I/O).
+int capture_graph(avc_context* ctx, const float* const* params) {
+  avc_gen_graph& g = ctx->gen;
+  const size_t nx = (size_t)g.B * 80 * g.T, nc = (size_t)g.B * 256, ncode = (size_t)g.B * codes_len(g.T);
+  const size_t need = (3 * nx + 2 * nc + ncode) * sizeof(float);
+  if (g.stage_bytes < need) {
+    if (g.stage) (void)hipFree(g.stage);
+    g.stage = nullptr;
+    g.stage_bytes = 0;
+    AVC_HIP(hipMalloc(&g.stage, need));
+    g.stage_bytes = need;
+  }
+  if (!ctx->capture_stream) AVC_HIP(hipStreamCreateWithFlags(&ctx->capture_stream, hipStreamNonBlocking));
+  float* sx = g.stage;
+  float* so = sx + nx;
+  float* st = so + nc;
+  float* sm = st + nc;
+  float* sp = sm + nx;
+  float* sc = sp + nx;
+  hipStream_t cs = ctx->capture_stream;
+  AVC_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
+  const int rc = generator_forward(ctx, g.T, g.B, params, sx, so, st, g.training, sm, sp, sc, cs);
+  hipGraph_t graph = nullptr;
+  const hipError_t e = hipStreamEndCapture(cs, &graph);
+  if (rc != AVC_OK) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  AVC_HIP(e);
+  g.graph = graph;
+  AVC_HIP(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
+  return AVC_OK;
+}
+
+}  // namespace
+}  // namespace avc
+
+int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* const* params,
+                                 long weights_version, const float* x, const float* c_org,
+                                 const float* c_trg, int training, float* mel, float* mel_post,
+                                 float* codes, void* stream) {
+  AVC_CHECK_ARG(ctx && params && x && c_org && c_trg && mel && mel_post && codes, "NULL pointer");
+  AVC_CHECK_ARG(weights_version >= 0, "weights_version must be >= 0");
+  for (int i = 0; i < P_COUNT; ++i) AVC_CHECK_ARG(params[i] != nullptr, "NULL parameter pointer");
+  AVC_TRY(ensure_arena(ctx, gen_scratch(T, B)));
+  hipStream_t s = S(stream);
+  avc_gen_graph& g = ctx->gen;
+  const bool timing = timing_on(TC_GEMM) || timing_on(TC_LSTM_STEP_FWD) || timing_on(TC_LSTM32);
+  const bool same = g.T == T && g.B == B && g.training == training && g.version == weights_version &&
+                    g.params.size() == (size_t)P_COUNT &&
+                    std::equal(g.params.begin(), g.params.end(), params);
+  ctx->prep_version = weights_version;
+  int rc = AVC_OK;
+  if (same && !timing && (g.exec || g.seen >= 1)) {
+    if (!g.exec) {
+      rc = capture_graph(ctx, params);
+      if (rc != AVC_OK) {
+        drop_graph(ctx);
+        g.seen = -1000000;  // capture failed: stay eager for this key
+        ctx->prep_version = -1;
+        (void)hipGetLastError();
+        return generator_forward(ctx, T, B, params, x, c_org, c_trg, training, mel, mel_post, codes, s);
+      }
+    }
+    const size_t nx = (size_t)B * 80 * T, nc = (size_t)B * 256, ncode = (size_t)B * codes_len(T);
+    float* sx = g.stage;
+    float* so = sx + nx;
+    float* st = so + nc;
+    float* sm = st + nc;
+    float* sp = sm + nx;
+    float* sc = sp + nx;
+    ctx->prep_version = -1;
+    AVC_HIP(hipMemcpyAsync(sx, x, nx * sizeof(float), hipMemcpyDeviceToDevice, s));
+    AVC_HIP(hipMemcpyAsync(so, c_org, nc * sizeof(float), hipMemcpyDeviceToDevice, s));
+    AVC_HIP(hipMemcpyAsync(st, c_trg, nc * sizeof(float), hipMemcpyDeviceToDevice, s));
+    AVC_HIP(hipGraphLaunch(g.exec, s));
+    AVC_HIP(hipMemcpyAsync(mel, sm, nx * sizeof(float), hipMemcpyDeviceToDevice, s));
+    AVC_HIP(hipMemcpyAsync(mel_post, sp, nx * sizeof(float), hipMemcpyDeviceToDevice, s));
+    AVC_HIP(hipMemcpyAsync(codes, sc, ncode * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return AVC_OK;
+  }
+  // eager call; a second consecutive call with the same key captures the graph
+  if (!same) {
+    drop_graph(ctx);
+    g.T = T; g.B = B; g.training = training; g.version = weights_version;
+    g.params.assign(params, params + P_COUNT);
+    g.seen = 0;
+  }
+  rc = generator_forward(ctx, T, B, params, x, c_org, c_trg, training, mel, mel_post, codes, s);
+  ctx->prep_version = -1;
+  if (rc == AVC_OK) ++g.seen;
+  return rc;
+}
+
+int avc_prepared_release(avc_context* ctx) {
+  AVC_CHECK_ARG(ctx != nullptr, "ctx is NULL");
+  AVC_HIP(hipDeviceSynchronize());
+  drop_graph(ctx);
+  ctx->gen = avc_gen_graph();
+  for (auto& e : ctx->prep) (void)hipFree(e.buf);
+  ctx->prep.clear();
+  return AVC_OK;
 }
 
 }  // extern "C"

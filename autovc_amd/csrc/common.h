@@ -62,8 +62,37 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // Device arena owned by a context.  Scratch is handed out stack-like inside one API call
 // (mark/release); every call on a context is stream-ordered on the stream it was given, so a
 // region is never reused while an earlier kernel on that stream could still read it.
+// Derived weight layouts kept across calls (split / permuted / transposed copies of weights),
+// keyed by what they are derived from and valid for one caller-supplied weights version.
+struct avc_prep_entry {
+  int kind = 0;
+  const void* key0 = nullptr;
+  const void* key1 = nullptr;
+  size_t bytes = 0;
+  long version = -1;
+  void* buf = nullptr;
+};
+
+// One captured whole-Generator forward (avc_generator_forward_cached): replayed with a single
+// hipGraphLaunch when the next call has the same shapes, parameters and weights version.  The
+// graph reads/writes fixed staging buffers; the caller's tensors are copied in and out.
+struct avc_gen_graph {
+  int T = 0, B = 0, training = -1;
+  long version = -1;
+  std::vector<const float*> params;
+  int seen = 0;                 // consecutive eager calls with this key
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  float* stage = nullptr;       // x | c_org | c_trg | mel | mel_post | codes
+  size_t stage_bytes = 0;
+};
+
 struct avc_context {
   int device = 0;
+  std::vector<avc_prep_entry> prep;
+  avc_gen_graph gen;
+  hipStream_t capture_stream = nullptr;
+  long prep_version = -1;       // >= 0 while a caching call (avc_generator_forward_cached) runs
   std::vector<void*> retired;   // grown-out blocks, freed at destroy
   char* base = nullptr;
   size_t cap = 0;
@@ -95,6 +124,31 @@ struct Scratch {
 #define AVC_TAKE(var, T, n, scratch)                 \
   T* var = (scratch).template take<T>(n);            \
   if (var == nullptr) return AVC_ERR_WORKSPACE
+
+enum PrepKind : int {
+  PREP_CONV_WT = 1,     // conv W [co][ci][5] -> Wt [5][ci][co] fp32
+  PREP_CONV_BFRAG,      // ... and its split-f16 fragment-major copy
+  PREP_GEMM_BFRAG,      // plain B operand split (key: the fp32 B)
+  PREP_LSTM_WIH,        // permuted W_ih fp32
+  PREP_LSTM_WIH_BFRAG,  // ... split fragment-major for the input GEMM
+  PREP_LSTM_BIAS,       // permuted b_ih + b_hh
+  PREP_LSTM_WHH,        // split-f16 fragment-major W_hh (+ per-row unscale after it)
+};
+
+// Persistent buffer for derived weights, or nullptr when no caching call is active (the caller
+// then derives into scratch as usual).  *fresh: the contents must be (re)computed now.
+void* prep_buffer(avc_context* ctx, int kind, const void* key0, const void* key1, size_t bytes,
+                  bool* fresh);
+
+// Derived-weight buffer: the cached one when a caching call is active, else scratch.
+template <typename T>
+T* prep_or_scratch(avc_context* ctx, Scratch& sc, int kind, const void* key0, const void* key1,
+                   size_t count, bool* fresh) {
+  T* p = static_cast<T*>(prep_buffer(ctx, kind, key0, key1, count * sizeof(T), fresh));
+  if (p) return p;
+  *fresh = true;
+  return sc.template take<T>(count);
+}
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 

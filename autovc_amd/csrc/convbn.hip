@@ -73,10 +73,22 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   AVC_CHECK_ARG(training || (running_mean && running_var), "conv: eval mode needs running stats");
   AVC_CHECK_ARG(!training || (long)T * B > 1, "BatchNorm in training mode needs more than 1 value per channel");
   Scratch sc(ctx);
-  AVC_TAKE(wt, float, 5UL * cin * cout, sc);
-  conv_weight_fwd_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wt, cin, cout);
-  AVC_LAUNCH_CHECK();
+  bool fresh = true;
+  float* wt = prep_or_scratch<float>(ctx, sc, PREP_CONV_WT, weight, nullptr, 5UL * cin * cout, &fresh);
+  if (!wt) return AVC_ERR_WORKSPACE;
+  if (fresh) {
+    conv_weight_fwd_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wt, cin, cout);
+    AVC_LAUNCH_CHECK();
+  }
   GemmDesc g = conv_fwd_desc(T, B, cin, cout, x, wt, bias, y_pre);
+  if (ctx->prep_version >= 0) {  // cache the split-f16 copy of the taps as well
+    bool fb = true;
+    auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_CONV_BFRAG, weight, nullptr, gemm_bfrag_bytes(g), &fb));
+    if (bf) {
+      if (fb) AVC_TRY(gemm_prepare_bfrag(g, bf, s));
+      g.b_frag = bf;
+    }
+  }
   float* stats = nullptr;
   int nparts = 0;
   if (training) {

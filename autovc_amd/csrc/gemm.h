@@ -25,6 +25,7 @@ struct GemmDesc {
   float* C = nullptr; long ldc = 0; long ldc_col = 1; int accumulate = 0;
   const float* bias0 = nullptr; const float* bias1 = nullptr; int act = AVC_ACT_NONE;
   int prec16 = 0;           // 1: split-fp16 ("3xf16") MFMA kernel; forward operands only (|x| < 65504)
+  const _Float16* b_frag = nullptr;  // optional B already split by gemm_prepare_bfrag (prec16 only)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
   int stats_bm = 0;         // filled by gemm_run: rows per stats partial
 };
@@ -35,5 +36,9 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split =
 int gemm_stats_rows(int M, int N);
 // Scratch bytes gemm_run may take for this problem.
 size_t gemm_scratch_bytes(const GemmDesc& d);
+// B operand of a forward (prec16) product split once into the fragment-major layout the
+// split-f16 kernel streams (all taps); pass it back as GemmDesc::b_frag to skip the per-call split.
+size_t gemm_bfrag_bytes(const GemmDesc& d);
+int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream);
 
 }  // namespace avc

@@ -905,6 +905,22 @@ int gemm_stats_rows(int M, int N) {
   return make_plan(d, 1).bm;
 }
 
+size_t gemm_bfrag_bytes(const GemmDesc& d) { return (size_t)d.ntaps * frag_bytes(d.N, d.Kc); }
+
+int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
+  const long b_ntile = frag_ntile(d.N);
+  const int nkc = frag_nkc(d.Kc);
+  const long tapstride = b_ntile * nkc * 1024;  // halves
+  const long tb = b_ntile * 32 * nkc * 2;
+  const long b_rows = d.b_rows ? d.b_rows : (d.b_trans ? d.N : d.Kc);
+  for (int tau = 0; tau < d.ntaps; ++tau)
+    split_frag32_kernel<<<(int)std::min<long>((tb + 255) / 256, 8192), 256, 0, stream>>>(
+        d.B + (long)tau * d.b_tapoff, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N,
+        d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows), (int)b_ntile, nkc, dst + tau * tapstride);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
 size_t gemm_scratch_bytes(const GemmDesc& d) {
   Plan p = make_plan(d, 0);
   size_t s = p.nsplit <= 1 ? 0 : (size_t)p.nsplit * d.nz * d.M * d.N * sizeof(float) + 256;
@@ -940,17 +956,18 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     const int nkc = frag_nkc(d.Kc);
     const long b_ntile = frag_ntile(d.N);
     _Float16* as = sc.take<_Float16>(frag_bytes(d.a_rows, d.Kc) / 2);
-    _Float16* bs = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, d.Kc) / 2);
-    if (!as || !bs) return AVC_ERR_WORKSPACE;
+    if (!as) return AVC_ERR_WORKSPACE;
     const long ta = a_ntile * 32 * nkc * 2;
     split_frag32_kernel<<<(int)std::min<long>((ta + 255) / 256, 8192), 256, 0, stream>>>(
         d.A, d.lda, 1, (int)d.a_rows, d.Kc, (int)a_ntile, nkc, as);
     const long tapstride = b_ntile * nkc * 1024;  // halves
-    const long tb = b_ntile * 32 * nkc * 2;
-    for (int tau = 0; tau < d.ntaps; ++tau)
-      split_frag32_kernel<<<(int)std::min<long>((tb + 255) / 256, 8192), 256, 0, stream>>>(
-          d.B + (long)tau * d.b_tapoff, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N,
-          d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, d.b_rows), (int)b_ntile, nkc, bs + tau * tapstride);
+    const _Float16* bs = d.b_frag;
+    if (!bs) {
+      _Float16* tmp = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, d.Kc) / 2);
+      if (!tmp) return AVC_ERR_WORKSPACE;
+      AVC_TRY(gemm_prepare_bfrag(d, tmp, stream));
+      bs = tmp;
+    }
     AVC_LAUNCH_CHECK();
     fa.As = as; fa.a_ntile = (int)a_ntile; fa.a_nkc = nkc;
     fa.a_shift0 = d.a_shift0; fa.a_tapshift = d.a_tapshift;

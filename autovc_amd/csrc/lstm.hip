@@ -699,6 +699,14 @@ int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const fl
     g.b_trans = 1; g.ldb = din; g.B = w[0]; g.bias0 = w[2]; g.bias1 = w[3];
     g.C = gx + dir * 128; g.ldc = 256;
     g.prec16 = 1;
+    if (ctx->prep_version >= 0) {
+      bool fb = true;
+      auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_GEMM_BFRAG, w[0], nullptr, gemm_bfrag_bytes(g), &fb));
+      if (bf) {
+        if (fb) AVC_TRY(gemm_prepare_bfrag(g, bf, s));
+        g.b_frag = bf;
+      }
+    }
     AVC_TRY(gemm_run(ctx, g, s));
   }
   hipEvent_t ev = timing_begin(TC_LSTM32, s);

@@ -568,6 +568,18 @@ inline size_t al(size_t b) { return (b + 255) & ~size_t(255); }
 
 }  // namespace
 
+// Cached split-f16 copy of a (permuted) input-projection weight for the gemm16f path, rebuilt
+// when the weight itself was rebuilt this call.
+int attach_bfrag(avc_context* ctx, GemmDesc& g, const void* key, bool rebuilt, hipStream_t s) {
+  if (ctx->prep_version < 0) return AVC_OK;
+  bool fb = true;
+  auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_LSTM_WIH_BFRAG, key, nullptr, gemm_bfrag_bytes(g), &fb));
+  if (!bf) return AVC_OK;
+  if (fb || rebuilt) AVC_TRY(gemm_prepare_bfrag(g, bf, s));
+  g.b_frag = bf;
+  return AVC_OK;
+}
+
 bool lstm_split_supported(int H, int din) { return H % 64 == 0 && din % 4 == 0; }
 
 size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
@@ -598,10 +610,14 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   const long TB = (long)T * B;
   const int nrb = (B + 63) / 64;
   AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
-  AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
-  AVC_TAKE(b_p, float, (size_t)4 * H, sc);
-  AVC_TAKE(whh_s, _Float16, (size_t)4 * H * H * 2, sc);
-  AVC_TAKE(winv, float, (size_t)4 * H, sc);
+  bool f_wih, f_b, f_whh;
+  float* wih_p = prep_or_scratch<float>(ctx, sc, PREP_LSTM_WIH, w_ih, nullptr, (size_t)4 * H * din, &f_wih);
+  float* b_p = prep_or_scratch<float>(ctx, sc, PREP_LSTM_BIAS, b_ih, b_hh, (size_t)4 * H, &f_b);
+  // split W_hh (fragment-major, 4H*H*2 halves) followed by its per-row unscale (4H floats)
+  _Float16* whh_s = prep_or_scratch<_Float16>(ctx, sc, PREP_LSTM_WHH, w_hh, nullptr,
+                                              (size_t)4 * H * H * 2 + 8 * H, &f_whh);
+  if (!wih_p || !b_p || !whh_s) return AVC_ERR_WORKSPACE;
+  float* winv = reinterpret_cast<float*>(whh_s + (size_t)4 * H * H * 2);
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2;  // halves per split-h buffer
   AVC_TAKE(hs, _Float16, (size_t)2 * hsz, sc);
@@ -612,16 +628,17 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   }
   // W_ih is consumed by the fp32 GEMM in permuted row order: reuse the split kernel's permutation
   // through a plain gather (lstm.hip's permute_rows_kernel lives in that translation unit).
-  split_rows_kernel<<<4 * H, 256, 0, s>>>(w_hh, H, nullptr, 0, H, 1, whh_s, winv);
-  perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(b_ih, b_hh, b_p, H);
+  if (f_whh) split_rows_kernel<<<4 * H, 256, 0, s>>>(w_hh, H, nullptr, 0, H, 1, whh_s, winv);
+  if (f_b) perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(b_ih, b_hh, b_p, H);
   AVC_LAUNCH_CHECK();
-  AVC_TRY(permute_rows(w_ih, wih_p, H, din, s));
+  if (f_wih) AVC_TRY(permute_rows(w_ih, wih_p, H, din, s));
   GemmDesc g;
   g.M = (int)TB; g.N = 4 * H; g.Kc = din;
   g.A = x; g.lda = ldx; g.a_rows = TB;
   g.b_trans = 1; g.ldb = din; g.B = wih_p; g.bias0 = b_p;
   g.C = gx; g.ldc = 4 * H;
   g.prec16 = 1;
+  AVC_TRY(attach_bfrag(ctx, g, w_ih, f_wih, s));
   AVC_TRY(gemm_run(ctx, g, s));
 
   const int NW = pick_nw(H);
@@ -699,33 +716,37 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   const int NC = 4;
   const int nrb = (B + 63) / 64, ncb = 4 * H / (16 * NC);
   AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
-  AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
-  AVC_TAKE(b0_p, float, (size_t)4 * H, sc);
-  AVC_TAKE(b1_p, float, (size_t)4 * H, sc);
-  AVC_TAKE(w0_s, _Float16, (size_t)4 * H * H * 2, sc);
-  AVC_TAKE(w1i_s, _Float16, (size_t)4 * H * H * 2, sc);
-  AVC_TAKE(w1h_s, _Float16, (size_t)4 * H * H * 2, sc);
-  AVC_TAKE(winv0, float, (size_t)4 * H, sc);
-  AVC_TAKE(winv1i, float, (size_t)4 * H, sc);
-  AVC_TAKE(winv1h, float, (size_t)4 * H, sc);
+  bool f_wih, f_b0, f_b1, f_w0, f_w1i, f_w1h;
+  float* wih_p = prep_or_scratch<float>(ctx, sc, PREP_LSTM_WIH, w0[0], nullptr, (size_t)4 * H * din, &f_wih);
+  float* b0_p = prep_or_scratch<float>(ctx, sc, PREP_LSTM_BIAS, w0[2], w0[3], (size_t)4 * H, &f_b0);
+  float* b1_p = prep_or_scratch<float>(ctx, sc, PREP_LSTM_BIAS, w1[2], w1[3], (size_t)4 * H, &f_b1);
+  const size_t wsz = (size_t)4 * H * H * 2 + 8 * H;  // split weights + per-row unscale
+  _Float16* w0_s = prep_or_scratch<_Float16>(ctx, sc, PREP_LSTM_WHH, w0[1], nullptr, wsz, &f_w0);
+  _Float16* w1i_s = prep_or_scratch<_Float16>(ctx, sc, PREP_LSTM_WHH, w1[0], nullptr, wsz, &f_w1i);
+  _Float16* w1h_s = prep_or_scratch<_Float16>(ctx, sc, PREP_LSTM_WHH, w1[1], nullptr, wsz, &f_w1h);
+  if (!wih_p || !b0_p || !b1_p || !w0_s || !w1i_s || !w1h_s) return AVC_ERR_WORKSPACE;
+  float* winv0 = reinterpret_cast<float*>(w0_s + (size_t)4 * H * H * 2);
+  float* winv1i = reinterpret_cast<float*>(w1i_s + (size_t)4 * H * H * 2);
+  float* winv1h = reinterpret_cast<float*>(w1h_s + (size_t)4 * H * H * 2);
   AVC_TAKE(gx1, float, (size_t)2 * B * 4 * H, sc);
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2;  // halves per split-h buffer
   AVC_TAKE(hs0, _Float16, (size_t)2 * hsz, sc);
   AVC_TAKE(hs1, _Float16, (size_t)2 * hsz, sc);
-  split_rows_kernel<<<4 * H, 256, 0, s>>>(w0[1], H, nullptr, 0, H, 1, w0_s, winv0);
-  split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[0], H, nullptr, 0, H, 1, w1i_s, winv1i);
-  split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[1], H, nullptr, 0, H, 1, w1h_s, winv1h);
-  perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w0[2], w0[3], b0_p, H);
-  perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w1[2], w1[3], b1_p, H);
+  if (f_w0) split_rows_kernel<<<4 * H, 256, 0, s>>>(w0[1], H, nullptr, 0, H, 1, w0_s, winv0);
+  if (f_w1i) split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[0], H, nullptr, 0, H, 1, w1i_s, winv1i);
+  if (f_w1h) split_rows_kernel<<<4 * H, 256, 0, s>>>(w1[1], H, nullptr, 0, H, 1, w1h_s, winv1h);
+  if (f_b0) perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w0[2], w0[3], b0_p, H);
+  if (f_b1) perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w1[2], w1[3], b1_p, H);
   AVC_LAUNCH_CHECK();
-  AVC_TRY(permute_rows(w0[0], wih_p, H, din, s));
+  if (f_wih) AVC_TRY(permute_rows(w0[0], wih_p, H, din, s));
   GemmDesc g;
   g.M = (int)TB; g.N = 4 * H; g.Kc = din;
   g.A = x; g.lda = ldx; g.a_rows = TB;
   g.b_trans = 1; g.ldb = din; g.B = wih_p; g.bias0 = b0_p;
   g.C = gx; g.ldc = 4 * H;
   g.prec16 = 1;
+  AVC_TRY(attach_bfrag(ctx, g, w0[0], f_wih, s));
   AVC_TRY(gemm_run(ctx, g, s));
 
   float* cpp0 = nullptr;

@@ -186,6 +186,20 @@ int avc_generator_forward(avc_context* ctx, int T, int B, const float* const* pa
                           const float* x, const float* c_org, const float* c_trg, int training,
                           float* mel, float* mel_post, float* codes, void* stream);
 
+/* Same as avc_generator_forward, but the derived weight layouts (split-f16 fragment-major
+ * copies, permuted LSTM gate rows, conv tap transposes) are kept in the context between calls
+ * and rebuilt only when `weights_version` differs from the last call's (or a parameter pointer
+ * changed).  The caller bumps the version whenever any weight changes (the Python drop-in
+ * derives it from the parameters' in-place version counters and its optimizer's step count).
+ * Replaces the reference's convert() hot loop (voice_converter.py:163-175) for repeated calls
+ * on fixed weights. */
+int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* const* params,
+                                 long weights_version, const float* x, const float* c_org,
+                                 const float* c_trg, int training, float* mel, float* mel_post,
+                                 float* codes, void* stream);
+/* Frees every cached derived-weight buffer of the context. */
+int avc_prepared_release(avc_context* ctx);
+
 /* ---- measurement (bench.py) ---------------------------------------------------------------
  * When bit `cls` of mask is set, every launch of that kernel class is bracketed by HIP events on
  * its stream; avc_timing_read sums the event-measured durations and the algorithmic FLOPs/bytes

@@ -167,3 +167,41 @@ def test_gradients_match_oracle(cuda_device):
         worst = max(worst, rel)
         assert rel < 1e-4, f"{k}: relative gradient error {rel:.2e}"
     print(f"worst relative gradient error over parameters: {worst:.2e}")
+
+
+@pytest.mark.gpu
+def test_fused_forward_sees_weight_updates(cuda_device):
+    """The fused forward caches derived weight layouts across calls; every way the drop-in
+    changes weights must invalidate them (in-place torch op, load_state_dict, optimizer step,
+    load_flattened_params)."""
+    torch.manual_seed(0)
+    m = AutoEncoder(device=cuda_device, verbose=False).to(cuda_device)
+    m.load_state_dict(torch_state_dict(3))
+    m.eval()
+    x = torch.rand(2, 80, 64, device=cuda_device)
+    c = torch.rand(2, 256, device=cuda_device)
+
+    def fwd():
+        with torch.no_grad():
+            return m(x, c, c)[1].clone()
+
+    def ref():
+        m._param_epoch += 1_000_000  # force a rebuild: the uncached answer for the current weights
+        return fwd()
+
+    y0 = fwd()
+    assert torch.equal(y0, fwd())  # cached second call: identical
+    with torch.no_grad():
+        m.decoder.lstm2.weight_hh_l0.mul_(0.9)          # in-place torch op
+    y1 = fwd()
+    assert not torch.equal(y1, y0) and torch.equal(y1, ref())
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd["postnet.convolutions.0.0.conv.weight"] *= 1.1
+    m.load_state_dict(sd)                                 # load_state_dict
+    y2 = fwd()
+    assert not torch.equal(y2, y1) and torch.equal(y2, ref())
+    flat = m.flatten_params().clone()
+    flat[:1000] *= 0.5
+    m.load_flattened_params(flat)                         # .data copies
+    y3 = fwd()
+    assert not torch.equal(y3, y2) and torch.equal(y3, ref())
