@@ -549,7 +549,14 @@ void launch_split(int NW, int NC, dim3 grid, const SplitArgs& a, hipStream_t s) 
       const SplitSlot& S = a.s[L];
       const double kk = (S.A ? S.K0 : 0) + (S.A1 ? S.K - S.K0 : 0);
       flops += 2.0 * a.B * kk * 4.0 * a.H;
-      bytes += 4.0 * 4.0 * (double)a.H * S.K;  // split weights: 4 B per element
+      // algorithmic bytes: split weights (4 B per element), the split h operand once, the input
+      // projection rows, and the fp32 c/h state + split h written (or the projection output)
+      bytes += 4.0 * 4.0 * (double)a.H * S.K + 4.0 * a.B * kk;
+      if (S.mode == 1) {
+        bytes += 4.0 * a.B * 4.0 * a.H;
+      } else {
+        bytes += (S.ldgx ? 4.0 * a.B * 4.0 * a.H : 0.0) + 4.0 * a.B * a.H * ((S.c_prev ? 1 : 0) + 3);
+      }
     }
     timing_end(TC_LSTM_STEP_FWD, ev, s, flops, bytes);
   }

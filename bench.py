@@ -29,7 +29,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 PEAK_FP32_MATRIX_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_*_f32, dense
+PEAK_F16_MATRIX_TFLOPS = 2500.0   # dense f16/bf16 MFMA
 PEAK_HBM_GBS = 8000.0
+# Roofline of each timed kernel class.  Forward contractions run as 3 f16 MFMA products per
+# fp32 product, so their fp32-equivalent MFMA ceiling is 2500/3 TFLOP/s; the LSTM step streams
+# its (split) weights every time step and is priced against HBM; backward products are fp32.
+ROOFLINE = {
+    "fwd": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
+            "lstm32": ("hbm", PEAK_HBM_GBS)},
+    "train": {"gemm": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
+              "lstm_step_bwd": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm32": ("hbm", PEAK_HBM_GBS)},
+}
 METRIC = "mel-frames/sec/GPU AutoVC fwd, 80×128 batch; max|Δmel| vs ref"
 
 
@@ -164,13 +174,20 @@ def main():
         dom = max(kern, key=lambda c: per[c]["ms"]) if kern else None
         if dom:
             r = per[dom]
-            achieved = r["flops"] / (r["ms"] * 1e-3) / 1e12
+            bound, peak = ROOFLINE[args.mode][dom]
+            if bound == "hbm":
+                achieved = r["bytes"] / (r["ms"] * 1e-3) / 1e9
+                unit = "GB/s"
+            else:
+                achieved = r["flops"] / (r["ms"] * 1e-3) / 1e12
+                unit = "TFLOP/s" + (" (fp32-equivalent, 3 f16 products each)" if peak < 1000 and peak > 500 else "")
             result["roofline"] = {
-                "kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_MATRIX_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MATRIX_TFLOPS, 4),
+                "kernel": dom, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
+                "unit": unit, "frac": round(achieved / peak, 4),
                 "traffic": None,
                 "avg_launch_us": kern[dom]["avg_us"],
                 "flop_per_launch": round(r["flops"] / r["launches"]),
+                "algorithmic_bytes_per_launch": round(r["bytes"] / r["launches"]),
             }
             tr = pmc_traffic(dom, args)
             if tr:
