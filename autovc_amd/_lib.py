@@ -53,8 +53,9 @@ _SIGS = {
     "avc_clip_adam_ema": [_P, _Z, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, ctypes.c_double, _P, _P],
     "avc_timing_enable": [_I],
     "avc_lstm_tune": [_I, _I],
-    "avc_lstm_split_tune": [_I, _I],
+    "avc_lstm_split_tune": [_I, _I, _I],
     "avc_gemm_tune": [_I],
+    "avc_gemm_stages": [_I],
     "avc_timing_reset": [],
     "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)],

@@ -577,7 +577,7 @@ struct Frag16Args {
   const _Float16* Bs; int b_ntile, b_nkc; long b_tapstride;            // halves per tap
 };
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NS>
 __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag16Args f, int tilesM,
                                                                int tilesN, int kt_per_tap, int kps,
                                                                int nsplit, float* __restrict__ slab) {
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
   static_assert(NBLK % NWAVE == 0, "blocks per K-tile must split evenly over the waves");
   constexpr int DPW = NBLK / NWAVE;  // LDS-DMA instructions per wave per K-tile
   constexpr int STAGE = NBLK * 1024;
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // 3 stages
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // NS stages
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -619,9 +619,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
   {                                                                                               \
     const int tau = (KT) / kt_per_tap;                                                            \
     const int kc0 = ((KT) - tau * kt_per_tap) * 2;                                                \
+    unsigned char* const stage_base = lds + (ST) * STAGE;                                         \
     _Pragma("unroll") for (int i = 0; i < DPW; ++i) {                                             \
       const int b = w * DPW + i;                                                                  \
-      unsigned char* dst = lds + (ST) * STAGE + b * 1024;                                         \
+      unsigned char* dst = stage_base + b * 1024;                                                 \
       if (b < ABLK) {                                                                             \
         const int rt = b >> 2, kc = (b >> 1) & 1, hl = b & 1;                                     \
         const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)tau * a_tapshift) / 32; \
@@ -652,18 +653,25 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
     for (int j = 0; j < TN; ++j) acc[i][j] = cmp[i][j] = part[i][j] = crs[i][j] = zero16;
 
   constexpr int KB = 4;  // K-tiles (128 k) per compensated partial
-  if (kt0 < kt1) AVC16F_ISSUE(kt0, 0);
-  if (kt0 + 1 < kt1) AVC16F_ISSUE(kt0 + 1, 1);
+  // NS-stage ring: NS-1 K-tiles in flight ahead of the one being consumed
+#pragma unroll
+  for (int pre = 0; pre < NS - 1; ++pre)  // (not `i`: the macro's own loop variable)
+    if (kt0 + pre < kt1) AVC16F_ISSUE(kt0 + pre, pre);
   for (int kt = kt0; kt < kt1; ++kt) {
-    const int st = (kt - kt0) % 3;
-    // this wave's blocks of tile kt have landed once at most the next tile's DPW are pending
-    if (kt + 1 < kt1) {
+    const int st = (kt - kt0) % NS;
+    // this wave's blocks of tile kt have landed once at most the later tiles' DPW each are pending
+    const int ahead = min(NS - 2, kt1 - kt - 1);
+    if (ahead >= 3) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * DPW) : "memory");
+    } else if (ahead == 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPW) : "memory");
+    } else if (ahead == 1) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + 2 < kt1) AVC16F_ISSUE(kt + 2, (kt + 2 - kt0) % 3);
+    if (kt + NS - 1 < kt1) AVC16F_ISSUE(kt + NS - 1, (kt + NS - 1 - kt0) % NS);
     const unsigned char* Ai = lds + st * STAGE;
     const unsigned char* Bi = Ai + ABLK * 1024;
 #pragma unroll
@@ -855,19 +863,28 @@ size_t frag16_scratch(const GemmDesc& d) {
   return frag_bytes(a_rows, d.Kc) + (size_t)d.ntaps * frag_bytes(d.N, d.Kc) + 1024;
 }
 
-template <int BM, int BN, int WM, int WN>
-void launch16f(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
+int g_gemm_stages = 4;  // avc_gemm_stages(): LDS ring depth of gemm16f (3..5); 4 measured best
+
+template <int BM, int BN, int WM, int WN, int NS>
+void launch16f_ns(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
   constexpr int NBLK = (BM / 32) * 4 + (BN / 32) * 4;
-  const size_t lds = 3 * NBLK * 1024;
+  const size_t lds = (size_t)NS * NBLK * 1024;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16f_kernel<BM, BN, WM, WN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16f_kernel<BM, BN, WM, WN, NS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   dim3 grid(p.tilesM * p.tilesN, p.nsplit);
-  gemm16f_kernel<BM, BN, WM, WN><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, p.kt_per_tap,
-                                                                p.kps, p.nsplit, slab);
+  gemm16f_kernel<BM, BN, WM, WN, NS><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, p.kt_per_tap,
+                                                                    p.kps, p.nsplit, slab);
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch16f(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
+  if (g_gemm_stages >= 5) launch16f_ns<BM, BN, WM, WN, 5>(d, f, p, slab, s);
+  else if (g_gemm_stages == 4) launch16f_ns<BM, BN, WM, WN, 4>(d, f, p, slab, s);
+  else launch16f_ns<BM, BN, WM, WN, 3>(d, f, p, slab, s);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -1008,5 +1025,14 @@ extern "C" int avc_gemm_tune(int mode) {
     return AVC_ERR_INVALID;
   }
   avc::g_gemm16 = mode;
+  return AVC_OK;
+}
+
+extern "C" int avc_gemm_stages(int stages) {
+  if (stages < 3 || stages > 5) {
+    avc::set_error("avc_gemm_stages: stages must be 3, 4 or 5");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_gemm_stages = stages;
   return AVC_OK;
 }

@@ -142,14 +142,15 @@ struct SplitArgs {
 
 // NC = 16-column gate blocks (4 hidden units x 4 gates) per workgroup tile: 4 for the wide
 // split-K tiles of decoder.lstm2, 1 for the narrow full-K tiles of lstm1 (no slab hand-off).
-template <int NW, int NCH, int NC>
+template <int NW, int NCH, int NC, int RT>
 __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a) {
+  constexpr int MB = 16 * RT;      // batch rows per workgroup (RT 16-row tiles)
   constexpr int TW = 16 * NC;      // tile width (gate rows)
   constexpr int RP = TW + 4;       // LDS row stride (floats): conflict-free partial writes
-  constexpr int TSZ = 64 * TW;     // floats per tile partial
+  constexpr int TSZ = MB * TW;     // floats per tile partial
   extern __shared__ float part[];  // [NW][64][RP] + flag
   constexpr int NT = NW * 64;
-  constexpr int NPAIR = 64 * NC;   // (row, 16-column block) pairs of the tile
+  constexpr int NPAIR = MB * NC;   // (row, 16-column block) pairs of the tile
   constexpr int PP = (NPAIR + NT - 1) / NT;  // pairs per thread in the epilogue
   // wave index through readfirstlane: the buffer descriptors below must be provably uniform, or
   // hipcc wraps every buffer load in a waterfall loop
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
 #pragma unroll
   for (int i = 0; i < PP; ++i) {
     const int pr = min(tid + NT * i, NPAIR - 1), row = pr / NC, blk = pr % NC;
-    const int b = min(rb * 64 + row, B - 1);
+    const int b = min(rb * MB + row, B - 1);
     const int p0 = cb * TW + blk * 16;
     const float* gxr = S.gx + (long)b * S.ldgx + p0;
 #pragma unroll
@@ -189,9 +190,9 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     cpv[i] = hasc ? cv : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  f32x4 acc[4][NC];
+  f32x4 acc[RT][NC];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < RT; ++r)
 #pragma unroll
     for (int n = 0; n < NC; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     // range and read as zero (rows of a partial tile are computed and never stored).
     const long nck = second ? S.lda1 : S.lda;
     const int kc0 = (second ? k0 - S.K0 : k0) >> 5;
-    const long hbase = ((long)rb * 4 * nck + kc0) * 2048;
+    const long hbase = ((long)rb * RT * nck + kc0) * 2048;
     const auto hrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<unsigned char*>(src) + hbase, 0, (int)((long)S.ntile * nck * 2048 - hbase), 0x00020000);
     const long wbase = ((long)cb * NC * S.ldw + (k0 >> 5)) * 2048;
@@ -214,10 +215,10 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     const int hvo = lane * 16, wvo = lane * 16;
     const int hrow16 = (int)nck * 2048, wrow16 = (int)S.ldw * 2048;
 
-    f16x8 hA[4][2], wA[NC][2], hB[4][2], wB[NC][2];
+    f16x8 hA[RT][2], wA[NC][2], hB[RT][2], wB[NC][2];
 #define AVC_LD(RS, VO, SO) __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(RS, VO, SO, 0))
 #define AVC_LOAD(HV, WV, C)                                                                       \
-  _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                                 \
+  _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                                \
     HV[r][0] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 2048);                                         \
     HV[r][1] = AVC_LD(hrs, hvo, r * hrow16 + (C) * 2048 + 1024);                                  \
   }                                                                                               \
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     WV[n][1] = AVC_LD(wrs, wvo, n * wrow16 + (C) * 2048 + 1024);                                  \
   }
 #define AVC_MFMA(HV, WV)                                                                          \
-  _Pragma("unroll") for (int r = 0; r < 4; ++r)                                                   \
+  _Pragma("unroll") for (int r = 0; r < RT; ++r)                                                  \
     _Pragma("unroll") for (int n = 0; n < NC; ++n) {                                              \
       acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][1], WV[n][0], acc[r][n], 0, 0, 0); \
       acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], WV[n][1], acc[r][n], 0, 0, 0); \
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     if constexpr (NC == 1 && NCH <= 4) {
       // narrow tile: every chunk of the wave's K range in flight at once (40 VGPRs per chunk),
       // consumed in issue order under counted waits
-      f16x8 hC[NCH][4][2], wC[NCH][NC][2];
+      f16x8 hC[NCH][RT][2], wC[NCH][NC][2];
 #pragma unroll
       for (int c = 0; c < NCH; ++c) { AVC_LOAD(hC[c], wC[c], c) }
 #ifdef AVC_STAMPS
@@ -276,8 +277,9 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   // Narrow tiles (NC = 1, 4 waves): 64 rows x 4 hidden units = 256 cells, one per thread, summed
   // straight from the wave partials (the host never splits K for them).
   if constexpr (NC == 1 && NW == 4) {
-    const int row = tid >> 2, u = tid & 3;
-    const int b = rb * 64 + row;
+    const int row = min(tid >> 2, MB - 1), u = tid & 3;
+    const bool live = (tid >> 2) < MB;
+    const int b = rb * MB + row;
     const int bc = min(b, B - 1);
     const int p0 = cb * 16 + u;
     const float* gxr = S.gx + (long)bc * S.ldgx + p0;
@@ -292,9 +294,9 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     const float cpl = *(hasc ? S.c_prev + (long)bc * H + j : S.winv);
     const float cp = hasc ? cpl : 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < RT; ++r)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) part[w * 64 * RP + (r * 16 + 4 * lq + e) * RP + l15] = acc[r][0][e];
+      for (int e = 0; e < 4; ++e) part[w * MB * RP + (r * 16 + 4 * lq + e) * RP + l15] = acc[r][0][e];
     __syncthreads();
     AVC_STAMP(3);
     float z[4];
@@ -302,11 +304,11 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     for (int g = 0; g < 4; ++g) {
       float v = part[row * RP + 4 * g + u];
 #pragma unroll
-      for (int ww = 1; ww < NW; ++ww) v += part[ww * 64 * RP + row * RP + 4 * g + u];
+      for (int ww = 1; ww < NW; ++ww) v += part[ww * MB * RP + row * RP + 4 * g + u];
       z[g] = v * wis[g] + gxs[g];
     }
     AVC_STAMP(5);
-    if (b < B) {
+    if (live && b < B) {
       const float ig = sigmoidf_(z[0]), fg = sigmoidf_(z[1]), gg = tanhf(z[2]), og = sigmoidf_(z[3]);
       const float cn = fg * cp + ig * gg;
       const float hv = og * tanhf(cn);
@@ -333,9 +335,9 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
   }
 
   // wave partials -> LDS; C layout of 16x16: column lane&15, rows 4(lane>>4) + e
-  float* mine = part + w * 64 * RP;
+  float* mine = part + w * MB * RP;
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < RT; ++r)
 #pragma unroll
     for (int n = 0; n < NC; ++n)
 #pragma unroll
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
       const int off = row * RP + blk * 16 + 4 * g;
       f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
 #pragma unroll
-      for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * 64 * RP + off);
+      for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * MB * RP + off);
       sum[i][g] = v;
     }
   }
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int* flag = reinterpret_cast<int*>(part + NW * 64 * RP);
+    int* flag = reinterpret_cast<int*>(part + NW * MB * RP);
     if (tid == 0) {
       const int old = __hip_atomic_fetch_add(S.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = old;
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
 #pragma unroll
     for (int i = 0; i < PP; ++i) {
       const int pr = tid + NT * i, row = pr / NC, blk = pr % NC;
-      const int b = rb * 64 + row;
+      const int b = rb * MB + row;
       if (pr >= NPAIR || b >= B) continue;
       float* o = S.h_out + (long)b * S.ldh + cb * TW + blk * 16;
 #pragma unroll
@@ -429,7 +431,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
 #pragma unroll
   for (int i = 0; i < PP; ++i) {
     const int pr = tid + NT * i, row = pr / NC, blk = pr % NC;
-    const int b = rb * 64 + row;
+    const int b = rb * MB + row;
     if (pr >= NPAIR || b >= B) continue;
     const int j0 = cb * 4 * NC + blk * 4;
     const f32x4 zi = sum[i][0] * wiv[i][0] + gxv[i][0];
@@ -478,6 +480,7 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
 
 int g_split_kslice = 0;  // avc_lstm_split_tune() overrides (0 = automatic)
 int g_split_nc = 0;
+int g_split_rows64 = 0;  // 1: never use 32-row workgroups
 
 // K-slice per workgroup: start at min(K, 1024); halve while the launch has fewer than 128
 // workgroups and each wave keeps >= 2 chunks of 32 (measured: scripts/sweep_split.py; the slab
@@ -519,8 +522,8 @@ void* g_sstamp_buf = nullptr;
 long g_sstamp_target = -1, g_sstamp_count = 0;
 #endif
 
-void launch_split(int NW, int NC, dim3 grid, const SplitArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)NW * 64 * (16 * NC + 4) * sizeof(float) + 16;
+void launch_split(int NW, int NC, int RT, dim3 grid, const SplitArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)NW * 16 * RT * (16 * NC + 4) * sizeof(float) + 16;
 #ifdef AVC_STAMPS
   const bool rec = g_sstamp_count++ == g_sstamp_target && g_sstamp_buf;
   if (rec) (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sstamps), &g_sstamp_buf, sizeof(void*), 0, hipMemcpyHostToDevice, s);
@@ -529,17 +532,19 @@ void launch_split(int NW, int NC, dim3 grid, const SplitArgs& a, hipStream_t s) 
   // every active slot uses the same per-wave K range (choose_kslices keeps kslice/NW equal)
   const int first = a.nb[0] > 0 ? 0 : (a.nb[1] > 0 ? 1 : 2);
   const int nch = a.s[first].kslice / NW / 32;
-#define AVC_SPLIT_LAUNCH(NWV, NCV)                                                                \
+#define AVC_SPLIT_LAUNCH(NWV, NCV, RTV)                                                           \
   switch (nch) {                                                                                  \
-    case 1: lstm_split_step_kernel<NWV, 1, NCV><<<grid, NWV * 64, lds, s>>>(a); break;            \
-    case 2: lstm_split_step_kernel<NWV, 2, NCV><<<grid, NWV * 64, lds, s>>>(a); break;            \
-    case 4: lstm_split_step_kernel<NWV, 4, NCV><<<grid, NWV * 64, lds, s>>>(a); break;            \
-    default: lstm_split_step_kernel<NWV, 8, NCV><<<grid, NWV * 64, lds, s>>>(a); break;           \
+    case 1: lstm_split_step_kernel<NWV, 1, NCV, RTV><<<grid, NWV * 64, lds, s>>>(a); break;       \
+    case 2: lstm_split_step_kernel<NWV, 2, NCV, RTV><<<grid, NWV * 64, lds, s>>>(a); break;       \
+    case 4: lstm_split_step_kernel<NWV, 4, NCV, RTV><<<grid, NWV * 64, lds, s>>>(a); break;       \
+    default: lstm_split_step_kernel<NWV, 8, NCV, RTV><<<grid, NWV * 64, lds, s>>>(a); break;      \
   }
   if (NW == 4) {
-    if (NC == 4) { AVC_SPLIT_LAUNCH(4, 4) } else { AVC_SPLIT_LAUNCH(4, 1) }
+    if (NC == 4) { AVC_SPLIT_LAUNCH(4, 4, 4) }
+    else if (RT == 2) { AVC_SPLIT_LAUNCH(4, 1, 2) }
+    else { AVC_SPLIT_LAUNCH(4, 1, 4) }
   } else {
-    if (NC == 4) { AVC_SPLIT_LAUNCH(2, 4) } else { AVC_SPLIT_LAUNCH(2, 1) }
+    if (NC == 4) { AVC_SPLIT_LAUNCH(2, 4, 4) } else { AVC_SPLIT_LAUNCH(2, 1, 4) }
   }
 #undef AVC_SPLIT_LAUNCH
   if (ev) {
@@ -615,7 +620,6 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm split path: H must be a multiple of 32, >= 64");
   Scratch sc(ctx);
   const long TB = (long)T * B;
-  const int nrb = (B + 63) / 64;
   AVC_TAKE(gx, float, (size_t)TB * 4 * H, sc);
   bool f_wih, f_b, f_whh;
   float* wih_p = prep_or_scratch<float>(ctx, sc, PREP_LSTM_WIH, w_ih, nullptr, (size_t)4 * H * din, &f_wih);
@@ -651,8 +655,11 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   const int NW = pick_nw(H);
   // narrow full-K tiles when they alone fill the chip (no slab hand-off: one memory round trip
   // less per step); otherwise 64-column tiles with the K range split over workgroups
-  int NC = (4 * H / 16) * nrb >= 96 && H <= 512 ? 1 : 4;
+  int NC = (4 * H / 16) * ((B + 63) / 64) >= 96 && H <= 512 ? 1 : 4;
   if (g_split_nc) NC = g_split_nc;
+  // narrow tiles: 32-row workgroups when 64-row ones would leave CUs idle (h bytes per CU halve)
+  const int RT = (NC == 1 && NW == 4 && (4 * H / 16) * ((B + 63) / 64) < 256 && B > 32 && !g_split_rows64) ? 2 : 4;
+  const int nrb = (B + 16 * RT - 1) / (16 * RT);
   const int ncb = 4 * H / (16 * NC);
   int K[1] = {H}, nc[1] = {ncb}, ksl[1];
   if (NC == 1) {  // narrow tiles reduce the whole K range in one workgroup
@@ -701,7 +708,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
     S.gates_out = saved_gates ? saved_gates + (long)t * B * 4 * H : nullptr;
     S.slab = slab;
     S.cnt = cnt ? cnt + (long)st * nrb * ncb : nullptr;
-    launch_split(NW, NC, grid, a, s);
+    launch_split(NW, NC, RT, grid, a, s);
   }
   AVC_LAUNCH_CHECK();
   return AVC_OK;
@@ -854,7 +861,7 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
       S.gates_out = g1 ? g1 + (long)t1 * B * 4 * H : nullptr;
       a.nb[2] = nbl;
     }
-    launch_split(NW, NC, dim3(a.nb[0] + a.nb[1] + a.nb[2], nrb), a, s);
+    launch_split(NW, NC, 4, dim3(a.nb[0] + a.nb[1] + a.nb[2], nrb), a, s);
   }
   AVC_LAUNCH_CHECK();
   return AVC_OK;
@@ -871,7 +878,7 @@ extern "C" int avc_debug_stamps_split(void* buf, long target_launch) {
 }
 #endif
 
-extern "C" int avc_lstm_split_tune(int kslice, int col_blocks) {
+extern "C" int avc_lstm_split_tune(int kslice, int col_blocks, int rows64) {
   if (kslice < 0 || kslice % 32 != 0) {
     avc::set_error("avc_lstm_split_tune: kslice must be a non-negative multiple of 32");
     return AVC_ERR_INVALID;
@@ -882,5 +889,6 @@ extern "C" int avc_lstm_split_tune(int kslice, int col_blocks) {
   }
   avc::g_split_kslice = kslice;
   avc::g_split_nc = col_blocks;
+  avc::g_split_rows64 = rows64 ? 1 : 0;
   return AVC_OK;
 }

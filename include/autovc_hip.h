@@ -210,11 +210,15 @@ int avc_timing_enable(int mask);
  * number of waves splitting the reduction (1..8); 0 restores the automatic choice. */
 int avc_lstm_tune(int rows_per_block, int waves);
 /* Tuning hook for the split-fp16 forward step (lstm_split.hip): force the K range per workgroup
- * (a multiple of 32) and the 16-column gate blocks per workgroup tile (1 or 4); 0 = automatic. */
-int avc_lstm_split_tune(int kslice, int col_blocks);
+ * (a multiple of 32) and the 16-column gate blocks per workgroup tile (1 or 4); 0 = automatic.
+ * rows64 = 1 keeps 64 batch rows per workgroup on the narrow tiles (else 32 when that fills
+ * more CUs). */
+int avc_lstm_split_tune(int kslice, int col_blocks, int rows64);
 /* Tuning hook for forward products: 0 runs them on the fp32 MFMA kernel instead of the
  * split-fp16 one (default 1). */
 int avc_gemm_tune(int prec16);
+/* Tuning hook: LDS ring depth (3..5 stages) of the pre-split split-f16 GEMM. */
+int avc_gemm_stages(int stages);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,
                     long* launches);

@@ -6,7 +6,7 @@ import time
 import torch
 
 sys.path.insert(0, __file__.rsplit("/", 2)[0])
-from autovc_amd import ops  # noqa: E402
+from autovc_amd import _lib, ops  # noqa: E402
 
 
 def timeit(fn, reps=10, warm=2):
@@ -23,6 +23,13 @@ def timeit(fn, reps=10, warm=2):
 
 
 def main():
+    for st in (3, 4, 5):
+        _lib.call("avc_gemm_stages", st)
+        run(f"stages{st}")
+    _lib.call("avc_gemm_stages", 4)
+
+
+def run(tag):
     dev = torch.device("cuda:0")
     B, T = 64, 128
     M = B * T
@@ -51,7 +58,7 @@ def main():
             bb = torch.rand(kk, n, device=dev)
             ms = timeit(lambda: ops.gemm(a, bb))
             out[f"gemm {m}x{n}x{kk}"] = {"ms": round(ms, 4), "tflops": round(2.0 * m * n * kk / ms / 1e9, 1)}
-    print(json.dumps(out, indent=1))
+    print(tag, json.dumps({k: v["ms"] for k, v in out.items()}))
 
 
 if __name__ == "__main__":

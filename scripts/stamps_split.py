@@ -31,8 +31,8 @@ torch.cuda.synchronize()
 buf = torch.zeros(65536 * 8, dtype=torch.int64, device=dev)
 names = ["first chunk", "mfma loop", "lds reduce", "slab+ticket", "slab reduce", "epilogue"]
 for arg in sys.argv[1:] or ["0:0"]:
-    ks, nc = (int(v) for v in arg.split(":"))
-    _lib.call("avc_lstm_split_tune", ks, nc)
+    ks, nc, r64 = (int(v) for v in (arg + ":0").split(":")[:3])
+    _lib.call("avc_lstm_split_tune", ks, nc, r64)
     for name, idx in [("lstm1 H=512 step 64", 64), ("lstm2 pair step 64", 128 + 64)]:
         buf.zero_()
         lib.avc_debug_stamps_split(ctypes.c_void_p(buf.data_ptr()), idx)
@@ -60,4 +60,4 @@ for arg in sys.argv[1:] or ["0:0"]:
             if len(v):
                 print(f"   {ph:14s} median {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}  max {v.max():8.0f}  n {len(v)}")
         print(f"   wave start offset median {np.median(st[:, 0] - t0):8.0f}  max {(st[:, 0] - t0).max():8.0f}")
-_lib.call("avc_lstm_split_tune", 0, 0)
+_lib.call("avc_lstm_split_tune", 0, 0, 0)

@@ -31,8 +31,8 @@ def layer(din, H):
 
 
 cases = {"generator": lambda: model(x, c1, c2), "lstm H=512": layer(320, 512), "lstm H=1024": layer(1024, 1024)}
-for ks, nc in [(0, 0), (0, 1), (0, 4), (256, 1), (1024, 4), (512, 4), (256, 4)]:
-    _lib.call("avc_lstm_split_tune", ks, nc)
+for ks, nc, r64 in [(0, 0, 0), (0, 0, 1), (0, 4, 0), (1024, 4, 0)]:
+    _lib.call("avc_lstm_split_tune", ks, nc, r64)
     row = {}
     for name, fn in cases.items():
         with torch.no_grad():
@@ -52,5 +52,5 @@ for ks, nc in [(0, 0), (0, 1), (0, 4), (256, 1), (1024, 4), (512, 4), (256, 4)]:
             _lib.timing_enable([])
         row[name] = {"ms": round(ms, 3), "step_us": round(1000 * r["ms"] / max(1, r["launches"]), 2),
                      "launches": r["launches"]}
-    print(f"kslice={ks} nc={nc}", json.dumps(row), flush=True)
-_lib.call("avc_lstm_split_tune", 0, 0)
+    print(f"kslice={ks} nc={nc} rows64={r64}", json.dumps(row), flush=True)
+_lib.call("avc_lstm_split_tune", 0, 0, 0)
