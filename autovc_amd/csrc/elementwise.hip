@@ -41,13 +41,22 @@ __global__ void colsum_partial_kernel(int M, int N, const float* __restrict__ X,
   part[(long)blockIdx.y * N + n] = s;
 }
 
-__global__ void colsum_final_kernel(int R, int N, const float* __restrict__ part,
-                                    float* __restrict__ out, int accumulate) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+// 64 columns per block, the 16 waves split the R partial rows; fp64 combine through LDS.
+__global__ __launch_bounds__(1024) void colsum_final_kernel(int R, int N, const float* __restrict__ part,
+                                                            float* __restrict__ out, int accumulate) {
+  __shared__ double red[16][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + cl;
   double s = 0.0;
-  for (int r = 0; r < R; ++r) s += part[(long)r * N + n];
-  out[n] = accumulate ? out[n] + (float)s : (float)s;
+  if (n < N)
+    for (int r = grp; r < R; r += 16) s += part[(long)r * N + n];
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp != 0 || n >= N) return;
+  double t = 0.0;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) t += red[g][cl];
+  out[n] = accumulate ? out[n] + (float)t : (float)t;
 }
 
 void colsum_geometry(int M, int N, int& R, int& rows_per) {
@@ -158,20 +167,32 @@ __global__ void bn_bwd_reduce_kernel(int M, int C, const float* __restrict__ dou
   part[((long)blockIdx.y * 2 + 1) * C + c] = s2;
 }
 
-__global__ void bn_bwd_final_kernel(int R, int C, const float* __restrict__ part,
-                                    float* __restrict__ sums, float* __restrict__ d_gamma,
-                                    float* __restrict__ d_beta, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const float* __restrict__ part,
+                                                            float* __restrict__ sums, float* __restrict__ d_gamma,
+                                                            float* __restrict__ d_beta, int accumulate) {
+  __shared__ double red[2][16][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
-  for (int r = 0; r < R; ++r) {
-    s1 += part[((long)r * 2 + 0) * C + c];
-    s2 += part[((long)r * 2 + 1) * C + c];
+  if (c < C)
+    for (int r = grp; r < R; r += 16) {
+      s1 += part[((long)r * 2 + 0) * C + c];
+      s2 += part[((long)r * 2 + 1) * C + c];
+    }
+  red[0][grp][cl] = s1;
+  red[1][grp][cl] = s2;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    t1 += red[0][g][cl];
+    t2 += red[1][g][cl];
   }
-  sums[c] = (float)s1;
-  sums[C + c] = (float)s2;
-  if (d_beta) d_beta[c] = accumulate ? d_beta[c] + (float)s1 : (float)s1;
-  if (d_gamma) d_gamma[c] = accumulate ? d_gamma[c] + (float)s2 : (float)s2;
+  sums[c] = (float)t1;
+  sums[C + c] = (float)t2;
+  if (d_beta) d_beta[c] = accumulate ? d_beta[c] + (float)t1 : (float)t1;
+  if (d_gamma) d_gamma[c] = accumulate ? d_gamma[c] + (float)t2 : (float)t2;
 }
 
 __global__ void bn_bwd_apply_kernel(long M, int C, const float* __restrict__ dout,
@@ -452,7 +473,7 @@ int colsum(avc_context* ctx, int M, int N, const float* X, long ld, float* out, 
   Scratch sc(ctx);
   AVC_TAKE(part, float, (size_t)R * N, sc);
   colsum_partial_kernel<<<dim3((N + 255) / 256, R), 256, 0, s>>>(M, N, X, ld, rp, part);
-  colsum_final_kernel<<<(N + 255) / 256, 256, 0, s>>>(R, N, part, out, accumulate);
+  colsum_final_kernel<<<(N + 63) / 64, 1024, 0, s>>>(R, N, part, out, accumulate);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
@@ -495,7 +516,7 @@ int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* 
   AVC_TAKE(sums, float, (size_t)2 * C, sc);
   bn_bwd_reduce_kernel<<<dim3((C + 255) / 256, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
                                                                 beta, act, rp, part);
-  bn_bwd_final_kernel<<<(C + 255) / 256, 256, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate);
+  bn_bwd_final_kernel<<<(C + 63) / 64, 1024, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate);
   bn_bwd_apply_kernel<<<ew_blocks((long)M * C), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
                                                               beta, act, training, sums,
                                                               1.f / (float)M, dy);

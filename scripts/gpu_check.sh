@@ -26,6 +26,7 @@ for step in "$@"; do
     pmcf)  run pmcf 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcF -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
     pmcw)  run pmcw 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcW -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
     sweep) run sweep 600 python scripts/sweep_lstm.py ;;
+    proftrain) run proftrain 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/proftrain -o train -- python3 bench.py --mode train --steps 3 --warmup 1 --no-cpu --no-timing ;;
     ssplit) run ssplit 400 python scripts/sweep_split.py ;;
     sstamps) run sstamps 300 python scripts/stamps_split.py 0:0 0:4 ;;
     probe) run probe 200 python scripts/probe_cache.py ;;
