@@ -17,7 +17,7 @@ from collections import defaultdict
 
 # bench.py kernel classes -> predicate on the demangled kernel name
 CLASSES = {
-    "gemm": lambda n: "gemm_kernel<" in n or "gemm16_kernel<" in n,
+    "gemm": lambda n: "gemm_kernel<" in n or "gemm16_kernel<" in n or "gemm16f_kernel<" in n,
     "lstm_step_fwd": lambda n: "lstm_split_step_kernel<" in n or re.search(r"lstm_step_kernel<\d+, false", n) is not None,
     "lstm_step_bwd": lambda n: re.search(r"lstm_step_kernel<\d+, true", n) is not None,
     "lstm32": lambda n: "lstm32_" in n,
