@@ -55,7 +55,7 @@ _SIGS = {
     "avc_lstm_tune": [_I, _I],
     "avc_lstm_split_tune": [_I, _I, _I],
     "avc_gemm_tune": [_I],
-    "avc_gemm_stages": [_I],
+    "avc_gemm_config": [_I],
     "avc_timing_reset": [],
     "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)],

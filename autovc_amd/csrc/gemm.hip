@@ -543,25 +543,42 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
 __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restrict__ src, long rs,
                                                            long ks, int R, int K, int ntile, int nkc,
                                                            _Float16* __restrict__ dst) {
-  const int G8 = nkc * 2;  // 8-element groups per row
+  const int G8 = nkc * 2;  // 8-element groups per row (a multiple of 4)
   const long total = (long)ntile * 32 * G8;
+  const bool vec = ks == 1 && (rs & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
     long r;
     int g8;
-    if (ks == 1) {  // row-major source: consecutive threads read consecutive 32-B pieces of a row
-      r = idx / G8;
-      g8 = (int)(idx - r * G8);
+    if (ks == 1) {
+      // row-major source: thread -> (tile, 32-k group quad, row, group) with the group fastest, so
+      // a wave reads 16 rows x 128 B and each of its stores writes two 256-B runs (whole lines)
+      const int gq = (int)(idx & 3);
+      const long rest = idx >> 2;
+      const int rr = (int)(rest & 31);
+      const long tq = rest >> 5;  // tile * (G8/4) + quad
+      const long t = tq / (G8 >> 2);
+      const int quad = (int)(tq - t * (G8 >> 2));
+      r = t * 32 + rr;
+      g8 = quad * 4 + gq;
     } else {        // transposed source (column stride 1): consecutive threads take consecutive rows
       const long rows = (long)ntile * 32;
       g8 = (int)(idx / rows);
       r = idx - (long)g8 * rows;
     }
     float v[8];
+    const int k0 = 8 * g8;
+    if (vec && r < R && k0 + 8 <= K) {
+      const float4* q = reinterpret_cast<const float4*>(src + r * rs + k0);
+      const float4 a = q[0], b = q[1];
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = 8 * g8 + e;
-      v[e] = (r < R && k < K) ? src[r * rs + (long)k * ks] : 0.f;
+      for (int e = 0; e < 8; ++e) {
+        const int k = k0 + e;
+        v[e] = (r < R && k < K) ? src[r * rs + (long)k * ks] : 0.f;
+      }
     }
     f16x8 hi, lo;
     split8(v, hi, lo);
@@ -577,14 +594,14 @@ struct Frag16Args {
   const _Float16* Bs; int b_ntile, b_nkc; long b_tapstride;            // halves per tap
 };
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, int KC>
 __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag16Args f, int tilesM,
                                                                int tilesN, int kt_per_tap, int kps,
                                                                int nsplit, float* __restrict__ slab) {
   constexpr int NT = 64 * WM * WN, NWAVE = WM * WN;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int ABLK = (BM / 32) * 4, BBLK = (BN / 32) * 4;  // 1 KiB blocks per K-tile (2 kc x hi/lo)
+  constexpr int ABLK = (BM / 32) * KC * 2, BBLK = (BN / 32) * KC * 2;  // 1 KiB blocks per K-tile (KC kc x hi/lo)
   constexpr int NBLK = ABLK + BBLK;
   static_assert(NBLK % NWAVE == 0, "blocks per K-tile must split evenly over the waves");
   constexpr int DPW = NBLK / NWAVE;  // LDS-DMA instructions per wave per K-tile
@@ -618,23 +635,23 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
 #define AVC16F_ISSUE(KT, ST)                                                                      \
   {                                                                                               \
     const int tau = (KT) / kt_per_tap;                                                            \
-    const int kc0 = ((KT) - tau * kt_per_tap) * 2;                                                \
+    const int kc0 = ((KT) - tau * kt_per_tap) * KC;                                               \
     unsigned char* const stage_base = lds + (ST) * STAGE;                                         \
     _Pragma("unroll") for (int i = 0; i < DPW; ++i) {                                             \
       const int b = w * DPW + i;                                                                  \
       unsigned char* dst = stage_base + b * 1024;                                                 \
       if (b < ABLK) {                                                                             \
-        const int rt = b >> 2, kc = (b >> 1) & 1, hl = b & 1;                                     \
+        const int rt = b / (2 * KC), kc = (b >> 1) % KC, hl = b & 1;                              \
         const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)tau * a_tapshift) / 32; \
-        const bool ok = src_tile >= 0 && src_tile < a_ntile;                                      \
+        const bool ok = src_tile >= 0 && src_tile < a_ntile && kc0 + kc < a_nkc;                 \
         const unsigned off = ok ? (unsigned)(((src_tile * a_nkc + kc0 + kc) * 2 + hl) * 1024) : kOut; \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)dst, 16, \
                                                  off + lane * 16, 0, 0, 0);                       \
       } else {                                                                                    \
         const int bb = b - ABLK;                                                                  \
-        const int ct = bb >> 2, kc = (bb >> 1) & 1, hl = bb & 1;                                  \
+        const int ct = bb / (2 * KC), kc = (bb >> 1) % KC, hl = bb & 1;                           \
         const int src_tile = tn * (BN / 32) + ct;                                                 \
-        const bool ok = src_tile < b_ntile;                                                       \
+        const bool ok = src_tile < b_ntile && kc0 + kc < b_nkc;                                   \
         const unsigned off = ok ? (unsigned)(tau * b_tapstride * 2 +                              \
                                              ((long)(src_tile * b_nkc + kc0 + kc) * 2 + hl) * 1024) : kOut; \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16, \
@@ -652,7 +669,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = cmp[i][j] = part[i][j] = crs[i][j] = zero16;
 
-  constexpr int KB = 4;  // K-tiles (128 k) per compensated partial
+  constexpr int KB = 8 / KC;  // K-tiles (128 k) per compensated partial
   // NS-stage ring: NS-1 K-tiles in flight ahead of the one being consumed
 #pragma unroll
   for (int pre = 0; pre < NS - 1; ++pre)  // (not `i`: the macro's own loop variable)
@@ -675,17 +692,17 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
     const unsigned char* Ai = lds + st * STAGE;
     const unsigned char* Bi = Ai + ABLK * 1024;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < KC; ++s) {
       f16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const unsigned char* p = Ai + (((wm * TM + i) * 2 + s) * 2) * 1024 + lane * 16;
+        const unsigned char* p = Ai + (((wm * TM + i) * KC + s) * 2) * 1024 + lane * 16;
         ah[i] = *reinterpret_cast<const f16x8*>(p);
         al[i] = *reinterpret_cast<const f16x8*>(p + 1024);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const unsigned char* p = Bi + (((wn * TN + j) * 2 + s) * 2) * 1024 + lane * 16;
+        const unsigned char* p = Bi + (((wn * TN + j) * KC + s) * 2) * 1024 + lane * 16;
         bh[j] = *reinterpret_cast<const f16x8*>(p);
         bl[j] = *reinterpret_cast<const f16x8*>(p + 1024);
       }
@@ -863,28 +880,37 @@ size_t frag16_scratch(const GemmDesc& d) {
   return frag_bytes(a_rows, d.Kc) + (size_t)d.ntaps * frag_bytes(d.N, d.Kc) + 1024;
 }
 
-int g_gemm_stages = 4;  // avc_gemm_stages(): LDS ring depth of gemm16f (3..5); 4 measured best
+int g_gemm_cfg = 1;  // avc_gemm_config(): tile/ring variant of gemm16f for 128x128 tiles (1 measured best)
 
-template <int BM, int BN, int WM, int WN, int NS>
-void launch16f_ns(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
-  constexpr int NBLK = (BM / 32) * 4 + (BN / 32) * 4;
+template <int BM, int BN, int WM, int WN, int NS, int KC>
+void launch16f_cfg(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
+  constexpr int NBLK = (BM / 32) * KC * 2 + (BN / 32) * KC * 2;
   const size_t lds = (size_t)NS * NBLK * 1024;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16f_kernel<BM, BN, WM, WN, NS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16f_kernel<BM, BN, WM, WN, NS, KC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
+  // K-tiles of KC 16-deep chunks; the split-K plan is re-cut in these units (every split
+  // writes its slab, an empty range writes zeros)
+  const int kt_per_tap = (f.a_nkc + KC - 1) / KC;
+  const int ktotal = d.ntaps * kt_per_tap;
+  const int kps = (ktotal + p.nsplit - 1) / p.nsplit;
   dim3 grid(p.tilesM * p.tilesN, p.nsplit);
-  gemm16f_kernel<BM, BN, WM, WN, NS><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, p.kt_per_tap,
-                                                                    p.kps, p.nsplit, slab);
+  gemm16f_kernel<BM, BN, WM, WN, NS, KC><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, kt_per_tap,
+                                                                        kps, p.nsplit, slab);
 }
 
-template <int BM, int BN, int WM, int WN>
-void launch16f(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
-  if (g_gemm_stages >= 5) launch16f_ns<BM, BN, WM, WN, 5>(d, f, p, slab, s);
-  else if (g_gemm_stages == 4) launch16f_ns<BM, BN, WM, WN, 4>(d, f, p, slab, s);
-  else launch16f_ns<BM, BN, WM, WN, 3>(d, f, p, slab, s);
+void launch16f_128(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
+  switch (g_gemm_cfg) {
+    case 1: launch16f_cfg<128, 128, 4, 2, 2, 4>(d, f, p, slab, s); break;
+    case 2: launch16f_cfg<128, 128, 4, 2, 3, 3>(d, f, p, slab, s); break;
+    case 3: launch16f_cfg<128, 128, 2, 4, 4, 2>(d, f, p, slab, s); break;
+    case 4: launch16f_cfg<128, 128, 2, 4, 2, 4>(d, f, p, slab, s); break;
+    case 5: launch16f_cfg<128, 128, 4, 2, 3, 2>(d, f, p, slab, s); break;
+    default: launch16f_cfg<128, 128, 4, 2, 4, 2>(d, f, p, slab, s); break;
+  }
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -992,8 +1018,8 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
   }
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
   if (frag) {
-    if (p.bm == 128) launch16f<128, 128, 4, 2>(d, fa, p, slab, stream);
-    else launch16f<64, 64, 2, 2>(d, fa, p, slab, stream);
+    if (p.bm == 128) launch16f_128(d, fa, p, slab, stream);
+    else launch16f_cfg<64, 64, 2, 2, 4, 2>(d, fa, p, slab, stream);
   } else if (d.prec16 && !d.a_trans && g_gemm16) {
     if (p.bm == 128) launch16<128, 128, 4, 2>(d, p, slab, stream);
     else launch16<64, 64, 2, 2>(d, p, slab, stream);
@@ -1028,11 +1054,11 @@ extern "C" int avc_gemm_tune(int mode) {
   return AVC_OK;
 }
 
-extern "C" int avc_gemm_stages(int stages) {
-  if (stages < 3 || stages > 5) {
-    avc::set_error("avc_gemm_stages: stages must be 3, 4 or 5");
+extern "C" int avc_gemm_config(int cfg) {
+  if (cfg < 0 || cfg > 5) {
+    avc::set_error("avc_gemm_config: cfg must be 0..5");
     return AVC_ERR_INVALID;
   }
-  avc::g_gemm_stages = stages;
+  avc::g_gemm_cfg = cfg;
   return AVC_OK;
 }

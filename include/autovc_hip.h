@@ -217,8 +217,10 @@ int avc_lstm_split_tune(int kslice, int col_blocks, int rows64);
 /* Tuning hook for forward products: 0 runs them on the fp32 MFMA kernel instead of the
  * split-fp16 one (default 1). */
 int avc_gemm_tune(int prec16);
-/* Tuning hook: LDS ring depth (3..5 stages) of the pre-split split-f16 GEMM. */
-int avc_gemm_stages(int stages);
+/* Tuning hook: variant of the pre-split split-f16 GEMM for 128x128 tiles (8 waves each):
+ * 0 = 4x2 waves, 4-stage ring of 32-deep K-tiles; 1 = 4x2, 2 stages of 64-deep K-tiles (default);
+ * 2 = 4x2, 3 stages x 48; 3 = 2x4, 4 x 32; 4 = 2x4, 2 x 64; 5 = 4x2, 3 x 32. */
+int avc_gemm_config(int cfg);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,
                     long* launches);

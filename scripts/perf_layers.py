@@ -23,10 +23,11 @@ def timeit(fn, reps=10, warm=2):
 
 
 def main():
-    for st in (3, 4, 5):
-        _lib.call("avc_gemm_stages", st)
-        run(f"stages{st}")
-    _lib.call("avc_gemm_stages", 4)
+    cfgs = [int(c) for c in sys.argv[1:]] or [0]
+    for c in cfgs:
+        _lib.call("avc_gemm_config", c)
+        run(f"cfg{c}")
+    _lib.call("avc_gemm_config", 1)
 
 
 def run(tag):

@@ -290,3 +290,38 @@ def test_conv_fragment_path(cuda_device, B, T, cin, cout):
                                   1e-5, ops.ACT_NONE, None, T, B)
     out_cf = out.cpu().reshape(T, B, cout).permute(1, 2, 0).double()
     assert (out_cf - y).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+def test_gemm16f_configs(cuda_device, cfg):
+    """Every 128x128 variant of the pre-split split-f16 GEMM (avc_gemm_config): a Linear with
+    a ragged K (336: the 64-deep K-tiles end half out of range) and N (1040: a partial column
+    tile), and a 512->512 Conv1d k5 + BN whose taps are 32-row tile shifts, against fp64."""
+    g = torch.Generator().manual_seed(1000 + cfg)
+    x = torch.randn(2048, 336, generator=g)
+    w = torch.randn(1040, 336, generator=g) / np.sqrt(336)
+    b = torch.randn(1040, generator=g) * 0.1
+    ref = x.double() @ w.double().T + b.double()
+    B, T, cin, cout = 64, 64, 512, 512
+    xc = torch.rand(B, cin, T, generator=g)
+    W = (torch.rand(cout, cin, 5, generator=g) - 0.5) * 0.1
+    bias = (torch.rand(cout, generator=g) - 0.5) * 0.1
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = (torch.rand(cout, generator=g) - 0.5) * 0.4
+    yc = F.batch_norm(F.conv1d(xc.double(), W.double(), bias.double(), padding=2), None, None,
+                      gamma.double(), beta.double(), training=True, eps=1e-5)
+    fr = xc.permute(2, 0, 1).reshape(T * B, cin)
+    try:
+        _lib.call("avc_gemm_config", cfg)
+        with torch.no_grad():
+            y = ops.Linear.apply(_t(x, cuda_device), _t(w, cuda_device), _t(b, cuda_device))
+            out = ops.ConvBNAct.apply(_t(fr, cuda_device), _t(W, cuda_device), _t(bias, cuda_device),
+                                      _t(gamma, cuda_device), _t(beta, cuda_device), None, None, True, 0.1,
+                                      1e-5, ops.ACT_NONE, None, T, B)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("avc_gemm_config", 1)
+    err = (y.cpu().double() - ref).abs().max().item()
+    assert err < 2e-6 * max(1.0, ref.abs().max().item()), err
+    out_cf = out.cpu().reshape(T, B, cout).permute(1, 2, 0).double()
+    assert (out_cf - yc).abs().max().item() < 1e-5
