@@ -16,7 +16,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AUTOVC_HIP_LIB", os.path.join(_HERE, "libautovc_hip.so"))
 
-ACT_NONE, ACT_RELU, ACT_TANH = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_TANH, ACT_DBNORM = 0, 1, 2, 3
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
@@ -63,6 +63,12 @@ _SIGS = {
     "avc_generator_forward": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P],
     "avc_generator_forward_cached": [_P, _I, _I, _P, ctypes.c_long, _P, _P, _P, _I, _P, _P, _P, _P],
     "avc_prepared_release": [_P],
+    "avc_stft_frames": [ctypes.c_long, _I],
+    "avc_mel_basis": [ctypes.c_double, _I, _I, ctypes.c_double, ctypes.c_double, _I, _P, _P],
+    "avc_mel_spectrogram": [_P, _P, ctypes.c_long, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P],
+    "avc_speaker_encoder_param_count": [],
+    "avc_speaker_encoder_forward": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P],
+    "avc_embedding_mean_normalize": [_I, _I, _P, _P, _P],
 }
 _RESTYPES = {"avc_last_error": ctypes.c_char_p}
 

@@ -27,6 +27,10 @@ __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
 __device__ __forceinline__ float act_apply(float v, int act) {
   if (act == AVC_ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == AVC_ACT_TANH) return tanhf(v);
+  if (act == AVC_ACT_DBNORM) {
+    const float db = 20.f * log10f(fmaxf(1e-5f, v));
+    return fminf(fmaxf((db + 100.f) / 100.f, 0.f), 1.f);
+  }
   return v;
 }
 

@@ -1,6 +1,7 @@
 """Hot-path slice of the reference's global config (autovc/utils/hparams.py:4-48).
 
-Only the keys the Generator path reads are restated: model dims, learn-loop defaults, Adam
+Only the keys the Generator path and its neighbours (mel frontends, partial slices,
+speaker encoder) read are restated: model dims, spectrogram settings, learn-loop defaults, Adam
 settings and the dataloader batch size.  When this package is dropped into the reference tree
  the reference's own `AutoEncoderParams` dict can be passed in instead.
 """
@@ -8,6 +9,9 @@ from datetime import date
 
 AutoEncoderParams = {
     "model_dir": "models/AutoVC",
+    # hparams.py:6-14
+    "spectrogram": {"sr": 22050, "n_mels": 80, "n_fft": 2048, "hop_length": 275, "window_length": 1100,
+                    "fmin": 40, "mel_window_step": 12.5, "partial_utterance_n_frames": 400},
     "model": {"dim_neck": 32, "dim_emb": 256, "dim_pre": 512, "freq": 32},
     "learn": {
         "n_epochs": 1,
@@ -27,4 +31,14 @@ AutoEncoderParams = {
         "n_warmup_steps": 256,
     },
     "dataloader": {"batch_size": 16},
+}
+
+# hparams.py:50-65 (inference keys of the speaker encoder)
+SpeakerEncoderParams = {
+    "model_dir": "models/SpeakerEncoder",
+    "spectrogram": {"sr": 16000, "n_mels": 40, "mel_window_step": 10, "mel_window_length": 25,
+                    "partial_utterance_n_frames": 160},
+    "model": {"input_size": 40, "hidden_size": 256, "embedding_size": 256, "num_layers": 3,
+              "batch_first": True},
+    "learn": {"save_dir": "models/SpeakerEncoder"},
 }

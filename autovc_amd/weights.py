@@ -153,3 +153,46 @@ def onehot_embedding(B: int, dim: int = 256, offset: int = 0) -> np.ndarray:
     c = np.zeros((B, dim), np.float32)
     c[np.arange(B), (np.arange(B) + offset) % dim] = 1.0
     return c
+
+
+# ---- speaker encoder ---------------------------------------------------
+
+def speaker_encoder_state_dict(seed: int = 0, n_in: int = 40, H: int = 256, E: int = 256, layers: int = 3,
+                               device="cpu"):
+    """SpeakerEncoder.state_dict() keys/shapes (speaker_encoder/model.py:48-57) with PyTorch's
+    default init bounds: LSTM U(±1/√H), Linear U(±1/√fan_in)."""
+    import torch
+    out = OrderedDict()
+    k = 1.0 / np.sqrt(H)
+    stream = 50_000_000
+    for l in range(layers):
+        din = n_in if l == 0 else H
+        for name, shape in (("weight_ih", (4 * H, din)), ("weight_hh", (4 * H, H)), ("bias_ih", (4 * H,)),
+                            ("bias_hh", (4 * H,))):
+            out[f"lstm.{name}_l{l}"] = _u(seed, stream, shape, -k, k)
+            stream += 1
+    kl = 1.0 / np.sqrt(H)
+    out["linear.weight"] = _u(seed, stream, (E, H), -kl, kl)
+    out["linear.bias"] = _u(seed, stream + 1, (E,), -kl, kl)
+    return OrderedDict((n, torch.from_numpy(v).to(device)) for n, v in out.items())
+
+
+def synthetic_speech(seed: int, n: int, sr: int) -> np.ndarray:
+    """A deterministic speech-like test waveform in [-1, 1]: a 110-220 Hz glottal-pulse-like
+    harmonic series with a slow formant sweep, syllable-rate amplitude envelope and a little
+    noise, so spectra span > 80 dB like real speech."""
+    t = np.arange(n, dtype=np.float64) / sr
+    u = uniform01(seed, 30_000_001, 8)
+    f0 = 110.0 + 110.0 * u[0] + 20.0 * np.sin(2 * np.pi * 0.7 * t)
+    ph = 2 * np.pi * np.cumsum(f0) / sr
+    form = 500.0 + 1500.0 * (0.5 + 0.5 * np.sin(2 * np.pi * (0.3 + u[1]) * t))
+    y = np.zeros(n)
+    for h in range(1, 40):
+        fh = h * f0
+        gain = np.exp(-((fh - form) / 400.0) ** 2) + 0.3 * np.exp(-((fh - 2.5 * form) / 600.0) ** 2) + 0.02 / h
+        y += gain * np.sin(h * ph)
+    env = 0.5 + 0.5 * np.sin(2 * np.pi * (3.0 + u[2]) * t) ** 2
+    noise = (uniform01(seed, 30_000_003, n) - 0.5) * 2e-3
+    y = y * env
+    y = 0.5 * y / np.max(np.abs(y)) + noise
+    return y.astype(np.float32)

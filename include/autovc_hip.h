@@ -37,6 +37,7 @@ extern "C" {
 #define AVC_ACT_NONE 0
 #define AVC_ACT_RELU 1 /* encoder.py:70, decoder.py:70 */
 #define AVC_ACT_TANH 2 /* postnet.py:55 */
+#define AVC_ACT_DBNORM 3 /* clip((20*log10(max(1e-5,x)) + 100) / 100, 0, 1): spectrogram.py:14-31,53-55 */
 
 typedef struct avc_context avc_context;
 
@@ -224,6 +225,40 @@ int avc_gemm_config(int cfg);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,
                     long* launches);
+
+/* ---- rows either side of the Generator ----------------------------------------
+ * Mel frontends of autovc/audio/spectrogram.py and the speaker encoder of
+ * autovc/speaker_encoder/model.py (inference).  librosa's algorithms (stft center=True with a
+ * periodic Hann window centred in n_fft; filters.mel with the Slaney scale and norm) restated.
+ *
+ * avc_stft_frames: frames of a centred STFT, 1 + n_samples / hop.
+ * avc_mel_basis: librosa.filters.mel(sr, n_fft, n_mels, fmin, fmax) as [n_mels][ld] fp32 rows
+ *   (ld >= n_fft/2 + 1, zero tail); replaces the call inside librosa.feature.melspectrogram
+ *   (spectrogram.py:118, 200-205). */
+int avc_stft_frames(long n_samples, int hop);
+int avc_mel_basis(double sr, int n_fft, int n_mels, double fmin, double fmax, int ld, float* out,
+                  void* stream);
+/* avc_mel_spectrogram: wav [n_samples] -> out = mel_basis . |stft(wav)|^power, then with
+ * db_normalize = 1 the dB + normalisation of spectrogram.py:121-125 (AVC_ACT_DBNORM).
+ *   pad_mode 0 = zeros, 1 = reflect (librosa < 0.10); power 1 (auto-encoder
+ *   frontend, spectrogram.py:112-118) or 2 (speaker encoder, spectrogram.py:200-205);
+ *   mel_basis [n_mels][ld_basis] from avc_mel_basis with ld_basis = (n_fft/2 + 1) rounded up to 4;
+ *   out (n_mels, F) if channels_first else (F, n_mels), F = avc_stft_frames(n_samples, hop). */
+int avc_mel_spectrogram(avc_context* ctx, const float* wav, long n_samples, int n_fft, int hop,
+                        int win_length, int pad_mode, int power, const float* mel_basis, int n_mels,
+                        int ld_basis, int db_normalize, int channels_first, float* out, void* stream);
+/* Speaker encoder forward (speaker_encoder/model.py:71-91): 3-layer LSTM (n_in -> H, zero
+ * state), Linear(H -> E) + ReLU on the last layer's final hidden state, L2-normalised rows.
+ *   x (B, T, n_in) batch-first; params = the 14 tensors of SpeakerEncoder.state_dict() in order
+ *   (lstm.{weight_ih,weight_hh,bias_ih,bias_hh}_l{0,1,2}, linear.weight, linear.bias);
+ *   embeds (B, E). */
+int avc_speaker_encoder_param_count(void);
+int avc_speaker_encoder_forward(avc_context* ctx, int T, int B, int n_in, int H, int E,
+                                const float* const* params, const float* x, float* embeds,
+                                void* stream);
+/* embed_utterance's reduction (speaker_encoder/model.py:189-190): out[E] = mean_b(embeds[b]),
+ * L2-normalised. */
+int avc_embedding_mean_normalize(int B, int E, const float* embeds, float* out, void* stream);
 
 #ifdef __cplusplus
 }
