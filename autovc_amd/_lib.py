@@ -148,7 +148,7 @@ def ptr(t) -> int | None:
     return t.data_ptr()
 
 
-TIMING_CLASSES = {"gemm": 0, "lstm_step_fwd": 1, "lstm_step_bwd": 2, "lstm32": 3}
+TIMING_CLASSES = {"gemm": 0, "lstm_step_fwd": 1, "lstm_step_bwd": 2, "lstm32": 3, "dft64": 4}
 
 
 def timing_enable(names):

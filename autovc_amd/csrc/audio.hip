@@ -21,6 +21,7 @@
 #include "common.h"
 #include "gemm.h"
 #include "kernels.h"
+#include "timing.h"
 
 namespace avc {
 namespace {
@@ -280,8 +281,12 @@ int avc_mel_spectrogram(avc_context* ctx, const float* wav, long n_samples, int 
                                                                  p.F, pad_mode, frames);
   dft_basis_kernel<<<ew_grid(2L * p.nb * p.Kp), 256, 0, s>>>(n_fft, win_length, p.nb, p.Kp, basis);
   AVC_LAUNCH_CHECK();
+  hipEvent_t ev = timing_begin(TC_DFT, s);
   dft64_kernel<<<dim3((p.F + 63) / 64, (2 * p.nb + 63) / 64), 256, 0, s>>>(p.F, 2 * p.nb, p.Kp, frames, basis, spec);
   AVC_LAUNCH_CHECK();
+  if (ev)
+    timing_end(TC_DFT, ev, s, 2.0 * p.F * 2.0 * p.nb * p.Kp,
+               4.0 * p.F * p.Kp + 8.0 * 2.0 * p.nb * p.Kp + 4.0 * p.F * 2.0 * p.nb);
   spec_power_kernel<<<ew_grid((long)p.F * p.ld), 256, 0, s>>>(p.F, p.nb, spec, power == 2, p.ld, mag);
   AVC_LAUNCH_CHECK();
   p.mel.A = mag; p.mel.B = mel_basis; p.mel.C = out;

@@ -11,6 +11,11 @@ scaling is "weak" and `value` = all frames of all ranks / max-over-ranks time.
 --mode train runs BASELINE config 3/4 instead (batch 256 training step: forward, loss with the
 second encoder pass, backward, RCCL gradient all-reduce when N>1, fused clip+Adam+EMA).
 
+The SURVEY §8f rows either side of the Generator have their own lines (replicas, like fwd):
+--mode mel  the auto-encoder mel frontend (spectrogram.py:62-142) of one 60 s utterance;
+--mode se   the speaker encoder's embed_utterance (speaker_encoder/model.py:142-194) of one
+            10 s utterance (16 kHz mel, 12 partials through the 3-layer LSTM, mean + L2).
+
 Also reported on the same line: `roofline` for the dominant kernel class, measured with HIP
 events around every launch of that class inside the timed region, and `cpu_baseline`: the CPU
 oracle (oracle/autovc_oracle.py, a torch-CPU restatement pinned to the reference's outputs) timed
@@ -31,6 +36,7 @@ sys.path.insert(0, HERE)
 PEAK_FP32_MATRIX_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_*_f32, dense
 PEAK_F16_MATRIX_TFLOPS = 2500.0   # dense f16/bf16 MFMA
 PEAK_HBM_GBS = 8000.0
+PEAK_FP64_MATRIX_TFLOPS = 78.6    # AMD MI355X datasheet (fp64 matrix = fp64 vector); not in the guide
 # Roofline of each timed kernel class.  Forward contractions run as 3 f16 MFMA products per
 # fp32 product, so their fp32-equivalent MFMA ceiling is 2500/3 TFLOP/s; the LSTM step streams
 # its (split) weights every time step and is priced against HBM; backward products are fp32.
@@ -39,7 +45,11 @@ ROOFLINE = {
             "lstm32": ("hbm", PEAK_HBM_GBS)},
     "train": {"gemm": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
               "lstm_step_bwd": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm32": ("hbm", PEAK_HBM_GBS)},
+    "mel": {"dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS), "gemm": ("mfma", PEAK_FP32_MATRIX_TFLOPS)},
+    "se": {"lstm_step_fwd": ("hbm", PEAK_HBM_GBS), "gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
+           "dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS)},
 }
+MEL_SECONDS, SE_SECONDS = 60, 10
 METRIC = "mel-frames/sec/GPU AutoVC fwd, 80×128 batch; max|Δmel| vs ref"
 
 
@@ -48,7 +58,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["fwd", "train"], default="fwd")
+    ap.add_argument("--mode", choices=["fwd", "train", "mel", "se"], default="fwd")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 64 fwd / 256 train)")
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
@@ -72,6 +82,120 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from autovc_amd import _lib
+
+    if args.mode in ("fwd", "train"):
+        m = setup_generator(args, dev, rank)
+    elif args.mode == "mel":
+        m = setup_mel(args, dev, rank)
+    else:
+        m = setup_se(args, dev, rank)
+    step = m["step"]
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # Roofline region: the same K steps again with every launch of the kernel classes bracketed
+    # by HIP events on its stream (the events cost ~7 us per launch, so `value` above is taken
+    # from the uninstrumented region).
+    classes = m["classes"]
+    inst_elapsed = None
+    if not args.no_timing:
+        _lib.timing_enable(classes)
+        _lib.timing_reset()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        inst_elapsed = time.perf_counter() - t1
+        _lib.timing_enable([])
+
+    units = world * m["units_per_step"] * args.steps
+    value = units / elapsed
+    result = {
+        "metric": m["metric"],
+        "value": round(value, 1),
+        "unit": m["unit"],
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": m["dtype"],
+        "data": m["data"],
+        "config": m["config"](world),
+    }
+    if m.get("flop_per_unit"):
+        result["achieved_tflops_whole_step"] = round(m["flop_per_unit"] * value / world / 1e12, 2)
+
+    if not args.no_timing:
+        per = {c: _lib.timing_read(c) for c in classes}
+        kern = {}
+        for c, r in per.items():
+            if r["launches"] == 0 or r["ms"] <= 0:
+                continue
+            kern[c] = {"launches_per_step": r["launches"] / args.steps, "avg_us": round(1000 * r["ms"] / r["launches"], 2),
+                       "share_of_step": round(r["ms"] / (1000 * inst_elapsed), 3),
+                       "tflops": round(r["flops"] / (r["ms"] * 1e-3) / 1e12, 2),
+                       "gbs_weights": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1)}
+        dom = max(kern, key=lambda c: per[c]["ms"]) if kern else None
+        if dom:
+            r = per[dom]
+            bound, peak = ROOFLINE[args.mode][dom]
+            if bound == "hbm":
+                achieved = r["bytes"] / (r["ms"] * 1e-3) / 1e9
+                unit = "GB/s"
+            else:
+                achieved = r["flops"] / (r["ms"] * 1e-3) / 1e12
+                unit = "TFLOP/s" + (" (fp32-equivalent, 3 f16 products each)" if peak < 1000 and peak > 500 else
+                                    " (fp64)" if peak == PEAK_FP64_MATRIX_TFLOPS else "")
+            result["roofline"] = {
+                "kernel": dom, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
+                "unit": unit, "frac": round(achieved / peak, 4),
+                "traffic": None,
+                "avg_launch_us": kern[dom]["avg_us"],
+                "flop_per_launch": round(r["flops"] / r["launches"]),
+                "algorithmic_bytes_per_launch": round(r["bytes"] / r["launches"]),
+            }
+            tr = pmc_traffic(dom, args)
+            if tr:
+                result["roofline"]["traffic"] = tr["traffic_bytes"]
+                result["roofline"]["traffic_source"] = tr["source"]
+        result["kernels"] = kern
+        result["instrumented_ms_per_step"] = round(1000 * inst_elapsed / args.steps, 3)
+
+    if rank == 0 and world == 1 and not args.no_cpu and m.get("cpu"):
+        result["cpu_baseline"], extra = m["cpu"](out)
+        result.update(extra)
+    elif "cpu_baseline" not in result:
+        result["cpu_baseline"] = None
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def setup_generator(args, dev, rank):
+    """C2 forward (default) or C3/C4 training step of the Generator."""
     from autovc_amd.auto_encoder import AutoEncoder
     from autovc_amd.weights import onehot_embedding, synthetic_embedding, synthetic_mel, torch_state_dict
 
@@ -97,114 +221,116 @@ def main():
         def step():
             return model.train_step(x, c)
 
-    for _ in range(args.warmup):
-        out = step()
-    torch.cuda.synchronize()
-
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # Roofline region: the same K steps again with every launch of the kernel classes bracketed
-    # by HIP events on its stream (the events cost ~7 us per launch, so `value` above is taken
-    # from the uninstrumented region).
-    classes = ["gemm", "lstm_step_fwd", "lstm32"] + (["lstm_step_bwd"] if args.mode == "train" else [])
-    inst_elapsed = None
-    if not args.no_timing:
-        _lib.timing_enable(classes)
-        _lib.timing_reset()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
-        torch.cuda.synchronize()
-        inst_elapsed = time.perf_counter() - t1
-        _lib.timing_enable([])
-
-    frames = world * B * T * args.steps
-    value = frames / elapsed
-    fwd_flop_per_frame = 56.77e6
-    result = {
-        "metric": METRIC if args.mode == "fwd" else "mel-frames/sec AutoVC train step, 80×128 batch",
-        "value": round(value, 1),
-        "unit": "mel-frames/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1000 * elapsed / args.steps, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
+    fwd = args.mode == "fwd"
+    return {
+        "step": step, "units_per_step": B * T, "unit": "mel-frames/s", "dtype": "f32",
+        "metric": METRIC if fwd else "mel-frames/sec AutoVC train step, 80×128 batch",
         "data": "synthetic (U[0,1) mels, |N(0,1)| L2-normalised speaker embeddings; seeded synthetic weights)",
-        "config": {
+        "classes": ["gemm", "lstm_step_fwd", "lstm32"] + ([] if fwd else ["lstm_step_bwd"]),
+        "flop_per_unit": 56.77e6 if fwd else 192.2e6,
+        "config": lambda world: {
             "workload": ("C2: batch=64 synthetic 80x128 mels, Generator forward (conversion path, train-mode BN "
-                         "as convert() runs), whole-Generator HIP path") if args.mode == "fwd" else
+                         "as convert() runs), whole-Generator HIP path") if fwd else
                         ("C3/C4: batch=256/GPU training step: fwd + loss (2nd encoder pass) + bwd + "
                          "RCCL all-reduce + fused clip/Adam/EMA"),
             "global_batch": world * B,
             "frames_per_utterance": T,
-            "parallelism": (f"replicas x{world}" if args.mode == "fwd" else f"dp{world}"),
-            "algorithmic_gflop_per_step": round((fwd_flop_per_frame if args.mode == "fwd" else 192.2e6) * B * T / 1e9, 1),
+            "parallelism": (f"replicas x{world}" if fwd else f"dp{world}"),
+            "algorithmic_gflop_per_step": round((56.77e6 if fwd else 192.2e6) * B * T / 1e9, 1),
         },
-        "achieved_tflops_whole_step": round((fwd_flop_per_frame if args.mode == "fwd" else 192.2e6) * value / world / 1e12, 2),
+        "cpu": (lambda out: _with_dmel(cpu_baseline(args, sd, x_np, out, B, T, rank))) if fwd else None,
     }
 
-    if not args.no_timing:
-        per = {c: _lib.timing_read(c) for c in classes}
-        kern = {}
-        for c, r in per.items():
-            if r["launches"] == 0 or r["ms"] <= 0:
-                continue
-            kern[c] = {"launches_per_step": r["launches"] / args.steps, "avg_us": round(1000 * r["ms"] / r["launches"], 2),
-                       "share_of_step": round(r["ms"] / (1000 * inst_elapsed), 3),
-                       "tflops": round(r["flops"] / (r["ms"] * 1e-3) / 1e12, 2),
-                       "gbs_weights": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1)}
-        dom = max(kern, key=lambda c: per[c]["ms"]) if kern else None
-        if dom:
-            r = per[dom]
-            bound, peak = ROOFLINE[args.mode][dom]
-            if bound == "hbm":
-                achieved = r["bytes"] / (r["ms"] * 1e-3) / 1e9
-                unit = "GB/s"
-            else:
-                achieved = r["flops"] / (r["ms"] * 1e-3) / 1e12
-                unit = "TFLOP/s" + (" (fp32-equivalent, 3 f16 products each)" if peak < 1000 and peak > 500 else "")
-            result["roofline"] = {
-                "kernel": dom, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
-                "unit": unit, "frac": round(achieved / peak, 4),
-                "traffic": None,
-                "avg_launch_us": kern[dom]["avg_us"],
-                "flop_per_launch": round(r["flops"] / r["launches"]),
-                "algorithmic_bytes_per_launch": round(r["bytes"] / r["launches"]),
-            }
-            tr = pmc_traffic(dom, args)
-            if tr:
-                result["roofline"]["traffic"] = tr["traffic_bytes"]
-                result["roofline"]["traffic_source"] = tr["source"]
-        result["kernels"] = kern
-        result["instrumented_ms_per_step"] = round(1000 * inst_elapsed / args.steps, 3)
 
-    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "fwd":
-        result["cpu_baseline"], result["max_abs_dmel_vs_cpu"] = cpu_baseline(args, sd, x_np, out, B, T, rank)
-    elif "cpu_baseline" not in result:
-        result["cpu_baseline"] = None
+def _with_dmel(r):
+    return r[0], {"max_abs_dmel_vs_cpu": r[1]}
 
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if dist:
-        dist.destroy_process_group()
+
+def setup_mel(args, dev, rank):
+    """AE mel frontend (spectrogram.py:62-142) of one 60 s synthetic-speech utterance."""
+    from autovc_amd.audio import spectrogram as sp
+    from autovc_amd.weights import synthetic_speech
+
+    sr, hop = 22050, 275
+    wav_np = synthetic_speech(11 + rank, MEL_SECONDS * sr, sr)
+    wav = torch.from_numpy(wav_np).to(dev)
+    F = 1 + len(wav_np) // hop
+
+    def step():
+        return sp.mel_spec_auto_encoder(wav, device=dev)
+
+    def cpu(out):
+        from oracle import audio_oracle as ao
+        ao.mel_spec_auto_encoder(wav_np[: sr * 5])  # warm
+        times = []
+        t_start = time.perf_counter()
+        while len(times) < 2 or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 20):
+            t1 = time.perf_counter()
+            ref = ao.mel_spec_auto_encoder(wav_np)
+            times.append(time.perf_counter() - t1)
+        times.sort()
+        med = times[len(times) // 2]
+        d = float((out.float().cpu() - ref).abs().max())
+        return ({"value": round(F / med, 1), "unit": "mel-frames/s", "cores": 1, "kind": "port",
+                 "sample": f"{len(times)} timed reps of the same 60 s utterance through the float64 numpy "
+                           f"restatement (oracle/audio_oracle.py; numpy rfft, single thread), median"},
+                {"max_abs_dmel_vs_cpu": d})
+
+    return {
+        "step": step, "units_per_step": F, "unit": "mel-frames/s", "dtype": "f64 DFT / f32 mel",
+        "metric": "mel-frames/sec AE mel frontend (|STFT| n_fft 2048 hop 275 win 1100 -> 80 mels -> dB-normalised)",
+        "data": "synthetic speech-like waveform (autovc_amd.weights.synthetic_speech), 22.05 kHz",
+        "classes": ["dft64", "gemm"], "flop_per_unit": 2.0 * 2 * 1025 * 1100 + 2.0 * 1028 * 80,
+        "config": lambda world: {"workload": f"one {MEL_SECONDS} s utterance per GPU ({F} frames), "
+                                             "mel_spec_auto_encoder", "global_batch": world,
+                                 "frames_per_utterance": F, "parallelism": f"replicas x{world}"},
+        "cpu": cpu,
+    }
+
+
+def setup_se(args, dev, rank):
+    """Speaker encoder embed_utterance (speaker_encoder/model.py:142-194) of one 10 s utterance."""
+    from autovc_amd.speaker_encoder import SpeakerEncoder
+    from autovc_amd.weights import speaker_encoder_state_dict, synthetic_speech
+
+    sr = 16000
+    sd = speaker_encoder_state_dict(0)
+    se = SpeakerEncoder(device=dev, verbose=False)
+    se.load_state_dict(sd)
+    wav_np = synthetic_speech(21 + rank, SE_SECONDS * sr, sr)
+
+    def step():
+        return se.embed_utterance(wav_np)
+
+    def cpu(out):
+        from oracle import audio_oracle as ao
+        cores = min(16, len(os.sched_getaffinity(0)))
+        torch.set_num_threads(cores)
+        ref = ao.embed_utterance(sd, wav_np)
+        times = []
+        t_start = time.perf_counter()
+        while len(times) < 2 or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 20):
+            t1 = time.perf_counter()
+            ao.embed_utterance(sd, wav_np)
+            times.append(time.perf_counter() - t1)
+        times.sort()
+        med = times[len(times) // 2]
+        d = float(abs(out.numpy() - ref).max())
+        return ({"value": round(SE_SECONDS / med, 2), "unit": "audio-seconds/s", "cores": cores, "kind": "port",
+                 "sample": f"{len(times)} timed reps of the same 10 s utterance through the oracle (numpy float64 "
+                           f"mel + torch-CPU LSTM, {torch.get_num_threads()} threads), median"},
+                {"max_abs_dembed_vs_cpu": d})
+
+    return {
+        "step": step, "units_per_step": SE_SECONDS, "unit": "audio-seconds/s", "dtype": "f32 (f64 DFT)",
+        "metric": "audio-seconds/sec speaker-encoder embed_utterance (16 kHz, 160-frame partials, 3x256 LSTM)",
+        "data": "synthetic speech-like waveform, 16 kHz; seeded synthetic weights",
+        "classes": ["lstm_step_fwd", "gemm", "dft64"],
+        "config": lambda world: {"workload": f"one {SE_SECONDS} s utterance per GPU per step (12 partials x 160 "
+                                             "frames), embed_utterance incl. its mel frontend",
+                                 "global_batch": world, "parallelism": f"replicas x{world}"},
+        "cpu": cpu,
+    }
 
 
 def pmc_traffic(cls, args):

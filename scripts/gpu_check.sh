@@ -35,6 +35,10 @@ for step in "$@"; do
     stamps) run stamps 300 python scripts/stamps_lstm.py ;;
     audio) run audio 600 python -m pytest tests/test_gpu_audio.py -v -m gpu -s --timeout 200 -p no:cacheprovider ;;
     benchtrain) run benchtrain 400 python bench.py --mode train --steps 5 --warmup 2 --no-cpu ;;
+    benchmel) run benchmel 400 python bench.py --mode mel --steps 10 --warmup 2 ;;
+    benchse) run benchse 400 python bench.py --mode se --steps 10 --warmup 2 ;;
+    profmel) run profmel 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profmel -o mel -- python3 bench.py --mode mel --steps 10 --warmup 2 --no-cpu --no-timing ;;
+    profse) run profse 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profse -o se -- python3 bench.py --mode se --steps 10 --warmup 2 --no-cpu --no-timing ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
