@@ -846,7 +846,10 @@ struct Plan {
 
 Plan make_plan(const GemmDesc& d, int force_split) {
   Plan p;
-  const bool big = (long)d.M * d.N >= 256L * 128 * 128 / 2;
+  // long-K products (weight gradients: K = T*B rows) take 128x128 tiles and split K until the
+  // grid has ~4 workgroups per CU
+  const bool longk = (long)d.Kc * d.ntaps >= 8192 && d.M >= 128 && d.N >= 128;
+  const bool big = (long)d.M * d.N >= 256L * 128 * 128 / 2 || longk;
   p.bm = big ? 128 : 64;
   p.bn = big ? 128 : 64;
   p.tilesM = (d.M + p.bm - 1) / p.bm;
@@ -857,6 +860,11 @@ Plan make_plan(const GemmDesc& d, int force_split) {
   int ns = 1;
   if (force_split > 0) {
     ns = force_split;
+  } else if (!d.stats && longk && blocks < 1024) {
+    ns = (int)((1024 + blocks - 1) / blocks);
+    ns = std::min(ns, p.ktotal / 16);
+    ns = std::min(ns, 32);
+    ns = std::max(ns, 1);
   } else if (!d.stats && blocks < 256 && p.ktotal >= 16) {
     ns = (int)((512 + blocks - 1) / blocks);
     ns = std::min(ns, p.ktotal / 8);
