@@ -108,9 +108,11 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
 size_t conv_bn_backward_scratch(int T, int B, int cin, int cout) {
   const size_t TB = (size_t)T * B;
   GemmDesc w;
-  w.M = cout; w.N = cin; w.Kc = (int)TB; w.a_trans = 1; w.nz = 5;
+  w.M = cout; w.N = cin; w.Kc = (int)TB; w.a_trans = 1; w.nz = 5; w.b_rows = TB; w.b_zshift = B;
+  w.prec16 = 1; w.split_scale = 1;
   GemmDesc dg;
-  dg.M = (int)TB; dg.N = cin; dg.Kc = cout; dg.ntaps = 5;
+  dg.M = (int)TB; dg.N = cin; dg.Kc = cout; dg.ntaps = 5; dg.a_rows = TB;
+  dg.prec16 = 1; dg.split_scale = 1;
   return (TB * cout + 5UL * cin * cout) * sizeof(float) + bn_backward_scratch((int)TB, cout) +
          colsum_scratch((int)TB, cout) + std::max(gemm_scratch_bytes(w), gemm_scratch_bytes(dg)) + 2048;
 }
@@ -138,6 +140,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
     g.A = dy; g.lda = cout; g.a_rows = TB; g.a_shift0 = -2L * B; g.a_tapshift = B;
     g.B = wd; g.ldb = cin; g.b_rows = cout; g.b_tapoff = (long)cout * cin;
     g.C = d_x; g.ldc = cin; g.accumulate = accumulate;
+    g.prec16 = 1; g.split_scale = 1;
     AVC_TRY(gemm_run(ctx, g, s));
   }
   if (d_weight) {
@@ -148,6 +151,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
     g.B = x; g.ldb = cin; g.b_rows = TB; g.b_shift0 = -2L * B; g.b_zshift = B;
     g.nz = 5; g.c_zoff = 1;
     g.C = d_weight; g.ldc = 5L * cin; g.ldc_col = 5; g.accumulate = accumulate;
+    g.prec16 = 1; g.split_scale = 1;
     AVC_TRY(gemm_run(ctx, g, s));
   }
   return AVC_OK;

@@ -24,7 +24,10 @@ struct GemmDesc {
   int nz = 1; long a_zoff = 0; long c_zoff = 0;
   float* C = nullptr; long ldc = 0; long ldc_col = 1; int accumulate = 0;
   const float* bias0 = nullptr; const float* bias1 = nullptr; int act = AVC_ACT_NONE;
-  int prec16 = 0;           // 1: split-fp16 ("3xf16") MFMA kernel; forward operands only (|x| < 65504)
+  int prec16 = 0;           // 1: split-fp16 ("3xf16") MFMA kernel (forward operands: |x| < 65504)
+  int split_scale = 0;      // with prec16: scale each operand by a power of two from its device-side
+                            // max |x| before splitting (gradients: any magnitude), unscale exactly
+  const unsigned* amax = nullptr;  // filled by gemm_run: [2] max |A|, max |B| as float bits
   const _Float16* b_frag = nullptr;  // optional B already split by gemm_prepare_bfrag (prec16 only)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
   int stats_bm = 0;         // filled by gemm_run: rows per stats partial

@@ -34,6 +34,20 @@ __device__ __forceinline__ float act_apply(float v, int act) {
   return v;
 }
 
+// power-of-two operand scale for the split-f16 products: max |x| -> [2^14, 2^15)
+__device__ __forceinline__ float split_scale_of(const unsigned* amax, int i) {
+  if (!amax) return 1.f;
+  const float m = __uint_as_float(amax[i]);
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, 15 - e);
+}
+
+__device__ __forceinline__ float split_unscale(const unsigned* amax) {
+  return amax ? 1.f / (split_scale_of(amax, 0) * split_scale_of(amax, 1)) : 1.f;
+}
+
 template <int BM, int BN, int WM, int WN, int AT, int BT>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tilesM, int tilesN,
                                                             int kt_per_tap, int kps, int nsplit,
@@ -546,8 +560,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
 // land as zeros.
 __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restrict__ src, long rs,
                                                            long ks, int R, int K, int ntile, int nkc,
-                                                           _Float16* __restrict__ dst) {
+                                                           _Float16* __restrict__ dst,
+                                                           const unsigned* __restrict__ amax = nullptr,
+                                                           int which = 0) {
   const int G8 = nkc * 2;  // 8-element groups per row (a multiple of 4)
+  const float sc = split_scale_of(amax, which);
   const long total = (long)ntile * 32 * G8;
   const bool vec = ks == 1 && (rs & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -584,6 +601,10 @@ __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restri
         v[e] = (r < R && k < K) ? src[r * rs + (long)k * ks] : 0.f;
       }
     }
+    if (amax) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= sc;
+    }
     f16x8 hi, lo;
     split8(v, hi, lo);
     const long blk = ((r >> 5) * nkc + (g8 >> 1)) * 2;
@@ -593,9 +614,29 @@ __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restri
   }
 }
 
+// max |x| over a rows x cols region (row stride ld) into *out (float bits; out pre-zeroed)
+__global__ __launch_bounds__(256) void absmax2d_kernel(const float* __restrict__ src, long rows, long cols, long ld,
+                                                       unsigned* __restrict__ out) {
+  float m = 0.f;
+  const long total = rows * cols;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const long r = idx / cols, c = idx - r * cols;
+    m = fmaxf(m, fabsf(src[r * ld + c]));
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t s) {
+  const long total = rows * cols;
+  absmax2d_kernel<<<(int)std::max<long>(1, std::min<long>((total + 255) / 256, 2048)), 256, 0, s>>>(src, rows, cols,
+                                                                                                   ld, out);
+}
+
 struct Frag16Args {
   const _Float16* As; int a_ntile, a_nkc; long a_shift0, a_tapshift;  // shifts in rows (x32)
   const _Float16* Bs; int b_ntile, b_nkc; long b_tapstride;            // halves per tap
+  int b_shift0_c, b_zshift_c;  // B K-shift of product z in 16-deep chunks (weight gradients)
 };
 
 template <int BM, int BN, int WM, int WN, int NS, int KC>
@@ -620,7 +661,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
   const int tm = wgid / tilesN, tn = wgid - tm * tilesN;
-  const int split = blockIdx.y;
+  const int split = blockIdx.y % nsplit, z = blockIdx.y / nsplit;
   const int ktotal = d.ntaps * kt_per_tap;
   const int kt0 = split * kps;
   const int kt1 = min(ktotal, kt0 + kps);
@@ -634,6 +675,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
   constexpr unsigned kOut = 0x7FFFFF00u;
   const int a_ntile = f.a_ntile, a_nkc = f.a_nkc, b_ntile = f.b_ntile, b_nkc = f.b_nkc;
   const long a_shift0 = f.a_shift0, a_tapshift = f.a_tapshift, b_tapstride = f.b_tapstride;
+  const int bzs = f.b_shift0_c + z * f.b_zshift_c;  // uniform per workgroup
 
   // issue the LDS-DMA of K-tile kt into stage st: this wave's DPW blocks of the NBLK
 #define AVC16F_ISSUE(KT, ST)                                                                      \
@@ -655,9 +697,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
         const int bb = b - ABLK;                                                                  \
         const int ct = bb / (2 * KC), kc = (bb >> 1) % KC, hl = bb & 1;                           \
         const int src_tile = tn * (BN / 32) + ct;                                                 \
-        const bool ok = src_tile < b_ntile && kc0 + kc < b_nkc;                                   \
+        const int bkc = kc0 + kc + bzs;                                                           \
+        const bool ok = src_tile < b_ntile && bkc >= 0 && bkc < b_nkc;                            \
         const unsigned off = ok ? (unsigned)(tau * b_tapstride * 2 +                              \
-                                             ((long)(src_tile * b_nkc + kc0 + kc) * 2 + hl) * 1024) : kOut; \
+                                             ((long)(src_tile * b_nkc + bkc) * 2 + hl) * 1024) : kOut; \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16, \
                                                  off + lane * 16, 0, 0, 0);                       \
       }                                                                                           \
@@ -742,12 +785,21 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = (acc[i][j][e] - cmp[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
 #undef AVC16F_ISSUE
+  if (d.amax && nsplit == 1) {  // split-K partials stay scaled; splitk_reduce_kernel unscales
+    const float us = split_unscale(d.amax);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] *= us;
+  }
 
   // ---- epilogue (32x32 C layout: col = lane&31, row = (e&3) + 8(e>>2) + 4(lane>>5)) --------
   const int row_base = tm * BM + wm * WTM + 4 * (lane >> 5);
   const int col_base = tn * BN + wn * WTN + (lane & 31);
   if (nsplit > 1) {
-    float* out = slab + (long)split * d.M * d.N;
+    float* out = slab + ((long)split * d.nz + z) * d.M * d.N;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -762,7 +814,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
       }
     return;
   }
-  float* __restrict__ C = d.C;
+  float* __restrict__ C = d.C + (long)z * d.c_zoff;
   float csum[TN], csq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -828,6 +880,7 @@ __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __rest
     const int m = (int)(rem / d.N), n = (int)(rem - (long)m * d.N);
     float s = 0.f;
     for (int sp = 0; sp < nsplit; ++sp) s += slab[((long)sp * d.nz + z) * MN + rem];
+    if (d.amax) s *= split_unscale(d.amax);
     if (d.bias0) s += d.bias0[n];
     if (d.bias1) s += d.bias1[n];
     s = act_apply(s, d.act);
@@ -837,7 +890,8 @@ __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __rest
 }
 
 // avc_gemm_tune(): forward (prec16) products on 0 = the fp32 kernel, 1 = gemm16 (operands split
-// while staged), 2 = gemm16f on pre-split fragment-major operands where eligible (default)
+// while staged), 2 = gemm16f on pre-split fragment-major operands where eligible (default);
+// 3 = as 2 for forward products but backward (split_scale) products on the fp32 kernel
 int g_gemm16 = 2;
 
 struct Plan {
@@ -882,14 +936,30 @@ inline int frag_nkc(int K) { return (K + 31) / 32 * 2; }
 inline size_t frag_bytes(long rows, int K) { return (size_t)frag_ntile(rows) * frag_nkc(K) * 2048; }
 
 bool frag16_eligible(const GemmDesc& d) {
-  return d.prec16 && g_gemm16 == 2 && !d.a_trans && d.nz == 1 && d.b_shift0 == 0 && d.b_zshift == 0 &&
-         d.a_shift0 % 32 == 0 && (d.ntaps == 1 || d.a_tapshift % 32 == 0) &&
-         (d.b_trans || d.b_rows >= d.Kc);
+  if (!d.prec16 || d.a_zoff != 0) return false;
+  if (g_gemm16 != 2 && !(g_gemm16 == 3 && !d.split_scale)) return false;
+  if (d.a_trans) {
+    if (d.ntaps != 1 || d.a_shift0 != 0) return false;
+  } else if (d.a_shift0 % 32 != 0 || (d.ntaps > 1 && d.a_tapshift % 32 != 0)) {
+    return false;
+  }
+  const bool bshift = d.b_shift0 != 0 || d.b_zshift != 0;
+  if (bshift && (d.b_trans || d.b_shift0 % 16 != 0 || d.b_zshift % 16 != 0 || d.ntaps != 1)) return false;
+  if (d.nz > 1 && !bshift) return false;
+  return d.b_trans || bshift || d.b_rows >= d.Kc;
+}
+
+// rows of the B operand's source that its fragments cover
+inline long frag16_b_krows(const GemmDesc& d) {
+  const long b_rows = d.b_rows ? d.b_rows : (d.b_trans ? d.N : d.Kc);
+  if (d.b_trans) return d.Kc;
+  if (d.b_shift0 != 0 || d.b_zshift != 0) return b_rows;
+  return std::min<long>(d.Kc, b_rows);
 }
 
 size_t frag16_scratch(const GemmDesc& d) {
-  const long a_rows = d.a_rows ? d.a_rows : d.M;
-  return frag_bytes(a_rows, d.Kc) + (size_t)d.ntaps * frag_bytes(d.N, d.Kc) + 1024;
+  const long a_rows = d.a_trans ? d.M : (d.a_rows ? d.a_rows : d.M);
+  return frag_bytes(a_rows, d.Kc) + (size_t)d.ntaps * frag_bytes(d.N, (int)frag16_b_krows(d)) + 2048;
 }
 
 int g_gemm_cfg = 1;  // avc_gemm_config(): tile/ring variant of gemm16f for 128x128 tiles (1 measured best)
@@ -909,7 +979,7 @@ void launch16f_cfg(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
   const int kt_per_tap = (f.a_nkc + KC - 1) / KC;
   const int ktotal = d.ntaps * kt_per_tap;
   const int kps = (ktotal + p.nsplit - 1) / p.nsplit;
-  dim3 grid(p.tilesM * p.tilesN, p.nsplit);
+  dim3 grid(p.tilesM * p.tilesN, d.nz * p.nsplit);
   gemm16f_kernel<BM, BN, WM, WN, NS, KC><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, kt_per_tap,
                                                                         kps, p.nsplit, slab);
 }
@@ -979,7 +1049,7 @@ int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
 size_t gemm_scratch_bytes(const GemmDesc& d) {
   Plan p = make_plan(d, 0);
   size_t s = p.nsplit <= 1 ? 0 : (size_t)p.nsplit * d.nz * d.M * d.N * sizeof(float) + 256;
-  if (d.prec16 && !d.a_trans) s += frag16_scratch(d);
+  if (d.prec16) s += frag16_scratch(d);
   return s;
 }
 
@@ -1007,32 +1077,53 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
   const bool frag = frag16_eligible(d);
   if (frag) {
     // split both operands once into the fragment-major layout gemm16f_kernel streams
-    const long a_ntile = frag_ntile(d.a_rows);
+    if (d.split_scale) {  // power-of-two operand scales from max |A|, max |B| (device side)
+      unsigned* amax = sc.take<unsigned>(64);
+      if (!amax) return AVC_ERR_WORKSPACE;
+      AVC_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(unsigned), stream));
+      if (d.a_trans) absmax2d(d.A, d.Kc, d.M, d.lda, amax, stream);
+      else absmax2d(d.A, d.a_rows, d.Kc, d.lda, amax, stream);
+      const long kb = frag16_b_krows(d);
+      for (int tau = 0; tau < d.ntaps; ++tau) {
+        if (d.b_trans) absmax2d(d.B + (long)tau * d.b_tapoff, d.N, d.Kc, d.ldb, amax + 1, stream);
+        else absmax2d(d.B + (long)tau * d.b_tapoff, kb, d.N, d.ldb, amax + 1, stream);
+      }
+      d.amax = amax;
+    }
+    const long a_src_rows = d.a_trans ? d.M : d.a_rows;
+    const long a_ntile = frag_ntile(a_src_rows);
     const int nkc = frag_nkc(d.Kc);
     const long b_ntile = frag_ntile(d.N);
-    _Float16* as = sc.take<_Float16>(frag_bytes(d.a_rows, d.Kc) / 2);
+    const long b_krows = frag16_b_krows(d);
+    const int b_nkc = frag_nkc((int)b_krows);
+    _Float16* as = sc.take<_Float16>(frag_bytes(a_src_rows, d.Kc) / 2);
     if (!as) return AVC_ERR_WORKSPACE;
     const long ta = a_ntile * 32 * nkc * 2;
     split_frag32_kernel<<<(int)std::min<long>((ta + 255) / 256, 8192), 256, 0, stream>>>(
-        d.A, d.lda, 1, (int)d.a_rows, d.Kc, (int)a_ntile, nkc, as);
-    const long tapstride = b_ntile * nkc * 1024;  // halves
-    const _Float16* bs = d.b_frag;
+        d.A, d.a_trans ? 1 : d.lda, d.a_trans ? d.lda : 1, (int)a_src_rows, d.Kc, (int)a_ntile, nkc, as, d.amax, 0);
+    const long tapstride = b_ntile * b_nkc * 1024;  // halves
+    const _Float16* bs = d.split_scale ? nullptr : d.b_frag;
     if (!bs) {
-      _Float16* tmp = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, d.Kc) / 2);
+      _Float16* tmp = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, (int)b_krows) / 2);
       if (!tmp) return AVC_ERR_WORKSPACE;
-      AVC_TRY(gemm_prepare_bfrag(d, tmp, stream));
+      const long tb = b_ntile * 32 * b_nkc * 2;
+      for (int tau = 0; tau < d.ntaps; ++tau)
+        split_frag32_kernel<<<(int)std::min<long>((tb + 255) / 256, 8192), 256, 0, stream>>>(
+            d.B + (long)tau * d.b_tapoff, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N, (int)b_krows,
+            (int)b_ntile, b_nkc, tmp + tau * tapstride, d.amax, 1);
       bs = tmp;
     }
     AVC_LAUNCH_CHECK();
     fa.As = as; fa.a_ntile = (int)a_ntile; fa.a_nkc = nkc;
     fa.a_shift0 = d.a_shift0; fa.a_tapshift = d.a_tapshift;
-    fa.Bs = bs; fa.b_ntile = (int)b_ntile; fa.b_nkc = nkc; fa.b_tapstride = tapstride;
+    fa.Bs = bs; fa.b_ntile = (int)b_ntile; fa.b_nkc = b_nkc; fa.b_tapstride = tapstride;
+    fa.b_shift0_c = (int)(d.b_shift0 / 16); fa.b_zshift_c = (int)(d.b_zshift / 16);
   }
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
   if (frag) {
     if (p.bm == 128) launch16f_128(d, fa, p, slab, stream);
     else launch16f_cfg<64, 64, 2, 2, 4, 2>(d, fa, p, slab, stream);
-  } else if (d.prec16 && !d.a_trans && g_gemm16) {
+  } else if (d.prec16 && !d.split_scale && !d.a_trans && g_gemm16) {
     if (p.bm == 128) launch16<128, 128, 4, 2>(d, p, slab, stream);
     else launch16<64, 64, 2, 2>(d, p, slab, stream);
   } else if (p.bm == 128) {
@@ -1058,8 +1149,8 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
 }  // namespace avc
 
 extern "C" int avc_gemm_tune(int mode) {
-  if (mode < 0 || mode > 2) {
-    avc::set_error("avc_gemm_tune: mode must be 0, 1 or 2");
+  if (mode < 0 || mode > 3) {
+    avc::set_error("avc_gemm_tune: mode must be 0..3");
     return AVC_ERR_INVALID;
   }
   avc::g_gemm16 = mode;

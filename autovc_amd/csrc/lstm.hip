@@ -831,9 +831,11 @@ size_t lstm_backward_scratch(int T, int B, int din, int H) {
   size_t s = TB * 4 * H * f + (size_t)B * H * f + (size_t)4 * H * (din + H) * 2 * f +
              (size_t)4 * H * f + 8192;
   GemmDesc d1;  // dW_ih
-  d1.M = 4 * H; d1.N = din; d1.Kc = (int)TB; d1.a_trans = 1;
-  GemmDesc d2 = d1; d2.N = H;
-  GemmDesc d3; d3.M = (int)TB; d3.N = din; d3.Kc = 4 * H;
+  d1.M = 4 * H; d1.N = din; d1.Kc = (int)TB; d1.a_trans = 1; d1.b_rows = TB;
+  d1.prec16 = 1; d1.split_scale = 1;
+  GemmDesc d2 = d1; d2.N = H; d2.b_shift0 = B;
+  GemmDesc d3; d3.M = (int)TB; d3.N = din; d3.Kc = 4 * H; d3.a_rows = TB;
+  d3.prec16 = 1; d3.split_scale = 1;
   size_t gs = std::max(gemm_scratch_bytes(d1), std::max(gemm_scratch_bytes(d2), gemm_scratch_bytes(d3)));
   return s + gs + colsum_scratch((int)TB, 4 * H);
 }
@@ -903,6 +905,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   g1.A = dg; g1.a_trans = 1; g1.lda = 4 * H;
   g1.B = x; g1.ldb = ldx; g1.b_rows = TB;
   g1.C = dwih_dst; g1.ldc = din; g1.accumulate = acc_w;
+  g1.prec16 = 1; g1.split_scale = 1;
   AVC_TRY(gemm_run(ctx, g1, s));
   GemmDesc g2 = g1;
   g2.N = H;
@@ -929,6 +932,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     g3.B = wih_use; g3.ldb = din;
     g3.b_trans = small ? 0 : 0;
     g3.C = d_x; g3.ldc = din; g3.accumulate = accumulate_dx;
+    g3.prec16 = 1; g3.split_scale = 1;
     AVC_TRY(gemm_run(ctx, g3, s));
   }
   return AVC_OK;

@@ -205,7 +205,7 @@ int avc_prepared_release(avc_context* ctx);
  * When bit `cls` of mask is set, every launch of that kernel class is bracketed by HIP events on
  * its stream; avc_timing_read sums the event-measured durations and the algorithmic FLOPs/bytes
  * of the recorded launches.  Classes: 0 GEMM (gemm_kernel), 1 LSTM step forward,
- * 2 LSTM step backward, 3 H=32 persistent LSTM. */
+ * 2 LSTM step backward, 3 H=32 persistent LSTM, 4 fp64 DFT of the mel frontends. */
 int avc_timing_enable(int mask);
 /* Tuning hook for the per-step LSTM kernel: force the batch rows per workgroup (16/32/64) and the
  * number of waves splitting the reduction (1..8); 0 restores the automatic choice. */
@@ -215,8 +215,9 @@ int avc_lstm_tune(int rows_per_block, int waves);
  * rows64 = 1 keeps 64 batch rows per workgroup on the narrow tiles (else 32 when that fills
  * more CUs). */
 int avc_lstm_split_tune(int kslice, int col_blocks, int rows64);
-/* Tuning hook for forward products: 0 runs them on the fp32 MFMA kernel instead of the
- * split-fp16 one (default 1). */
+/* Tuning hook for split-f16 products: 0 = every product on the fp32 MFMA kernel; 1 = forward
+ * products split while staged; 2 = forward products on pre-split fragments and backward products
+ * scaled-split (default); 3 = as 2 but backward products on the fp32 kernel. */
 int avc_gemm_tune(int prec16);
 /* Tuning hook: variant of the pre-split split-f16 GEMM for 128x128 tiles (8 waves each):
  * 0 = 4x2 waves, 4-stage ring of 32-deep K-tiles; 1 = 4x2, 2 stages of 64-deep K-tiles (default);

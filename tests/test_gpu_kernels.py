@@ -81,7 +81,7 @@ def test_conv_bn_act_forward_backward(cuda_device, B, T, cin, cout, act, trainin
             o32 = ops.ConvBNAct.apply(xg.detach(), *[p.detach() for p in pg], rm_g.clone(), rv_g.clone(),
                                       training, 0.1, 1e-5, act, rg, T, B)
     finally:
-        _lib.call("avc_gemm_tune", 1)
+        _lib.call("avc_gemm_tune", 2)
     err32 = (o32.cpu().reshape(T, B, cout).permute(1, 2, 0).double() - y.detach()).abs().max().item()
     print(f"conv {cin}->{cout}: max err split-f16 GEMM {err16:.2e}, fp32 GEMM {err32:.2e}")
     # CPU fp32 (oneDNN) reaches ~2.5e-6 on these layers: the compensated fp32 kernel stays below
@@ -325,3 +325,84 @@ def test_gemm16f_configs(cuda_device, cfg):
     assert err < 2e-6 * max(1.0, ref.abs().max().item()), err
     out_cf = out.cpu().reshape(T, B, cout).permute(1, 2, 0).double()
     assert (out_cf - yc).abs().max().item() < 1e-5
+
+
+def _conv_grads(dev, B, T, cin, cout, gscale, mode):
+    g = torch.Generator().manual_seed(B * 7 + T + cin + cout)
+    x = torch.rand(B, cin, T, generator=g)
+    W = (torch.rand(cout, cin, 5, generator=g) - 0.5) * 0.1
+    bias = (torch.rand(cout, generator=g) - 0.5) * 0.1
+    gamma = torch.rand(cout, generator=g) + 0.5
+    beta = (torch.rand(cout, generator=g) - 0.5) * 0.4
+    dout = torch.randn(B, cout, T, generator=g) * gscale
+    params = [t.double().clone().requires_grad_(True) for t in (x, W, bias, gamma, beta)]
+    y = torch.relu(F.batch_norm(F.conv1d(params[0], params[1], params[2], padding=2), None, None, params[3],
+                                params[4], training=True, eps=1e-5))
+    y.backward(dout.double())
+    fr = x.permute(2, 0, 1).reshape(T * B, cin)
+    xg = _t(fr, dev).requires_grad_(True)
+    pg = [_t(t, dev).requires_grad_(True) for t in (W, bias, gamma, beta)]
+    _lib.call("avc_gemm_tune", mode)
+    try:
+        out = ops.ConvBNAct.apply(xg, *pg, None, None, True, 0.1, 1e-5, ops.ACT_RELU, None, T, B)
+        out.backward(_t(dout.permute(2, 0, 1).reshape(T * B, cout), dev))
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("avc_gemm_tune", 2)
+    dx = xg.grad.cpu().reshape(T, B, cin).permute(1, 2, 0).double()
+    rel = lambda a, r: (a - r).abs().max().item() / max(r.abs().max().item(), 1e-300)
+    return rel(dx, params[0].grad), rel(pg[0].grad.cpu().double(), params[1].grad)
+
+
+@pytest.mark.parametrize("B,T,cin,cout,gscale", [(32, 16, 512, 512, 1.0), (64, 8, 80, 512, 1.0),
+                                                 (32, 16, 512, 80, 1e-9), (32, 8, 336, 512, 1e7)])
+def test_conv_backward_split_path(cuda_device, B, T, cin, cout, gscale):
+    """Batch a multiple of 32: dgrad (tap shifts = whole fragment tiles) and wgrad (dY^T with a
+    per-tap K shift of B rows) run as scaled split-f16 products.  Errors relative to the
+    largest gradient, against fp64, must match the compensated fp32 kernel's within 2x, at any
+    gradient magnitude (the power-of-two operand scales)."""
+    e16 = _conv_grads(cuda_device, B, T, cin, cout, gscale, 2)
+    e32 = _conv_grads(cuda_device, B, T, cin, cout, gscale, 0)
+    print(f"conv bwd B={B} {cin}->{cout} scale {gscale:g}: split dx {e16[0]:.1e} dW {e16[1]:.1e}; "
+          f"fp32 dx {e32[0]:.1e} dW {e32[1]:.1e}")
+    assert e16[0] < max(2 * e32[0], 2e-6) and e16[1] < max(2 * e32[1], 2e-6)
+
+
+@pytest.mark.parametrize("B,T,din,H", [(32, 6, 320, 512), (32, 5, 512, 1024)])
+def test_lstm_backward_split_path(cuda_device, B, T, din, H):
+    """LSTM weight gradients (dG^T x, dG^T h_prev with a one-step K shift) and dX on the
+    scaled split-f16 products at a batch that is a multiple of 16, against fp64."""
+    g = torch.Generator().manual_seed(B + T + H)
+    x = torch.randn(B, T, din, generator=g) * 0.5
+    k = 1.0 / np.sqrt(H)
+    ws = [(torch.rand(*s, generator=g) * 2 - 1) * k for s in [(4 * H, din), (4 * H, H), (4 * H,), (4 * H,)]]
+    dy = torch.randn(B, T, H, generator=g) * 1e-6
+    flat = [w.double().clone().requires_grad_(True) for w in ws]
+    xr = x.double().clone().requires_grad_(True)
+    h0 = torch.zeros(1, B, H, dtype=torch.float64)
+    yr, _, _ = torch.lstm(xr, (h0, h0.clone()), flat, True, 1, 0.0, False, False, True)
+    yr.backward(dy.double())
+    xg = _t(x.transpose(0, 1).reshape(T * B, din), cuda_device).requires_grad_(True)
+    wg = [_t(w, cuda_device).requires_grad_(True) for w in ws]
+    yg = ops.LSTMLayer.apply(xg, *wg, T, B, True)
+    yg.backward(_t(dy.transpose(0, 1).reshape(T * B, H), cuda_device))
+    dx = xg.grad.cpu().reshape(T, B, din).transpose(0, 1).double()
+    rel = lambda a, r: (a - r).abs().max().item() / r.abs().max().item()
+    assert rel(dx, xr.grad) < 5e-5
+    for a, b in zip(wg, flat):
+        assert rel(a.grad.cpu().double(), b.grad) < 5e-5
+
+
+def test_linear_backward_split_path(cuda_device):
+    g = torch.Generator().manual_seed(3)
+    M, din, dout = 2048, 1024, 80
+    x = torch.randn(M, din, generator=g)
+    w = torch.randn(dout, din, generator=g) / 32
+    b = torch.randn(dout, generator=g)
+    dy = torch.randn(M, dout, generator=g) * 1e-8
+    xr, wr = x.double().requires_grad_(True), w.double().requires_grad_(True)
+    (xr @ wr.T + b.double()).backward(dy.double())
+    xg, wgt, bg = (_t(t, cuda_device).requires_grad_(True) for t in (x, w, b))
+    ops.Linear.apply(xg, wgt, bg).backward(_t(dy, cuda_device))
+    rel = lambda a, r: (a.cpu().double() - r).abs().max().item() / r.abs().max().item()
+    assert rel(xg.grad, xr.grad) < 2e-6 and rel(wgt.grad, wr.grad) < 2e-6

@@ -169,6 +169,61 @@ def test_gradients_match_oracle(cuda_device):
     print(f"worst relative gradient error over parameters: {worst:.2e}")
 
 
+def test_gradients_split_backward_path(cuda_device):
+    """B = 32 (T = 64): every backward product of the step runs as a scaled split-f16 product
+    (conv dgrad/wgrad, LSTM dX / dW_ih / dW_hh, Linear).
+
+    The loss is not smooth at this size: its L1 term (sign of Enc(post) - codes) and the ReLU
+    masks flip on forward rounding.  Perturbing the weights by 1e-6 (relative, in float64)
+    moves some parameter gradients by 1.5e-3, and 1e-7 moves them by 2e-6.  A comparison
+    against fp64 therefore mostly measures forward noise.  The backward arithmetic is isolated
+    by running the SAME forward (bitwise identical, so identical masks and signs) with the
+    backward products on the compensated fp32 kernel (avc_gemm_tune(3)).  The split-path
+    gradients must match those within 2e-5 relative L2 per tensor.  Against the float64 oracle
+    both are reported, bounded by 5e-3."""
+    from oracle import autovc_oracle as orc
+    from autovc_amd import _lib
+    from autovc_amd.weights import onehot_embedding, synthetic_mel
+    sd = torch_state_dict(0)
+    X = torch.from_numpy(synthetic_mel(9, 32, 64))
+    c = torch.from_numpy(onehot_embedding(32))
+    tr = orc.Trainer({k: v.double() for k, v in sd.items()})
+    sdc = tr.sd()
+    od, op, oc = orc.forward(sdc, X.double(), c.double(), c.double(), True, tr.bufs)
+    loss_c = orc.loss_fn(sdc, X.double(), c.double(), od, op, oc, tr.bufs)
+    gc = dict(zip(tr.names, torch.autograd.grad(loss_c, [tr.p[k] for k in tr.names])))
+
+    def grads(mode):
+        _lib.call("avc_gemm_tune", mode)
+        try:
+            ae = make_model(cuda_device)
+            Xg, cg = X.to(cuda_device), c.to(cuda_device)
+            md, mp, mc = ae(Xg, cg, cg)
+            loss = ae._loss(Xg, cg, md, mp, mc)
+            loss.backward()
+            torch.cuda.synchronize()
+        finally:
+            _lib.call("avc_gemm_tune", 2)
+        return loss.item(), {k: p.grad.detach().cpu().double() for k, p in ae.named_parameters()}
+
+    l16, g16 = grads(2)
+    l32, g32 = grads(3)
+    assert l16 == l32 and l16 == pytest.approx(loss_c.item(), rel=2e-6)
+    worst_arith, worst_truth = (0.0, ""), (0.0, "")
+    for k, b in gc.items():
+        if k.endswith(".0.conv.bias"):
+            assert g16[k].norm().item() < 1e-5, k
+            continue
+        d = ((g16[k] - g32[k]).norm() / g32[k].norm()).item()
+        t = ((g16[k] - b).norm() / b.norm()).item()
+        worst_arith = max(worst_arith, (d, k))
+        worst_truth = max(worst_truth, (t, k))
+        assert d < 2e-5, f"{k}: split vs fp32 backward products differ by {d:.2e}"
+        assert t < 5e-3, f"{k}: {t:.2e} from the float64 oracle"
+    print(f"B=32: split vs fp32 backward products: worst {worst_arith[0]:.2e} ({worst_arith[1]}); "
+          f"vs float64 oracle: worst {worst_truth[0]:.2e} ({worst_truth[1]})")
+
+
 @pytest.mark.gpu
 def test_fused_forward_sees_weight_updates(cuda_device):
     """The fused forward caches derived weight layouts across calls; every way the drop-in
