@@ -330,6 +330,10 @@ int avc_linear_backward(avc_context* ctx, int M, int din, int dout, const float*
   dw.prec16 = 1; dw.split_scale = 1;
   AVC_TRY(ensure_arena(ctx, std::max(gemm_scratch_bytes(dx), gemm_scratch_bytes(dw)) +
                                 colsum_scratch(M, dout) + 8192));
+  Scratch sc(ctx);
+  AVC_TAKE(amax_dy, unsigned, 64, sc);  // one max|dY| scan shared by both products
+  AVC_TRY(gemm_absmax(d_y, M, dout, dout, amax_dy, S(stream)));
+  dx.amax_a = dw.amax_a = amax_dy;
   if (d_x) AVC_TRY(gemm_run(ctx, dx, S(stream)));
   if (d_weight) AVC_TRY(gemm_run(ctx, dw, S(stream)));
   if (d_bias) AVC_TRY(colsum(ctx, M, dout, d_y, dout, d_bias, accumulate, S(stream)));

@@ -131,6 +131,8 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
   AVC_TRY(bn_backward(ctx, (int)TB, cout, d_out, y_pre, mean, invstd, gamma, beta, act, training,
                       d_gamma, d_beta, accumulate, dy, s));
   if (d_bias) AVC_TRY(colsum(ctx, (int)TB, cout, dy, cout, d_bias, accumulate, s));
+  AVC_TAKE(amax_dy, unsigned, 64, sc);  // one max|dY| scan shared by dgrad and wgrad
+  AVC_TRY(gemm_absmax(dy, TB, cout, cout, amax_dy, s));
   if (d_x) {
     AVC_TAKE(wd, float, 5UL * cin * cout, sc);
     conv_weight_dgrad_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wd, cin, cout);
@@ -140,7 +142,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
     g.A = dy; g.lda = cout; g.a_rows = TB; g.a_shift0 = -2L * B; g.a_tapshift = B;
     g.B = wd; g.ldb = cin; g.b_rows = cout; g.b_tapoff = (long)cout * cin;
     g.C = d_x; g.ldc = cin; g.accumulate = accumulate;
-    g.prec16 = 1; g.split_scale = 1;
+    g.prec16 = 1; g.split_scale = 1; g.amax_a = amax_dy;
     AVC_TRY(gemm_run(ctx, g, s));
   }
   if (d_weight) {
@@ -151,7 +153,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
     g.B = x; g.ldb = cin; g.b_rows = TB; g.b_shift0 = -2L * B; g.b_zshift = B;
     g.nz = 5; g.c_zoff = 1;
     g.C = d_weight; g.ldc = 5L * cin; g.ldc_col = 5; g.accumulate = accumulate;
-    g.prec16 = 1; g.split_scale = 1;
+    g.prec16 = 1; g.split_scale = 1; g.amax_a = amax_dy;
     AVC_TRY(gemm_run(ctx, g, s));
   }
   return AVC_OK;

@@ -27,7 +27,9 @@ struct GemmDesc {
   int prec16 = 0;           // 1: split-fp16 ("3xf16") MFMA kernel (forward operands: |x| < 65504)
   int split_scale = 0;      // with prec16: scale each operand by a power of two from its device-side
                             // max |x| before splitting (gradients: any magnitude), unscale exactly
-  const unsigned* amax = nullptr;  // filled by gemm_run: [2] max |A|, max |B| as float bits
+  const unsigned* amax_a = nullptr;  // max |A| as float bits (device); preset by the caller to
+                                     // share one scan between products, else filled by gemm_run
+  const unsigned* amax_b = nullptr;  // max |B| (filled by gemm_run)
   const _Float16* b_frag = nullptr;  // optional B already split by gemm_prepare_bfrag (prec16 only)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
   int stats_bm = 0;         // filled by gemm_run: rows per stats partial
@@ -43,5 +45,7 @@ size_t gemm_scratch_bytes(const GemmDesc& d);
 // split-f16 kernel streams (all taps); pass it back as GemmDesc::b_frag to skip the per-call split.
 size_t gemm_bfrag_bytes(const GemmDesc& d);
 int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream);
+// max |x| of a rows x cols region (row stride ld) into *out (float bits), for GemmDesc::amax_a
+int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t stream);
 
 }  // namespace avc

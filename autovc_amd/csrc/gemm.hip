@@ -35,17 +35,17 @@ __device__ __forceinline__ float act_apply(float v, int act) {
 }
 
 // power-of-two operand scale for the split-f16 products: max |x| -> [2^14, 2^15)
-__device__ __forceinline__ float split_scale_of(const unsigned* amax, int i) {
+__device__ __forceinline__ float split_scale_of(const unsigned* amax) {
   if (!amax) return 1.f;
-  const float m = __uint_as_float(amax[i]);
+  const float m = __uint_as_float(*amax);
   if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
   int e;
   (void)frexpf(m, &e);
   return ldexpf(1.f, 15 - e);
 }
 
-__device__ __forceinline__ float split_unscale(const unsigned* amax) {
-  return amax ? 1.f / (split_scale_of(amax, 0) * split_scale_of(amax, 1)) : 1.f;
+__device__ __forceinline__ float split_unscale(const unsigned* amax_a, const unsigned* amax_b) {
+  return 1.f / (split_scale_of(amax_a) * split_scale_of(amax_b));
 }
 
 template <int BM, int BN, int WM, int WN, int AT, int BT>
@@ -561,10 +561,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
 __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restrict__ src, long rs,
                                                            long ks, int R, int K, int ntile, int nkc,
                                                            _Float16* __restrict__ dst,
-                                                           const unsigned* __restrict__ amax = nullptr,
-                                                           int which = 0) {
+                                                           const unsigned* __restrict__ amax = nullptr) {
   const int G8 = nkc * 2;  // 8-element groups per row (a multiple of 4)
-  const float sc = split_scale_of(amax, which);
+  const float sc = split_scale_of(amax);
   const long total = (long)ntile * 32 * G8;
   const bool vec = ks == 1 && (rs & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -614,23 +613,45 @@ __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restri
   }
 }
 
-// max |x| over a rows x cols region (row stride ld) into *out (float bits; out pre-zeroed)
-__global__ __launch_bounds__(256) void absmax2d_kernel(const float* __restrict__ src, long rows, long cols, long ld,
-                                                       unsigned* __restrict__ out) {
+// max |x| over a rows x cols region (row stride ld) into *out (float bits; out pre-zeroed).
+// Contiguous regions stream as float4; strided ones walk rows per block (no 64-bit division).
+__global__ __launch_bounds__(256) void absmax_vec_kernel(const float4* __restrict__ src, long n4,
+                                                         const float* __restrict__ tail, int ntail,
+                                                         unsigned* __restrict__ out) {
+  __shared__ float red[4];
   float m = 0.f;
-  const long total = rows * cols;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const long r = idx / cols, c = idx - r * cols;
-    m = fmaxf(m, fabsf(src[r * ld + c]));
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float4 v = src[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
   }
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) m = fmaxf(m, fabsf(tail[threadIdx.x]));
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+__global__ __launch_bounds__(256) void absmax_rows_kernel(const float* __restrict__ src, long rows, int cols,
+                                                          long ld, unsigned* __restrict__ out) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (long r = blockIdx.x; r < rows; r += gridDim.x)
+    for (int c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, fabsf(src[r * ld + c]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t s) {
-  const long total = rows * cols;
-  absmax2d_kernel<<<(int)std::max<long>(1, std::min<long>((total + 255) / 256, 2048)), 256, 0, s>>>(src, rows, cols,
-                                                                                                   ld, out);
+  if (ld == cols && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    const long n = rows * cols, n4 = n / 4;
+    absmax_vec_kernel<<<(int)std::max<long>(1, std::min<long>((n4 + 255) / 256, 1024)), 256, 0, s>>>(
+        reinterpret_cast<const float4*>(src), n4, src + 4 * n4, (int)(n - 4 * n4), out);
+  } else {
+    absmax_rows_kernel<<<(int)std::max<long>(1, std::min<long>(rows, 2048)), 256, 0, s>>>(src, rows, (int)cols, ld,
+                                                                                          out);
+  }
 }
 
 struct Frag16Args {
@@ -785,8 +806,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = (acc[i][j][e] - cmp[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
 #undef AVC16F_ISSUE
-  if (d.amax && nsplit == 1) {  // split-K partials stay scaled; splitk_reduce_kernel unscales
-    const float us = split_unscale(d.amax);
+  if (d.split_scale && nsplit == 1) {  // split-K partials stay scaled; splitk_reduce_kernel unscales
+    const float us = split_unscale(d.amax_a, d.amax_b);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -880,7 +901,7 @@ __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __rest
     const int m = (int)(rem / d.N), n = (int)(rem - (long)m * d.N);
     float s = 0.f;
     for (int sp = 0; sp < nsplit; ++sp) s += slab[((long)sp * d.nz + z) * MN + rem];
-    if (d.amax) s *= split_unscale(d.amax);
+    if (d.split_scale) s *= split_unscale(d.amax_a, d.amax_b);
     if (d.bias0) s += d.bias0[n];
     if (d.bias1) s += d.bias1[n];
     s = act_apply(s, d.act);
@@ -1046,6 +1067,13 @@ int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
   return AVC_OK;
 }
 
+int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t stream) {
+  AVC_HIP(hipMemsetAsync(out, 0, sizeof(unsigned), stream));
+  absmax2d(src, rows, cols, ld, out, stream);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
 size_t gemm_scratch_bytes(const GemmDesc& d) {
   Plan p = make_plan(d, 0);
   size_t s = p.nsplit <= 1 ? 0 : (size_t)p.nsplit * d.nz * d.M * d.N * sizeof(float) + 256;
@@ -1075,20 +1103,28 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
   }
   Frag16Args fa{};
   const bool frag = frag16_eligible(d);
+  const bool scaled_product = d.split_scale != 0;
+  if (!frag) {  // only the split-f16 path scales its operands
+    d.split_scale = 0;
+    d.amax_a = d.amax_b = nullptr;
+  }
   if (frag) {
     // split both operands once into the fragment-major layout gemm16f_kernel streams
     if (d.split_scale) {  // power-of-two operand scales from max |A|, max |B| (device side)
       unsigned* amax = sc.take<unsigned>(64);
       if (!amax) return AVC_ERR_WORKSPACE;
       AVC_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(unsigned), stream));
-      if (d.a_trans) absmax2d(d.A, d.Kc, d.M, d.lda, amax, stream);
-      else absmax2d(d.A, d.a_rows, d.Kc, d.lda, amax, stream);
+      if (!d.amax_a) {
+        if (d.a_trans) absmax2d(d.A, d.Kc, d.M, d.lda, amax, stream);
+        else absmax2d(d.A, d.a_rows, d.Kc, d.lda, amax, stream);
+        d.amax_a = amax;
+      }
       const long kb = frag16_b_krows(d);
       for (int tau = 0; tau < d.ntaps; ++tau) {
         if (d.b_trans) absmax2d(d.B + (long)tau * d.b_tapoff, d.N, d.Kc, d.ldb, amax + 1, stream);
         else absmax2d(d.B + (long)tau * d.b_tapoff, kb, d.N, d.ldb, amax + 1, stream);
       }
-      d.amax = amax;
+      d.amax_b = amax + 1;
     }
     const long a_src_rows = d.a_trans ? d.M : d.a_rows;
     const long a_ntile = frag_ntile(a_src_rows);
@@ -1100,7 +1136,7 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     if (!as) return AVC_ERR_WORKSPACE;
     const long ta = a_ntile * 32 * nkc * 2;
     split_frag32_kernel<<<(int)std::min<long>((ta + 255) / 256, 8192), 256, 0, stream>>>(
-        d.A, d.a_trans ? 1 : d.lda, d.a_trans ? d.lda : 1, (int)a_src_rows, d.Kc, (int)a_ntile, nkc, as, d.amax, 0);
+        d.A, d.a_trans ? 1 : d.lda, d.a_trans ? d.lda : 1, (int)a_src_rows, d.Kc, (int)a_ntile, nkc, as, d.amax_a);
     const long tapstride = b_ntile * b_nkc * 1024;  // halves
     const _Float16* bs = d.split_scale ? nullptr : d.b_frag;
     if (!bs) {
@@ -1110,7 +1146,7 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
       for (int tau = 0; tau < d.ntaps; ++tau)
         split_frag32_kernel<<<(int)std::min<long>((tb + 255) / 256, 8192), 256, 0, stream>>>(
             d.B + (long)tau * d.b_tapoff, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N, (int)b_krows,
-            (int)b_ntile, b_nkc, tmp + tau * tapstride, d.amax, 1);
+            (int)b_ntile, b_nkc, tmp + tau * tapstride, d.amax_b);
       bs = tmp;
     }
     AVC_LAUNCH_CHECK();
@@ -1123,7 +1159,7 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
   if (frag) {
     if (p.bm == 128) launch16f_128(d, fa, p, slab, stream);
     else launch16f_cfg<64, 64, 2, 2, 4, 2>(d, fa, p, slab, stream);
-  } else if (d.prec16 && !d.split_scale && !d.a_trans && g_gemm16) {
+  } else if (d.prec16 && !scaled_product && !d.a_trans && g_gemm16) {
     if (p.bm == 128) launch16<128, 128, 4, 2>(d, p, slab, stream);
     else launch16<64, 64, 2, 2>(d, p, slab, stream);
   } else if (p.bm == 128) {

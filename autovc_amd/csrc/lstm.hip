@@ -900,12 +900,14 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   }
 
   // weight gradients: dW_ih = dG^T x ; dW_hh = dG^T h_prev (h_prev = y shifted one step)
+  AVC_TAKE(amax_dg, unsigned, 64, sc);  // one max|dG| scan shared by the three products
+  AVC_TRY(gemm_absmax(dg, TB, 4L * H, 4L * H, amax_dg, s));
   GemmDesc g1;
   g1.M = 4 * H; g1.N = din; g1.Kc = (int)TB;
   g1.A = dg; g1.a_trans = 1; g1.lda = 4 * H;
   g1.B = x; g1.ldb = ldx; g1.b_rows = TB;
   g1.C = dwih_dst; g1.ldc = din; g1.accumulate = acc_w;
-  g1.prec16 = 1; g1.split_scale = 1;
+  g1.prec16 = 1; g1.split_scale = 1; g1.amax_a = amax_dg;
   AVC_TRY(gemm_run(ctx, g1, s));
   GemmDesc g2 = g1;
   g2.N = H;
@@ -932,7 +934,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     g3.B = wih_use; g3.ldb = din;
     g3.b_trans = small ? 0 : 0;
     g3.C = d_x; g3.ldc = din; g3.accumulate = accumulate_dx;
-    g3.prec16 = 1; g3.split_scale = 1;
+    g3.prec16 = 1; g3.split_scale = 1; g3.amax_a = amax_dg;
     AVC_TRY(gemm_run(ctx, g3, s));
   }
   return AVC_OK;
