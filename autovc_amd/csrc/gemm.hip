@@ -34,6 +34,21 @@ __device__ __forceinline__ float act_apply(float v, int act) {
   return v;
 }
 
+// Tile order: workgroup ids are XCD-contiguous (wgid ranges per XCD), and within them bands of 8
+// tile rows are walked column by column, so the ~32 workgroups an XCD runs at once cover an 8 x 4
+// block and the next ones reuse the same 8 row tiles from that XCD's L2 while the column tiles
+// stream through once (row-major order re-fetched every column tile per row: 51 % L2 hits on
+// the 8192 x 4096 x 512 LSTM input product).
+__device__ __forceinline__ void tile_of(int wgid, int tilesM, int tilesN, int& tm, int& tn) {
+  constexpr int G = 8;
+  const int band = G * tilesN;
+  const int group = wgid / band, first = group * G;
+  const int gsize = min(tilesM - first, G);
+  const int local = wgid - group * band;
+  tm = first + local % gsize;
+  tn = local / gsize;
+}
+
 // power-of-two operand scale for the split-f16 products: max |x| -> [2^14, 2^15)
 __device__ __forceinline__ float split_scale_of(const unsigned* amax) {
   if (!amax) return 1.f;
@@ -69,7 +84,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
-  const int tm = wgid / tilesN, tn = wgid - tm * tilesN;
+  int tm, tn;
+  tile_of(wgid, tilesM, tilesN, tm, tn);
   const int z = blockIdx.y % d.nz, split = blockIdx.y / d.nz;
 
   // kernel-argument fields copied to scalars (a lambda capturing `d` would force it to scratch)
@@ -334,7 +350,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
-  const int tm = wgid / tilesN, tn = wgid - tm * tilesN;
+  int tm, tn;
+  tile_of(wgid, tilesM, tilesN, tm, tn);
   const int z = blockIdx.y % d.nz, split = blockIdx.y / d.nz;
 
   const int M = d.M, N = d.N, Kc = d.Kc;
@@ -660,8 +677,10 @@ struct Frag16Args {
   int b_shift0_c, b_zshift_c;  // B K-shift of product z in 16-deep chunks (weight gradients)
 };
 
-template <int BM, int BN, int WM, int WN, int NS, int KC>
-__global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag16Args f, int tilesM,
+// OCC = 2: two workgroups per CU (waves capped at 128 VGPRs): the 128-k partials are folded
+// into the accumulator with a plain add instead of Kahan-compensated ones (no cmp registers).
+template <int BM, int BN, int WM, int WN, int NS, int KC, int OCC = 1>
+__global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kernel(GemmDesc d, Frag16Args f, int tilesM,
                                                                int tilesN, int kt_per_tap, int kps,
                                                                int nsplit, float* __restrict__ slab) {
   constexpr int NT = 64 * WM * WN, NWAVE = WM * WN;
@@ -681,7 +700,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
-  const int tm = wgid / tilesN, tn = wgid - tm * tilesN;
+  int tm, tn;
+  tile_of(wgid, tilesM, tilesN, tm, tn);
   const int split = blockIdx.y % nsplit, z = blockIdx.y / nsplit;
   const int ktotal = d.ntaps * kt_per_tap;
   const int kt0 = split * kps;
@@ -790,10 +810,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
         for (int j = 0; j < TN; ++j) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            const float y = part[i][j][e] - cmp[i][j][e];
-            const float t = acc[i][j][e] + y;
-            cmp[i][j][e] = (t - acc[i][j][e]) - y;
-            acc[i][j][e] = t;
+            if constexpr (OCC == 1) {
+              const float y = part[i][j][e] - cmp[i][j][e];
+              const float t = acc[i][j][e] + y;
+              cmp[i][j][e] = (t - acc[i][j][e]) - y;
+              acc[i][j][e] = t;
+            } else {
+              acc[i][j][e] += part[i][j][e];
+            }
           }
           part[i][j] = zero16;
         }
@@ -804,7 +828,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16f_kernel(GemmDesc d, Frag1
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = (acc[i][j][e] - cmp[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
+      for (int e = 0; e < 16; ++e)
+        acc[i][j][e] = (OCC == 1 ? acc[i][j][e] - cmp[i][j][e] : acc[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
 #undef AVC16F_ISSUE
   if (d.split_scale && nsplit == 1) {  // split-K partials stay scaled; splitk_reduce_kernel unscales
     const float us = split_unscale(d.amax_a, d.amax_b);
@@ -985,13 +1010,13 @@ size_t frag16_scratch(const GemmDesc& d) {
 
 int g_gemm_cfg = 1;  // avc_gemm_config(): tile/ring variant of gemm16f for 128x128 tiles (1 measured best)
 
-template <int BM, int BN, int WM, int WN, int NS, int KC>
+template <int BM, int BN, int WM, int WN, int NS, int KC, int OCC = 1>
 void launch16f_cfg(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
   constexpr int NBLK = (BM / 32) * KC * 2 + (BN / 32) * KC * 2;
   const size_t lds = (size_t)NS * NBLK * 1024;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16f_kernel<BM, BN, WM, WN, NS, KC>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16f_kernel<BM, BN, WM, WN, NS, KC, OCC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
@@ -1001,7 +1026,7 @@ void launch16f_cfg(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
   const int ktotal = d.ntaps * kt_per_tap;
   const int kps = (ktotal + p.nsplit - 1) / p.nsplit;
   dim3 grid(p.tilesM * p.tilesN, d.nz * p.nsplit);
-  gemm16f_kernel<BM, BN, WM, WN, NS, KC><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, kt_per_tap,
+  gemm16f_kernel<BM, BN, WM, WN, NS, KC, OCC><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, kt_per_tap,
                                                                         kps, p.nsplit, slab);
 }
 
@@ -1012,6 +1037,8 @@ void launch16f_128(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
     case 3: launch16f_cfg<128, 128, 2, 4, 4, 2>(d, f, p, slab, s); break;
     case 4: launch16f_cfg<128, 128, 2, 4, 2, 4>(d, f, p, slab, s); break;
     case 5: launch16f_cfg<128, 128, 4, 2, 3, 2>(d, f, p, slab, s); break;
+    case 6: launch16f_cfg<128, 128, 4, 2, 2, 2, 2>(d, f, p, slab, s); break;
+    case 7: launch16f_cfg<128, 128, 4, 2, 2, 4, 2>(d, f, p, slab, s); break;
     default: launch16f_cfg<128, 128, 4, 2, 4, 2>(d, f, p, slab, s); break;
   }
 }
@@ -1194,8 +1221,8 @@ extern "C" int avc_gemm_tune(int mode) {
 }
 
 extern "C" int avc_gemm_config(int cfg) {
-  if (cfg < 0 || cfg > 5) {
-    avc::set_error("avc_gemm_config: cfg must be 0..5");
+  if (cfg < 0 || cfg > 7) {
+    avc::set_error("avc_gemm_config: cfg must be 0..7");
     return AVC_ERR_INVALID;
   }
   avc::g_gemm_cfg = cfg;

@@ -221,7 +221,9 @@ int avc_lstm_split_tune(int kslice, int col_blocks, int rows64);
 int avc_gemm_tune(int prec16);
 /* Tuning hook: variant of the pre-split split-f16 GEMM for 128x128 tiles (8 waves each):
  * 0 = 4x2 waves, 4-stage ring of 32-deep K-tiles; 1 = 4x2, 2 stages of 64-deep K-tiles (default);
- * 2 = 4x2, 3 stages x 48; 3 = 2x4, 4 x 32; 4 = 2x4, 2 x 64; 5 = 4x2, 3 x 32. */
+ * 2 = 4x2, 3 stages x 48; 3 = 2x4, 4 x 32; 4 = 2x4, 2 x 64; 5 = 4x2, 3 x 32; 6 / 7 = 4x2,
+ * 2 x 32 / 2 x 64 with plain (not Kahan-compensated) 128-k partial folds, 128 VGPRs (two
+ * workgroups per CU for 6). */
 int avc_gemm_config(int cfg);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,

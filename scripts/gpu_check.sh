@@ -21,7 +21,7 @@ for step in "$@"; do
     gpu)   run gpu 900 python -m pytest tests -v -m gpu --timeout 300 -p no:cacheprovider ;;
     bench) run bench 400 python bench.py --steps 10 --warmup 2 ;;
     benchnt) run benchnt 400 python bench.py --steps 20 --warmup 3 --no-timing --no-cpu ;;
-    perf)  run perf 400 python scripts/perf_layers.py 0 1 2 3 4 5 ;;
+    perf)  run perf 400 python scripts/perf_layers.py 1 6 7 ;;
     prof)  run prof 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o fwd -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-timing ;;
     pmcf)  run pmcf 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcF -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
     pmcw)  run pmcw 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcW -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
