@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Summarise the `gpu_check.sh gpmc` passes (rocprofv3 --pmc on scripts/gemm_micro.py) for the
+split-f16 GEMM: MFMA busy fraction, wait fractions and L2 hit rate per kernel shape.
+
+Usage: gemm_counters.py GPMC_DIR OUT.json
+
+SQ_*_CYCLES / SQ_WAIT_* count in quad-cycles except SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed
+over SIMDs); MFMA busy fraction = MFMA_BUSY / (SIMDs x kernel cycles), kernel cycles from
+SQ_BUSY_CYCLES / (shader engines) — both as read on gfx950 (MI355X: 1024 SIMDs, 32 SEs).
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+
+def main():
+    d, out = sys.argv[1:3]
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            n = r["Kernel_Name"]
+            if "gemm16f" not in n:
+                continue
+            g = r.get("Grid_Size", "")
+            shape = {"131072": "conv 512->512 k5, M=8192 N=512 K=2560",
+                     "1048576": "lstm2 input projection, M=8192 N=4096 K=512"}.get(g, "")
+            key = f"gemm16f grid={g} {shape}".strip()
+            vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    res = {}
+    for k, c in vals.items():
+        m = {n: sum(v) / len(v) for n, v in c.items()}
+        cyc = m["SQ_BUSY_CYCLES"] / 32.0
+        res[k] = {
+            "counters": {n: round(v) for n, v in m.items()},
+            "kernel_cycles_est": round(cyc),
+            "mfma_busy_frac": round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * cyc), 3),
+            "wait_inst_frac_of_wave_cycles": round(m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"], 3),
+            "l2_hit_rate": round(m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 3),
+        }
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps({k: {x: v[x] for x in v if x != "counters"} for k, v in res.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
