@@ -100,6 +100,22 @@ __global__ void transpose_permute_kernel(const float* __restrict__ W, float* __r
   for (int r = ty; r < 32; r += 8) WT[(long)(j0 + r) * 4 * H + p0 + tx] = tile[tx][r];
 }
 
+// W_hh [4H][H] -> W_hh^T fragment-major for the BPTT product (StepArgs::frag): row j (hidden
+// unit), k = permuted gate row p; block (j>>4, p>>4), lane (j&15) + 16((p&15)>>2), element p&3.
+__global__ void whhT_frag_kernel(const float* __restrict__ W, float* __restrict__ dst, int H) {
+  const long total = 4L * H * H;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int e = (int)(idx & 3), lane = (int)((idx >> 2) & 63);
+    const long blk = idx >> 8;
+    const int nkc = H >> 2;  // 16-k chunks of 4H
+    const int ct = (int)(blk / nkc), c = (int)(blk - (long)ct * nkc);
+    const int j = ct * 16 + (lane & 15);
+    const int p = c * 16 + 4 * (lane >> 4) + e;
+    dst[idx] = W[(long)perm_to_orig(p, H) * H + j];
+  }
+}
+
 // dst[orig(p)][:] (+)= src[p][:]
 __global__ void unpermute_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, int H,
                                       int D, int accumulate) {
@@ -143,6 +159,11 @@ struct StepArgs {
   // backward (slot 0 only)
   const float* dy; long lddy; const float* gates; const float* c_cur; const float* c_prv;
   float* dc; float* dg_out;
+  // BPTT operands fragment-major (frag = 1): A[0] (dG of the later step) and W[0] (W_hh^T) in
+  // 1 KiB blocks of 16 rows x 16 k, lane l = r + 16q holding row r, k = 4q..4q+3; lda[0] = 16-k
+  // chunks per 16-row tile.  One wave load is then one contiguous 1 KiB (full cache lines).
+  int frag;
+  float* dgf_out;  // the step's dG in that layout (input of the next BPTT step)
 };
 
 template <int MB, bool BWD, int CPT>
@@ -212,14 +233,18 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
   if (src != nullptr) {
     const long lds_ = second ? a.lda1[L] : a.lda[L];
     const int koff = second ? kbeg - a.K0[L] : kbeg;
-    const float* wrow = a.W[L] + (long)(cb * 16 + l15) * a.K[L] + kbeg + lk;
+    // element offset of group g at K offset C: base + C*sC + g*sG (row-major: 1 / 4 floats;
+    // fragment-major: a 16-k chunk is 256 floats)
+    const bool fr = BWD && a.frag;
+    const int sC = fr ? 16 : 1, sG = fr ? 256 : 4;
+    const float* wrow = fr ? a.W[L] + ((long)cb * (a.K[L] >> 4) + (kbeg >> 4)) * 256 + lane * 4
+                           : a.W[L] + (long)(cb * 16 + l15) * a.K[L] + kbeg + lk;
     const float* arow[RT];
-    bool aok[RT];
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       const int b = rb * MB + r * 16 + l15;
-      aok[r] = b < a.B;
-      arow[r] = src + (long)(aok[r] ? b : 0) * lds_ + koff + lk;
+      arow[r] = fr ? src + ((long)(rb * RT + r) * lds_ + (koff >> 4)) * 256 + lane * 4
+                   : src + (long)(b < a.B ? b : 0) * lds_ + koff + lk;
     }
     // Register double-buffering: the loads of group g+1 are in flight while group g's MFMAs
     // run (named buffers, unrolled by two, so no register array is indexed at run time).
@@ -229,9 +254,9 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
     float4 wA[G], hA[G][RT], wB[G], hB[G][RT];
 #define AVC_GROUP_LOAD(WV, HV, C0)                                                               \
   _Pragma("unroll") for (int g = 0; g < G; ++g) {                                               \
-    WV[g] = *reinterpret_cast<const float4*>(wrow + (C0) + 4 * g);                              \
+    WV[g] = *reinterpret_cast<const float4*>(wrow + (C0) * sC + g * sG);                        \
     _Pragma("unroll") for (int r = 0; r < RT; ++r)                                              \
-      HV[g][r] = *reinterpret_cast<const float4*>(arow[r] + (C0) + 4 * g);                     \
+      HV[g][r] = *reinterpret_cast<const float4*>(arow[r] + (C0) * sC + g * sG);               \
   }
 #define AVC_GROUP_MFMA(WV, HV)                                                                   \
   _Pragma("unroll") for (int g = 0; g < G; ++g)                                                 \
@@ -350,10 +375,19 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
       const float tc = tanhf(c);
       const float dct = dh * og * (1.f - tc * tc) + pf[i][6];
       a.dc[(long)b * H + j] = dct * fg;
-      a.dg_out[pb] = dct * gg * ig * (1.f - ig);
-      a.dg_out[pb + 4] = dct * cp * fg * (1.f - fg);
-      a.dg_out[pb + 8] = dct * ig * (1.f - gg * gg);
-      a.dg_out[pb + 12] = dh * tc * og * (1.f - og);
+      const float d0 = dct * gg * ig * (1.f - ig), d1 = dct * cp * fg * (1.f - fg);
+      const float d2 = dct * ig * (1.f - gg * gg), d3 = dh * tc * og * (1.f - og);
+      a.dg_out[pb] = d0;
+      a.dg_out[pb + 4] = d1;
+      a.dg_out[pb + 8] = d2;
+      a.dg_out[pb + 12] = d3;
+      if (a.dgf_out) {  // gate g of unit j = permuted column (j>>2)*16 + 4g + (j&3)
+        float* f = a.dgf_out + ((long)(b >> 4) * (H >> 2) + (j >> 2)) * 256 + (b & 15) * 4 + (j & 3);
+        f[0] = d0;
+        f[64] = d1;
+        f[128] = d2;
+        f[192] = d3;
+      }
     }
   }
   AVC_STAMP(4);
@@ -830,6 +864,7 @@ size_t lstm_backward_scratch(int T, int B, int din, int H) {
   const size_t TB = (size_t)T * B;
   size_t s = TB * 4 * H * f + (size_t)B * H * f + (size_t)4 * H * (din + H) * 2 * f +
              (size_t)4 * H * f + 8192;
+  s += 2 * ((size_t)B + 64) * 4 * H * f + 512;  // fragment-major dG ping-pong
   GemmDesc d1;  // dW_ih
   d1.M = 4 * H; d1.N = din; d1.Kc = (int)TB; d1.a_trans = 1; d1.b_rows = TB;
   d1.prec16 = 1; d1.split_scale = 1;
@@ -865,12 +900,16 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
     AVC_TAKE(whhT_p, float, (size_t)4 * H * H, sc);
     AVC_TAKE(dc, float, (size_t)B * H, sc);
-    permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w_ih, wih_p, H, din);
-    transpose_permute_kernel<<<dim3(4 * H / 32, H / 32), 256, 0, s>>>(w_hh, whhT_p, H);
-    AVC_HIP(hipMemsetAsync(dc, 0, sizeof(float) * B * H, s));
-    AVC_LAUNCH_CHECK();
     const StepCfg cfg = step_cfg(B, H / 16, 4 * H);
     dim3 grid(H / 16, (B + cfg.mb - 1) / cfg.mb);
+    // the recurrent dG (and W_hh^T) travel fragment-major, padded to whole row tiles
+    const long fsz = (long)grid.y * cfg.mb * 4 * H;
+    AVC_TAKE(dgf, float, (size_t)2 * fsz, sc);
+    permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w_ih, wih_p, H, din);
+    whhT_frag_kernel<<<ew_blocks(4L * H * H), 256, 0, s>>>(w_hh, whhT_p, H);
+    AVC_HIP(hipMemsetAsync(dc, 0, sizeof(float) * B * H, s));
+    AVC_HIP(hipMemsetAsync(dgf, 0, sizeof(float) * 2 * fsz, s));
+    AVC_LAUNCH_CHECK();
     for (int st = T - 1; st >= 0; --st) {
       const int t = reverse ? T - 1 - st : st;
       const int tn = reverse ? t - 1 : t + 1;  // time index processed after t in the forward pass
@@ -878,8 +917,11 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
       StepArgs a{};
       a.B = B; a.H = H; a.nblk0 = (int)grid.x;
       a.K[0] = 4 * H; a.K0[0] = 4 * H; a.kw[0] = 4 * H / cfg.nw;
-      a.A[0] = st < T - 1 ? dg + (long)tn * B * 4 * H : nullptr;
-      a.lda[0] = 4 * H;
+      const int it = T - 1 - st;  // iteration index: the previous launch wrote buffer (it-1)&1
+      a.A[0] = st < T - 1 ? dgf + (long)((it - 1) & 1) * fsz : nullptr;
+      a.lda[0] = H / 4;  // 16-k chunks per row tile
+      a.frag = 1;
+      a.dgf_out = st > 0 ? dgf + (long)(it & 1) * fsz : nullptr;
       a.W[0] = whhT_p;
       a.dy = d_y + (long)t * B * ldy;
       a.lddy = ldy;
