@@ -260,3 +260,31 @@ def test_fused_forward_sees_weight_updates(cuda_device):
     m.load_flattened_params(flat)                         # .data copies
     y3 = fwd()
     assert not torch.equal(y3, y2) and torch.equal(y3, ref())
+
+
+def test_c5_long_form_against_oracle(cuda_device):
+    """BASELINE config 5 shape: B = 32 utterances of lengths U{256..1024} (seed 2), zero-padded to
+    1024 frames (collate_fn, dataloader.py:112-121), train-mode BN as convert() runs.  Fused
+    forward against the CPU oracle (pinned to the reference by the golden cases, incl. the
+    B = 2 T = 1024 ragged one), tolerance 1e-4 max-abs on mel / mel_post / codes."""
+    from oracle import autovc_oracle as orc
+    from autovc_amd.weights import synthetic_embedding, synthetic_mel
+    B, T = 32, 1024
+    rng = np.random.default_rng(2)
+    lengths = rng.integers(256, 1025, size=B)
+    x = synthetic_mel(12, B, T)
+    for i, L in enumerate(lengths):
+        x[i, :, L:] = 0.0
+    co, ct = synthetic_embedding(112, B), synthetic_embedding(212, B)
+    sd = torch_state_dict(0)
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    with torch.no_grad():
+        bufs = {k: v.clone() for k, v in sd.items() if "running" in k or "num_batches" in k}
+        rm, rp, rc = orc.forward(sd, torch.from_numpy(x), torch.from_numpy(co), torch.from_numpy(ct), True, bufs)
+    ae = make_model(cuda_device)
+    with torch.no_grad():
+        mel, post, codes = ae(_t(x, cuda_device), _t(co, cuda_device), _t(ct, cuda_device))
+    torch.cuda.synchronize()
+    e = [np.abs(a.cpu().numpy() - b.numpy()).max() for a, b in ((mel, rm), (post, rp), (codes, rc))]
+    print(f"C5 B=32 T=1024 ragged: max|d mel|={e[0]:.2e} max|d mel_post|={e[1]:.2e} max|d codes|={e[2]:.2e}")
+    assert max(e) <= TOL_MEL
