@@ -515,15 +515,22 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx,
     const long rn = grow(s + 3);
     const float zd0 = gx[rn + lane], zd1 = gx[rn + lane + 64];
     float z0 = za0, z1 = za1;
-    float d0 = 0.f, d1 = 0.f;
+    // four independent FMA chains per gate row (8 deep instead of 32: the step is a latency chain)
+    float p0[4] = {0.f, 0.f, 0.f, 0.f}, p1[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k4 = 0; k4 < 8; ++k4) {
       const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
-      d0 += w0[4 * k4] * h4.x + w0[4 * k4 + 1] * h4.y + w0[4 * k4 + 2] * h4.z + w0[4 * k4 + 3] * h4.w;
-      d1 += w1[4 * k4] * h4.x + w1[4 * k4 + 1] * h4.y + w1[4 * k4 + 2] * h4.z + w1[4 * k4 + 3] * h4.w;
+      p0[0] = fmaf(w0[4 * k4], h4.x, p0[0]);
+      p0[1] = fmaf(w0[4 * k4 + 1], h4.y, p0[1]);
+      p0[2] = fmaf(w0[4 * k4 + 2], h4.z, p0[2]);
+      p0[3] = fmaf(w0[4 * k4 + 3], h4.w, p0[3]);
+      p1[0] = fmaf(w1[4 * k4], h4.x, p1[0]);
+      p1[1] = fmaf(w1[4 * k4 + 1], h4.y, p1[1]);
+      p1[2] = fmaf(w1[4 * k4 + 2], h4.z, p1[2]);
+      p1[3] = fmaf(w1[4 * k4 + 3], h4.w, p1[3]);
     }
-    z0 += d0;
-    z1 += d1;
+    z0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
+    z1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
     const float a0 = sigmoidf_(z0);                              // i (lane<32) or f
     const float a1 = lane < 32 ? tanhf(z1) : sigmoidf_(z1);      // g (lane<32) or o
     const float fg = __shfl(a0, (lane + 32) & 63);

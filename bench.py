@@ -110,6 +110,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    extra = m["extra"]() if m.get("extra") else {}
+
     # Roofline region: the same K steps again with every launch of the kernel classes bracketed
     # by HIP events on its stream (the events cost ~7 us per launch, so `value` above is taken
     # from the uninstrumented region).
@@ -145,6 +147,7 @@ def main():
     }
     if m.get("flop_per_unit"):
         result["achieved_tflops_whole_step"] = round(m["flop_per_unit"] * value / world / 1e12, 2)
+    result.update(extra)
 
     if not args.no_timing:
         per = {c: _lib.timing_read(c) for c in classes}
@@ -222,6 +225,23 @@ def setup_generator(args, dev, rank):
             return model.train_step(x, c)
 
     fwd = args.mode == "fwd"
+
+    def eval_bn():
+        """The same batch with eval-mode BN (running statistics), reported beside the train-mode
+        headline ("eval also reported")."""
+        model.eval()
+        with torch.no_grad():
+            for _ in range(max(2, args.warmup)):  # eager, then graph capture
+                model(x, c_org, c_trg)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                model(x, c_org, c_trg)
+            torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        model.train()
+        return {"eval_bn": {"value": round(B * T / dt, 1), "unit": "mel-frames/s", "ms_per_step": round(1000 * dt, 3)}}
+
     return {
         "step": step, "units_per_step": B * T, "unit": "mel-frames/s", "dtype": "f32",
         "metric": METRIC if fwd else "mel-frames/sec AutoVC train step, 80×128 batch",
@@ -239,6 +259,7 @@ def setup_generator(args, dev, rank):
             "algorithmic_gflop_per_step": round((56.77e6 if fwd else 192.2e6) * B * T / 1e9, 1),
         },
         "cpu": (lambda out: _with_dmel(cpu_baseline(args, sd, x_np, out, B, T, rank))) if fwd else None,
+        "extra": eval_bn if fwd else None,
     }
 
 
