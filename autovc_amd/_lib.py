@@ -56,6 +56,8 @@ _SIGS = {
     "avc_lstm_split_tune": [_I, _I, _I],
     "avc_gemm_tune": [_I],
     "avc_gemm_config": [_I],
+    "avc_lstm_persist_tune": [_I],
+    "avc_lstm_persist_status": [ctypes.POINTER(ctypes.c_long)],
     "avc_timing_reset": [],
     "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)],
@@ -148,7 +150,7 @@ def ptr(t) -> int | None:
     return t.data_ptr()
 
 
-TIMING_CLASSES = {"gemm": 0, "lstm_step_fwd": 1, "lstm_step_bwd": 2, "lstm32": 3, "dft64": 4}
+TIMING_CLASSES = {"gemm": 0, "lstm_step_fwd": 1, "lstm_step_bwd": 2, "lstm32": 3, "dft64": 4, "lstm2_persist": 5}
 
 
 def timing_enable(names):

@@ -14,6 +14,7 @@ thread_local std::string g_err;
 }
 
 void set_error(const std::string& msg) { g_err = msg; }
+int g_config_epoch = 0;
 const char* get_error() { return g_err.c_str(); }
 
 void* prep_buffer(avc_context* ctx, int kind, const void* key0, const void* key1, size_t bytes,
@@ -481,8 +482,10 @@ int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* co
   AVC_TRY(ensure_arena(ctx, gen_scratch(T, B)));
   hipStream_t s = S(stream);
   avc_gen_graph& g = ctx->gen;
-  const bool timing = timing_on(TC_GEMM) || timing_on(TC_LSTM_STEP_FWD) || timing_on(TC_LSTM32);
+  const bool timing = timing_on(TC_GEMM) || timing_on(TC_LSTM_STEP_FWD) || timing_on(TC_LSTM32) ||
+                      timing_on(TC_LSTM2_PERSIST);
   const bool same = g.T == T && g.B == B && g.training == training && g.version == weights_version &&
+                    g.epoch == g_config_epoch &&
                     g.params.size() == (size_t)P_COUNT &&
                     std::equal(g.params.begin(), g.params.end(), params);
   ctx->prep_version = weights_version;
@@ -518,7 +521,7 @@ int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* co
   // eager call; a second consecutive call with the same key captures the graph
   if (!same) {
     drop_graph(ctx);
-    g.T = T; g.B = B; g.training = training; g.version = weights_version;
+    g.T = T; g.B = B; g.training = training; g.version = weights_version; g.epoch = g_config_epoch;
     g.params.assign(params, params + P_COUNT);
     g.seen = 0;
   }

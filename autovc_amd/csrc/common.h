@@ -21,6 +21,9 @@
 namespace avc {
 
 void set_error(const std::string& msg);
+// bumped by every tuning hook (avc_*_tune / avc_gemm_config): a captured forward graph is only
+// replayed under the kernel configuration it was captured with
+extern int g_config_epoch;
 const char* get_error();
 
 #define AVC_CHECK_ARG(cond, msg)                         \
@@ -78,6 +81,7 @@ struct avc_prep_entry {
 // graph reads/writes fixed staging buffers; the caller's tensors are copied in and out.
 struct avc_gen_graph {
   int T = 0, B = 0, training = -1;
+  int epoch = -1;               // avc::g_config_epoch at capture (tuning hooks invalidate graphs)
   long version = -1;
   std::vector<const float*> params;
   int seen = 0;                 // consecutive eager calls with this key

@@ -1217,6 +1217,7 @@ extern "C" int avc_gemm_tune(int mode) {
     return AVC_ERR_INVALID;
   }
   avc::g_gemm16 = mode;
+  ++avc::g_config_epoch;
   return AVC_OK;
 }
 
@@ -1226,5 +1227,6 @@ extern "C" int avc_gemm_config(int cfg) {
     return AVC_ERR_INVALID;
   }
   avc::g_gemm_cfg = cfg;
+  ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -46,6 +46,16 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
 int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                              const float* const* w0, const float* const* w1, float* y0, float* y1,
                              float* g0, float* c0, float* g1, float* c1, hipStream_t s);
+// decoder.lstm2 as one weight-stationary launch (lstm_persist.hip); gx0 = layer 0's input
+// projection, w*_s = split weights (each followed by its per-row unscale), b1_p = permuted
+// b_ih1 + b_hh1
+bool lstm2_persist_eligible(int T, int B, int H);
+size_t lstm2_persist_scratch(int T, int B, int H);
+int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx0,
+                          const _Float16* w0_s, const float* winv0, const _Float16* w1i_s,
+                          const float* winv1i, const _Float16* w1h_s, const float* winv1h,
+                          const float* b1_p, float* y0, float* y1, float* g0, float* c0, float* g1,
+                          float* c1, hipStream_t s);
 // rows of a [4H][D] gate matrix into the permuted gate order p = blk*16 + gate*4 + u (lstm.hip)
 int permute_rows(const float* src, float* dst, int H, int D, hipStream_t s);
 

@@ -1011,5 +1011,6 @@ extern "C" int avc_lstm_tune(int rows_per_block, int waves) {
   }
   avc::g_force_mb = rows_per_block;
   avc::g_force_nw = waves;
+  ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -1,0 +1,458 @@
+// Weight-stationary two-layer LSTM recurrence (decoder.lstm2, decoder.py:53,74) as ONE launch.
+//
+// Why: the launch-per-step three-slot wavefront (lstm_split.hip) streams all 48 MB of split
+// weights (W_hh0, W_ih1, W_hh1 as hi/lo f16) from the Infinity Cache in EVERY time step: 192
+// workgroups x (256 KB of weights + 256 KB of h) per step is both the per-CU intake limit
+// (~80 GB/s per CU) and the chip's Infinity-Cache rate (~8.6 TB/s; MI355X_MICROARCH.md), which is
+// why a step costs ~15 us.  Here every workgroup loads its 64 gate rows (256 KB split) ONCE into
+// registers (three 16-row tiles) and LDS (the fourth), and per time step only the 256 KB split h
+// operand moves — read from the XCD's L2, which all of the XCD's CUs share.
+//
+// Structure: grid = 3 slots x ncb workgroups, one per CU (LDS use forces one workgroup per CU;
+// 3*ncb <= CUs is checked on the host, so every workgroup is resident and the waits below always
+// make progress).  Slot L's workgroup cb owns permuted gate rows [64cb, 64cb+64) of
+//   slot 0: W_hh0  (layer 0's recurrence, h0_t = cell(h0_{t-1} W_hh0^T + gx0_t)),
+//   slot 1: W_ih1  (layer 1's input product gx1_t = h0_t W_ih1^T + b_ih1 + b_hh1),
+//   slot 2: W_hh1  (layer 1's recurrence, h1_t = cell(h1_{t-1} W_hh1^T + gx1_t)),
+// and walks t = 0..T-1 on its own.  Every hand-off writes a buffer of its own per time step
+// (split h0_t / h1_t, gx1_t), so there is never a write-after-read hazard; the cell state c
+// stays in registers (the epilogue thread of a (batch row, 4 hidden units) pair never changes).
+//
+// Dependencies (counters per slot and time step, zeroed per call):
+//   slot 0 at t waits  cnt0[t-1] == ncb           (all of h0_{t-1})
+//   slot 1 at t waits  cnt0[t]   == ncb           (all of h0_t)
+//   slot 2 at t waits  cnt1[t]   == ncb and cnt2[t-1] == ncb
+// Hand-off protocol (cdna_hip_programming.md Guideline 16, counter form): payload stored
+// write-through (sc1), every storing wave drains vmcnt, workgroup barrier, one lane adds to the
+// counter (agent scope); the consumer polls one word relaxed, one lane runs the agent-scope
+// acquire, drains, barrier, then plain loads (the XCD's L2 serves the other CUs of that XCD).
+// Every spin is bounded: on timeout the workgroup sets a shared give-up word, every waiter sees
+// it and leaves, and the host reports the failure (avc_lstm_persist_status).
+//
+// Arithmetic is identical to lstm_split_step_kernel's NC = 4 tiles: the same 3xf16 products
+// (hi.lo, lo.hi, hi.hi per 32-deep chunk, in that order), the same K split over 4 waves and
+// the same fixed-order LDS reduction, so the two paths agree bit for bit.
+#include <algorithm>
+
+#include "kernels.h"
+#include "timing.h"
+
+namespace avc {
+
+int g_persist_mode = 1;  // avc_lstm_persist_tune(): 0 = never, 1 = when eligible
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+constexpr float kHScale = 32768.0f;   // split h is stored as h * 2^15 (lstm_split.hip)
+constexpr unsigned kSpinLimit = 1u << 21;
+
+__device__ unsigned g_persist_giveups = 0;  // sticky count of timed-out launches (host-read)
+
+#ifdef AVC_STAMPS
+// diagnostic build only: s_memtime per (workgroup, step, phase), written by thread 0
+__device__ unsigned long long* g_pstamps = nullptr;
+#define AVC_PSTAMP(slot)                                                                          \
+  do {                                                                                            \
+    unsigned long long _t;                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (g_pstamps && tid == 0) g_pstamps[((long)blockIdx.x * T + t) * 8 + (slot)] = _t;           \
+  } while (0)
+// s_memrealtime (constant clock shared by all XCDs) for cross-workgroup comparisons
+#define AVC_PRSTAMP(slot)                                                                         \
+  do {                                                                                            \
+    unsigned long long _t;                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (g_pstamps && tid == 0) g_pstamps[((long)blockIdx.x * T + t) * 8 + (slot)] = _t;           \
+  } while (0)
+#else
+#define AVC_PSTAMP(slot) do { } while (0)
+#define AVC_PRSTAMP(slot) do { } while (0)
+#endif
+
+struct PersistArgs {
+  int B, T, H, ncb, ntile;
+  const unsigned char* W[3];  // split fragment-major weights, permuted gate rows
+  const float* winv[3];       // per-row unscale
+  const float* gx0;           // [T][B][4H] layer-0 input projection + biases (permuted)
+  const float* b1;            // [4H] b_ih1 + b_hh1 (permuted)
+  float* gx1;                 // [T][B][4H]
+  unsigned char* hs0;         // [T][hsz] split h0_t (fragment-major, 2 KiB per 16-row x 32-k block)
+  unsigned char* hs1;
+  long hsz;                   // bytes per time step of a split-h buffer
+  float* y0; float* y1;       // [T][B][H] fp32 h
+  float* g0; float* g1;       // optional [T][B][4H] activated gates (training)
+  float* c0; float* c1;       // optional [T][B][H] cell state (training)
+  unsigned* cnt;              // [3][T] arrivals
+  unsigned* tmo;              // give-up word
+};
+
+// One lane waits until *p >= target (relaxed agent-scope polls).  false = gave up (or someone
+// else did: the shared give-up word is checked every 64 polls).
+__device__ bool wait_ge(unsigned* p, unsigned target, unsigned* tmo) {
+  gu32* gp = (gu32*)(p);
+  gu32* gt = (gu32*)(tmo);
+  for (unsigned spins = 0;; ++spins) {
+    if (__hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    if ((spins & 63) == 63 && __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+      return false;
+    if (spins >= kSpinLimit) {
+      __hip_atomic_store(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(&g_persist_giveups, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <int NCH, int RT>
+__global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
+  constexpr int NW = 4, NC = 4;
+  constexpr int MB = 16 * RT;        // batch rows computed (B <= MB)
+  constexpr int TW = 16 * NC;        // 64 gate rows
+  constexpr int RP = TW + 4;
+  constexpr int NPAIR = MB * NC;     // (row, 16-column block) epilogue pairs, <= 256
+  // LDS: gate tile 3's weights for every wave (NW x NCH x 2 KiB), then the reduction partials
+  extern __shared__ float lds[];
+  unsigned char* wl = reinterpret_cast<unsigned char*>(lds);
+  float* part = lds + NW * NCH * 512;
+  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int L = blockIdx.x / a.ncb, cb = blockIdx.x - L * a.ncb;
+  const int B = a.B, H = a.H, T = a.T;
+  const int nck = H >> 5;            // 32-deep chunks per row
+  const long G4 = 4L * H;
+
+  // ---- stationary weights: wave w owns K chunks [w*NCH, (w+1)*NCH) of the 4 gate tiles ----
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(a.W[L]) + (long)cb * NC * nck * 2048, 0, NC * nck * 2048, 0x00020000);
+  const int kc0 = w * NCH;
+  f16x8 wreg[3][NCH][2];
+#pragma unroll
+  for (int n = 0; n < 3; ++n)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl)
+        wreg[n][c][hl] = __builtin_bit_cast(
+            f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (n * nck + kc0 + c) * 2048 + hl * 1024, 0));
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (3 * nck + kc0 + c) * 2048 + hl * 1024, 0);
+      *reinterpret_cast<u32x4*>(wl + ((w * NCH + c) * 2 + hl) * 1024 + lane * 16) = v;
+    }
+
+  // ---- epilogue ownership: thread tid handles (row, blk) = (tid / 4, tid % 4) -------------
+  const bool epi = tid < NPAIR;
+  const int row = min(tid, NPAIR - 1) / NC, blk = min(tid, NPAIR - 1) % NC;
+  const int b = row;
+  const bool live = epi && b < B;
+  const int bc = min(b, B - 1);
+  const int p0 = cb * TW + blk * 16;   // first permuted gate column of the pair
+  const int j0 = cb * 4 * NC + blk * 4;  // first hidden unit
+  f32x4 wiv[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) wiv[g] = *reinterpret_cast<const f32x4*>(a.winv[L] + p0 + 4 * g);
+  f32x4 cst = f32x4{0.f, 0.f, 0.f, 0.f};
+  // slot 1 stores gx1 in whole lines: lane -> (row 4i + lane/16 of the wave's 16, columns 4*pc..)
+  const int pc = lane & 15;
+  f32x4 wiv1 = f32x4{0.f, 0.f, 0.f, 0.f}, b1v = wiv1;
+  if (L == 1) {
+    wiv1 = *reinterpret_cast<const f32x4*>(a.winv[1] + cb * TW + 4 * pc);
+    b1v = *reinterpret_cast<const f32x4*>(a.b1 + cb * TW + 4 * pc);
+  }
+  float* c_save = L == 0 ? a.c0 : a.c1;
+  float* g_save = L == 0 ? a.g0 : a.g1;
+  float* y_out = L == 0 ? a.y0 : a.y1;
+  unsigned char* hs_out = L == 0 ? a.hs0 : a.hs1;
+  unsigned* my_cnt = a.cnt + (long)L * T;
+
+  for (int t = 0; t < T; ++t) {
+    // ---- wait for this step's operands ----------------------------------------------------
+    AVC_PSTAMP(0);
+    if (tid == 0) {
+      bool ok = true;
+      if (L == 0) {
+        if (t > 0) ok = wait_ge(a.cnt + (t - 1), a.ncb, a.tmo);
+      } else if (L == 1) {
+        ok = wait_ge(a.cnt + t, a.ncb, a.tmo);
+      } else {
+        ok = wait_ge(a.cnt + T + t, a.ncb, a.tmo);
+        if (ok && t > 0) ok = wait_ge(a.cnt + 2L * T + (t - 1), a.ncb, a.tmo);
+      }
+      AVC_PSTAMP(1);
+      AVC_PRSTAMP(7);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      *flag = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (*flag == 0) break;
+    AVC_PSTAMP(2);
+
+    // ---- epilogue operands (gx1 is a hand-off: loaded after the acquire) ------------------
+    f32x4 gxv[4];
+    {
+      const float* gxr = L == 0 ? a.gx0 + ((long)t * B + bc) * G4 + p0
+                                : (L == 1 ? a.b1 + p0 : a.gx1 + ((long)t * B + bc) * G4 + p0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gxv[g] = *reinterpret_cast<const f32x4*>(gxr + 4 * g);
+    }
+
+    // ---- recurrent / input product over this wave's K quarter ----------------------------
+    f32x4 acc[RT][NC];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int n = 0; n < NC; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const unsigned char* src = L == 0 ? (t > 0 ? a.hs0 + (long)(t - 1) * a.hsz : nullptr)
+                                      : (L == 1 ? a.hs0 + (long)t * a.hsz
+                                                : (t > 0 ? a.hs1 + (long)(t - 1) * a.hsz : nullptr));
+    if (src != nullptr) {
+      const long hbase = (long)kc0 * 2048;
+      const auto hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(src) + hbase, 0,
+                                                         (int)((long)a.ntile * nck * 2048 - hbase), 0x00020000);
+      const int hrow16 = nck * 2048;
+      f16x8 hA[RT][2], hB[RT][2], wt[2];
+#define AVC_PLD(HV, C)                                                                             \
+  _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                                 \
+    HV[r][0] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048, 0)); \
+    HV[r][1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048 + 1024, 0)); \
+  }
+#define AVC_PMFMA(HV, C)                                                                           \
+  wt[0] = *reinterpret_cast<const f16x8*>(wl + ((w * NCH + (C)) * 2 + 0) * 1024 + lane * 16);      \
+  wt[1] = *reinterpret_cast<const f16x8*>(wl + ((w * NCH + (C)) * 2 + 1) * 1024 + lane * 16);      \
+  _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                                 \
+    _Pragma("unroll") for (int n = 0; n < 3; ++n) {                                                \
+      acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][1], wreg[n][C][0], acc[r][n], 0, 0, 0); \
+      acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wreg[n][C][1], acc[r][n], 0, 0, 0); \
+      acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wreg[n][C][0], acc[r][n], 0, 0, 0); \
+    }                                                                                              \
+    acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][1], wt[0], acc[r][3], 0, 0, 0);      \
+    acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[1], acc[r][3], 0, 0, 0);      \
+    acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[0], acc[r][3], 0, 0, 0);      \
+  }
+      AVC_PLD(hA, 0)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH) {
+          if (c & 1) { AVC_PLD(hA, c + 1) } else { AVC_PLD(hB, c + 1) }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (c & 1) { AVC_PMFMA(hB, c) } else { AVC_PMFMA(hA, c) }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#undef AVC_PMFMA
+#undef AVC_PLD
+    }
+
+    AVC_PSTAMP(3);
+    // ---- fixed-order cross-wave reduction (as lstm_split_step_kernel) --------------------
+    float* mine = part + w * MB * RP;
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int n = 0; n < NC; ++n)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e];
+    __syncthreads();
+    if (L == 1) {
+      // projection slot: the same fixed-order sum, scale and bias per 4 columns, but stored as
+      // whole 128-B lines (a wave instruction writes 4 rows x 256 B): partial-line write-through
+      // stores took ~10 us per step to drain
+      AVC_PSTAMP(4);
+      const auto ors = __builtin_amdgcn_make_buffer_rsrc(a.gx1 + (long)t * B * G4 + cb * TW, 0,
+                                                         (int)((long)B * G4 * 4), 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = w * 16 + i * 4 + (lane >> 4);
+        if (r < MB && r < B) {
+          const int off = r * RP + 4 * pc;
+          f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
+#pragma unroll
+          for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * MB * RP + off);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v * wiv1 + b1v), ors,
+                                                 (int)(r * G4 * 4 + 16 * pc), 0, 16 /*sc1*/);
+        }
+      }
+    }
+    f32x4 sum[4];
+    if (L != 1) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int off = row * RP + blk * 16 + 4 * g;
+        f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
+#pragma unroll
+        for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * MB * RP + off);
+        sum[g] = v;
+      }
+      AVC_PSTAMP(4);
+    }
+    // ---- epilogue (recurrent slots) --------------------------------------------------------
+    if (L != 1 && live) {
+      const f32x4 zi = sum[0] * wiv[0] + gxv[0];
+      const f32x4 zf = sum[1] * wiv[1] + gxv[1];
+      const f32x4 zg = sum[2] * wiv[2] + gxv[2];
+      const f32x4 zo = sum[3] * wiv[3] + gxv[3];
+      f32x4 hv, ig, fg, gg, og;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ig[u] = sigmoidf_(zi[u]);
+        fg[u] = sigmoidf_(zf[u]);
+        gg[u] = tanhf(zg[u]);
+        og[u] = sigmoidf_(zo[u]);
+        cst[u] = fg[u] * cst[u] + ig[u] * gg[u];
+        hv[u] = og[u] * tanhf(cst[u]);
+      }
+      *reinterpret_cast<f32x4*>(y_out + ((long)t * B + b) * H + j0) = hv;
+      if (c_save) *reinterpret_cast<f32x4*>(c_save + ((long)t * B + b) * H + j0) = cst;
+      if (g_save) {
+        float* go = g_save + ((long)t * B + b) * G4 + p0;
+        *reinterpret_cast<f32x4*>(go) = ig;
+        *reinterpret_cast<f32x4*>(go + 4) = fg;
+        *reinterpret_cast<f32x4*>(go + 8) = gg;
+        *reinterpret_cast<f32x4*>(go + 12) = og;
+      }
+      if (t + 1 < T || L == 0) {
+        f16x4 hi, lo;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float v = hv[u] * kHScale;
+          hi[u] = (_Float16)v;
+          lo[u] = (_Float16)(v - (float)hi[u]);
+        }
+        const long off = ((long)(b >> 4) * nck + (j0 >> 5)) * 2048 + (((b & 15) + 16 * ((j0 & 31) >> 3)) * 8 + (j0 & 7)) * 2;
+        const auto ors = __builtin_amdgcn_make_buffer_rsrc(hs_out + (long)t * a.hsz, 0, (int)a.hsz, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hi), ors, (int)off, 0, 16 /*sc1*/);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lo), ors, (int)off + 1024, 0, 16 /*sc1*/);
+      }
+    }
+    // ---- publish: every storing wave drains, barrier, one lane counts the workgroup in ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    AVC_PSTAMP(5);
+    AVC_PRSTAMP(6);
+    if (tid == 0)
+      __hip_atomic_fetch_add((gu32*)(my_cnt + t), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+inline size_t al(size_t b) { return (b + 255) & ~size_t(255); }
+
+}  // namespace
+
+bool lstm2_persist_eligible(int T, int B, int H) {
+  if (g_persist_mode == 0 || T < 1 || B < 1 || B > 64 || !(H == 1024 || H == 512)) return false;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  return 3 * (4 * H / 64) <= cus;  // one resident workgroup per CU for every slot
+}
+
+size_t lstm2_persist_scratch(int T, int B, int H) {
+  const size_t ntile = (size_t)(B + 15) / 16;
+  const size_t hsz = ntile * 16 * H * 2 * 2;
+  return 2 * al((size_t)T * hsz) + al((size_t)T * B * 4 * H * sizeof(float)) +
+         al((size_t)(3 * T + 64) * sizeof(unsigned)) + 4096;
+}
+
+// gx0 [T][B][4H] (layer 0's input projection + biases, permuted columns) is computed by the
+// caller; w*_s are the split weights with their per-row unscale (lstm_split.hip layout).
+int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx0,
+                          const _Float16* w0_s, const float* winv0, const _Float16* w1i_s,
+                          const float* winv1i, const _Float16* w1h_s, const float* winv1h,
+                          const float* b1_p, float* y0, float* y1, float* g0, float* c0, float* g1,
+                          float* c1, hipStream_t s) {
+  AVC_CHECK_ARG(lstm2_persist_eligible(T, B, H), "lstm2 persistent path: not eligible for this shape");
+  Scratch sc(ctx);
+  const int ntile = (B + 15) / 16;
+  const long hsz = (long)ntile * 16 * H * 2 * 2;  // bytes per split-h step buffer
+  AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
+  AVC_TAKE(hs1, unsigned char, (size_t)T * hsz, sc);
+  AVC_TAKE(gx1, float, (size_t)T * B * 4 * H, sc);
+  AVC_TAKE(words, unsigned, (size_t)3 * T + 64, sc);  // counters [3][T], give-up word after them
+  // counters and give-up word start at the allocation's start, padded to 16 B (Guideline 16)
+  const size_t wbytes = (((size_t)3 * T + 1) * sizeof(unsigned) + 15) & ~size_t(15);
+  AVC_HIP(hipMemsetAsync(words, 0, wbytes, s));
+  PersistArgs a{};
+  a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
+  a.W[0] = reinterpret_cast<const unsigned char*>(w0_s);
+  a.W[1] = reinterpret_cast<const unsigned char*>(w1i_s);
+  a.W[2] = reinterpret_cast<const unsigned char*>(w1h_s);
+  a.winv[0] = winv0; a.winv[1] = winv1i; a.winv[2] = winv1h;
+  a.gx0 = gx0; a.b1 = b1_p; a.gx1 = gx1;
+  a.hs0 = hs0; a.hs1 = hs1; a.hsz = hsz;
+  a.y0 = y0; a.y1 = y1; a.g0 = g0; a.g1 = g1; a.c0 = c0; a.c1 = c1;
+  a.cnt = words; a.tmo = words + 3 * T;
+  const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
+  const int nch = H / 32 / 4;
+  const size_t lds = (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16;
+  hipEvent_t ev = timing_begin(TC_LSTM2_PERSIST, s);
+  const dim3 grid(3 * a.ncb);
+#define AVC_PERSIST(NCHV, RTV)                                                                    \
+  {                                                                                               \
+    lstm2_persist_kernel<NCHV, RTV><<<grid, 256, lds, s>>>(a);                                    \
+  }
+  if (nch == 8) {
+    if (RT == 1) AVC_PERSIST(8, 1) else if (RT == 2) AVC_PERSIST(8, 2) else AVC_PERSIST(8, 4)
+  } else {
+    if (RT == 1) AVC_PERSIST(4, 1) else if (RT == 2) AVC_PERSIST(4, 2) else AVC_PERSIST(4, 4)
+  }
+#undef AVC_PERSIST
+  AVC_LAUNCH_CHECK();
+  if (ev) {
+    // one launch = the whole 2-layer recurrence: 3 products of [B x H] . [H x 4H] per time step;
+    // algorithmic bytes = the split weights read once + per step the split h operands and the
+    // gx / h / c traffic
+    const double flops = 3.0 * T * 2.0 * B * (double)H * 4.0 * H;
+    const double bytes = 3.0 * 16.0 * (double)H * H + (double)T * (3.0 * 4.0 * B * H + 3.0 * 4.0 * B * 4.0 * H +
+                                                                   2.0 * 4.0 * B * H * 2.0);
+    timing_end(TC_LSTM2_PERSIST, ev, s, flops, bytes);
+  }
+  return AVC_OK;
+}
+
+}  // namespace avc
+
+#ifdef AVC_STAMPS
+extern "C" int avc_debug_stamps_persist(void* buf) {
+  AVC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(avc::g_pstamps), &buf, sizeof(void*), 0, hipMemcpyHostToDevice));
+  return AVC_OK;
+}
+#endif
+
+extern "C" int avc_lstm_persist_tune(int mode) {
+  if (mode < 0 || mode > 1) {
+    avc::set_error("avc_lstm_persist_tune: mode must be 0 (off) or 1 (auto)");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_mode = mode;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_status(long* giveups) {
+  if (!giveups) {
+    avc::set_error("avc_lstm_persist_status: NULL pointer");
+    return AVC_ERR_INVALID;
+  }
+  unsigned v = 0;
+  AVC_HIP(hipDeviceSynchronize());
+  AVC_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(avc::g_persist_giveups), sizeof(unsigned), 0, hipMemcpyDeviceToHost));
+  *giveups = (long)v;
+  return AVC_OK;
+}

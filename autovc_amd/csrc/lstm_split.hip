@@ -607,6 +607,7 @@ size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
   // slabs: at most K/128 splits of every 64-column tile, per slot
   s += (size_t)(nlayers + 1) * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
   s += al((size_t)(T + 2) * 3 * nrb * (4 * H / 64) * sizeof(int));
+  if (nlayers == 2 && B <= 64 && (H == 512 || H == 1024)) s += lstm2_persist_scratch(T, B, H);
   GemmDesc d;
   d.M = (int)TB; d.N = 4 * H; d.Kc = din; d.prec16 = 1;
   return s + gemm_scratch_bytes(d) + 4096;
@@ -762,6 +763,9 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   g.prec16 = 1;
   AVC_TRY(attach_bfrag(ctx, g, w0[0], f_wih, s));
   AVC_TRY(gemm_run(ctx, g, s));
+  if (lstm2_persist_eligible(T, B, H))  // the whole recurrence as one weight-stationary launch
+    return lstm2_persist_forward(ctx, T, B, H, gx, w0_s, winv0, w1i_s, winv1i, w1h_s, winv1h, b1_p,
+                                 y0, y1, g0, c0, g1, c1, s);
 
   float* cpp0 = nullptr;
   float* cpp1 = nullptr;
@@ -888,6 +892,7 @@ extern "C" int avc_lstm_split_tune(int kslice, int col_blocks, int rows64) {
     return AVC_ERR_INVALID;
   }
   avc::g_split_kslice = kslice;
+  ++avc::g_config_epoch;
   avc::g_split_nc = col_blocks;
   avc::g_split_rows64 = rows64 ? 1 : 0;
   return AVC_OK;

@@ -10,6 +10,8 @@ scaling is "weak" and `value` = all frames of all ranks / max-over-ranks time.
 
 --mode train runs BASELINE config 3/4 instead (batch 256 training step: forward, loss with the
 second encoder pass, backward, RCCL gradient all-reduce when N>1, fused clip+Adam+EMA).
+--mode long runs BASELINE config 5: 32 utterances of U{256..1024} frames zero-padded to 1024
+(collate_fn), one Generator forward; `value` counts the utterances' own (unpadded) frames.
 
 The SURVEY §8f rows either side of the Generator have their own lines (replicas, like fwd):
 --mode mel  the auto-encoder mel frontend (spectrogram.py:62-142) of one 60 s utterance;
@@ -37,14 +39,18 @@ PEAK_FP32_MATRIX_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_*_f32, dense
 PEAK_F16_MATRIX_TFLOPS = 2500.0   # dense f16/bf16 MFMA
 PEAK_HBM_GBS = 8000.0
 PEAK_FP64_MATRIX_TFLOPS = 78.6    # AMD MI355X datasheet (fp64 matrix = fp64 vector); not in the guide
-# Roofline of each timed kernel class.  Forward contractions run as 3 f16 MFMA products per
-# fp32 product, so their fp32-equivalent MFMA ceiling is 2500/3 TFLOP/s; the LSTM step streams
-# its (split) weights every time step and is priced against HBM; backward products are fp32.
+# Roofline of each timed kernel class.  Forward and backward contractions run as 3 f16 MFMA
+# products per fp32 product, so their fp32-equivalent MFMA ceiling is 2500/3
+# TFLOP/s; the LSTM step streams its (split) weights every time step and is priced against HBM;
+# the BPTT step (lstm_step_bwd) runs on fp32 MFMA.
 ROOFLINE = {
     "fwd": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
-            "lstm32": ("hbm", PEAK_HBM_GBS)},
-    "train": {"gemm": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
-              "lstm_step_bwd": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm32": ("hbm", PEAK_HBM_GBS)},
+            "lstm32": ("hbm", PEAK_HBM_GBS), "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
+    "long": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
+             "lstm32": ("hbm", PEAK_HBM_GBS), "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
+    "train": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
+              "lstm_step_bwd": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm32": ("hbm", PEAK_HBM_GBS),
+              "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
     "mel": {"dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS), "gemm": ("mfma", PEAK_FP32_MATRIX_TFLOPS)},
     "se": {"lstm_step_fwd": ("hbm", PEAK_HBM_GBS), "gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
            "dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS)},
@@ -58,7 +64,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["fwd", "train", "mel", "se"], default="fwd")
+    ap.add_argument("--mode", choices=["fwd", "train", "long", "mel", "se"], default="fwd")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 64 fwd / 256 train)")
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
@@ -85,6 +91,8 @@ def main():
 
     if args.mode in ("fwd", "train"):
         m = setup_generator(args, dev, rank)
+    elif args.mode == "long":
+        m = setup_long(args, dev, rank)
     elif args.mode == "mel":
         m = setup_mel(args, dev, rank)
     else:
@@ -246,7 +254,7 @@ def setup_generator(args, dev, rank):
         "step": step, "units_per_step": B * T, "unit": "mel-frames/s", "dtype": "f32",
         "metric": METRIC if fwd else "mel-frames/sec AutoVC train step, 80×128 batch",
         "data": "synthetic (U[0,1) mels, |N(0,1)| L2-normalised speaker embeddings; seeded synthetic weights)",
-        "classes": ["gemm", "lstm_step_fwd", "lstm32"] + ([] if fwd else ["lstm_step_bwd"]),
+        "classes": ["gemm", "lstm_step_fwd", "lstm32", "lstm2_persist"] + ([] if fwd else ["lstm_step_bwd"]),
         "flop_per_unit": 56.77e6 if fwd else 192.2e6,
         "config": lambda world: {
             "workload": ("C2: batch=64 synthetic 80x128 mels, Generator forward (conversion path, train-mode BN "
@@ -258,8 +266,80 @@ def setup_generator(args, dev, rank):
             "parallelism": (f"replicas x{world}" if fwd else f"dp{world}"),
             "algorithmic_gflop_per_step": round((56.77e6 if fwd else 192.2e6) * B * T / 1e9, 1),
         },
-        "cpu": (lambda out: _with_dmel(cpu_baseline(args, sd, x_np, out, B, T, rank))) if fwd else None,
+        "cpu": ((lambda out: _with_dmel(cpu_baseline(args, sd, x_np, out, B, T, rank))) if fwd else
+                (lambda out: (cpu_train_baseline(args, sd, T), {}))),
         "extra": eval_bn if fwd else None,
+    }
+
+
+def setup_long(args, dev, rank):
+    """C5 long-form conversion: B = 32 utterances, lengths U{256..1024} (seed 2), zero-padded to
+    1024 frames as collate_fn does (dataloader.py:112-121), one fused Generator forward with
+    train-mode BN (what convert() runs).  The same batch is the C5 parity case of
+    tests/test_gpu_model.py::test_c5_long_form_against_oracle."""
+    import numpy as np
+    from autovc_amd.auto_encoder import AutoEncoder
+    from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_dict
+
+    B = args.batch or 32
+    T = 1024 if args.frames == 128 else args.frames
+    rng = np.random.default_rng(2 + rank)
+    lengths = rng.integers(min(256, T), T + 1, size=B)
+    x_np = synthetic_mel(12 + rank, B, T)
+    for i, n in enumerate(lengths):
+        x_np[i, :, n:] = 0.0
+    valid = int(lengths.sum())
+    sd = torch_state_dict(0)
+    model = AutoEncoder(device=dev, verbose=False)
+    model.load_state_dict(sd)
+    model.to(dev).train()
+    x = torch.from_numpy(x_np).to(dev)
+    c_org = torch.from_numpy(synthetic_embedding(112 + rank, B)).to(dev)
+    c_trg = torch.from_numpy(synthetic_embedding(212 + rank, B)).to(dev)
+
+    def step():
+        with torch.no_grad():
+            return model(x, c_org, c_trg)
+
+    def cpu(out):
+        from oracle import autovc_oracle as orc
+        cores = min(16, len(os.sched_getaffinity(0)))
+        torch.set_num_threads(cores)
+        # bounded sample: the first 4 utterances of the batch (same lengths, same padding)
+        n = min(4, B)
+        xs = torch.from_numpy(x_np[:n])
+        co, ct = c_org[:n].cpu(), c_trg[:n].cpu()
+        bufs = {k: v.clone() for k, v in sd.items() if "running" in k}
+        times = []
+        with torch.no_grad():
+            orc.forward(sd, xs, co, ct, True, bufs)
+            t_start = time.perf_counter()
+            while len(times) < 2 or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 10):
+                t1 = time.perf_counter()
+                orc.forward(sd, xs, co, ct, True, bufs)
+                times.append(time.perf_counter() - t1)
+        times.sort()
+        med = times[len(times) // 2]
+        return ({"value": round(float(lengths[:n].sum()) / med, 1), "unit": "mel-frames/s", "cores": cores,
+                 "kind": "port",
+                 "sample": f"{len(times)} timed reps of the first {n} utterances of the C5 batch (padded to {T}) "
+                           f"through the oracle forward, median; unpadded frames counted; "
+                           f"{torch.get_num_threads()} torch threads"}, {})
+
+    return {
+        "step": step, "units_per_step": valid, "unit": "mel-frames/s", "dtype": "f32",
+        "metric": "mel-frames/sec AutoVC long-form fwd (C5: ragged lengths <= 1024, zero-padded)",
+        "data": "synthetic (U[0,1) mels zero-padded past each length, |N(0,1)| L2-normalised embeddings; "
+                "seeded synthetic weights)",
+        "classes": ["gemm", "lstm_step_fwd", "lstm32", "lstm2_persist"],
+        "flop_per_unit": 56.77e6 * B * T / valid,
+        "config": lambda world: {
+            "workload": f"C5: batch={B} utterances, lengths U{{256..{T}}} zero-padded to {T} frames, Generator "
+                        "forward (train-mode BN), whole-Generator HIP path",
+            "global_batch": world * B, "frames_per_utterance": T, "valid_frames_per_step": valid,
+            "parallelism": f"replicas x{world}",
+            "algorithmic_gflop_per_step": round(56.77e6 * B * T / 1e9, 1)},
+        "cpu": cpu,
     }
 
 
@@ -370,6 +450,33 @@ def pmc_traffic(cls, args):
     if not c:
         return None
     return {"traffic_bytes": c["traffic_bytes"], "source": os.path.relpath(files[-1], HERE)}
+
+
+def cpu_train_baseline(args, sd, T):
+    """Oracle training step (oracle/autovc_oracle.py Trainer: fwd, _loss with the second encoder
+    pass, autograd backward, clip 1.0, Adam, EMA — model.py:303-321) on this host's cores.  A full
+    B = 256 step takes tens of seconds on CPU, so the sample is a bounded B = 32 batch (frames/s
+    is per-frame work; BN statistics are per batch either way)."""
+    from oracle import autovc_oracle as orc
+    from autovc_amd.weights import onehot_embedding, synthetic_mel
+    cores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    Bs = 32
+    X = torch.from_numpy(synthetic_mel(1, Bs, T))
+    c = torch.from_numpy(onehot_embedding(Bs))
+    tr = orc.Trainer(sd)
+    tr.step(X, c)  # warm
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 2 or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 10):
+        t1 = time.perf_counter()
+        tr.step(X, c)
+        times.append(time.perf_counter() - t1)
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": round(Bs * T / med, 1), "unit": "mel-frames/s", "cores": cores, "kind": "port",
+            "sample": f"{len(times)} timed training steps (+1 warm) of a B={Bs}, T={T} one-hot batch through the "
+                      f"oracle Trainer, median; {torch.get_num_threads()} torch threads"}
 
 
 def cpu_baseline(args, sd, x_np, gpu_out, B, T, rank):

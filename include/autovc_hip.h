@@ -205,7 +205,8 @@ int avc_prepared_release(avc_context* ctx);
  * When bit `cls` of mask is set, every launch of that kernel class is bracketed by HIP events on
  * its stream; avc_timing_read sums the event-measured durations and the algorithmic FLOPs/bytes
  * of the recorded launches.  Classes: 0 GEMM (gemm_kernel), 1 LSTM step forward,
- * 2 LSTM step backward, 3 H=32 persistent LSTM, 4 fp64 DFT of the mel frontends. */
+ * 2 LSTM step backward, 3 H=32 persistent LSTM, 4 fp64 DFT of the mel frontends,
+ * 5 the weight-stationary decoder.lstm2 recurrence (one launch per forward). */
 int avc_timing_enable(int mask);
 /* Tuning hook for the per-step LSTM kernel: force the batch rows per workgroup (16/32/64) and the
  * number of waves splitting the reduction (1..8); 0 restores the automatic choice. */
@@ -225,6 +226,13 @@ int avc_gemm_tune(int prec16);
  * 2 x 32 / 2 x 64 with plain (not Kahan-compensated) 128-k partial folds, 128 VGPRs (two
  * workgroups per CU for 6). */
 int avc_gemm_config(int cfg);
+/* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) as ONE weight-stationary launch
+ * (lstm_persist.hip) instead of T + 2 step launches: 0 = never, 1 = whenever eligible (default).
+ * Both paths compute the same arithmetic in the same order (bit-identical outputs). */
+int avc_lstm_persist_tune(int mode);
+/* Synchronises the device and returns in *giveups the number of persistent-recurrence workgroups
+ * that abandoned a bounded wait since the library was loaded (0 = every launch completed). */
+int avc_lstm_persist_status(long* giveups);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,
                     long* launches);

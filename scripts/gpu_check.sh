@@ -15,6 +15,7 @@ run() {
 }
 for step in "$@"; do
   case $step in
+    persist) run persist 300 python -u -m pytest tests/test_gpu_model.py -x -v -s -k persistent --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kern)  run kern 600 python -m pytest tests/test_gpu_kernels.py -v -m gpu -x --timeout 120 -p no:cacheprovider ;;
     model) run model 600 python -m pytest tests/test_gpu_model.py -v -m gpu -s --timeout 200 -p no:cacheprovider ;;
@@ -29,12 +30,16 @@ for step in "$@"; do
     proftrain) run proftrain 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/proftrain -o train -- python3 bench.py --mode train --steps 3 --warmup 1 --no-cpu --no-timing ;;
     ssplit) run ssplit 400 python scripts/sweep_split.py ;;
     sstamps) run sstamps 300 python scripts/stamps_split.py 0:0 0:4 ;;
+    pstamps) run pstamps 300 python scripts/stamps_persist.py ;;
     probe) run probe 200 python scripts/probe_cache.py ;;
     gpmc)  for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" "TA_BUSY_avr TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
              n=$(echo $grp | cut -d' ' -f1); run gpmc_$n 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/gpmc/$n -o g -- python3 scripts/gemm_micro.py; done ;;
     stamps) run stamps 300 python scripts/stamps_lstm.py ;;
     audio) run audio 600 python -m pytest tests/test_gpu_audio.py -v -m gpu -s --timeout 200 -p no:cacheprovider ;;
     benchtrain) run benchtrain 400 python bench.py --mode train --steps 5 --warmup 2 --no-cpu ;;
+    benchtraincpu) run benchtraincpu 500 python bench.py --mode train --steps 5 --warmup 2 ;;
+    benchlong) run benchlong 400 python bench.py --mode long --steps 5 --warmup 2 ;;
+    proflong) run proflong 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/proflong -o long -- python3 bench.py --mode long --steps 5 --warmup 2 --no-cpu --no-timing ;;
     benchmel) run benchmel 400 python bench.py --mode mel --steps 10 --warmup 2 ;;
     benchse) run benchse 400 python bench.py --mode se --steps 10 --warmup 2 ;;
     profmel) run profmel 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profmel -o mel -- python3 bench.py --mode mel --steps 10 --warmup 2 --no-cpu --no-timing ;;

@@ -288,3 +288,37 @@ def test_c5_long_form_against_oracle(cuda_device):
     e = [np.abs(a.cpu().numpy() - b.numpy()).max() for a, b in ((mel, rm), (post, rp), (codes, rc))]
     print(f"C5 B=32 T=1024 ragged: max|d mel|={e[0]:.2e} max|d mel_post|={e[1]:.2e} max|d codes|={e[2]:.2e}")
     assert max(e) <= TOL_MEL
+
+
+@pytest.mark.parametrize("B,T", [(64, 128), (2, 100), (33, 40), (3, 33), (16, 64)])
+def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
+    """decoder.lstm2 as one weight-stationary launch (lstm_persist.hip) against the
+    launch-per-step three-slot wavefront (lstm_split.hip) inside the same fused forward: the two
+    compute the same products in the same order, so every output is bit-identical, on the eager
+    call and on the captured-graph replays; and no workgroup of the persistent launch abandoned a
+    bounded wait."""
+    import ctypes
+    from autovc_amd import _lib
+    from autovc_amd.weights import synthetic_embedding, synthetic_mel
+    ae = make_model(cuda_device)
+    x = _t(synthetic_mel(40 + B, B, T), cuda_device)
+    co, ct = _t(synthetic_embedding(41, B), cuda_device), _t(synthetic_embedding(42, B), cuda_device)
+    outs = {}
+    try:
+        for mode in (0, 1):
+            _lib.call("avc_lstm_persist_tune", mode)
+            runs = []
+            for _ in range(3):  # eager, capture + replay, replay
+                with torch.no_grad():
+                    runs.append([t.clone() for t in ae(x, co, ct)])
+            torch.cuda.synchronize()
+            for r in runs[1:]:
+                assert all(torch.equal(a, b) for a, b in zip(r, runs[0])), f"mode {mode}: replays differ"
+            outs[mode] = runs[0]
+    finally:
+        _lib.call("avc_lstm_persist_tune", 1)
+    giveups = ctypes.c_long(0)
+    _lib.call("avc_lstm_persist_status", ctypes.byref(giveups))
+    assert giveups.value == 0, f"{giveups.value} persistent workgroups abandoned a wait"
+    for name, a, b in zip(("mel", "mel_post", "codes"), outs[0], outs[1]):
+        assert torch.equal(a, b), f"{name}: max|d| {(a - b).abs().max().item():.3e}"
