@@ -19,13 +19,15 @@
 // stays in registers (the epilogue thread of a (batch row, 4 hidden units) pair never changes).
 //
 // Dependencies (counters per slot and time step, zeroed per call):
-//   slot 0 at t waits  cnt0[t-1] == ncb           (all of h0_{t-1})
+//   slot 0 at t waits  cnt0[t-1] == ncb           (all of h0_{t-1})  [replicated: see kRep]
 //   slot 1 at t waits  cnt0[t]   == ncb           (all of h0_t)
 //   slot 2 at t waits  cnt1[t]   == ncb and cnt2[t-1] == ncb
-// Hand-off protocol (cdna_hip_programming.md Guideline 16, counter form): payload stored
-// write-through (sc1), every storing wave drains vmcnt, workgroup barrier, one lane adds to the
-// counter (agent scope); the consumer polls one word relaxed, one lane runs the agent-scope
-// acquire, drains, barrier, then plain loads (the XCD's L2 serves the other CUs of that XCD).
+// Hand-off protocol (cdna_hip_programming.md Guideline 16, counter form with replicas): payload
+// stored write-through (sc1; every 128-B line written whole by one wave instruction), every
+// storing wave drains vmcnt, workgroup barrier, one 8-lane instruction adds to the 8 counter
+// replicas (agent scope); the consumer polls one replica relaxed, workgroup barrier, then EVERY
+// load of handed-off bytes is an sc1 load (default, mode 2: 9.8 us per step), or one agent-scope
+// acquire followed by plain loads (mode 1: 11.4 us per step).
 // Every spin is bounded: on timeout the workgroup sets a shared give-up word, every waiter sees
 // it and leaves, and the host reports the failure (avc_lstm_persist_status).
 //
@@ -39,7 +41,7 @@
 
 namespace avc {
 
-int g_persist_mode = 1;  // avc_lstm_persist_tune(): 0 = never, 1 = when eligible
+int g_persist_mode = 2;  // avc_lstm_persist_tune(): 0 = never; 1 / 2 = when eligible (hand-off form)
 
 namespace {
 
@@ -52,6 +54,19 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 
 constexpr float kHScale = 32768.0f;   // split h is stored as h * 2^15 (lstm_split.hip)
 constexpr unsigned kSpinLimit = 1u << 21;
+// Arrival counters are kept in kRep replicas, each on a 128-B line of its own: a producer adds to
+// every replica with one 8-lane wave instruction, a consumer polls the replica of its own
+// blockIdx % 8 (the XCD under round-robin placement: speed only, any replica is complete once all
+// adds landed).  One shared counter had 128 pollers and 64 adders on one line.
+constexpr int kRep = 8, kLine = 32;  // replicas; unsigned words per 128-B line
+__host__ __device__ __forceinline__ long cnt_index(int L, int T, int t, int r) {
+  return (((long)L * T + t) * kRep + r) * kLine;
+}
+// gx1 hand-off: a ring of kGxRing steps of per-column-block slabs [64 rows][64 columns] fp32, so
+// each (step, column block) pair exchanges one contiguous 16 KB; slot 1 re-fills a ring entry
+// only after every slot-2 workgroup has finished the step that read it (back-pressure wait)
+constexpr int kGxRing = 4;
+constexpr int kLead = 3;  // slot 0 may run at most this many steps ahead of slot 2
 
 __device__ unsigned g_persist_giveups = 0;  // sticky count of timed-out launches (host-read)
 
@@ -86,16 +101,18 @@ struct PersistArgs {
   const float* winv[3];       // per-row unscale
   const float* gx0;           // [T][B][4H] layer-0 input projection + biases (permuted)
   const float* b1;            // [4H] b_ih1 + b_hh1 (permuted)
-  float* gx1;                 // [T][B][4H]
+  float* gx1;                 // [kGxRing][ncb][64][64] slabs (see gx1_slab)
   unsigned char* hs0;         // [T][hsz] split h0_t (fragment-major, 2 KiB per 16-row x 32-k block)
-  unsigned char* hs1;
+  unsigned char* hs1;         // [2][hsz] ring (only slot 2 reads it, one step later)
   long hsz;                   // bytes per time step of a split-h buffer
   float* y0; float* y1;       // [T][B][H] fp32 h
   float* g0; float* g1;       // optional [T][B][4H] activated gates (training)
   float* c0; float* c1;       // optional [T][B][H] cell state (training)
   unsigned* cnt;              // [3][T] arrivals
   unsigned* tmo;              // give-up word
+  int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
 };
+int g_persist_diag = 0;
 
 // One lane waits until *p >= target (relaxed agent-scope polls).  false = gave up (or someone
 // else did: the shared give-up word is checked every 64 polls).
@@ -115,7 +132,10 @@ __device__ bool wait_ge(unsigned* p, unsigned target, unsigned* tmo) {
   }
 }
 
-template <int NCH, int RT>
+// HO = hand-off form on the consumer side: 0 = one agent-scope acquire (L1 invalidate) then plain
+// loads; 1 = no invalidate, EVERY load of handed-off bytes (split h, gx1) an sc1 load
+// (cdna_hip_programming.md Guideline 16, "Valid forms": producer stores sc1 + drained).
+template <int NCH, int RT, int HO>
 __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
   constexpr int NW = 4, NC = 4;
   constexpr int MB = 16 * RT;        // batch rows computed (B <= MB)
@@ -126,7 +146,7 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
   extern __shared__ float lds[];
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds);
   float* part = lds + NW * NCH * 512;
-  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);
+  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);  // [2]: the two polling lanes' results
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
@@ -178,42 +198,68 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
   float* c_save = L == 0 ? a.c0 : a.c1;
   float* g_save = L == 0 ? a.g0 : a.g1;
   float* y_out = L == 0 ? a.y0 : a.y1;
-  unsigned char* hs_out = L == 0 ? a.hs0 : a.hs1;
-  unsigned* my_cnt = a.cnt + (long)L * T;
+  auto gx1_slab = [&](int tt, int c) -> long { return ((long)(tt % kGxRing) * a.ncb + c) * (64 * TW); };
+  const int rep = blockIdx.x & (kRep - 1);
 
   for (int t = 0; t < T; ++t) {
     // ---- wait for this step's operands ----------------------------------------------------
     AVC_PSTAMP(0);
-    if (tid == 0) {
-      bool ok = true;
-      if (L == 0) {
-        if (t > 0) ok = wait_ge(a.cnt + (t - 1), a.ncb, a.tmo);
-      } else if (L == 1) {
-        ok = wait_ge(a.cnt + t, a.ncb, a.tmo);
-      } else {
-        ok = wait_ge(a.cnt + T + t, a.ncb, a.tmo);
-        if (ok && t > 0) ok = wait_ge(a.cnt + 2L * T + (t - 1), a.ncb, a.tmo);
+    // Two lanes poll in parallel (lane 0 of waves 0 and 1): the data this step reads, and the
+    // back-pressure that keeps slots 0 and 1 at most kLead / kGxRing steps ahead of slot 2 (a
+    // slot running far ahead streams gx0 / writes h0 through the Infinity Cache and starves the
+    // others: measured as a bistable 10 vs 20 us per step).  Each polling lane then acquires.
+    if (tid == 0 || tid == 64) {
+      const bool primary = tid == 0;
+      long idx = -1;
+      if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, T, t - 1, rep) : -1)
+                                : (t >= kLead ? cnt_index(2, T, t - kLead, rep) : -1);
+      else if (L == 1) idx = primary ? cnt_index(0, T, t, rep)
+                                     : (t >= kGxRing ? cnt_index(2, T, t - kGxRing, rep) : -1);
+      else idx = primary ? (t > 0 ? cnt_index(2, T, t - 1, rep) : -1) : cnt_index(1, T, t, rep);
+      const bool ok = idx < 0 || wait_ge(a.cnt + idx, a.ncb, a.tmo);
+      if (primary) {
+        AVC_PSTAMP(1);
+        AVC_PRSTAMP(7);
       }
-      AVC_PSTAMP(1);
-      AVC_PRSTAMP(7);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *flag = ok ? 1 : 0;
+      if constexpr (HO == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+      }
+      flag[primary ? 0 : 1] = ok ? 1 : 0;
     }
     __syncthreads();
-    if (*flag == 0) break;
+    if (flag[0] == 0 || flag[1] == 0) break;
     AVC_PSTAMP(2);
 
-    // ---- epilogue operands (gx1 is a hand-off: loaded after the acquire) ------------------
-    f32x4 gxv[4];
-    {
-      const float* gxr = L == 0 ? a.gx0 + ((long)t * B + bc) * G4 + p0
-                                : (L == 1 ? a.b1 + p0 : a.gx1 + ((long)t * B + bc) * G4 + p0);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) gxv[g] = *reinterpret_cast<const f32x4*>(gxr + 4 * g);
-    }
-
     // ---- recurrent / input product over this wave's K quarter ----------------------------
+    // The epilogue operands (gx0 / b1 / the gx1 hand-off) are loaded right after the LAST h
+    // chunk's loads: vmcnt retires in issue order, so loads issued ahead of the h chunks would
+    // hold every MFMA until they land.
+    f32x4 gxv[4];
+    const float* gxr = L == 0 ? a.gx0 + ((long)t * B + bc) * G4 + p0 : a.b1 + p0;
+    auto load_gx = [&]() {
+#ifdef AVC_STAMPS
+      if ((a.diag & 1) && L == 2) {  // timing experiment: skip the gx1 hand-off loads
+#pragma unroll
+        for (int g = 0; g < 4; ++g) gxv[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        return;
+      }
+#endif
+      if (L == 2) {
+        // descriptor base uniform (the slab), lane offset in the VGPR: a per-lane base would make
+        // hipcc wrap each load in a waterfall loop over the 64 distinct descriptors (~10 us/step)
+        const auto grs = __builtin_amdgcn_make_buffer_rsrc(a.gx1 + gx1_slab(t, cb), 0, 64 * TW * 4, 0x00020000);
+        const int vo = (bc * TW + blk * 16) * 4;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          gxv[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(grs, vo + 16 * g, 0, HO ? 16 : 0));
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) gxv[g] = *reinterpret_cast<const f32x4*>(gxr + 4 * g);
+      }
+    };
     f32x4 acc[RT][NC];
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -221,8 +267,10 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
       for (int n = 0; n < NC; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     const unsigned char* src = L == 0 ? (t > 0 ? a.hs0 + (long)(t - 1) * a.hsz : nullptr)
                                       : (L == 1 ? a.hs0 + (long)t * a.hsz
-                                                : (t > 0 ? a.hs1 + (long)(t - 1) * a.hsz : nullptr));
-    if (src != nullptr) {
+                                                : (t > 0 ? a.hs1 + (long)((t - 1) & 1) * a.hsz : nullptr));
+    if (src == nullptr) {
+      load_gx();
+    } else {
       const long hbase = (long)kc0 * 2048;
       const auto hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(src) + hbase, 0,
                                                          (int)((long)a.ntile * nck * 2048 - hbase), 0x00020000);
@@ -230,8 +278,8 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
       f16x8 hA[RT][2], hB[RT][2], wt[2];
 #define AVC_PLD(HV, C)                                                                             \
   _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                                 \
-    HV[r][0] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048, 0)); \
-    HV[r][1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048 + 1024, 0)); \
+    HV[r][0] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048, HO ? 16 : 0)); \
+    HV[r][1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048 + 1024, HO ? 16 : 0)); \
   }
 #define AVC_PMFMA(HV, C)                                                                           \
   wt[0] = *reinterpret_cast<const f16x8*>(wl + ((w * NCH + (C)) * 2 + 0) * 1024 + lane * 16);      \
@@ -247,10 +295,12 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
     acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[0], acc[r][3], 0, 0, 0);      \
   }
       AVC_PLD(hA, 0)
+      if constexpr (NCH == 1) load_gx();
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         if (c + 1 < NCH) {
           if (c & 1) { AVC_PLD(hA, c + 1) } else { AVC_PLD(hB, c + 1) }
+          if (c + 2 == NCH) load_gx();
         }
         __builtin_amdgcn_sched_barrier(0);
         if (c & 1) { AVC_PMFMA(hB, c) } else { AVC_PMFMA(hA, c) }
@@ -270,13 +320,13 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e];
     __syncthreads();
+    f32x4 hv, ig, fg, gg, og;
     if (L == 1) {
-      // projection slot: the same fixed-order sum, scale and bias per 4 columns, but stored as
-      // whole 128-B lines (a wave instruction writes 4 rows x 256 B): partial-line write-through
-      // stores took ~10 us per step to drain
+      // projection slot: the same fixed-order sum, scale and bias per 4 columns, stored to this
+      // (step, column block)'s contiguous 16 KB slab as whole 128-B lines (a wave instruction
+      // writes 4 rows x 256 B; partial-line write-through stores took ~10 us per step to drain)
       AVC_PSTAMP(4);
-      const auto ors = __builtin_amdgcn_make_buffer_rsrc(a.gx1 + (long)t * B * G4 + cb * TW, 0,
-                                                         (int)((long)B * G4 * 4), 0x00020000);
+      const auto ors = __builtin_amdgcn_make_buffer_rsrc(a.gx1 + gx1_slab(t, cb), 0, 64 * TW * 4, 0x00020000);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = w * 16 + i * 4 + (lane >> 4);
@@ -286,12 +336,11 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
 #pragma unroll
           for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * MB * RP + off);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v * wiv1 + b1v), ors,
-                                                 (int)(r * G4 * 4 + 16 * pc), 0, 16 /*sc1*/);
+                                                 (r * TW + 4 * pc) * 4, 0, 16 /*sc1*/);
         }
       }
-    }
-    f32x4 sum[4];
-    if (L != 1) {
+    } else {
+      f32x4 sum[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int off = row * RP + blk * 16 + 4 * g;
@@ -301,23 +350,47 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
         sum[g] = v;
       }
       AVC_PSTAMP(4);
-    }
-    // ---- epilogue (recurrent slots) --------------------------------------------------------
-    if (L != 1 && live) {
-      const f32x4 zi = sum[0] * wiv[0] + gxv[0];
-      const f32x4 zf = sum[1] * wiv[1] + gxv[1];
-      const f32x4 zg = sum[2] * wiv[2] + gxv[2];
-      const f32x4 zo = sum[3] * wiv[3] + gxv[3];
-      f32x4 hv, ig, fg, gg, og;
+      // ---- gate epilogue; only the split h (the hand-off) is stored before publishing ------
+      if (live) {
+        const f32x4 zi = sum[0] * wiv[0] + gxv[0];
+        const f32x4 zf = sum[1] * wiv[1] + gxv[1];
+        const f32x4 zg = sum[2] * wiv[2] + gxv[2];
+        const f32x4 zo = sum[3] * wiv[3] + gxv[3];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        ig[u] = sigmoidf_(zi[u]);
-        fg[u] = sigmoidf_(zf[u]);
-        gg[u] = tanhf(zg[u]);
-        og[u] = sigmoidf_(zo[u]);
-        cst[u] = fg[u] * cst[u] + ig[u] * gg[u];
-        hv[u] = og[u] * tanhf(cst[u]);
+        for (int u = 0; u < 4; ++u) {
+          ig[u] = sigmoidf_(zi[u]);
+          fg[u] = sigmoidf_(zf[u]);
+          gg[u] = tanhf(zg[u]);
+          og[u] = sigmoidf_(zo[u]);
+          cst[u] = fg[u] * cst[u] + ig[u] * gg[u];
+          hv[u] = og[u] * tanhf(cst[u]);
+        }
+        if (t + 1 < T || L == 0) {
+          f16x4 hi, lo;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float v = hv[u] * kHScale;
+            hi[u] = (_Float16)v;
+            lo[u] = (_Float16)(v - (float)hi[u]);
+          }
+          const long off = ((long)(b >> 4) * nck + (j0 >> 5)) * 2048 + (((b & 15) + 16 * ((j0 & 31) >> 3)) * 8 + (j0 & 7)) * 2;
+          unsigned char* hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
+          const auto ors = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)a.hsz, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hi), ors, (int)off, 0, 16 /*sc1*/);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lo), ors, (int)off + 1024, 0, 16 /*sc1*/);
+        }
       }
+    }
+    // ---- publish: every storing wave drains, barrier, the workgroup counts itself in ------
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    AVC_PSTAMP(5);
+    AVC_PRSTAMP(6);
+    if (tid < kRep)
+      __hip_atomic_fetch_add((gu32*)(a.cnt + cnt_index(L, T, t, tid)), 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    // outputs nobody reads inside this launch: stored after publishing (off the hand-off path)
+    if (L != 1 && live) {
       *reinterpret_cast<f32x4*>(y_out + ((long)t * B + b) * H + j0) = hv;
       if (c_save) *reinterpret_cast<f32x4*>(c_save + ((long)t * B + b) * H + j0) = cst;
       if (g_save) {
@@ -327,27 +400,7 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
         *reinterpret_cast<f32x4*>(go + 8) = gg;
         *reinterpret_cast<f32x4*>(go + 12) = og;
       }
-      if (t + 1 < T || L == 0) {
-        f16x4 hi, lo;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float v = hv[u] * kHScale;
-          hi[u] = (_Float16)v;
-          lo[u] = (_Float16)(v - (float)hi[u]);
-        }
-        const long off = ((long)(b >> 4) * nck + (j0 >> 5)) * 2048 + (((b & 15) + 16 * ((j0 & 31) >> 3)) * 8 + (j0 & 7)) * 2;
-        const auto ors = __builtin_amdgcn_make_buffer_rsrc(hs_out + (long)t * a.hsz, 0, (int)a.hsz, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hi), ors, (int)off, 0, 16 /*sc1*/);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lo), ors, (int)off + 1024, 0, 16 /*sc1*/);
-      }
     }
-    // ---- publish: every storing wave drains, barrier, one lane counts the workgroup in ----
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    AVC_PSTAMP(5);
-    AVC_PRSTAMP(6);
-    if (tid == 0)
-      __hip_atomic_fetch_add((gu32*)(my_cnt + t), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -366,8 +419,8 @@ bool lstm2_persist_eligible(int T, int B, int H) {
 size_t lstm2_persist_scratch(int T, int B, int H) {
   const size_t ntile = (size_t)(B + 15) / 16;
   const size_t hsz = ntile * 16 * H * 2 * 2;
-  return 2 * al((size_t)T * hsz) + al((size_t)T * B * 4 * H * sizeof(float)) +
-         al((size_t)(3 * T + 64) * sizeof(unsigned)) + 4096;
+  return al((size_t)T * hsz) + al((size_t)2 * hsz) + al((size_t)kGxRing * (4 * H / 64) * 64 * 64 * sizeof(float)) +
+         al((size_t)(3 * T * kRep + 1) * kLine * sizeof(unsigned)) + 4096;
 }
 
 // gx0 [T][B][4H] (layer 0's input projection + biases, permuted columns) is computed by the
@@ -382,11 +435,12 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2 * 2;  // bytes per split-h step buffer
   AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
-  AVC_TAKE(hs1, unsigned char, (size_t)T * hsz, sc);
-  AVC_TAKE(gx1, float, (size_t)T * B * 4 * H, sc);
-  AVC_TAKE(words, unsigned, (size_t)3 * T + 64, sc);  // counters [3][T], give-up word after them
+  AVC_TAKE(hs1, unsigned char, (size_t)2 * hsz, sc);                      // ring of 2
+  AVC_TAKE(gx1, float, (size_t)kGxRing * (4 * H / 64) * 64 * 64, sc);     // slab ring
+  // counters [3][T][kRep] (one 128-B line each), then the give-up word on a line of its own
+  AVC_TAKE(words, unsigned, (size_t)(3 * T * kRep + 1) * kLine, sc);
   // counters and give-up word start at the allocation's start, padded to 16 B (Guideline 16)
-  const size_t wbytes = (((size_t)3 * T + 1) * sizeof(unsigned) + 15) & ~size_t(15);
+  const size_t wbytes = (size_t)(3 * T * kRep + 1) * kLine * sizeof(unsigned);
   AVC_HIP(hipMemsetAsync(words, 0, wbytes, s));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
@@ -397,7 +451,8 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   a.gx0 = gx0; a.b1 = b1_p; a.gx1 = gx1;
   a.hs0 = hs0; a.hs1 = hs1; a.hsz = hsz;
   a.y0 = y0; a.y1 = y1; a.g0 = g0; a.g1 = g1; a.c0 = c0; a.c1 = c1;
-  a.cnt = words; a.tmo = words + 3 * T;
+  a.diag = g_persist_diag;
+  a.cnt = words; a.tmo = words + (size_t)3 * T * kRep * kLine;
   const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
   const int nch = H / 32 / 4;
   const size_t lds = (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16;
@@ -405,7 +460,8 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   const dim3 grid(3 * a.ncb);
 #define AVC_PERSIST(NCHV, RTV)                                                                    \
   {                                                                                               \
-    lstm2_persist_kernel<NCHV, RTV><<<grid, 256, lds, s>>>(a);                                    \
+    if (g_persist_mode == 2) lstm2_persist_kernel<NCHV, RTV, 1><<<grid, 256, lds, s>>>(a);        \
+    else lstm2_persist_kernel<NCHV, RTV, 0><<<grid, 256, lds, s>>>(a);                            \
   }
   if (nch == 8) {
     if (RT == 1) AVC_PERSIST(8, 1) else if (RT == 2) AVC_PERSIST(8, 2) else AVC_PERSIST(8, 4)
@@ -429,6 +485,11 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
 }  // namespace avc
 
 #ifdef AVC_STAMPS
+extern "C" int avc_debug_persist_diag(int bits) {
+  avc::g_persist_diag = bits;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
 extern "C" int avc_debug_stamps_persist(void* buf) {
   AVC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(avc::g_pstamps), &buf, sizeof(void*), 0, hipMemcpyHostToDevice));
   return AVC_OK;
@@ -436,8 +497,8 @@ extern "C" int avc_debug_stamps_persist(void* buf) {
 #endif
 
 extern "C" int avc_lstm_persist_tune(int mode) {
-  if (mode < 0 || mode > 1) {
-    avc::set_error("avc_lstm_persist_tune: mode must be 0 (off) or 1 (auto)");
+  if (mode < 0 || mode > 2) {
+    avc::set_error("avc_lstm_persist_tune: mode must be 0 (off), 1 (acquire hand-off) or 2 (sc1 loads)");
     return AVC_ERR_INVALID;
   }
   avc::g_persist_mode = mode;

@@ -227,8 +227,9 @@ int avc_gemm_tune(int prec16);
  * workgroups per CU for 6). */
 int avc_gemm_config(int cfg);
 /* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) as ONE weight-stationary launch
- * (lstm_persist.hip) instead of T + 2 step launches: 0 = never, 1 = whenever eligible (default).
- * Both paths compute the same arithmetic in the same order (bit-identical outputs). */
+ * (lstm_persist.hip) instead of T + 2 step launches: 0 = never; whenever eligible with the
+ * in-launch hand-offs read 1 = after an agent-scope acquire, 2 = by sc1 loads (default).
+ * Every path computes the same arithmetic in the same order (bit-identical outputs). */
 int avc_lstm_persist_tune(int mode);
 /* Synchronises the device and returns in *giveups the number of persistent-recurrence workgroups
  * that abandoned a bounded wait since the library was loaded (0 = every launch completed). */

@@ -30,7 +30,12 @@ for step in "$@"; do
     proftrain) run proftrain 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/proftrain -o train -- python3 bench.py --mode train --steps 3 --warmup 1 --no-cpu --no-timing ;;
     ssplit) run ssplit 400 python scripts/sweep_split.py ;;
     sstamps) run sstamps 300 python scripts/stamps_split.py 0:0 0:4 ;;
-    pstamps) run pstamps 300 python scripts/stamps_persist.py ;;
+    pstamps) run pstamps 300 python scripts/stamps_persist.py 1 ;;
+    pstamps2) run pstamps2 300 python scripts/stamps_persist.py 2 ;;
+    pstampsd1) run pstampsd1 300 python scripts/stamps_persist.py 1 1 ;;
+    pstampsd2) run pstampsd2 300 python scripts/stamps_persist.py 1 2 ;;
+    pmodes) run pmodes 300 python scripts/persist_modes.py ;;
+    pmodes1) run pmodes1 300 python scripts/persist_modes.py 1 0 1 1 ;;
     probe) run probe 200 python scripts/probe_cache.py ;;
     gpmc)  for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" "TA_BUSY_avr TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
              n=$(echo $grp | cut -d' ' -f1); run gpmc_$n 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/gpmc/$n -o g -- python3 scripts/gemm_micro.py; done ;;

@@ -20,6 +20,11 @@ from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_d
 
 B, T, NCB = 64, 128, 64
 lib = _lib.load()
+if len(sys.argv) > 1:
+    _lib.call("avc_lstm_persist_tune", int(sys.argv[1]))
+if len(sys.argv) > 2:  # diagnostic bits (timing experiments; outputs not meaningful)
+    lib.avc_debug_persist_diag.argtypes = [ctypes.c_int]
+    lib.avc_debug_persist_diag(int(sys.argv[2]))
 lib.avc_debug_stamps_persist.argtypes = [ctypes.c_void_p]
 dev = torch.device("cuda:0")
 ae = AutoEncoder(device=dev, verbose=False)

@@ -305,7 +305,7 @@ def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
     co, ct = _t(synthetic_embedding(41, B), cuda_device), _t(synthetic_embedding(42, B), cuda_device)
     outs = {}
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             _lib.call("avc_lstm_persist_tune", mode)
             runs = []
             for _ in range(3):  # eager, capture + replay, replay
@@ -316,9 +316,10 @@ def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
                 assert all(torch.equal(a, b) for a, b in zip(r, runs[0])), f"mode {mode}: replays differ"
             outs[mode] = runs[0]
     finally:
-        _lib.call("avc_lstm_persist_tune", 1)
+        _lib.call("avc_lstm_persist_tune", 2)
     giveups = ctypes.c_long(0)
     _lib.call("avc_lstm_persist_status", ctypes.byref(giveups))
     assert giveups.value == 0, f"{giveups.value} persistent workgroups abandoned a wait"
-    for name, a, b in zip(("mel", "mel_post", "codes"), outs[0], outs[1]):
-        assert torch.equal(a, b), f"{name}: max|d| {(a - b).abs().max().item():.3e}"
+    for mode in (1, 2):
+        for name, a, b in zip(("mel", "mel_post", "codes"), outs[0], outs[mode]):
+            assert torch.equal(a, b), f"mode {mode} {name}: max|d| {(a - b).abs().max().item():.3e}"
