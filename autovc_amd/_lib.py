@@ -150,7 +150,8 @@ def ptr(t) -> int | None:
     return t.data_ptr()
 
 
-TIMING_CLASSES = {"gemm": 0, "lstm_step_fwd": 1, "lstm_step_bwd": 2, "lstm32": 3, "dft64": 4, "lstm2_persist": 5}
+TIMING_CLASSES = {"gemm": 0, "lstm_step_fwd": 1, "lstm_step_bwd": 2, "lstm32": 3, "dft64": 4, "lstm2_persist": 5,
+                  "lstm1_persist": 6}
 
 
 def timing_enable(names):

@@ -483,7 +483,7 @@ int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* co
   hipStream_t s = S(stream);
   avc_gen_graph& g = ctx->gen;
   const bool timing = timing_on(TC_GEMM) || timing_on(TC_LSTM_STEP_FWD) || timing_on(TC_LSTM32) ||
-                      timing_on(TC_LSTM2_PERSIST);
+                      timing_on(TC_LSTM2_PERSIST) || timing_on(TC_LSTM1_PERSIST);
   const bool same = g.T == T && g.B == B && g.training == training && g.version == weights_version &&
                     g.epoch == g_config_epoch &&
                     g.params.size() == (size_t)P_COUNT &&

@@ -56,6 +56,12 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
                           const float* winv1i, const _Float16* w1h_s, const float* winv1h,
                           const float* b1_p, float* y0, float* y1, float* g0, float* c0, float* g1,
                           float* c1, hipStream_t s);
+// one forward layer (decoder.lstm1) as one weight-stationary launch, batch split into
+// independent groups; gx = input projection + biases, whh_s = split W_hh followed by winv
+bool lstm1_persist_eligible(int T, int B, int H);
+size_t lstm1_persist_scratch(int T, int B, int H);
+int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx, const _Float16* whh_s,
+                          const float* winv, float* y, float* g, float* c, hipStream_t s);
 // rows of a [4H][D] gate matrix into the permuted gate order p = blk*16 + gate*4 + u (lstm.hip)
 int permute_rows(const float* src, float* dst, int H, int D, hipStream_t s);
 

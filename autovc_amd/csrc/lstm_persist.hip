@@ -31,6 +31,12 @@
 // Every spin is bounded: on timeout the workgroup sets a shared give-up word, every waiter sees
 // it and leaves, and the host reports the failure (avc_lstm_persist_status).
 //
+// One-layer form (decoder.lstm1, decoder.py:50,69): slot 0 alone, grid (ncb, ngrp).  Batch rows
+// never interact in an LSTM, so the batch is split into ngrp independent groups of 16/32/64 rows
+// (blockIdx.y), each with counters of its own: a workgroup then reads only its group's rows of
+// split h per step (32 KB at 16 rows, H = 512) and waits on ncb peers, not ncb x ngrp.  C2 lstm1
+// (B = 64, H = 512): 4 groups x 32 workgroups, 3.7 us per step against ~6.9 us per step launch.
+//
 // Arithmetic is identical to lstm_split_step_kernel's NC = 4 tiles: the same 3xf16 products
 // (hi.lo, lo.hi, hi.hi per 32-deep chunk, in that order), the same K split over 4 waves and
 // the same fixed-order LDS reduction, so the two paths agree bit for bit.
@@ -97,6 +103,8 @@ __device__ unsigned long long* g_pstamps = nullptr;
 
 struct PersistArgs {
   int B, T, H, ncb, ntile;
+  int nslot;                  // 3 = two-layer wavefront (lstm2); 1 = one layer (slot 0 only: lstm1)
+  long cnt_gstride;           // counter words per batch group (blockIdx.y; one-layer form only)
   const unsigned char* W[3];  // split fragment-major weights, permuted gate rows
   const float* winv[3];       // per-row unscale
   const float* gx0;           // [T][B][4H] layer-0 input projection + biases (permuted)
@@ -136,7 +144,7 @@ __device__ bool wait_ge(unsigned* p, unsigned target, unsigned* tmo) {
 // loads; 1 = no invalidate, EVERY load of handed-off bytes (split h, gx1) an sc1 load
 // (cdna_hip_programming.md Guideline 16, "Valid forms": producer stores sc1 + drained).
 template <int NCH, int RT, int HO>
-__global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
+__global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   constexpr int NW = 4, NC = 4;
   constexpr int MB = 16 * RT;        // batch rows computed (B <= MB)
   constexpr int TW = 16 * NC;        // 64 gate rows
@@ -152,6 +160,10 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
   const int l15 = lane & 15, lq = lane >> 4;
   const int L = blockIdx.x / a.ncb, cb = blockIdx.x - L * a.ncb;
   const int B = a.B, H = a.H, T = a.T;
+  // batch group: rows [grp * MB, grp * MB + MB).  LSTM batch rows never interact, so in the
+  // one-layer form every group is an independent recurrence with counters of its own.
+  const int grp = blockIdx.y;
+  unsigned* const cnt = a.cnt + (long)grp * a.cnt_gstride;
   const int nck = H >> 5;            // 32-deep chunks per row
   const long G4 = 4L * H;
 
@@ -179,7 +191,7 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
   // ---- epilogue ownership: thread tid handles (row, blk) = (tid / 4, tid % 4) -------------
   const bool epi = tid < NPAIR;
   const int row = min(tid, NPAIR - 1) / NC, blk = min(tid, NPAIR - 1) % NC;
-  const int b = row;
+  const int b = grp * MB + row;
   const bool live = epi && b < B;
   const int bc = min(b, B - 1);
   const int p0 = cb * TW + blk * 16;   // first permuted gate column of the pair
@@ -212,11 +224,11 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
       const bool primary = tid == 0;
       long idx = -1;
       if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, T, t - 1, rep) : -1)
-                                : (t >= kLead ? cnt_index(2, T, t - kLead, rep) : -1);
+                                : (t >= kLead && a.nslot == 3 ? cnt_index(2, T, t - kLead, rep) : -1);
       else if (L == 1) idx = primary ? cnt_index(0, T, t, rep)
                                      : (t >= kGxRing ? cnt_index(2, T, t - kGxRing, rep) : -1);
       else idx = primary ? (t > 0 ? cnt_index(2, T, t - 1, rep) : -1) : cnt_index(1, T, t, rep);
-      const bool ok = idx < 0 || wait_ge(a.cnt + idx, a.ncb, a.tmo);
+      const bool ok = idx < 0 || wait_ge(cnt + idx, a.ncb, a.tmo);
       if (primary) {
         AVC_PSTAMP(1);
         AVC_PRSTAMP(7);
@@ -271,10 +283,10 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
     if (src == nullptr) {
       load_gx();
     } else {
-      const long hbase = (long)kc0 * 2048;
+      const int hrow16 = nck * 2048;
+      const long hbase = (long)grp * RT * hrow16 + (long)kc0 * 2048;
       const auto hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(src) + hbase, 0,
                                                          (int)((long)a.ntile * nck * 2048 - hbase), 0x00020000);
-      const int hrow16 = nck * 2048;
       f16x8 hA[RT][2], hB[RT][2], wt[2];
 #define AVC_PLD(HV, C)                                                                             \
   _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                                 \
@@ -387,7 +399,7 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
     AVC_PSTAMP(5);
     AVC_PRSTAMP(6);
     if (tid < kRep)
-      __hip_atomic_fetch_add((gu32*)(a.cnt + cnt_index(L, T, t, tid)), 1u, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add((gu32*)(cnt + cnt_index(L, T, t, tid)), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     // outputs nobody reads inside this launch: stored after publishing (off the hand-off path)
     if (L != 1 && live) {
@@ -406,14 +418,97 @@ __global__ __launch_bounds__(256, 1) void lstm2_persist_kernel(PersistArgs a) {
 
 inline size_t al(size_t b) { return (b + 255) & ~size_t(255); }
 
+int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  return cus;
+}
+
+// One-layer form: the narrowest batch groups (16, 32 or 64 rows) whose workgroups all fit the
+// chip side by side.  Every group is an independent recurrence over ncb workgroups, and per step
+// each workgroup reads only its own group's rows of split h.
+int lstm1_rows_per_group(int B, int H) {
+  const int ntile = (B + 15) / 16, ncb = 4 * H / 64, cus = device_cus();
+  for (int RT = 1; RT < 4; RT *= 2)
+    if ((ntile + RT - 1) / RT * ncb <= cus) return RT;
+  return 4;
+}
+
+// Launch: grid (nslot * ncb, ngrp), one resident workgroup per CU (checked by the callers).
+void persist_launch(const PersistArgs& a, int RT, int ngrp, hipStream_t s) {
+  const int nch = a.H / 32 / 4;
+  const size_t lds = (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16;
+  const dim3 grid(a.nslot * a.ncb, ngrp);
+#define AVC_PERSIST(NCHV, RTV)                                                                    \
+  {                                                                                               \
+    if (g_persist_mode == 2) lstm_persist_kernel<NCHV, RTV, 1><<<grid, 256, lds, s>>>(a);        \
+    else lstm_persist_kernel<NCHV, RTV, 0><<<grid, 256, lds, s>>>(a);                            \
+  }
+  if (nch == 8) {
+    if (RT == 1) AVC_PERSIST(8, 1) else if (RT == 2) AVC_PERSIST(8, 2) else AVC_PERSIST(8, 4)
+  } else {
+    if (RT == 1) AVC_PERSIST(4, 1) else if (RT == 2) AVC_PERSIST(4, 2) else AVC_PERSIST(4, 4)
+  }
+#undef AVC_PERSIST
+}
+
 }  // namespace
 
 bool lstm2_persist_eligible(int T, int B, int H) {
   if (g_persist_mode == 0 || T < 1 || B < 1 || B > 64 || !(H == 1024 || H == 512)) return false;
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-  return 3 * (4 * H / 64) <= cus;  // one resident workgroup per CU for every slot
+  return 3 * (4 * H / 64) <= device_cus();  // one resident workgroup per CU for every slot
+}
+
+bool lstm1_persist_eligible(int T, int B, int H) {
+  if (g_persist_mode == 0 || T < 1 || B < 1 || B > 256 || !(H == 1024 || H == 512)) return false;
+  const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
+  return ngrp * (4 * H / 64) <= device_cus();
+}
+
+size_t lstm1_persist_scratch(int T, int B, int H) {
+  const size_t ntile = (size_t)(B + 15) / 16;
+  const size_t hsz = ntile * 16 * H * 2 * 2;
+  return al((size_t)T * hsz) + al((ntile * T * kRep + 1) * kLine * sizeof(unsigned)) + 4096;
+}
+
+// One LSTM layer (decoder.lstm1, decoder.py:50,69) as one weight-stationary launch: slot 0 of the
+// kernel above, with the batch split into independent groups.  gx [T][B][4H] is the input
+// projection + biases (permuted columns); whh_s / winv the split W_hh (lstm_split.hip layout).
+// y / c [T][B][H], g [T][B][4H] (permuted, optional: training).  Bit-identical to the
+// launch-per-step form (same products, same K split, same reduction order).
+int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx, const _Float16* whh_s,
+                          const float* winv, float* y, float* g, float* c, hipStream_t s) {
+  AVC_CHECK_ARG(lstm1_persist_eligible(T, B, H), "lstm1 persistent path: not eligible for this shape");
+  Scratch sc(ctx);
+  const int ntile = (B + 15) / 16;
+  const long hsz = (long)ntile * 16 * H * 2 * 2;
+  const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
+  AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
+  const long gstride = (long)T * kRep * kLine;  // counter words per group: [T][kRep] lines
+  AVC_TAKE(words, unsigned, (size_t)ngrp * gstride + kLine, sc);
+  AVC_HIP(hipMemsetAsync(words, 0, ((size_t)ngrp * gstride + kLine) * sizeof(unsigned), s));
+  PersistArgs a{};
+  a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
+  a.nslot = 1; a.cnt_gstride = gstride;
+  a.W[0] = reinterpret_cast<const unsigned char*>(whh_s);
+  a.winv[0] = winv;
+  a.gx0 = gx;
+  a.hs0 = hs0; a.hsz = hsz;
+  a.y0 = y; a.g0 = g; a.c0 = c;
+  a.diag = g_persist_diag;
+  a.cnt = words; a.tmo = words + (size_t)ngrp * gstride;
+  hipEvent_t ev = timing_begin(TC_LSTM1_PERSIST, s);
+  persist_launch(a, RT, ngrp, s);
+  AVC_LAUNCH_CHECK();
+  if (ev) {
+    // split W_hh read once; per step the split h operand of every workgroup's group, gx, h, c
+    const double flops = (double)T * 2.0 * B * H * 4.0 * H;
+    const double bytes = 16.0 * (double)H * H +
+                         (double)T * (4.0 * B * H * a.ncb + 4.0 * B * 4.0 * H + 2.0 * 4.0 * B * H);
+    timing_end(TC_LSTM1_PERSIST, ev, s, flops, bytes);
+  }
+  return AVC_OK;
 }
 
 size_t lstm2_persist_scratch(int T, int B, int H) {
@@ -444,6 +539,7 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   AVC_HIP(hipMemsetAsync(words, 0, wbytes, s));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
+  a.nslot = 3; a.cnt_gstride = 0;
   a.W[0] = reinterpret_cast<const unsigned char*>(w0_s);
   a.W[1] = reinterpret_cast<const unsigned char*>(w1i_s);
   a.W[2] = reinterpret_cast<const unsigned char*>(w1h_s);
@@ -454,21 +550,8 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   a.diag = g_persist_diag;
   a.cnt = words; a.tmo = words + (size_t)3 * T * kRep * kLine;
   const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
-  const int nch = H / 32 / 4;
-  const size_t lds = (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16;
   hipEvent_t ev = timing_begin(TC_LSTM2_PERSIST, s);
-  const dim3 grid(3 * a.ncb);
-#define AVC_PERSIST(NCHV, RTV)                                                                    \
-  {                                                                                               \
-    if (g_persist_mode == 2) lstm2_persist_kernel<NCHV, RTV, 1><<<grid, 256, lds, s>>>(a);        \
-    else lstm2_persist_kernel<NCHV, RTV, 0><<<grid, 256, lds, s>>>(a);                            \
-  }
-  if (nch == 8) {
-    if (RT == 1) AVC_PERSIST(8, 1) else if (RT == 2) AVC_PERSIST(8, 2) else AVC_PERSIST(8, 4)
-  } else {
-    if (RT == 1) AVC_PERSIST(4, 1) else if (RT == 2) AVC_PERSIST(4, 2) else AVC_PERSIST(4, 4)
-  }
-#undef AVC_PERSIST
+  persist_launch(a, RT, 1, s);
   AVC_LAUNCH_CHECK();
   if (ev) {
     // one launch = the whole 2-layer recurrence: 3 products of [B x H] . [H x 4H] per time step;

@@ -608,6 +608,7 @@ size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
   s += (size_t)(nlayers + 1) * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
   s += al((size_t)(T + 2) * 3 * nrb * (4 * H / 64) * sizeof(int));
   if (nlayers == 2 && B <= 64 && (H == 512 || H == 1024)) s += lstm2_persist_scratch(T, B, H);
+  if (nlayers == 1 && B <= 256 && (H == 512 || H == 1024)) s += lstm1_persist_scratch(T, B, H);
   GemmDesc d;
   d.M = (int)TB; d.N = 4 * H; d.Kc = din; d.prec16 = 1;
   return s + gemm_scratch_bytes(d) + 4096;
@@ -652,6 +653,8 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   g.prec16 = 1;
   AVC_TRY(attach_bfrag(ctx, g, w_ih, f_wih, s));
   AVC_TRY(gemm_run(ctx, g, s));
+  if (!reverse && ldy == H && lstm1_persist_eligible(T, B, H))  // the recurrence as one launch
+    return lstm1_persist_forward(ctx, T, B, H, gx, whh_s, winv, y, saved_gates, saved_c, s);
 
   const int NW = pick_nw(H);
   // narrow full-K tiles when they alone fill the chip (no slab hand-off: one memory round trip

@@ -45,12 +45,15 @@ PEAK_FP64_MATRIX_TFLOPS = 78.6    # AMD MI355X datasheet (fp64 matrix = fp64 vec
 # the BPTT step (lstm_step_bwd) runs on fp32 MFMA.
 ROOFLINE = {
     "fwd": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
-            "lstm32": ("hbm", PEAK_HBM_GBS), "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
+            "lstm32": ("hbm", PEAK_HBM_GBS), "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
+            "lstm1_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
     "long": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
-             "lstm32": ("hbm", PEAK_HBM_GBS), "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
+             "lstm32": ("hbm", PEAK_HBM_GBS), "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
+            "lstm1_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
     "train": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
               "lstm_step_bwd": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm32": ("hbm", PEAK_HBM_GBS),
-              "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
+              "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
+            "lstm1_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
     "mel": {"dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS), "gemm": ("mfma", PEAK_FP32_MATRIX_TFLOPS)},
     "se": {"lstm_step_fwd": ("hbm", PEAK_HBM_GBS), "gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
            "dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS)},
@@ -254,7 +257,7 @@ def setup_generator(args, dev, rank):
         "step": step, "units_per_step": B * T, "unit": "mel-frames/s", "dtype": "f32",
         "metric": METRIC if fwd else "mel-frames/sec AutoVC train step, 80×128 batch",
         "data": "synthetic (U[0,1) mels, |N(0,1)| L2-normalised speaker embeddings; seeded synthetic weights)",
-        "classes": ["gemm", "lstm_step_fwd", "lstm32", "lstm2_persist"] + ([] if fwd else ["lstm_step_bwd"]),
+        "classes": ["gemm", "lstm_step_fwd", "lstm32", "lstm2_persist", "lstm1_persist"] + ([] if fwd else ["lstm_step_bwd"]),
         "flop_per_unit": 56.77e6 if fwd else 192.2e6,
         "config": lambda world: {
             "workload": ("C2: batch=64 synthetic 80x128 mels, Generator forward (conversion path, train-mode BN "
@@ -331,7 +334,7 @@ def setup_long(args, dev, rank):
         "metric": "mel-frames/sec AutoVC long-form fwd (C5: ragged lengths <= 1024, zero-padded)",
         "data": "synthetic (U[0,1) mels zero-padded past each length, |N(0,1)| L2-normalised embeddings; "
                 "seeded synthetic weights)",
-        "classes": ["gemm", "lstm_step_fwd", "lstm32", "lstm2_persist"],
+        "classes": ["gemm", "lstm_step_fwd", "lstm32", "lstm2_persist", "lstm1_persist"],
         "flop_per_unit": 56.77e6 * B * T / valid,
         "config": lambda world: {
             "workload": f"C5: batch={B} utterances, lengths U{{256..{T}}} zero-padded to {T} frames, Generator "

@@ -34,6 +34,7 @@ for step in "$@"; do
     pstamps2) run pstamps2 300 python scripts/stamps_persist.py 2 ;;
     pstampsd1) run pstampsd1 300 python scripts/stamps_persist.py 1 1 ;;
     pstampsd2) run pstampsd2 300 python scripts/stamps_persist.py 1 2 ;;
+    gcfg) run gcfg 300 python scripts/gemm_cfgs.py ;;
     pmodes) run pmodes 300 python scripts/persist_modes.py ;;
     pmodes1) run pmodes1 300 python scripts/persist_modes.py 1 0 1 1 ;;
     probe) run probe 200 python scripts/probe_cache.py ;;

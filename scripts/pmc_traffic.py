@@ -21,6 +21,10 @@ CLASSES = {
     "lstm_step_fwd": lambda n: "lstm_split_step_kernel<" in n or re.search(r"lstm_step_kernel<\d+, false", n) is not None,
     "lstm_step_bwd": lambda n: re.search(r"lstm_step_kernel<\d+, true", n) is not None,
     "lstm32": lambda n: "lstm32_" in n,
+    # the persistent recurrences share one kernel template, told apart by NCH = H / 128: decoder
+    # lstm2 (H = 1024) instantiates NCH = 8, decoder lstm1 (H = 512) NCH = 4
+    "lstm2_persist": lambda n: "lstm_persist_kernel<8," in n,
+    "lstm1_persist": lambda n: "lstm_persist_kernel<4," in n,
 }
 
 

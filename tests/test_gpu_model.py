@@ -290,10 +290,11 @@ def test_c5_long_form_against_oracle(cuda_device):
     assert max(e) <= TOL_MEL
 
 
-@pytest.mark.parametrize("B,T", [(64, 128), (2, 100), (33, 40), (3, 33), (16, 64)])
+@pytest.mark.parametrize("B,T", [(64, 128), (2, 100), (33, 40), (3, 33), (16, 64), (256, 32)])
 def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
-    """decoder.lstm2 as one weight-stationary launch (lstm_persist.hip) against the
-    launch-per-step three-slot wavefront (lstm_split.hip) inside the same fused forward: the two
+    """decoder.lstm2 (B <= 64) and decoder.lstm1 (B <= 256, batch split into independent row
+    groups) as weight-stationary launches (lstm_persist.hip) against the launch-per-step forms
+    (lstm_split.hip) inside the same fused forward: the two
     compute the same products in the same order, so every output is bit-identical, on the eager
     call and on the captured-graph replays; and no workgroup of the persistent launch abandoned a
     bounded wait."""
