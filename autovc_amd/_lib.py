@@ -57,6 +57,8 @@ _SIGS = {
     "avc_gemm_tune": [_I],
     "avc_gemm_config": [_I],
     "avc_lstm_persist_tune": [_I],
+    "avc_lstm_persist_depth": [_I],
+    "avc_lstm_persist_layers": [_I],
     "avc_lstm_persist_status": [ctypes.POINTER(ctypes.c_long)],
     "avc_timing_reset": [],
     "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),

@@ -105,6 +105,10 @@ struct avc_context {
 
 namespace avc {
 
+// zero `bytes` at p (16-B aligned) on stream s with a kernel (elementwise.hip); used instead of
+// hipMemsetAsync everywhere (see there)
+int zero_async(void* p, size_t bytes, hipStream_t s);
+
 struct Scratch {
   avc_context* ctx;
   size_t mark;

@@ -540,6 +540,29 @@ int frames_from_mel_backward(int T, int B, int cm, int ce, const float* df, int 
   return AVC_OK;
 }
 
+// Stream-ordered zeroing by a kernel of our own.  hipMemsetAsync is NOT used anywhere in the
+// library: on ROCm 7.2 a memset issued ahead of a persistent (spin-waiting) launch was measured to
+// land out of order with it (stale counters -> wrong recurrence outputs in the first calls of a
+// process; scripts/persist_repeat.py "modes"), while a kernel is ordered like every other launch.
+__global__ void zero_bytes_kernel(unsigned char* __restrict__ p, size_t n) {
+  const size_t n16 = n / 16;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+    reinterpret_cast<uint4*>(p)[i] = make_uint4(0u, 0u, 0u, 0u);
+  const size_t tail = n16 * 16 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tail < n) p[tail] = 0;
+}
+
+int zero_async(void* p, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return AVC_OK;
+  AVC_CHECK_ARG(p != nullptr && (reinterpret_cast<uintptr_t>(p) & 15) == 0, "zero_async: NULL or unaligned");
+  const size_t n16 = bytes / 16;
+  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>((n16 + 255) / 256, 2048));
+  zero_bytes_kernel<<<blocks, 256, 0, s>>>(static_cast<unsigned char*>(p), bytes);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
 int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s) {
   mel_from_frames_kernel<<<ew_blocks((long)B * cm * T), 256, 0, s>>>(T, B, cm, fr, mel);
   AVC_LAUNCH_CHECK();
@@ -557,7 +580,7 @@ int codes_from_encoder(int T, int B, const float* enc, float* codes, hipStream_t
 int codes_from_encoder_backward(int T, int B, const float* dcodes, float* denc, int accumulate,
                                 hipStream_t s) {
   AVC_CHECK_ARG(T >= 32, "content codes need T >= 32 frames");
-  if (!accumulate) AVC_HIP(hipMemsetAsync(denc, 0, sizeof(float) * (size_t)T * B * 64, s));
+  if (!accumulate) AVC_TRY(zero_async(denc, sizeof(float) * (size_t)T * B * 64, s));
   const long total = (long)B * 32 * (T / 32 + (T + 31) / 32);
   codes_kernel<<<ew_blocks(total), 256, 0, s>>>(T, B, nullptr, const_cast<float*>(dcodes), 1, 1, denc);
   AVC_LAUNCH_CHECK();
@@ -575,7 +598,7 @@ int decoder_input(int T, int B, const float* enc, int ce, const float* ctrg, flo
 int decoder_input_backward(int T, int B, int ce, const float* dd, float* denc, int accumulate,
                            hipStream_t s) {
   AVC_CHECK_ARG(T >= 32, "decoder input needs T >= 32 frames");
-  if (!accumulate) AVC_HIP(hipMemsetAsync(denc, 0, sizeof(float) * (size_t)T * B * 64, s));
+  if (!accumulate) AVC_TRY(zero_async(denc, sizeof(float) * (size_t)T * B * 64, s));
   const long total = (long)B * (T / 32 + (T + 31) / 32) * 32;
   decoder_input_bwd_kernel<<<ew_blocks(total), 256, 0, s>>>(T, B, ce, dd, denc);
   AVC_LAUNCH_CHECK();

@@ -1095,7 +1095,7 @@ int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
 }
 
 int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t stream) {
-  AVC_HIP(hipMemsetAsync(out, 0, sizeof(unsigned), stream));
+  AVC_TRY(zero_async(out, sizeof(unsigned), stream));
   absmax2d(src, rows, cols, ld, out, stream);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
@@ -1140,7 +1140,7 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     if (d.split_scale) {  // power-of-two operand scales from max |A|, max |B| (device side)
       unsigned* amax = sc.take<unsigned>(64);
       if (!amax) return AVC_ERR_WORKSPACE;
-      AVC_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(unsigned), stream));
+      AVC_TRY(zero_async(amax, 2 * sizeof(unsigned), stream));
       if (!d.amax_a) {
         if (d.a_trans) absmax2d(d.A, d.Kc, d.M, d.lda, amax, stream);
         else absmax2d(d.A, d.a_rows, d.Kc, d.lda, amax, stream);

@@ -914,8 +914,8 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TAKE(dgf, float, (size_t)2 * fsz, sc);
     permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w_ih, wih_p, H, din);
     whhT_frag_kernel<<<ew_blocks(4L * H * H), 256, 0, s>>>(w_hh, whhT_p, H);
-    AVC_HIP(hipMemsetAsync(dc, 0, sizeof(float) * B * H, s));
-    AVC_HIP(hipMemsetAsync(dgf, 0, sizeof(float) * 2 * fsz, s));
+    AVC_TRY(zero_async(dc, sizeof(float) * B * H, s));
+    AVC_TRY(zero_async(dgf, sizeof(float) * 2 * fsz, s));
     AVC_LAUNCH_CHECK();
     for (int st = T - 1; st >= 0; --st) {
       const int t = reverse ? T - 1 - st : st;

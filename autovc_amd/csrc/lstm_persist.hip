@@ -48,6 +48,8 @@
 namespace avc {
 
 int g_persist_mode = 2;  // avc_lstm_persist_tune(): 0 = never; 1 / 2 = when eligible (hand-off form)
+int g_persist_layers = 3;  // avc_lstm_persist_layers(): bit 0 = one-layer form, bit 1 = two-layer form
+int g_persist_pd = 2;    // avc_lstm_persist_depth(): h chunks in flight ahead of the MFMAs (1 or 2)
 
 namespace {
 
@@ -143,7 +145,8 @@ __device__ bool wait_ge(unsigned* p, unsigned target, unsigned* tmo) {
 // HO = hand-off form on the consumer side: 0 = one agent-scope acquire (L1 invalidate) then plain
 // loads; 1 = no invalidate, EVERY load of handed-off bytes (split h, gx1) an sc1 load
 // (cdna_hip_programming.md Guideline 16, "Valid forms": producer stores sc1 + drained).
-template <int NCH, int RT, int HO>
+// PD = h chunks loaded ahead of the chunk being multiplied (register buffers PD + 1).
+template <int NCH, int RT, int HO, int PD>
 __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   constexpr int NW = 4, NC = 4;
   constexpr int MB = 16 * RT;        // batch rows computed (B <= MB)
@@ -155,6 +158,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds);
   float* part = lds + NW * NCH * 512;
   int* flag = reinterpret_cast<int*>(part + NW * MB * RP);  // [2]: the two polling lanes' results
+  // [TW] per-row unscale of this block's gate rows, then [TW] b_ih1 + b_hh1 (slot 1): read from
+  // LDS in the epilogue instead of living in registers through the MFMA loop
+  float* cpar = reinterpret_cast<float*>(flag + 4);
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
@@ -196,17 +202,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   const int bc = min(b, B - 1);
   const int p0 = cb * TW + blk * 16;   // first permuted gate column of the pair
   const int j0 = cb * 4 * NC + blk * 4;  // first hidden unit
-  f32x4 wiv[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) wiv[g] = *reinterpret_cast<const f32x4*>(a.winv[L] + p0 + 4 * g);
+  if (tid < TW) {  // published to the epilogue by the first step's barriers
+    cpar[tid] = a.winv[L][cb * TW + tid];
+    if (L == 1) cpar[TW + tid] = a.b1[cb * TW + tid];
+  }
   f32x4 cst = f32x4{0.f, 0.f, 0.f, 0.f};
   // slot 1 stores gx1 in whole lines: lane -> (row 4i + lane/16 of the wave's 16, columns 4*pc..)
   const int pc = lane & 15;
-  f32x4 wiv1 = f32x4{0.f, 0.f, 0.f, 0.f}, b1v = wiv1;
-  if (L == 1) {
-    wiv1 = *reinterpret_cast<const f32x4*>(a.winv[1] + cb * TW + 4 * pc);
-    b1v = *reinterpret_cast<const f32x4*>(a.b1 + cb * TW + 4 * pc);
-  }
   float* c_save = L == 0 ? a.c0 : a.c1;
   float* g_save = L == 0 ? a.g0 : a.g1;
   float* y_out = L == 0 ? a.y0 : a.y1;
@@ -287,7 +289,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       const long hbase = (long)grp * RT * hrow16 + (long)kc0 * 2048;
       const auto hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(src) + hbase, 0,
                                                          (int)((long)a.ntile * nck * 2048 - hbase), 0x00020000);
-      f16x8 hA[RT][2], hB[RT][2], wt[2];
+      constexpr int NB = PD + 1;  // h chunk buffers: PD chunks in flight ahead of the MFMAs
+      f16x8 hb[NB][RT][2], wt[2];
 #define AVC_PLD(HV, C)                                                                             \
   _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                                 \
     HV[r][0] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048, HO ? 16 : 0)); \
@@ -306,16 +309,17 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[1], acc[r][3], 0, 0, 0);      \
     acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[0], acc[r][3], 0, 0, 0);      \
   }
-      AVC_PLD(hA, 0)
-      if constexpr (NCH == 1) load_gx();
+#pragma unroll
+      for (int c = 0; c < PD && c < NCH; ++c) { AVC_PLD(hb[c], c) }
+      if constexpr (NCH <= PD) load_gx();
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        if (c + 1 < NCH) {
-          if (c & 1) { AVC_PLD(hA, c + 1) } else { AVC_PLD(hB, c + 1) }
-          if (c + 2 == NCH) load_gx();
+        if (c + PD < NCH) {
+          AVC_PLD(hb[(c + PD) % NB], c + PD)
+          if (c + PD == NCH - 1) load_gx();
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (c & 1) { AVC_PMFMA(hB, c) } else { AVC_PMFMA(hA, c) }
+        AVC_PMFMA(hb[c % NB], c)
         __builtin_amdgcn_sched_barrier(0);
       }
 #undef AVC_PMFMA
@@ -347,6 +351,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
 #pragma unroll
           for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * MB * RP + off);
+          const f32x4 wiv1 = *reinterpret_cast<const f32x4*>(cpar + 4 * pc);
+          const f32x4 b1v = *reinterpret_cast<const f32x4*>(cpar + TW + 4 * pc);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v * wiv1 + b1v), ors,
                                                  (r * TW + 4 * pc) * 4, 0, 16 /*sc1*/);
         }
@@ -364,6 +370,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       AVC_PSTAMP(4);
       // ---- gate epilogue; only the split h (the hand-off) is stored before publishing ------
       if (live) {
+        f32x4 wiv[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) wiv[g] = *reinterpret_cast<const f32x4*>(cpar + blk * 16 + 4 * g);
         const f32x4 zi = sum[0] * wiv[0] + gxv[0];
         const f32x4 zf = sum[1] * wiv[1] + gxv[1];
         const f32x4 zg = sum[2] * wiv[2] + gxv[2];
@@ -418,6 +427,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 
 inline size_t al(size_t b) { return (b + 255) & ~size_t(255); }
 
+
 int device_cus() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -438,12 +448,13 @@ int lstm1_rows_per_group(int B, int H) {
 // Launch: grid (nslot * ncb, ngrp), one resident workgroup per CU (checked by the callers).
 void persist_launch(const PersistArgs& a, int RT, int ngrp, hipStream_t s) {
   const int nch = a.H / 32 / 4;
-  const size_t lds = (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16;
+  const size_t lds = (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16 + 2 * 64 * sizeof(float);
   const dim3 grid(a.nslot * a.ncb, ngrp);
 #define AVC_PERSIST(NCHV, RTV)                                                                    \
   {                                                                                               \
-    if (g_persist_mode == 2) lstm_persist_kernel<NCHV, RTV, 1><<<grid, 256, lds, s>>>(a);        \
-    else lstm_persist_kernel<NCHV, RTV, 0><<<grid, 256, lds, s>>>(a);                            \
+    if (g_persist_mode == 1) lstm_persist_kernel<NCHV, RTV, 0, 1><<<grid, 256, lds, s>>>(a);      \
+    else if (g_persist_pd == 1) lstm_persist_kernel<NCHV, RTV, 1, 1><<<grid, 256, lds, s>>>(a);   \
+    else lstm_persist_kernel<NCHV, RTV, 1, 2><<<grid, 256, lds, s>>>(a);                          \
   }
   if (nch == 8) {
     if (RT == 1) AVC_PERSIST(8, 1) else if (RT == 2) AVC_PERSIST(8, 2) else AVC_PERSIST(8, 4)
@@ -456,12 +467,12 @@ void persist_launch(const PersistArgs& a, int RT, int ngrp, hipStream_t s) {
 }  // namespace
 
 bool lstm2_persist_eligible(int T, int B, int H) {
-  if (g_persist_mode == 0 || T < 1 || B < 1 || B > 64 || !(H == 1024 || H == 512)) return false;
+  if (g_persist_mode == 0 || !(g_persist_layers & 2) || T < 1 || B < 1 || B > 64 || !(H == 1024 || H == 512)) return false;
   return 3 * (4 * H / 64) <= device_cus();  // one resident workgroup per CU for every slot
 }
 
 bool lstm1_persist_eligible(int T, int B, int H) {
-  if (g_persist_mode == 0 || T < 1 || B < 1 || B > 256 || !(H == 1024 || H == 512)) return false;
+  if (g_persist_mode == 0 || !(g_persist_layers & 1) || T < 1 || B < 1 || B > 256 || !(H == 1024 || H == 512)) return false;
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
   return ngrp * (4 * H / 64) <= device_cus();
 }
@@ -484,10 +495,10 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2 * 2;
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
-  AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
   const long gstride = (long)T * kRep * kLine;  // counter words per group: [T][kRep] lines
+  AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
   AVC_TAKE(words, unsigned, (size_t)ngrp * gstride + kLine, sc);
-  AVC_HIP(hipMemsetAsync(words, 0, ((size_t)ngrp * gstride + kLine) * sizeof(unsigned), s));
+  AVC_TRY(zero_async(words, ((size_t)ngrp * gstride + kLine) * sizeof(unsigned), s));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = 1; a.cnt_gstride = gstride;
@@ -534,9 +545,10 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   AVC_TAKE(gx1, float, (size_t)kGxRing * (4 * H / 64) * 64 * 64, sc);     // slab ring
   // counters [3][T][kRep] (one 128-B line each), then the give-up word on a line of its own
   AVC_TAKE(words, unsigned, (size_t)(3 * T * kRep + 1) * kLine, sc);
-  // counters and give-up word start at the allocation's start, padded to 16 B (Guideline 16)
+  // counters and give-up word start at the allocation's start, padded to 16 B (Guideline 16),
+  // zeroed by zero_async (a kernel: a hipMemsetAsync here was measured landing out of order)
   const size_t wbytes = (size_t)(3 * T * kRep + 1) * kLine * sizeof(unsigned);
-  AVC_HIP(hipMemsetAsync(words, 0, wbytes, s));
+  AVC_TRY(zero_async(words, wbytes, s));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = 3; a.cnt_gstride = 0;
@@ -585,6 +597,26 @@ extern "C" int avc_lstm_persist_tune(int mode) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_mode = mode;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_depth(int chunks) {
+  if (chunks < 1 || chunks > 2) {
+    avc::set_error("avc_lstm_persist_depth: chunks must be 1 or 2");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_pd = chunks;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_layers(int mask) {
+  if (mask < 0 || mask > 3) {
+    avc::set_error("avc_lstm_persist_layers: mask must be 0..3");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_layers = mask;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -678,7 +678,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   if (nks > 1) {
     AVC_TAKE(sl, float, (size_t)nrb * ncb * nks * 1024 * NC, sc);
     AVC_TAKE(ct, int, (size_t)T * nrb * ncb, sc);
-    AVC_HIP(hipMemsetAsync(ct, 0, sizeof(int) * T * nrb * ncb, s));
+    AVC_TRY(zero_async(ct, sizeof(int) * T * nrb * ncb, s));
     slab = sl;
     cnt = ct;
   }
@@ -790,7 +790,7 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
       slab[L] = sl;
     }
     AVC_TAKE(ct, int, (size_t)(T + 2) * cstride, sc);
-    AVC_HIP(hipMemsetAsync(ct, 0, sizeof(int) * (T + 2) * cstride, s));
+    AVC_TRY(zero_async(ct, sizeof(int) * (T + 2) * cstride, s));
     cnt = ct;
   }
   auto hs0p = [&](int t) { return hs0 + (long)(t & 1) * hsz; };

@@ -226,11 +226,18 @@ int avc_gemm_tune(int prec16);
  * 2 x 32 / 2 x 64 with plain (not Kahan-compensated) 128-k partial folds, 128 VGPRs (two
  * workgroups per CU for 6). */
 int avc_gemm_config(int cfg);
-/* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) as ONE weight-stationary launch
- * (lstm_persist.hip) instead of T + 2 step launches: 0 = never; whenever eligible with the
- * in-launch hand-offs read 1 = after an agent-scope acquire, 2 = by sc1 loads (default).
+/* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) and decoder lstm1 (one layer,
+ * batch <= 256) as ONE weight-stationary launch each (lstm_persist.hip) instead of one launch per
+ * time step: 0 = never; whenever eligible with the in-launch hand-offs read 1 = after an
+ * agent-scope acquire, 2 = by sc1 loads (default).
  * Every path computes the same arithmetic in the same order (bit-identical outputs). */
 int avc_lstm_persist_tune(int mode);
+/* Tuning hook: split-h chunks the persistent recurrence keeps in flight ahead of the chunk being
+ * multiplied (1 or 2 = default); same arithmetic either way. */
+int avc_lstm_persist_depth(int chunks);
+/* Tuning hook: which recurrences may take the persistent form (bit 0 = one layer, e.g. decoder
+ * lstm1; bit 1 = two stacked layers, decoder lstm2; default 3 = both). */
+int avc_lstm_persist_layers(int mask);
 /* Synchronises the device and returns in *giveups the number of persistent-recurrence workgroups
  * that abandoned a bounded wait since the library was loaded (0 = every launch completed). */
 int avc_lstm_persist_status(long* giveups);

@@ -37,6 +37,11 @@ for step in "$@"; do
     gcfg) run gcfg 300 python scripts/gemm_cfgs.py ;;
     pmodes) run pmodes 300 python scripts/persist_modes.py ;;
     pmodes1) run pmodes1 300 python scripts/persist_modes.py 1 0 1 1 ;;
+    playr) run playr1 100 python scripts/persist_layer_repeat.py && run playr2 100 python scripts/persist_layer_repeat.py conv ;;
+    prep) run prepb 200 python scripts/persist_repeat.py bump && run prepg 200 python scripts/persist_repeat.py graph && run prepe 200 python scripts/persist_repeat.py eager && run prep0 200 python scripts/persist_repeat.py graph 2 0 && run prep1 200 python scripts/persist_repeat.py graph 1 1 ;;
+    palt) run palt2 200 python scripts/persist_alternate.py 2 && run palt1 200 python scripts/persist_alternate.py 1 && run palt0 200 python scripts/persist_alternate.py 0 ;;
+    pident) run pident 300 python scripts/persist_identity.py ;;
+    pdepth) run pdepth 300 python scripts/persist_modes.py 0 2:1 2:2 2:1 2:2 1:2 ;;
     probe) run probe 200 python scripts/probe_cache.py ;;
     gpmc)  for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" "TA_BUSY_avr TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
              n=$(echo $grp | cut -d' ' -f1); run gpmc_$n 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/gpmc/$n -o g -- python3 scripts/gemm_micro.py; done ;;

@@ -1,6 +1,7 @@
 """Fused C2 forward (B=64, T=128) under each decoder.lstm2 path: 0 = T+2 step launches
 (lstm_split.hip), 1 = weight-stationary launch with acquire hand-offs, 2 = with sc1-load
-hand-offs.  Prints ms per forward (graph replay, 20 reps) and checks outputs are bit-identical."""
+hand-offs; an argument "m:d" also sets the split-h prefetch depth d (avc_lstm_persist_depth).
+Prints ms per forward (graph replay, 20 reps) and checks outputs are bit-identical."""
 import ctypes
 import sys
 import time
@@ -14,7 +15,7 @@ from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_d
 
 dev = torch.device("cuda:0")
 B, T = 64, 128
-modes = [int(v) for v in sys.argv[1:]] or [0, 1, 2, 1, 2]
+modes = sys.argv[1:] or ["0", "1", "2", "1", "2"]
 ae = AutoEncoder(device=dev, verbose=False)
 ae.load_state_dict(torch_state_dict(0))
 ae.to(dev).train()
@@ -22,8 +23,11 @@ x = torch.from_numpy(synthetic_mel(1, B, T)).to(dev)
 co = torch.from_numpy(synthetic_embedding(101, B)).to(dev)
 ct = torch.from_numpy(synthetic_embedding(201, B)).to(dev)
 ref = None
-for mode in modes:
+for spec in modes:
+    mode, _, depth = spec.partition(":")
+    mode = int(mode)
     _lib.call("avc_lstm_persist_tune", mode)
+    _lib.call("avc_lstm_persist_depth", int(depth or 2))
     with torch.no_grad():
         for _ in range(3):
             out = ae(x, co, ct)
@@ -36,8 +40,11 @@ for mode in modes:
     if ref is None:
         ref = [o.clone() for o in out]
     same = all(torch.equal(a, b) for a, b in zip(out, ref))
-    print(f"mode {mode}: {ms:.3f} ms per forward, {B * T / ms * 1e3 / 1e6:.3f} M frames/s, bit-identical {same}")
+    dmax = max((a - b).abs().max().item() for a, b in zip(out, ref))
+    print(f"mode {spec}: {ms:.3f} ms per forward, {B * T / ms * 1e3 / 1e6:.3f} M frames/s, bit-identical {same} "
+          f"(max|d| {dmax:.2e})")
 g = ctypes.c_long(0)
 _lib.call("avc_lstm_persist_status", ctypes.byref(g))
 print("giveups", g.value)
 _lib.call("avc_lstm_persist_tune", 2)
+_lib.call("avc_lstm_persist_depth", 2)

@@ -324,3 +324,31 @@ def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
     for mode in (1, 2):
         for name, a, b in zip(("mel", "mel_post", "codes"), outs[0], outs[mode]):
             assert torch.equal(a, b), f"mode {mode} {name}: max|d| {(a - b).abs().max().item():.3e}"
+
+
+def test_back_to_back_forwards_match(cuda_device):
+    """Twenty fused C2 forwards enqueued back to back (no host sync between them; alternating two
+    input batches so a stale read cannot hide behind equal bytes), each output cloned on the
+    stream and compared with that batch's eager result.  This is the pattern that caught counter
+    zeroing by hipMemsetAsync landing out of order with the persistent recurrences (the library
+    now zeroes with a kernel of its own, zero_async)."""
+    from autovc_amd import _lib
+    from autovc_amd.weights import synthetic_embedding, synthetic_mel
+    ae = make_model(cuda_device)
+    B, T = 64, 128
+    xs = [_t(synthetic_mel(s, B, T), cuda_device) for s in (61, 62)]
+    co, ct = _t(synthetic_embedding(63, B), cuda_device), _t(synthetic_embedding(64, B), cuda_device)
+    with torch.no_grad():
+        _lib.timing_enable(["dft64"])  # timing on => eager launches (no graph) for the references
+        try:
+            refs = [[o.clone() for o in ae(x, co, ct)] for x in xs]
+        finally:
+            _lib.timing_enable([])
+        torch.cuda.synchronize()
+        keep = []
+        for i in range(20):
+            keep.append([o.clone() for o in ae(xs[i % 2], co, ct)])
+        torch.cuda.synchronize()
+    for i, k in enumerate(keep):
+        for name, a, b in zip(("mel", "mel_post", "codes"), k, refs[i % 2]):
+            assert torch.equal(a, b), f"call {i} {name}: max|d| {(a - b).abs().max().item():.3e}"
