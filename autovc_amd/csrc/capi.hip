@@ -87,7 +87,8 @@ struct GenBufs {
 
 size_t gen_scratch(int T, int B) {
   const size_t TB = (size_t)T * B, f = sizeof(float);
-  size_t own = TB * (336 + 512 + 512 + 64 + 64 + 320 + 1024 + 1024 + 80 + 80) * f + 4 * 512 * f + 64 * 256;
+  size_t own = TB * (336 + 512 + 512 + 64 + 64 + 320 + 1024 + 1024 + 80 + 80) * f + 4 * 512 * f + 64 * 256 +
+               2 * gemm_afrag_bytes((long)TB, 512) + 512;
   size_t nested = 0;
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 336, 512));
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 512, 512));
@@ -120,23 +121,32 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TAKE(melf, float, (size_t)TB * 80, sc);
   AVC_TAKE(postf, float, (size_t)TB * 80, sc);
   AVC_TAKE(stat, float, 4 * 512, sc);
+  // conv -> conv links hand the activation over already split for the next GEMM (bn_apply's
+  // fragment output): no fp32 store, no separate split pass
+  AVC_TAKE(fa, _Float16, gemm_afrag_bytes(TB, 512) / 2, sc);
+  AVC_TAKE(fb, _Float16, gemm_afrag_bytes(TB, 512) / 2, sc);
   float* mean = stat;
   float* invstd = stat + 512;
   const float eps = 1e-5f, mom = 0.1f;
   auto M = [&](int i) { return const_cast<float*>(P[i]); };
 
+  // in_frag: the input already split; out_frag: emit the split output instead of the fp32 one
+  // (its only reader is the next conv's GEMM); off when that GEMM would not stream fragments
+  const bool chain = conv_frag_chain_ok(T, B, 512, 512) && conv_frag_chain_ok(T, B, 512, 80);
   auto cba = [&](int base, int cin, int cout, const float* in, float* out, int act,
-                 const float* residual) {
+                 const float* residual, const _Float16* in_frag = nullptr, _Float16* out_frag = nullptr) {
+    if (!chain) in_frag = nullptr, out_frag = nullptr;
     return conv_bn_act_forward_impl(ctx, T, B, cin, cout, in, P[base], P[base + 1], P[base + 2],
                                     P[base + 3], M(base + 4), M(base + 5), training, mom, eps, act,
-                                    residual, out, out, mean, invstd, s);
+                                    residual, out, out_frag ? nullptr : out, mean, invstd, s, in_frag,
+                                    out_frag);
   };
 
   // Encoder (encoder.py:53-97)
   AVC_TRY(frames_from_mel(T, B, 80, x, 256, c_org, x0, s));
-  AVC_TRY(cba(P_ENC_CONV + 0, 336, 512, x0, ba, AVC_ACT_RELU, nullptr));
-  AVC_TRY(cba(P_ENC_CONV + 6, 512, 512, ba, bb, AVC_ACT_RELU, nullptr));
-  AVC_TRY(cba(P_ENC_CONV + 12, 512, 512, bb, ba, AVC_ACT_RELU, nullptr));
+  AVC_TRY(cba(P_ENC_CONV + 0, 336, 512, x0, ba, AVC_ACT_RELU, nullptr, nullptr, fa));
+  AVC_TRY(cba(P_ENC_CONV + 6, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, fa, fb));
+  AVC_TRY(cba(P_ENC_CONV + 12, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fb));
   const int EL = P_ENC_LSTM;
   AVC_TRY(bilstm_forward_impl(ctx, T, B, 512, 32, ba, 512, P + EL, P + EL + 4, e1, 64, nullptr, nullptr,
                               nullptr, nullptr, s));
@@ -149,9 +159,9 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   const int D1 = P_DEC_LSTM1;
   AVC_TRY(lstm_forward_impl(ctx, T, B, 320, 512, 0, din, 320, P[D1], P[D1 + 1], P[D1 + 2], P[D1 + 3],
                             ba, 512, nullptr, nullptr, s));
-  AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr));
-  AVC_TRY(cba(P_DEC_CONV + 6, 512, 512, bb, ba, AVC_ACT_RELU, nullptr));
-  AVC_TRY(cba(P_DEC_CONV + 12, 512, 512, ba, bb, AVC_ACT_RELU, nullptr));
+  AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, nullptr, fa));
+  AVC_TRY(cba(P_DEC_CONV + 6, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fa, fb));
+  AVC_TRY(cba(P_DEC_CONV + 12, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, fb));
   const int D2 = P_DEC_LSTM2;
   // decoder.lstm2: both layers advanced as one wavefront (lstm.hip: lstm2_forward_impl)
   AVC_TRY(lstm2_forward_impl(ctx, T, B, 512, 1024, bb, 512, P + D2, P + D2 + 4, l1, l2, nullptr,
@@ -174,11 +184,11 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TRY(gemm_run(ctx, lin, s));
 
   // Postnet + residual (postnet.py:50-63, model.py:131-132)
-  AVC_TRY(cba(P_POST + 0, 80, 512, melf, ba, AVC_ACT_TANH, nullptr));
-  AVC_TRY(cba(P_POST + 6, 512, 512, ba, bb, AVC_ACT_TANH, nullptr));
-  AVC_TRY(cba(P_POST + 12, 512, 512, bb, ba, AVC_ACT_TANH, nullptr));
-  AVC_TRY(cba(P_POST + 18, 512, 512, ba, bb, AVC_ACT_TANH, nullptr));
-  AVC_TRY(cba(P_POST + 24, 512, 80, bb, postf, AVC_ACT_NONE, melf));
+  AVC_TRY(cba(P_POST + 0, 80, 512, melf, ba, AVC_ACT_TANH, nullptr, nullptr, fa));
+  AVC_TRY(cba(P_POST + 6, 512, 512, ba, bb, AVC_ACT_TANH, nullptr, fa, fb));
+  AVC_TRY(cba(P_POST + 12, 512, 512, bb, ba, AVC_ACT_TANH, nullptr, fb, fa));
+  AVC_TRY(cba(P_POST + 18, 512, 512, ba, bb, AVC_ACT_TANH, nullptr, fa, fb));
+  AVC_TRY(cba(P_POST + 24, 512, 80, bb, postf, AVC_ACT_NONE, melf, fb));
   AVC_TRY(mel_from_frames(T, B, 80, melf, mel, s));
   AVC_TRY(mel_from_frames(T, B, 80, postf, mel_post, s));
   return AVC_OK;

@@ -55,6 +55,11 @@ GemmDesc conv_fwd_desc(int T, int B, int cin, int cout, const float* x, const fl
 
 }  // namespace
 
+bool conv_frag_chain_ok(int T, int B, int cin, int cout) {
+  const GemmDesc g = conv_fwd_desc(T, B, cin, cout, nullptr, nullptr, nullptr, nullptr);
+  return cin % 8 == 0 && gemm_frag_eligible(g);
+}
+
 size_t conv_bn_forward_scratch(int T, int B, int cin, int cout) {
   const int bm = gemm_stats_rows(T * B, cout);
   const size_t parts = (size_t)((T * B + bm - 1) / bm) * 2 * cout;
@@ -67,7 +72,10 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
                              const float* beta, float* running_mean, float* running_var,
                              int training, float momentum, float eps, int act,
                              const float* residual, float* y_pre, float* out, float* mean,
-                             float* invstd, hipStream_t s) {
+                             float* invstd, hipStream_t s, const _Float16* x_frag,
+                             _Float16* out_frag) {
+  // x_frag: x already split (the previous layer's bn_apply wrote it); out_frag: also emit the
+  // output split for the next layer (out may then be NULL: the fp32 output is not stored)
   AVC_CHECK_ARG(T > 0 && B > 0, "conv: empty input");
   AVC_CHECK_ARG(cin % 4 == 0 && cout % 4 == 0, "conv: channel counts must be multiples of 4");
   AVC_CHECK_ARG(training || (running_mean && running_var), "conv: eval mode needs running stats");
@@ -81,6 +89,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
     AVC_LAUNCH_CHECK();
   }
   GemmDesc g = conv_fwd_desc(T, B, cin, cout, x, wt, bias, y_pre);
+  g.a_frag = x_frag;
   if (ctx->prep_version >= 0) {  // cache the split-f16 copy of the taps as well
     bool fb = true;
     auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_CONV_BFRAG, weight, nullptr, gemm_bfrag_bytes(g), &fb));
@@ -101,7 +110,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   AVC_TRY(gemm_run(ctx, g, s));
   AVC_TRY(bn_finalize(cout, nparts, stats, (double)T * B, training, momentum, eps, running_mean,
                       running_var, mean, invstd, s));
-  AVC_TRY(bn_apply((long)T * B, cout, y_pre, mean, invstd, gamma, beta, act, residual, out, s));
+  AVC_TRY(bn_apply((long)T * B, cout, y_pre, mean, invstd, gamma, beta, act, residual, out, s, out_frag));
   return AVC_OK;
 }
 

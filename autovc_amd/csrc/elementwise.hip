@@ -145,6 +145,73 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
   }
 }
 
+// bn_apply with the output also split for the next contraction: thread -> (32-row tile, group
+// quad, row, 8-channel group) exactly as gemm.hip's split_frag32_kernel walks a row-major source,
+// same arithmetic as bn_apply_kernel, same hi / lo split (lo scaled by 2^11); padding rows and
+// channels (to 32-row tiles and 32-deep K) are written as zeros.
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int nkc, long ntile,
+                                                            const float* __restrict__ y,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, int act,
+                                                            const float* __restrict__ residual,
+                                                            float* __restrict__ out,
+                                                            _Float16* __restrict__ frag) {
+  const int G8 = nkc * 2;
+  const long total = ntile * 32 * G8;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int gq = (int)(idx & 3);
+    const long rest = idx >> 2;
+    const int rr = (int)(rest & 31);
+    const long tq = rest >> 5;
+    const long t = tq / (G8 >> 2);
+    const int quad = (int)(tq - t * (G8 >> 2));
+    const long r = t * 32 + rr;
+    const int g8 = quad * 4 + gq, k0 = 8 * g8;
+    float o[8];
+    if (r < M && k0 < C) {  // C % 8 == 0: a group is all in or all out
+      const float4* q = reinterpret_cast<const float4*>(y + r * C + k0);
+      const float4 a = q[0], b = q[1];
+      o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = k0 + e;
+        const float sc = invstd[c] * gamma[c];
+        const float sh = beta[c] - mean[c] * sc;
+        o[e] = act_fwd(o[e] * sc + sh, act);
+      }
+      if (residual) {
+        const float4* rq = reinterpret_cast<const float4*>(residual + r * C + k0);
+        const float4 ra = rq[0], rb = rq[1];
+        o[0] += ra.x; o[1] += ra.y; o[2] += ra.z; o[3] += ra.w;
+        o[4] += rb.x; o[5] += rb.y; o[6] += rb.z; o[7] += rb.w;
+      }
+      if (out) {
+        float4* oq = reinterpret_cast<float4*>(out + r * C + k0);
+        oq[0] = make_float4(o[0], o[1], o[2], o[3]);
+        oq[1] = make_float4(o[4], o[5], o[6], o[7]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    }
+    h16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const _Float16 h = (_Float16)o[j];
+      hi[j] = h;
+      lo[j] = (_Float16)((o[j] - (float)h) * 2048.0f);
+    }
+    const long blk = ((r >> 5) * nkc + (g8 >> 1)) * 2;
+    const int lane = (int)(r & 31) + 32 * (g8 & 1);
+    *reinterpret_cast<h16x8*>(frag + blk * 512 + lane * 8) = hi;
+    *reinterpret_cast<h16x8*>(frag + (blk + 1) * 512 + lane * 8) = lo;
+  }
+}
+
 // partial sums over a row range of dA = d_out * act'(a) and dA * xhat  -> part[r][2][C]
 __global__ void bn_bwd_reduce_kernel(int M, int C, const float* __restrict__ dout,
                                      const float* __restrict__ y, const float* __restrict__ mean,
@@ -488,8 +555,18 @@ int bn_finalize(int C, int nparts, const float* stats, double count, int trainin
 
 int bn_apply(long M, int C, const float* y, const float* mean, const float* invstd,
              const float* gamma, const float* beta, int act, const float* residual, float* out,
-             hipStream_t s) {
+             hipStream_t s, _Float16* frag) {
   AVC_CHECK_ARG(C % 4 == 0, "bn_apply: channels must be a multiple of 4");
+  if (frag) {
+    AVC_CHECK_ARG(C % 8 == 0, "bn_apply: the split output needs channels in multiples of 8");
+    const int nkc = (C + 31) / 32 * 2;
+    const long ntile = (M + 31) / 32;
+    const long total = ntile * 32 * nkc * 2;
+    bn_apply_frag_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(
+        M, C, nkc, ntile, y, mean, invstd, gamma, beta, act, residual, out, frag);
+    AVC_LAUNCH_CHECK();
+    return AVC_OK;
+  }
   // ~4 float4 per thread; every thread owns one channel quad for the whole launch
   const long Q = C / 4;
   const long threads = std::max<long>(256, std::min<long>(M * Q / 4, 2048L * 256));

@@ -31,6 +31,9 @@ struct GemmDesc {
                                      // share one scan between products, else filled by gemm_run
   const unsigned* amax_b = nullptr;  // max |B| (filled by gemm_run)
   const _Float16* b_frag = nullptr;  // optional B already split by gemm_prepare_bfrag (prec16 only)
+  const _Float16* a_frag = nullptr;  // optional A already split (row-major A, unscaled forward
+                                     // products only): gemm_afrag_bytes(a_rows, Kc) bytes in the
+                                     // layout split_frag32_kernel writes (e.g. by bn_apply's frag)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
   int stats_bm = 0;         // filled by gemm_run: rows per stats partial
 };
@@ -45,6 +48,10 @@ size_t gemm_scratch_bytes(const GemmDesc& d);
 // split-f16 kernel streams (all taps); pass it back as GemmDesc::b_frag to skip the per-call split.
 size_t gemm_bfrag_bytes(const GemmDesc& d);
 int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream);
+// bytes of a row-major [rows][K] operand in the fragment-major split layout (GemmDesc::a_frag)
+size_t gemm_afrag_bytes(long rows, int K);
+// true when gemm_run would stream this product from split fragments (so a_frag is honoured)
+bool gemm_frag_eligible(const GemmDesc& d);
 // max |x| of a rows x cols region (row stride ld) into *out (float bits), for GemmDesc::amax_a
 int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t stream);
 

@@ -1101,6 +1101,9 @@ int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, 
   return AVC_OK;
 }
 
+size_t gemm_afrag_bytes(long rows, int K) { return frag_bytes(rows, K); }
+bool gemm_frag_eligible(const GemmDesc& d) { return frag16_eligible(d); }
+
 size_t gemm_scratch_bytes(const GemmDesc& d) {
   Plan p = make_plan(d, 0);
   size_t s = p.nsplit <= 1 ? 0 : (size_t)p.nsplit * d.nz * d.M * d.N * sizeof(float) + 256;
@@ -1159,11 +1162,15 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     const long b_ntile = frag_ntile(d.N);
     const long b_krows = frag16_b_krows(d);
     const int b_nkc = frag_nkc((int)b_krows);
-    _Float16* as = sc.take<_Float16>(frag_bytes(a_src_rows, d.Kc) / 2);
-    if (!as) return AVC_ERR_WORKSPACE;
-    const long ta = a_ntile * 32 * nkc * 2;
-    split_frag32_kernel<<<(int)std::min<long>((ta + 255) / 256, 8192), 256, 0, stream>>>(
-        d.A, d.a_trans ? 1 : d.lda, d.a_trans ? d.lda : 1, (int)a_src_rows, d.Kc, (int)a_ntile, nkc, as, d.amax_a);
+    const _Float16* as = d.a_frag;
+    if (!as || d.split_scale || d.a_trans) {
+      _Float16* at = sc.take<_Float16>(frag_bytes(a_src_rows, d.Kc) / 2);
+      if (!at) return AVC_ERR_WORKSPACE;
+      const long ta = a_ntile * 32 * nkc * 2;
+      split_frag32_kernel<<<(int)std::min<long>((ta + 255) / 256, 8192), 256, 0, stream>>>(
+          d.A, d.a_trans ? 1 : d.lda, d.a_trans ? d.lda : 1, (int)a_src_rows, d.Kc, (int)a_ntile, nkc, at, d.amax_a);
+      as = at;
+    }
     const long tapstride = b_ntile * b_nkc * 1024;  // halves
     const _Float16* bs = d.split_scale ? nullptr : d.b_frag;
     if (!bs) {

@@ -71,8 +71,11 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
                              const float* beta, float* running_mean, float* running_var,
                              int training, float momentum, float eps, int act,
                              const float* residual, float* y_pre, float* out, float* mean,
-                             float* invstd, hipStream_t s);
+                             float* invstd, hipStream_t s, const _Float16* x_frag = nullptr,
+                             _Float16* out_frag = nullptr);
 size_t conv_bn_forward_scratch(int T, int B, int cin, int cout);
+// true when a conv with cin input channels takes its input as split fragments (x_frag honoured)
+bool conv_frag_chain_ok(int T, int B, int cin, int cout);
 int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
                               const float* weight, const float* gamma, const float* beta,
                               const float* y_pre, const float* mean, const float* invstd,
