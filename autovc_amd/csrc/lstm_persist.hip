@@ -291,11 +291,33 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
                                                          (int)((long)a.ntile * nck * 2048 - hbase), 0x00020000);
       constexpr int NB = PD + 1;  // h chunk buffers: PD chunks in flight ahead of the MFMAs
       f16x8 hb[NB][RT][2], wt[2];
+#ifdef AVC_STAMPS
+#define AVC_PLD_SKIP (a.diag & 4)  // timing experiment: no h loads (zeros)
+#else
+#define AVC_PLD_SKIP false
+#endif
 #define AVC_PLD(HV, C)                                                                             \
+  if (AVC_PLD_SKIP) { _Pragma("unroll") for (int r = 0; r < RT; ++r) HV[r][0] = HV[r][1] = f16x8{}; } else \
   _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                                 \
     HV[r][0] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048, HO ? 16 : 0)); \
     HV[r][1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048 + 1024, HO ? 16 : 0)); \
   }
+#ifdef AVC_MFMA_PASSES
+// experiment: the three products of a chunk in passes over all accumulators (each accumulator
+// still sees hi.lo, lo.hi, hi.hi in that order, so bit-identical); measured slower on gfx950
+// (mfma loop 10.3k -> 11.7k ticks/step), hence off by default
+#define AVC_PMFMA(HV, C)                                                                           \
+  wt[0] = *reinterpret_cast<const f16x8*>(wl + ((w * NCH + (C)) * 2 + 0) * 1024 + lane * 16);      \
+  wt[1] = *reinterpret_cast<const f16x8*>(wl + ((w * NCH + (C)) * 2 + 1) * 1024 + lane * 16);      \
+  _Pragma("unroll") for (int pass = 0; pass < 3; ++pass) {                                         \
+    const int ha = pass == 0 ? 1 : 0, wb = pass == 1 ? 1 : 0;                                      \
+    _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                               \
+      _Pragma("unroll") for (int n = 0; n < 3; ++n)                                                \
+        acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][ha], wreg[n][C][wb], acc[r][n], 0, 0, 0); \
+      acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][ha], wt[wb], acc[r][3], 0, 0, 0);  \
+    }                                                                                              \
+  }
+#else
 #define AVC_PMFMA(HV, C)                                                                           \
   wt[0] = *reinterpret_cast<const f16x8*>(wl + ((w * NCH + (C)) * 2 + 0) * 1024 + lane * 16);      \
   wt[1] = *reinterpret_cast<const f16x8*>(wl + ((w * NCH + (C)) * 2 + 1) * 1024 + lane * 16);      \
@@ -309,6 +331,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[1], acc[r][3], 0, 0, 0);      \
     acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[0], acc[r][3], 0, 0, 0);      \
   }
+#endif
 #pragma unroll
       for (int c = 0; c < PD && c < NCH; ++c) { AVC_PLD(hb[c], c) }
       if constexpr (NCH <= PD) load_gx();
@@ -324,6 +347,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       }
 #undef AVC_PMFMA
 #undef AVC_PLD
+#undef AVC_PLD_SKIP
     }
 
     AVC_PSTAMP(3);

@@ -34,6 +34,7 @@ for step in "$@"; do
     pstamps2) run pstamps2 300 python scripts/stamps_persist.py 2 ;;
     pstampsd1) run pstampsd1 300 python scripts/stamps_persist.py 1 1 ;;
     pstampsd2) run pstampsd2 300 python scripts/stamps_persist.py 1 2 ;;
+    pstampsd4) run pstamps 300 python scripts/stamps_persist.py 2 && run pstampsd4 300 python scripts/stamps_persist.py 2 4 ;;
     gcfg) run gcfg 300 python scripts/gemm_cfgs.py ;;
     pmodes) run pmodes 300 python scripts/persist_modes.py ;;
     pmodes1) run pmodes1 300 python scripts/persist_modes.py 1 0 1 1 ;;
