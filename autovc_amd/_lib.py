@@ -60,6 +60,10 @@ _SIGS = {
     "avc_lstm_persist_depth": [_I],
     "avc_lstm_persist_layers": [_I],
     "avc_lstm_persist_status": [ctypes.POINTER(ctypes.c_long)],
+    "avc_persist_check": [_P, _P, ctypes.POINTER(_I)],
+    "avc_lstm_persist_coop": [_I],
+    "avc_debug_persist_inject": [_I],
+    "avc_graph_mode": [_I],
     "avc_timing_reset": [],
     "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)],

@@ -97,6 +97,43 @@ class FusedAdam(torch.optim.Optimizer):
                     g[k] = v
 
 
+class _FusedGenerator(torch.autograd.Function):
+    """Whole-Generator forward (avc_generator_forward_cached: cached derived weights, HIP-graph
+    replay) as ONE autograd node, for grad-enabled calls such as convert()'s
+    (voice_converter.py:172-174).  Nothing but the three inputs is saved; backward recomputes
+    the per-layer forward (same kernels, same batch statistics) with the BatchNorm running
+    buffers restored afterwards, so they move once per forward call as in nn.BatchNorm1d."""
+
+    @staticmethod
+    def forward(ctx, model, x, c_org, c_trg, *params):
+        ctx.model = model
+        ctx.params = params
+        ctx.save_for_backward(x, c_org, c_trg)
+        ctx.set_materialize_grads(False)
+        return model._generator_forward(x, c_org, c_trg)
+
+    @staticmethod
+    def backward(ctx, d_mel, d_post, d_codes):
+        model, params = ctx.model, ctx.params
+        x, c_org, c_trg = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        bufs = [b for b in model.buffers()]
+        kept = [b.detach().clone() for b in bufs]
+        ins = [t.detach().requires_grad_(bool(n)) for t, n in zip((x, c_org, c_trg), need[1:4])]
+        with torch.enable_grad():
+            outs = model._forward_layers(*ins)
+        for b, k in zip(bufs, kept):  # .data: no version bump (keeps the derived-weight cache)
+            b.data.copy_(k)
+        pairs = [(o, d) for o, d in zip(outs, (d_mel, d_post, d_codes)) if d is not None]
+        wrt = [t for t in ins if t.requires_grad] + [p for p, n in zip(params, need[4:]) if n]
+        if not pairs or not wrt:
+            return (None,) * (4 + len(params))
+        grads = iter(torch.autograd.grad([o for o, _ in pairs], wrt, [d for _, d in pairs], allow_unused=True))
+        dins = [next(grads) if t.requires_grad else None for t in ins]
+        dps = [next(grads) if n else None for n in need[4:]]
+        return (None, *dins, *dps)
+
+
 class AutoEncoder(nn.Module):
     """Generator network (reference model.py:27): Encoder + Decoder + Postnet."""
 
@@ -119,6 +156,9 @@ class AutoEncoder(nn.Module):
         self._flat_slices = []
         self._gen_cache = None
         self._param_epoch = 0  # bumped by FusedAdam.step (it writes parameters behind torch's back)
+        # grad-enabled forwards with c_trg run the fused forward under one autograd Function whose
+        # backward recomputes the per-layer path; False = always the per-layer path
+        self.fused_autograd = True
         self._uid = next(_INSTANCES)
 
     # ---- flat parameter storage (one buffer for Adam/EMA/all-reduce) -----------------------
@@ -172,16 +212,19 @@ class AutoEncoder(nn.Module):
     def _bns(self):
         return [m for m in self.modules() if isinstance(m, nn.BatchNorm1d)]
 
-    def _fast_path_ok(self, x, c_org, c_trg):
-        if c_trg is None:
-            return False
-        if torch.is_grad_enabled() and (x.requires_grad or c_org.requires_grad or c_trg.requires_grad
-                                        or any(p.requires_grad for p in self.parameters())):
-            return False
+    def _bn_uniform(self):
+        """The fused forward handles every BatchNorm in one mode with nn.BatchNorm1d defaults."""
         bns = self._bns()
         modes = {b.training for b in bns}
         return len(modes) == 1 and all(b.momentum == 0.1 and b.eps == 1e-5 and b.track_running_stats
                                        for b in bns)
+
+    def _needs_graph(self, x, c_org, c_trg):
+        return torch.is_grad_enabled() and (x.requires_grad or c_org.requires_grad or c_trg.requires_grad
+                                            or any(p.requires_grad for p in self.parameters()))
+
+    def _fast_path_ok(self, x, c_org, c_trg):
+        return c_trg is not None and self._bn_uniform() and not self._needs_graph(x, c_org, c_trg)
 
     def _gen_params(self):
         tensors = [v for k, v in self.state_dict(keep_vars=True).items()
@@ -219,6 +262,14 @@ class AutoEncoder(nn.Module):
             torch._foreach_add_([b.num_batches_tracked for b in self._bns()], 1)
         return mel, mel_post, codes
 
+    def check_health(self):
+        """Synchronise this model's device stream and raise RuntimeError if a persistent LSTM
+        recurrence launched since the last check abandoned a bounded wait (its outputs were
+        written as NaN).  Every later call that reaches a persistent recurrence raises the same
+        error by itself; this is the explicit form (e.g. after the last forward of a job)."""
+        dev = self._flat_param.device if self._flat_param is not None else next(self.parameters()).device
+        _lib.call("avc_persist_check", _lib.context(dev), _lib.stream(dev), None)
+
     @staticmethod
     def _check(x, c, name):
         if not x.is_cuda:
@@ -240,8 +291,18 @@ class AutoEncoder(nn.Module):
         if c_trg is not None:
             c_trg = c_trg.to(torch.float32).contiguous()
         x = x.contiguous()
-        if self._fast_path_ok(x, c_org, c_trg):
-            return self._generator_forward(x, c_org, c_trg)
+        if c_trg is not None and self._bn_uniform():
+            if not self._needs_graph(x, c_org, c_trg):
+                return self._generator_forward(x, c_org, c_trg)
+            if self.fused_autograd:
+                # grad-enabled conversion (voice_converter.py:172-174 calls self.AE(...) with grad
+                # on): the same fused forward, with a recomputing backward
+                return _FusedGenerator.apply(self, x, c_org, c_trg, *self.parameters())
+        return self._forward_layers(x, c_org, c_trg)
+
+    def _forward_layers(self, x, c_org, c_trg):
+        """Per-layer autograd path: one Function per layer, each a C-ABI forward/backward pair."""
+        B, _, T = x.shape
         save = torch.is_grad_enabled()
         enc = self.encoder.frames(x, c_org, save)
         codes = ops.Codes.apply(enc, T, B)
@@ -306,7 +367,8 @@ class AutoEncoder(nn.Module):
             self.configure_optimizer()
         X = X.to(self._flat_param.device, torch.float32).contiguous()
         c_org = c_org.to(self._flat_param.device, torch.float32).contiguous()
-        out_decoder, out_postnet, content_codes = self(X, c_org, c_org)
+        self._check(X, None, "X")
+        out_decoder, out_postnet, content_codes = self._forward_layers(X, c_org, c_org)
         loss = self._loss(X=X, c_org=c_org, out_decoder=out_decoder, out_postnet=out_postnet,
                           content_codes=content_codes)
         self.optimiser.zero_grad()

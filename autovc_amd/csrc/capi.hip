@@ -15,6 +15,7 @@ thread_local std::string g_err;
 
 void set_error(const std::string& msg) { g_err = msg; }
 int g_config_epoch = 0;
+int g_graph_mode = 1;  // avc_graph_mode()
 const char* get_error() { return g_err.c_str(); }
 
 void* prep_buffer(avc_context* ctx, int kind, const void* key0, const void* key1, size_t bytes,
@@ -218,6 +219,7 @@ int avc_context_create(int device, avc_context** out) {
 int avc_context_destroy(avc_context* ctx) {
   if (!ctx) return AVC_OK;
   AVC_HIP(hipDeviceSynchronize());
+  persist_release(ctx);
   for (void* p : ctx->retired) (void)hipFree(p);
   for (auto& e : ctx->prep) (void)hipFree(e.buf);
   if (ctx->gen.exec) (void)hipGraphExecDestroy(ctx->gen.exec);
@@ -490,6 +492,7 @@ int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* co
   AVC_CHECK_ARG(weights_version >= 0, "weights_version must be >= 0");
   for (int i = 0; i < P_COUNT; ++i) AVC_CHECK_ARG(params[i] != nullptr, "NULL parameter pointer");
   AVC_TRY(ensure_arena(ctx, gen_scratch(T, B)));
+  AVC_TRY(persist_guard(ctx));  // an earlier persistent launch timed out: report it, reset state
   hipStream_t s = S(stream);
   avc_gen_graph& g = ctx->gen;
   const bool timing = timing_on(TC_GEMM) || timing_on(TC_LSTM_STEP_FWD) || timing_on(TC_LSTM32) ||
@@ -500,7 +503,7 @@ int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* co
                     std::equal(g.params.begin(), g.params.end(), params);
   ctx->prep_version = weights_version;
   int rc = AVC_OK;
-  if (same && !timing && (g.exec || g.seen >= 1)) {
+  if (same && !timing && g_graph_mode && (g.exec || g.seen >= 1)) {
     if (!g.exec) {
       rc = capture_graph(ctx, params);
       if (rc != AVC_OK) {
@@ -539,6 +542,12 @@ int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* co
   ctx->prep_version = -1;
   if (rc == AVC_OK) ++g.seen;
   return rc;
+}
+
+int avc_graph_mode(int on) {
+  g_graph_mode = on ? 1 : 0;
+  ++g_config_epoch;
+  return AVC_OK;
 }
 
 int avc_prepared_release(avc_context* ctx) {

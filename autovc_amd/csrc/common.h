@@ -91,8 +91,25 @@ struct avc_gen_graph {
   size_t stage_bytes = 0;
 };
 
+// Counter region of a persistent recurrence (lstm_persist.hip): arrival counters that are never
+// reset between launches.  Every launch takes a ticket per workgroup; ticket / grid size gives
+// the launch's epoch E, and a wait for "all ncb producers of step t" is a wait for the counter to
+// reach E * ncb, so a value left by an earlier launch can never satisfy it.  One region per
+// launch layout (kind, T, groups, producers per step, grid size), because every word must advance
+// by exactly ncb per launch and the ticket count per launch must be the grid size.
+struct avc_persist_region {
+  int kind = 0, T = 0, ngrp = 0, ncb = 0, nwg = 0;
+  size_t bytes = 0;
+  void* mem = nullptr;
+  unsigned long last_use = 0;
+};
+
 struct avc_context {
   int device = 0;
+  std::vector<avc_persist_region> regions;
+  unsigned long region_clock = 0;
+  unsigned* fail_host = nullptr;  // pinned host word: device-wide number of the last timed-out persistent launch
+  unsigned fail_seen = 0;         // value of *fail_host already reported to the caller
   std::vector<avc_prep_entry> prep;
   avc_gen_graph gen;
   hipStream_t capture_stream = nullptr;
@@ -108,6 +125,12 @@ namespace avc {
 // zero `bytes` at p (16-B aligned) on stream s with a kernel (elementwise.hip); used instead of
 // hipMemsetAsync everywhere (see there)
 int zero_async(void* p, size_t bytes, hipStream_t s);
+
+// Reports (once) a persistent-recurrence launch that abandoned a bounded wait since the last
+// report: AVC_ERR_DEVICE with a message, after dropping the counter regions and the captured
+// forward graph so the next call starts from fresh state (lstm_persist.hip).
+int persist_guard(avc_context* ctx);
+void persist_release(avc_context* ctx);
 
 struct Scratch {
   avc_context* ctx;

@@ -16,7 +16,7 @@ namespace {
 inline int ew_blocks(long n, int per = 256) { return (int)std::max<long>(1, std::min<long>((n + per - 1) / per, 16384)); }
 
 __device__ __forceinline__ float act_fwd(float a, int act) {
-  if (act == AVC_ACT_RELU) return a > 0.f ? a : 0.f;
+  if (act == AVC_ACT_RELU) return a < 0.f ? 0.f : a;  // NaN propagates, as torch.relu
   if (act == AVC_ACT_TANH) return tanhf(a);
   return a;
 }

@@ -25,7 +25,7 @@ __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
 }
 
 __device__ __forceinline__ float act_apply(float v, int act) {
-  if (act == AVC_ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == AVC_ACT_RELU) return v < 0.f ? 0.f : v;  // NaN propagates, as torch.relu
   if (act == AVC_ACT_TANH) return tanhf(v);
   if (act == AVC_ACT_DBNORM) {
     const float db = 20.f * log10f(fmaxf(1e-5f, v));

@@ -18,18 +18,31 @@
 // (split h0_t / h1_t, gx1_t), so there is never a write-after-read hazard; the cell state c
 // stays in registers (the epilogue thread of a (batch row, 4 hidden units) pair never changes).
 //
-// Dependencies (counters per slot and time step, zeroed per call):
-//   slot 0 at t waits  cnt0[t-1] == ncb           (all of h0_{t-1})  [replicated: see kRep]
-//   slot 1 at t waits  cnt0[t]   == ncb           (all of h0_t)
-//   slot 2 at t waits  cnt1[t]   == ncb and cnt2[t-1] == ncb
+// Dependencies (arrival counters per slot and time step; E = this launch's epoch, below):
+//   slot 0 at t waits  cnt0[t-1] >= E*ncb         (all of h0_{t-1})  [replicated: see kRep]
+//   slot 1 at t waits  cnt0[t]   >= E*ncb         (all of h0_t)
+//   slot 2 at t waits  cnt1[t]   >= E*ncb and cnt2[t-1] >= E*ncb
+// The counters are never reset: they live in a per-context region of their own (one per counter
+// layout), every successful launch adds exactly ncb to every word, and each workgroup derives the
+// launch's epoch E from a ticket it takes at start (E = ticket / grid size + 1).  A counter value
+// left by an earlier launch is at most (E-1)*ncb, so it can never satisfy a wait of this launch:
+// correctness does not depend on any reset being ordered before the waiters (the round-1 design
+// zeroed the counters per call and was exposed to exactly that).
 // Hand-off protocol (cdna_hip_programming.md Guideline 16, counter form with replicas): payload
 // stored write-through (sc1; every 128-B line written whole by one wave instruction), every
 // storing wave drains vmcnt, workgroup barrier, one 8-lane instruction adds to the 8 counter
 // replicas (agent scope); the consumer polls one replica relaxed, workgroup barrier, then EVERY
 // load of handed-off bytes is an sc1 load (default, mode 2: 9.8 us per step), or one agent-scope
 // acquire followed by plain loads (mode 1: 11.4 us per step).
-// Every spin is bounded: on timeout the workgroup sets a shared give-up word, every waiter sees
-// it and leaves, and the host reports the failure (avc_lstm_persist_status).
+// Every spin is bounded: on timeout the workgroup raises the region's give-up word to E, every
+// waiter of this launch sees it and leaves, the rows a workgroup did not compute are written as
+// NaN (a timed-out launch can never return plausible numbers), and the first workgroup to give up
+// stores the device's running failure count into the context's pinned host word.  The next call on the context that reaches a
+// persistent recurrence (or avc_persist_check) sees it, drops the counter regions and the
+// captured graph, and fails with AVC_ERR_DEVICE (a RuntimeError in Python).
+// Co-residency of the grid (every wait assumes its producers run) is checked before launching:
+// the occupancy API's resident workgroups per CU x CUs must cover the grid, else the
+// launch-per-step kernels run instead; avc_lstm_persist_coop(1) launches cooperatively.
 //
 // One-layer form (decoder.lstm1, decoder.py:50,69): slot 0 alone, grid (ncb, ngrp).  Batch rows
 // never interact in an LSTM, so the batch is split into ngrp independent groups of 16/32/64 rows
@@ -41,6 +54,7 @@
 // (hi.lo, lo.hi, hi.hi per 32-deep chunk, in that order), the same K split over 4 waves and
 // the same fixed-order LDS reduction, so the two paths agree bit for bit.
 #include <algorithm>
+#include <vector>
 
 #include "kernels.h"
 #include "timing.h"
@@ -77,6 +91,10 @@ constexpr int kGxRing = 4;
 constexpr int kLead = 3;  // slot 0 may run at most this many steps ahead of slot 2
 
 __device__ unsigned g_persist_giveups = 0;  // sticky count of timed-out launches (host-read)
+
+// Counter region layout: line 0 = the launch ticket (u64), line 1 = the give-up word (epoch of
+// the last launch that gave up), then the counters.
+constexpr int kRegionHeaderWords = 2 * 32;
 
 #ifdef AVC_STAMPS
 // diagnostic build only: s_memtime per (workgroup, step, phase), written by thread 0
@@ -118,24 +136,33 @@ struct PersistArgs {
   float* y0; float* y1;       // [T][B][H] fp32 h
   float* g0; float* g1;       // optional [T][B][4H] activated gates (training)
   float* c0; float* c1;       // optional [T][B][H] cell state (training)
-  unsigned* cnt;              // [3][T] arrivals
-  unsigned* tmo;              // give-up word
+  unsigned* cnt;              // [3][T] arrivals (never reset; see the epoch above)
+  unsigned* tmo;              // give-up word: epoch of the last launch that gave up
+  unsigned long long* tickets;  // one per workgroup per launch
+  unsigned* fail_host;        // pinned host word (avc_context::fail_host): last failure number
+  int nwg;                    // workgroups in the grid
+  unsigned spin_limit;        // polls before giving up (0 = test injection: give up at once)
   int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
 };
 int g_persist_diag = 0;
 
-// One lane waits until *p >= target (relaxed agent-scope polls).  false = gave up (or someone
-// else did: the shared give-up word is checked every 64 polls).
-__device__ bool wait_ge(unsigned* p, unsigned target, unsigned* tmo) {
+// One lane waits until *p reaches target (wrap-safe; relaxed agent-scope polls).  false = gave
+// up, or another workgroup of this launch (epoch E) did: the give-up word is checked every 64
+// polls.  The first workgroup to give up reports the launch to the host.
+__device__ bool wait_ge(unsigned* p, unsigned target, const PersistArgs& a, unsigned E) {
   gu32* gp = (gu32*)(p);
-  gu32* gt = (gu32*)(tmo);
+  gu32* gt = (gu32*)(a.tmo);
   for (unsigned spins = 0;; ++spins) {
-    if (__hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-    if ((spins & 63) == 63 && __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+    if ((int)(__hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) return true;
+    if ((spins & 63) == 63 && __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E)
       return false;
-    if (spins >= kSpinLimit) {
-      __hip_atomic_store(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      atomicAdd(&g_persist_giveups, 1u);
+    if (spins >= a.spin_limit) {
+      const unsigned old = __hip_atomic_fetch_max(gt, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old != E) {  // first to give up in this launch: a device-wide unique failure number
+        const unsigned n = atomicAdd(&g_persist_giveups, 1u) + 1u;
+        if (a.fail_host)
+          __hip_atomic_store(a.fail_host, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -215,7 +242,17 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   auto gx1_slab = [&](int tt, int c) -> long { return ((long)(tt % kGxRing) * a.ncb + c) * (64 * TW); };
   const int rep = blockIdx.x & (kRep - 1);
 
-  for (int t = 0; t < T; ++t) {
+  // this launch's epoch (see the header): every workgroup takes one ticket
+  if (tid == 0) {
+    const unsigned long long tk = __hip_atomic_fetch_add(a.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[2] = (int)(unsigned)(tk / (unsigned long long)a.nwg + 1ull);
+  }
+  __syncthreads();
+  const unsigned E = (unsigned)flag[2];
+  const unsigned target = E * (unsigned)a.ncb;
+
+  int t = 0;
+  for (; t < T; ++t) {
     // ---- wait for this step's operands ----------------------------------------------------
     AVC_PSTAMP(0);
     // Two lanes poll in parallel (lane 0 of waves 0 and 1): the data this step reads, and the
@@ -230,7 +267,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       else if (L == 1) idx = primary ? cnt_index(0, T, t, rep)
                                      : (t >= kGxRing ? cnt_index(2, T, t - kGxRing, rep) : -1);
       else idx = primary ? (t > 0 ? cnt_index(2, T, t - 1, rep) : -1) : cnt_index(1, T, t, rep);
-      const bool ok = idx < 0 || wait_ge(cnt + idx, a.ncb, a.tmo);
+      const bool ok = idx < 0 || wait_ge(cnt + idx, target, a, E);
       if (primary) {
         AVC_PSTAMP(1);
         AVC_PRSTAMP(7);
@@ -447,6 +484,21 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       }
     }
   }
+  // gave up at step t: the rows this workgroup owns for steps t..T-1 are written as NaN, so a
+  // timed-out launch never hands plausible numbers downstream (the host reports it, see above)
+  if (t < T && L != 1 && live) {
+    const float qnan = __builtin_nanf("");
+    const f32x4 nv = f32x4{qnan, qnan, qnan, qnan};
+    for (int tt = t; tt < T; ++tt) {
+      *reinterpret_cast<f32x4*>(y_out + ((long)tt * B + b) * H + j0) = nv;
+      if (c_save) *reinterpret_cast<f32x4*>(c_save + ((long)tt * B + b) * H + j0) = nv;
+      if (g_save) {
+        float* go = g_save + ((long)tt * B + b) * G4 + p0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4*>(go + 4 * g) = nv;
+      }
+    }
+  }
 }
 
 inline size_t al(size_t b) { return (b + 255) & ~size_t(255); }
@@ -469,42 +521,155 @@ int lstm1_rows_per_group(int B, int H) {
   return 4;
 }
 
-// Launch: grid (nslot * ncb, ngrp), one resident workgroup per CU (checked by the callers).
-void persist_launch(const PersistArgs& a, int RT, int ngrp, hipStream_t s) {
-  const int nch = a.H / 32 / 4;
-  const size_t lds = (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16 + 2 * 64 * sizeof(float);
-  const dim3 grid(a.nslot * a.ncb, ngrp);
-#define AVC_PERSIST(NCHV, RTV)                                                                    \
-  {                                                                                               \
-    if (g_persist_mode == 1) lstm_persist_kernel<NCHV, RTV, 0, 1><<<grid, 256, lds, s>>>(a);      \
-    else if (g_persist_pd == 1) lstm_persist_kernel<NCHV, RTV, 1, 1><<<grid, 256, lds, s>>>(a);   \
-    else lstm_persist_kernel<NCHV, RTV, 1, 2><<<grid, 256, lds, s>>>(a);                          \
-  }
+size_t persist_lds(int H, int RT) {
+  const int nch = H / 32 / 4;
+  return (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16 + 2 * 64 * sizeof(float);
+}
+
+// The template instance a launch of (H, RT) runs under the current tuning.
+const void* persist_fn(int H, int RT) {
+  const int nch = H / 32 / 4;
+#define AVC_PERSIST_FN(NCHV, RTV)                                                                 \
+  return g_persist_mode == 1 ? (const void*)lstm_persist_kernel<NCHV, RTV, 0, 1>                  \
+       : g_persist_pd == 1   ? (const void*)lstm_persist_kernel<NCHV, RTV, 1, 1>                  \
+                             : (const void*)lstm_persist_kernel<NCHV, RTV, 1, 2>;
   if (nch == 8) {
-    if (RT == 1) AVC_PERSIST(8, 1) else if (RT == 2) AVC_PERSIST(8, 2) else AVC_PERSIST(8, 4)
+    if (RT == 1) { AVC_PERSIST_FN(8, 1) } else if (RT == 2) { AVC_PERSIST_FN(8, 2) } else { AVC_PERSIST_FN(8, 4) }
   } else {
-    if (RT == 1) AVC_PERSIST(4, 1) else if (RT == 2) AVC_PERSIST(4, 2) else AVC_PERSIST(4, 4)
+    if (RT == 1) { AVC_PERSIST_FN(4, 1) } else if (RT == 2) { AVC_PERSIST_FN(4, 2) } else { AVC_PERSIST_FN(4, 4) }
   }
-#undef AVC_PERSIST
+#undef AVC_PERSIST_FN
+}
+
+// Workgroups of instance (H, RT) the device can hold at once: the occupancy API's resident
+// workgroups per CU (LDS, VGPRs, waves) x CUs.  Cached per instance.
+int persist_capacity(int H, int RT) {
+  struct Entry { const void* fn; int dev; int cap; };
+  static std::vector<Entry> cache;
+  const void* fn = persist_fn(H, RT);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  for (const auto& e : cache)
+    if (e.fn == fn && e.dev == dev) return e.cap;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, persist_lds(H, RT)) != hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = 0;
+  }
+  const int cap = per_cu * device_cus();
+  cache.push_back({fn, dev, cap});
+  return cap;
+}
+
+int g_persist_coop = 0;          // avc_lstm_persist_coop()
+int g_persist_inject = 0;        // avc_debug_persist_inject(): launches left that give up at once
+
+// Launch: grid (nslot * ncb, ngrp); co-residency was checked by the eligibility test.
+int persist_launch(PersistArgs a, int RT, int ngrp, hipStream_t s) {
+  const dim3 grid(a.nslot * a.ncb, ngrp);
+  a.nwg = (int)(grid.x * grid.y);
+  a.spin_limit = kSpinLimit;
+  if (g_persist_inject > 0) {
+    --g_persist_inject;
+    a.spin_limit = 0;
+  }
+  const void* fn = persist_fn(a.H, RT);
+  void* args[] = {&a};
+  if (g_persist_coop)
+    AVC_HIP(hipLaunchCooperativeKernel(fn, grid, dim3(256), args, (unsigned)persist_lds(a.H, RT), s));
+  else
+    AVC_HIP(hipLaunchKernel(fn, grid, dim3(256), args, persist_lds(a.H, RT), s));
+  return AVC_OK;
+}
+
+// The counter region of launch layout (kind, T, ngrp, ncb, nwg) on this context: created zeroed (stream-ordered, before
+// the first launch that uses it) and kept; least recently used regions beyond kMaxRegions are
+// retired (freed when the context is destroyed: a captured graph may still reference them).
+constexpr int kMaxRegions = 32;
+int persist_region(avc_context* ctx, int kind, int T, int ngrp, int ncb, int nwg, size_t counter_words,
+                   hipStream_t s, unsigned** out) {
+  const size_t bytes = (kRegionHeaderWords + counter_words) * sizeof(unsigned);
+  for (auto& r : ctx->regions) {
+    if (r.kind == kind && r.T == T && r.ngrp == ngrp && r.ncb == ncb && r.nwg == nwg && r.bytes == bytes) {
+      r.last_use = ++ctx->region_clock;
+      *out = static_cast<unsigned*>(r.mem);
+      return AVC_OK;
+    }
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  AVC_HIP(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone) {
+    set_error("persistent recurrence: counter region missing during graph capture");
+    return AVC_ERR_WORKSPACE;  // the caller falls back to eager calls
+  }
+  if ((int)ctx->regions.size() >= kMaxRegions) {
+    auto lru = std::min_element(ctx->regions.begin(), ctx->regions.end(),
+                                [](const avc_persist_region& x, const avc_persist_region& y) { return x.last_use < y.last_use; });
+    ctx->retired.push_back(lru->mem);
+    ctx->regions.erase(lru);
+  }
+  void* mem = nullptr;
+  AVC_HIP(hipMalloc(&mem, bytes));
+  AVC_TRY(zero_async(mem, bytes, s));
+  avc_persist_region r;
+  r.kind = kind; r.T = T; r.ngrp = ngrp; r.ncb = ncb; r.nwg = nwg; r.bytes = bytes; r.mem = mem;
+  r.last_use = ++ctx->region_clock;
+  ctx->regions.push_back(r);
+  *out = static_cast<unsigned*>(mem);
+  return AVC_OK;
+}
+
+void set_region_args(PersistArgs& a, avc_context* ctx, unsigned* region) {
+  a.tickets = reinterpret_cast<unsigned long long*>(region);
+  a.tmo = region + 32;
+  a.cnt = region + kRegionHeaderWords;
+  a.fail_host = ctx->fail_host;
 }
 
 }  // namespace
 
+int persist_guard(avc_context* ctx) {
+  if (!ctx->fail_host) {
+    AVC_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->fail_host), 256, hipHostMallocDefault));
+    *ctx->fail_host = 0;
+    ctx->fail_seen = 0;
+  }
+  const unsigned v = __atomic_load_n(ctx->fail_host, __ATOMIC_ACQUIRE);
+  if (v == ctx->fail_seen) return AVC_OK;
+  ctx->fail_seen = v;
+  // the timed-out launch left its counters part-way: start every layout from a fresh region
+  for (auto& r : ctx->regions) ctx->retired.push_back(r.mem);
+  ctx->regions.clear();
+  ctx->gen.epoch = -2;  // the captured forward graph references the retired regions: re-capture
+  set_error("a persistent LSTM recurrence launched by an earlier call on this context abandoned a "
+            "bounded wait (a workgroup was not resident); that call's outputs were written as NaN and "
+            "the BatchNorm running statistics it updated are not valid. State has been reset.");
+  return AVC_ERR_DEVICE;
+}
+
+void persist_release(avc_context* ctx) {
+  for (auto& r : ctx->regions) (void)hipFree(r.mem);
+  ctx->regions.clear();
+  if (ctx->fail_host) (void)hipHostFree(ctx->fail_host);
+  ctx->fail_host = nullptr;
+}
+
 bool lstm2_persist_eligible(int T, int B, int H) {
   if (g_persist_mode == 0 || !(g_persist_layers & 2) || T < 1 || B < 1 || B > 64 || !(H == 1024 || H == 512)) return false;
-  return 3 * (4 * H / 64) <= device_cus();  // one resident workgroup per CU for every slot
+  const int ntile = (B + 15) / 16, RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
+  return 3 * (4 * H / 64) <= persist_capacity(H, RT);  // every workgroup co-resident
 }
 
 bool lstm1_persist_eligible(int T, int B, int H) {
   if (g_persist_mode == 0 || !(g_persist_layers & 1) || T < 1 || B < 1 || B > 256 || !(H == 1024 || H == 512)) return false;
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
-  return ngrp * (4 * H / 64) <= device_cus();
+  return ngrp * (4 * H / 64) <= persist_capacity(H, RT);
 }
 
 size_t lstm1_persist_scratch(int T, int B, int H) {
   const size_t ntile = (size_t)(B + 15) / 16;
   const size_t hsz = ntile * 16 * H * 2 * 2;
-  return al((size_t)T * hsz) + al((ntile * T * kRep + 1) * kLine * sizeof(unsigned)) + 4096;
+  return al((size_t)T * hsz) + 4096;
 }
 
 // One LSTM layer (decoder.lstm1, decoder.py:50,69) as one weight-stationary launch: slot 0 of the
@@ -515,14 +680,15 @@ size_t lstm1_persist_scratch(int T, int B, int H) {
 int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx, const _Float16* whh_s,
                           const float* winv, float* y, float* g, float* c, hipStream_t s) {
   AVC_CHECK_ARG(lstm1_persist_eligible(T, B, H), "lstm1 persistent path: not eligible for this shape");
+  AVC_TRY(persist_guard(ctx));
   Scratch sc(ctx);
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2 * 2;
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
   const long gstride = (long)T * kRep * kLine;  // counter words per group: [T][kRep] lines
   AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
-  AVC_TAKE(words, unsigned, (size_t)ngrp * gstride + kLine, sc);
-  AVC_TRY(zero_async(words, ((size_t)ngrp * gstride + kLine) * sizeof(unsigned), s));
+  unsigned* region = nullptr;
+  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, ngrp * (4 * H / 64), (size_t)ngrp * gstride, s, &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = 1; a.cnt_gstride = gstride;
@@ -532,10 +698,9 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   a.hs0 = hs0; a.hsz = hsz;
   a.y0 = y; a.g0 = g; a.c0 = c;
   a.diag = g_persist_diag;
-  a.cnt = words; a.tmo = words + (size_t)ngrp * gstride;
+  set_region_args(a, ctx, region);
   hipEvent_t ev = timing_begin(TC_LSTM1_PERSIST, s);
-  persist_launch(a, RT, ngrp, s);
-  AVC_LAUNCH_CHECK();
+  AVC_TRY(persist_launch(a, RT, ngrp, s));
   if (ev) {
     // split W_hh read once; per step the split h operand of every workgroup's group, gx, h, c
     const double flops = (double)T * 2.0 * B * H * 4.0 * H;
@@ -550,7 +715,7 @@ size_t lstm2_persist_scratch(int T, int B, int H) {
   const size_t ntile = (size_t)(B + 15) / 16;
   const size_t hsz = ntile * 16 * H * 2 * 2;
   return al((size_t)T * hsz) + al((size_t)2 * hsz) + al((size_t)kGxRing * (4 * H / 64) * 64 * 64 * sizeof(float)) +
-         al((size_t)(3 * T * kRep + 1) * kLine * sizeof(unsigned)) + 4096;
+         4096;
 }
 
 // gx0 [T][B][4H] (layer 0's input projection + biases, permuted columns) is computed by the
@@ -561,18 +726,16 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
                           const float* b1_p, float* y0, float* y1, float* g0, float* c0, float* g1,
                           float* c1, hipStream_t s) {
   AVC_CHECK_ARG(lstm2_persist_eligible(T, B, H), "lstm2 persistent path: not eligible for this shape");
+  AVC_TRY(persist_guard(ctx));
   Scratch sc(ctx);
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2 * 2;  // bytes per split-h step buffer
   AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
   AVC_TAKE(hs1, unsigned char, (size_t)2 * hsz, sc);                      // ring of 2
   AVC_TAKE(gx1, float, (size_t)kGxRing * (4 * H / 64) * 64 * 64, sc);     // slab ring
-  // counters [3][T][kRep] (one 128-B line each), then the give-up word on a line of its own
-  AVC_TAKE(words, unsigned, (size_t)(3 * T * kRep + 1) * kLine, sc);
-  // counters and give-up word start at the allocation's start, padded to 16 B (Guideline 16),
-  // zeroed by zero_async (a kernel: a hipMemsetAsync here was measured landing out of order)
-  const size_t wbytes = (size_t)(3 * T * kRep + 1) * kLine * sizeof(unsigned);
-  AVC_TRY(zero_async(words, wbytes, s));
+  // counters [3][T][kRep] (one 128-B line each) in the persistent region of this layout
+  unsigned* region = nullptr;
+  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, 3 * (4 * H / 64), (size_t)3 * T * kRep * kLine, s, &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = 3; a.cnt_gstride = 0;
@@ -584,11 +747,10 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   a.hs0 = hs0; a.hs1 = hs1; a.hsz = hsz;
   a.y0 = y0; a.y1 = y1; a.g0 = g0; a.g1 = g1; a.c0 = c0; a.c1 = c1;
   a.diag = g_persist_diag;
-  a.cnt = words; a.tmo = words + (size_t)3 * T * kRep * kLine;
+  set_region_args(a, ctx, region);
   const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
   hipEvent_t ev = timing_begin(TC_LSTM2_PERSIST, s);
-  persist_launch(a, RT, 1, s);
-  AVC_LAUNCH_CHECK();
+  AVC_TRY(persist_launch(a, RT, 1, s));
   if (ev) {
     // one launch = the whole 2-layer recurrence: 3 products of [B x H] . [H x 4H] per time step;
     // algorithmic bytes = the split weights read once + per step the split h operands and the
@@ -643,6 +805,30 @@ extern "C" int avc_lstm_persist_layers(int mask) {
   avc::g_persist_layers = mask;
   ++avc::g_config_epoch;
   return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_coop(int on) {
+  avc::g_persist_coop = on ? 1 : 0;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_debug_persist_inject(int launches) {
+  if (launches < 0) {
+    avc::set_error("avc_debug_persist_inject: launches must be >= 0");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_inject = launches;
+  ++avc::g_config_epoch;  // drop a captured graph: the injection applies to eager launches
+  return AVC_OK;
+}
+
+extern "C" int avc_persist_check(avc_context* ctx, void* stream, int* failed) {
+  AVC_CHECK_ARG(ctx != nullptr, "ctx is NULL");
+  AVC_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+  const int rc = avc::persist_guard(ctx);
+  if (failed) *failed = rc == AVC_ERR_DEVICE ? 1 : 0;
+  return rc;
 }
 
 extern "C" int avc_lstm_persist_status(long* giveups) {

@@ -32,6 +32,9 @@ extern "C" {
 #define AVC_ERR_INVALID 1
 #define AVC_ERR_HIP 2
 #define AVC_ERR_WORKSPACE 3
+/* a device-side failure detected after the fact: a persistent recurrence launched by an
+ * earlier call on this context abandoned a bounded wait (its outputs were written as NaN) */
+#define AVC_ERR_DEVICE 4
 
 /* activation codes used by the conv/BN/linear entry points */
 #define AVC_ACT_NONE 0
@@ -238,9 +241,25 @@ int avc_lstm_persist_depth(int chunks);
 /* Tuning hook: which recurrences may take the persistent form (bit 0 = one layer, e.g. decoder
  * lstm1; bit 1 = two stacked layers, decoder lstm2; default 3 = both). */
 int avc_lstm_persist_layers(int mask);
-/* Synchronises the device and returns in *giveups the number of persistent-recurrence workgroups
+/* Synchronises the device and returns in *giveups the number of persistent-recurrence launches
  * that abandoned a bounded wait since the library was loaded (0 = every launch completed). */
 int avc_lstm_persist_status(long* giveups);
+/* Health check of a context (the persistent recurrences' safety net, lstm_persist.hip):
+ * synchronises `stream`, then returns AVC_ERR_DEVICE if a persistent launch of this context timed
+ * out since the last check (*failed = 1) and AVC_OK otherwise (*failed = 0).  Every entry point
+ * that launches a persistent recurrence performs the same check (without the synchronisation)
+ * before launching, so a failure is reported by the next call at the latest. */
+int avc_persist_check(avc_context* ctx, void* stream, int* failed);
+/* Tuning hook: launch the persistent recurrences with hipLaunchCooperativeKernel (1) instead of
+ * a plain launch after an occupancy check (0, default).  Both require every workgroup to be
+ * co-resident; the cooperative launch has the runtime guarantee it. */
+int avc_lstm_persist_coop(int on);
+/* Test hook: the next `launches` persistent launches give up at their first unsatisfied wait (as
+ * if a peer workgroup never became resident); eager launches only (captured graphs are dropped). */
+int avc_debug_persist_inject(int launches);
+/* Forward-graph policy of avc_generator_forward_cached: 1 = capture on the second call with the
+ * same key and replay (default); 0 = always eager (tests that need eager reference outputs). */
+int avc_graph_mode(int on);
 int avc_timing_reset(void);
 int avc_timing_read(int cls, double* total_ms, double* total_flops, double* total_bytes,
                     long* launches);

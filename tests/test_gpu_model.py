@@ -40,10 +40,13 @@ def check_bn(ae, g):
 
 
 @pytest.mark.parametrize("case", FWD_CASES)
-@pytest.mark.parametrize("path", ["fused", "autograd"])
+@pytest.mark.parametrize("path", ["fused", "autograd", "layers"])
 def test_forward_matches_reference(cuda_device, case, path):
+    """fused: no_grad whole-Generator call; autograd: grad enabled (convert()'s call), the fused
+    forward under one recomputing autograd node; layers: the per-layer autograd path."""
     g = load_golden(case)
     ae = make_model(cuda_device, bool(g["train"]))
+    ae.fused_autograd = path != "layers"
     x, co, ct = (_t(g[k], cuda_device) for k in ("x", "c_org", "c_trg"))
     if path == "fused":
         with torch.no_grad():
@@ -128,6 +131,7 @@ def test_fused_and_autograd_paths_agree(cuda_device):
     c = torch.rand(4, 256, generator=g).to(cuda_device)
     a = make_model(cuda_device, True)
     b = make_model(cuda_device, True)
+    b.fused_autograd = False  # the per-layer path
     with torch.no_grad():
         m1, p1, c1 = a(x, c, c)
     m2, p2, c2 = b(x.clone().requires_grad_(True), c, c)
@@ -329,9 +333,9 @@ def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
 def test_back_to_back_forwards_match(cuda_device):
     """Twenty fused C2 forwards enqueued back to back (no host sync between them; alternating two
     input batches so a stale read cannot hide behind equal bytes), each output cloned on the
-    stream and compared with that batch's eager result.  This is the pattern that caught counter
-    zeroing by hipMemsetAsync landing out of order with the persistent recurrences (the library
-    now zeroes with a kernel of its own, zero_async)."""
+    stream and compared with that batch's eager result.  This is the pattern that caught the
+    round-1 per-call counter reset misbehaving on graph replay (the counters are now epoch-tagged
+    and never reset)."""
     from autovc_amd import _lib
     from autovc_amd.weights import synthetic_embedding, synthetic_mel
     ae = make_model(cuda_device)
@@ -339,11 +343,11 @@ def test_back_to_back_forwards_match(cuda_device):
     xs = [_t(synthetic_mel(s, B, T), cuda_device) for s in (61, 62)]
     co, ct = _t(synthetic_embedding(63, B), cuda_device), _t(synthetic_embedding(64, B), cuda_device)
     with torch.no_grad():
-        _lib.timing_enable(["dft64"])  # timing on => eager launches (no graph) for the references
+        _lib.call("avc_graph_mode", 0)  # eager launches for the references
         try:
             refs = [[o.clone() for o in ae(x, co, ct)] for x in xs]
         finally:
-            _lib.timing_enable([])
+            _lib.call("avc_graph_mode", 1)
         torch.cuda.synchronize()
         keep = []
         for i in range(20):

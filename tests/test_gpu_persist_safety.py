@@ -1,0 +1,136 @@
+"""Safety net of the persistent weight-stationary recurrences (lstm_persist.hip).
+
+Every wait inside a persistent launch assumes that its producer workgroups are resident.  If one is
+not (another process or stream holding CUs), the wait is bounded: the launch gives up, writes the
+rows it did not compute as NaN and reports itself through a pinned host word, and the next call on
+the context fails with RuntimeError (AVC_ERR_DEVICE) after resetting the counter state.  The test
+hook avc_debug_persist_inject makes the next launch give up at its first unsatisfied wait."""
+import ctypes
+
+import pytest
+import torch
+
+from autovc_amd import _lib
+from autovc_amd.auto_encoder import AutoEncoder
+from autovc_amd.weights import onehot_embedding, synthetic_embedding, synthetic_mel, torch_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev):
+    ae = AutoEncoder(device=dev, verbose=False)
+    ae.load_state_dict(torch_state_dict(0))
+    return ae.to(dev).train()
+
+
+def _giveups():
+    n = ctypes.c_long(0)
+    _lib.call("avc_lstm_persist_status", ctypes.byref(n))
+    return n.value
+
+
+def _batch(dev, B=64, T=128):
+    x = torch.from_numpy(synthetic_mel(71, B, T)).to(dev)
+    co = torch.from_numpy(synthetic_embedding(72, B)).to(dev)
+    ct = torch.from_numpy(synthetic_embedding(73, B)).to(dev)
+    return x, co, ct
+
+
+def test_timed_out_forward_is_nan_and_next_call_raises(cuda_device):
+    ae = _model(cuda_device)
+    x, co, ct = _batch(cuda_device)
+    with torch.no_grad():
+        ref = [o.clone() for o in ae(x, co, ct)]
+        torch.cuda.synchronize()
+        before = _giveups()
+        _lib.call("avc_debug_persist_inject", 1)
+        bad = [o.clone() for o in ae(x, co, ct)]
+        torch.cuda.synchronize()
+        assert _giveups() > before, "the injected launch did not give up"
+        assert torch.isnan(bad[0]).any() and torch.isnan(bad[1]).any(), "timed-out launch returned numbers"
+        with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+            ae(x, co, ct)
+        # state was reset: the persistent path runs again and gives the eager answer bit for bit
+        # (train-mode BN normalises with batch statistics, so the NaN running buffers the failed
+        # call left do not enter the outputs)
+        outs = [[o.clone() for o in ae(x, co, ct)] for _ in range(3)]  # eager, capture, replay
+        torch.cuda.synchronize()
+    for run in outs:
+        for a, b in zip(run, ref):
+            assert torch.equal(a, b)
+    ae.check_health()  # nothing pending
+
+
+def test_check_health_reports_a_timeout(cuda_device):
+    ae = _model(cuda_device)
+    x, co, ct = _batch(cuda_device, 16, 64)
+    with torch.no_grad():
+        ae(x, co, ct)
+        ae.check_health()
+        _lib.call("avc_debug_persist_inject", 1)
+        ae(x, co, ct)
+        with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+            ae.check_health()
+        ae.check_health()  # reported once
+
+
+def test_train_step_after_timeout_raises(cuda_device):
+    ae = _model(cuda_device)
+    B, T = 32, 64
+    X = torch.from_numpy(synthetic_mel(74, B, T)).to(cuda_device)
+    c = torch.from_numpy(onehot_embedding(B)).to(cuda_device)
+    ae.configure_optimizer()
+    ae.train_step(X, c)
+    _lib.call("avc_debug_persist_inject", 1)
+    loss, _ = ae.train_step(X, c)
+    assert not torch.isfinite(loss).item()
+    with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+        ae.train_step(X, c)
+
+
+def test_cooperative_launch_matches(cuda_device):
+    """avc_lstm_persist_coop(1): the same kernels under hipLaunchCooperativeKernel (runtime
+    co-residency guarantee), eager and graph-replayed, bit-identical to the default launch."""
+    ae = _model(cuda_device)
+    x, co, ct = _batch(cuda_device)
+    with torch.no_grad():
+        ref = [o.clone() for o in ae(x, co, ct)]
+        _lib.call("avc_lstm_persist_coop", 1)
+        try:
+            runs = [[o.clone() for o in ae(x, co, ct)] for _ in range(3)]
+            torch.cuda.synchronize()
+        finally:
+            _lib.call("avc_lstm_persist_coop", 0)
+    for run in runs:
+        for a, b in zip(run, ref):
+            assert torch.equal(a, b)
+    ae.check_health()
+
+
+def test_alternating_launch_layouts(cuda_device):
+    """One-layer persistent launches of different H at the same (T, batch groups) alternate on one
+    context (decoder.lstm1 H=512 and the per-layer decoder.lstm2 H=1024 in training): each launch
+    layout owns its counter region, so no epoch arithmetic leaks between them.  Outputs against
+    the launch-per-step kernel (avc_lstm_persist_tune(0)), no give-ups."""
+    from autovc_amd import ops
+    T, B = 128, 64
+    g = torch.Generator(device="cpu").manual_seed(3)
+    layers = []
+    for H, din in ((512, 320), (1024, 512)):
+        w = [((torch.rand(4 * H, din, generator=g) - 0.5) * 0.1), ((torch.rand(4 * H, H, generator=g) - 0.5) * 0.1),
+             torch.rand(4 * H, generator=g) * 0.1, torch.rand(4 * H, generator=g) * 0.1]
+        layers.append(([t.to(cuda_device) for t in w], torch.rand(T * B, din, generator=g).to(cuda_device)))
+    refs = []
+    _lib.call("avc_lstm_persist_tune", 0)
+    try:
+        for w, x in layers:
+            refs.append(ops.LSTMLayer.apply(x, *w, T, B, False))
+    finally:
+        _lib.call("avc_lstm_persist_tune", 2)
+    before = _giveups()
+    for _ in range(4):
+        for (w, x), ref in zip(layers, refs):
+            for save in (False, True):
+                y = ops.LSTMLayer.apply(x, *w, T, B, save)
+                assert float((y - ref).abs().max()) <= 1e-6
+    assert _giveups() == before
