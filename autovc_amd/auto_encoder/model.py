@@ -46,7 +46,8 @@ class FusedAdam(torch.optim.Optimizer):
         model._ensure_flat()
         params = list(model.parameters())
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
-                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None)
+                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None,
+                        decoupled_weight_decay=False)
         super().__init__(params, defaults)
         self.model = model
         self.exp_avg = torch.zeros_like(model._flat_param)
@@ -83,13 +84,23 @@ class FusedAdam(torch.optim.Optimizer):
         return loss
 
     def load_state_dict(self, state_dict):
+        """torch.optim.Adam's state_dict (the reference checkpoint's optimizer_state, model.py:175):
+        moments copied into the flat buffers, the step count restored, param_groups settings."""
         st = state_dict["state"]
         params = list(self.model.parameters())
+        if len(state_dict["param_groups"]) != 1 or len(state_dict["param_groups"][0]["params"]) != len(params):
+            raise ValueError("optimizer state does not match this AutoEncoder's parameters")
+        steps = set()
         for i, p in enumerate(params):
             if i in st:
+                if st[i]["exp_avg"].shape != p.shape:
+                    raise ValueError(f"optimizer state {i}: shape {tuple(st[i]['exp_avg'].shape)} != {tuple(p.shape)}")
                 self.state[p]["exp_avg"].copy_(st[i]["exp_avg"])
                 self.state[p]["exp_avg_sq"].copy_(st[i]["exp_avg_sq"])
-                self._step = int(float(st[i]["step"]))
+                steps.add(int(float(st[i]["step"])))
+        if len(steps) > 1:
+            raise ValueError("per-parameter Adam step counts differ; the fused update keeps one")
+        self._step = steps.pop() if steps else 0
         self._step_t.fill_(float(self._step))
         for g, sg in zip(self.param_groups, state_dict["param_groups"]):
             for k, v in sg.items():
@@ -324,8 +335,12 @@ class AutoEncoder(nn.Module):
             print("Loaded auto encoder \"%s\" trained to step %d" % (model_path, checkpoint["step"]))
 
     def save(self, model_name, save_dir=AutoEncoderParams["learn"]["save_dir"], wandb_run=None):
+        """model.py:158-181.  Data parallel: every rank must call it (the BN buffers are broadcast
+        from rank 0 first); only rank 0 writes the file."""
         model_path = save_dir.strip("/") + "/" + model_name
         self._sync_bn_buffers()
+        if dp.rank() != 0:
+            return
         torch.save({
             "step": self.logging.get("step"),
             "model_state": {k: v.detach().clone() for k, v in self.state_dict().items()},
@@ -388,6 +403,9 @@ class AutoEncoder(nn.Module):
         per-epoch ExponentialLR(0.95)); the optimizer is FusedAdam with the reference's Adam
         settings (hparams optimizer dict; like the reference, **opt_params are not applied)."""
         self.logging.update(step=0, running_loss=0.0, log_steps=0, total_time=0.0)
+        # data parallel (torchrun, one process per GPU): each rank trains on its own shard of the
+        # caller's loader; train_step all-reduces the gradient (dp.py)
+        trainloader = dp.shard_loader(trainloader)
         N_iterations = n_epochs * len(trainloader)
         self.train()
         if wandb_run is not None:
@@ -396,11 +414,12 @@ class AutoEncoder(nn.Module):
         self.criterion2 = ops.l1_loss
         self.configure_optimizer()
         self.lr_scheduler = torch.optim.lr_scheduler.ExponentialLR(self.optimiser, gamma=0.95)
-        if self.verbose:
-            print(f"Training Auto Encoder on {torch.cuda.get_device_name()} (cuda)...")
+        if self.verbose and dp.rank() == 0:
+            print(f"Training Auto Encoder on {torch.cuda.get_device_name()} (cuda), {dp.world()} rank(s)...")
         for epoch in range(n_epochs):
             self.logging["step_start_time"] = time.time()
             self.logging["batch"] = 0
+            dp.set_epoch(trainloader, epoch)
             for X, c_org in trainloader:
                 loss, _ = self.train_step(X, c_org, ema_decay=ema_decay)
                 self.logging["step"] += 1
@@ -409,7 +428,7 @@ class AutoEncoder(nn.Module):
                 self.logging["epoch"] = epoch + 1
                 self.logging["batch"] += 1
                 self.logging["lr"] = self.optimiser.param_groups[0]["lr"]
-                if self.verbose:
+                if self.verbose and dp.rank() == 0:
                     self.logging["total_time"] += (time.time() - self.logging["step_start_time"])
                     print(f"\rstep {self.logging['step']}/{N_iterations} | loss {float(loss):.5f}", end="")
                 if (self.logging["step"] % log_freq == 0 or self.logging["step"] == N_iterations) \
@@ -417,7 +436,7 @@ class AutoEncoder(nn.Module):
                     self._log(wandb_run, X, None)
             if self.logging["epoch"] % save_freq == 0 or self.logging["epoch"] == n_epochs:
                 self.save(model_name, save_dir, wandb_run)
-            if voice_converter is not None:
+            if voice_converter is not None and dp.rank() == 0:
                 assert source_examples is not None and target_examples is not None
                 voice_converter.convert_multiple(
                     sources=source_examples, targets=target_examples,

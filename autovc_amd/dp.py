@@ -49,6 +49,41 @@ def params_in_sync(flat_param: torch.Tensor) -> bool:
     return bool(torch.equal(lo, hi))
 
 
+def broadcast_seed(src: int = 0) -> int:
+    """A 63-bit seed drawn from rank `src`'s torch RNG, the same on every rank."""
+    seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
+    if world() > 1:
+        dist.broadcast(seed, src)
+    return int(seed.item())
+
+
+def shard_loader(loader, seed: int | None = None):
+    """The caller's DataLoader (voice_converter.py:282-285 builds it: dataloader.py:123-144,
+    batch_size utterances per batch, shuffle=True, zero-padding collate_fn) re-built over a
+    DistributedSampler: rank r loads only its own 1/world of the utterances, in batches of the
+    same batch_size (the per-GPU batch of BASELINE config 4), every rank runs the same number of
+    steps (drop_last on the shard), and all ranks draw their shuffles from one seed broadcast from
+    rank 0 (call set_epoch(epoch) on the returned loader's sampler each epoch, as learn() does).
+    World 1: the loader itself."""
+    from torch.utils.data import DataLoader, DistributedSampler, RandomSampler
+    if world() == 1:
+        return loader
+    if not isinstance(loader, DataLoader) or loader.batch_size is None:
+        raise TypeError("data-parallel learn() needs a torch DataLoader with a batch_size (dataloader.py:137)")
+    seed = broadcast_seed() if seed is None else seed
+    sampler = DistributedSampler(loader.dataset, num_replicas=world(), rank=rank(),
+                                 shuffle=isinstance(loader.sampler, RandomSampler), seed=seed, drop_last=True)
+    return DataLoader(loader.dataset, batch_size=loader.batch_size, sampler=sampler,
+                      collate_fn=loader.collate_fn, num_workers=loader.num_workers,
+                      pin_memory=loader.pin_memory, drop_last=loader.drop_last)
+
+
+def set_epoch(loader, epoch: int) -> None:
+    from torch.utils.data import DistributedSampler
+    if isinstance(getattr(loader, "sampler", None), DistributedSampler):
+        loader.sampler.set_epoch(epoch)
+
+
 def shard_indices(n: int, r: int | None = None, ws: int | None = None) -> range:
     """Contiguous, equal-size shard of n utterance minibatches for rank r (drops the remainder
     so every rank runs the same number of steps, as the collective requires)."""

@@ -76,12 +76,32 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(args):
+    """`bench.py --gpus N` (N > 1) started without torchrun: launch N ranks (one process per GPU)
+    under torch.distributed.run as a child process, before anything touches the GPU, and exit with
+    its status.  A multi-GPU request is never measured on fewer GPUs than asked for."""
+    import socket
+    import subprocess
+    n = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if n < args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} requested but only {n} GPU(s) are visible")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    raise SystemExit(subprocess.call(cmd))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
+    if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -237,9 +257,27 @@ def setup_generator(args, dev, rank):
 
     fwd = args.mode == "fwd"
 
+    def convert_call():
+        """The same batch called exactly as VoiceConverter.convert() calls the Generator
+        (voice_converter.py:172-174): grad mode on, parameters requiring grad, outputs carrying a
+        grad_fn (the fused forward under one recomputing autograd node)."""
+        assert all(p.requires_grad for p in model.parameters())
+        outs = None
+        for _ in range(max(2, args.warmup)):
+            outs = model(x, c_org, c_trg)
+        assert outs[1].grad_fn is not None
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            outs = model(x, c_org, c_trg)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        return {"value": round(B * T / dt, 1), "unit": "mel-frames/s", "ms_per_step": round(1000 * dt, 3)}
+
     def eval_bn():
         """The same batch with eval-mode BN (running statistics), reported beside the train-mode
-        headline ("eval also reported")."""
+        headline ("eval also reported"); and the convert()-style grad-enabled call."""
+        conv = convert_call()
         model.eval()
         with torch.no_grad():
             for _ in range(max(2, args.warmup)):  # eager, then graph capture
@@ -251,7 +289,8 @@ def setup_generator(args, dev, rank):
             torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
         model.train()
-        return {"eval_bn": {"value": round(B * T / dt, 1), "unit": "mel-frames/s", "ms_per_step": round(1000 * dt, 3)}}
+        return {"eval_bn": {"value": round(B * T / dt, 1), "unit": "mel-frames/s", "ms_per_step": round(1000 * dt, 3)},
+                "convert_call": conv}
 
     return {
         "step": step, "units_per_step": B * T, "unit": "mel-frames/s", "dtype": "f32",

@@ -159,6 +159,44 @@ class Trainer:
     def flatten(self):
         return torch.cat([self.p[k].detach().reshape(-1) for k in self.names])
 
+    def grads(self, X, c, bufs):
+        """Loss and parameter gradients of one batch; `bufs` takes the BN running-stat updates."""
+        sd = dict(self.p)
+        sd.update(bufs)
+        out_dec, out_post, codes = forward(sd, X, c, c, True, bufs)
+        loss = loss_fn(sd, X, c, out_dec, out_post, codes, bufs)
+        return float(loss.detach()), torch.autograd.grad(loss, [self.p[k] for k in self.names])
+
+    def step_dp(self, shards, bufs_per_rank):
+        """Data-parallel form of step() (BASELINE config 4): every rank r computes
+        the gradient of its own shard (its own BN batch statistics and running buffers), the
+        gradients are averaged (the all-reduce), then clip_grad_norm_(1) + Adam + EMA exactly as
+        the single-process step (model.py:313-321).  Returns (per-rank losses, pre-clip norm)."""
+        losses, acc = [], None
+        for (X, c), bufs in zip(shards, bufs_per_rank):
+            l, g = self.grads(X, c, bufs)
+            losses.append(l)
+            acc = list(g) if acc is None else [a + b for a, b in zip(acc, g)]
+        grads = [a / len(shards) for a in acc]
+        return losses, self._apply(grads)
+
+    def _apply(self, grads):
+        norm = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g) for g in grads]))
+        coef = torch.clamp(1.0 / (norm + 1e-6), max=1.0)
+        self.t += 1
+        b1, b2 = self.betas
+        with torch.no_grad():
+            for k, g in zip(self.names, grads):
+                g = g * coef
+                self.m[k].mul_(b1).add_(g, alpha=1 - b1)
+                self.v[k].mul_(b2).addcmul_(g, g, value=1 - b2)
+                bc1 = 1 - b1 ** self.t
+                bc2 = 1 - b2 ** self.t
+                denom = (self.v[k].sqrt() / math.sqrt(bc2)).add_(self.eps)
+                self.p[k].addcdiv_(self.m[k], denom, value=-self.lr / bc1)
+            self.avg = self.ema_decay * self.avg + (1 - self.ema_decay) * self.flatten()
+        return float(norm)
+
     def step(self, X, c):
         sd = self.sd()
         out_dec, out_post, codes = forward(sd, X, c, c, True, self.bufs)

@@ -153,8 +153,52 @@ def train_case(AE, hparams, steps=3, B=4, T=128):
     return d
 
 
+def checkpoint_layout_case(AE, hparams, B=2, T=64):
+    """The checkpoint dict the reference's learn() writes through save() (model.py:158-176): one
+    training step, then the file's structure (model_state keys/shapes/dtypes, optimizer_state's
+    torch.optim.Adam layout and param_groups, step) and a few value sums.  Written as JSON."""
+    ae, ck = make_ae(AE)
+    hp_opt = hparams["optimizer"]
+    saved = dict(hp_opt)
+    X, c = torch.from_numpy(synthetic_mel(91, B, T)), torch.from_numpy(onehot_embedding(B))
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        os.makedirs("ckpt")
+        try:
+            ae.learn([(X, c)], n_epochs=1, save_dir="ckpt", model_name="m.pt")
+            ckpt = torch.load("ckpt/m.pt", weights_only=True)
+        finally:
+            os.chdir(cwd)
+            hp_opt.clear()
+            hp_opt.update(saved)
+    ms = ckpt["model_state"]
+    opt = ckpt["optimizer_state"]
+    st0 = opt["state"][0]
+    return {
+        "top_keys": sorted(ckpt.keys()),
+        "step": ckpt["step"],
+        "model_state": [[k, list(v.shape), str(v.dtype)] for k, v in ms.items()],
+        "optimizer_state_keys": sorted(opt.keys()),
+        "n_state": len(opt["state"]),
+        "state_entry_keys": sorted(st0.keys()),
+        "state_step_dtype": str(st0["step"].dtype), "state_step_shape": list(st0["step"].shape),
+        "param_groups": [{k: (len(v) if k == "params" else v) for k, v in g.items()} for g in opt["param_groups"]],
+        "exp_avg_abs_sum": float(sum(float(s["exp_avg"].double().abs().sum()) for s in opt["state"].values())),
+        "weights_checksum": ck,
+    }
+
+
 def main():
     AE, hparams = load_reference()
+    if sys.argv[1:] == ["reference_checkpoint_layout"]:
+        import json
+        d = checkpoint_layout_case(AE, hparams)
+        path = os.path.join(HERE, "reference_checkpoint_layout.json")
+        with open(path, "w") as fh:
+            json.dump(d, fh, indent=1, default=str)
+        print(f"wrote {path}")
+        return
     torch.set_num_threads(8)
     cases = {
         "fwd_b2_t128_train": lambda: fwd_case(AE, 2, 128, True, 1),

@@ -89,3 +89,17 @@ def test_golden_fixture_shapes():
     assert g["codes"].shape == (2, 224)
     g = load_golden("batch_forward_m5_n128")
     assert g["out"].shape == (80, 4 * 64 + 128)
+
+
+def test_bench_refuses_fewer_gpus_than_requested():
+    """bench.py --gpus N without torchrun spawns N ranks itself, and never measures a multi-GPU
+    request on fewer GPUs (here: none visible) -> non-zero exit, no JSON line."""
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0 and "GPU(s) are visible" in (r.stdout + r.stderr)
+    assert '"metric"' not in r.stdout

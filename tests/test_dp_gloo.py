@@ -76,3 +76,74 @@ def test_dp_gloo_world2():
 def test_shard_single_process():
     assert list(dp.shard_indices(7, 0, 1)) == list(range(7))
     assert dp.world() == 1 and dp.rank() == 0
+
+
+class _Toy(torch.utils.data.Dataset):
+    def __len__(self):
+        return 23
+
+    def __getitem__(self, i):
+        return torch.full((80, 4), float(i)), torch.zeros(256)
+
+
+def _loader_worker(rank, ws, port, q, tmp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        torch.manual_seed(7 + rank)  # ranks' own RNGs differ; the shuffle seed comes from rank 0
+        loader = torch.utils.data.DataLoader(_Toy(), batch_size=3, shuffle=True)
+        sh = dp.shard_loader(loader)
+        epochs = []
+        for e in range(2):
+            dp.set_epoch(sh, e)
+            epochs.append([[int(v) for v in X[:, 0, 0]] for X, _ in sh])
+        # save(): the BN buffers come from rank 0 and only rank 0 writes
+        from autovc_amd.auto_encoder import AutoEncoder
+        ae = AutoEncoder(device="cpu", verbose=False)
+        for m in ae.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.fill_(float(rank + 1))
+        ae.configure_optimizer()
+        calls = []
+        real = torch.save
+        torch.save = lambda obj, path: (calls.append(path), real(obj, path))
+        os.chdir(tmp)  # save() paths are relative like the reference's (save_dir.strip("/"))
+        try:
+            ae.save("ae.pt", save_dir="ckpt")
+        finally:
+            torch.save = real
+        bn = float(ae.encoder.convolutions[0][1].running_mean[0])
+        q.put((rank, epochs, len(calls), bn))
+    except Exception as e:  # report instead of leaving the parent waiting
+        q.put((rank, repr(e), -1, -1.0))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_learn_sharding_and_save_world2(tmp_path):
+    """learn()'s data-parallel pieces: dp.shard_loader gives every rank a disjoint, equal-size
+    share of the caller's loader with the same batch size, reshuffled per epoch from one seed
+    broadcast by rank 0; AutoEncoder.save broadcasts rank 0's BN buffers and writes on rank 0 only."""
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    (tmp_path / "ckpt").mkdir()
+    procs = [ctx.Process(target=_loader_worker, args=(r, ws, port, q, str(tmp_path))) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in range(ws)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[2] >= 0 for r in res), res
+    assert all(p.exitcode == 0 for p in procs)
+    (_, e0, calls0, bn0), (_, e1, calls1, bn1) = res
+    for e in range(2):
+        a = [i for b in e0[e] for i in b]
+        b = [i for b in e1[e] for i in b]
+        assert len(a) == len(b) == 11 and not set(a) & set(b)
+        assert [len(x) for x in e0[e]] == [len(x) for x in e1[e]] == [3, 3, 3, 2]
+    assert e0[0] != e0[1]  # reshuffled per epoch
+    assert (calls0, calls1) == (1, 0) and bn0 == bn1 == 1.0
+    assert (tmp_path / "ckpt" / "ae.pt").exists()

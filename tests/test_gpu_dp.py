@@ -1,0 +1,101 @@
+"""Data-parallel training step on the GPU (BASELINE config 4's path at world size 2): two ranks on
+the box's one MI355X, gloo carrying the gradient all-reduce (RCCL does not run two ranks on one
+device; the product path is the same dp.average_gradients call).  Each rank runs
+AutoEncoder.train_step on its own half of the batch; the ordering under test is forward + loss +
+backward per rank -> all-reduce mean -> clip_grad_norm_(1) -> Adam -> EMA on every rank, checked
+against the oracle's step_dp (oracle/autovc_oracle.py), and the ranks' parameters must stay
+bit-identical."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B_RANK, T = 16, 64
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard(rank):
+    from autovc_amd.weights import onehot_embedding, synthetic_mel
+    X = synthetic_mel(81, 2 * B_RANK, T)[rank * B_RANK:(rank + 1) * B_RANK]
+    c = onehot_embedding(2 * B_RANK)[rank * B_RANK:(rank + 1) * B_RANK]
+    return torch.from_numpy(np.ascontiguousarray(X)), torch.from_numpy(np.ascontiguousarray(c))
+
+
+def _worker(rank, ws, port, q, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        from autovc_amd import dp
+        from autovc_amd.auto_encoder import AutoEncoder
+        from autovc_amd.weights import torch_state_dict
+        dev = torch.device("cuda:0")
+        ae = AutoEncoder(device=dev, verbose=False)
+        ae.load_state_dict(torch_state_dict(0))
+        ae.to(dev).train()
+        ae.configure_optimizer()
+        X, c = _shard(rank)
+        loss, norm = ae.train_step(X.to(dev), c.to(dev))
+        rec = {"loss": loss.item(), "norm": norm.item(), "sync1": dp.params_in_sync(ae._flat_param)}
+        if rank == 0:
+            torch.save({"flat": ae._flat_param.cpu(), "ema_sum": float(ae.avg_params.double().sum())},
+                       os.path.join(out_dir, "rank0.pt"))
+        rec["bufs"] = {k: v.cpu().numpy().copy() for k, v in ae.state_dict().items() if "running" in k}
+        ae.train_step(X.to(dev), c.to(dev))
+        rec["sync2"] = dp.params_in_sync(ae._flat_param)
+        ae.check_health()
+        q.put((rank, rec))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, {"error": repr(e)}))
+        raise
+
+
+def test_dp_train_step_world2_against_oracle(tmp_path):
+    from oracle import autovc_oracle as orc
+    from autovc_amd.weights import torch_state_dict
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, q, str(tmp_path))) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+    assert all("error" not in r for r in res.values()), res
+    assert all(p.exitcode == 0 for p in procs)
+
+    sd = torch_state_dict(0)
+    tr = orc.Trainer(sd)
+    bufs = [{k: v.clone() for k, v in sd.items() if k not in tr.p} for _ in range(ws)]
+    losses, norm = tr.step_dp([_shard(r) for r in range(ws)], bufs)
+    print(f"DP world 2: losses {[res[r]['loss'] for r in range(ws)]} (oracle {losses}); "
+          f"norm {[res[r]['norm'] for r in range(ws)]} (oracle {norm:.6f})")
+    for r in range(ws):
+        assert res[r]["sync1"] and res[r]["sync2"], "ranks' parameters diverged"
+        assert res[r]["loss"] == pytest.approx(losses[r], rel=1e-5)
+        assert res[r]["norm"] == pytest.approx(norm, rel=1e-3)  # the global (averaged) gradient's norm
+        for k, v in res[r]["bufs"].items():  # per-rank BN statistics (no SyncBN)
+            assert float((torch.from_numpy(v) - bufs[r][k]).abs().max()) <= 1e-5, (r, k)
+    got = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    flat_ref = tr.flatten()
+    d = (got["flat"].double() - flat_ref.double()).abs()
+    frac = float((d <= 1e-6).double().mean())
+    print(f"params after one DP step: worst |d| {float(d.max()):.2e}, agreeing to 1e-6: {100 * frac:.3f} %")
+    assert float(d.max()) <= 2 * 1e-3 * 1.01 and frac >= 0.98
+    assert got["ema_sum"] == pytest.approx(float(tr.avg.double().sum()), rel=1e-6)
