@@ -111,6 +111,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_CHECK_ARG(B >= 1, "batch must be >= 1");
   const long TB = (long)T * B;
   Scratch sc(ctx);
+  RangeScope ranges(ctx);  // producers register activations whose range they checked (gemm.hip guard)
   AVC_TAKE(x0, float, (size_t)TB * 336, sc);
   AVC_TAKE(ba, float, (size_t)TB * 512, sc);
   AVC_TAKE(bb, float, (size_t)TB * 512, sc);
@@ -151,6 +152,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   const int EL = P_ENC_LSTM;
   AVC_TRY(bilstm_forward_impl(ctx, T, B, 512, 32, ba, 512, P + EL, P + EL + 4, e1, 64, nullptr, nullptr,
                               nullptr, nullptr, s));
+  mark_range_checked(ctx, e1);  // an LSTM's h: |h| < 1
   AVC_TRY(bilstm_forward_impl(ctx, T, B, 64, 32, e1, 64, P + EL + 8, P + EL + 12, e2, 64, nullptr, nullptr,
                               nullptr, nullptr, s));
   AVC_TRY(codes_from_encoder(T, B, e2, codes, s));
@@ -160,6 +162,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   const int D1 = P_DEC_LSTM1;
   AVC_TRY(lstm_forward_impl(ctx, T, B, 320, 512, 0, din, 320, P[D1], P[D1 + 1], P[D1 + 2], P[D1 + 3],
                             ba, 512, nullptr, nullptr, s));
+  mark_range_checked(ctx, ba);  // lstm1's h
   AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, nullptr, fa));
   AVC_TRY(cba(P_DEC_CONV + 6, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fa, fb));
   AVC_TRY(cba(P_DEC_CONV + 12, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, fb));
@@ -174,6 +177,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   lin.bias0 = P[P_LIN + 1];
   lin.C = melf; lin.ldc = 80;
   lin.prec16 = 1;
+  lin.a_bound = 1.f;  // |h| < 1 (lstm2's output): no range scan needed
   if (ctx->prep_version >= 0) {
     bool fb = true;
     auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_GEMM_BFRAG, P[P_LIN], nullptr, gemm_bfrag_bytes(lin), &fb));
@@ -430,6 +434,7 @@ int avc_generator_forward(avc_context* ctx, int T, int B, const float* const* pa
   AVC_CHECK_ARG(ctx && params && x && c_org && c_trg && mel && mel_post && codes, "NULL pointer");
   for (int i = 0; i < P_COUNT; ++i) AVC_CHECK_ARG(params[i] != nullptr, "NULL parameter pointer");
   AVC_TRY(ensure_arena(ctx, gen_scratch(T, B)));
+  AVC_TRY(persist_guard(ctx));
   return generator_forward(ctx, T, B, params, x, c_org, c_trg, training, mel, mel_post, codes,
                            S(stream));
 }

@@ -109,6 +109,11 @@ struct avc_context {
   std::vector<avc_persist_region> regions;
   unsigned long region_clock = 0;
   unsigned* fail_host = nullptr;  // pinned host word: device-wide number of the last timed-out persistent launch
+  unsigned* guard_ticket = nullptr;  // self-resetting ticket of the single-launch range scan (gemm.hip)
+  // activations whose range a producer already checked (or bounds by construction: an LSTM's h)
+  // inside the current whole-Generator forward; their contractions skip the range scan
+  bool track_ranges = false;
+  std::vector<const void*> range_ok;
   unsigned fail_seen = 0;         // value of *fail_host already reported to the caller
   std::vector<avc_prep_entry> prep;
   avc_gen_graph gen;
@@ -126,9 +131,26 @@ namespace avc {
 // hipMemsetAsync everywhere (see there)
 int zero_async(void* p, size_t bytes, hipStream_t s);
 
-// Reports (once) a persistent-recurrence launch that abandoned a bounded wait since the last
-// report: AVC_ERR_DEVICE with a message, after dropping the counter regions and the captured
-// forward graph so the next call starts from fresh state (lstm_persist.hip).
+// Device-side failures reported through the context's pinned host words (host_flags):
+//   [0] number of the last persistent-recurrence launch that abandoned a bounded wait;
+//   [1] set when a conv -> conv hand-over held a finite value beyond the f16 split's range.
+// persist_guard reports each (once) as AVC_ERR_DEVICE with a message; for [0] it first drops the
+// counter regions and the captured forward graph so the next call starts from fresh state.
+unsigned* host_flags(avc_context* ctx);  // nullptr (error set) if the pinned words cannot be allocated
+inline void mark_range_checked(avc_context* ctx, const void* p) {
+  if (ctx->track_ranges) ctx->range_ok.push_back(p);
+}
+// scope of range tracking: one whole-Generator forward
+struct RangeScope {
+  avc_context* ctx;
+  explicit RangeScope(avc_context* c) : ctx(c) { ctx->track_ranges = true; ctx->range_ok.clear(); }
+  ~RangeScope() { ctx->track_ranges = false; ctx->range_ok.clear(); }
+};
+inline bool range_checked(const avc_context* ctx, const void* p) {
+  for (const void* q : ctx->range_ok)
+    if (q == p) return true;
+  return false;
+}
 int persist_guard(avc_context* ctx);
 void persist_release(avc_context* ctx);
 

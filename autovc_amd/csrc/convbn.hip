@@ -110,7 +110,16 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   AVC_TRY(gemm_run(ctx, g, s));
   AVC_TRY(bn_finalize(cout, nparts, stats, (double)T * B, training, momentum, eps, running_mean,
                       running_var, mean, invstd, s));
-  AVC_TRY(bn_apply((long)T * B, cout, y_pre, mean, invstd, gamma, beta, act, residual, out, s, out_frag));
+  // inside the whole-Generator forward the output's range is checked here (its consumer then
+  // skips the scan); a value the next split could not hold is reported to the host.  The layer
+  // with a residual (postnet's last, model.py:131-132) produces the final mel_post, which no
+  // contraction reads: nothing to check.
+  const bool check = out_frag || (ctx->track_ranges && !residual);
+  unsigned* flags = check ? host_flags(ctx) : nullptr;
+  if (check && !flags) return AVC_ERR_HIP;
+  AVC_TRY(bn_apply((long)T * B, cout, y_pre, mean, invstd, gamma, beta, act, residual, out, s, out_frag,
+                   flags ? flags + 1 : nullptr));
+  if (check && out) mark_range_checked(ctx, out);
   return AVC_OK;
 }
 

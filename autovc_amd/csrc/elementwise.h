@@ -7,10 +7,12 @@ namespace avc {
 int bn_finalize(int C, int nparts, const float* stats, double count, int training, float momentum,
                 float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s);
 // frag != NULL: also write the output split into the GEMM's fragment-major A layout
-// (gemm_afrag_bytes(M, C) bytes, for GemmDesc::a_frag); out may then be NULL (not stored)
+// (gemm_afrag_bytes(M, C) bytes, for GemmDesc::a_frag); out may then be NULL (not stored).
+// range_flag (pinned host word): set when a finite output exceeds the f16 split's range (the
+// output is then range-checked: mark_range_checked lets its consumer skip the scan)
 int bn_apply(long M, int C, const float* y, const float* mean, const float* invstd,
              const float* gamma, const float* beta, int act, const float* residual, float* out,
-             hipStream_t s, _Float16* frag = nullptr);
+             hipStream_t s, _Float16* frag = nullptr, unsigned* range_flag = nullptr);
 size_t bn_backward_scratch(int M, int C);
 int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* y,
                 const float* mean, const float* invstd, const float* gamma, const float* beta,

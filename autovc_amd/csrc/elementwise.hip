@@ -116,7 +116,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, int act,
                                                        const float* __restrict__ residual,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ out,
+                                                       unsigned* __restrict__ range_flag) {
   const int Q = C / 4;
   const long nthreads = (long)gridDim.x * blockDim.x;
   const long gt = blockIdx.x * (long)blockDim.x + threadIdx.x;
@@ -141,6 +142,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
       const float4 rr = reinterpret_cast<const float4*>(residual)[i4];
       o[0] += rr.x; o[1] += rr.y; o[2] += rr.z; o[3] += rr.w;
     }
+    if (range_flag) {  // the consumer contraction skips its range scan (see bn_apply_frag_kernel)
+      bool over = false;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) over |= fabsf(o[e]) >= 65504.f && fabsf(o[e]) < __builtin_inff();
+      if (over) __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     reinterpret_cast<float4*>(out)[i4] = make_float4(o[0], o[1], o[2], o[3]);
   }
 }
@@ -158,7 +165,8 @@ __global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int n
                                                             const float* __restrict__ beta, int act,
                                                             const float* __restrict__ residual,
                                                             float* __restrict__ out,
-                                                            _Float16* __restrict__ frag) {
+                                                            _Float16* __restrict__ frag,
+                                                            unsigned* __restrict__ range_flag) {
   const int G8 = nkc * 2;
   const long total = ntile * 32 * G8;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -199,12 +207,18 @@ __global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int n
       for (int e = 0; e < 8; ++e) o[e] = 0.f;
     }
     h16x8 hi, lo;
+    bool over = false;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const _Float16 h = (_Float16)o[j];
       hi[j] = h;
       lo[j] = (_Float16)((o[j] - (float)h) * 2048.0f);
+      over |= fabsf(o[j]) >= 65504.f && fabsf(o[j]) < __builtin_inff();
     }
+    // range guard of the conv -> conv hand-over: a finite activation the f16 split cannot hold
+    // (a BatchNorm affine far outside any trained range) is reported to the host (pinned word),
+    // and the next call on the context fails with AVC_ERR_DEVICE
+    if (over && range_flag) __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const long blk = ((r >> 5) * nkc + (g8 >> 1)) * 2;
     const int lane = (int)(r & 31) + 32 * (g8 & 1);
     *reinterpret_cast<h16x8*>(frag + blk * 512 + lane * 8) = hi;
@@ -555,7 +569,7 @@ int bn_finalize(int C, int nparts, const float* stats, double count, int trainin
 
 int bn_apply(long M, int C, const float* y, const float* mean, const float* invstd,
              const float* gamma, const float* beta, int act, const float* residual, float* out,
-             hipStream_t s, _Float16* frag) {
+             hipStream_t s, _Float16* frag, unsigned* range_flag) {
   AVC_CHECK_ARG(C % 4 == 0, "bn_apply: channels must be a multiple of 4");
   if (frag) {
     AVC_CHECK_ARG(C % 8 == 0, "bn_apply: the split output needs channels in multiples of 8");
@@ -563,7 +577,7 @@ int bn_apply(long M, int C, const float* y, const float* mean, const float* invs
     const long ntile = (M + 31) / 32;
     const long total = ntile * 32 * nkc * 2;
     bn_apply_frag_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(
-        M, C, nkc, ntile, y, mean, invstd, gamma, beta, act, residual, out, frag);
+        M, C, nkc, ntile, y, mean, invstd, gamma, beta, act, residual, out, frag, range_flag);
     AVC_LAUNCH_CHECK();
     return AVC_OK;
   }
@@ -571,7 +585,7 @@ int bn_apply(long M, int C, const float* y, const float* mean, const float* invs
   const long Q = C / 4;
   const long threads = std::max<long>(256, std::min<long>(M * Q / 4, 2048L * 256));
   const long blocks = (threads + 255) / 256;
-  bn_apply_kernel<<<(int)blocks, 256, 0, s>>>(M, C, y, mean, invstd, gamma, beta, act, residual, out);
+  bn_apply_kernel<<<(int)blocks, 256, 0, s>>>(M, C, y, mean, invstd, gamma, beta, act, residual, out, range_flag);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

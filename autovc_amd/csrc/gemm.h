@@ -24,13 +24,17 @@ struct GemmDesc {
   int nz = 1; long a_zoff = 0; long c_zoff = 0;
   float* C = nullptr; long ldc = 0; long ldc_col = 1; int accumulate = 0;
   const float* bias0 = nullptr; const float* bias1 = nullptr; int act = AVC_ACT_NONE;
-  int prec16 = 0;           // 1: split-fp16 ("3xf16") MFMA kernel (forward operands: |x| < 65504)
+  int prec16 = 0;           // 1: split-fp16 ("3xf16") MFMA kernel; forward products are range-
+                            // guarded: an operand whose max |x| reaches 2^15 is scaled down by a
+                            // power of two before splitting (scale 1, bit-identical, otherwise)
+  float a_bound = 0.f;      // forward: host-known bound on |A| (an LSTM's h: 1); < 2^15 skips the scan
   int split_scale = 0;      // with prec16: scale each operand by a power of two from its device-side
                             // max |x| before splitting (gradients: any magnitude), unscale exactly
   const unsigned* amax_a = nullptr;  // max |A| as float bits (device); preset by the caller to
                                      // share one scan between products, else filled by gemm_run
   const unsigned* amax_b = nullptr;  // max |B| (filled by gemm_run)
-  const _Float16* b_frag = nullptr;  // optional B already split by gemm_prepare_bfrag (prec16 only)
+  const _Float16* b_frag = nullptr;  // optional B already split by gemm_prepare_bfrag (prec16 only;
+                                     // carries its range-guard word, see gemm_prepare_bfrag)
   const _Float16* a_frag = nullptr;  // optional A already split (row-major A, unscaled forward
                                      // products only): gemm_afrag_bytes(a_rows, Kc) bytes in the
                                      // layout split_frag32_kernel writes (e.g. by bn_apply's frag)
@@ -45,7 +49,8 @@ int gemm_stats_rows(int M, int N);
 // Scratch bytes gemm_run may take for this problem.
 size_t gemm_scratch_bytes(const GemmDesc& d);
 // B operand of a forward (prec16) product split once into the fragment-major layout the
-// split-f16 kernel streams (all taps); pass it back as GemmDesc::b_frag to skip the per-call split.
+// split-f16 kernel streams (all taps), range-guarded (its guard word trails the fragments); pass
+// it back as GemmDesc::b_frag to skip the per-call split.
 size_t gemm_bfrag_bytes(const GemmDesc& d);
 int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream);
 // bytes of a row-major [rows][K] operand in the fragment-major split layout (GemmDesc::a_frag)

@@ -315,8 +315,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
 // Kahan-added into the running sum (the same compensation the fp32 kernel uses), and the two
 // cross terms hi.lo + lo.hi into a separate fp32 accumulator scaled by 2^11.  3 f16 products run
 // 5.3x faster than one fp32 MFMA; the error matches the compensated fp32 kernel.
-// Activations and weights only: |x| must stay below the f16 range (65504) — backward products
-// (tiny gradients) stay on the fp32 kernel.
+// Forward operands are range-guarded like the pre-split path below (amax_a / amax_b guard words,
+// scale exactly 1 in the normal range).
 //
 // Block: NT = 64*WM*WN threads; each thread stages one octet (8 consecutive k) of A and of B
 // per 32-deep K-tile.  LDS holds MFMA fragment images: [tile32][ksub16][hi|lo][64 lanes][16 B],
@@ -376,6 +376,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
   const int b_slot = ((bc >> 5) * 2 + (boct >> 1)) * 2048 + ((bc & 31) + 32 * (boct & 1)) * 16;
 
   float va[8], vb[8];
+  // range guard (forward products, see guard_init_kernel): exactly 1 unless max |x| >= 2^15
+  const float sa = split_scale_of(d.amax_a), sb = split_scale_of(d.amax_b);
 #define AVC16_LOAD(KT)                                                                           \
   {                                                                                              \
     const int tau = (KT) / kt_per_tap;                                                           \
@@ -413,6 +415,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
     unsigned char* Ai = lds + (BUF) * (AIMG + BIMG);                                             \
     unsigned char* Bi = Ai + AIMG;                                                               \
     f16x8 hi, lo;                                                                                \
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) { va[j] *= sa; vb[j] *= sb; }                  \
     split8(va, hi, lo);                                                                          \
     *reinterpret_cast<f16x8*>(Ai + a_slot) = hi;                                                 \
     *reinterpret_cast<f16x8*>(Ai + a_slot + 1024) = lo;                                          \
@@ -487,6 +490,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = (acc[i][j][e] - cmp[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
+  if (d.split_scale && nsplit == 1) {  // split-K partials stay scaled; splitk_reduce_kernel unscales
+    const float us = split_unscale(d.amax_a, d.amax_b);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] *= us;
+  }
 
   // ---- epilogue (32x32 C layout: col = lane&31, row = (e&3) + 8(e>>2) + 4(lane>>5)) --------
   const int row_base = tm * BM + wm * WTM + 4 * (lane >> 5);
@@ -1078,7 +1090,75 @@ int gemm_stats_rows(int M, int N) {
   return make_plan(d, 1).bm;
 }
 
-size_t gemm_bfrag_bytes(const GemmDesc& d) { return (size_t)d.ntaps * frag_bytes(d.N, d.Kc); }
+size_t gemm_bfrag_bytes(const GemmDesc& d) { return (size_t)d.ntaps * frag_bytes(d.N, d.Kc) + 256; }
+
+namespace {
+// the range-guard word behind a prepared B operand's fragments
+unsigned* bfrag_guard_word(const GemmDesc& d, const _Float16* bf) {
+  return reinterpret_cast<unsigned*>(const_cast<char*>(reinterpret_cast<const char*>(bf)) +
+                                     (size_t)d.ntaps * frag_bytes(d.N, d.Kc));
+}
+
+// max |B| over all taps of a forward product's B operand into a guard word
+void absmax_b(const GemmDesc& d, unsigned* w, hipStream_t s) {
+  const long b_rows = d.b_rows ? d.b_rows : (d.b_trans ? d.N : d.Kc);
+  const long kb = d.b_trans ? d.Kc : std::min<long>(d.Kc, b_rows);
+  for (int tau = 0; tau < d.ntaps; ++tau) {
+    if (d.b_trans) absmax2d(d.B + (long)tau * d.b_tapoff, d.N, kb, d.ldb, w, s);
+    else absmax2d(d.B + (long)tau * d.b_tapoff, kb, d.N, d.ldb, w, s);
+  }
+}
+}  // namespace
+
+// Range guard of the forward split: a guard word starts at 2^14 and takes the
+// operand's max |x| (atomicMax on float bits), so split_scale_of() returns exactly 1 unless
+// max |x| >= 2^15, and otherwise the power of two that brings it into [2^14, 2^15): overflow-free
+// splits for any magnitude, bit-identical results in the normal range.
+__global__ void guard_init_kernel(unsigned* w, int n) {
+  if ((int)threadIdx.x < n) w[threadIdx.x] = 0x46800000u;  // 16384.0f
+}
+
+// The same guard word in ONE launch (no initialisation kernel): every block writes its maximum
+// to partial[blockIdx], and the last block to take a ticket (atomicInc wraps the per-context
+// ticket back to 0, so it is ready for the next scan) writes max(all, 2^14) to *out.
+constexpr int kGuardBlocks = 256;
+__global__ __launch_bounds__(256) void guard_scan_kernel(const float* __restrict__ src, long rows, int cols,
+                                                         long ld, float* __restrict__ partial,
+                                                         unsigned* __restrict__ ticket, unsigned* __restrict__ out) {
+  __shared__ float red[4];
+  __shared__ bool last;
+  float m = 0.f;
+  if (ld == cols && (reinterpret_cast<uintptr_t>(src) & 15) == 0 && (cols & 3) == 0) {
+    const long n4 = rows * cols / 4;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+      const float4 v = s4[i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  } else {
+    for (long r = blockIdx.x; r < rows; r += gridDim.x)
+      for (int c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, fabsf(src[r * ld + c]));
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(partial + blockIdx.x, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    last = atomicInc(ticket, gridDim.x - 1) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  float v = 16384.f;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += 256)
+    v = fmaxf(v, __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
 
 int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
   const long b_ntile = frag_ntile(d.N);
@@ -1086,10 +1166,13 @@ int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
   const long tapstride = b_ntile * nkc * 1024;  // halves
   const long tb = b_ntile * 32 * nkc * 2;
   const long b_rows = d.b_rows ? d.b_rows : (d.b_trans ? d.N : d.Kc);
+  unsigned* guard = bfrag_guard_word(d, dst);
+  guard_init_kernel<<<1, 64, 0, stream>>>(guard, 1);
+  absmax_b(d, guard, stream);
   for (int tau = 0; tau < d.ntaps; ++tau)
     split_frag32_kernel<<<(int)std::min<long>((tb + 255) / 256, 8192), 256, 0, stream>>>(
         d.B + (long)tau * d.b_tapoff, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N,
-        d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows), (int)b_ntile, nkc, dst + tau * tapstride);
+        d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows), (int)b_ntile, nkc, dst + tau * tapstride, guard);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
@@ -1110,6 +1193,28 @@ size_t gemm_scratch_bytes(const GemmDesc& d) {
   if (d.prec16) s += frag16_scratch(d);
   return s;
 }
+
+namespace {
+int guard_scan(avc_context* ctx, const float* src, long rows, long cols, long ld, float* part, unsigned* out,
+               hipStream_t s) {
+  if (!ctx->guard_ticket) {  // first use happens eagerly (graphs are captured on a later call)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    AVC_HIP(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone) {
+      set_error("range guard: ticket not allocated before graph capture");
+      return AVC_ERR_WORKSPACE;
+    }
+    AVC_HIP(hipMalloc(&ctx->guard_ticket, 256));
+    AVC_HIP(hipMemsetAsync(ctx->guard_ticket, 0, 256, s));
+    AVC_HIP(hipStreamSynchronize(s));
+  }
+  const long n4 = rows * cols / 4;
+  const int blocks = (int)std::max<long>(1, std::min<long>((n4 + 1023) / 1024, kGuardBlocks));
+  guard_scan_kernel<<<blocks, 256, 0, s>>>(src, rows, (int)cols, ld, part, ctx->guard_ticket, out);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+}  // namespace
 
 int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) {
   AVC_CHECK_ARG(d.M > 0 && d.N > 0 && d.Kc > 0 && d.ntaps > 0 && d.nz > 0, "gemm: empty problem");
@@ -1138,9 +1243,30 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     d.split_scale = 0;
     d.amax_a = d.amax_b = nullptr;
   }
+  if (frag && !scaled_product) {
+    // forward product: range guard (see guard_init_kernel).  B from gemm_prepare_bfrag carries
+    // its guard word; an A handed over pre-split (bn_apply's fragment output) was range-checked
+    // by its producer; every other operand is scanned here unless its bound is known.
+    unsigned* gw = sc.take<unsigned>(64);
+    float* part = sc.take<float>(kGuardBlocks);
+    if (!gw || !part) return AVC_ERR_WORKSPACE;
+    d.amax_a = nullptr;
+    if (!d.a_frag && !(d.a_bound > 0.f && d.a_bound < 32768.f) && !range_checked(ctx, d.A)) {
+      AVC_TRY(guard_scan(ctx, d.A, d.a_rows, d.Kc, d.lda, part, gw, stream));
+      d.amax_a = gw;
+    }
+    if (d.b_frag) {
+      d.amax_b = bfrag_guard_word(d, d.b_frag);
+    } else {
+      guard_init_kernel<<<1, 64, 0, stream>>>(gw + 1, 1);
+      absmax_b(d, gw + 1, stream);
+      d.amax_b = gw + 1;
+    }
+    d.split_scale = 1;  // the epilogue unscales by 1 / (scale_a * scale_b): exactly 1 in range
+  }
   if (frag) {
     // split both operands once into the fragment-major layout gemm16f_kernel streams
-    if (d.split_scale) {  // power-of-two operand scales from max |A|, max |B| (device side)
+    if (scaled_product) {  // power-of-two operand scales from max |A|, max |B| (device side)
       unsigned* amax = sc.take<unsigned>(64);
       if (!amax) return AVC_ERR_WORKSPACE;
       AVC_TRY(zero_async(amax, 2 * sizeof(unsigned), stream));
@@ -1163,7 +1289,7 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     const long b_krows = frag16_b_krows(d);
     const int b_nkc = frag_nkc((int)b_krows);
     const _Float16* as = d.a_frag;
-    if (!as || d.split_scale || d.a_trans) {
+    if (!as || scaled_product || d.a_trans) {
       _Float16* at = sc.take<_Float16>(frag_bytes(a_src_rows, d.Kc) / 2);
       if (!at) return AVC_ERR_WORKSPACE;
       const long ta = a_ntile * 32 * nkc * 2;
@@ -1172,7 +1298,7 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
       as = at;
     }
     const long tapstride = b_ntile * b_nkc * 1024;  // halves
-    const _Float16* bs = d.split_scale ? nullptr : d.b_frag;
+    const _Float16* bs = scaled_product ? nullptr : d.b_frag;
     if (!bs) {
       _Float16* tmp = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, (int)b_krows) / 2);
       if (!tmp) return AVC_ERR_WORKSPACE;
@@ -1189,11 +1315,26 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     fa.Bs = bs; fa.b_ntile = (int)b_ntile; fa.b_nkc = b_nkc; fa.b_tapstride = tapstride;
     fa.b_shift0_c = (int)(d.b_shift0 / 16); fa.b_zshift_c = (int)(d.b_zshift / 16);
   }
+  const bool staged16 = !frag && d.prec16 && !scaled_product && !d.a_trans && g_gemm16;
+  if (staged16) {  // forward product on the staged-split kernel: the same range guard
+    unsigned* gw = sc.take<unsigned>(64);
+    float* part = sc.take<float>(kGuardBlocks);
+    if (!gw || !part) return AVC_ERR_WORKSPACE;
+    d.amax_a = nullptr;
+    if (!(d.a_bound > 0.f && d.a_bound < 32768.f) && !range_checked(ctx, d.A)) {
+      AVC_TRY(guard_scan(ctx, d.A, d.a_rows, d.Kc, d.lda, part, gw, stream));
+      d.amax_a = gw;
+    }
+    guard_init_kernel<<<1, 64, 0, stream>>>(gw + 1, 1);
+    absmax_b(d, gw + 1, stream);
+    d.amax_b = gw + 1;
+    d.split_scale = 1;
+  }
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
   if (frag) {
     if (p.bm == 128) launch16f_128(d, fa, p, slab, stream);
     else launch16f_cfg<64, 64, 2, 2, 4, 2>(d, fa, p, slab, stream);
-  } else if (d.prec16 && !scaled_product && !d.a_trans && g_gemm16) {
+  } else if (staged16) {
     if (p.bm == 128) launch16<128, 128, 4, 2>(d, p, slab, stream);
     else launch16<64, 64, 2, 2>(d, p, slab, stream);
   } else if (p.bm == 128) {

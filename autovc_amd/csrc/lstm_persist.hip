@@ -628,11 +628,28 @@ void set_region_args(PersistArgs& a, avc_context* ctx, unsigned* region) {
 
 }  // namespace
 
-int persist_guard(avc_context* ctx) {
+unsigned* host_flags(avc_context* ctx) {
   if (!ctx->fail_host) {
-    AVC_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->fail_host), 256, hipHostMallocDefault));
-    *ctx->fail_host = 0;
+    void* p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, 256, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      set_error(std::string("hipHostMalloc of the context's health words: ") + hipGetErrorString(e));
+      return nullptr;
+    }
+    ctx->fail_host = static_cast<unsigned*>(p);
+    ctx->fail_host[0] = ctx->fail_host[1] = 0;
     ctx->fail_seen = 0;
+  }
+  return ctx->fail_host;
+}
+
+int persist_guard(avc_context* ctx) {
+  if (!host_flags(ctx)) return AVC_ERR_HIP;
+  if (__atomic_exchange_n(ctx->fail_host + 1, 0u, __ATOMIC_ACQ_REL) != 0) {
+    set_error("a forward activation handed from one convolution to the next exceeded the split-f16 "
+              "operand range (|x| >= 65504) in an earlier call on this context; that call's outputs are "
+              "not valid (inf/NaN)");
+    return AVC_ERR_DEVICE;
   }
   const unsigned v = __atomic_load_n(ctx->fail_host, __ATOMIC_ACQUIRE);
   if (v == ctx->fail_seen) return AVC_OK;

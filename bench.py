@@ -59,6 +59,9 @@ ROOFLINE = {
            "dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS)},
 }
 MEL_SECONDS, SE_SECONDS = 60, 10
+# fp32 storage and accumulation; contractions as 3 f16 MFMA products of hi/lo-split operands
+# (22 significant bits per operand, range-guarded), DESIGN.md §3
+DTYPE = "f32 (3xf16 split, fp32 accumulate)"
 METRIC = "mel-frames/sec/GPU AutoVC fwd, 80×128 batch; max|Δmel| vs ref"
 
 
@@ -293,7 +296,7 @@ def setup_generator(args, dev, rank):
                 "convert_call": conv}
 
     return {
-        "step": step, "units_per_step": B * T, "unit": "mel-frames/s", "dtype": "f32",
+        "step": step, "units_per_step": B * T, "unit": "mel-frames/s", "dtype": DTYPE,
         "metric": METRIC if fwd else "mel-frames/sec AutoVC train step, 80×128 batch",
         "data": "synthetic (U[0,1) mels, |N(0,1)| L2-normalised speaker embeddings; seeded synthetic weights)",
         "classes": ["gemm", "lstm_step_fwd", "lstm32", "lstm2_persist", "lstm1_persist"] + ([] if fwd else ["lstm_step_bwd"]),
@@ -369,7 +372,7 @@ def setup_long(args, dev, rank):
                            f"{torch.get_num_threads()} torch threads"}, {})
 
     return {
-        "step": step, "units_per_step": valid, "unit": "mel-frames/s", "dtype": "f32",
+        "step": step, "units_per_step": valid, "unit": "mel-frames/s", "dtype": DTYPE,
         "metric": "mel-frames/sec AutoVC long-form fwd (C5: ragged lengths <= 1024, zero-padded)",
         "data": "synthetic (U[0,1) mels zero-padded past each length, |N(0,1)| L2-normalised embeddings; "
                 "seeded synthetic weights)",

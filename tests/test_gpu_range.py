@@ -1,0 +1,86 @@
+"""Range guard of the forward 3xf16 split.
+
+Every forward contraction splits its fp32 operands into hi/lo f16 halves.  An operand whose
+max |x| reaches 2^15 is scaled down by a power of two before splitting (weights once per weights
+version, inputs and fp32 activations per call) and the product is unscaled exactly; in the normal
+range the scale is exactly 1, so ordinary results are bit-identical to the unguarded kernels.  The
+conv -> conv hand-overs of the fused forward are split by their producer (bn_apply's fragment
+output) and are range-checked there: a value beyond the split's range makes the next call fail.
+
+Tolerance: these inputs are far outside the 1e-4 absolute bar's scale (mels ~1e5), so parity is
+stated relative to the output's magnitude: max|d| <= 1e-4 * max|ref| per output."""
+import numpy as np
+import pytest
+import torch
+
+from autovc_amd.auto_encoder import AutoEncoder
+from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(B=16, T=64):
+    x = synthetic_mel(51, B, T) * 1e5  # un-normalised "mels" beyond the f16 range
+    return x, synthetic_embedding(52, B), synthetic_embedding(53, B)
+
+
+def _scaled_sd():
+    sd = torch_state_dict(0)
+    sd["decoder.linear_projection.linear_layer.weight"] = sd["decoder.linear_projection.linear_layer.weight"] * 1e6
+    sd["encoder.convolutions.0.0.conv.weight"] = sd["encoder.convolutions.0.0.conv.weight"] * 1e3
+    return sd
+
+
+def _oracle(sd, x, co, ct, train=True):
+    from oracle import autovc_oracle as orc
+    bufs = {k: v.clone() for k, v in sd.items() if "running" in k or "num_batches" in k}
+    with torch.no_grad():
+        return orc.forward(sd, torch.from_numpy(x), torch.from_numpy(co), torch.from_numpy(ct), train, bufs)
+
+
+@pytest.mark.parametrize("path", ["fused", "layers"])
+def test_out_of_range_inputs_and_weights(cuda_device, path):
+    sd = _scaled_sd()
+    x, co, ct = _case()
+    ref = _oracle(sd, x, co, ct)
+    assert float(ref[0].abs().max()) > 65504  # the decoder output itself is beyond f16
+    ae = AutoEncoder(device=cuda_device, verbose=False)
+    ae.load_state_dict(sd)
+    ae.to(cuda_device).train()
+    ae.fused_autograd = path == "fused"
+    xs = [torch.from_numpy(a).to(cuda_device) for a in (x, co, ct)]
+    with torch.set_grad_enabled(path == "layers"):
+        outs = ae(*xs)
+    torch.cuda.synchronize()
+    for name, o, r in zip(("mel", "mel_post", "codes"), outs, ref):
+        o = o.detach().cpu()
+        assert torch.isfinite(o).all(), name
+        rel = float((o - r).abs().max()) / float(r.abs().max())
+        print(f"{path} {name}: max|ref| {float(r.abs().max()):.3e}, max|d|/max|ref| {rel:.2e}")
+        assert rel <= 1e-4, name
+    ae.check_health()
+
+
+def test_fused_handover_beyond_range_raises(cuda_device):
+    """A BatchNorm gamma of 1e6 makes decoder conv 0's output exceed the split range inside the
+    fused forward's conv -> conv hand-over: the next call reports it.  The per-layer path splits
+    the same fp32 activation with a guard scale instead and stays correct."""
+    sd = torch_state_dict(0)
+    sd["decoder.convolutions.0.1.weight"] = sd["decoder.convolutions.0.1.weight"] * 1e6
+    x, co, ct = _case(B=32)  # conv -> conv hand-overs need whole 32-row tap shifts
+    x = x / 1e5
+    ae = AutoEncoder(device=cuda_device, verbose=False)
+    ae.load_state_dict(sd)
+    ae.to(cuda_device).train()
+    xs = [torch.from_numpy(a).to(cuda_device) for a in (x, co, ct)]
+    with torch.no_grad():
+        ae(*xs)
+        with pytest.raises(RuntimeError, match="split-f16 operand range"):
+            ae(*xs)
+        ae.fused_autograd = False
+    outs = ae(*xs)  # grad enabled, per-layer path
+    ref = _oracle(sd, x, co, ct)
+    for name, o, r in zip(("mel", "mel_post", "codes"), outs, ref):
+        rel = float((o.detach().cpu() - r).abs().max()) / max(float(r.abs().max()), 1e-30)
+        print(f"layers, gamma x1e6: {name} max|d|/max|ref| {rel:.2e}")
+        assert rel <= 1e-4, name
