@@ -221,19 +221,24 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       *reinterpret_cast<u32x4*>(wl + ((w * NCH + c) * 2 + hl) * 1024 + lane * 16) = v;
     }
 
-  // ---- epilogue ownership: thread tid handles (row, blk) = (tid / 4, tid % 4) -------------
-  const bool epi = tid < NPAIR;
-  const int row = min(tid, NPAIR - 1) / NC, blk = min(tid, NPAIR - 1) % NC;
+  // ---- epilogue ownership: every thread owns UPT = RT hidden units of one (row, 16-column
+  // block) pair: tid -> pair tid / SUB, units u0 .. u0 + UPT - 1 of the block's 4 (the gate
+  // math of a step is spread over all 256 threads whatever the batch tile)
+  constexpr int UPT = RT, SUB = 4 / UPT;
+  static_assert(NPAIR * SUB == 256, "one epilogue slot per thread");
+  const int pair = tid / SUB, sub = tid % SUB, u0 = sub * UPT;
+  const int row = pair / NC, blk = pair % NC;
   const int b = grp * MB + row;
-  const bool live = epi && b < B;
+  const bool live = b < B;
   const int bc = min(b, B - 1);
-  const int p0 = cb * TW + blk * 16;   // first permuted gate column of the pair
-  const int j0 = cb * 4 * NC + blk * 4;  // first hidden unit
+  const int p0 = cb * TW + blk * 16;       // first permuted gate column of the pair
+  const int j0 = cb * 4 * NC + blk * 4;    // first hidden unit of the pair
+  typedef float fu __attribute__((ext_vector_type(UPT)));
   if (tid < TW) {  // published to the epilogue by the first step's barriers
     cpar[tid] = a.winv[L][cb * TW + tid];
     if (L == 1) cpar[TW + tid] = a.b1[cb * TW + tid];
   }
-  f32x4 cst = f32x4{0.f, 0.f, 0.f, 0.f};
+  fu cst = fu{};
   // slot 1 stores gx1 in whole lines: lane -> (row 4i + lane/16 of the wave's 16, columns 4*pc..)
   const int pc = lane & 15;
   float* c_save = L == 0 ? a.c0 : a.c1;
@@ -288,13 +293,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     // The epilogue operands (gx0 / b1 / the gx1 hand-off) are loaded right after the LAST h
     // chunk's loads: vmcnt retires in issue order, so loads issued ahead of the h chunks would
     // hold every MFMA until they land.
-    f32x4 gxv[4];
-    const float* gxr = L == 0 ? a.gx0 + ((long)t * B + bc) * G4 + p0 : a.b1 + p0;
+    fu gxv[4];
+    const float* gxr = L == 0 ? a.gx0 + ((long)t * B + bc) * G4 + p0 + u0 : a.b1 + p0 + u0;
     auto load_gx = [&]() {
 #ifdef AVC_STAMPS
       if ((a.diag & 1) && L == 2) {  // timing experiment: skip the gx1 hand-off loads
 #pragma unroll
-        for (int g = 0; g < 4; ++g) gxv[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int g = 0; g < 4; ++g) gxv[g] = fu{};
         return;
       }
 #endif
@@ -302,13 +307,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         // descriptor base uniform (the slab), lane offset in the VGPR: a per-lane base would make
         // hipcc wrap each load in a waterfall loop over the 64 distinct descriptors (~10 us/step)
         const auto grs = __builtin_amdgcn_make_buffer_rsrc(a.gx1 + gx1_slab(t, cb), 0, 64 * TW * 4, 0x00020000);
-        const int vo = (bc * TW + blk * 16) * 4;
+        const int vo = (bc * TW + blk * 16 + u0) * 4;
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          gxv[g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(grs, vo + 16 * g, 0, HO ? 16 : 0));
+        for (int g = 0; g < 4; ++g) {
+          if constexpr (UPT == 4) {
+            gxv[g] = __builtin_bit_cast(fu, __builtin_amdgcn_raw_buffer_load_b128(grs, vo + 16 * g, 0, HO ? 16 : 0));
+          } else {  // 4-B sc1 loads (an 8-B sc1 load is not a validated hand-off form)
+#pragma unroll
+            for (int uu = 0; uu < UPT; ++uu)
+              gxv[g][uu] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, vo + 16 * g + 4 * uu, 0, HO ? 16 : 0));
+          }
+        }
       } else {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) gxv[g] = *reinterpret_cast<const f32x4*>(gxr + 4 * g);
+        for (int g = 0; g < 4; ++g) gxv[g] = *reinterpret_cast<const fu*>(gxr + 4 * g);
       }
     };
     f32x4 acc[RT][NC];
@@ -326,7 +338,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       const long hbase = (long)grp * RT * hrow16 + (long)kc0 * 2048;
       const auto hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(src) + hbase, 0,
                                                          (int)((long)a.ntile * nck * 2048 - hbase), 0x00020000);
-      constexpr int NB = PD + 1;  // h chunk buffers: PD chunks in flight ahead of the MFMAs
+      // h chunk buffers: PDX chunks in flight ahead of the MFMAs.  With one 16-row tile (the
+      // one-layer form's batch groups) a chunk is only 8 VGPRs, so every chunk of the wave's K
+      // quarter is requested at once: one load round trip per step instead of NCH / PD
+      constexpr int PDX = RT == 1 ? NCH : PD;
+      constexpr int NB = PDX + 1;
       f16x8 hb[NB][RT][2], wt[2];
 #ifdef AVC_STAMPS
 #define AVC_PLD_SKIP (a.diag & 4)  // timing experiment: no h loads (zeros)
@@ -370,13 +386,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   }
 #endif
 #pragma unroll
-      for (int c = 0; c < PD && c < NCH; ++c) { AVC_PLD(hb[c], c) }
-      if constexpr (NCH <= PD) load_gx();
+      for (int c = 0; c < PDX && c < NCH; ++c) { AVC_PLD(hb[c], c) }
+      if constexpr (NCH <= PDX) load_gx();
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        if (c + PD < NCH) {
-          AVC_PLD(hb[(c + PD) % NB], c + PD)
-          if (c + PD == NCH - 1) load_gx();
+        if (c + PDX < NCH) {
+          AVC_PLD(hb[(c + PDX) % NB], c + PDX)
+          if (c + PDX == NCH - 1) load_gx();
         }
         __builtin_amdgcn_sched_barrier(0);
         AVC_PMFMA(hb[c % NB], c)
@@ -397,7 +413,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e];
     __syncthreads();
-    f32x4 hv, ig, fg, gg, og;
+    fu hv, ig, fg, gg, og;
     if (L == 1) {
       // projection slot: the same fixed-order sum, scale and bias per 4 columns, stored to this
       // (step, column block)'s contiguous 16 KB slab as whole 128-B lines (a wave instruction
@@ -419,47 +435,59 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         }
       }
     } else {
-      f32x4 sum[4];
+      fu sum[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int off = row * RP + blk * 16 + 4 * g;
-        f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
+        const int off = row * RP + blk * 16 + 4 * g + u0;
+        fu v = *reinterpret_cast<const fu*>(part + off);
 #pragma unroll
-        for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * MB * RP + off);
+        for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const fu*>(part + ww * MB * RP + off);
         sum[g] = v;
       }
       AVC_PSTAMP(4);
       // ---- gate epilogue; only the split h (the hand-off) is stored before publishing ------
+      unsigned hl[UPT] = {};  // split h of this thread's units: f16 hi | f16 lo << 16
       if (live) {
-        f32x4 wiv[4];
+        fu wiv[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) wiv[g] = *reinterpret_cast<const f32x4*>(cpar + blk * 16 + 4 * g);
-        const f32x4 zi = sum[0] * wiv[0] + gxv[0];
-        const f32x4 zf = sum[1] * wiv[1] + gxv[1];
-        const f32x4 zg = sum[2] * wiv[2] + gxv[2];
-        const f32x4 zo = sum[3] * wiv[3] + gxv[3];
+        for (int g = 0; g < 4; ++g) wiv[g] = *reinterpret_cast<const fu*>(cpar + blk * 16 + 4 * g + u0);
+        const fu zi = sum[0] * wiv[0] + gxv[0];
+        const fu zf = sum[1] * wiv[1] + gxv[1];
+        const fu zg = sum[2] * wiv[2] + gxv[2];
+        const fu zo = sum[3] * wiv[3] + gxv[3];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < UPT; ++u) {
           ig[u] = sigmoidf_(zi[u]);
           fg[u] = sigmoidf_(zf[u]);
           gg[u] = tanhf(zg[u]);
           og[u] = sigmoidf_(zo[u]);
           cst[u] = fg[u] * cst[u] + ig[u] * gg[u];
           hv[u] = og[u] * tanhf(cst[u]);
+          const float v = hv[u] * kHScale;
+          const _Float16 hi = (_Float16)v;
+          const _Float16 lo = (_Float16)(v - (float)hi);
+          hl[u] = (unsigned)__builtin_bit_cast(unsigned short, hi) |
+                  ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
         }
-        if (t + 1 < T || L == 0) {
-          f16x4 hi, lo;
+      }
+      if (t + 1 < T || L == 0) {
+        // the pair's 4 units go out as one 8-B hi and one 8-B lo store (whole fragment rows) from
+        // its first thread; the other SUB - 1 threads hand their units over by lane shuffles
+        unsigned q[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float v = hv[u] * kHScale;
-            hi[u] = (_Float16)v;
-            lo[u] = (_Float16)(v - (float)hi[u]);
-          }
+        for (int u = 0; u < UPT; ++u) q[u] = hl[u];
+#pragma unroll
+        for (int k = 1; k < SUB; ++k)
+#pragma unroll
+          for (int u = 0; u < UPT; ++u) q[k * UPT + u] = __shfl_down(hl[u], k);
+        if (live && sub == 0) {
+          const u32x2 hi2 = {(q[0] & 0xffffu) | (q[1] << 16), (q[2] & 0xffffu) | (q[3] << 16)};
+          const u32x2 lo2 = {(q[0] >> 16) | (q[1] & 0xffff0000u), (q[2] >> 16) | (q[3] & 0xffff0000u)};
           const long off = ((long)(b >> 4) * nck + (j0 >> 5)) * 2048 + (((b & 15) + 16 * ((j0 & 31) >> 3)) * 8 + (j0 & 7)) * 2;
           unsigned char* hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
           const auto ors = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)a.hsz, 0x00020000);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hi), ors, (int)off, 0, 16 /*sc1*/);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lo), ors, (int)off + 1024, 0, 16 /*sc1*/);
+          __builtin_amdgcn_raw_buffer_store_b64(hi2, ors, (int)off, 0, 16 /*sc1*/);
+          __builtin_amdgcn_raw_buffer_store_b64(lo2, ors, (int)off + 1024, 0, 16 /*sc1*/);
         }
       }
     }
@@ -473,29 +501,30 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
                              __HIP_MEMORY_SCOPE_AGENT);
     // outputs nobody reads inside this launch: stored after publishing (off the hand-off path)
     if (L != 1 && live) {
-      *reinterpret_cast<f32x4*>(y_out + ((long)t * B + b) * H + j0) = hv;
-      if (c_save) *reinterpret_cast<f32x4*>(c_save + ((long)t * B + b) * H + j0) = cst;
+      *reinterpret_cast<fu*>(y_out + ((long)t * B + b) * H + j0 + u0) = hv;
+      if (c_save) *reinterpret_cast<fu*>(c_save + ((long)t * B + b) * H + j0 + u0) = cst;
       if (g_save) {
-        float* go = g_save + ((long)t * B + b) * G4 + p0;
-        *reinterpret_cast<f32x4*>(go) = ig;
-        *reinterpret_cast<f32x4*>(go + 4) = fg;
-        *reinterpret_cast<f32x4*>(go + 8) = gg;
-        *reinterpret_cast<f32x4*>(go + 12) = og;
+        float* go = g_save + ((long)t * B + b) * G4 + p0 + u0;
+        *reinterpret_cast<fu*>(go) = ig;
+        *reinterpret_cast<fu*>(go + 4) = fg;
+        *reinterpret_cast<fu*>(go + 8) = gg;
+        *reinterpret_cast<fu*>(go + 12) = og;
       }
     }
   }
   // gave up at step t: the rows this workgroup owns for steps t..T-1 are written as NaN, so a
   // timed-out launch never hands plausible numbers downstream (the host reports it, see above)
   if (t < T && L != 1 && live) {
-    const float qnan = __builtin_nanf("");
-    const f32x4 nv = f32x4{qnan, qnan, qnan, qnan};
-    for (int tt = t; tt < T; ++tt) {
-      *reinterpret_cast<f32x4*>(y_out + ((long)tt * B + b) * H + j0) = nv;
-      if (c_save) *reinterpret_cast<f32x4*>(c_save + ((long)tt * B + b) * H + j0) = nv;
-      if (g_save) {
-        float* go = g_save + ((long)tt * B + b) * G4 + p0;
+    fu nv;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4*>(go + 4 * g) = nv;
+    for (int u = 0; u < UPT; ++u) nv[u] = __builtin_nanf("");
+    for (int tt = t; tt < T; ++tt) {
+      *reinterpret_cast<fu*>(y_out + ((long)tt * B + b) * H + j0 + u0) = nv;
+      if (c_save) *reinterpret_cast<fu*>(c_save + ((long)tt * B + b) * H + j0 + u0) = nv;
+      if (g_save) {
+        float* go = g_save + ((long)tt * B + b) * G4 + p0 + u0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) *reinterpret_cast<fu*>(go + 4 * g) = nv;
       }
     }
   }
