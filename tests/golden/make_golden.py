@@ -90,6 +90,30 @@ def batch_forward_case(AE):
                 weights_checksum=np.array(ck))
 
 
+def c1_case(AE):
+    """BASELINE config 1 / SURVEY §8c: a (1, 80, 128) mel of data/samples/mette_183.wav through the
+    reference Generator on the CPU.  The mel comes from the float64 restatement of the reference's
+    librosa frontend (oracle/audio_oracle.py; librosa is absent, so that step is unpinned) applied
+    to the committed waveform head (tests/golden/mette_183_head.npz), first 128 frames; the
+    Generator outputs are the reference class's own.  Both BN modes."""
+    from oracle import audio_oracle as ao
+    head = np.load(os.path.join(HERE, "mette_183_head.npz"))
+    mel = ao.mel_spec_auto_encoder(head["wav"].astype(np.float64), sr=int(head["sr"]))[:, :128]
+    x = np.asarray(mel, dtype=np.float32)[None]
+    c_org = synthetic_embedding(301, 1)
+    c_trg = synthetic_embedding(302, 1)
+    d = dict(x=x, c_org=c_org, c_trg=c_trg, weights_checksum=np.array(0), seed=np.array(0))
+    for train in (True, False):
+        ae, ck = make_ae(AE)
+        ae.train(train)
+        with torch.no_grad():
+            mel_o, post, codes = ae(torch.from_numpy(x), torch.from_numpy(c_org), torch.from_numpy(c_trg))
+        tag = "train" if train else "eval"
+        d[f"mel_{tag}"], d[f"mel_post_{tag}"], d[f"codes_{tag}"] = mel_o.numpy(), post.numpy(), codes.numpy()
+        d["weights_checksum"] = np.array(ck)
+    return d
+
+
 TRACE_TENSORS = ["encoder.convolutions.0.0.conv.weight", "encoder.lstm.weight_hh_l0_reverse",
                  "decoder.lstm2.weight_hh_l1", "decoder.linear_projection.linear_layer.bias",
                  "postnet.convolutions.4.1.weight"]
@@ -208,6 +232,7 @@ def main():
         "fwd_b3_t33_train": lambda: fwd_case(AE, 3, 33, True, 4),
         "fwd_b2_t1024_ragged": lambda: fwd_case(AE, 2, 1024, True, 5, lengths=[1024, 700]),
         "batch_forward_m5_n128": lambda: batch_forward_case(AE),
+        "c1_mette_183_b1_t128": lambda: c1_case(AE),
         "train_b4_t128_3steps": lambda: train_case(AE, hparams),
     }
     only = sys.argv[1:]

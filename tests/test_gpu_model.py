@@ -356,3 +356,23 @@ def test_back_to_back_forwards_match(cuda_device):
     for i, k in enumerate(keep):
         for name, a, b in zip(("mel", "mel_post", "codes"), k, refs[i % 2]):
             assert torch.equal(a, b), f"call {i} {name}: max|d| {(a - b).abs().max().item():.3e}"
+
+
+@pytest.mark.parametrize("mode", ["train", "eval"])
+def test_c1_real_mel_end_to_end(cuda_device, mode):
+    """BASELINE config 1 on the GPU end to end: the GPU mel frontend on the committed head of
+    data/samples/mette_183.wav, first 128 frames, then the Generator; against the reference
+    Generator's outputs on the oracle frontend's mel (tests/golden/c1_mette_183_b1_t128.npz).
+    The frontend step itself is parity-unpinned (librosa absent); both stages are held to 1e-4."""
+    from autovc_amd.audio import spectrogram as sp
+    g = load_golden("c1_mette_183_b1_t128")
+    head = load_golden("mette_183_head")
+    x = sp.mel_spec_auto_encoder(head["wav"], device=cuda_device)[:, :128][None].contiguous()
+    assert np.abs(x.cpu().numpy() - g["x"]).max() <= TOL_MEL
+    ae = make_model(cuda_device, mode == "train")
+    with torch.no_grad():
+        mel, post, codes = ae(x, _t(g["c_org"], cuda_device), _t(g["c_trg"], cuda_device))
+    for name, got in (("mel", mel), ("mel_post", post), ("codes", codes)):
+        err = np.abs(got.cpu().numpy() - g[f"{name}_{mode}"]).max()
+        print(f"C1 {mode} {name}: max|d| = {err:.2e}")
+        assert err <= TOL_MEL, name

@@ -99,3 +99,21 @@ def test_known_answers():
     """Code length 32*(floor(T/32)+ceil(T/32)) and ValueError at T<32."""
     for T, n in [(128, 256), (100, 224), (33, 96), (1024, 2048)]:
         assert 32 * (T // 32 + -(-T // 32)) == n
+
+
+@pytest.mark.parametrize("mode", ["train", "eval"])
+def test_oracle_c1_real_mel(sd, mode):
+    """BASELINE config 1: the (1, 80, 128) mel of data/samples/mette_183.wav (oracle frontend on the
+    committed waveform head) through the reference Generator (tests/golden/make_golden.py c1_case)."""
+    from oracle import audio_oracle as ao
+    g = load_golden("c1_mette_183_b1_t128")
+    head = load_golden("mette_183_head")
+    mel_in = np.asarray(ao.mel_spec_auto_encoder(head["wav"].astype(np.float64), sr=int(head["sr"])))[:, :128]
+    np.testing.assert_array_equal(mel_in.astype(np.float32)[None], g["x"])
+    bufs = {k: v.clone() for k, v in sd.items() if "running" in k or "num_batches" in k}
+    with torch.no_grad():
+        mel, post, codes = orc.forward(sd, torch.from_numpy(g["x"]), torch.from_numpy(g["c_org"]),
+                                       torch.from_numpy(g["c_trg"]), mode == "train", bufs)
+    np.testing.assert_allclose(mel.numpy(), g[f"mel_{mode}"], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(post.numpy(), g[f"mel_post_{mode}"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(codes.numpy(), g[f"codes_{mode}"], rtol=0, atol=2e-6)
