@@ -77,6 +77,11 @@ _SIGS = {
     "avc_speaker_encoder_param_count": [],
     "avc_speaker_encoder_forward": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P],
     "avc_embedding_mean_normalize": [_I, _I, _P, _P, _P],
+    "avc_wavernn_param_count": [_I],
+    "avc_wavernn_upsample": [_P, _P, _I, _P, _P, _P, _P, _P],
+    "avc_wavernn_generate": [_P, _P, _I, _P, _P, _I, _I, _I, _I, ctypes.c_ulonglong, _P, _P, _P, _P, _P],
+    "avc_wavernn_fold_shape": [ctypes.c_long, _I, _I, _I, ctypes.POINTER(ctypes.c_long),
+                               ctypes.POINTER(ctypes.c_long)],
 }
 _RESTYPES = {"avc_last_error": ctypes.c_char_p}
 

@@ -1,0 +1,682 @@
+// WaveRNN vocoder `generate` (autovc/wavernn/model.py:214-329,
+// autovc/wavernn/distribution.py:87-123) on gfx950.
+//
+// The work splits into a parallel prologue and a strictly sequential sample loop:
+//   * up-sampling (model.py:34-93, eval-mode BN): MelResNet as frame-row kernels, the mel's
+//     Stretch2d + (1, 2s+1) smoothing as three stencil passes; the aux features stay at frame
+//     rate (the ×275 stretch is an index, never materialised), the fold into target + 2·overlap
+//     rows (model.py:296-339) is an index too;
+//   * the input layer's mel / aux part, which does not depend on the sampled signal, is
+//     contracted for every sample position up front (pI = W_I[:, 1:] · [m; a1] + b_I); per step
+//     only W_I[:, 0] · x_prev remains;
+//   * the loop: per sample step five dependent launches over every fold row at once — GRU1,
+//     GRU2, fc1, fc2, fc3 + sampling — captured into a hipGraph in chunks of kChunk steps and
+//     replayed.  The step index lives in device memory (the sampling kernel's last workgroup
+//     advances it), so one captured chunk serves every position.  Each step streams ~17 MB of
+//     weights, spread over 128-256 workgroups so that each pulls at most ~50 KB from its XCD's L2;
+//     with a stable block -> XCD placement an XCD keeps its eighth of the weights L2-resident
+//     across steps.  What bounds a step is the chain of five kernel boundaries (~1.3 us each,
+//     MI355X_MICROARCH.md 'boundary') plus each kernel's load -> reduce -> store latency.
+//   * sampling uses a counter-based stream (splitmix64 of (row, step, draw)), restated by the
+//     oracle, in place of torch's global RNG; the cross-fade and fade-out (model.py:316-329,
+//     341-399) run in float64 like the reference's numpy.
+#include <algorithm>
+#include <cmath>
+
+#include "kernels.h"
+
+namespace avc {
+namespace {
+
+inline int ew(long n) { return (int)std::max<long>(1, std::min<long>((n + 255) / 256, 65536)); }
+
+// ---- up-sampling network ------------------------------------------------------------------
+
+// (80, T) channel-major mel -> the generate() padding (2 zero frames each side, model.py:250)
+// in both layouts the next kernels read: time-major [T+2p][C] and channel-major [C][T+2p].
+__global__ void wr_pad_mel_kernel(int C, int T, int pad, const float* __restrict__ mel, float* __restrict__ tm,
+                                  float* __restrict__ cm) {
+  const int Tp = T + 2 * pad;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < (long)C * Tp; idx += (long)gridDim.x * 256) {
+    const int c = (int)(idx / Tp), q = (int)(idx - (long)c * Tp);
+    const float v = (q >= pad && q < pad + T) ? mel[(long)c * T + q - pad] : 0.f;
+    cm[idx] = v;
+    tm[(long)q * C + c] = v;
+  }
+}
+
+// One MelResNet layer over frame rows (model.py:24-31, 41-49):
+//   out[t][n] = act(bn_eval(sum_{k, tap} W[n][k][tap] · in[t + tap][k] + bias[n])) (+ res[t][n])
+// with valid (unpadded) taps: Tout = Tin - taps + 1.  BN eval as alpha·x + beta
+// (alpha = gamma / sqrt(var + eps), beta = beta - mean·alpha), then ReLU, then the residual.
+__global__ void wr_frame_layer_kernel(int Tout, int Cin, int Cout, int taps, const float* __restrict__ in,
+                                      const float* __restrict__ W, const float* __restrict__ bias,
+                                      const float* __restrict__ g, const float* __restrict__ b,
+                                      const float* __restrict__ rm, const float* __restrict__ rv, int relu,
+                                      const float* __restrict__ res, float* __restrict__ out) {
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < (long)Tout * Cout; idx += (long)gridDim.x * 256) {
+    const int t = (int)(idx / Cout), n = (int)(idx - (long)t * Cout);
+    const float* w = W + (long)n * Cin * taps;
+    float s = 0.f;
+    for (int k = 0; k < Cin; ++k) {
+#pragma unroll 1
+      for (int tap = 0; tap < taps; ++tap) s = fmaf(w[k * taps + tap], in[(long)(t + tap) * Cin + k], s);
+    }
+    if (bias) s += bias[n];
+    if (g) {
+      const float alpha = g[n] / sqrtf(rv[n] + 1e-5f);
+      s = s * alpha + (b[n] - rm[n] * alpha);
+    }
+    if (relu) s = fmaxf(s, 0.f);
+    if (res) s += res[idx];
+    out[idx] = s;
+  }
+}
+
+// Stretch2d(s, 1) + Conv2d(1, 1, (1, 2s+1), padding (0, s)) along time (model.py:52-63, 79-92):
+//   out[c][j] = sum_u w[u] · xs[c][j + u - s],  xs[c][q] = in[c][q / s] for 0 <= q < Lin·s, else 0.
+// final != 0: write the cropped (indent on both sides), time-major [Lout - 2·indent][C] result.
+__global__ void wr_stretch_conv_kernel(int C, int Lin, int s, const float* __restrict__ w, const float* __restrict__ in,
+                                       float* __restrict__ out, int final_crop, int indent) {
+  const long Lout = (long)Lin * s;
+  const long Lw = final_crop ? Lout - 2L * indent : Lout;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < (long)C * Lw; idx += (long)gridDim.x * 256) {
+    long j;
+    int c;
+    if (final_crop) {
+      const long q = idx / C;
+      c = (int)(idx - q * C);
+      j = q + indent;
+    } else {
+      c = (int)(idx / Lout);
+      j = idx - (long)c * Lout;
+    }
+    const float* row = in + (long)c * Lin;
+    float acc = 0.f;
+    for (int u = 0; u <= 2 * s; ++u) {
+      const long q = j + u - s;
+      const float v = (q >= 0 && q < Lout) ? row[q / s] : 0.f;
+      acc = fmaf(w[u], v, acc);
+    }
+    out[idx] = acc;
+  }
+}
+
+// pI[src][q][u] = b_I[u] + W_I[u][1:1+F] · m[src][q] + W_I[u][1+F:1+F+A] · aux[src][q / hop][0:A],
+// for q < Ltot; row q = Ltot holds b_I alone (fold padding: m = aux = 0, model.py:318-321).
+__global__ void wr_input_proj_kernel(int nsrc, long Ltot, int H, int F, int A, int hop, int Tf, int auxd,
+                                     const float* __restrict__ m, const float* __restrict__ auxf,
+                                     const float* __restrict__ WI, const float* __restrict__ bI,
+                                     float* __restrict__ pI) {
+  const int K = 1 + F + A;
+  const long rows = (long)nsrc * (Ltot + 1);
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < rows * H; idx += (long)gridDim.x * 256) {
+    const long rq = idx / H;
+    const int u = (int)(idx - rq * H);
+    const int src = (int)(rq / (Ltot + 1));
+    const long q = rq - (long)src * (Ltot + 1);
+    float s = 0.f;
+    if (q < Ltot) {
+      const float* w = WI + (long)u * K + 1;
+      const float* mv = m + ((long)src * Ltot + q) * F;
+      for (int k = 0; k < F; ++k) s = fmaf(w[k], mv[k], s);
+      const float* av = auxf + ((long)src * Tf + q / hop) * auxd;
+      for (int k = 0; k < A; ++k) s = fmaf(w[F + k], av[k], s);
+    }
+    pI[idx] = s + bI[u];
+  }
+}
+
+// ---- the sample loop ------------------------------------------------------------------------
+
+struct WrStep {
+  int R, L, H, Fc, A, NC, auxd, hop, Tf;
+  long Ltot, stride;      // stride = target + overlap (batched), 0 = one source row per fold row
+  int batched, mol, teacher;
+  unsigned long long seed;
+  int* step;              // current step (device); advanced by wr_out_kernel's last workgroup
+  int* done;              // arrivals of wr_out_kernel's workgroups in the current step
+  const float* pI;        // [nsrc][Ltot + 1][H]
+  const float* auxf;      // [nsrc][Tf][auxd] frame-rate aux features
+  const float* WI; long wi_ld;  // I.weight: column 0 multiplies x_prev
+  const float *Wih1, *Whh1, *bih1, *bhh1, *Wih2, *Whh2, *bih2, *bhh2;
+  const float *W1, *b1, *W2, *b2, *W3, *b3;
+  float *x_prev, *h1, *h2, *t1, *t2, *y1, *y2;  // h1 / h2: [2][R][H] (step parity)
+  float* out;             // [R][L] samples
+  float* logits;          // teacher mode: [R][L][NC]
+  const float* x_tf;      // teacher mode: [R][L] previous samples
+};
+
+__device__ __forceinline__ int cur_step(const WrStep& a) {
+  return __hip_atomic_load(a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// source row and position of fold row r at step i (valid positions < Ltot; fold padding reads
+// the pI row Ltot and zero aux)
+__device__ __forceinline__ void fold_pos(const WrStep& a, int r, int i, int& src, long& q) {
+  src = a.batched ? 0 : r;
+  q = a.batched ? (long)r * a.stride + i : (long)i;
+  if (q > a.Ltot) q = a.Ltot;
+}
+
+__device__ __forceinline__ float aux_at(const WrStep& a, int src, long q, int k) {
+  return q < a.Ltot ? a.auxf[((long)src * a.Tf + q / a.hop) * a.auxd + k] : 0.f;
+}
+
+// the previous sample a step consumes: the last draw, or (teacher-forced, model.py:195-197) the
+// given sequence at the same index
+__device__ __forceinline__ float xprev_at(const WrStep& a, int r, int i) {
+  return a.teacher ? a.x_tf[(long)r * a.L + i] : a.x_prev[r];
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+constexpr int kRB = 8;   // fold rows per register batch
+constexpr int kKJ = 9;   // k = lane + 64 j, j < kKJ: K <= 576
+
+// GRU layer WHICH (1: rnn1 on xI; 2: rnn2 on [t1, a2]) for two hidden units per workgroup.
+// Waves 0/1: the input gates (r, z, n rows) of units u0 / u0+1, waves 2/3: their hidden gates;
+// lanes split K, a wave sum reduces.  torch's GRU cell order (aten RNN.cpp GRUCell):
+// r = σ(gh_r + gi_r), z = σ(gh_z + gi_z), n = tanh(gi_n + gh_n·r), h' = (h − n)·z + n.
+template <int WHICH>
+__global__ __launch_bounds__(256) void wr_gru_kernel(WrStep a) {
+  const int i = cur_step(a);
+  if (i >= a.L) return;
+  __shared__ float gates[4][3][kRB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int H = a.H, R = a.R;
+  const int u0 = blockIdx.x * 2;
+  const int u = u0 + (w & 1);
+  const bool hid = w >= 2;
+  const int Kin = WHICH == 1 ? H : H + a.A;
+  const int K = hid ? H : Kin;
+  const float* W = hid ? (WHICH == 1 ? a.Whh1 : a.Whh2) : (WHICH == 1 ? a.Wih1 : a.Wih2);
+  const int cur = i & 1;
+  const float* hprev = (WHICH == 1 ? a.h1 : a.h2) + (long)cur * R * H;
+  float* hnext = (WHICH == 1 ? a.h1 : a.h2) + (long)(cur ^ 1) * R * H;
+  float wv[3][kKJ];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int j = 0; j < kKJ; ++j) {
+      const int k = lane + 64 * j;
+      wv[g][j] = k < K ? W[(long)(g * H + u) * K + k] : 0.f;
+    }
+  for (int rb = 0; rb < R; rb += kRB) {
+    const int nr = min(kRB, R - rb);
+    float acc[3][kRB];
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int rr = 0; rr < kRB; ++rr) acc[g][rr] = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < kRB; ++rr) {
+      if (rr >= nr) continue;
+      const int r = rb + rr;
+      int src;
+      long q;
+      fold_pos(a, r, i, src, q);
+      const float xp = xprev_at(a, r, i);
+#pragma unroll
+      for (int j = 0; j < kKJ; ++j) {
+        const int k = lane + 64 * j;
+        if (k >= K) continue;
+        float v;
+        if (hid) v = hprev[(long)r * H + k];
+        else if (WHICH == 1) v = a.pI[((long)src * (a.Ltot + 1) + q) * H + k] + a.WI[(long)k * a.wi_ld] * xp;
+        else v = k < H ? a.t1[(long)r * H + k] : aux_at(a, src, q, a.A + (k - H));
+#pragma unroll
+        for (int g = 0; g < 3; ++g) acc[g][rr] = fmaf(wv[g][j], v, acc[g][rr]);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int rr = 0; rr < kRB; ++rr) {
+        const float s = wave_sum(acc[g][rr]);
+        if (lane == 0) gates[w][g][rr] = s;
+      }
+    __syncthreads();
+    if (tid < 2 * nr) {
+      const int uu = tid & 1, rr = tid >> 1, r = rb + rr;
+      const int un = u0 + uu;
+      const float* bi = WHICH == 1 ? a.bih1 : a.bih2;
+      const float* bh = WHICH == 1 ? a.bhh1 : a.bhh2;
+      const float gi_r = gates[uu][0][rr] + bi[un], gi_z = gates[uu][1][rr] + bi[H + un],
+                  gi_n = gates[uu][2][rr] + bi[2 * H + un];
+      const float gh_r = gates[2 + uu][0][rr] + bh[un], gh_z = gates[2 + uu][1][rr] + bh[H + un],
+                  gh_n = gates[2 + uu][2][rr] + bh[2 * H + un];
+      const float rg = sigmoidf_(gh_r + gi_r), zg = sigmoidf_(gh_z + gi_z);
+      const float ng = tanhf(gi_n + gh_n * rg);
+      const float hp = hprev[(long)r * H + un];
+      const float hn = (hp - ng) * zg + ng;
+      hnext[(long)r * H + un] = hn;
+      if (WHICH == 1) {  // x = x + h1 (model.py:269), x = I(...) recomputed for this unit
+        int src;
+        long q;
+        fold_pos(a, r, i, src, q);
+        const float xi = a.pI[((long)src * (a.Ltot + 1) + q) * H + un] + a.WI[(long)un * a.wi_ld] * xprev_at(a, r, i);
+        a.t1[(long)r * H + un] = xi + hn;
+      } else {           // x = x + h2 (model.py:273)
+        a.t2[(long)r * H + un] = a.t1[(long)r * H + un] + hn;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// fc1 / fc2 (model.py:274-278): y = relu(W · [v, a] + b), v = t2 (WHICH 1, a = a3) or y1
+// (WHICH 2, a = a4); one output row per wave, four per workgroup.
+template <int WHICH>
+__global__ __launch_bounds__(256) void wr_fc_kernel(WrStep a) {
+  const int i = cur_step(a);
+  if (i >= a.L) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = blockIdx.x * 4 + w;
+  const int Kv = WHICH == 1 ? a.H : a.Fc, K = Kv + a.A;
+  const float* W = WHICH == 1 ? a.W1 : a.W2;
+  const float* bias = WHICH == 1 ? a.b1 : a.b2;
+  const float* vin = WHICH == 1 ? a.t2 : a.y1;
+  float* y = WHICH == 1 ? a.y1 : a.y2;
+  const int aoff = (WHICH == 1 ? 2 : 3) * a.A;
+  if (n >= a.Fc) return;
+  float wv[kKJ];
+#pragma unroll
+  for (int j = 0; j < kKJ; ++j) {
+    const int k = lane + 64 * j;
+    wv[j] = k < K ? W[(long)n * K + k] : 0.f;
+  }
+  for (int r = 0; r < a.R; ++r) {
+    int src;
+    long q;
+    fold_pos(a, r, i, src, q);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < kKJ; ++j) {
+      const int k = lane + 64 * j;
+      if (k >= K) continue;
+      const float v = k < Kv ? vin[(long)r * Kv + k] : aux_at(a, src, q, aoff + (k - Kv));
+      acc = fmaf(wv[j], v, acc);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) y[(long)r * a.Fc + n] = fmaxf(acc + bias[n], 0.f);
+  }
+}
+
+// counter-based uniform in [1e-5, 1 - 1e-5] (oracle/wavernn_oracle.py:uniforms, the same bits)
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float uniform_draw(unsigned long long seed, int r, int i, int d) {
+  const unsigned long long base = mix64((seed + 1ull) * 0x9E3779B97F4A7C15ull);
+  const unsigned long long ctr = ((unsigned long long)r << 40) | ((unsigned long long)(unsigned)i << 8) | (unsigned)d;
+  const unsigned long long z = mix64(ctr * 0x9E3779B97F4A7C15ull + base);
+  const float u = (float)(z >> 40) * (1.0f / 16777216.0f);
+  return __fadd_rn(1e-5f, __fmul_rn(0.99998f, u));
+}
+
+// fc3 + sampling (model.py:279-315; distribution.py:87-123), one workgroup per fold row; the last
+// workgroup to finish advances the step counter for the next launch.
+__global__ __launch_bounds__(256) void wr_out_kernel(WrStep a) {
+  const int i = cur_step(a);
+  if (i >= a.L) return;
+  __shared__ float lg[64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = blockIdx.x, Fc = a.Fc, NC = a.NC;
+  float yv[kKJ];
+#pragma unroll
+  for (int j = 0; j < kKJ; ++j) {
+    const int k = lane + 64 * j;
+    yv[j] = k < Fc ? a.y2[(long)r * Fc + k] : 0.f;
+  }
+  for (int c = w; c < NC; c += 4) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < kKJ; ++j) {
+      const int k = lane + 64 * j;
+      if (k < Fc) acc = fmaf(a.W3[(long)c * Fc + k], yv[j], acc);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) lg[c] = acc + a.b3[c];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const long o = (long)r * a.L + i;
+    float x;
+    if (a.teacher) {
+      for (int c = 0; c < NC; ++c) a.logits[o * NC + c] = lg[c];
+      x = a.x_tf[o];  // (unused by the next step, which reads x_tf itself)
+    } else if (a.mol) {
+      const int nr = NC / 3;
+      int best = 0;
+      float bv = 0.f;
+      for (int k = 0; k < nr; ++k) {  // Gumbel-max mixture choice; first maximum wins (torch.max)
+        const float u = uniform_draw(a.seed, r, i, k);
+        const float t = lg[k] - logf(-logf(u));
+        if (k == 0 || t > bv) { bv = t; best = k; }
+      }
+      const float mean = lg[nr + best];
+      const float ls = fmaxf(lg[2 * nr + best], -32.236191301916641f);  // log(1e-14)
+      const float u = uniform_draw(a.seed, r, i, nr);
+      x = mean + expf(ls) * (logf(u) - logf(1.0f - u));
+      x = fminf(fmaxf(x, -1.f), 1.f);
+    } else {  // RAW: Categorical(softmax) by inverse CDF, 2k / (n_classes - 1) - 1
+      float mx = lg[0];
+      for (int c = 1; c < NC; ++c) mx = fmaxf(mx, lg[c]);
+      float e[64], sum = 0.f;
+      for (int c = 0; c < NC; ++c) { e[c] = expf(lg[c] - mx); sum += e[c]; }
+      const float u = uniform_draw(a.seed, r, i, 0);
+      float cdf = 0.f;
+      int k = 0;
+      for (int c = 0; c < NC; ++c) { cdf += e[c] / sum; if (cdf < u) k = c + 1; }
+      k = min(k, NC - 1);
+      x = 2.f * (float)k / ((float)NC - 1.f) - 1.f;
+    }
+    a.out[o] = x;
+    a.x_prev[r] = x;
+    if (atomicAdd(a.done, 1) == a.R - 1) {  // every workgroup has read this step: advance it
+      __hip_atomic_store(a.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.step, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ void wr_init_state_kernel(int R, int H, int Fc, int* step, int* done, float* x_prev, float* h1,
+                                     float* h2) {
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < 2L * R * H; idx += (long)gridDim.x * 256) {
+    h1[idx] = 0.f;
+    h2[idx] = 0.f;
+    if (idx < R) x_prev[idx] = 0.f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *step = 0;
+    *done = 0;
+  }
+}
+
+// numpy.linspace(a, b, n)[k] in float64: a + k·(b - a)/(n - 1), the last point exactly b
+__device__ __forceinline__ double linspace_at(double a, double b, int n, int k) {
+  if (n == 1) return a;
+  if (k == n - 1) return b;
+  return a + (double)k * ((b - a) / (double)(n - 1));
+}
+
+// xfade_and_unfold + crop + 20-hop fade-out (model.py:316-329, 341-399) in float64, then float32
+__global__ void wr_unfold_kernel(int R, int L, int batched, int target, int overlap, long wave_len, int fade_n,
+                                 const float* __restrict__ y, float* __restrict__ wave) {
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < wave_len; q += (long)gridDim.x * 256) {
+    double v = 0.0;
+    if (batched) {
+      const long stride = (long)target + overlap;
+      const int silence = overlap / 2, fade = overlap - silence;
+      long b0 = (q - L) / stride;
+      if (b0 < 0) b0 = 0;
+      for (long b = b0; b < R; ++b) {
+        const long p = q - b * stride;
+        if (p < 0) break;
+        if (p >= L) continue;
+        double s = (double)y[b * L + p];
+        if (p < overlap) s *= p < silence ? 0.0 : sqrt(0.5 * (1.0 + linspace_at(-1.0, 1.0, fade, (int)p - silence)));
+        if (p >= L - overlap) {
+          const long pp = p - (L - overlap);
+          s *= pp < silence ? 1.0 : sqrt(0.5 * (1.0 - linspace_at(-1.0, 1.0, fade, (int)(pp - silence))));
+        }
+        v += s;
+      }
+    } else {
+      v = (double)y[q];
+    }
+    const long tail0 = wave_len - fade_n;
+    if (q >= tail0 && tail0 >= 0) v *= linspace_at(1.0, 0.0, fade_n, (int)(q - tail0));
+    wave[q] = (float)v;
+  }
+}
+
+constexpr int kChunk = 32;  // sample steps per captured graph
+
+// the five launches of one sample step
+int launch_step(const WrStep& a, hipStream_t s) {
+  wr_gru_kernel<1><<<a.H / 2, 256, 0, s>>>(a);
+  wr_gru_kernel<2><<<a.H / 2, 256, 0, s>>>(a);
+  wr_fc_kernel<1><<<(a.Fc + 3) / 4, 256, 0, s>>>(a);
+  wr_fc_kernel<2><<<(a.Fc + 3) / 4, 256, 0, s>>>(a);
+  wr_out_kernel<<<a.R, 256, 0, s>>>(a);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+// Parameter order: the float tensors of WaveRNN.state_dict() (step and num_batches_tracked left out).
+enum : int {
+  W_CONV_IN = 0, W_BN0 = 1, W_LAYERS = 5, W_PER_LAYER = 10,
+};
+
+struct WrDims {
+  int F, C, A4, RB, H, Fc, NC, pad, f0, f1, f2;
+  int base_after_layers() const { return W_LAYERS + W_PER_LAYER * RB; }
+  int count() const { return base_after_layers() + 2 + 3 + 2 + 8 + 6; }
+};
+
+int check_dims(const WrDims& d) {
+  AVC_CHECK_ARG(d.F > 0 && d.F <= 512 && d.C > 0 && d.A4 > 0 && d.A4 % 4 == 0 && d.RB >= 0 && d.RB <= 64,
+                "wavernn: feat_dims, compute_dims, res_out_dims (multiple of 4) or res_blocks out of range");
+  AVC_CHECK_ARG(d.H >= 64 && d.H % 2 == 0 && d.H + d.A4 / 4 <= 64 * kKJ && d.Fc >= 4 && d.Fc + d.A4 / 4 <= 64 * kKJ,
+                "wavernn: rnn_dims / fc_dims must leave rnn_dims + aux_dims and fc_dims + aux_dims <= 576");
+  AVC_CHECK_ARG(d.NC > 0 && d.NC <= 64, "wavernn: n_classes must be 1..64");
+  AVC_CHECK_ARG(d.pad >= 0 && d.f0 > 0 && d.f1 > 0 && d.f2 > 0, "wavernn: bad pad / upsample factors");
+  return AVC_OK;
+}
+
+// Up-sampling of a generate() input (1, F, T) with the padding generate applies:
+// m [Ltot][F], auxf [T][A4] (frame rate), Ltot = T·hop.  Scratch from sc.
+// add_pad = 0: the mel already carries `pad` context frames on both sides (the reference's
+// forward(x, mels), model.py:186): then Ltot = (T - 2 pad)·hop and auxf has T - 2 pad frames.
+int upsample(avc_context* ctx, Scratch& sc, const WrDims& d, int T, const float* mel, const float* const* P,
+             float* m, float* auxf, hipStream_t s, int add_pad = 1) {
+  (void)ctx;
+  const int padf = add_pad ? d.pad : 0;
+  const int Tp = T + 2 * padf, k = 2 * d.pad + 1;
+  AVC_CHECK_ARG(Tp - 2 * d.pad >= 1, "wavernn: need at least one mel frame beyond the context");
+  AVC_TAKE(tm, float, (size_t)Tp * d.F, sc);
+  AVC_TAKE(cm, float, (size_t)Tp * d.F, sc);
+  wr_pad_mel_kernel<<<ew((long)d.F * Tp), 256, 0, s>>>(d.F, T, padf, mel, tm, cm);
+  // MelResNet: conv_in (valid, k = 2 pad + 1) -> BN -> relu, res blocks, conv_out (model.py:34-49)
+  const int Tr = Tp - k + 1;  // frames of the aux features (== T when generate pads)
+  AVC_TAKE(xa, float, (size_t)Tr * d.C, sc);
+  AVC_TAKE(xb, float, (size_t)Tr * d.C, sc);
+  AVC_TAKE(xc, float, (size_t)Tr * d.C, sc);
+  wr_frame_layer_kernel<<<ew((long)Tr * d.C), 256, 0, s>>>(Tr, d.F, d.C, k, tm, P[W_CONV_IN], nullptr, P[W_BN0],
+                                                          P[W_BN0 + 1], P[W_BN0 + 2], P[W_BN0 + 3], 1, nullptr, xa);
+  for (int l = 0; l < d.RB; ++l) {
+    const float* const* q = P + W_LAYERS + W_PER_LAYER * l;
+    wr_frame_layer_kernel<<<ew((long)Tr * d.C), 256, 0, s>>>(Tr, d.C, d.C, 1, xa, q[0], nullptr, q[2], q[3], q[4],
+                                                            q[5], 1, nullptr, xb);
+    wr_frame_layer_kernel<<<ew((long)Tr * d.C), 256, 0, s>>>(Tr, d.C, d.C, 1, xb, q[1], nullptr, q[6], q[7], q[8],
+                                                            q[9], 0, xa, xc);
+    std::swap(xa, xc);
+  }
+  const int o = d.base_after_layers();
+  wr_frame_layer_kernel<<<ew((long)Tr * d.A4), 256, 0, s>>>(Tr, d.C, d.A4, 1, xa, P[o], P[o + 1], nullptr, nullptr,
+                                                           nullptr, nullptr, 0, nullptr, auxf);
+  // mel: three stretch + smoothing passes, the last one cropped and time-major (model.py:86-93)
+  const int fs[3] = {d.f0, d.f1, d.f2};
+  const long hop = (long)d.f0 * d.f1 * d.f2;
+  const long L1 = (long)Tp * fs[0], L2 = L1 * fs[1];
+  AVC_TAKE(s1, float, (size_t)d.F * L1, sc);
+  AVC_TAKE(s2, float, (size_t)d.F * L2, sc);
+  wr_stretch_conv_kernel<<<ew((long)d.F * L1), 256, 0, s>>>(d.F, Tp, fs[0], P[o + 2], cm, s1, 0, 0);
+  wr_stretch_conv_kernel<<<ew((long)d.F * L2), 256, 0, s>>>(d.F, (int)L1, fs[1], P[o + 3], s1, s2, 0, 0);
+  wr_stretch_conv_kernel<<<ew((long)d.F * Tr * hop), 256, 0, s>>>(d.F, (int)L2, fs[2], P[o + 4], s2, m, 1,
+                                                                  (int)(d.pad * hop));
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+size_t upsample_scratch(const WrDims& d, int T) {
+  const size_t Tp = T + 2 * d.pad, hop = (size_t)d.f0 * d.f1 * d.f2;
+  return 4 * (2 * Tp * d.F + 3 * (size_t)T * d.C + (size_t)d.F * Tp * d.f0 + (size_t)d.F * Tp * d.f0 * d.f1) +
+         8 * 256;
+}
+
+}  // namespace
+}  // namespace avc
+
+using namespace avc;
+
+extern "C" {
+
+int avc_wavernn_param_count(int res_blocks) { return W_LAYERS + W_PER_LAYER * res_blocks + 2 + 3 + 2 + 8 + 6; }
+
+int avc_wavernn_upsample(avc_context* ctx, const int* dims, int T, const float* const* params, const float* mel,
+                         float* m, float* aux, void* stream) {
+  AVC_CHECK_ARG(ctx && dims && params && mel && m && aux, "NULL pointer");
+  const WrDims d{dims[0], dims[1], dims[2], dims[3], dims[4], dims[5], dims[6], dims[7], dims[8], dims[9], dims[10]};
+  AVC_TRY(check_dims(d));
+  for (int k = 0; k < d.count(); ++k) AVC_CHECK_ARG(params[k] != nullptr, "wavernn: NULL parameter");
+  AVC_TRY(ensure_arena(ctx, upsample_scratch(d, T)));
+  Scratch sc(ctx);
+  return upsample(ctx, sc, d, T, mel, params, m, aux, reinterpret_cast<hipStream_t>(stream));
+}
+
+int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* const* params, const float* mel,
+                         int batched, int target, int overlap, int mol, unsigned long long seed,
+                         const float* x_teacher, float* logits, float* samples, float* wave, void* stream) {
+  AVC_CHECK_ARG(ctx && dims && params && mel, "NULL pointer");
+  const WrDims d{dims[0], dims[1], dims[2], dims[3], dims[4], dims[5], dims[6], dims[7], dims[8], dims[9], dims[10]};
+  AVC_TRY(check_dims(d));
+  for (int k = 0; k < d.count(); ++k) AVC_CHECK_ARG(params[k] != nullptr, "wavernn: NULL parameter");
+  AVC_CHECK_ARG(T >= 1, "wavernn: need at least one mel frame");
+  AVC_CHECK_ARG(!batched || (target > 0 && overlap > 0), "wavernn: batched generation needs target, overlap > 0");
+  AVC_CHECK_ARG(!x_teacher || logits, "wavernn: teacher-forced mode writes logits");
+  const long hop = (long)d.f0 * d.f1 * d.f2;
+  // generate() pads `pad` zero frames on both sides; teacher-forced calls are the reference's
+  // forward(x, mels), whose mel carries real context frames there instead
+  const int add_pad = x_teacher ? 0 : 1;
+  const int Tf = add_pad ? T : T - 2 * d.pad;
+  AVC_CHECK_ARG(Tf >= 1, "wavernn: forward(x, mels) needs more than 2 * pad mel frames");
+  const long Ltot = (long)Tf * hop;
+  const int A = d.A4 / 4;
+  // fold geometry (model.py:311-324): rows of target + 2 overlap positions, stride target + overlap
+  long R = 1, L = Ltot, stride = 0;
+  if (batched) {
+    R = (Ltot - overlap) / (target + overlap);
+    const long ext = R * (overlap + target) + overlap;
+    if (Ltot - ext != 0) ++R;
+    L = (long)target + 2 * overlap;
+    stride = (long)target + overlap;
+  }
+  AVC_CHECK_ARG(R >= 1 && R <= 65535 && L <= (1L << 30), "wavernn: sequence too long for one call");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t H = d.H;
+  const size_t need = upsample_scratch(d, T) + 4 * ((size_t)Ltot * d.F + (size_t)T * d.A4 + (Ltot + 1) * H +
+                                                    (size_t)R * (1 + 7 * H + 2 * d.Fc) + (size_t)R * L) +
+                      32 * 256;
+  AVC_TRY(ensure_arena(ctx, need));
+  Scratch sc(ctx);
+  AVC_TAKE(m, float, (size_t)Ltot * d.F, sc);
+  AVC_TAKE(auxf, float, (size_t)Tf * d.A4, sc);
+  {
+    Scratch up(ctx);
+    AVC_TRY(upsample(ctx, up, d, T, mel, params, m, auxf, s, add_pad));
+  }
+  const int o = d.base_after_layers() + 5;  // I.weight
+  AVC_TAKE(pI, float, (size_t)(Ltot + 1) * H, sc);
+  wr_input_proj_kernel<<<ew((Ltot + 1) * (long)H), 256, 0, s>>>(1, Ltot, d.H, d.F, A, (int)hop, Tf, d.A4, m, auxf,
+                                                              params[o], params[o + 1], pI);
+  AVC_LAUNCH_CHECK();
+  AVC_TAKE(ctr, int, 64, sc);
+  AVC_TAKE(x_prev, float, R, sc);
+  AVC_TAKE(h1, float, 2 * R * H, sc);
+  AVC_TAKE(h2, float, 2 * R * H, sc);
+  AVC_TAKE(t1, float, R * H, sc);
+  AVC_TAKE(t2, float, R * H, sc);
+  AVC_TAKE(y1, float, (size_t)R * d.Fc, sc);
+  AVC_TAKE(y2, float, (size_t)R * d.Fc, sc);
+  float* out = samples;
+  if (!out) {
+    out = sc.take<float>((size_t)R * L);
+    if (!out) return AVC_ERR_WORKSPACE;
+  }
+  WrStep a{};
+  a.R = (int)R; a.L = (int)L; a.H = d.H; a.Fc = d.Fc; a.A = A; a.NC = d.NC; a.auxd = d.A4; a.hop = (int)hop;
+  a.Tf = Tf; a.Ltot = Ltot; a.stride = stride; a.batched = batched ? 1 : 0; a.mol = mol ? 1 : 0;
+  a.teacher = x_teacher ? 1 : 0; a.seed = seed;
+  a.step = ctr; a.done = ctr + 32;
+  a.pI = pI; a.auxf = auxf; a.WI = params[o]; a.wi_ld = 1 + d.F + A;
+  a.Wih1 = params[o + 2]; a.Whh1 = params[o + 3]; a.bih1 = params[o + 4]; a.bhh1 = params[o + 5];
+  a.Wih2 = params[o + 6]; a.Whh2 = params[o + 7]; a.bih2 = params[o + 8]; a.bhh2 = params[o + 9];
+  a.W1 = params[o + 10]; a.b1 = params[o + 11]; a.W2 = params[o + 12]; a.b2 = params[o + 13];
+  a.W3 = params[o + 14]; a.b3 = params[o + 15];
+  a.x_prev = x_prev; a.h1 = h1; a.h2 = h2; a.t1 = t1; a.t2 = t2; a.y1 = y1; a.y2 = y2;
+  a.out = out; a.logits = logits; a.x_tf = x_teacher;
+  wr_init_state_kernel<<<ew(2 * R * (long)H), 256, 0, s>>>((int)R, d.H, d.Fc, a.step, a.done, x_prev, h1, h2);
+  AVC_LAUNCH_CHECK();
+  // the sequential loop: chunks of kChunk steps captured once into a graph and replayed
+  if (!ctx->capture_stream) AVC_HIP(hipStreamCreateWithFlags(&ctx->capture_stream, hipStreamNonBlocking));
+  hipStream_t cs = ctx->capture_stream;
+  const long chunks = (L + kChunk - 1) / kChunk;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  if (chunks > 1) {
+    AVC_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
+    int rc = AVC_OK;
+    for (int k = 0; k < kChunk && rc == AVC_OK; ++k) rc = launch_step(a, cs);
+    const hipError_t e = hipStreamEndCapture(cs, &graph);
+    if (rc != AVC_OK) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    AVC_HIP(e);
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      (void)hipGraphDestroy(graph);
+      AVC_HIP(ei);
+    }
+    for (long c = 0; c < chunks; ++c) {
+      const hipError_t el = hipGraphLaunch(exec, s);
+      if (el != hipSuccess) {
+        (void)hipGraphExecDestroy(exec);
+        (void)hipGraphDestroy(graph);
+        AVC_HIP(el);
+      }
+    }
+    // generate() returns a host waveform anyway: wait here, then release the graph
+    const hipError_t es = hipStreamSynchronize(s);
+    (void)hipGraphExecDestroy(exec);
+    (void)hipGraphDestroy(graph);
+    AVC_HIP(es);
+  } else {
+    for (long k = 0; k < L; ++k) AVC_TRY(launch_step(a, s));
+  }
+  if (wave && !x_teacher) {
+    const long wave_len = (long)(T - 1) * hop;
+    AVC_CHECK_ARG(wave_len >= 20 * hop, "wavernn: generate() fades out the last 20 hops; need T >= 21 frames");
+    wr_unfold_kernel<<<ew(wave_len), 256, 0, s>>>((int)R, (int)L, batched ? 1 : 0, target, overlap, wave_len,
+                                                  (int)(20 * hop), out, wave);
+    AVC_LAUNCH_CHECK();
+  }
+  return AVC_OK;
+}
+
+// Rows and steps of a generate() call (so the caller can size `samples` [rows][steps]).
+int avc_wavernn_fold_shape(long n_positions, int batched, int target, int overlap, long* rows, long* steps) {
+  AVC_CHECK_ARG(rows && steps && n_positions > 0, "wavernn_fold_shape: bad arguments");
+  if (!batched) {
+    *rows = 1;
+    *steps = n_positions;
+    return AVC_OK;
+  }
+  AVC_CHECK_ARG(target > 0 && overlap > 0, "wavernn_fold_shape: target, overlap > 0");
+  long R = (n_positions - overlap) / (target + overlap);
+  if (n_positions - (R * (overlap + target) + overlap) != 0) ++R;
+  *rows = R;
+  *steps = (long)target + 2 * overlap;
+  return AVC_OK;
+}
+
+}  // extern "C"

@@ -42,3 +42,11 @@ SpeakerEncoderParams = {
               "batch_first": True},
     "learn": {"save_dir": "models/SpeakerEncoder"},
 }
+
+# hparams.py:92-115 (WaveRNNParams)
+WaveRNNParams = {
+    "model_dir": "models/WaveRNN",
+    "model": {"hop_length": 275, "rnn_dims": 512, "res_out_dims": 128, "feat_dims": 80, "fc_dims": 512, "bits": 9,
+              "upsample_factors": (5, 5, 11), "compute_dims": 128, "pad": 2, "res_blocks": 10, "mode": "MOL"},
+    "generate": {"batched": True, "target": 11_000, "overlap": 550, "mu_law": False},
+}

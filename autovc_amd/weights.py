@@ -196,3 +196,75 @@ def synthetic_speech(seed: int, n: int, sr: int) -> np.ndarray:
     y = y * env
     y = 0.5 * y / np.max(np.abs(y)) + noise
     return y.astype(np.float32)
+
+
+# ---- WaveRNN vocoder ---------------------------------------------------
+
+WAVERNN_DIMS = dict(rnn_dims=512, fc_dims=512, feat_dims=80, res_out_dims=128, compute_dims=128,
+                    res_blocks=10, pad=2, upsample_factors=(5, 5, 11), bits=9)
+
+
+def wavernn_state_dict(seed: int = 0, mode: str = "MOL", device="cpu", **dims):
+    """WaveRNN.state_dict() keys/shapes (wavernn/model.py:16-180) with PyTorch's default init
+    bounds (Conv/Linear U(±1/√fan_in), GRU U(±1/√H)).  BatchNorm affine and running statistics
+    are drawn from small ranges (generate() runs eval-mode BN, so identities would hide bugs);
+    the up-sampling smoothing kernels start at the reference's 1/k fill (model.py:85) scaled by
+    U(0.8, 1.2) per tap for the same reason."""
+    import torch
+    d = dict(WAVERNN_DIMS)
+    d.update(dims)
+    R, F_, C, A, Fc = d["rnn_dims"], d["feat_dims"], d["compute_dims"], d["res_out_dims"], d["fc_dims"]
+    aux = A // 4
+    k_size = 2 * d["pad"] + 1
+    n_classes = 2 * d["bits"] if mode == "RAW" else 30
+    out = OrderedDict()
+    stream = [60_000_000]
+
+    def u(shape, lo, hi):
+        v = _u(seed, stream[0], shape, lo, hi)
+        stream[0] += 1
+        return v
+
+    def bn(prefix, n):
+        out[prefix + ".weight"] = u((n,), 0.8, 1.2)
+        out[prefix + ".bias"] = u((n,), -0.1, 0.1)
+        out[prefix + ".running_mean"] = u((n,), -0.2, 0.2)
+        out[prefix + ".running_var"] = u((n,), 0.5, 1.5)
+        out[prefix + ".num_batches_tracked"] = np.array(0, dtype=np.int64)
+
+    out["step"] = np.zeros(1, dtype=np.int64)
+    kb = 1.0 / math.sqrt(F_ * k_size)
+    out["upsample.resnet.conv_in.weight"] = u((C, F_, k_size), -kb, kb)
+    bn("upsample.resnet.batch_norm", C)
+    kb = 1.0 / math.sqrt(C)
+    for i in range(d["res_blocks"]):
+        p = f"upsample.resnet.layers.{i}"
+        out[p + ".conv1.weight"] = u((C, C, 1), -kb, kb)
+        out[p + ".conv2.weight"] = u((C, C, 1), -kb, kb)
+        bn(p + ".batch_norm1", C)
+        bn(p + ".batch_norm2", C)
+    out["upsample.resnet.conv_out.weight"] = u((A, C, 1), -kb, kb)
+    out["upsample.resnet.conv_out.bias"] = u((A,), -kb, kb)
+    for j, s in enumerate(d["upsample_factors"]):
+        k = 2 * s + 1
+        out[f"upsample.up_layers.{2 * j + 1}.weight"] = (u((1, 1, 1, k), 0.8, 1.2) / k).astype(np.float32)
+
+    def linear(name, n_out, n_in):
+        kl = 1.0 / math.sqrt(n_in)
+        out[name + ".weight"] = u((n_out, n_in), -kl, kl)
+        out[name + ".bias"] = u((n_out,), -kl, kl)
+
+    def gru(name, n_in):
+        kg = 1.0 / math.sqrt(R)
+        out[name + ".weight_ih_l0"] = u((3 * R, n_in), -kg, kg)
+        out[name + ".weight_hh_l0"] = u((3 * R, R), -kg, kg)
+        out[name + ".bias_ih_l0"] = u((3 * R,), -kg, kg)
+        out[name + ".bias_hh_l0"] = u((3 * R,), -kg, kg)
+
+    linear("I", R, F_ + aux + 1)
+    gru("rnn1", R)
+    gru("rnn2", R + aux)
+    linear("fc1", Fc, R + aux)
+    linear("fc2", Fc, Fc + aux)
+    linear("fc3", n_classes, Fc)
+    return OrderedDict((n, torch.from_numpy(np.asarray(v)).to(device)) for n, v in out.items())

@@ -298,6 +298,31 @@ int avc_speaker_encoder_forward(avc_context* ctx, int T, int B, int n_in, int H,
  * L2-normalised. */
 int avc_embedding_mean_normalize(int B, int E, const float* embeds, float* out, void* stream);
 
+/* ---- WaveRNN vocoder `generate` (autovc/wavernn/model.py:214-329) ---------
+ * dims[11] = {feat_dims, compute_dims, res_out_dims, res_blocks, rnn_dims, fc_dims, n_classes,
+ *             pad, upsample_factors[0..2]} (hparams.py:92-107; n_classes 30 for MOL, 2 * bits RAW).
+ * params = the float tensors of WaveRNN.state_dict() in order, without `step` and the BatchNorm
+ *   `num_batches_tracked` counters (avc_wavernn_param_count(res_blocks) pointers).
+ * avc_wavernn_upsample: generate()'s up-sampling (model.py:249-252) of a (1, F, T) mel:
+ *   m [T * hop][F] (time-major), aux [T][res_out_dims] at frame rate (replaces
+ *   UpsampleNetwork.forward, model.py:80-93, eval-mode BN).
+ * avc_wavernn_generate: replaces WaveRNN.generate's body (model.py:243-329).  batched folds the
+ *   T * hop positions into rows of target + 2 * overlap (avc_wavernn_fold_shape gives rows x steps);
+ *   mol = 1 samples the mixture of logistics (distribution.py:87-123), 0 the RAW categorical;
+ *   uniforms come from a counter-based stream keyed by `seed`.  Outputs: samples [rows][steps]
+ *   (optional), wave [(T - 1) * hop] float32 after cross-fade and fade-out (needs T >= 21).
+ *   With x_teacher [rows][steps] != NULL the call is the reference's teacher-forced
+ *   forward(x, mels) (model.py:180-211): the mel carries `pad` real context frames on each side,
+ *   the previous samples come from x_teacher and logits [rows][steps][n_classes] are written.
+ *   The call returns after the generated samples are complete (stream-synchronous). */
+int avc_wavernn_param_count(int res_blocks);
+int avc_wavernn_fold_shape(long n_positions, int batched, int target, int overlap, long* rows, long* steps);
+int avc_wavernn_upsample(avc_context* ctx, const int* dims, int T, const float* const* params, const float* mel,
+                         float* m, float* aux, void* stream);
+int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* const* params, const float* mel,
+                         int batched, int target, int overlap, int mol, unsigned long long seed,
+                         const float* x_teacher, float* logits, float* samples, float* wave, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
