@@ -162,7 +162,7 @@ def ptr(t) -> int | None:
 
 
 TIMING_CLASSES = {"gemm": 0, "lstm_step_fwd": 1, "lstm_step_bwd": 2, "lstm32": 3, "dft64": 4, "lstm2_persist": 5,
-                  "lstm1_persist": 6}
+                  "lstm1_persist": 6, "wavernn": 7}
 
 
 def timing_enable(names):

@@ -5,7 +5,7 @@
 
 namespace avc {
 
-enum TimingClass : int { TC_GEMM = 0, TC_LSTM_STEP_FWD = 1, TC_LSTM_STEP_BWD = 2, TC_LSTM32 = 3, TC_DFT = 4, TC_LSTM2_PERSIST = 5, TC_LSTM1_PERSIST = 6, TC_COUNT = 7 };
+enum TimingClass : int { TC_GEMM = 0, TC_LSTM_STEP_FWD = 1, TC_LSTM_STEP_BWD = 2, TC_LSTM32 = 3, TC_DFT = 4, TC_LSTM2_PERSIST = 5, TC_LSTM1_PERSIST = 6, TC_WAVERNN = 7, TC_COUNT = 8 };
 
 bool timing_on(int cls);
 // returns an event to record after the launch (nullptr when timing is off for cls)

@@ -24,6 +24,7 @@
 #include <cmath>
 
 #include "kernels.h"
+#include "timing.h"
 
 namespace avc {
 namespace {
@@ -139,6 +140,7 @@ struct WrStep {
   const float* pI;        // [nsrc][Ltot + 1][H]
   const float* auxf;      // [nsrc][Tf][auxd] frame-rate aux features
   const float* WI; long wi_ld;  // I.weight: column 0 multiplies x_prev
+  const float* wi0;       // I.weight[:, 0], contiguous
   const float *Wih1, *Whh1, *bih1, *bhh1, *Wih2, *Whh2, *bih2, *bhh2;
   const float *W1, *b1, *W2, *b2, *W3, *b3;
   float *x_prev, *h1, *h2, *t1, *t2, *y1, *y2;  // h1 / h2: [2][R][H] (step parity)
@@ -169,24 +171,135 @@ __device__ __forceinline__ float xprev_at(const WrStep& a, int r, int i) {
   return a.teacher ? a.x_tf[(long)r * a.L + i] : a.x_prev[r];
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
+constexpr int kRC = 24;  // fold rows per LDS chunk
+constexpr int kKJ = 9;   // K <= 64 * kKJ = 576 (staging capacity)
+constexpr int kJ4 = 3;   // float4 k4 = lane + 64 j4, j4 < kJ4 (K / 4 <= 192)
+constexpr int kRP = 65;  // padded row of the partial-sum transpose (conflict-free column sums)
+
+// Inputs of the step's contractions (model.py:263-278): K = Kv + A, the vector part, then its
+// aux slice a2 / a3 / a4 (xI and the hidden states have no aux part).
+enum WrIn : int { IN_XI = 0, IN_H1 = 1, IN_T1A2 = 2, IN_H2 = 3, IN_T2A3 = 4, IN_Y1A4 = 5 };
+
+// Stage rows [rb, rb + kRC) of input `which` (K elements each, K % 4 == 0) into xs[kRC][K] as
+// float4s: stage_load brings every float4 of the chunk into registers, stage_store then writes
+// LDS, so all loads of a kernel (weights, both inputs, epilogue operands) are in flight together;
+// rows past R are zero.
+constexpr int kStage4 = (kRC * 576 / 4 + 255) / 256;  // float4s per thread (K <= 576)
+__device__ __forceinline__ void stage_load(const WrStep& a, int which, int i, int rb, int K, float4 (&v)[kStage4]) {
+  const int cur = i & 1, K4 = K >> 2, H = a.H;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  for (int m = 0; m < kStage4; ++m) {
+    const int e = threadIdx.x + 256 * m;
+    const int rr = e / K4, k = 4 * (e - rr * K4), r = rb + rr;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rr < kRC && r < a.R) {
+      int src;
+      long q;
+      fold_pos(a, r, i, src, q);
+      const float* p = nullptr;
+      switch (which) {
+        case IN_XI: {
+          const float4 pi = *reinterpret_cast<const float4*>(a.pI + ((long)src * (a.Ltot + 1) + q) * H + k);
+          const float4 w0 = *reinterpret_cast<const float4*>(a.wi0 + k);
+          const float xp = xprev_at(a, r, i);
+          x = make_float4(pi.x + w0.x * xp, pi.y + w0.y * xp, pi.z + w0.z * xp, pi.w + w0.w * xp);
+          break;
+        }
+        case IN_H1: p = a.h1 + ((long)cur * a.R + r) * H + k; break;
+        case IN_H2: p = a.h2 + ((long)cur * a.R + r) * H + k; break;
+        case IN_T1A2: p = k < H ? a.t1 + (long)r * H + k : nullptr; break;
+        case IN_T2A3: p = k < H ? a.t2 + (long)r * H + k : nullptr; break;
+        default: p = k < a.Fc ? a.y1 + (long)r * a.Fc + k : nullptr; break;
+      }
+      if (which != IN_XI) {
+        if (p) {
+          x = *reinterpret_cast<const float4*>(p);
+        } else if (q < a.Ltot) {  // the layer's aux slice
+          const int kv = which == IN_Y1A4 ? a.Fc : H;
+          const int off = (which == IN_T1A2 ? 1 : which == IN_T2A3 ? 2 : 3) * a.A + (k - kv);
+          x = *reinterpret_cast<const float4*>(a.auxf + ((long)src * a.Tf + q / a.hop) * a.auxd + off);
+        }
+      }
+    }
+    v[m] = x;
+  }
+}
+__device__ __forceinline__ void stage_store(int K, const float4 (&v)[kStage4], float* xs) {
+  const int K4 = K >> 2;
+#pragma unroll
+  for (int m = 0; m < kStage4; ++m) {
+    const int e = threadIdx.x + 256 * m;
+    if (e < kRC * K4) reinterpret_cast<float4*>(xs)[e] = v[m];
+  }
 }
 
-constexpr int kRB = 8;   // fold rows per register batch
-constexpr int kKJ = 9;   // k = lane + 64 j, j < kKJ: K <= 576
+// This wave's NG output rows against the kRC staged rows: lane holds float4 k4 = lane + 64 j4 of
+// each row's weights (wv) and reads the same float4 of every staged row; acc[g][rr].
+template <int NG>
+__device__ __forceinline__ void rows_dot(const float4 (&wv)[NG][kJ4], const float* xs, int K, int lane,
+                                         float (&acc)[NG][kRC]) {
+  const int K4 = K >> 2;
+  const float4* xs4 = reinterpret_cast<const float4*>(xs);
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int rr = 0; rr < kRC; ++rr) acc[g][rr] = 0.f;
+#pragma unroll
+  for (int j = 0; j < kJ4; ++j) {
+    const int k4 = lane + 64 * j;
+    if (k4 < K4) {
+#pragma unroll
+      for (int rr = 0; rr < kRC; ++rr) {
+        const float4 x = xs4[rr * K4 + k4];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          float t = acc[g][rr];
+          t = fmaf(wv[g][j].x, x.x, t);
+          t = fmaf(wv[g][j].y, x.y, t);
+          t = fmaf(wv[g][j].z, x.z, t);
+          acc[g][rr] = fmaf(wv[g][j].w, x.w, t);
+        }
+      }
+    }
+  }
+}
+
+// float4 k4 of weight row `row` (K % 4 == 0), zero past K
+__device__ __forceinline__ float4 wrow4(const float* W, long row, int K, int k4) {
+  return k4 < (K >> 2) ? reinterpret_cast<const float4*>(W + row * K)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Lane partials -> sums: every lane writes its NG x kRC partials as a column of red[w][.][lane],
+// then thread t sums row t over the 64 lanes (fixed order) into sums[t] (t < 4 * NG * kRC).
+template <int NG>
+__device__ __forceinline__ void reduce_lanes(const float (&acc)[NG][kRC], int w, int lane, float* red,
+                                             float* sums) {
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int rr = 0; rr < kRC; ++rr) red[((w * NG + g) * kRC + rr) * kRP + lane] = acc[g][rr];
+  __syncthreads();
+  for (int t = threadIdx.x; t < 4 * NG * kRC; t += 256) {
+    const float* row = red + t * kRP;
+    float s = 0.f;
+#pragma unroll 8
+    for (int l = 0; l < 64; ++l) s += row[l];
+    sums[t] = s;
+  }
+  __syncthreads();
+}
 
 // GRU layer WHICH (1: rnn1 on xI; 2: rnn2 on [t1, a2]) for two hidden units per workgroup.
-// Waves 0/1: the input gates (r, z, n rows) of units u0 / u0+1, waves 2/3: their hidden gates;
-// lanes split K, a wave sum reduces.  torch's GRU cell order (aten RNN.cpp GRUCell):
-// r = σ(gh_r + gi_r), z = σ(gh_z + gi_z), n = tanh(gi_n + gh_n·r), h' = (h − n)·z + n.
+// Waves 0/1: the input gates (r, z, n rows) of units u0 / u0+1, waves 2/3: their hidden gates.
+// torch's GRU cell order (aten RNN.cpp GRUCell): r = σ(gh_r + gi_r), z = σ(gh_z + gi_z),
+// n = tanh(gi_n + gh_n·r), h' = (h − n)·z + n.
 template <int WHICH>
 __global__ __launch_bounds__(256) void wr_gru_kernel(WrStep a) {
   const int i = cur_step(a);
   if (i >= a.L) return;
-  __shared__ float gates[4][3][kRB];
+  constexpr int KI = 576;  // staging row capacity (checked on the host: H + A <= 576)
+  __shared__ float smem[kRC * (KI + 512) > 4 * 3 * kRC * kRP ? kRC * (KI + 512) : 4 * 3 * kRC * kRP];
+  __shared__ float sums[4 * 3 * kRC];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = a.H, R = a.R;
   const int u0 = blockIdx.x * 2;
@@ -196,114 +309,102 @@ __global__ __launch_bounds__(256) void wr_gru_kernel(WrStep a) {
   const int K = hid ? H : Kin;
   const float* W = hid ? (WHICH == 1 ? a.Whh1 : a.Whh2) : (WHICH == 1 ? a.Wih1 : a.Wih2);
   const int cur = i & 1;
-  const float* hprev = (WHICH == 1 ? a.h1 : a.h2) + (long)cur * R * H;
-  float* hnext = (WHICH == 1 ? a.h1 : a.h2) + (long)(cur ^ 1) * R * H;
-  float wv[3][kKJ];
+  float4 wv[3][kJ4];
 #pragma unroll
   for (int g = 0; g < 3; ++g)
 #pragma unroll
-    for (int j = 0; j < kKJ; ++j) {
-      const int k = lane + 64 * j;
-      wv[g][j] = k < K ? W[(long)(g * H + u) * K + k] : 0.f;
+    for (int j = 0; j < kJ4; ++j) wv[g][j] = wrow4(W, (long)g * H + u, K, lane + 64 * j);
+  float* xin = smem;             // [kRC][Kin]
+  float* xh = smem + kRC * Kin;  // [kRC][H]
+  const float* bi = WHICH == 1 ? a.bih1 : a.bih2;
+  const float* bh = WHICH == 1 ? a.bhh1 : a.bhh2;
+  float* hb = WHICH == 1 ? a.h1 : a.h2;
+  for (int rb = 0; rb < R; rb += kRC) {
+    // epilogue operands of thread (unit uu, row rr), fetched with the staging loads
+    const int nr = min(kRC, R - rb);
+    const int uu = tid & 1, rr0 = tid >> 1, un = u0 + uu, r0 = rb + rr0;
+    const bool ep = tid < 2 * nr;
+    float ebi[3], ebh[3], ehp = 0.f, ex = 0.f;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      ebi[g] = bi[g * H + un];
+      ebh[g] = bh[g * H + un];
     }
-  for (int rb = 0; rb < R; rb += kRB) {
-    const int nr = min(kRB, R - rb);
-    float acc[3][kRB];
-#pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-      for (int rr = 0; rr < kRB; ++rr) acc[g][rr] = 0.f;
-#pragma unroll
-    for (int rr = 0; rr < kRB; ++rr) {
-      if (rr >= nr) continue;
-      const int r = rb + rr;
-      int src;
-      long q;
-      fold_pos(a, r, i, src, q);
-      const float xp = xprev_at(a, r, i);
-#pragma unroll
-      for (int j = 0; j < kKJ; ++j) {
-        const int k = lane + 64 * j;
-        if (k >= K) continue;
-        float v;
-        if (hid) v = hprev[(long)r * H + k];
-        else if (WHICH == 1) v = a.pI[((long)src * (a.Ltot + 1) + q) * H + k] + a.WI[(long)k * a.wi_ld] * xp;
-        else v = k < H ? a.t1[(long)r * H + k] : aux_at(a, src, q, a.A + (k - H));
-#pragma unroll
-        for (int g = 0; g < 3; ++g) acc[g][rr] = fmaf(wv[g][j], v, acc[g][rr]);
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-      for (int rr = 0; rr < kRB; ++rr) {
-        const float s = wave_sum(acc[g][rr]);
-        if (lane == 0) gates[w][g][rr] = s;
-      }
-    __syncthreads();
-    if (tid < 2 * nr) {
-      const int uu = tid & 1, rr = tid >> 1, r = rb + rr;
-      const int un = u0 + uu;
-      const float* bi = WHICH == 1 ? a.bih1 : a.bih2;
-      const float* bh = WHICH == 1 ? a.bhh1 : a.bhh2;
-      const float gi_r = gates[uu][0][rr] + bi[un], gi_z = gates[uu][1][rr] + bi[H + un],
-                  gi_n = gates[uu][2][rr] + bi[2 * H + un];
-      const float gh_r = gates[2 + uu][0][rr] + bh[un], gh_z = gates[2 + uu][1][rr] + bh[H + un],
-                  gh_n = gates[2 + uu][2][rr] + bh[2 * H + un];
-      const float rg = sigmoidf_(gh_r + gi_r), zg = sigmoidf_(gh_z + gi_z);
-      const float ng = tanhf(gi_n + gh_n * rg);
-      const float hp = hprev[(long)r * H + un];
-      const float hn = (hp - ng) * zg + ng;
-      hnext[(long)r * H + un] = hn;
-      if (WHICH == 1) {  // x = x + h1 (model.py:269), x = I(...) recomputed for this unit
+    if (ep) {
+      ehp = hb[((long)cur * R + r0) * H + un];
+      if (WHICH == 1) {
         int src;
         long q;
-        fold_pos(a, r, i, src, q);
-        const float xi = a.pI[((long)src * (a.Ltot + 1) + q) * H + un] + a.WI[(long)un * a.wi_ld] * xprev_at(a, r, i);
-        a.t1[(long)r * H + un] = xi + hn;
-      } else {           // x = x + h2 (model.py:273)
-        a.t2[(long)r * H + un] = a.t1[(long)r * H + un] + hn;
+        fold_pos(a, r0, i, src, q);
+        ex = a.pI[((long)src * (a.Ltot + 1) + q) * H + un] + a.wi0[un] * xprev_at(a, r0, i);
+      } else {
+        ex = a.t1[(long)r0 * H + un];
       }
+    }
+    {
+      float4 v0[kStage4], v1[kStage4];
+      stage_load(a, WHICH == 1 ? IN_XI : IN_T1A2, i, rb, Kin, v0);
+      stage_load(a, WHICH == 1 ? IN_H1 : IN_H2, i, rb, H, v1);
+      stage_store(Kin, v0, xin);
+      stage_store(H, v1, xh);
+    }
+    __syncthreads();
+    float acc[3][kRC];
+    rows_dot<3>(wv, hid ? xh : xin, K, lane, acc);
+    __syncthreads();  // staged rows fully read: the partial transpose reuses the space
+    reduce_lanes<3>(acc, w, lane, smem, sums);
+    if (ep) {
+      const float* gi = sums + (uu * 3) * kRC + rr0;        // wave uu: input gates
+      const float* gh = sums + ((2 + uu) * 3) * kRC + rr0;  // wave 2 + uu: hidden gates
+      const float gi_r = gi[0] + ebi[0], gi_z = gi[kRC] + ebi[1], gi_n = gi[2 * kRC] + ebi[2];
+      const float gh_r = gh[0] + ebh[0], gh_z = gh[kRC] + ebh[1], gh_n = gh[2 * kRC] + ebh[2];
+      const float rg = sigmoidf_(gh_r + gi_r), zg = sigmoidf_(gh_z + gi_z);
+      const float ng = tanhf(gi_n + gh_n * rg);
+      const float hn = (ehp - ng) * zg + ng;
+      hb[((long)(cur ^ 1) * R + r0) * H + un] = hn;
+      // x = I(...) + h1 (model.py:269) after rnn1, x + h2 (model.py:273) after rnn2
+      (WHICH == 1 ? a.t1 : a.t2)[(long)r0 * H + un] = ex + hn;
     }
     __syncthreads();
   }
 }
 
 // fc1 / fc2 (model.py:274-278): y = relu(W · [v, a] + b), v = t2 (WHICH 1, a = a3) or y1
-// (WHICH 2, a = a4); one output row per wave, four per workgroup.
+// (WHICH 2, a = a4); two output rows per wave, eight per workgroup.
 template <int WHICH>
 __global__ __launch_bounds__(256) void wr_fc_kernel(WrStep a) {
   const int i = cur_step(a);
   if (i >= a.L) return;
+  __shared__ float smem[kRC * 576 > 4 * 2 * kRC * kRP ? kRC * 576 : 4 * 2 * kRC * kRP];
+  __shared__ float sums[4 * 2 * kRC];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int n = blockIdx.x * 4 + w;
   const int Kv = WHICH == 1 ? a.H : a.Fc, K = Kv + a.A;
   const float* W = WHICH == 1 ? a.W1 : a.W2;
   const float* bias = WHICH == 1 ? a.b1 : a.b2;
-  const float* vin = WHICH == 1 ? a.t2 : a.y1;
   float* y = WHICH == 1 ? a.y1 : a.y2;
-  const int aoff = (WHICH == 1 ? 2 : 3) * a.A;
-  if (n >= a.Fc) return;
-  float wv[kKJ];
+  const int n0 = blockIdx.x * 8 + 2 * w;
+  float4 wv[2][kJ4];
 #pragma unroll
-  for (int j = 0; j < kKJ; ++j) {
-    const int k = lane + 64 * j;
-    wv[j] = k < K ? W[(long)n * K + k] : 0.f;
-  }
-  for (int r = 0; r < a.R; ++r) {
-    int src;
-    long q;
-    fold_pos(a, r, i, src, q);
-    float acc = 0.f;
+  for (int g = 0; g < 2; ++g)
 #pragma unroll
-    for (int j = 0; j < kKJ; ++j) {
-      const int k = lane + 64 * j;
-      if (k >= K) continue;
-      const float v = k < Kv ? vin[(long)r * Kv + k] : aux_at(a, src, q, aoff + (k - Kv));
-      acc = fmaf(wv[j], v, acc);
+    for (int j = 0; j < kJ4; ++j) wv[g][j] = wrow4(W, min(n0 + g, a.Fc - 1), K, lane + 64 * j);
+  for (int rb = 0; rb < a.R; rb += kRC) {
+    {
+      float4 v0[kStage4];
+      stage_load(a, WHICH == 1 ? IN_T2A3 : IN_Y1A4, i, rb, K, v0);
+      stage_store(K, v0, smem);
     }
-    acc = wave_sum(acc);
-    if (lane == 0) y[(long)r * a.Fc + n] = fmaxf(acc + bias[n], 0.f);
+    __syncthreads();
+    float acc[2][kRC];
+    rows_dot<2>(wv, smem, K, lane, acc);
+    __syncthreads();
+    reduce_lanes<2>(acc, w, lane, smem, sums);
+    const int nr = min(kRC, a.R - rb);
+    for (int t = tid; t < 8 * nr; t += 256) {  // (output row, fold row)
+      const int o = t / nr, rr = t - o * nr, n = blockIdx.x * 8 + o;
+      if (n < a.Fc) y[(long)(rb + rr) * a.Fc + n] = fmaxf(sums[o * kRC + rr] + bias[n], 0.f);
+    }
+    __syncthreads();
   }
 }
 
@@ -326,24 +427,41 @@ __device__ __forceinline__ float uniform_draw(unsigned long long seed, int r, in
 __global__ __launch_bounds__(256) void wr_out_kernel(WrStep a) {
   const int i = cur_step(a);
   if (i >= a.L) return;
+  __shared__ float red[4 * 8 * kRP];
   __shared__ float lg[64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = blockIdx.x, Fc = a.Fc, NC = a.NC;
-  float yv[kKJ];
+  float4 yv[kJ4];
 #pragma unroll
-  for (int j = 0; j < kKJ; ++j) {
-    const int k = lane + 64 * j;
-    yv[j] = k < Fc ? a.y2[(long)r * Fc + k] : 0.f;
-  }
-  for (int c = w; c < NC; c += 4) {
-    float acc = 0.f;
+  for (int j = 0; j < kJ4; ++j) yv[j] = wrow4(a.y2, r, Fc, lane + 64 * j);
+  // class c = w + 4 m (m < 8, NC <= 32): lanes over float4 k, one transpose-reduction through LDS
+  float acc[8];
 #pragma unroll
-    for (int j = 0; j < kKJ; ++j) {
-      const int k = lane + 64 * j;
-      if (k < Fc) acc = fmaf(a.W3[(long)c * Fc + k], yv[j], acc);
+  for (int m = 0; m < 8; ++m) {
+    const float4* wr = reinterpret_cast<const float4*>(a.W3 + (long)min(w + 4 * m, NC - 1) * Fc);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kJ4; ++j) {
+      const float4 v = wr[min(lane + 64 * j, (Fc >> 2) - 1)];  // yv is zero past Fc
+      s = fmaf(v.x, yv[j].x, s);
+      s = fmaf(v.y, yv[j].y, s);
+      s = fmaf(v.z, yv[j].z, s);
+      s = fmaf(v.w, yv[j].w, s);
     }
-    acc = wave_sum(acc);
-    if (lane == 0) lg[c] = acc + a.b3[c];
+    acc[m] = s;
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) red[(w * 8 + m) * kRP + lane] = acc[m];
+  __syncthreads();
+  if (tid < 32) {
+    const int ww = tid & 3, m = tid >> 2, c = ww + 4 * m;
+    if (c < NC) {
+      const float* row = red + (ww * 8 + m) * kRP;
+      float s = 0.f;
+#pragma unroll 8
+      for (int l = 0; l < 64; ++l) s += row[l];
+      lg[c] = s + a.b3[c];
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -385,6 +503,10 @@ __global__ __launch_bounds__(256) void wr_out_kernel(WrStep a) {
       __hip_atomic_store(a.step, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+__global__ void wr_column_kernel(int n, long ld, const float* __restrict__ W, float* __restrict__ col) {
+  for (int k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) col[k] = W[(long)k * ld];
 }
 
 __global__ void wr_init_state_kernel(int R, int H, int Fc, int* step, int* done, float* x_prev, float* h1,
@@ -444,8 +566,8 @@ constexpr int kChunk = 32;  // sample steps per captured graph
 int launch_step(const WrStep& a, hipStream_t s) {
   wr_gru_kernel<1><<<a.H / 2, 256, 0, s>>>(a);
   wr_gru_kernel<2><<<a.H / 2, 256, 0, s>>>(a);
-  wr_fc_kernel<1><<<(a.Fc + 3) / 4, 256, 0, s>>>(a);
-  wr_fc_kernel<2><<<(a.Fc + 3) / 4, 256, 0, s>>>(a);
+  wr_fc_kernel<1><<<(a.Fc + 7) / 8, 256, 0, s>>>(a);
+  wr_fc_kernel<2><<<(a.Fc + 7) / 8, 256, 0, s>>>(a);
   wr_out_kernel<<<a.R, 256, 0, s>>>(a);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
@@ -465,9 +587,12 @@ struct WrDims {
 int check_dims(const WrDims& d) {
   AVC_CHECK_ARG(d.F > 0 && d.F <= 512 && d.C > 0 && d.A4 > 0 && d.A4 % 4 == 0 && d.RB >= 0 && d.RB <= 64,
                 "wavernn: feat_dims, compute_dims, res_out_dims (multiple of 4) or res_blocks out of range");
-  AVC_CHECK_ARG(d.H >= 64 && d.H % 2 == 0 && d.H + d.A4 / 4 <= 64 * kKJ && d.Fc >= 4 && d.Fc + d.A4 / 4 <= 64 * kKJ,
-                "wavernn: rnn_dims / fc_dims must leave rnn_dims + aux_dims and fc_dims + aux_dims <= 576");
-  AVC_CHECK_ARG(d.NC > 0 && d.NC <= 64, "wavernn: n_classes must be 1..64");
+  AVC_CHECK_ARG(d.H >= 64 && d.H <= 512 && d.H % 2 == 0 && d.H + d.A4 / 4 <= 64 * kKJ && d.Fc >= 8 &&
+                    d.Fc + d.A4 / 4 <= 64 * kKJ,
+                "wavernn: need 64 <= rnn_dims <= 512 (even) and rnn_dims + aux_dims, fc_dims + aux_dims <= 576");
+  AVC_CHECK_ARG(d.H % 4 == 0 && d.Fc % 4 == 0 && (d.A4 / 4) % 4 == 0,
+                "wavernn: rnn_dims, fc_dims and res_out_dims / 4 must be multiples of 4 (float4 staging)");
+  AVC_CHECK_ARG(d.NC > 0 && d.NC <= 32, "wavernn: n_classes must be 1..32 (MOL 30, RAW 2 * bits)");
   AVC_CHECK_ARG(d.pad >= 0 && d.f0 > 0 && d.f1 > 0 && d.f2 > 0, "wavernn: bad pad / upsample factors");
   return AVC_OK;
 }
@@ -590,6 +715,8 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
                                                               params[o], params[o + 1], pI);
   AVC_LAUNCH_CHECK();
   AVC_TAKE(ctr, int, 64, sc);
+  AVC_TAKE(wi0, float, H, sc);
+  wr_column_kernel<<<ew(d.H), 256, 0, s>>>(d.H, 1 + d.F + A, params[o], wi0);
   AVC_TAKE(x_prev, float, R, sc);
   AVC_TAKE(h1, float, 2 * R * H, sc);
   AVC_TAKE(h2, float, 2 * R * H, sc);
@@ -607,7 +734,7 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
   a.Tf = Tf; a.Ltot = Ltot; a.stride = stride; a.batched = batched ? 1 : 0; a.mol = mol ? 1 : 0;
   a.teacher = x_teacher ? 1 : 0; a.seed = seed;
   a.step = ctr; a.done = ctr + 32;
-  a.pI = pI; a.auxf = auxf; a.WI = params[o]; a.wi_ld = 1 + d.F + A;
+  a.pI = pI; a.auxf = auxf; a.WI = params[o]; a.wi_ld = 1 + d.F + A; a.wi0 = wi0;
   a.Wih1 = params[o + 2]; a.Whh1 = params[o + 3]; a.bih1 = params[o + 4]; a.bhh1 = params[o + 5];
   a.Wih2 = params[o + 6]; a.Whh2 = params[o + 7]; a.bih2 = params[o + 8]; a.bhh2 = params[o + 9];
   a.W1 = params[o + 10]; a.b1 = params[o + 11]; a.W2 = params[o + 12]; a.b2 = params[o + 13];
@@ -637,8 +764,15 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
       (void)hipGraphDestroy(graph);
       AVC_HIP(ei);
     }
+    // per-step algorithmic work of every fold row (timing class "wavernn", one record per chunk):
+    // GRU1 6·H·H, GRU2 3·H·(H + A) + 3·H·H, fc1 Fc·(H + A), fc2 Fc·(Fc + A), fc3 NC·Fc MACs,
+    // every weight read once per step
+    const double macs = 6.0 * H * H + 3.0 * H * (H + A) + 3.0 * H * H + (double)d.Fc * (H + A) +
+                        (double)d.Fc * (d.Fc + A) + (double)d.NC * d.Fc;
     for (long c = 0; c < chunks; ++c) {
+      hipEvent_t ev = timing_begin(TC_WAVERNN, s);
       const hipError_t el = hipGraphLaunch(exec, s);
+      if (ev) timing_end(TC_WAVERNN, ev, s, kChunk * 2.0 * macs * R, kChunk * 4.0 * macs);
       if (el != hipSuccess) {
         (void)hipGraphExecDestroy(exec);
         (void)hipGraphDestroy(graph);

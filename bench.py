@@ -17,6 +17,8 @@ The SURVEY §8f rows either side of the Generator have their own lines (replicas
 --mode mel  the auto-encoder mel frontend (spectrogram.py:62-142) of one 60 s utterance;
 --mode se   the speaker encoder's embed_utterance (speaker_encoder/model.py:142-194) of one
             10 s utterance (16 kHz mel, 12 partials through the 3-layer LSTM, mean + L2).
+--mode vocoder  the WaveRNN vocoder's generate (wavernn/model.py:214-329) of one 10 s utterance's
+            mel: up-sampling, the batched per-sample loop (20 fold rows x 12,100 steps), cross-fade.
 
 Also reported on the same line: `roofline` for the dominant kernel class, measured with HIP
 events around every launch of that class inside the timed region, and `cpu_baseline`: the CPU
@@ -57,8 +59,12 @@ ROOFLINE = {
     "mel": {"dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS), "gemm": ("mfma", PEAK_FP32_MATRIX_TFLOPS)},
     "se": {"lstm_step_fwd": ("hbm", PEAK_HBM_GBS), "gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
            "dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS)},
+    # the sample loop re-reads every loop weight (15.1 MB) once per step from the XCD L2s; priced
+    # against HBM bandwidth as the streaming ceiling, the loop itself is bound by its 5 dependent
+    # launches per step
+    "vocoder": {"wavernn": ("hbm", PEAK_HBM_GBS)},
 }
-MEL_SECONDS, SE_SECONDS = 60, 10
+MEL_SECONDS, SE_SECONDS, VOC_SECONDS = 60, 10, 10
 # fp32 storage and accumulation; contractions as 3 f16 MFMA products of hi/lo-split operands
 # (22 significant bits per operand, range-guarded), DESIGN.md §3
 DTYPE = "f32 (3xf16 split, fp32 accumulate)"
@@ -70,7 +76,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["fwd", "train", "long", "mel", "se"], default="fwd")
+    ap.add_argument("--mode", choices=["fwd", "train", "long", "mel", "se", "vocoder"], default="fwd")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 64 fwd / 256 train)")
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample")
@@ -121,6 +127,8 @@ def main():
         m = setup_long(args, dev, rank)
     elif args.mode == "mel":
         m = setup_mel(args, dev, rank)
+    elif args.mode == "vocoder":
+        m = setup_vocoder(args, dev, rank)
     else:
         m = setup_se(args, dev, rank)
     step = m["step"]
@@ -475,6 +483,53 @@ def setup_se(args, dev, rank):
         "config": lambda world: {"workload": f"one {SE_SECONDS} s utterance per GPU per step (12 partials x 160 "
                                              "frames), embed_utterance incl. its mel frontend",
                                  "global_batch": world, "parallelism": f"replicas x{world}"},
+        "cpu": cpu,
+    }
+
+
+def setup_vocoder(args, dev, rank):
+    """WaveRNN generate (wavernn/model.py:214-329) of one 10 s utterance's 80-mel (802 frames):
+    batched fold (target 11,000, overlap 550) -> 20 rows x 12,100 sequential sample steps."""
+    from autovc_amd.wavernn import WaveRNN
+    from autovc_amd.weights import synthetic_mel, wavernn_state_dict
+
+    sr, hop = 22050, 275
+    T = VOC_SECONDS * sr // hop
+    sd = wavernn_state_dict(0)
+    net = WaveRNN(device=dev)
+    net.load_state_dict(sd)
+    mel_np = synthetic_mel(31 + rank, 1, T)
+    mel = torch.from_numpy(mel_np).to(dev)
+    audio_s = (T - 1) * hop / sr
+
+    def step():
+        return net.generate(mel)
+
+    def cpu(out):
+        from oracle import wavernn_oracle as wo
+        cores = min(16, len(os.sched_getaffinity(0)))
+        torch.set_num_threads(cores)
+        n = 60
+        wo.generate(sd, torch.from_numpy(mel_np), steps=4)  # warm
+        t1 = time.perf_counter()
+        part = wo.generate(sd, torch.from_numpy(mel_np), steps=n)
+        dt = time.perf_counter() - t1
+        L = 11_000 + 2 * 550
+        per_call = dt / n * L
+        return ({"value": round(audio_s / per_call, 3), "unit": "audio-seconds/s", "cores": cores, "kind": "port",
+                 "sample": f"the first {n} of the {L} sequential steps (all {part.shape[0]} fold rows) of the same "
+                           f"generate() through the oracle (torch-CPU, {torch.get_num_threads()} threads), "
+                           f"extrapolated linearly to the whole loop (every step is the same work)"},
+                {"fold_rows": int(part.shape[0]), "sequential_steps": L})
+
+    return {
+        "step": step, "units_per_step": audio_s, "unit": "audio-seconds/s", "dtype": "f32",
+        "metric": "audio-seconds/sec WaveRNN generate (MOL, batched: target 11000, overlap 550)",
+        "data": "synthetic U[0,1) 80-mel of a 10 s utterance; seeded synthetic weights (no checkpoint offline)",
+        "classes": ["wavernn"],
+        "config": lambda world: {"workload": f"one {VOC_SECONDS} s utterance per GPU ({T} mel frames -> "
+                                             f"{(T - 1) * hop} samples), WaveRNN.generate incl. up-sampling and "
+                                             "cross-fade", "global_batch": world, "parallelism": f"replicas x{world}"},
         "cpu": cpu,
     }
 

@@ -54,6 +54,8 @@ for step in "$@"; do
     proflong) run proflong 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/proflong -o long -- python3 bench.py --mode long --steps 5 --warmup 2 --no-cpu --no-timing ;;
     benchmel) run benchmel 400 python bench.py --mode mel --steps 10 --warmup 2 ;;
     benchse) run benchse 400 python bench.py --mode se --steps 10 --warmup 2 ;;
+    benchvoc) run benchvoc 400 python bench.py --mode vocoder --steps 3 --warmup 1 ;;
+    profvoc) run profvoc 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profvoc -o voc -- python3 bench.py --mode vocoder --steps 2 --warmup 1 --no-cpu --no-timing ;;
     profmel) run profmel 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profmel -o mel -- python3 bench.py --mode mel --steps 10 --warmup 2 --no-cpu --no-timing ;;
     profse) run profse 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profse -o se -- python3 bench.py --mode se --steps 10 --warmup 2 --no-cpu --no-timing ;;
     *) echo "unknown step $step"; exit 2 ;;
