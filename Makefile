@@ -26,6 +26,26 @@ clean:
 
 .PHONY: all clean check-abi
 
+# Host-side AddressSanitizer + UndefinedBehaviorSanitizer build of the whole library linked into
+# tests/host_sanitize/abi_driver.cpp (the sanitizers instrument HOST code only: every -fsanitize
+# sits behind -Xarch_host; GPU code is compiled as usual).  `make sanitize` builds and runs it.
+SAN_FLAGS := -O2 -g -std=c++17 -fno-omit-frame-pointer -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+             -Xarch_host -fno-sanitize-recover=undefined
+SAN_OBJ   := $(patsubst autovc_amd/csrc/%.hip,build/sanitize/%.o,$(SRC))
+SAN_BIN   := tests/host_sanitize/abi_driver
+
+build/sanitize/%.o: autovc_amd/csrc/%.hip $(HDR)
+	@mkdir -p build/sanitize
+	$(HIPCC) --offload-arch=$(ARCH) $(SAN_FLAGS) -c $< -o $@
+
+$(SAN_BIN): $(SAN_OBJ) tests/host_sanitize/abi_driver.cpp include/autovc_hip.h
+	$(HIPCC) --offload-arch=$(ARCH) $(SAN_FLAGS) $(SAN_OBJ) tests/host_sanitize/abi_driver.cpp -o $@
+
+sanitize: $(SAN_BIN)
+	ASAN_OPTIONS=protect_shadow_gap=0:detect_leaks=1:abort_on_error=1 LSAN_OPTIONS=suppressions=tests/host_sanitize/lsan.supp UBSAN_OPTIONS=print_stacktrace=1 ./$(SAN_BIN)
+
+.PHONY: sanitize
+
 # diagnostic build with in-kernel s_memtime stamps (never shipped): diag/libautovc_hip_stamps.so
 stamps:
 	@mkdir -p diag
