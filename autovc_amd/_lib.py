@@ -53,6 +53,7 @@ _SIGS = {
     "avc_clip_adam_ema": [_P, _Z, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, ctypes.c_double, _P, _P],
     "avc_timing_enable": [_I],
     "avc_lstm_tune": [_I, _I],
+    "avc_bptt_mode": [_I],
     "avc_lstm_split_tune": [_I, _I, _I],
     "avc_gemm_tune": [_I],
     "avc_gemm_config": [_I],

@@ -57,6 +57,12 @@ int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream);
 size_t gemm_afrag_bytes(long rows, int K);
 // true when gemm_run would stream this product from split fragments (so a_frag is honoured)
 bool gemm_frag_eligible(const GemmDesc& d);
+// slab[split][M][N] = raw split-K partials of A_frag(M x K) . B_frag(N x K)^T (both split by
+// gemm_split_frag / split_frag32_kernel; tile 64 or 128); no scale, bias or epilogue
+int gemm_frag_partials(int M, int N, int K, const _Float16* As, const _Float16* Bs, int tile, int nsplit,
+                       float* slab, hipStream_t s);
+// [R][K] fp32 (row stride rs) -> fragment-major split, scaled by the power of two of *amax
+int gemm_split_frag(const float* src, long rs, int R, int K, const unsigned* amax, _Float16* dst, hipStream_t s);
 // max |x| of a rows x cols region (row stride ld) into *out (float bits), for GemmDesc::amax_a
 int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t stream);
 

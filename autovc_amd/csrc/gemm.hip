@@ -1185,6 +1185,42 @@ int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, 
 }
 
 size_t gemm_afrag_bytes(long rows, int K) { return frag_bytes(rows, K); }
+
+// Raw split-K partial products of two operands already split into the fragment-major layout
+// (split_frag32_kernel): slab[split][M][N] = A_frag(M x K) . B_frag(N x K)^T, no scale, no
+// epilogue.  The BPTT recurrence (lstm.hip) reduces the slabs in its own epilogue.
+int gemm_frag_partials(int M, int N, int K, const _Float16* As, const _Float16* Bs, int tile, int nsplit,
+                       float* slab, hipStream_t s) {
+  AVC_CHECK_ARG(M > 0 && N > 0 && K > 0 && As && Bs && slab && nsplit >= 1 && (tile == 64 || tile == 128),
+                "gemm_frag_partials: bad arguments");
+  GemmDesc d;
+  d.M = M; d.N = N; d.Kc = K; d.ntaps = 1;
+  Frag16Args f{};
+  f.As = As; f.a_ntile = (int)frag_ntile(M); f.a_nkc = frag_nkc(K); f.a_shift0 = 0; f.a_tapshift = 0;
+  f.Bs = Bs; f.b_ntile = (int)frag_ntile(N); f.b_nkc = frag_nkc(K);
+  f.b_tapstride = (long)f.b_ntile * f.b_nkc * 1024;  // halves: the descriptor covers all of B
+  Plan p{};
+  p.bm = p.bn = tile;
+  p.tilesM = (M + tile - 1) / tile;
+  p.tilesN = (N + tile - 1) / tile;
+  p.nsplit = nsplit;
+  if (tile == 128) launch16f_cfg<128, 128, 4, 2, 2, 4>(d, f, p, slab, s);
+  else launch16f_cfg<64, 64, 2, 2, 4, 2>(d, f, p, slab, s);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+// split a [R][K] row-major fp32 matrix (row stride rs) into the fragment-major layout, scaled
+// by the power of two split_scale_of(amax) (amax NULL: unscaled)
+int gemm_split_frag(const float* src, long rs, int R, int K, const unsigned* amax, _Float16* dst, hipStream_t s) {
+  const long ntile = frag_ntile(R);
+  const int nkc = frag_nkc(K);
+  const long total = ntile * 32 * nkc * 2;
+  split_frag32_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(src, rs, 1, R, K, (int)ntile,
+                                                                                   nkc, dst, amax);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
 bool gemm_frag_eligible(const GemmDesc& d) { return frag16_eligible(d); }
 
 size_t gemm_scratch_bytes(const GemmDesc& d) {

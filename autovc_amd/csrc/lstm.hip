@@ -393,6 +393,108 @@ __global__ __launch_bounds__(512) void lstm_step_kernel(StepArgs a) {
   AVC_STAMP(4);
 }
 
+// ---- BPTT as split-K 3xf16 products + a per-batch-row epilogue ---------------------------
+//
+// lstm_step_kernel's backward step gives each workgroup 16 hidden units x 64 batch rows over the
+// whole K = 4H, so every one of its 256 workgroups re-reads 1 MB of dG per step (320 MB chip-wide,
+// intake-bound at ~40 GB/s per CU: 32 us per H = 1024 step at B = 256).  Here one step is
+//   1. gemm_frag_partials: slab[s] = dG_{t+1} . W_hh over K-split s, 3xf16 on pre-split operands
+//      (128x128 tiles, split-K to ~256 workgroups: ~256 KB of operands per CU);
+//   2. bptt_row_kernel (one workgroup per batch row): dh = dy_t + sum_s slab[s] (unscaled),
+//      the gate derivatives, dc, the fp32 dG_t row, and dG_t split for the next step's product.
+// The split needs a power-of-two operand scale; a product's A rows may be scaled independently
+// (diag(s) A W = diag(s) (A W)), so each row b of dG_t is scaled from its own max |dG_t[b, :]|,
+// known inside its workgroup, and the next epilogue unscales row b by 1 / (s_b s_w).  W_hh is
+// split once per call with the scale of its max |W|.
+struct BpttArgs {
+  int B, H, nsplit, first, last;
+  const float* slab;       // [nsplit][B][H] raw partials (first: unused)
+  float* rowscale;         // [B] power-of-two scale of the row's split dG (read, then replaced)
+  const unsigned* amax_w;  // max |W_hh| (float bits)
+  const float* dy; long lddy;
+  const float* gates; const float* c_cur; const float* c_prv;
+  float* dc;               // [B][H] carried cell-state gradient
+  float* dg_out;           // [B][4H] fp32 dG_t (permuted gate order)
+  _Float16* dgs;           // fragment-major split dG_t (rows padded to 32), for the next product
+};
+
+__device__ __forceinline__ float pow2_scale(float m) {  // max |x| -> [2^14, 2^15) (split_scale_of)
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, 15 - e);
+}
+
+template <int UPT, int NS>  // hidden units per thread (H / 256), K-splits of the partial slabs
+__global__ __launch_bounds__(256) void bptt_row_kernel(BpttArgs a) {
+  constexpr int NT = 256;
+  const int H = a.H, G4 = 4 * H, b = blockIdx.x, tid = threadIdx.x;
+  extern __shared__ float row[];  // [4H] the dG_t row, permuted order
+  __shared__ float red[NT / 64];
+  const float unscale = a.first ? 0.f : 1.f / (a.rowscale[b] * pow2_scale(__uint_as_float(*a.amax_w)));
+  // every operand of the row first (UPT x NS partials and the epilogue operands in flight
+  // together), then the arithmetic; partials summed in split order
+  float part[UPT][NS];
+#pragma unroll
+  for (int m = 0; m < UPT; ++m)
+#pragma unroll
+    for (int sp = 0; sp < NS; ++sp)
+      part[m][sp] = a.first ? 0.f : a.slab[((long)sp * a.B + b) * H + tid + NT * m];
+  float mx = 0.f;
+#pragma unroll
+  for (int m = 0; m < UPT; ++m) {
+    const int j = tid + NT * m;
+    float rec = 0.f;
+#pragma unroll
+    for (int sp = 0; sp < NS; ++sp) rec += part[m][sp];
+    rec *= unscale;
+    const float dh = a.dy[(long)b * a.lddy + j] + rec;
+    const long pb = (long)b * G4 + (j >> 2) * 16 + (j & 3);
+    const float ig = a.gates[pb], fg = a.gates[pb + 4], gg = a.gates[pb + 8], og = a.gates[pb + 12];
+    const float c = a.c_cur[(long)b * H + j], cp = a.c_prv ? a.c_prv[(long)b * H + j] : 0.f;
+    const float tc = tanhf(c);
+    const float dct = dh * og * (1.f - tc * tc) + a.dc[(long)b * H + j];
+    a.dc[(long)b * H + j] = dct * fg;
+    const float d0 = dct * gg * ig * (1.f - ig), d1 = dct * cp * fg * (1.f - fg);
+    const float d2 = dct * ig * (1.f - gg * gg), d3 = dh * tc * og * (1.f - og);
+    const int p = (j >> 2) * 16 + (j & 3);
+    row[p] = d0;
+    row[p + 4] = d1;
+    row[p + 8] = d2;
+    row[p + 12] = d3;
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(d0), fabsf(d1)), fmaxf(fabsf(d2), fabsf(d3))));
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  const float sb = pow2_scale(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  // the fp32 row (weight gradients, dX) and, for the next step, its split, both from LDS
+  float4* out4 = reinterpret_cast<float4*>(a.dg_out + (long)b * G4);
+  for (int q = tid; q < G4 / 4; q += NT) out4[q] = reinterpret_cast<const float4*>(row)[q];
+  if (!a.last) {
+    const int nkc = G4 / 16;
+    for (int g8 = tid; g8 < G4 / 8; g8 += NT) {  // one octet of k per thread (split_frag32 layout)
+      typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+      h8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = row[8 * g8 + e] * sb;
+        const _Float16 h = (_Float16)v;
+        hi[e] = h;
+        lo[e] = (_Float16)((v - (float)h) * 2048.0f);
+      }
+      const long blk = ((long)(b >> 5) * nkc + (g8 >> 1)) * 2;
+      const int lane = (b & 31) + 32 * (g8 & 1);
+      *reinterpret_cast<h8*>(a.dgs + blk * 512 + lane * 8) = hi;
+      *reinterpret_cast<h8*>(a.dgs + (blk + 1) * 512 + lane * 8) = lo;
+    }
+  }
+  __syncthreads();  // every thread read the old row scale before it is replaced
+  if (tid == 0) a.rowscale[b] = sb;
+}
+
+int g_bptt_mode = 1;  // avc_bptt_mode(): 1 = split-K 3xf16 products (default where eligible), 0 = step kernel
+
 struct StepCfg {
   int mb, nw;
 };
@@ -872,6 +974,8 @@ size_t lstm_backward_scratch(int T, int B, int din, int H) {
   size_t s = TB * 4 * H * f + (size_t)B * H * f + (size_t)4 * H * (din + H) * 2 * f +
              (size_t)4 * H * f + 8192;
   s += 2 * ((size_t)B + 64) * 4 * H * f + 512;  // fragment-major dG ping-pong
+  // split-K BPTT (bptt_row_kernel): split W_hh^T, split dG rows, <= 32 partial slabs, row scales
+  s += gemm_afrag_bytes(H, 4 * H) + gemm_afrag_bytes(B + 31, 4 * H) + 32 * (size_t)B * H * f + (size_t)B * f + 2048;
   GemmDesc d1;  // dW_ih
   d1.M = 4 * H; d1.N = din; d1.Kc = (int)TB; d1.a_trans = 1; d1.b_rows = TB;
   d1.prec16 = 1; d1.split_scale = 1;
@@ -900,9 +1004,68 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   float* dwhh_dst = d_w_hh;
   int acc_w = accumulate_dw;
 
+  const bool gemm_bptt = !small && g_bptt_mode >= 1 && B >= 32 && (H == 512 || H == 1024);
   if (small) {
     lstm32_bwd_kernel<<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
     AVC_LAUNCH_CHECK();
+  } else if (gemm_bptt) {
+    // W_hh^T permuted ([H][4H]: row j = hidden unit, k = permuted gate row), split once with the
+    // scale of max |W_hh|; per step the split-K product and the row epilogue (see bptt_row_kernel)
+    AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
+    AVC_TAKE(whhT, float, (size_t)4 * H * H, sc);
+    AVC_TAKE(whhT_s, _Float16, gemm_afrag_bytes(H, 4 * H) / 2, sc);
+    const long arows = (B + 31) / 32 * 32;
+    AVC_TAKE(dgs, _Float16, gemm_afrag_bytes(arows, 4 * H) / 2, sc);
+    AVC_TAKE(dc, float, (size_t)B * H, sc);
+    AVC_TAKE(rowscale, float, (size_t)B, sc);
+    AVC_TAKE(amax_w, unsigned, 64, sc);
+    // tiles and split-K toward ~256 workgroups: 128x128 tiles with 8/16/32 splits of >= two
+    // 64-deep K-tiles (mode 1), or 64x64 tiles with 4/8/16 splits (mode 2: a quarter of the slab
+    // traffic for the row epilogue, twice the operand intake per workgroup)
+    const int tile = g_bptt_mode == 2 ? 64 : 128;
+    const int tiles = (int)((B + tile - 1) / tile) * ((H + tile - 1) / tile);
+    const int ktiles = 4 * H / 64;
+    const int want = std::min(ktiles / 2, (256 + tiles - 1) / tiles);
+    const int nsplit = tile == 64 ? (want >= 16 ? 16 : want >= 8 ? 8 : 4) : (want >= 32 ? 32 : want >= 16 ? 16 : 8);
+    AVC_TAKE(slab, float, (size_t)nsplit * B * H, sc);
+    permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w_ih, wih_p, H, din);
+    transpose_permute_kernel<<<dim3(4 * H / 32, H / 32), 256, 0, s>>>(w_hh, whhT, H);
+    AVC_TRY(zero_async(amax_w, 64 * sizeof(unsigned), s));
+    AVC_TRY(gemm_absmax(w_hh, 4L * H, H, H, amax_w, s));
+    AVC_TRY(gemm_split_frag(whhT, 4L * H, H, 4 * H, amax_w, whhT_s, s));
+    AVC_TRY(zero_async(dc, sizeof(float) * B * H, s));
+    AVC_TRY(zero_async(dgs, gemm_afrag_bytes(arows, 4 * H), s));  // padding rows stay zero
+    AVC_LAUNCH_CHECK();
+    for (int st = T - 1; st >= 0; --st) {
+      const int t = reverse ? T - 1 - st : st;
+      const int tp = reverse ? t + 1 : t - 1;
+      BpttArgs a{};
+      a.B = B; a.H = H; a.nsplit = nsplit; a.first = st == T - 1; a.last = st == 0;
+      // timing class lstm_step_bwd: the whole step (product + row epilogue)
+      hipEvent_t ev = timing_begin(TC_LSTM_STEP_BWD, s);
+      if (!a.first) AVC_TRY(gemm_frag_partials(B, H, 4 * H, dgs, whhT_s, tile, nsplit, slab, s));
+      a.slab = slab; a.rowscale = rowscale; a.amax_w = amax_w;
+      a.dy = d_y + (long)t * B * ldy; a.lddy = ldy;
+      a.gates = saved_gates + (long)t * B * 4 * H;
+      a.c_cur = saved_c + (long)t * B * H;
+      a.c_prv = st > 0 ? saved_c + (long)tp * B * H : nullptr;
+      a.dc = dc; a.dg_out = dg + (long)t * B * 4 * H; a.dgs = dgs;
+#define AVC_BPTT_ROW(NSV)                                                                         \
+  if (H == 1024) bptt_row_kernel<4, NSV><<<B, 256, 4 * H * sizeof(float), s>>>(a);                \
+  else bptt_row_kernel<2, NSV><<<B, 256, 4 * H * sizeof(float), s>>>(a);
+      if (nsplit == 32) { AVC_BPTT_ROW(32) } else if (nsplit == 16) { AVC_BPTT_ROW(16) } else if (nsplit == 8) { AVC_BPTT_ROW(8) } else { AVC_BPTT_ROW(4) }
+#undef AVC_BPTT_ROW
+      AVC_LAUNCH_CHECK();
+      // algorithmic bytes: the split operands of the product, dy / gates / c / dc in, dG / dc out
+      if (ev) timing_end(TC_LSTM_STEP_BWD, ev, s, a.first ? 0.0 : 2.0 * B * H * 4.0 * H,
+                         (a.first ? 0.0 : 4.0 * (4.0 * H * H + 4.0 * B * H)) + 4.0 * B * H * 9.0);
+    }
+    wih_use = wih_p;
+    AVC_TAKE(dwih_p, float, (size_t)4 * H * din, sc);
+    AVC_TAKE(dwhh_p, float, (size_t)4 * H * H, sc);
+    dwih_dst = dwih_p;
+    dwhh_dst = dwhh_p;
+    acc_w = 0;
   } else {
     AVC_TAKE(wih_p, float, (size_t)4 * H * din, sc);
     AVC_TAKE(whhT_p, float, (size_t)4 * H * H, sc);
@@ -999,6 +1162,16 @@ extern "C" int avc_debug_stamps(void* buf, long target_launch) {
   return AVC_OK;
 }
 #endif
+
+extern "C" int avc_bptt_mode(int mode) {
+  if (mode < 0 || mode > 2) {
+    avc::set_error("avc_bptt_mode: mode must be 0 (step kernel), 1 (split-K 3xf16, 128x128 tiles) or 2 (64x64 tiles)");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_bptt_mode = mode;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
 
 extern "C" int avc_lstm_tune(int rows_per_block, int waves) {
   if (!(rows_per_block == 0 || rows_per_block == 16 || rows_per_block == 32 || rows_per_block == 64)) {

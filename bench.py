@@ -44,7 +44,7 @@ PEAK_FP64_MATRIX_TFLOPS = 78.6    # AMD MI355X datasheet (fp64 matrix = fp64 vec
 # Roofline of each timed kernel class.  Forward and backward contractions run as 3 f16 MFMA
 # products per fp32 product, so their fp32-equivalent MFMA ceiling is 2500/3
 # TFLOP/s; the LSTM step streams its (split) weights every time step and is priced against HBM;
-# the BPTT step (lstm_step_bwd) runs on fp32 MFMA.
+# the BPTT step (lstm_step_bwd: split-K 3xf16 product + row epilogue) likewise against 2500/3.
 ROOFLINE = {
     "fwd": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
             "lstm32": ("hbm", PEAK_HBM_GBS), "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
@@ -53,7 +53,7 @@ ROOFLINE = {
              "lstm32": ("hbm", PEAK_HBM_GBS), "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
             "lstm1_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
     "train": {"gemm": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm_step_fwd": ("hbm", PEAK_HBM_GBS),
-              "lstm_step_bwd": ("mfma", PEAK_FP32_MATRIX_TFLOPS), "lstm32": ("hbm", PEAK_HBM_GBS),
+              "lstm_step_bwd": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3), "lstm32": ("hbm", PEAK_HBM_GBS),
               "lstm2_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3),
             "lstm1_persist": ("mfma", PEAK_F16_MATRIX_TFLOPS / 3)},
     "mel": {"dft64": ("mfma", PEAK_FP64_MATRIX_TFLOPS), "gemm": ("mfma", PEAK_FP32_MATRIX_TFLOPS)},

@@ -406,3 +406,39 @@ def test_linear_backward_split_path(cuda_device):
     ops.Linear.apply(xg, wgt, bg).backward(_t(dy, cuda_device))
     rel = lambda a, r: (a.cpu().double() - r).abs().max().item() / r.abs().max().item()
     assert rel(xg.grad, xr.grad) < 2e-6 and rel(wgt.grad, wr.grad) < 2e-6
+
+
+@pytest.mark.parametrize("B,T,din,H,scale", [(64, 12, 512, 1024, 1.0), (48, 9, 320, 512, 1e-9), (256, 4, 512, 1024, 1e5)])
+def test_bptt_split_products_match_fp64(cuda_device, B, T, din, H, scale):
+    """The BPTT recurrence as split-K 3xf16 products with per-row power-of-two scales of dG
+    (avc_bptt_mode(1), the default) and the fp32 step kernel (mode 0) against fp64 autograd;
+    gradient magnitudes from 1e-9 to 1e5 (the scales follow each row's max |dG|)."""
+    g = torch.Generator().manual_seed(B * 7 + H)
+    x = torch.randn(B, T, din, generator=g) * 0.5
+    k = 1.0 / np.sqrt(H)
+    ws = [(torch.rand(*s, generator=g) * 2 - 1) * k for s in [(4 * H, din), (4 * H, H), (4 * H,), (4 * H,)]]
+    dy = torch.randn(B, T, H, generator=g) * scale
+    flat = [w.double().clone().requires_grad_(True) for w in ws]
+    xr = x.double().clone().requires_grad_(True)
+    h0 = torch.zeros(1, B, H, dtype=torch.float64)
+    yr, _, _ = torch.lstm(xr, (h0, h0.clone()), flat, True, 1, 0.0, False, False, True)
+    yr.backward(dy.double())
+    rel = lambda a, r: (a - r).abs().max().item() / r.abs().max().item()
+    grads = {}
+    try:
+        for mode in (1, 0):
+            _lib.call("avc_bptt_mode", mode)
+            xg = _t(x.transpose(0, 1).reshape(T * B, din), cuda_device).requires_grad_(True)
+            wg = [_t(w, cuda_device).requires_grad_(True) for w in ws]
+            yg = ops.LSTMLayer.apply(xg, *wg, T, B, True)
+            yg.backward(_t(dy.transpose(0, 1).reshape(T * B, H), cuda_device))
+            torch.cuda.synchronize()
+            grads[mode] = [xg.grad.cpu().reshape(T, B, din).transpose(0, 1).double()] + \
+                          [w.grad.cpu().double() for w in wg]
+    finally:
+        _lib.call("avc_bptt_mode", 1)
+    refs = [xr.grad] + [w.grad for w in flat]
+    for mode in (1, 0):
+        errs = [rel(a, r) for a, r in zip(grads[mode], refs)]
+        print(f"bptt mode {mode} B={B} H={H} scale={scale:g}: max rel err vs fp64 {max(errs):.2e}")
+        assert max(errs) < 5e-5
