@@ -493,7 +493,7 @@ __global__ __launch_bounds__(256) void bptt_row_kernel(BpttArgs a) {
   if (tid == 0) a.rowscale[b] = sb;
 }
 
-int g_bptt_mode = 1;  // avc_bptt_mode(): 1 = split-K 3xf16 products (default where eligible), 0 = step kernel
+int g_bptt_mode = 1;  // avc_bptt_mode(): 0 = step kernel, 1 = split-K products where faster (H = 1024), 2 = wherever eligible
 
 struct StepCfg {
   int mb, nw;
@@ -1004,7 +1004,10 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   float* dwhh_dst = d_w_hh;
   int acc_w = accumulate_dw;
 
-  const bool gemm_bptt = !small && g_bptt_mode >= 1 && B >= 32 && (H == 512 || H == 1024);
+  // split-K products where they measured faster (scripts/bptt_ab.py, B = 256: H = 1024 7.95 vs
+  // 9.44 ms per layer backward; H = 512 4.02 vs 3.40 ms, so the step kernel stays there)
+  const bool gemm_bptt = !small && B >= 32 && (H == 512 || H == 1024) &&
+                         (g_bptt_mode == 2 || (g_bptt_mode == 1 && H == 1024));
   if (small) {
     lstm32_bwd_kernel<<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
     AVC_LAUNCH_CHECK();
@@ -1019,14 +1022,14 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TAKE(dc, float, (size_t)B * H, sc);
     AVC_TAKE(rowscale, float, (size_t)B, sc);
     AVC_TAKE(amax_w, unsigned, 64, sc);
-    // tiles and split-K toward ~256 workgroups: 128x128 tiles with 8/16/32 splits of >= two
-    // 64-deep K-tiles (mode 1), or 64x64 tiles with 4/8/16 splits (mode 2: a quarter of the slab
-    // traffic for the row epilogue, twice the operand intake per workgroup)
-    const int tile = g_bptt_mode == 2 ? 64 : 128;
+    // 128x128 tiles, split-K toward ~256 workgroups with >= two 64-deep K-tiles each (8, 16 or
+    // 32 splits).  64x64 tiles with 4-16 splits (a quarter of the slab traffic, twice the operand
+    // intake per workgroup) measured 9.13 vs 7.95 ms per H = 1024 layer backward.
+    const int tile = 128;
     const int tiles = (int)((B + tile - 1) / tile) * ((H + tile - 1) / tile);
     const int ktiles = 4 * H / 64;
     const int want = std::min(ktiles / 2, (256 + tiles - 1) / tiles);
-    const int nsplit = tile == 64 ? (want >= 16 ? 16 : want >= 8 ? 8 : 4) : (want >= 32 ? 32 : want >= 16 ? 16 : 8);
+    const int nsplit = want >= 32 ? 32 : want >= 16 ? 16 : 8;
     AVC_TAKE(slab, float, (size_t)nsplit * B * H, sc);
     permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w_ih, wih_p, H, din);
     transpose_permute_kernel<<<dim3(4 * H / 32, H / 32), 256, 0, s>>>(w_hh, whhT, H);
@@ -1053,7 +1056,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
 #define AVC_BPTT_ROW(NSV)                                                                         \
   if (H == 1024) bptt_row_kernel<4, NSV><<<B, 256, 4 * H * sizeof(float), s>>>(a);                \
   else bptt_row_kernel<2, NSV><<<B, 256, 4 * H * sizeof(float), s>>>(a);
-      if (nsplit == 32) { AVC_BPTT_ROW(32) } else if (nsplit == 16) { AVC_BPTT_ROW(16) } else if (nsplit == 8) { AVC_BPTT_ROW(8) } else { AVC_BPTT_ROW(4) }
+      if (nsplit == 32) { AVC_BPTT_ROW(32) } else if (nsplit == 16) { AVC_BPTT_ROW(16) } else { AVC_BPTT_ROW(8) }
 #undef AVC_BPTT_ROW
       AVC_LAUNCH_CHECK();
       // algorithmic bytes: the split operands of the product, dy / gates / c / dc in, dG / dc out
@@ -1165,7 +1168,7 @@ extern "C" int avc_debug_stamps(void* buf, long target_launch) {
 
 extern "C" int avc_bptt_mode(int mode) {
   if (mode < 0 || mode > 2) {
-    avc::set_error("avc_bptt_mode: mode must be 0 (step kernel), 1 (split-K 3xf16, 128x128 tiles) or 2 (64x64 tiles)");
+    avc::set_error("avc_bptt_mode: mode must be 0 (step kernel), 1 (automatic) or 2 (split-K products wherever eligible)");
     return AVC_ERR_INVALID;
   }
   avc::g_bptt_mode = mode;

@@ -214,9 +214,10 @@ int avc_timing_enable(int mask);
 /* Tuning hook for the per-step LSTM kernel: force the batch rows per workgroup (16/32/64) and the
  * number of waves splitting the reduction (1..8); 0 restores the automatic choice. */
 int avc_lstm_tune(int rows_per_block, int waves);
-/* BPTT recurrence of H = 512 / 1024 LSTMs with batch >= 32 (training backward): 1 = per step a
- * split-K 3xf16 product on pre-split operands + a per-batch-row epilogue (default), 0 = the
- * fp32 step kernel (lstm_step_kernel). */
+/* BPTT recurrence of H = 512 / 1024 LSTMs with batch >= 32 (training backward): per step a
+ * split-K 3xf16 product on pre-split operands + a per-batch-row epilogue, or the fp32 step
+ * kernel (lstm_step_kernel).  0 = step kernel always, 1 = split-K where it measured faster
+ * (H = 1024; default), 2 = split-K wherever eligible. */
 int avc_bptt_mode(int mode);
 /* Tuning hook for the split-fp16 forward step (lstm_split.hip): force the K range per workgroup
  * (a multiple of 32) and the 16-column gate blocks per workgroup tile (1 or 4); 0 = automatic.
