@@ -16,6 +16,12 @@ namespace avc {
 namespace {
 
 constexpr int BK = 32;
+#ifndef AVC_GEMM_NOLOAD
+#define AVC_GEMM_NOLOAD 0  // diagnostic build only (-DAVC_GEMM_NOLOAD=1): gemm16f skips its LDS-DMA
+#endif
+#ifndef AVC_GEMM_DIAG_NOKAHAN
+#define AVC_GEMM_DIAG_NOKAHAN 0  // diagnostic: gemm16f folds 128-k partials with a plain add
+#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // branch-free masked operand load: the address is clamped to the (valid) operand base when the
@@ -744,6 +750,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
         const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)tau * a_tapshift) / 32; \
         const bool ok = src_tile >= 0 && src_tile < a_ntile && kc0 + kc < a_nkc;                 \
         const unsigned off = ok ? (unsigned)(((src_tile * a_nkc + kc0 + kc) * 2 + hl) * 1024) : kOut; \
+        if (!AVC_GEMM_NOLOAD)                                                                     \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)dst, 16, \
                                                  off + lane * 16, 0, 0, 0);                       \
       } else {                                                                                    \
@@ -754,6 +761,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
         const bool ok = src_tile < b_ntile && bkc >= 0 && bkc < b_nkc;                            \
         const unsigned off = ok ? (unsigned)(tau * b_tapstride * 2 +                              \
                                              ((long)(src_tile * b_nkc + bkc) * 2 + hl) * 1024) : kOut; \
+        if (!AVC_GEMM_NOLOAD)                                                                     \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16, \
                                                  off + lane * 16, 0, 0, 0);                       \
       }                                                                                           \
@@ -791,30 +799,48 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
     if (kt + NS - 1 < kt1) AVC16F_ISSUE(kt + NS - 1, (kt + NS - 1 - kt0) % NS);
     const unsigned char* Ai = lds + st * STAGE;
     const unsigned char* Bi = Ai + ABLK * 1024;
+    // Fragments of chunk s + 1 are read while chunk s's MFMAs issue (two register buffers), and
+    // the MFMAs go in passes over the accumulators (hi.hi for every tile, then hi.lo, then
+    // lo.hi): no MFMA waits on a just-issued LDS read or on the MFMA right before it.  Each
+    // accumulator still sees hi.hi, hi.lo, lo.hi per chunk in the same order (bit-identical).
+    f16x8 fah[2][TM], fal[2][TM], fbh[2][TN], fbl[2][TN];
+#define AVC16F_FRAGS(S, BUF)                                                                      \
+    _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                              \
+      const unsigned char* p = Ai + (((wm * TM + i) * KC + (S)) * 2) * 1024 + lane * 16;          \
+      fah[BUF][i] = *reinterpret_cast<const f16x8*>(p);                                           \
+      fal[BUF][i] = *reinterpret_cast<const f16x8*>(p + 1024);                                    \
+    }                                                                                             \
+    _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                              \
+      const unsigned char* p = Bi + (((wn * TN + j) * KC + (S)) * 2) * 1024 + lane * 16;          \
+      fbh[BUF][j] = *reinterpret_cast<const f16x8*>(p);                                           \
+      fbl[BUF][j] = *reinterpret_cast<const f16x8*>(p + 1024);                                    \
+    }
+    AVC16F_FRAGS(0, 0)
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
-      f16x8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const unsigned char* p = Ai + (((wm * TM + i) * KC + s) * 2) * 1024 + lane * 16;
-        ah[i] = *reinterpret_cast<const f16x8*>(p);
-        al[i] = *reinterpret_cast<const f16x8*>(p + 1024);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const unsigned char* p = Bi + (((wn * TN + j) * KC + s) * 2) * 1024 + lane * 16;
-        bh[j] = *reinterpret_cast<const f16x8*>(p);
-        bl[j] = *reinterpret_cast<const f16x8*>(p + 1024);
-      }
+      if (s + 1 < KC) { AVC16F_FRAGS(s + 1, (s + 1) & 1) }
+      // pin the order: without it the scheduler sinks the next chunk's reads back under these
+      // MFMAs and every pass waits on lgkmcnt(0) again
+      __builtin_amdgcn_sched_barrier(0);
+      const int cb = s & 1;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], part[i][j], 0, 0, 0);
-          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], crs[i][j], 0, 0, 0);
-          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], crs[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < TN; ++j)
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbh[cb][j], part[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbl[cb][j], crs[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[cb][i], fbh[cb][j], crs[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
+#undef AVC16F_FRAGS
     if ((kt - kt0) % KB == KB - 1 || kt + 1 == kt1) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -822,7 +848,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
         for (int j = 0; j < TN; ++j) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            if constexpr (OCC == 1) {
+            if constexpr (OCC == 1 && !AVC_GEMM_DIAG_NOKAHAN) {
               const float y = part[i][j][e] - cmp[i][j][e];
               const float t = acc[i][j][e] + y;
               cmp[i][j][e] = (t - acc[i][j][e]) - y;
