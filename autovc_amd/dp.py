@@ -1,9 +1,11 @@
 """Data-parallel training support for the Generator (BASELINE config 4).
 
 One process per GPU.  Each rank runs the reference training step on its own shard of utterance
-minibatches; the only exchange is ONE all-reduce (sum, then /world) of the flat 113.7 MB
-gradient per step, after which every rank applies the same fused clip/Adam/EMA update, so the
-parameters stay bit-identical across ranks.  BatchNorm batch statistics stay per rank (no
+minibatches; the only exchange is the all-reduce (sum, then /world) of the flat 113.7 MB
+gradient, after which every rank applies the same fused clip/Adam/EMA update, so the parameters
+stay bit-identical across ranks.  The all-reduce is bucketed and overlapped with backward
+(`GradBuckets`): contiguous ranges of the flat gradient, in reverse parameter order, are reduced
+asynchronously as soon as backward has produced every gradient in them.  BatchNorm batch statistics stay per rank (no
 SyncBN); the running buffers are broadcast from rank 0 before a checkpoint is written.
 With the nccl backend torch.distributed is RCCL over xGMI on MI355X.
 """
@@ -28,6 +30,112 @@ def average_gradients(flat_grad: torch.Tensor) -> torch.Tensor:
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM)
         flat_grad.div_(ws)
     return flat_grad
+
+
+class GradBuckets:
+    """Bucketed all-reduce of a flat gradient, overlapped with backward.
+
+    `params[i].grad` must be the view `flat_grad[off_i : off_i + n_i]` (AutoEncoder._ensure_flat),
+    offsets increasing with i.  Buckets are runs of consecutive parameters of about
+    `bucket_bytes`, formed from the LAST parameter backwards: backward produces the postnet's and
+    decoder's gradients first and the encoder's last (the encoder is also the only block the
+    loss runs twice, model.py:215-219, so its gradients are final only at the very end).  Each
+    bucket is a contiguous slice of `flat_grad`, so it is reduced in place, without a copy.
+
+    A post-accumulate-grad hook counts each parameter once per backward (the autograd engine sums
+    every use of a leaf before its one AccumulateGrad call).  When a bucket is complete its
+    all-reduce is issued with async_op=True, which orders it after the gradient kernels already
+    on the stream and lets the rest of backward run beside it.  Buckets are issued strictly in
+    index order, so every rank issues the same collectives in the same order.  `finish()` issues
+    whatever is left (parameters that got no gradient this step), waits for all of them (a
+    stream wait, not a host sync, with the nccl/RCCL backend) and divides by the world size.
+
+    Outside `armed()` the hooks do nothing, so other backward passes (tests, user code) never
+    start a collective."""
+
+    def __init__(self, params, flat_grad: torch.Tensor, bucket_bytes: int = 16 << 20):
+        params = list(params)
+        self.flat = flat_grad
+        base = flat_grad.data_ptr()
+        spans = []
+        for p in params:
+            if p.grad is None:
+                raise ValueError("GradBuckets needs every parameter's .grad to be a view of the flat gradient")
+            off = (p.grad.data_ptr() - base) // flat_grad.element_size()
+            spans.append((off, p.numel()))
+        if any(spans[i][0] + spans[i][1] != spans[i + 1][0] for i in range(len(spans) - 1)):
+            raise ValueError("parameter gradients are not consecutive slices of the flat gradient")
+        per = max(1, bucket_bytes // flat_grad.element_size())
+        self.buckets = []           # (lo, hi) element ranges, in launch order
+        self.bucket_of = [0] * len(params)
+        members = []
+        hi, size = None, 0
+        for i in reversed(range(len(params))):
+            off, n = spans[i]
+            if hi is None:
+                hi, size, cur = off + n, 0, []
+            cur.append(i)
+            size += n
+            if size >= per or i == 0:
+                self.buckets.append((off, hi))
+                members.append(cur)
+                hi = None
+        for b, idx in enumerate(members):
+            for i in idx:
+                self.bucket_of[i] = b
+        self.sizes = [len(m) for m in members]
+        self._armed = False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
+        self.reset()
+
+    def reset(self):
+        self.pending = list(self.sizes)
+        self.next = 0
+        self.handles = []
+        self.launch_log = []        # (bucket, parameters still pending overall) per issue
+
+    def _make_hook(self, i):
+        def hook(_p):
+            if not self._armed:
+                return
+            b = self.bucket_of[i]
+            self.pending[b] -= 1
+            self._issue(ready_only=True)
+        return hook
+
+    def _issue(self, ready_only):
+        while self.next < len(self.buckets) and (not ready_only or self.pending[self.next] <= 0):
+            lo, hi = self.buckets[self.next]
+            self.launch_log.append((self.next, sum(max(0, c) for c in self.pending)))
+            self.handles.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+            self.next += 1
+
+    def armed(self):
+        outer = self
+
+        class _Arm:
+            def __enter__(self):
+                outer.reset()
+                outer._armed = True
+                return outer
+
+            def __exit__(self, *exc):
+                outer._armed = False
+                return False
+        return _Arm()
+
+    def finish(self) -> torch.Tensor:
+        self._issue(ready_only=False)
+        for h in self.handles:
+            h.wait()
+        self.handles = []
+        self.flat.div_(world())
+        return self.flat
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
 
 
 def broadcast_buffers(module: torch.nn.Module, src: int = 0) -> None:

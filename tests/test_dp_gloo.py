@@ -147,3 +147,79 @@ def test_learn_sharding_and_save_world2(tmp_path):
     assert e0[0] != e0[1]  # reshuffled per epoch
     assert (calls0, calls1) == (1, 0) and bn0 == bn1 == 1.0
     assert (tmp_path / "ckpt" / "ae.pt").exists()
+
+
+def _flat_model(seed):
+    """A small stack whose first block is used twice per loss (like the encoder, which the
+    reference loss runs again on the postnet output), with flat parameter/gradient storage."""
+    torch.manual_seed(seed)
+    net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Tanh(), torch.nn.Linear(32, 32),
+                              torch.nn.Tanh(), torch.nn.Linear(32, 16))
+    params = list(net.parameters())
+    total = sum(p.numel() for p in params)
+    flat, grad, off = torch.empty(total), torch.zeros(total), 0
+    with torch.no_grad():
+        for p in params:
+            n = p.numel()
+            flat[off:off + n].copy_(p.reshape(-1))
+            p.data = flat[off:off + n].view_as(p)
+            p.grad = grad[off:off + n].view_as(p)
+            off += n
+    return net, params, grad
+
+
+def _loss(net, x):
+    y = net(x)
+    return (y ** 2).mean() + net[0](y).abs().mean()  # block 0 used a second time
+
+
+def _bucket_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        net, params, grad = _flat_model(0)
+        torch.manual_seed(50 + rank)
+        x = torch.randn(8, 16)
+        # reference: plain backward, then one all-reduce of the whole flat gradient
+        _loss(net, x).backward()
+        expect = dp.average_gradients(grad.clone())
+        grad.zero_()
+        # the product path: buckets issued from the post-accumulate hooks during backward
+        red = dp.GradBuckets(params, grad, bucket_bytes=4 * 300)
+        with red.armed():
+            _loss(net, x).backward()
+        log = list(red.launch_log)
+        red.finish()
+        same = torch.equal(grad, expect)
+        # disarmed: a backward outside train_step issues no collective
+        grad.zero_()
+        _loss(net, x).backward()
+        quiet = len(red.handles) == 0 and red.launch_log == log
+        q.put((rank, same, red.buckets, log, quiet, grad.numel()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_buckets_overlap_world2():
+    """dp.GradBuckets gives exactly the single flat all-reduce's mean, its buckets cover the flat
+    gradient back to front, and buckets are issued while backward still has gradients pending."""
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, same, buckets, log, quiet, total in res:
+        assert same, rank
+        assert quiet, rank
+        assert len(buckets) >= 3
+        assert buckets[0][1] == total and buckets[-1][0] == 0
+        assert all(buckets[i][0] == buckets[i + 1][1] for i in range(len(buckets) - 1))
+        assert [b for b, _ in log] == list(range(len(log)))   # strictly in bucket order
+        assert log[0][1] > 0, "first bucket was only issued after backward finished"
+    assert res[0][3] == res[1][3]  # same issue order on both ranks
