@@ -49,13 +49,22 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
 // decoder.lstm2 as one weight-stationary launch (lstm_persist.hip); gx0 = layer 0's input
 // projection, w*_s = split weights (each followed by its per-row unscale), b1_p = permuted
 // b_ih1 + b_hh1
+// With `ip`, layer 0's input projection runs inside the launch (slot 3) and gx0 is its output
+// buffer [T][B][4H]; without it gx0 is the caller's precomputed projection.
+struct InProj {
+  const float* x; long ldx; int din;  // layer 0's input [T*B][din], time-major rows
+  const _Float16* w_s;                // split W_ih0 (split_rows_kernel layout, K = din)
+  const float* winv;                  // its per-row unscale
+  const float* b0;                    // permuted b_ih0 + b_hh0
+};
 bool lstm2_persist_eligible(int T, int B, int H);
-size_t lstm2_persist_scratch(int T, int B, int H);
-int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx0,
+bool lstm2_inproj_eligible(int T, int B, int H, int din);
+size_t lstm2_persist_scratch(int T, int B, int H, int din);
+int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
                           const _Float16* w0_s, const float* winv0, const _Float16* w1i_s,
                           const float* winv1i, const _Float16* w1h_s, const float* winv1h,
                           const float* b1_p, float* y0, float* y1, float* g0, float* c0, float* g1,
-                          float* c1, hipStream_t s);
+                          float* c1, hipStream_t s, const InProj* ip = nullptr);
 // one forward layer (decoder.lstm1) as one weight-stationary launch, batch split into
 // independent groups; gx = input projection + biases, whh_s = split W_hh followed by winv
 bool lstm1_persist_eligible(int T, int B, int H);

@@ -123,11 +123,21 @@ __device__ unsigned long long* g_pstamps = nullptr;
 
 struct PersistArgs {
   int B, T, H, ncb, ntile;
-  int nslot;                  // 3 = two-layer wavefront (lstm2); 1 = one layer (slot 0 only: lstm1)
+  int nslot;                  // 3 = two-layer wavefront (lstm2), 4 = the same + slot 3 (input projection);
+                              // 1 = one layer (slot 0 only: lstm1)
   long cnt_gstride;           // counter words per batch group (blockIdx.y; one-layer form only)
-  const unsigned char* W[3];  // split fragment-major weights, permuted gate rows
-  const float* winv[3];       // per-row unscale
-  const float* gx0;           // [T][B][4H] layer-0 input projection + biases (permuted)
+  const unsigned char* W[4];  // split fragment-major weights, permuted gate rows
+  const float* winv[4];       // per-row unscale
+  const float* gx0;           // [T][B][4H] layer-0 input projection + biases (permuted); written
+                              // by slot 3 inside the launch when nslot == 4
+  // slot 3 (nslot == 4: layer 0's input projection inside the launch, on the CUs slots 0-2 leave
+  // idle): gx0_t = x_t W_ih0^T + b_ih0 + b_hh0 from the split x (split_steps16_kernel) and the
+  // split W_ih0 (split_rows_kernel layout, K = din)
+  const unsigned char* xs;    // [T][hszx] split x_t (fragment-major, 2 KiB per 16-row x 32-k block)
+  long hszx;                  // bytes per time step of xs
+  int din;                    // K of the input projection (128 * NCH3)
+  const float* b0;            // [4H] b_ih0 + b_hh0 (permuted)
+  const unsigned* x_amax;     // optional max |x| (float bits): x was split scaled by its power of two
   const float* b1;            // [4H] b_ih1 + b_hh1 (permuted)
   float* gx1;                 // [kGxRing][ncb][64][64] slabs (see gx1_slab)
   unsigned char* hs0;         // [T][hsz] split h0_t (fragment-major, 2 KiB per 16-row x 32-k block)
@@ -136,7 +146,7 @@ struct PersistArgs {
   float* y0; float* y1;       // [T][B][H] fp32 h
   float* g0; float* g1;       // optional [T][B][4H] activated gates (training)
   float* c0; float* c1;       // optional [T][B][H] cell state (training)
-  unsigned* cnt;              // [3][T] arrivals (never reset; see the epoch above)
+  unsigned* cnt;              // [nslot][T] arrivals (never reset; see the epoch above)
   unsigned* tmo;              // give-up word: epoch of the last launch that gave up
   unsigned long long* tickets;  // one per workgroup per launch
   unsigned* fail_host;        // pinned host word (avc_context::fail_host): last failure number
@@ -169,6 +179,124 @@ __device__ bool wait_ge(unsigned* p, unsigned target, const PersistArgs& a, unsi
   }
 }
 
+// power of two the x split was scaled by (split_steps16_kernel): max |x| -> [2^14, 2^15)
+__device__ __forceinline__ float x_split_scale(const unsigned* amax) {
+  if (!amax) return 1.f;
+  const float m = __uint_as_float(*amax);
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, 15 - e);
+}
+
+constexpr int kLead3 = 8;  // slot 3 runs at most this many steps ahead of slot 0
+
+// Slot 3 of the two-layer launch: layer 0's input projection, one time step per iteration, on the
+// 64 CUs the three recurrence slots leave idle (it replaces a separate 8192 x 4096 x 512 GEMM that
+// ran before the recurrence).  Workgroup cb owns the same 64 permuted gate rows as slot 0's cb and
+// keeps them in registers (W_ih0 rows, K = din = 512: 4 gate tiles x 4 chunks per wave); per
+// step it reads the split x_t (plain loads: x was written before the launch), forms
+// x_hi.W_hi + x_hi.W_lo and, in a second accumulator, x_lo.W_hi (x_lo carries 2^11, as
+// bn_apply_frag's split), reduces the 4 waves' K quarters in a fixed order and stores
+// gx0_t = sum * unscale + b0 with whole-line write-through stores, then counts itself in on
+// cnt[3][t].  Slot 0 waits for that counter and reads gx0_t with sc1 loads (the gx1 hand-off form).
+template <int RT>
+__device__ void input_slot(const PersistArgs& a, float* part, int* flag, unsigned E, unsigned target, int cb) {
+  constexpr int NW = 4, NC = 4, NCH3 = 4, MB = 16 * RT, TW = 16 * NC, RP = TW + 4;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int B = a.B, T = a.T;
+  const int nck3 = a.din >> 5;
+  const long G4 = 4L * a.H;
+  const int rep = blockIdx.x & (kRep - 1);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(a.W[3]) + (long)cb * NC * nck3 * 2048, 0, NC * nck3 * 2048, 0x00020000);
+  const int kc0 = w * NCH3;
+  f16x8 wr[NC][NCH3][2];
+#pragma unroll
+  for (int n = 0; n < NC; ++n)
+#pragma unroll
+    for (int c = 0; c < NCH3; ++c)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl)
+        wr[n][c][hl] = __builtin_bit_cast(
+            f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (n * nck3 + kc0 + c) * 2048 + hl * 1024, 0));
+  // store lanes: 4 consecutive gate columns 4*pc.. of the block for one batch row
+  const int pc = lane & 15;
+  const int p0 = cb * TW;
+  const float xun = 32768.f / x_split_scale(a.x_amax);  // W rows carry 2^15 more than winv undoes for h
+  f32x4 wiv, b0v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    wiv[e] = a.winv[3][p0 + 4 * pc + e] * xun;
+    b0v[e] = a.b0[p0 + 4 * pc + e];
+  }
+  const int ntile = a.ntile;
+  for (int t = 0; t < T; ++t) {
+    // back-pressure: at most kLead3 steps ahead of slot 0
+    if (tid == 0) {
+      const bool ok = t < kLead3 || wait_ge(a.cnt + cnt_index(0, T, t - kLead3, rep), target, a, E);
+      flag[0] = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (flag[0] == 0) return;
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(a.xs) + (long)t * a.hszx, 0,
+                                                       ntile * nck3 * 2048, 0x00020000);
+    f16x8 xv[NCH3][RT][2];
+#pragma unroll
+    for (int c = 0; c < NCH3; ++c)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+          xv[c][r][hl] = __builtin_bit_cast(
+              f16x8, __builtin_amdgcn_raw_buffer_load_b128(xrs, lane * 16, (r * nck3 + kc0 + c) * 2048 + hl * 1024, 0));
+    f32x4 acc[RT][NC], accl[RT][NC];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int n = 0; n < NC; ++n) acc[r][n] = accl[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH3; ++c)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int n = 0; n < NC; ++n) {
+          accl[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xv[c][r][1], wr[n][c][0], accl[r][n], 0, 0, 0);
+          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xv[c][r][0], wr[n][c][1], acc[r][n], 0, 0, 0);
+          acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xv[c][r][0], wr[n][c][0], acc[r][n], 0, 0, 0);
+        }
+    float* mine = part + w * MB * RP;
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int n = 0; n < NC; ++n)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e] + accl[r][n][e] * (1.f / 2048.f);
+    __syncthreads();
+    const auto ors = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.gx0) + (long)t * B * G4, 0,
+                                                       (int)(B * G4 * 4), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = w * 16 + i * 4 + (lane >> 4);
+      if (r < MB && r < B) {
+        const int off = r * RP + 4 * pc;
+        f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
+#pragma unroll
+        for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * MB * RP + off);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v * wiv + b0v), ors,
+                                               (int)((r * G4 + p0 + 4 * pc) * 4), 0, 16 /*sc1*/);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < kRep)
+      __hip_atomic_fetch_add((gu32*)(a.cnt + cnt_index(3, T, t, tid)), 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // HO = hand-off form on the consumer side: 0 = one agent-scope acquire (L1 invalidate) then plain
 // loads; 1 = no invalidate, EVERY load of handed-off bytes (split h, gx1) an sc1 load
 // (cdna_hip_programming.md Guideline 16, "Valid forms": producer stores sc1 + drained).
@@ -184,7 +312,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   extern __shared__ float lds[];
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds);
   float* part = lds + NW * NCH * 512;
-  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);  // [2]: the two polling lanes' results
+  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);  // [4]: polling lanes' results (0, 1, 3), epoch (2)
   // [TW] per-row unscale of this block's gate rows, then [TW] b_ih1 + b_hh1 (slot 1): read from
   // LDS in the epilogue instead of living in registers through the MFMA loop
   float* cpar = reinterpret_cast<float*>(flag + 4);
@@ -199,6 +327,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   unsigned* const cnt = a.cnt + (long)grp * a.cnt_gstride;
   const int nck = H >> 5;            // 32-deep chunks per row
   const long G4 = 4L * H;
+
+  // this launch's epoch (see the header): every workgroup takes one ticket
+  if (tid == 0) {
+    const unsigned long long tk = __hip_atomic_fetch_add(a.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[2] = (int)(unsigned)(tk / (unsigned long long)a.nwg + 1ull);
+  }
+  __syncthreads();
+  const unsigned E = (unsigned)flag[2];
+  const unsigned target = E * (unsigned)a.ncb;
+
+  if (L == 3) {  // layer 0's input projection (nslot == 4)
+    input_slot<RT>(a, part, flag, E, target, cb);
+    return;
+  }
 
   // ---- stationary weights: wave w owns K chunks [w*NCH, (w+1)*NCH) of the 4 gate tiles ----
   const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -247,15 +389,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   auto gx1_slab = [&](int tt, int c) -> long { return ((long)(tt % kGxRing) * a.ncb + c) * (64 * TW); };
   const int rep = blockIdx.x & (kRep - 1);
 
-  // this launch's epoch (see the header): every workgroup takes one ticket
-  if (tid == 0) {
-    const unsigned long long tk = __hip_atomic_fetch_add(a.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[2] = (int)(unsigned)(tk / (unsigned long long)a.nwg + 1ull);
-  }
-  __syncthreads();
-  const unsigned E = (unsigned)flag[2];
-  const unsigned target = E * (unsigned)a.ncb;
-
   int t = 0;
   for (; t < T; ++t) {
     // ---- wait for this step's operands ----------------------------------------------------
@@ -264,11 +397,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     // back-pressure that keeps slots 0 and 1 at most kLead / kGxRing steps ahead of slot 2 (a
     // slot running far ahead streams gx0 / writes h0 through the Infinity Cache and starves the
     // others: measured as a bistable 10 vs 20 us per step).  Each polling lane then acquires.
-    if (tid == 0 || tid == 64) {
+    // With slot 3 (nslot == 4) a third lane (wave 2) waits for this step's gx0.
+    if (tid == 0 || tid == 64 || tid == 128) {
       const bool primary = tid == 0;
       long idx = -1;
-      if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, T, t - 1, rep) : -1)
-                                : (t >= kLead && a.nslot == 3 ? cnt_index(2, T, t - kLead, rep) : -1);
+      if (tid == 128) idx = L == 0 && a.nslot == 4 ? cnt_index(3, T, t, rep) : -1;
+      else if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, T, t - 1, rep) : -1)
+                                     : (t >= kLead && a.nslot >= 3 ? cnt_index(2, T, t - kLead, rep) : -1);
       else if (L == 1) idx = primary ? cnt_index(0, T, t, rep)
                                      : (t >= kGxRing ? cnt_index(2, T, t - kGxRing, rep) : -1);
       else idx = primary ? (t > 0 ? cnt_index(2, T, t - 1, rep) : -1) : cnt_index(1, T, t, rep);
@@ -283,10 +418,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       } else {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
       }
-      flag[primary ? 0 : 1] = ok ? 1 : 0;
+      flag[tid == 128 ? 3 : (primary ? 0 : 1)] = ok ? 1 : 0;
     }
     __syncthreads();
-    if (flag[0] == 0 || flag[1] == 0) break;
+    if (flag[0] == 0 || flag[1] == 0 || flag[3] == 0) break;
     AVC_PSTAMP(2);
 
     // ---- recurrent / input product over this wave's K quarter ----------------------------
@@ -313,6 +448,21 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           if constexpr (UPT == 4) {
             gxv[g] = __builtin_bit_cast(fu, __builtin_amdgcn_raw_buffer_load_b128(grs, vo + 16 * g, 0, HO ? 16 : 0));
           } else {  // 4-B sc1 loads (an 8-B sc1 load is not a validated hand-off form)
+#pragma unroll
+            for (int uu = 0; uu < UPT; ++uu)
+              gxv[g][uu] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, vo + 16 * g + 4 * uu, 0, HO ? 16 : 0));
+          }
+        }
+      } else if (L == 0 && a.nslot == 4) {
+        // gx0_t handed off by slot 3 inside this launch: the same load form as gx1's
+        const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.gx0) + (long)t * B * G4, 0,
+                                                           (int)(B * G4 * 4), 0x00020000);
+        const int vo = (int)((bc * G4 + p0 + u0) * 4);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if constexpr (UPT == 4) {
+            gxv[g] = __builtin_bit_cast(fu, __builtin_amdgcn_raw_buffer_load_b128(grs, vo + 16 * g, 0, HO ? 16 : 0));
+          } else {
 #pragma unroll
             for (int uu = 0; uu < UPT; ++uu)
               gxv[g][uu] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, vo + 16 * g + 4 * uu, 0, HO ? 16 : 0));
@@ -527,6 +677,48 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         for (int g = 0; g < 4; ++g) *reinterpret_cast<fu*>(go + 4 * g) = nv;
       }
     }
+  }
+}
+
+// x [T*B][K] (row stride ldx, time-major rows t*B + b) -> per time step the fragment-major split
+// slot 3 reads: 16-row x 32-k blocks of 2 KiB (hi, then lo), lane (b & 15) + 16 * ((k & 31) >> 3)
+// holding k & 7 = 0..7, i.e. the layout split_rows_kernel gives the weights.  hi = f16(x s),
+// lo = f16((x s - hi) 2^11) with s the power of two of *amax (1 without it); rows b >= B are zero.
+__global__ __launch_bounds__(256) void split_steps16_kernel(const float* __restrict__ x, long ldx, int T, int B,
+                                                            int K, int ntile, long hszx,
+                                                            unsigned char* __restrict__ dst,
+                                                            const unsigned* __restrict__ amax) {
+  const int nck = K >> 5;
+  const long total = (long)T * ntile * nck * 64;
+  const float sc = x_split_scale(amax);
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int l = (int)(idx & 63);
+    const long blk = idx >> 6;
+    const int kc = (int)(blk % nck);
+    const long rest = blk / nck;
+    const int rt = (int)(rest % ntile);
+    const long t = rest / ntile;
+    const int b = rt * 16 + (l & 15), k0 = kc * 32 + 8 * (l >> 4);
+    float o[8];
+    if (b < B) {
+      const float4* q = reinterpret_cast<const float4*>(x + (t * B + b) * ldx + k0);
+      const float4 u = q[0], v = q[1];
+      o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w; o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = v.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    }
+    f16x8 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = o[e] * sc;
+      const _Float16 h = (_Float16)v;
+      hi[e] = h;
+      lo[e] = (_Float16)((v - (float)h) * 2048.0f);
+    }
+    unsigned char* d = dst + t * hszx + ((long)rt * nck + kc) * 2048 + l * 16;
+    *reinterpret_cast<f16x8*>(d) = hi;
+    *reinterpret_cast<f16x8*>(d + 1024) = lo;
   }
 }
 
@@ -757,21 +949,33 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   return AVC_OK;
 }
 
-size_t lstm2_persist_scratch(int T, int B, int H) {
+int g_persist_inproj = 1;  // avc_lstm_persist_inproj(): slot 3 computes lstm2's input projection
+
+// Slot 3 (layer 0's input projection inside the launch) needs K = 512 (4 chunks per wave) and a
+// fourth ncb-workgroup slot that is co-resident with the other three.
+bool lstm2_inproj_eligible(int T, int B, int H, int din) {
+  if (!g_persist_inproj || din != 512 || !lstm2_persist_eligible(T, B, H)) return false;
+  const int ntile = (B + 15) / 16, RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
+  return 4 * (4 * H / 64) <= persist_capacity(H, RT);
+}
+
+size_t lstm2_persist_scratch(int T, int B, int H, int din) {
   const size_t ntile = (size_t)(B + 15) / 16;
   const size_t hsz = ntile * 16 * H * 2 * 2;
   return al((size_t)T * hsz) + al((size_t)2 * hsz) + al((size_t)kGxRing * (4 * H / 64) * 64 * 64 * sizeof(float)) +
-         4096;
+         al((size_t)T * ntile * 16 * din * 2 * 2) + al((size_t)4 * H * din * 2 * 2 + 4 * H * sizeof(float)) +
+         al(2 * sizeof(unsigned)) + 4096;
 }
 
 // gx0 [T][B][4H] (layer 0's input projection + biases, permuted columns) is computed by the
 // caller; w*_s are the split weights with their per-row unscale (lstm_split.hip layout).
-int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx0,
+int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
                           const _Float16* w0_s, const float* winv0, const _Float16* w1i_s,
                           const float* winv1i, const _Float16* w1h_s, const float* winv1h,
                           const float* b1_p, float* y0, float* y1, float* g0, float* c0, float* g1,
-                          float* c1, hipStream_t s) {
+                          float* c1, hipStream_t s, const InProj* ip) {
   AVC_CHECK_ARG(lstm2_persist_eligible(T, B, H), "lstm2 persistent path: not eligible for this shape");
+  AVC_CHECK_ARG(!ip || lstm2_inproj_eligible(T, B, H, ip->din), "lstm2 input-projection slot: not eligible");
   AVC_TRY(persist_guard(ctx));
   Scratch sc(ctx);
   const int ntile = (B + 15) / 16;
@@ -779,12 +983,33 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
   AVC_TAKE(hs1, unsigned char, (size_t)2 * hsz, sc);                      // ring of 2
   AVC_TAKE(gx1, float, (size_t)kGxRing * (4 * H / 64) * 64 * 64, sc);     // slab ring
-  // counters [3][T][kRep] (one 128-B line each) in the persistent region of this layout
+  const int nslot = ip ? 4 : 3;
+  // counters [nslot][T][kRep] (one 128-B line each) in the persistent region of this layout
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, 3 * (4 * H / 64), (size_t)3 * T * kRep * kLine, s, &region));
+  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), (size_t)nslot * T * kRep * kLine, s,
+                         &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
-  a.nslot = 3; a.cnt_gstride = 0;
+  a.nslot = nslot; a.cnt_gstride = 0;
+  if (ip) {
+    // x split per time step for slot 3 (scaled by the power of two of max |x| unless its producer
+    // range-checked it: then unscaled, |x| < 65504, as the forward GEMM's guard would leave it)
+    const long hszx = (long)ntile * 16 * ip->din * 2 * 2;
+    AVC_TAKE(xs, unsigned char, (size_t)T * hszx, sc);
+    const unsigned* amax = nullptr;
+    if (!range_checked(ctx, ip->x)) {
+      AVC_TAKE(am, unsigned, 2, sc);
+      AVC_TRY(gemm_absmax(ip->x, (long)T * B, ip->din, ip->ldx, am, s));
+      amax = am;
+    }
+    const long total = (long)T * ntile * (ip->din / 32) * 64;
+    split_steps16_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(
+        ip->x, ip->ldx, T, B, ip->din, ntile, hszx, xs, amax);
+    AVC_LAUNCH_CHECK();
+    a.xs = xs; a.hszx = hszx; a.din = ip->din; a.b0 = ip->b0; a.x_amax = amax;
+    a.W[3] = reinterpret_cast<const unsigned char*>(ip->w_s);
+    a.winv[3] = ip->winv;
+  }
   a.W[0] = reinterpret_cast<const unsigned char*>(w0_s);
   a.W[1] = reinterpret_cast<const unsigned char*>(w1i_s);
   a.W[2] = reinterpret_cast<const unsigned char*>(w1h_s);
@@ -801,7 +1026,7 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
     // one launch = the whole 2-layer recurrence: 3 products of [B x H] . [H x 4H] per time step;
     // algorithmic bytes = the split weights read once + per step the split h operands and the
     // gx / h / c traffic
-    const double flops = 3.0 * T * 2.0 * B * (double)H * 4.0 * H;
+    const double flops = 3.0 * T * 2.0 * B * (double)H * 4.0 * H + (ip ? (double)T * 2.0 * B * ip->din * 4.0 * H : 0.0);
     const double bytes = 3.0 * 16.0 * (double)H * H + (double)T * (3.0 * 4.0 * B * H + 3.0 * 4.0 * B * 4.0 * H +
                                                                    2.0 * 4.0 * B * H * 2.0);
     timing_end(TC_LSTM2_PERSIST, ev, s, flops, bytes);
@@ -849,6 +1074,12 @@ extern "C" int avc_lstm_persist_layers(int mask) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_layers = mask;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_inproj(int on) {
+  avc::g_persist_inproj = on ? 1 : 0;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

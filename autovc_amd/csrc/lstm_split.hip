@@ -607,7 +607,7 @@ size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
   // slabs: at most K/128 splits of every 64-column tile, per slot
   s += (size_t)(nlayers + 1) * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
   s += al((size_t)(T + 2) * 3 * nrb * (4 * H / 64) * sizeof(int));
-  if (nlayers == 2 && B <= 64 && (H == 512 || H == 1024)) s += lstm2_persist_scratch(T, B, H);
+  if (nlayers == 2 && B <= 64 && (H == 512 || H == 1024)) s += lstm2_persist_scratch(T, B, H, din);
   if (nlayers == 1 && B <= 256 && (H == 512 || H == 1024)) s += lstm1_persist_scratch(T, B, H);
   GemmDesc d;
   d.M = (int)TB; d.N = 4 * H; d.Kc = din; d.prec16 = 1;
@@ -757,7 +757,21 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   if (f_b0) perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w0[2], w0[3], b0_p, H);
   if (f_b1) perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(w1[2], w1[3], b1_p, H);
   AVC_LAUNCH_CHECK();
-  if (f_wih) AVC_TRY(permute_rows(w0[0], wih_p, H, din, s));
+  if (f_wih) AVC_TRY(permute_rows(w0[0], wih_p, H, din, s));  // cached: kept valid for either path
+  if (lstm2_inproj_eligible(T, B, H, din) && ldx % 4 == 0 && aligned16(x)) {
+    // the whole recurrence AND layer 0's input projection as one weight-stationary launch: the
+    // projection runs per time step on the CUs the recurrence leaves idle (slot 3)
+    bool f_wis;
+    const size_t wisz = (size_t)4 * H * din * 2 + 8 * H;
+    _Float16* wi_s = prep_or_scratch<_Float16>(ctx, sc, PREP_LSTM_WIH_SPLIT, w0[0], nullptr, wisz, &f_wis);
+    if (!wi_s) return AVC_ERR_WORKSPACE;
+    float* winvi = reinterpret_cast<float*>(wi_s + (size_t)4 * H * din * 2);
+    if (f_wis) split_rows_kernel<<<4 * H, 256, 0, s>>>(w0[0], din, nullptr, 0, H, 1, wi_s, winvi);
+    AVC_LAUNCH_CHECK();
+    InProj ip{x, (long)ldx, din, wi_s, winvi, b0_p};
+    return lstm2_persist_forward(ctx, T, B, H, gx, w0_s, winv0, w1i_s, winv1i, w1h_s, winv1h, b1_p,
+                                 y0, y1, g0, c0, g1, c1, s, &ip);
+  }
   GemmDesc g;
   g.M = (int)TB; g.N = 4 * H; g.Kc = din;
   g.A = x; g.lda = ldx; g.a_rows = TB;

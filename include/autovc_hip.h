@@ -259,6 +259,11 @@ int avc_persist_check(avc_context* ctx, void* stream, int* failed);
  * a plain launch after an occupancy check (0, default).  Both require every workgroup to be
  * co-resident; the cooperative launch has the runtime guarantee it. */
 int avc_lstm_persist_coop(int on);
+/* Tuning hook: decoder lstm2's layer-0 input projection (decoder.py:53,74: the x W_ih0^T term of
+ * nn.LSTM) computed inside the persistent launch, one time step at a time on the CUs the
+ * recurrence leaves idle (1, default), or by a GEMM before the launch (0; then the persistent and
+ * launch-per-step forms are bit-identical). */
+int avc_lstm_persist_inproj(int on);
 /* Test hook: the next `launches` persistent launches give up at their first unsatisfied wait (as
  * if a peer workgroup never became resident); eager launches only (captured graphs are dropped). */
 int avc_debug_persist_inject(int launches);

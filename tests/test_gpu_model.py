@@ -298,10 +298,12 @@ def test_c5_long_form_against_oracle(cuda_device):
 def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
     """decoder.lstm2 (B <= 64) and decoder.lstm1 (B <= 256, batch split into independent row
     groups) as weight-stationary launches (lstm_persist.hip) against the launch-per-step forms
-    (lstm_split.hip) inside the same fused forward: the two
-    compute the same products in the same order, so every output is bit-identical, on the eager
-    call and on the captured-graph replays; and no workgroup of the persistent launch abandoned a
-    bounded wait."""
+    (lstm_split.hip) inside the same fused forward: with lstm2's input projection computed by the
+    GEMM beforehand (avc_lstm_persist_inproj(0)) the two compute the same products in the same
+    order, so every output is bit-identical, on the eager call and on the captured-graph replays.
+    With the projection inside the launch (slot 3, the default) the hand-off forms 1 and 2 agree
+    bit for bit, and both stay within 2e-5 of the GEMM-fed result (different summation order of
+    the K = 512 projection).  No workgroup of any persistent launch abandoned a bounded wait."""
     import ctypes
     from autovc_amd import _lib
     from autovc_amd.weights import synthetic_embedding, synthetic_mel
@@ -310,24 +312,32 @@ def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
     co, ct = _t(synthetic_embedding(41, B), cuda_device), _t(synthetic_embedding(42, B), cuda_device)
     outs = {}
     try:
-        for mode in (0, 1, 2):
+        for mode, inproj in ((0, 0), (1, 0), (2, 0), (1, 1), (2, 1)):
             _lib.call("avc_lstm_persist_tune", mode)
+            _lib.call("avc_lstm_persist_inproj", inproj)
             runs = []
             for _ in range(3):  # eager, capture + replay, replay
                 with torch.no_grad():
                     runs.append([t.clone() for t in ae(x, co, ct)])
             torch.cuda.synchronize()
             for r in runs[1:]:
-                assert all(torch.equal(a, b) for a, b in zip(r, runs[0])), f"mode {mode}: replays differ"
-            outs[mode] = runs[0]
+                assert all(torch.equal(a, b) for a, b in zip(r, runs[0])), f"mode {mode}/{inproj}: replays differ"
+            outs[mode, inproj] = runs[0]
     finally:
         _lib.call("avc_lstm_persist_tune", 2)
+        _lib.call("avc_lstm_persist_inproj", 1)
     giveups = ctypes.c_long(0)
     _lib.call("avc_lstm_persist_status", ctypes.byref(giveups))
     assert giveups.value == 0, f"{giveups.value} persistent workgroups abandoned a wait"
-    for mode in (1, 2):
-        for name, a, b in zip(("mel", "mel_post", "codes"), outs[0], outs[mode]):
-            assert torch.equal(a, b), f"mode {mode} {name}: max|d| {(a - b).abs().max().item():.3e}"
+    names = ("mel", "mel_post", "codes")
+    for key in ((1, 0), (2, 0)):
+        for name, a, b in zip(names, outs[0, 0], outs[key]):
+            assert torch.equal(a, b), f"mode {key} {name}: max|d| {(a - b).abs().max().item():.3e}"
+    for name, a, b in zip(names, outs[2, 1], outs[1, 1]):
+        assert torch.equal(a, b), f"input slot, hand-off forms differ on {name}: {(a - b).abs().max().item():.3e}"
+    d = max((a - b).abs().max().item() for a, b in zip(outs[0, 0], outs[2, 1]))
+    print(f"B={B} T={T}: input-projection slot vs GEMM-fed max|d| {d:.2e}")
+    assert d <= 2e-5
 
 
 def test_back_to_back_forwards_match(cuda_device):
