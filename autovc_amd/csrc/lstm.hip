@@ -585,8 +585,12 @@ struct L32Dir {
 };
 
 // Workgroups [0, B) run direction d0, [B, 2B) direction d1 (both directions of a bidirectional
-// layer in one launch).  The input projection of step s+3 is fetched while step s computes: the
-// per-step chain is then LDS + FMA + gate math only.
+// layer in one launch).  The step is one wave's latency chain (LDS h broadcast -> 32-deep dot
+// products -> gate math -> h), so everything else is taken off it: the input projection of step
+// s + PF is fetched while step s computes (a register ring of PF steps, the loop unrolled by PF
+// so ring slots are static), and FAST selects hardware exp / reciprocal gate math
+// (sigma(x) = rcp(1 + 2^(-x log2 e)), tanh(x) = 2 sigma(2x) - 1; within ~1e-7 of the libm forms).
+template <int PF, bool FAST>
 __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx, long ldy, L32Dir d0,
                                                         L32Dir d1) {
   const int dir = blockIdx.x >= B ? 1 : 0;
@@ -607,55 +611,108 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx,
     const int sc = st < T ? st : T - 1;
     return ((long)(reverse ? T - 1 - sc : sc) * B + b) * ldgx;
   };
-  float za0 = gx[grow(0) + lane], za1 = gx[grow(0) + lane + 64];
-  float zb0 = gx[grow(1) + lane], zb1 = gx[grow(1) + lane + 64];
-  float zc0 = gx[grow(2) + lane], zc1 = gx[grow(2) + lane + 64];
-  __syncthreads();
-  for (int s = 0; s < T; ++s) {
-    const int t = reverse ? T - 1 - s : s;
-    const long row = (long)t * B + b;
-    const long rn = grow(s + 3);
-    const float zd0 = gx[rn + lane], zd1 = gx[rn + lane + 64];
-    float z0 = za0, z1 = za1;
-    // four independent FMA chains per gate row (8 deep instead of 32: the step is a latency chain)
-    float p0[4] = {0.f, 0.f, 0.f, 0.f}, p1[4] = {0.f, 0.f, 0.f, 0.f};
+  auto sig = [](float x) {
+    if constexpr (FAST) return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+    else return sigmoidf_(x);
+  };
+  auto th = [&](float x) {
+    if constexpr (FAST) return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f;
+    else return tanhf(x);
+  };
+  float r0[PF], r1[PF];
 #pragma unroll
-    for (int k4 = 0; k4 < 8; ++k4) {
-      const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
-      p0[0] = fmaf(w0[4 * k4], h4.x, p0[0]);
-      p0[1] = fmaf(w0[4 * k4 + 1], h4.y, p0[1]);
-      p0[2] = fmaf(w0[4 * k4 + 2], h4.z, p0[2]);
-      p0[3] = fmaf(w0[4 * k4 + 3], h4.w, p0[3]);
-      p1[0] = fmaf(w1[4 * k4], h4.x, p1[0]);
-      p1[1] = fmaf(w1[4 * k4 + 1], h4.y, p1[1]);
-      p1[2] = fmaf(w1[4 * k4 + 2], h4.z, p1[2]);
-      p1[3] = fmaf(w1[4 * k4 + 3], h4.w, p1[3]);
-    }
-    z0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
-    z1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
-    const float a0 = sigmoidf_(z0);                              // i (lane<32) or f
-    const float a1 = lane < 32 ? tanhf(z1) : sigmoidf_(z1);      // g (lane<32) or o
-    const float fg = __shfl(a0, (lane + 32) & 63);
-    const float og = __shfl(a1, (lane + 32) & 63);
-    if (lane < 32) {
-      c = fg * c + a0 * a1;
-      const float h = og * tanhf(c);
-      D.y[row * ldy + lane] = h;
-      if (D.c) D.c[row * 32 + lane] = c;
-      if (D.gates) {
-        float* g = D.gates + row * 128;
-        g[lane] = a0;
-        g[32 + lane] = fg;
-        g[64 + lane] = a1;
-        g[96 + lane] = og;
-      }
-      hs[lane] = h;
-    }
-    __syncthreads();
-    za0 = zb0; za1 = zb1;
-    zb0 = zc0; zb1 = zc1;
-    zc0 = zd0; zc1 = zd1;
+  for (int u = 0; u < PF; ++u) {
+    r0[u] = gx[grow(u) + lane];
+    r1[u] = gx[grow(u) + lane + 64];
   }
+  __syncthreads();
+  for (int s0 = 0; s0 < T; s0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int s = s0 + u;
+      // the ring refill is unconditional (grow() clamps to the last row): a refill under the
+      // s < T guard would make the slot a join of old and new values and wait for the load here
+      float z0 = r0[u], z1 = r1[u];
+      const long rn = grow(s + PF);
+      r0[u] = gx[rn + lane];
+      r1[u] = gx[rn + lane + 64];
+      if (s < T) {
+        const int t = reverse ? T - 1 - s : s;
+        const long row = (long)t * B + b;
+        float a0, a1, fg, og;
+        if constexpr (FAST) {
+          // packed FMAs (v_pk_fma_f32: two k per instruction), two chains of 8 per gate row
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          f2 q0[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, q1[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+          for (int k4 = 0; k4 < 8; ++k4) {
+            const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
+            const f2 ha = {h4.x, h4.y}, hb = {h4.z, h4.w};
+            q0[0] = __builtin_elementwise_fma(f2{w0[4 * k4], w0[4 * k4 + 1]}, ha, q0[0]);
+            q0[1] = __builtin_elementwise_fma(f2{w0[4 * k4 + 2], w0[4 * k4 + 3]}, hb, q0[1]);
+            q1[0] = __builtin_elementwise_fma(f2{w1[4 * k4], w1[4 * k4 + 1]}, ha, q1[0]);
+            q1[1] = __builtin_elementwise_fma(f2{w1[4 * k4 + 2], w1[4 * k4 + 3]}, hb, q1[1]);
+          }
+          const f2 s0 = q0[0] + q0[1], s1 = q1[0] + q1[1];
+          z0 += s0.x + s0.y;
+          z1 += s1.x + s1.y;
+          a0 = sig(z0);                           // i (lane<32) or f
+          a1 = lane < 32 ? th(z1) : sig(z1);      // g (lane<32) or o
+          // lanes 32..63 -> 0..31 with one VALU swap of the wave halves instead of ds_bpermute
+          fg = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a0), false, false)[1]);
+          og = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(a1), __float_as_uint(a1), false, false)[1]);
+        } else {
+          // four independent FMA chains per gate row (8 deep instead of 32)
+          float p0[4] = {0.f, 0.f, 0.f, 0.f}, p1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k4 = 0; k4 < 8; ++k4) {
+            const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
+            p0[0] = fmaf(w0[4 * k4], h4.x, p0[0]);
+            p0[1] = fmaf(w0[4 * k4 + 1], h4.y, p0[1]);
+            p0[2] = fmaf(w0[4 * k4 + 2], h4.z, p0[2]);
+            p0[3] = fmaf(w0[4 * k4 + 3], h4.w, p0[3]);
+            p1[0] = fmaf(w1[4 * k4], h4.x, p1[0]);
+            p1[1] = fmaf(w1[4 * k4 + 1], h4.y, p1[1]);
+            p1[2] = fmaf(w1[4 * k4 + 2], h4.z, p1[2]);
+            p1[3] = fmaf(w1[4 * k4 + 3], h4.w, p1[3]);
+          }
+          z0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
+          z1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
+          a0 = sig(z0);
+          a1 = lane < 32 ? th(z1) : sig(z1);
+          fg = __shfl(a0, (lane + 32) & 63);
+          og = __shfl(a1, (lane + 32) & 63);
+        }
+        if (lane < 32) {
+          c = fg * c + a0 * a1;
+          const float h = og * th(c);
+          hs[lane] = h;
+          D.y[row * ldy + lane] = h;
+          if (D.c) D.c[row * 32 + lane] = c;
+          if (D.gates) {
+            float* g = D.gates + row * 128;
+            g[lane] = a0;
+            g[32 + lane] = fg;
+            g[64 + lane] = a1;
+            g[96 + lane] = og;
+          }
+        }
+        // one wave: LDS operations complete in issue order, so the next step's h reads only need
+        // the compiler not to move them above this write.  (__syncthreads() would also wait for
+        // every outstanding global load -- the prefetch ring -- and store on every step.)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+  }
+}
+
+int g_lstm32_mode = 1;  // avc_lstm32_tune(): 0 = libm gate math, 3-step prefetch; 1 = fast math, 8 steps
+
+void launch_lstm32(int nblk, int T, int B, long ldgx, long ldy, const L32Dir& d0, const L32Dir& d1, hipStream_t s) {
+  if (g_lstm32_mode == 0) lstm32_fwd_kernel<3, false><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
+  else lstm32_fwd_kernel<8, true><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
 }
 
 __global__ __launch_bounds__(64) void lstm32_bwd_kernel(int T, int B, int reverse,
@@ -762,7 +819,7 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
     AVC_TRY(gemm_run(ctx, g, s));
     hipEvent_t ev = timing_begin(TC_LSTM32, s);
     L32Dir d{gx, w_hh, y, saved_gates, saved_c, reverse};
-    lstm32_fwd_kernel<<<B, 64, 0, s>>>(T, B, 128, ldy, d, d);
+    launch_lstm32(B, T, B, 128, ldy, d, d, s);
     AVC_LAUNCH_CHECK();
     if (ev) timing_end(TC_LSTM32, ev, s, 2.0 * T * B * 128.0 * 32.0, 4.0 * T * B * (128.0 + 32.0));
     return AVC_OK;
@@ -855,7 +912,7 @@ int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const fl
   hipEvent_t ev = timing_begin(TC_LSTM32, s);
   L32Dir d0{gx, wf[1], y, g_f, c_f, 0};
   L32Dir d1{gx + 128, wr[1], y + 32, g_r, c_r, 1};
-  lstm32_fwd_kernel<<<2 * B, 64, 0, s>>>(T, B, 256, ldy, d0, d1);
+  launch_lstm32(2 * B, T, B, 256, ldy, d0, d1, s);
   AVC_LAUNCH_CHECK();
   if (ev) timing_end(TC_LSTM32, ev, s, 2.0 * 2 * T * B * 128.0 * 32.0, 2.0 * 4.0 * T * B * (128.0 + 32.0));
   return AVC_OK;
@@ -1187,6 +1244,16 @@ extern "C" int avc_lstm_tune(int rows_per_block, int waves) {
   }
   avc::g_force_mb = rows_per_block;
   avc::g_force_nw = waves;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm32_tune(int mode) {
+  if (mode < 0 || mode > 1) {
+    avc::set_error("avc_lstm32_tune: mode must be 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_lstm32_mode = mode;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -264,6 +264,9 @@ int avc_lstm_persist_coop(int on);
  * recurrence leaves idle (1, default), or by a GEMM before the launch (0; then the persistent and
  * launch-per-step forms are bit-identical). */
 int avc_lstm_persist_inproj(int on);
+/* Tuning hook for the encoder BiLSTM (H = 32) recurrence: 1 (default) = hardware exp/reciprocal
+ * gate math and an 8-step prefetch of the input projection; 0 = libm gate math, 3-step prefetch. */
+int avc_lstm32_tune(int mode);
 /* Test hook: the next `launches` persistent launches give up at their first unsatisfied wait (as
  * if a peer workgroup never became resident); eager launches only (captured graphs are dropped). */
 int avc_debug_persist_inject(int launches);
