@@ -954,6 +954,41 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   }
 }
 
+// splitk_reduce_kernel for the common case (one product, row-major C, N % 4 == 0): a thread sums
+// 4 consecutive columns of one row over the splits (float4 streams); grid.y walks row blocks.
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmDesc d, int nsplit, const float* __restrict__ slab,
+                                                             int rows_per_block) {
+  const int n4 = d.N >> 2;
+  const long MN = (long)d.M * d.N;
+  const float us = d.split_scale ? split_unscale(d.amax_a, d.amax_b) : 1.f;
+  const int r1 = min(d.M, (int)(blockIdx.y + 1) * rows_per_block);
+  for (int i = threadIdx.x; ; i += 256) {
+    const int m = blockIdx.y * rows_per_block + i / n4, c4 = i - (i / n4) * n4;
+    if (m >= r1) break;
+    const long off = (long)m * d.N + 4 * c4;
+    float4 a = *reinterpret_cast<const float4*>(slab + off);
+    for (int sp = 1; sp < nsplit; ++sp) {
+      const float4 b = *reinterpret_cast<const float4*>(slab + sp * MN + off);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = 4 * c4 + e;
+      float t = v[e] * us;
+      if (d.bias0) t += d.bias0[n];
+      if (d.bias1) t += d.bias1[n];
+      v[e] = act_apply(t, d.act);
+    }
+    float* p = d.C + (long)m * d.ldc + 4 * c4;
+    if (d.accumulate) {
+      const float4 o = *reinterpret_cast<const float4*>(p);
+      v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+    }
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __restrict__ slab) {
   const long total = (long)d.nz * d.M * d.N;
   const long MN = (long)d.M * d.N;
@@ -1413,7 +1448,12 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
   if (p.nsplit > 1) {
     const long total = (long)d.nz * d.M * d.N;
     const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-    splitk_reduce_kernel<<<blocks, 256, 0, stream>>>(d, p.nsplit, slab);
+    if (d.nz == 1 && d.ldc_col == 1 && d.N % 4 == 0 && d.ldc % 4 == 0 && aligned16(d.C)) {
+      const int rpb = std::max(1, 1024 / (d.N / 4));  // ~4 float4 per thread
+      splitk_reduce4_kernel<<<dim3(1, (d.M + rpb - 1) / rpb), 256, 0, stream>>>(d, p.nsplit, slab, rpb);
+    } else {
+      splitk_reduce_kernel<<<blocks, 256, 0, stream>>>(d, p.nsplit, slab);
+    }
     AVC_LAUNCH_CHECK();
   }
   return AVC_OK;
