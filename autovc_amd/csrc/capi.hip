@@ -158,7 +158,12 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TRY(codes_from_encoder(T, B, e2, codes, s));
 
   // Upsample + decoder (model.py:115-127, decoder.py:58-79)
-  AVC_TRY(decoder_input(T, B, e2, 256, c_trg, din, s));
+  {  // the decoder input's embedding part is range-checked on the way (codes are LSTM outputs)
+    unsigned* flags = host_flags(ctx);
+    if (!flags) return AVC_ERR_HIP;
+    AVC_TRY(decoder_input(T, B, e2, 256, c_trg, din, s, flags + 1));
+    mark_range_checked(ctx, din);
+  }
   const int D1 = P_DEC_LSTM1;
   AVC_TRY(lstm_forward_impl(ctx, T, B, 320, 512, 0, din, 320, P[D1], P[D1 + 1], P[D1 + 2], P[D1 + 3],
                             ba, 512, nullptr, nullptr, s));

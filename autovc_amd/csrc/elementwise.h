@@ -27,7 +27,7 @@ int codes_from_encoder(int T, int B, const float* enc, float* codes, hipStream_t
 int codes_from_encoder_backward(int T, int B, const float* dcodes, float* denc, int accumulate,
                                 hipStream_t s);
 int decoder_input(int T, int B, const float* enc, int ce, const float* ctrg, float* out,
-                  hipStream_t s);
+                  hipStream_t s, unsigned* range_flag = nullptr);
 int decoder_input_backward(int T, int B, int ce, const float* dd, float* denc, int accumulate,
                            hipStream_t s);
 int overlap_average(int M, int C, int N, int step, const float* fr, float* out, hipStream_t s);

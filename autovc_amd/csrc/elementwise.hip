@@ -364,7 +364,8 @@ __global__ void codes_kernel(int T, int B, const float* __restrict__ enc, float*
 }
 
 __global__ void decoder_input_kernel(int T, int B, const float* __restrict__ enc, int ce,
-                                     const float* __restrict__ ctrg, float* __restrict__ out) {
+                                     const float* __restrict__ ctrg, float* __restrict__ out,
+                                     unsigned* __restrict__ range_flag) {
   const int C = 64 + ce, nA = T / 32;
   const long total = (long)T * B * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
@@ -380,6 +381,10 @@ __global__ void decoder_input_kernel(int T, int B, const float* __restrict__ enc
       v = enc[((long)(32 * (t / 32)) * B + b) * 64 + c];
     } else {
       v = ctrg[(long)b * ce + (c - 64)];
+      // the codes are LSTM outputs (|h| < 1); the target embedding is the caller's: range-check it
+      // for the consumer's f16 split (see bn_apply_kernel)
+      if (range_flag && fabsf(v) >= 65504.f && fabsf(v) < __builtin_inff())
+        __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     out[i] = v;
   }
@@ -679,9 +684,9 @@ int codes_from_encoder_backward(int T, int B, const float* dcodes, float* denc, 
 }
 
 int decoder_input(int T, int B, const float* enc, int ce, const float* ctrg, float* out,
-                  hipStream_t s) {
+                  hipStream_t s, unsigned* range_flag) {
   AVC_CHECK_ARG(T >= 32, "decoder input needs T >= 32 frames (model.py:115-119)");
-  decoder_input_kernel<<<ew_blocks((long)T * B * (64 + ce)), 256, 0, s>>>(T, B, enc, ce, ctrg, out);
+  decoder_input_kernel<<<ew_blocks((long)T * B * (64 + ce)), 256, 0, s>>>(T, B, enc, ce, ctrg, out, range_flag);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

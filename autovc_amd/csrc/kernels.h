@@ -68,9 +68,13 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
 // one forward layer (decoder.lstm1) as one weight-stationary launch, batch split into
 // independent groups; gx = input projection + biases, whh_s = split W_hh followed by winv
 bool lstm1_persist_eligible(int T, int B, int H);
-size_t lstm1_persist_scratch(int T, int B, int H);
-int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx, const _Float16* whh_s,
-                          const float* winv, float* y, float* g, float* c, hipStream_t s);
+bool lstm1_inproj_eligible(int T, int B, int H, int din);
+size_t lstm1_persist_scratch(int T, int B, int H, int din);
+int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, const _Float16* whh_s,
+                          const float* winv, float* y, float* g, float* c, hipStream_t s,
+                          const InProj* ip = nullptr);
+// K of an input slot's split operands: din padded with zeros to 128 * (3 or 4) columns
+int inproj_kpad(int din);
 // rows of a [4H][D] gate matrix into the permuted gate order p = blk*16 + gate*4 + u (lstm.hip)
 int permute_rows(const float* src, float* dst, int H, int D, hipStream_t s);
 

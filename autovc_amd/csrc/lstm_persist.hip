@@ -130,12 +130,15 @@ struct PersistArgs {
   const float* winv[4];       // per-row unscale
   const float* gx0;           // [T][B][4H] layer-0 input projection + biases (permuted); written
                               // by slot 3 inside the launch when nslot == 4
-  // slot 3 (nslot == 4: layer 0's input projection inside the launch, on the CUs slots 0-2 leave
-  // idle): gx0_t = x_t W_ih0^T + b_ih0 + b_hh0 from the split x (split_steps16_kernel) and the
-  // split W_ih0 (split_rows_kernel layout, K = din)
+  // input slot (in_slot > 0: layer 0's input projection inside the launch, on CUs the recurrence
+  // leaves idle): gx0_t = x_t W_ih0^T + b_ih0 + b_hh0 from the split x (split_steps16_kernel) and
+  // the split W_ih0 (split_rows_kernel layout, K = din)
   const unsigned char* xs;    // [T][hszx] split x_t (fragment-major, 2 KiB per 16-row x 32-k block)
   long hszx;                  // bytes per time step of xs
-  int din;                    // K of the input projection (128 * NCH3)
+  int din;                    // K of the input projection, padded to 128 * NCH3 (3 or 4) with zeros
+  int in_slot;                // slot index of the input projection (3: lstm2, 1: lstm1), 0 = none
+  int in_lead;                // input slot back-pressure: 1 = none (default: measured fastest),
+                              // 2 = at most kLead3 steps ahead checked every 4th step, 3 = every step
   const float* b0;            // [4H] b_ih0 + b_hh0 (permuted)
   const unsigned* x_amax;     // optional max |x| (float bits): x was split scaled by its power of two
   const float* b1;            // [4H] b_ih1 + b_hh1 (permuted)
@@ -189,7 +192,8 @@ __device__ __forceinline__ float x_split_scale(const unsigned* amax) {
   return ldexpf(1.f, 15 - e);
 }
 
-constexpr int kLead3 = 8;  // slot 3 runs at most this many steps ahead of slot 0
+constexpr int kLead3 = 12;  // with back-pressure (in_lead 2 / 3) the input slot runs at most this many
+                            // steps ahead of slot 0 (> 3: see slot 0's every-4th-step wait)
 
 // Slot 3 of the two-layer launch: layer 0's input projection, one time step per iteration, on the
 // 64 CUs the three recurrence slots leave idle (it replaces a separate 8192 x 4096 x 512 GEMM that
@@ -200,17 +204,18 @@ constexpr int kLead3 = 8;  // slot 3 runs at most this many steps ahead of slot 
 // bn_apply_frag's split), reduces the 4 waves' K quarters in a fixed order and stores
 // gx0_t = sum * unscale + b0 with whole-line write-through stores, then counts itself in on
 // cnt[3][t].  Slot 0 waits for that counter and reads gx0_t with sc1 loads (the gx1 hand-off form).
-template <int RT>
-__device__ void input_slot(const PersistArgs& a, float* part, int* flag, unsigned E, unsigned target, int cb) {
-  constexpr int NW = 4, NC = 4, NCH3 = 4, MB = 16 * RT, TW = 16 * NC, RP = TW + 4;
+template <int RT, int NCH3>
+__device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* part, int* flag, unsigned E,
+                           unsigned target, int cb) {
+  constexpr int NW = 4, NC = 4, MB = 16 * RT, TW = 16 * NC, RP = TW + 4;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
   const int B = a.B, T = a.T;
-  const int nck3 = a.din >> 5;
+  const int nck3 = 4 * NCH3;  // a.din == 128 * NCH3
   const long G4 = 4L * a.H;
   const int rep = blockIdx.x & (kRep - 1);
   const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned char*>(a.W[3]) + (long)cb * NC * nck3 * 2048, 0, NC * nck3 * 2048, 0x00020000);
+      const_cast<unsigned char*>(a.W[a.in_slot]) + (long)cb * NC * nck3 * 2048, 0, NC * nck3 * 2048, 0x00020000);
   const int kc0 = w * NCH3;
   f16x8 wr[NC][NCH3][2];
 #pragma unroll
@@ -228,20 +233,24 @@ __device__ void input_slot(const PersistArgs& a, float* part, int* flag, unsigne
   f32x4 wiv, b0v;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    wiv[e] = a.winv[3][p0 + 4 * pc + e] * xun;
+    wiv[e] = a.winv[a.in_slot][p0 + 4 * pc + e] * xun;
     b0v[e] = a.b0[p0 + 4 * pc + e];
   }
-  const int ntile = a.ntile;
+  // this workgroup's batch rows: [grp * MB, grp * MB + MB) (one-layer form: its batch group)
+  const int tile0 = grp * RT;
+  const int ntile = a.ntile - tile0;
   for (int t = 0; t < T; ++t) {
     // back-pressure: at most kLead3 steps ahead of slot 0
     if (tid == 0) {
-      const bool ok = t < kLead3 || wait_ge(a.cnt + cnt_index(0, T, t - kLead3, rep), target, a, E);
+      const bool check = t >= kLead3 && (a.in_lead == 3 || (a.in_lead == 2 && (t & 3) == 0));
+      const bool ok = !check || wait_ge(cnt + cnt_index(0, T, t - kLead3, rep), target, a, E);
       flag[0] = ok ? 1 : 0;
     }
     __syncthreads();
     if (flag[0] == 0) return;
-    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(a.xs) + (long)t * a.hszx, 0,
-                                                       ntile * nck3 * 2048, 0x00020000);
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(a.xs) + (long)t * a.hszx + (long)tile0 * nck3 * 2048, 0, ntile * nck3 * 2048,
+        0x00020000);
     f16x8 xv[NCH3][RT][2];
 #pragma unroll
     for (int c = 0; c < NCH3; ++c)
@@ -280,19 +289,19 @@ __device__ void input_slot(const PersistArgs& a, float* part, int* flag, unsigne
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = w * 16 + i * 4 + (lane >> 4);
-      if (r < MB && r < B) {
+      if (r < MB && tile0 * 16 + r < B) {
         const int off = r * RP + 4 * pc;
         f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
 #pragma unroll
         for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(part + ww * MB * RP + off);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v * wiv + b0v), ors,
-                                               (int)((r * G4 + p0 + 4 * pc) * 4), 0, 16 /*sc1*/);
+                                               (int)(((tile0 * 16 + r) * G4 + p0 + 4 * pc) * 4), 0, 16 /*sc1*/);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid < kRep)
-      __hip_atomic_fetch_add((gu32*)(a.cnt + cnt_index(3, T, t, tid)), 1u, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add((gu32*)(cnt + cnt_index(a.in_slot, T, t, tid)), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -337,8 +346,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   const unsigned E = (unsigned)flag[2];
   const unsigned target = E * (unsigned)a.ncb;
 
-  if (L == 3) {  // layer 0's input projection (nslot == 4)
-    input_slot<RT>(a, part, flag, E, target, cb);
+  if (a.in_slot > 0 && L == a.in_slot) {  // layer 0's input projection
+    if (a.din == 512) input_slot<RT, 4>(a, cnt, grp, part, flag, E, target, cb);
+    else input_slot<RT, 3>(a, cnt, grp, part, flag, E, target, cb);
     return;
   }
 
@@ -401,7 +411,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     if (tid == 0 || tid == 64 || tid == 128) {
       const bool primary = tid == 0;
       long idx = -1;
-      if (tid == 128) idx = L == 0 && a.nslot == 4 ? cnt_index(3, T, t, rep) : -1;
+      // the input slot runs ahead (up to kLead3 steps), so its progress is checked every 4th step
+      // for 4 steps at once: its workgroups finish steps in order, so all of them counting in on
+      // step t + 3 implies steps t .. t + 2 are complete (and drained) as well
+      if (tid == 128) idx = L == 0 && a.in_slot > 0 && (t & 3) == 0 ? cnt_index(a.in_slot, T, min(t + 3, T - 1), rep) : -1;
       else if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, T, t - 1, rep) : -1)
                                      : (t >= kLead && a.nslot >= 3 ? cnt_index(2, T, t - kLead, rep) : -1);
       else if (L == 1) idx = primary ? cnt_index(0, T, t, rep)
@@ -453,7 +466,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
               gxv[g][uu] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, vo + 16 * g + 4 * uu, 0, HO ? 16 : 0));
           }
         }
-      } else if (L == 0 && a.nslot == 4) {
+      } else if (L == 0 && a.in_slot > 0) {
         // gx0_t handed off by slot 3 inside this launch: the same load form as gx1's
         const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.gx0) + (long)t * B * G4, 0,
                                                            (int)(B * G4 * 4), 0x00020000);
@@ -685,10 +698,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 // holding k & 7 = 0..7, i.e. the layout split_rows_kernel gives the weights.  hi = f16(x s),
 // lo = f16((x s - hi) 2^11) with s the power of two of *amax (1 without it); rows b >= B are zero.
 __global__ __launch_bounds__(256) void split_steps16_kernel(const float* __restrict__ x, long ldx, int T, int B,
-                                                            int K, int ntile, long hszx,
+                                                            int K, int Kp, int ntile, long hszx,
                                                             unsigned char* __restrict__ dst,
                                                             const unsigned* __restrict__ amax) {
-  const int nck = K >> 5;
+  const int nck = Kp >> 5;  // columns [K, Kp) are zeros (K % 8 == 0)
   const long total = (long)T * ntile * nck * 64;
   const float sc = x_split_scale(amax);
   for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
@@ -700,7 +713,7 @@ __global__ __launch_bounds__(256) void split_steps16_kernel(const float* __restr
     const long t = rest / ntile;
     const int b = rt * 16 + (l & 15), k0 = kc * 32 + 8 * (l >> 4);
     float o[8];
-    if (b < B) {
+    if (b < B && k0 < K) {
       const float4* q = reinterpret_cast<const float4*>(x + (t * B + b) * ldx + k0);
       const float4 u = q[0], v = q[1];
       o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w; o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = v.w;
@@ -789,6 +802,10 @@ int g_persist_inject = 0;        // avc_debug_persist_inject(): launches left th
 int persist_launch(PersistArgs a, int RT, int ngrp, hipStream_t s) {
   const dim3 grid(a.nslot * a.ncb, ngrp);
   a.nwg = (int)(grid.x * grid.y);
+  for (int L = 0; L < a.nslot; ++L)
+    AVC_CHECK_ARG(a.W[L] && a.winv[L], "persistent recurrence: a slot's split weights are missing");
+  AVC_CHECK_ARG(a.in_slot == 0 || (a.in_slot == a.nslot - 1 && a.xs && a.b0 && a.gx0 && (a.din == 384 || a.din == 512)),
+                "persistent recurrence: input slot operands are missing");
   a.spin_limit = kSpinLimit;
   if (g_persist_inject > 0) {
     --g_persist_inject;
@@ -904,10 +921,53 @@ bool lstm1_persist_eligible(int T, int B, int H) {
   return ngrp * (4 * H / 64) <= persist_capacity(H, RT);
 }
 
-size_t lstm1_persist_scratch(int T, int B, int H) {
+int g_persist_inproj = 1;  // avc_lstm_persist_inproj(): an input slot computes layer 0's input projection
+
+namespace {
+// The input slot's operands: x split per time step (scaled by the power of two of max |x| unless
+// its producer range-checked it: then unscaled, |x| < 65504, as the forward GEMM's guard would
+// leave it) into scratch; the split weights come from the caller (split_rows_kernel, K padded).
+int attach_inproj(avc_context* ctx, Scratch& sc, const InProj& ip, int T, int B, int slot, PersistArgs& a,
+                  hipStream_t s) {
+  const int Kp = inproj_kpad(ip.din);
+  const int ntile = (B + 15) / 16;
+  const long hszx = (long)ntile * 16 * Kp * 2 * 2;
+  AVC_TAKE(xs, unsigned char, (size_t)T * hszx, sc);
+  const unsigned* amax = nullptr;
+  if (!range_checked(ctx, ip.x)) {
+    AVC_TAKE(am, unsigned, 2, sc);
+    AVC_TRY(gemm_absmax(ip.x, (long)T * B, ip.din, ip.ldx, am, s));
+    amax = am;
+  }
+  const long total = (long)T * ntile * (Kp / 32) * 64;
+  split_steps16_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(
+      ip.x, ip.ldx, T, B, ip.din, Kp, ntile, hszx, xs, amax);
+  AVC_LAUNCH_CHECK();
+  a.xs = xs; a.hszx = hszx; a.din = Kp; a.b0 = ip.b0; a.x_amax = amax; a.in_slot = slot;
+  a.in_lead = g_persist_inproj;
+  a.W[slot] = reinterpret_cast<const unsigned char*>(ip.w_s);
+  a.winv[slot] = ip.winv;
+  return AVC_OK;
+}
+}  // namespace
+
+// the input slot's scratch: split x per time step, the split W_ih (when not cached), max |x|
+size_t inproj_scratch(int T, int B, int H, int din) {
+  const size_t ntile = (size_t)(B + 15) / 16, Kp = inproj_kpad(din);
+  return al((size_t)T * ntile * 16 * Kp * 2 * 2) + al((size_t)4 * H * Kp * 2 * 2 + 4 * H * sizeof(float)) +
+         al(2 * sizeof(unsigned));
+}
+
+bool lstm1_inproj_eligible(int T, int B, int H, int din) {
+  if (!g_persist_inproj || din <= 256 || din > 512 || din % 8 || !lstm1_persist_eligible(T, B, H)) return false;
+  const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
+  return 2 * ngrp * (4 * H / 64) <= persist_capacity(H, RT);
+}
+
+size_t lstm1_persist_scratch(int T, int B, int H, int din) {
   const size_t ntile = (size_t)(B + 15) / 16;
   const size_t hsz = ntile * 16 * H * 2 * 2;
-  return al((size_t)T * hsz) + 4096;
+  return al((size_t)T * hsz) + inproj_scratch(T, B, H, din) + 4096;
 }
 
 // One LSTM layer (decoder.lstm1, decoder.py:50,69) as one weight-stationary launch: slot 0 of the
@@ -915,21 +975,25 @@ size_t lstm1_persist_scratch(int T, int B, int H) {
 // projection + biases (permuted columns); whh_s / winv the split W_hh (lstm_split.hip layout).
 // y / c [T][B][H], g [T][B][4H] (permuted, optional: training).  Bit-identical to the
 // launch-per-step form (same products, same K split, same reduction order).
-int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx, const _Float16* whh_s,
-                          const float* winv, float* y, float* g, float* c, hipStream_t s) {
+int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, const _Float16* whh_s,
+                          const float* winv, float* y, float* g, float* c, hipStream_t s, const InProj* ip) {
   AVC_CHECK_ARG(lstm1_persist_eligible(T, B, H), "lstm1 persistent path: not eligible for this shape");
+  AVC_CHECK_ARG(!ip || lstm1_inproj_eligible(T, B, H, ip->din), "lstm1 input-projection slot: not eligible");
   AVC_TRY(persist_guard(ctx));
   Scratch sc(ctx);
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2 * 2;
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
-  const long gstride = (long)T * kRep * kLine;  // counter words per group: [T][kRep] lines
+  const int nslot = ip ? 2 : 1;
+  const long gstride = (long)nslot * T * kRep * kLine;  // counter words per group: [nslot][T][kRep] lines
   AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, ngrp * (4 * H / 64), (size_t)ngrp * gstride, s, &region));
+  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), (size_t)ngrp * gstride, s,
+                         &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
-  a.nslot = 1; a.cnt_gstride = gstride;
+  a.nslot = nslot; a.cnt_gstride = gstride;
+  if (ip) AVC_TRY(attach_inproj(ctx, sc, *ip, T, B, 1, a, s));
   a.W[0] = reinterpret_cast<const unsigned char*>(whh_s);
   a.winv[0] = winv;
   a.gx0 = gx;
@@ -941,7 +1005,7 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   AVC_TRY(persist_launch(a, RT, ngrp, s));
   if (ev) {
     // split W_hh read once; per step the split h operand of every workgroup's group, gx, h, c
-    const double flops = (double)T * 2.0 * B * H * 4.0 * H;
+    const double flops = (double)T * 2.0 * B * H * 4.0 * H + (ip ? (double)T * 2.0 * B * ip->din * 4.0 * H : 0.0);
     const double bytes = 16.0 * (double)H * H +
                          (double)T * (4.0 * B * H * a.ncb + 4.0 * B * 4.0 * H + 2.0 * 4.0 * B * H);
     timing_end(TC_LSTM1_PERSIST, ev, s, flops, bytes);
@@ -949,12 +1013,14 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, const float* gx
   return AVC_OK;
 }
 
-int g_persist_inproj = 1;  // avc_lstm_persist_inproj(): slot 3 computes lstm2's input projection
+
 
 // Slot 3 (layer 0's input projection inside the launch) needs K = 512 (4 chunks per wave) and a
 // fourth ncb-workgroup slot that is co-resident with the other three.
+int inproj_kpad(int din) { return din <= 384 ? 384 : 512; }
+
 bool lstm2_inproj_eligible(int T, int B, int H, int din) {
-  if (!g_persist_inproj || din != 512 || !lstm2_persist_eligible(T, B, H)) return false;
+  if (!g_persist_inproj || din <= 256 || din > 512 || din % 8 || !lstm2_persist_eligible(T, B, H)) return false;
   const int ntile = (B + 15) / 16, RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
   return 4 * (4 * H / 64) <= persist_capacity(H, RT);
 }
@@ -963,8 +1029,7 @@ size_t lstm2_persist_scratch(int T, int B, int H, int din) {
   const size_t ntile = (size_t)(B + 15) / 16;
   const size_t hsz = ntile * 16 * H * 2 * 2;
   return al((size_t)T * hsz) + al((size_t)2 * hsz) + al((size_t)kGxRing * (4 * H / 64) * 64 * 64 * sizeof(float)) +
-         al((size_t)T * ntile * 16 * din * 2 * 2) + al((size_t)4 * H * din * 2 * 2 + 4 * H * sizeof(float)) +
-         al(2 * sizeof(unsigned)) + 4096;
+         inproj_scratch(T, B, H, din) + 4096;
 }
 
 // gx0 [T][B][4H] (layer 0's input projection + biases, permuted columns) is computed by the
@@ -991,25 +1056,7 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = nslot; a.cnt_gstride = 0;
-  if (ip) {
-    // x split per time step for slot 3 (scaled by the power of two of max |x| unless its producer
-    // range-checked it: then unscaled, |x| < 65504, as the forward GEMM's guard would leave it)
-    const long hszx = (long)ntile * 16 * ip->din * 2 * 2;
-    AVC_TAKE(xs, unsigned char, (size_t)T * hszx, sc);
-    const unsigned* amax = nullptr;
-    if (!range_checked(ctx, ip->x)) {
-      AVC_TAKE(am, unsigned, 2, sc);
-      AVC_TRY(gemm_absmax(ip->x, (long)T * B, ip->din, ip->ldx, am, s));
-      amax = am;
-    }
-    const long total = (long)T * ntile * (ip->din / 32) * 64;
-    split_steps16_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(
-        ip->x, ip->ldx, T, B, ip->din, ntile, hszx, xs, amax);
-    AVC_LAUNCH_CHECK();
-    a.xs = xs; a.hszx = hszx; a.din = ip->din; a.b0 = ip->b0; a.x_amax = amax;
-    a.W[3] = reinterpret_cast<const unsigned char*>(ip->w_s);
-    a.winv[3] = ip->winv;
-  }
+  if (ip) AVC_TRY(attach_inproj(ctx, sc, *ip, T, B, 3, a, s));
   a.W[0] = reinterpret_cast<const unsigned char*>(w0_s);
   a.W[1] = reinterpret_cast<const unsigned char*>(w1i_s);
   a.W[2] = reinterpret_cast<const unsigned char*>(w1h_s);
@@ -1079,7 +1126,11 @@ extern "C" int avc_lstm_persist_layers(int mask) {
 }
 
 extern "C" int avc_lstm_persist_inproj(int on) {
-  avc::g_persist_inproj = on ? 1 : 0;
+  if (on < 0 || on > 3) {
+    avc::set_error("avc_lstm_persist_inproj: 0 (off), 1 (on), 2 / 3 (on with back-pressure every 4th / every step)");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_inproj = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -75,10 +75,11 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
                                                          const float* __restrict__ Bm, int Db,
                                                          int H, int perm,
                                                          _Float16* __restrict__ dst,
-                                                         float* __restrict__ winv) {
+                                                         float* __restrict__ winv, int Kp = 0) {
   const int p = blockIdx.x, tid = threadIdx.x;
   const int o = perm ? perm_to_orig(p, H) : p;
   const int K = Da + Db;
+  if (Kp < K) Kp = K;  // columns [K, Kp) are written as zeros (K padded to whole chunks per wave)
   const float* ra = A + (long)o * Da;
   const float* rb = Bm ? Bm + (long)o * Db : nullptr;
   float m = 0.f;
@@ -94,10 +95,10 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
   if (red[0] > 0.f) (void)frexpf(red[0], &e);  // max < 2^e
   const float sc = ldexpf(1.0f, 15 - e);
   if (tid == 0) winv[p] = ldexpf(1.0f, e - 15) * kHUnscale;
-  const int nck = K >> 5;
+  const int nck = Kp >> 5;
   _Float16* d = dst + (long)(p >> 4) * nck * 1024 + (p & 15) * 8;
-  for (int k = tid; k < K; k += 256) {
-    const float v = (k < Da ? ra[k] : rb[k - Da]) * sc;
+  for (int k = tid; k < Kp; k += 256) {
+    const float v = k >= K ? 0.f : (k < Da ? ra[k] : rb[k - Da]) * sc;
     _Float16 hi, lo;
     split16(v, hi, lo);
     _Float16* q = d + (k >> 5) * 1024 + ((k & 31) >> 3) * 128 + (k & 7);
@@ -608,10 +609,26 @@ size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers) {
   s += (size_t)(nlayers + 1) * al((size_t)nrb * (4 * H / 64) * (2 * H / 128 + 1) * 4096 * f);
   s += al((size_t)(T + 2) * 3 * nrb * (4 * H / 64) * sizeof(int));
   if (nlayers == 2 && B <= 64 && (H == 512 || H == 1024)) s += lstm2_persist_scratch(T, B, H, din);
-  if (nlayers == 1 && B <= 256 && (H == 512 || H == 1024)) s += lstm1_persist_scratch(T, B, H);
+  if (nlayers == 1 && B <= 256 && (H == 512 || H == 1024)) s += lstm1_persist_scratch(T, B, H, din);
   GemmDesc d;
   d.M = (int)TB; d.N = 4 * H; d.Kc = din; d.prec16 = 1;
   return s + gemm_scratch_bytes(d) + 4096;
+}
+
+// W_ih split for an input slot of a persistent recurrence (split_rows_kernel layout, K padded with
+// zero columns to inproj_kpad(din)), cached per weights version like the other derived weights.
+int split_wih(avc_context* ctx, Scratch& sc, const float* w_ih, int H, int din, InProj& ip, hipStream_t s) {
+  const int Kp = inproj_kpad(din);
+  bool fresh;
+  _Float16* ws = prep_or_scratch<_Float16>(ctx, sc, PREP_LSTM_WIH_SPLIT, w_ih, nullptr,
+                                           (size_t)4 * H * Kp * 2 + 8 * H, &fresh);
+  if (!ws) return AVC_ERR_WORKSPACE;
+  float* winv = reinterpret_cast<float*>(ws + (size_t)4 * H * Kp * 2);
+  if (fresh) split_rows_kernel<<<4 * H, 256, 0, s>>>(w_ih, din, nullptr, 0, H, 1, ws, winv, Kp);
+  AVC_LAUNCH_CHECK();
+  ip.w_s = ws;
+  ip.winv = winv;
+  return AVC_OK;
 }
 
 // One layer (lstm.hip: lstm_forward_impl's contract).  x [T*B][din] (ldx), y [T*B][ldy].
@@ -644,7 +661,14 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   if (f_whh) split_rows_kernel<<<4 * H, 256, 0, s>>>(w_hh, H, nullptr, 0, H, 1, whh_s, winv);
   if (f_b) perm_bias_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(b_ih, b_hh, b_p, H);
   AVC_LAUNCH_CHECK();
-  if (f_wih) AVC_TRY(permute_rows(w_ih, wih_p, H, din, s));
+  if (f_wih) AVC_TRY(permute_rows(w_ih, wih_p, H, din, s));  // cached: kept valid for either path
+  if (!reverse && ldy == H && lstm1_inproj_eligible(T, B, H, din) && ldx % 4 == 0 && aligned16(x)) {
+    // the recurrence and its input projection (an input slot on the CUs the batch groups leave
+    // idle) as one weight-stationary launch
+    InProj ip{x, (long)ldx, din, nullptr, nullptr, b_p};
+    AVC_TRY(split_wih(ctx, sc, w_ih, H, din, ip, s));
+    return lstm1_persist_forward(ctx, T, B, H, gx, whh_s, winv, y, saved_gates, saved_c, s, &ip);
+  }
   GemmDesc g;
   g.M = (int)TB; g.N = 4 * H; g.Kc = din;
   g.A = x; g.lda = ldx; g.a_rows = TB;
@@ -761,14 +785,8 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   if (lstm2_inproj_eligible(T, B, H, din) && ldx % 4 == 0 && aligned16(x)) {
     // the whole recurrence AND layer 0's input projection as one weight-stationary launch: the
     // projection runs per time step on the CUs the recurrence leaves idle (slot 3)
-    bool f_wis;
-    const size_t wisz = (size_t)4 * H * din * 2 + 8 * H;
-    _Float16* wi_s = prep_or_scratch<_Float16>(ctx, sc, PREP_LSTM_WIH_SPLIT, w0[0], nullptr, wisz, &f_wis);
-    if (!wi_s) return AVC_ERR_WORKSPACE;
-    float* winvi = reinterpret_cast<float*>(wi_s + (size_t)4 * H * din * 2);
-    if (f_wis) split_rows_kernel<<<4 * H, 256, 0, s>>>(w0[0], din, nullptr, 0, H, 1, wi_s, winvi);
-    AVC_LAUNCH_CHECK();
-    InProj ip{x, (long)ldx, din, wi_s, winvi, b0_p};
+    InProj ip{x, (long)ldx, din, nullptr, nullptr, b0_p};
+    AVC_TRY(split_wih(ctx, sc, w0[0], H, din, ip, s));
     return lstm2_persist_forward(ctx, T, B, H, gx, w0_s, winv0, w1i_s, winv1i, w1h_s, winv1h, b1_p,
                                  y0, y1, g0, c0, g1, c1, s, &ip);
   }

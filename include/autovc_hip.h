@@ -259,10 +259,11 @@ int avc_persist_check(avc_context* ctx, void* stream, int* failed);
  * a plain launch after an occupancy check (0, default).  Both require every workgroup to be
  * co-resident; the cooperative launch has the runtime guarantee it. */
 int avc_lstm_persist_coop(int on);
-/* Tuning hook: decoder lstm2's layer-0 input projection (decoder.py:53,74: the x W_ih0^T term of
- * nn.LSTM) computed inside the persistent launch, one time step at a time on the CUs the
- * recurrence leaves idle (1, default), or by a GEMM before the launch (0; then the persistent and
- * launch-per-step forms are bit-identical). */
+/* Tuning hook: decoder lstm1's and lstm2's layer-0 input projection (decoder.py:50,53: the
+ * x W_ih0^T term of nn.LSTM) computed inside the persistent launch, one time step at a time on the
+ * CUs the recurrence leaves idle (1, default), or by a GEMM before the launch (0; then the
+ * persistent and launch-per-step forms are bit-identical).  2 / 3: as 1 with the input slot held
+ * at most 12 steps ahead of the recurrence, checked every 4th step / every step (experiments). */
 int avc_lstm_persist_inproj(int on);
 /* Tuning hook for the encoder BiLSTM (H = 32) recurrence: 1 (default) = hardware exp/reciprocal
  * gate math and an 8-step prefetch of the input projection; 0 = libm gate math, 3-step prefetch. */

@@ -302,7 +302,7 @@ def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
     GEMM beforehand (avc_lstm_persist_inproj(0)) the two compute the same products in the same
     order, so every output is bit-identical, on the eager call and on the captured-graph replays.
     With the projection inside the launch (slot 3, the default) the hand-off forms 1 and 2 agree
-    bit for bit, and both stay within 2e-5 of the GEMM-fed result (different summation order of
+    bit for bit, and both stay within 5e-5 of the GEMM-fed result (different summation order of
     the K = 512 projection).  No workgroup of any persistent launch abandoned a bounded wait."""
     import ctypes
     from autovc_amd import _lib
@@ -337,7 +337,7 @@ def test_lstm2_persistent_matches_step_launches(cuda_device, B, T):
         assert torch.equal(a, b), f"input slot, hand-off forms differ on {name}: {(a - b).abs().max().item():.3e}"
     d = max((a - b).abs().max().item() for a, b in zip(outs[0, 0], outs[2, 1]))
     print(f"B={B} T={T}: input-projection slot vs GEMM-fed max|d| {d:.2e}")
-    assert d <= 2e-5
+    assert d <= 5e-5
 
 
 def test_back_to_back_forwards_match(cuda_device):
