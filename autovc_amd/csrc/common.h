@@ -187,6 +187,7 @@ enum PrepKind : int {
   PREP_LSTM_BIAS,       // permuted b_ih + b_hh
   PREP_LSTM_WHH,        // split-f16 fragment-major W_hh (+ per-row unscale after it)
   PREP_LSTM_WIH_SPLIT,  // W_ih in the same split layout (lstm2's input-projection slot)
+  PREP_BILSTM_WIH,      // [W_ih_f; W_ih_r] + summed biases (encoder BiLSTM's one input product)
 };
 
 // Persistent buffer for derived weights, or nullptr when no caching call is active (the caller

@@ -1022,7 +1022,7 @@ Plan make_plan(const GemmDesc& d, int force_split) {
   // long-K products (weight gradients: K = T*B rows) take 128x128 tiles and split K until the
   // grid has ~4 workgroups per CU
   const bool longk = (long)d.Kc * d.ntaps >= 8192 && d.M >= 128 && d.N >= 128;
-  const bool big = (long)d.M * d.N >= 256L * 128 * 128 / 2 || longk;
+  const bool big = (long)d.M * d.N > 256L * 128 * 128 / 2 || longk;
   p.bm = big ? 128 : 64;
   p.bn = big ? 128 : 64;
   p.tilesM = (d.M + p.bm - 1) / p.bm;

@@ -775,6 +775,24 @@ __global__ __launch_bounds__(64) void lstm32_bwd_kernel(int T, int B, int revers
 
 inline int ew_blocks(long n) { return (int)std::min<long>((n + 255) / 256, 8192); }
 
+// [W_ih_f; W_ih_r] (256 x din) followed by the 256 summed biases (b_ih + b_hh per direction)
+__global__ void concat_wih_kernel(const float* __restrict__ wf, const float* __restrict__ wr,
+                                  const float* __restrict__ bif, const float* __restrict__ bhf,
+                                  const float* __restrict__ bir, const float* __restrict__ bhr, int din,
+                                  float* __restrict__ out) {
+  const long n = 128L * din;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < 2 * n + 256; i += (long)gridDim.x * 256) {
+    float v;
+    if (i < n) v = wf[i];
+    else if (i < 2 * n) v = wr[i - n];
+    else {
+      const int j = (int)(i - 2 * n);
+      v = j < 128 ? bif[j] + bhf[j] : bir[j - 128] + bhr[j - 128];
+    }
+    out[i] = v;
+  }
+}
+
 }  // namespace
 
 size_t lstm_forward_scratch(int T, int B, int din, int H, bool training) {
@@ -874,8 +892,9 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
 size_t bilstm_forward_scratch(int T, int B, int din, int H, bool training) {
   if (H != 32) return lstm_forward_scratch(T, B, din, H, training);
   GemmDesc d;
-  d.M = T * B; d.N = 128; d.Kc = din; d.prec16 = 1;
-  return (size_t)T * B * 256 * sizeof(float) + gemm_scratch_bytes(d) + 1024;
+  d.M = T * B; d.N = 256; d.Kc = din; d.prec16 = 1;
+  return (size_t)T * B * 256 * sizeof(float) + ((size_t)256 * din + 256) * sizeof(float) + 256 +
+         gemm_scratch_bytes(d) + 1024;
 }
 
 // Bidirectional layer (encoder.py:51): y[:, 0:H] forward, y[:, H:2H] reverse.  H = 32: both input
@@ -891,24 +910,31 @@ int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const fl
   Scratch sc(ctx);
   const long TB = (long)T * B;
   AVC_TAKE(gx, float, (size_t)TB * 256, sc);
-  for (int dir = 0; dir < 2; ++dir) {
-    const float* const* w = dir ? wr : wf;
-    GemmDesc g;
-    g.M = (int)TB; g.N = 128; g.Kc = din;
-    g.A = x; g.lda = ldx; g.a_rows = TB;
-    g.b_trans = 1; g.ldb = din; g.B = w[0]; g.bias0 = w[2]; g.bias1 = w[3];
-    g.C = gx + dir * 128; g.ldc = 256;
-    g.prec16 = 1;
-    if (ctx->prep_version >= 0) {
-      bool fb = true;
-      auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_GEMM_BFRAG, w[0], nullptr, gemm_bfrag_bytes(g), &fb));
-      if (bf) {
-        if (fb) AVC_TRY(gemm_prepare_bfrag(g, bf, s));
-        g.b_frag = bf;
-      }
-    }
-    AVC_TRY(gemm_run(ctx, g, s));
+  // both directions' input projections as ONE product against [W_ih_f; W_ih_r] (256 x din) with
+  // the summed biases: x is split once, and gx comes out as [T*B][fwd 128 | bwd 128]
+  bool fw;
+  float* wcat = prep_or_scratch<float>(ctx, sc, PREP_BILSTM_WIH, wf[0], wr[0], (size_t)256 * din + 256, &fw);
+  if (!wcat) return AVC_ERR_WORKSPACE;
+  if (fw) {
+    concat_wih_kernel<<<ew_blocks(256L * din + 256), 256, 0, s>>>(wf[0], wr[0], wf[2], wf[3], wr[2], wr[3], din,
+                                                                  wcat);
+    AVC_LAUNCH_CHECK();
   }
+  GemmDesc g;
+  g.M = (int)TB; g.N = 256; g.Kc = din;
+  g.A = x; g.lda = ldx; g.a_rows = TB;
+  g.b_trans = 1; g.ldb = din; g.B = wcat; g.bias0 = wcat + 256L * din;
+  g.C = gx; g.ldc = 256;
+  g.prec16 = 1;
+  if (ctx->prep_version >= 0) {
+    bool fb = true;
+    auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_GEMM_BFRAG, wcat, nullptr, gemm_bfrag_bytes(g), &fb));
+    if (bf) {
+      if (fb || fw) AVC_TRY(gemm_prepare_bfrag(g, bf, s));
+      g.b_frag = bf;
+    }
+  }
+  AVC_TRY(gemm_run(ctx, g, s));
   hipEvent_t ev = timing_begin(TC_LSTM32, s);
   L32Dir d0{gx, wf[1], y, g_f, c_f, 0};
   L32Dir d1{gx + 128, wr[1], y + 32, g_r, c_r, 1};
