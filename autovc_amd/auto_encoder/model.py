@@ -383,19 +383,25 @@ class AutoEncoder(nn.Module):
         X = X.to(self._flat_param.device, torch.float32).contiguous()
         c_org = c_org.to(self._flat_param.device, torch.float32).contiguous()
         self._check(X, None, "X")
-        out_decoder, out_postnet, content_codes = self._forward_layers(X, c_org, c_org)
-        loss = self._loss(X=X, c_org=c_org, out_decoder=out_decoder, out_postnet=out_postnet,
-                          content_codes=content_codes)
-        self.optimiser.zero_grad()
-        if dp.world() > 1:
-            # data parallel: bucketed RCCL all-reduce of the flat gradient, issued while backward
-            # still runs (dp.GradBuckets), then /world
-            red = self._grad_buckets()
-            with red.armed():
+        # parameter gradients are accumulated in place into the flat gradient by the layers'
+        # backward kernels (ops.GradSink), not returned and added by autograd
+        red = self._grad_buckets() if dp.world() > 1 else None
+        ops.set_grad_sink(ops.GradSink(notify=red.param_ready if red is not None else None))
+        try:
+            out_decoder, out_postnet, content_codes = self._forward_layers(X, c_org, c_org)
+            loss = self._loss(X=X, c_org=c_org, out_decoder=out_decoder, out_postnet=out_postnet,
+                              content_codes=content_codes)
+            self.optimiser.zero_grad()
+            if red is not None:
+                # data parallel: bucketed RCCL all-reduce of the flat gradient, issued while
+                # backward still runs (dp.GradBuckets), then /world
+                with red.armed():
+                    loss.backward()
+                red.finish()
+            else:
                 loss.backward()
-            red.finish()
-        else:
-            loss.backward()
+        finally:
+            ops.set_grad_sink(None)
         self.optimiser.step(max_norm=max_norm, ema=self.avg_params, ema_decay=ema_decay)
         return loss.detach(), self.optimiser.last_grad_norm
 

@@ -342,13 +342,13 @@ int avc_linear_backward(avc_context* ctx, int M, int din, int dout, const float*
   dx.M = M; dx.N = din; dx.Kc = dout;
   dx.A = d_y; dx.lda = dout;
   dx.B = weight; dx.ldb = din;
-  dx.C = d_x; dx.ldc = din; dx.accumulate = accumulate;
+  dx.C = d_x; dx.ldc = din; dx.accumulate = accumulate == 1;
   dx.prec16 = 1; dx.split_scale = 1;
   GemmDesc dw;  // d_W = d_y^T x
   dw.M = dout; dw.N = din; dw.Kc = M;
   dw.A = d_y; dw.a_trans = 1; dw.lda = dout;
   dw.B = x; dw.ldb = din; dw.b_rows = M;
-  dw.C = d_weight; dw.ldc = din; dw.accumulate = accumulate;
+  dw.C = d_weight; dw.ldc = din; dw.accumulate = accumulate != 0;
   dw.prec16 = 1; dw.split_scale = 1;
   AVC_TRY(ensure_arena(ctx, std::max(gemm_scratch_bytes(dx), gemm_scratch_bytes(dw)) +
                                 colsum_scratch(M, dout) + 8192));
@@ -358,7 +358,7 @@ int avc_linear_backward(avc_context* ctx, int M, int din, int dout, const float*
   dx.amax_a = dw.amax_a = amax_dy;
   if (d_x) AVC_TRY(gemm_run(ctx, dx, S(stream)));
   if (d_weight) AVC_TRY(gemm_run(ctx, dw, S(stream)));
-  if (d_bias) AVC_TRY(colsum(ctx, M, dout, d_y, dout, d_bias, accumulate, S(stream)));
+  if (d_bias) AVC_TRY(colsum(ctx, M, dout, d_y, dout, d_bias, accumulate != 0, S(stream)));
   return AVC_OK;
 }
 

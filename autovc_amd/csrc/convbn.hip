@@ -143,12 +143,16 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
                               int accumulate, hipStream_t s) {
   AVC_CHECK_ARG(T > 0 && B > 0, "conv_backward: empty input");
   AVC_CHECK_ARG(cin % 4 == 0 && cout % 4 == 0, "conv_backward: channels must be multiples of 4");
+  AVC_CHECK_ARG(accumulate >= 0 && accumulate <= 2, "conv_backward: accumulate must be 0, 1 or 2");
   const long TB = (long)T * B;
+  // accumulate: 1 = every output adds into its buffer, 2 = only the parameter gradients do
+  // (d_x overwritten: the caller accumulates parameter gradients in place across uses)
+  const int acc_x = accumulate == 1, acc_p = accumulate != 0;
   Scratch sc(ctx);
   AVC_TAKE(dy, float, (size_t)TB * cout, sc);
   AVC_TRY(bn_backward(ctx, (int)TB, cout, d_out, y_pre, mean, invstd, gamma, beta, act, training,
-                      d_gamma, d_beta, accumulate, dy, s));
-  if (d_bias) AVC_TRY(colsum(ctx, (int)TB, cout, dy, cout, d_bias, accumulate, s));
+                      d_gamma, d_beta, acc_p, dy, s));
+  if (d_bias) AVC_TRY(colsum(ctx, (int)TB, cout, dy, cout, d_bias, acc_p, s));
   AVC_TAKE(amax_dy, unsigned, 64, sc);  // one max|dY| scan shared by dgrad and wgrad
   AVC_TRY(gemm_absmax(dy, TB, cout, cout, amax_dy, s));
   if (d_x) {
@@ -159,7 +163,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
     g.M = (int)TB; g.N = cin; g.Kc = cout; g.ntaps = 5;
     g.A = dy; g.lda = cout; g.a_rows = TB; g.a_shift0 = -2L * B; g.a_tapshift = B;
     g.B = wd; g.ldb = cin; g.b_rows = cout; g.b_tapoff = (long)cout * cin;
-    g.C = d_x; g.ldc = cin; g.accumulate = accumulate;
+    g.C = d_x; g.ldc = cin; g.accumulate = acc_x;
     g.prec16 = 1; g.split_scale = 1; g.amax_a = amax_dy;
     AVC_TRY(gemm_run(ctx, g, s));
   }
@@ -170,7 +174,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
     g.A = dy; g.a_trans = 1; g.lda = cout;
     g.B = x; g.ldb = cin; g.b_rows = TB; g.b_shift0 = -2L * B; g.b_zshift = B;
     g.nz = 5; g.c_zoff = 1;
-    g.C = d_weight; g.ldc = 5L * cin; g.ldc_col = 5; g.accumulate = accumulate;
+    g.C = d_weight; g.ldc = 5L * cin; g.ldc_col = 5; g.accumulate = acc_p;
     g.prec16 = 1; g.split_scale = 1; g.amax_a = amax_dy;
     AVC_TRY(gemm_run(ctx, g, s));
   }

@@ -43,7 +43,8 @@ __global__ void colsum_partial_kernel(int M, int N, const float* __restrict__ X,
 
 // 64 columns per block, the 16 waves split the R partial rows; fp64 combine through LDS.
 __global__ __launch_bounds__(1024) void colsum_final_kernel(int R, int N, const float* __restrict__ part,
-                                                            float* __restrict__ out, int accumulate) {
+                                                            float* __restrict__ out, int accumulate,
+                                                            float* __restrict__ out2) {
   __shared__ double red[16][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + cl;
@@ -57,6 +58,7 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(int R, int N, const 
 #pragma unroll
   for (int g = 0; g < 16; ++g) t += red[g][cl];
   out[n] = accumulate ? out[n] + (float)t : (float)t;
+  if (out2) out2[n] = accumulate ? out2[n] + (float)t : (float)t;  // a second sink (LSTM b_ih / b_hh)
 }
 
 void colsum_geometry(int M, int N, int& R, int& rows_per) {
@@ -553,13 +555,13 @@ size_t colsum_scratch(int M, int N) {
 }
 
 int colsum(avc_context* ctx, int M, int N, const float* X, long ld, float* out, int accumulate,
-           hipStream_t s) {
+           hipStream_t s, float* out2) {
   int R, rp;
   colsum_geometry(M, N, R, rp);
   Scratch sc(ctx);
   AVC_TAKE(part, float, (size_t)R * N, sc);
   colsum_partial_kernel<<<dim3((N + 255) / 256, R), 256, 0, s>>>(M, N, X, ld, rp, part);
-  colsum_final_kernel<<<(N + 63) / 64, 1024, 0, s>>>(R, N, part, out, accumulate);
+  colsum_final_kernel<<<(N + 63) / 64, 1024, 0, s>>>(R, N, part, out, accumulate, out2);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

@@ -8,7 +8,7 @@ namespace avc {
 // ---- reductions / elementwise (elementwise.hip) ----
 // out[n] (+)= sum_m X[m*ld + n]   (fixed-order, deterministic)
 int colsum(avc_context* ctx, int M, int N, const float* X, long ld, float* out, int accumulate,
-           hipStream_t s);
+           hipStream_t s, float* out2 = nullptr);
 size_t colsum_scratch(int M, int N);
 
 // ---- LSTM (lstm.hip) ----

@@ -715,6 +715,13 @@ void launch_lstm32(int nblk, int T, int B, long ldgx, long ldy, const L32Dir& d0
   else lstm32_fwd_kernel<8, true><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
 }
 
+// BPTT of an H = 32 direction: one single-wave workgroup per utterance walks the steps backwards.
+// Lane j (< 32) owns hidden unit j's cell math; lanes 32..63 add the other half of the
+// dh = W_hh^T dG sum.  The per-step operands (dy, the saved gates, c_t, c_{t-1}) come from a
+// register ring refilled PF steps ahead (loop unrolled by PF: static slots; refills are
+// unconditional and clamped so no join waits on them), and the dG broadcast through LDS needs
+// no barrier: one wave's LDS operations complete in issue order (see lstm32_fwd_kernel).
+template <int PF>
 __global__ __launch_bounds__(64) void lstm32_bwd_kernel(int T, int B, int reverse,
                                                         const float* __restrict__ whh,
                                                         const float* __restrict__ gates,
@@ -731,45 +738,73 @@ __global__ __launch_bounds__(64) void lstm32_bwd_kernel(int T, int B, int revers
   dgs[lane + 64] = 0.f;
   float dc = 0.f;
   __syncthreads();
-  for (int s = T - 1; s >= 0; --s) {
-    const int t = reverse ? T - 1 - s : s;
-    const long row = (long)t * B + b;
-    float part = 0.f;
+  // iteration k walks s = T-1-k; time index t(s) and its predecessor in forward order
+  auto tof = [&](int k) {
+    const int s = T - 1 - min(k, T - 1);
+    return reverse ? T - 1 - s : s;
+  };
+  auto tprev = [&](int k) {
+    const int s = T - 1 - min(k, T - 1);
+    return reverse ? T - s : s - 1;  // may be T or -1 at the ends (then unused)
+  };
+  float rdy[PF], rg[PF][4], rc[PF], rcp[PF];
+  auto fetch = [&](int k, int u) {
+    const long row = (long)tof(k) * B + b;
+    const int tp = tprev(k);
+    rdy[u] = dy[row * lddy + j];
+    const float* g = gates + row * 128;
+    rg[u][0] = g[j]; rg[u][1] = g[32 + j]; rg[u][2] = g[64 + j]; rg[u][3] = g[96 + j];
+    rc[u] = cs[row * 32 + j];
+    const int tpc = min(max(tp, 0), T - 1);
+    rcp[u] = cs[((long)tpc * B + b) * 32 + j];
+  };
 #pragma unroll
-    for (int q4 = 0; q4 < 16; ++q4) {
-      const float4 g4 = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
-      part += wc[4 * q4] * g4.x + wc[4 * q4 + 1] * g4.y + wc[4 * q4 + 2] * g4.z + wc[4 * q4 + 3] * g4.w;
+  for (int u = 0; u < PF; ++u) fetch(u, u);
+  for (int k0 = 0; k0 < T; k0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int k = k0 + u;
+      const float dyv = rdy[u], ig = rg[u][0], fg = rg[u][1], gg = rg[u][2], og = rg[u][3];
+      const float c = rc[u], cpv = rcp[u];
+      fetch(k + PF, u);  // unconditional (clamped): the slot is never a join of old and new values
+      if (k < T) {
+        const int s = T - 1 - k;
+        const int t = reverse ? T - 1 - s : s;
+        const long row = (long)t * B + b;
+        float part = 0.f;
+#pragma unroll
+        for (int q4 = 0; q4 < 16; ++q4) {
+          const float4 g4 = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
+          part += wc[4 * q4] * g4.x + wc[4 * q4 + 1] * g4.y + wc[4 * q4 + 2] * g4.z + wc[4 * q4 + 3] * g4.w;
+        }
+        part += __shfl_xor(part, 32);
+        float dzi = 0.f, dzf = 0.f, dzg = 0.f, dzo = 0.f;
+        if (lane < 32) {
+          const float dh = dyv + part;
+          const float cp = s > 0 ? cpv : 0.f;
+          const float tc = tanhf(c);
+          const float dct = dh * og * (1.f - tc * tc) + dc;
+          dc = dct * fg;
+          dzi = dct * gg * ig * (1.f - ig);
+          dzf = dct * cp * fg * (1.f - fg);
+          dzg = dct * ig * (1.f - gg * gg);
+          dzo = dh * tc * og * (1.f - og);
+          float* o = dg + row * 128;
+          o[j] = dzi;
+          o[32 + j] = dzf;
+          o[64 + j] = dzg;
+          o[96 + j] = dzo;
+          // one wave: these LDS writes land after this step's dgs reads (issue order)
+          dgs[j] = dzi;
+          dgs[32 + j] = dzf;
+          dgs[64 + j] = dzg;
+          dgs[96 + j] = dzo;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
     }
-    part += __shfl_xor(part, 32);
-    float dzi = 0.f, dzf = 0.f, dzg = 0.f, dzo = 0.f;
-    if (lane < 32) {
-      const float dh = dy[row * lddy + j] + part;
-      const float* g = gates + row * 128;
-      const float ig = g[j], fg = g[32 + j], gg = g[64 + j], og = g[96 + j];
-      const float c = cs[row * 32 + j];
-      const int tp = reverse ? t + 1 : t - 1;
-      const float cp = s > 0 ? cs[((long)tp * B + b) * 32 + j] : 0.f;
-      const float tc = tanhf(c);
-      const float dct = dh * og * (1.f - tc * tc) + dc;
-      dc = dct * fg;
-      dzi = dct * gg * ig * (1.f - ig);
-      dzf = dct * cp * fg * (1.f - fg);
-      dzg = dct * ig * (1.f - gg * gg);
-      dzo = dh * tc * og * (1.f - og);
-      float* o = dg + row * 128;
-      o[j] = dzi;
-      o[32 + j] = dzf;
-      o[64 + j] = dzg;
-      o[96 + j] = dzo;
-    }
-    __syncthreads();
-    if (lane < 32) {
-      dgs[j] = dzi;
-      dgs[32 + j] = dzf;
-      dgs[64 + j] = dzg;
-      dgs[96 + j] = dzo;
-    }
-    __syncthreads();
   }
 }
 
@@ -1092,7 +1127,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   const bool gemm_bptt = !small && B >= 32 && (H == 512 || H == 1024) &&
                          (g_bptt_mode == 2 || (g_bptt_mode == 1 && H == 1024));
   if (small) {
-    lstm32_bwd_kernel<<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
+    lstm32_bwd_kernel<8><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
     AVC_LAUNCH_CHECK();
   } else if (gemm_bptt) {
     // W_hh^T permuted ([H][4H]: row j = hidden unit, k = permuted gate row), split once with the
@@ -1214,8 +1249,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   AVC_TRY(gemm_run(ctx, g2, s));
 
   if (small) {
-    AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, d_b_ih, accumulate_dw, s));
-    AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, d_b_hh, accumulate_dw, s));
+    AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, d_b_ih, accumulate_dw, s, d_b_hh));  // d_b_ih = d_b_hh
   } else {
     AVC_TAKE(db_p, float, (size_t)4 * H, sc);
     AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, db_p, 0, s));

@@ -42,8 +42,10 @@ class GradBuckets:
     loss runs twice, model.py:215-219, so its gradients are final only at the very end).  Each
     bucket is a contiguous slice of `flat_grad`, so it is reduced in place, without a copy.
 
-    A post-accumulate-grad hook counts each parameter once per backward (the autograd engine sums
-    every use of a leaf before its one AccumulateGrad call).  When a bucket is complete its
+    A parameter counts once per backward, when its gradient is complete: from a
+    post-accumulate-grad hook (the autograd engine sums every use of a leaf before its one
+    AccumulateGrad call), or -- with in-place gradients (ops.GradSink, train_step) -- from
+    `param_ready`, which the layers' backward calls after the last use's gradient is written.  When a bucket is complete its
     all-reduce is issued with async_op=True, which orders it after the gradient kernels already
     on the stream and lets the rest of backward run beside it.  Buckets are issued strictly in
     index order, so every rank issues the same collectives in the same order.  `finish()` issues
@@ -85,6 +87,7 @@ class GradBuckets:
                 self.bucket_of[i] = b
         self.sizes = [len(m) for m in members]
         self._armed = False
+        self._index = {id(p): i for i, p in enumerate(params)}
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
         self.reset()
 
@@ -92,16 +95,27 @@ class GradBuckets:
         self.pending = list(self.sizes)
         self.next = 0
         self.handles = []
+        self.seen = set()
         self.launch_log = []        # (bucket, parameters still pending overall) per issue
+
+    def _ready(self, i):
+        if not self._armed or i in self.seen:
+            return
+        self.seen.add(i)
+        self.pending[self.bucket_of[i]] -= 1
+        self._issue(ready_only=True)
 
     def _make_hook(self, i):
         def hook(_p):
-            if not self._armed:
-                return
-            b = self.bucket_of[i]
-            self.pending[b] -= 1
-            self._issue(ready_only=True)
+            self._ready(i)
         return hook
+
+    def param_ready(self, p):
+        """A parameter's gradient is complete (in-place gradients, ops.GradSink: the layers write
+        `p.grad` themselves, so autograd's accumulate hooks never run)."""
+        i = self._index.get(id(p))
+        if i is not None:
+            self._ready(i)
 
     def _issue(self, ready_only):
         while self.next < len(self.buckets) and (not ready_only or self.pending[self.next] <= 0):

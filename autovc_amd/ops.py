@@ -37,6 +37,66 @@ def _c(t):
     return None if t is None else t.contiguous()
 
 
+class GradSink:
+    """In-place parameter gradients (AutoEncoder.train_step sets one for its forward + backward).
+
+    Without a sink every backward returns fresh parameter gradients and autograd adds each into
+    `p.grad` with a separate elementwise launch (~130 per training step).  With a sink, a layer's
+    backward accumulates its parameter gradients straight into `p.grad` (the views of the flat
+    gradient, AutoEncoder._ensure_flat) inside the same kernels (accumulate flag) and returns None
+    for them.  The forward counts every use of a parameter (the encoder runs twice per loss,
+    model.py:201); when the last use's backward has written, `notify(p)` fires -- the data-parallel
+    bucketed all-reduce (dp.GradBuckets.param_ready) hangs off it."""
+
+    def __init__(self, notify=None):
+        self.notify = notify
+        self.uses = {}
+
+    def use(self, *params):
+        for p in params:
+            if p is not None and p.requires_grad:
+                self.uses[id(p)] = self.uses.get(id(p), 0) + 1
+
+    def done(self, p):
+        n = self.uses.get(id(p), 1) - 1
+        self.uses[id(p)] = n
+        if n <= 0 and self.notify is not None:
+            self.notify(p)
+
+
+_sink: GradSink | None = None
+
+
+def set_grad_sink(sink: GradSink | None):
+    global _sink
+    _sink = sink
+
+
+def _use(*params):
+    if _sink is not None:
+        _sink.use(*params)
+
+
+def _param_grads(params, needs):
+    """Gradient buffers for a layer's parameters: their own `.grad` (in place, accumulating) when
+    a sink is active and every needed one exists, else fresh tensors.  Returns (buffers, direct)."""
+    if _sink is not None and all(p.grad is not None and p.grad.is_contiguous() and p.grad.shape == p.shape
+                                 for p, n in zip(params, needs) if n and p is not None):
+        return [p.grad if (n and p is not None) else None for p, n in zip(params, needs)], True
+    return [torch.empty_like(p) if (n and p is not None) else None for p, n in zip(params, needs)], False
+
+
+def _param_done(params, bufs, direct):
+    """What backward returns for the parameters: None (written in place; the sink is told) or the
+    fresh gradients."""
+    if not direct:
+        return bufs
+    for p, b in zip(params, bufs):
+        if b is not None:
+            _sink.done(p)
+    return [None] * len(bufs)
+
+
 class FramesFromMel(torch.autograd.Function):
     """x (B,cm,T) [+ emb (B,ce) broadcast over T] -> frames [T*B][cm+ce]
     (encoder.py:65-66 concat; model.py:127 transpose)."""
@@ -102,7 +162,9 @@ class ConvBNAct(torch.autograd.Function):
              ptr(_c(bias)), ptr(gamma), ptr(beta), ptr(running_mean), ptr(running_var),
              int(training), float(momentum), float(eps), act, ptr(_c(residual)), ptr(y_pre), ptr(out),
              ptr(mean), ptr(invstd), _stream(x))
+        _use(weight, bias, gamma, beta)
         ctx.save_for_backward(x, weight, gamma, beta, y_pre, mean, invstd)
+        ctx.bias = bias
         ctx.cfg = (T, B, cin, cout, int(training), act, residual is not None, bias is not None)
         return out
 
@@ -113,14 +175,13 @@ class ConvBNAct(torch.autograd.Function):
         d_out = d_out.contiguous()
         ng = ctx.needs_input_grad
         dx = _empty(x.shape, x) if ng[0] else None
-        dw = _empty(weight.shape, x) if ng[1] else None
-        db = _empty((cout,), x) if (has_bias and ng[2]) else None
-        dg = _empty((cout,), x) if ng[3] else None
-        dbt = _empty((cout,), x) if ng[4] else None
+        params = (weight, ctx.bias if has_bias else None, gamma, beta)
+        (dw, db, dg, dbt), direct = _param_grads(params, ng[1:5])
         call("avc_conv_bn_act_backward", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
              ptr(gamma), ptr(beta), ptr(y_pre), ptr(mean), ptr(invstd), training, act, ptr(d_out),
-             ptr(dx), ptr(dw), ptr(db), ptr(dg), ptr(dbt), 0, _stream(x))
+             ptr(dx), ptr(dw), ptr(db), ptr(dg), ptr(dbt), 2 if direct else 0, _stream(x))
         d_res = d_out if (has_res and ng[11]) else None
+        dw, db, dg, dbt = _param_done(params, (dw, db, dg, dbt), direct)
         return dx, dw, db, dg, dbt, None, None, None, None, None, None, d_res, None, None
 
 
@@ -135,18 +196,18 @@ def _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, reverse, save, T, B):
     return gates, cst
 
 
-def _lstm_bwd(x, w_ih, w_hh, y, col, ldy, gates, cst, d_y, d_x, reverse, acc, T, B):
+def _lstm_bwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, gates, cst, d_y, d_x, reverse, acc, T, B, needs):
     H = w_hh.shape[1]
     din = x.shape[1]
-    dwi = torch.empty_like(w_ih)
-    dwh = torch.empty_like(w_hh)
-    dbi = _empty((4 * H,), x)
-    dbh = _empty((4 * H,), x)
+    params = (w_ih, w_hh, b_ih, b_hh)
+    (dwi, dwh, dbi, dbh), direct = _param_grads(params, needs)
+    # the kernels write all four: fill the ones autograd does not want with scratch
+    scratch = [torch.empty_like(p) if b is None else b for p, b in zip(params, (dwi, dwh, dbi, dbh))]
     call("avc_lstm_backward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
          ptr(w_hh.contiguous()), y.data_ptr() + col * F32, ldy, ptr(gates), ptr(cst),
-         d_y.data_ptr() + col * F32, ptr(d_x), ptr(dwi), ptr(dwh), ptr(dbi), ptr(dbh), int(acc), 0,
+         d_y.data_ptr() + col * F32, ptr(d_x), *[ptr(t) for t in scratch], int(acc), int(direct),
          _stream(x))
-    return dwi, dwh, dbi, dbh
+    return tuple(_param_done(params, (dwi, dwh, dbi, dbh), direct))
 
 
 class LSTMLayer(torch.autograd.Function):
@@ -158,8 +219,10 @@ class LSTMLayer(torch.autograd.Function):
         H = w_hh.shape[1]
         y = _empty((T * B, H), x)
         gates, cst = _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, 0, H, False, save, T, B)
+        _use(w_ih, w_hh, b_ih, b_hh)
         if save:
             ctx.save_for_backward(x, w_ih, w_hh, y, gates, cst)
+            ctx.biases = (b_ih, b_hh)
         ctx.dims = (T, B)
         return y
 
@@ -169,7 +232,8 @@ class LSTMLayer(torch.autograd.Function):
         T, B = ctx.dims
         d_y = d_y.contiguous()
         d_x = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        dwi, dwh, dbi, dbh = _lstm_bwd(x, w_ih, w_hh, y, 0, y.shape[1], gates, cst, d_y, d_x, False, 0, T, B)
+        dwi, dwh, dbi, dbh = _lstm_bwd(x, w_ih, w_hh, *ctx.biases, y, 0, y.shape[1], gates, cst, d_y, d_x, False, 0,
+                                       T, B, ctx.needs_input_grad[1:5])
         return d_x, dwi, dwh, dbi, dbh, None, None, None
 
 
@@ -187,19 +251,23 @@ class BiLSTMLayer(torch.autograd.Function):
         ws = [(ctypes.c_void_p * 4)(*[ptr(t) for t in grp]) for grp in keep]
         call("avc_bilstm_forward", _ctx(x), T, B, x.shape[1], H, ptr(x), x.shape[1], ws[0], ws[1], ptr(y),
              2 * H, ptr(g_f), ptr(c_f), ptr(g_r), ptr(c_r), _stream(x))
+        _use(wi_f, wh_f, bi_f, bh_f, wi_r, wh_r, bi_r, bh_r)
         if save:
             ctx.save_for_backward(x, wi_f, wh_f, wi_r, wh_r, y, g_f, c_f, g_r, c_r)
+            ctx.biases = (bi_f, bh_f, bi_r, bh_r)
         ctx.dims = (T, B, H)
         return y
 
     @staticmethod
     def backward(ctx, d_y):
         x, wi_f, wh_f, wi_r, wh_r, y, g_f, c_f, g_r, c_r = ctx.saved_tensors
+        bi_f, bh_f, bi_r, bh_r = ctx.biases
         T, B, H = ctx.dims
         d_y = d_y.contiguous()
-        d_x = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        gf = _lstm_bwd(x, wi_f, wh_f, y, 0, 2 * H, g_f, c_f, d_y, d_x, False, 0, T, B)
-        gr = _lstm_bwd(x, wi_r, wh_r, y, H, 2 * H, g_r, c_r, d_y, d_x, True, 1, T, B)
+        ng = ctx.needs_input_grad
+        d_x = torch.empty_like(x) if ng[0] else None
+        gf = _lstm_bwd(x, wi_f, wh_f, bi_f, bh_f, y, 0, 2 * H, g_f, c_f, d_y, d_x, False, 0, T, B, ng[1:5])
+        gr = _lstm_bwd(x, wi_r, wh_r, bi_r, bh_r, y, H, 2 * H, g_r, c_r, d_y, d_x, True, 1, T, B, ng[5:9])
         return (d_x,) + gf + gr + (None, None, None)
 
 
@@ -262,7 +330,9 @@ class Linear(torch.autograd.Function):
         y = _empty((M, dout), x)
         call("avc_linear_forward", _ctx(x), M, din, dout, ptr(x), ptr(weight.contiguous()), ptr(_c(bias)),
              ptr(y), _stream(x))
+        _use(weight, bias)
         ctx.save_for_backward(x, weight)
+        ctx.bias = bias
         ctx.has_bias = bias is not None
         return y
 
@@ -274,10 +344,11 @@ class Linear(torch.autograd.Function):
         dout = weight.shape[0]
         ng = ctx.needs_input_grad
         dx = torch.empty_like(x) if ng[0] else None
-        dw = torch.empty_like(weight) if ng[1] else None
-        db = _empty((dout,), x) if (ctx.has_bias and ng[2]) else None
+        params = (weight, ctx.bias if ctx.has_bias else None)
+        (dw, db), direct = _param_grads(params, ng[1:3])
         call("avc_linear_backward", _ctx(x), M, din, dout, ptr(x), ptr(weight.contiguous()), ptr(d_y),
-             ptr(dx), ptr(dw), ptr(db), 0, _stream(x))
+             ptr(dx), ptr(dw), ptr(db), 2 if direct else 0, _stream(x))
+        dw, db = _param_done(params, (dw, db), direct)
         return dx, dw, db
 
 

@@ -85,6 +85,9 @@ int avc_conv_bn_act_backward(avc_context* ctx, int T, int B, int cin, int cout, 
                              int training, int act, const float* d_out, float* d_x,
                              float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
                              int accumulate, void* stream);
+/* accumulate (conv and linear backward): 0 = every output overwritten, 1 = every output adds
+ * into its buffer, 2 = only the parameter gradients add (d_x overwritten) -- parameter
+ * gradients accumulated in place across the uses of a layer (the encoder runs twice per loss). */
 
 /* ---- LSTM layer (one direction) -----------------------------------------------------------
  * Replaces one layer-direction of nn.LSTM (gates i,f,g,o; zero initial state) as used at

@@ -103,3 +103,22 @@ def test_bench_refuses_fewer_gpus_than_requested():
                        capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode != 0 and "GPU(s) are visible" in (r.stdout + r.stderr)
     assert '"metric"' not in r.stdout
+
+
+def test_grad_sink_counts_uses():
+    """ops.GradSink (in-place parameter gradients): a parameter is reported complete only after the
+    backward of its last forward use (the encoder's parameters are used twice per loss)."""
+    import torch
+    from autovc_amd import ops
+    done = []
+    sink = ops.GradSink(notify=done.append)
+    a = torch.nn.Parameter(torch.zeros(3))
+    b = torch.nn.Parameter(torch.zeros(2))
+    sink.use(a, b, None)
+    sink.use(a)
+    sink.done(a)
+    assert done == []
+    sink.done(b)
+    assert done == [b]
+    sink.done(a)
+    assert done == [b, a]
