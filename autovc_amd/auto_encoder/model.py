@@ -386,7 +386,8 @@ class AutoEncoder(nn.Module):
         # parameter gradients are accumulated in place into the flat gradient by the layers'
         # backward kernels (ops.GradSink), not returned and added by autograd
         red = self._grad_buckets() if dp.world() > 1 else None
-        ops.set_grad_sink(ops.GradSink(notify=red.param_ready if red is not None else None))
+        if self.inplace_grads:
+            ops.set_grad_sink(ops.GradSink(notify=red.param_ready if red is not None else None))
         try:
             out_decoder, out_postnet, content_codes = self._forward_layers(X, c_org, c_org)
             loss = self._loss(X=X, c_org=c_org, out_decoder=out_decoder, out_postnet=out_postnet,
@@ -414,6 +415,7 @@ class AutoEncoder(nn.Module):
         return red
 
     bucket_bytes = 16 << 20  # data-parallel all-reduce bucket (≈7 buckets over the 113.7 MB gradient)
+    inplace_grads = True     # train_step: layers accumulate parameter gradients in place (ops.GradSink)
 
     def learn(self, trainloader, n_epochs=AutoEncoderParams["learn"]["n_epochs"],
               log_freq=AutoEncoderParams["learn"]["log_freq"],
