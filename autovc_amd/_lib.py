@@ -65,6 +65,7 @@ _SIGS = {
     "avc_lstm_persist_coop": [_I],
     "avc_lstm_persist_inproj": [_I],
     "avc_lstm32_tune": [_I],
+    "avc_bptt_persist": [_I],
     "avc_debug_persist_inject": [_I],
     "avc_graph_mode": [_I],
     "avc_timing_reset": [],

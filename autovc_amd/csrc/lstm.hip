@@ -1094,6 +1094,7 @@ size_t lstm_backward_scratch(int T, int B, int din, int H) {
   s += 2 * ((size_t)B + 64) * 4 * H * f + 512;  // fragment-major dG ping-pong
   // split-K BPTT (bptt_row_kernel): split W_hh^T, split dG rows, <= 32 partial slabs, row scales
   s += gemm_afrag_bytes(H, 4 * H) + gemm_afrag_bytes(B + 31, 4 * H) + 32 * (size_t)B * H * f + (size_t)B * f + 2048;
+  s += bptt_persist_scratch(B, H);  // the persistent BPTT's double-buffered slabs, split dG, dc
   GemmDesc d1;  // dW_ih
   d1.M = 4 * H; d1.N = din; d1.Kc = (int)TB; d1.a_trans = 1; d1.b_rows = TB;
   d1.prec16 = 1; d1.split_scale = 1;
@@ -1122,10 +1123,12 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   float* dwhh_dst = d_w_hh;
   int acc_w = accumulate_dw;
 
+  // the whole recurrence as one persistent launch where eligible (lstm_persist.hip), else
   // split-K products where they measured faster (scripts/bptt_ab.py, B = 256: H = 1024 7.95 vs
   // 9.44 ms per layer backward; H = 512 4.02 vs 3.40 ms, so the step kernel stays there)
-  const bool gemm_bptt = !small && B >= 32 && (H == 512 || H == 1024) &&
-                         (g_bptt_mode == 2 || (g_bptt_mode == 1 && H == 1024));
+  const bool persist_bptt = !small && g_bptt_mode != 0 && saved_gates && saved_c && bptt_persist_eligible(T, B, H);
+  const bool gemm_bptt = persist_bptt || (!small && B >= 32 && (H == 512 || H == 1024) &&
+                                          (g_bptt_mode == 2 || (g_bptt_mode == 1 && H == 1024)));
   if (small) {
     lstm32_bwd_kernel<8><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
     AVC_LAUNCH_CHECK();
@@ -1157,7 +1160,9 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TRY(zero_async(dc, sizeof(float) * B * H, s));
     AVC_TRY(zero_async(dgs, gemm_afrag_bytes(arows, 4 * H), s));  // padding rows stay zero
     AVC_LAUNCH_CHECK();
-    for (int st = T - 1; st >= 0; --st) {
+    if (persist_bptt)
+      AVC_TRY(bptt_persist_run(ctx, T, B, H, reverse, whhT_s, amax_w, d_y, ldy, saved_gates, saved_c, dg, s));
+    for (int st = persist_bptt ? -1 : T - 1; st >= 0; --st) {
       const int t = reverse ? T - 1 - st : st;
       const int tp = reverse ? t + 1 : t - 1;
       BpttArgs a{};

@@ -68,6 +68,7 @@ int g_persist_pd = 2;    // avc_lstm_persist_depth(): h chunks in flight ahead o
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -162,24 +163,29 @@ int g_persist_diag = 0;
 // One lane waits until *p reaches target (wrap-safe; relaxed agent-scope polls).  false = gave
 // up, or another workgroup of this launch (epoch E) did: the give-up word is checked every 64
 // polls.  The first workgroup to give up reports the launch to the host.
-__device__ bool wait_ge(unsigned* p, unsigned target, const PersistArgs& a, unsigned E) {
+__device__ bool wait_ge_ctl(unsigned* p, unsigned target, unsigned* tmo, unsigned* fail_host, unsigned spin_limit,
+                            unsigned E) {
   gu32* gp = (gu32*)(p);
-  gu32* gt = (gu32*)(a.tmo);
+  gu32* gt = (gu32*)(tmo);
   for (unsigned spins = 0;; ++spins) {
     if ((int)(__hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) return true;
     if ((spins & 63) == 63 && __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E)
       return false;
-    if (spins >= a.spin_limit) {
+    if (spins >= spin_limit) {
       const unsigned old = __hip_atomic_fetch_max(gt, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old != E) {  // first to give up in this launch: a device-wide unique failure number
         const unsigned n = atomicAdd(&g_persist_giveups, 1u) + 1u;
-        if (a.fail_host)
-          __hip_atomic_store(a.fail_host, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (fail_host)
+          __hip_atomic_store(fail_host, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
   }
+}
+
+__device__ __forceinline__ bool wait_ge(unsigned* p, unsigned target, const PersistArgs& a, unsigned E) {
+  return wait_ge_ctl(p, target, a.tmo, a.fail_host, a.spin_limit, E);
 }
 
 // power of two the x split was scaled by (split_steps16_kernel): max |x| -> [2^14, 2^15)
@@ -864,6 +870,317 @@ void set_region_args(PersistArgs& a, avc_context* ctx, unsigned* region) {
   a.fail_host = ctx->fail_host;
 }
 
+
+// ---- Persistent BPTT (backward recurrence of a stacked-LSTM layer as ONE launch) ----------
+//
+// The launch-per-step BPTT (lstm.hip: gemm_frag_partials + bptt_row_kernel) costs ~28 us per
+// H = 1024 step at B = 256: two launches, a 16-split product whose workgroups re-stream their
+// W_hh^T slice every step, and a per-row epilogue.  Here all T steps run in one launch of 256
+// workgroups (one per CU), each with two roles per step:
+//   phase A (product):  workgroup (rt, ct, sp) owns a 128 x 128 output tile (batch rows x hidden
+//     units) over K-slice sp of the gate dimension; its W_hh^T slice (128 units x K/nsplit gates,
+//     split hi/lo) stays in LDS for the whole launch.  It reads the split dG_{t+1} rows of its
+//     tile and K-slice, multiplies (3xf16, like gemm16f), unscales each row by the row's scale
+//     for that K-slice and stores the fp32 partial to slab[sp].
+//   phase B (epilogue): workgroup (rb, q) owns 32 batch rows x U = H / nsplit hidden units,
+//     i.e. exactly K-slice q of dG_t: it sums the nsplit partials (fixed order) into dh, does the
+//     gate derivatives, dc, writes dG_t (fp32, for the weight gradients and dX) and splits dG_t
+//     for the next step's product with a power-of-two scale per (row, K-slice) -- a scale that
+//     is uniform over the slice a phase-A workgroup multiplies, so it factors out of the product.
+// Hand-offs use the protocol of the forward persistent kernels (write-through stores of whole
+// lines, drained before an agent-scope counter add; the consumer polls, then sc1 loads; epoch-
+// tagged counters that are never reset; bounded spins with a give-up word).  Dependencies:
+//   phase A (rt, ct, sp) at step k waits cntB[k-1][rt][sp] = 4 (the 4 row blocks of its K-slice),
+//   phase B (rb, q) at step k waits cntA[k][rt][ct] = nsplit (every K-slice of its tile).
+// Write-after-read safety: slab[sp] rows of tile rt are rewritten at step k+1 only after all of
+// the tile's phase-B readers of step k counted in (cntB), and a split dG block is rewritten at
+// step k+1 only after every phase-A reader of step k+1's tile counted in (cntA).
+__device__ __forceinline__ float pow2_scale(float m) {  // max |x| -> [2^14, 2^15) (split_scale_of)
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, 15 - e);
+}
+
+struct BpttPArgs {
+  int B, H, T, reverse, nsplit, nrt, ntn;
+  const _Float16* whhT_s;   // W_hh^T permuted, fragment-major split ([H] rows x [4H] k), scale of amax_w
+  const unsigned* amax_w;
+  float* slab;              // [2][nsplit][B][H] unscaled partials (step parity)
+  float* rowscale;          // [2][nsplit][B] power-of-two scale of split dG row b over K-slice q
+  _Float16* dgs;            // [2] x fragment-major split dG ([B/32] row blocks x [4H] k)
+  float* dc;                // [B][H] carried cell-state gradient
+  const float* dy; long lddy;
+  const float* gates;       // [T][B][4H] saved activated gates (permuted)
+  const float* c;           // [T][B][H] saved cell states
+  float* dg;                // [T][B][4H] output dG (permuted)
+  unsigned* cnt;            // cntA [T][nrt][ntn] then cntB [T][nrt][nsplit], one 128-B line each
+  unsigned* tmo;
+  unsigned long long* tickets;
+  unsigned* fail_host;
+  int nwg;
+  unsigned spin_limit;
+  int diag;                 // timing experiments (avc_debug_bptt_diag), 0 in production
+};
+
+// NCH: 16-deep chunks per K-slice (4H / nsplit / 16); U = H / nsplit hidden units per phase-B
+// workgroup (= 4 * NCH); NS = nsplit.  slab, rowscale and dgs are double-buffered by step parity:
+// a buffer written at step k is rewritten at step k + 2 only, and the counter chain in between
+// (B(k+1) waits on every K-slice of a tile, A(k+2) on B(k+1)) orders every reader of step k
+// before that.
+template <int NCH, int NS>
+__global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
+  constexpr int U = 4 * NCH;
+  constexpr int KS = 16 * NCH;               // gate columns per K-slice
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_b[];
+  unsigned char* wl = lds_b;                 // [4 col tiles][NCH][hi, lo] 1 KiB blocks
+  unsigned* rmax = reinterpret_cast<unsigned*>(lds_b + 4 * NCH * 2048);  // [32] row max (float bits)
+  int* flag = reinterpret_cast<int*>(rmax + 32);                         // [4]
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int B = a.B, H = a.H, T = a.T, G4 = 4 * H, nkc = G4 / 16;
+  constexpr int nsplit = NS;
+  const long dgs_buf = (long)(B / 32) * nkc * 1024;  // halves per dgs buffer
+  const int wg = blockIdx.x;
+  // phase A role
+  const int sp = wg % nsplit, tile = wg / nsplit, rt = tile / a.ntn, ct = tile % a.ntn;
+  const int wm = w >> 1, wn = w & 1;         // 4 x 2 waves over the 128 x 128 tile (32 x 64 each)
+  // phase B role (workgroups beyond the (row block, K-slice) pairs have none)
+  const int nrb = B / 32;
+  const bool has_b = wg < nrb * nsplit;
+  const int rb = wg / nsplit, q = wg % nsplit;
+  unsigned* cntA = a.cnt;
+  unsigned* cntB = a.cnt + (long)T * a.nrt * a.ntn * 32;
+  auto ia = [&](int k, int r, int c) { return (((long)k * a.nrt + r) * a.ntn + c) * 32; };
+  auto ib = [&](int k, int r, int s2) { return (((long)k * a.nrt + r) * nsplit + s2) * 32; };
+
+  // stationary W_hh^T slice: col tiles ct*4 .. ct*4+3, chunks sp*NCH .. sp*NCH+NCH-1
+  for (int blk = w; blk < 4 * NCH * 2; blk += 8) {
+    const int hl = blk & 1, c = (blk >> 1) % NCH, c4 = (blk >> 1) / NCH;
+    const long src = (((long)(ct * 4 + c4) * nkc + sp * NCH + c) * 2 + hl) * 512;  // halves
+    const f16x8 v = *reinterpret_cast<const f16x8*>(a.whhT_s + src + lane * 8);
+    *reinterpret_cast<f16x8*>(wl + ((c4 * NCH + c) * 2 + hl) * 1024 + lane * 16) = v;
+  }
+  if (tid == 0) {
+    const unsigned long long tk = __hip_atomic_fetch_add(a.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[2] = (int)(unsigned)(tk / (unsigned long long)a.nwg + 1ull);
+  }
+  __syncthreads();
+  const unsigned E = (unsigned)flag[2];
+  const float sw_inv = 1.f / pow2_scale(__uint_as_float(*a.amax_w));
+  // phase B thread task: row r (of 32), unit group g4 (4 units = one 16-deep k chunk of the slice)
+  const int br = tid & 31, bg = tid >> 5;   // 32 rows x 16 groups per pass (U / 4 groups)
+  const bool b_task = has_b && bg < U / 4;
+  const int b_row = rb * 32 + br;
+  const int j0 = q * U + bg * 4;           // first hidden unit of the task
+  const int kq = q * KS + bg * 16;         // first (permuted) gate column of the task
+
+  int k = 0;
+  bool ok = true;
+  for (; k < T && ok; ++k) {
+    const int st = T - 1 - k;
+    const int t = a.reverse ? T - 1 - st : st;
+    const int tp = a.reverse ? t + 1 : t - 1;
+    // ---------------- phase A: slab[sp] = (dG_{t+1} . W_hh)[tile, K-slice sp] ----------------
+    if (k > 0) {
+      if (tid == 0) flag[0] = (a.diag & 4) ? 1 : wait_ge_ctl(cntB + ib(k - 1, rt, sp), E * 4u, a.tmo, a.fail_host, a.spin_limit, E);
+      __syncthreads();
+      if (!flag[0]) { ok = false; break; }
+      const int rblk = rt * 4 + wm;  // this wave's 32-row block
+      const int rbuf = (k - 1) & 1;  // dG_{t+1}, written by phase B of step k - 1
+      const auto ars = __builtin_amdgcn_make_buffer_rsrc(a.dgs + rbuf * dgs_buf + ((long)rblk * nkc + sp * NCH) * 1024,
+                                                         0, NCH * 2048, 0x00020000);
+      f32x16 part[2], crs[2];
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) part[jn][e] = crs[jn][e] = 0.f;
+      // A chunks in batches of CB, the next batch's loads issued before this batch's MFMAs
+      constexpr int CB = NCH < 4 ? NCH : 4;
+      constexpr int NB = NCH / CB;
+      f16x8 ah[2][CB], al[2][CB];
+#define AVC_BP_LOAD(BI)                                                                           \
+  _Pragma("unroll") for (int c = 0; c < CB; ++c) {                                                \
+    if (a.diag & 1) { ah[(BI) & 1][c] = al[(BI) & 1][c] = f16x8{}; } else {                       \
+    ah[(BI) & 1][c] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(ars, lane * 16, ((BI) * CB + c) * 2048, 16)); \
+    al[(BI) & 1][c] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(ars, lane * 16, ((BI) * CB + c) * 2048 + 1024, 16)); } \
+  }
+      AVC_BP_LOAD(0)
+#pragma unroll
+      for (int bi = 0; bi < NB; ++bi) {
+        if (bi + 1 < NB) { AVC_BP_LOAD(bi + 1) }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+#pragma unroll
+          for (int jn = 0; jn < 2; ++jn) {
+            const unsigned char* pb = wl + (((wn * 2 + jn) * NCH + bi * CB + c) * 2) * 1024 + lane * 16;
+            const f16x8 bh = *reinterpret_cast<const f16x8*>(pb);
+            const f16x8 bl = *reinterpret_cast<const f16x8*>(pb + 1024);
+            part[jn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bi & 1][c], bh, part[jn], 0, 0, 0);
+            crs[jn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bi & 1][c], bl, crs[jn], 0, 0, 0);
+            crs[jn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[bi & 1][c], bh, crs[jn], 0, 0, 0);
+          }
+        }
+      }
+#undef AVC_BP_LOAD
+      // unscale row by row: 1 / (scale of this row's split over K-slice sp * scale of W)
+      const int row0 = rt * 128 + wm * 32;
+      const float rsv = lane < 32 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                           __builtin_amdgcn_make_buffer_rsrc(a.rowscale + ((long)rbuf * nsplit + sp) * B + row0, 0, 128, 0x00020000),
+                                                           lane * 4, 0, 16))
+                                  : 1.f;
+      const float inv = sw_inv / rsv;
+      const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.slab + ((long)(k & 1) * nsplit + sp) * B * H, 0, B * H * 4,
+                                                         0x00020000);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const float ie = __shfl(inv, r);
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) {
+          const int col = ct * 128 + wn * 64 + jn * 32 + (lane & 31);
+          const float v = (part[jn][e] + crs[jn][e] * (1.f / 2048.f)) * ie;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), srs, ((row0 + r) * H + col) * 4, 0,
+                                                16 /*sc1*/);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_fetch_add((gu32*)(cntA + ia(k, rt, ct)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---------------- phase B: dG_t for rows rb, K-slice q -------------------------------------
+    if (has_b) {
+      // this step's own operands (written before the launch, or by this workgroup) are loaded
+      // before the wait for the partials
+      const long tb = (long)t * B + b_row;
+      f32x4 dyv = {}, ig = {}, fg = {}, gg = {}, og = {}, cc = {}, cpv = {}, dcv = {};
+      if (b_task) {
+        dyv = *reinterpret_cast<const f32x4*>(a.dy + (long)t * B * a.lddy + (long)b_row * a.lddy + j0);
+        const float* gp = a.gates + tb * G4 + kq;
+        ig = *reinterpret_cast<const f32x4*>(gp);
+        fg = *reinterpret_cast<const f32x4*>(gp + 4);
+        gg = *reinterpret_cast<const f32x4*>(gp + 8);
+        og = *reinterpret_cast<const f32x4*>(gp + 12);
+        cc = *reinterpret_cast<const f32x4*>(a.c + tb * H + j0);
+        if (st > 0) cpv = *reinterpret_cast<const f32x4*>(a.c + ((long)tp * B + b_row) * H + j0);
+        dcv = *reinterpret_cast<f32x4*>(a.dc + (long)b_row * H + j0);
+      }
+      if (k > 0) {
+        if (tid == 0)
+          flag[1] = (a.diag & 4) ? 1 : wait_ge_ctl(cntA + ia(k, rb / 4, (q * U) / 128), E * (unsigned)nsplit, a.tmo, a.fail_host,
+                                a.spin_limit, E);
+        if (tid < 32) rmax[tid] = 0u;
+        __syncthreads();
+        if (!flag[1]) { ok = false; break; }
+      } else {
+        if (tid < 32) rmax[tid] = 0u;
+        __syncthreads();
+      }
+      float d[16];
+      float mx = 0.f;
+      if (b_task) {
+        f32x4 rec = {0.f, 0.f, 0.f, 0.f};
+        if (k > 0) {
+          const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)(k & 1) * nsplit * B * H, 0,
+                                                             nsplit * B * H * 4, 0x00020000);
+          constexpr int SB = NS < 16 ? NS : 16;  // partials in flight per batch (registers)
+#pragma unroll
+          for (int s0 = 0; s0 < NS; s0 += SB) {
+            f32x4 pv[SB];
+#pragma unroll
+            for (int s2 = 0; s2 < SB; ++s2)
+              pv[s2] = (a.diag & 2) ? f32x4{} : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     srs, (int)((((long)(s0 + s2) * B + b_row) * H + j0) * 4), 0, 16));
+#pragma unroll
+            for (int s2 = 0; s2 < SB; ++s2) rec += pv[s2];  // fixed split order
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float dh = dyv[u] + rec[u];
+          const float tc = tanhf(cc[u]);
+          const float dct = dh * og[u] * (1.f - tc * tc) + dcv[u];
+          dcv[u] = dct * fg[u];
+          d[u] = dct * gg[u] * ig[u] * (1.f - ig[u]);
+          d[4 + u] = dct * cpv[u] * fg[u] * (1.f - fg[u]);
+          d[8 + u] = dct * ig[u] * (1.f - gg[u] * gg[u]);
+          d[12 + u] = dh * tc * og[u] * (1.f - og[u]);
+        }
+        *reinterpret_cast<f32x4*>(a.dc + (long)b_row * H + j0) = dcv;
+        float* go = a.dg + tb * G4 + kq;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(go + 4 * g) = f32x4{d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]};
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, fabsf(d[e]));
+        atomicMax(rmax + br, __float_as_uint(mx));
+      }
+      __syncthreads();
+      if (st > 0) {  // the split for the next step's product (none after the last step)
+        if (b_task) {
+          const float sb = pow2_scale(__uint_as_float(rmax[br]));
+          // chunk kq / 16 of row block rb: lanes (row) and (row + 32) hold k 0-7 and 8-15
+          typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+          h8 hi0, lo0, hi1, lo1;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v0 = d[e] * sb, v1 = d[8 + e] * sb;
+            const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+            hi0[e] = h0; lo0[e] = (_Float16)((v0 - (float)h0) * 2048.0f);
+            hi1[e] = h1; lo1[e] = (_Float16)((v1 - (float)h1) * 2048.0f);
+          }
+          const auto drs = __builtin_amdgcn_make_buffer_rsrc(a.dgs + (k & 1) * dgs_buf + ((long)rb * nkc + kq / 16) * 1024,
+                                                             0, 2048, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi0), drs, br * 16, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi1), drs, (br + 32) * 16, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo0), drs, 1024 + br * 16, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo1), drs, 1024 + (br + 32) * 16, 0, 16);
+          if (bg == 0) {
+            const auto rrs = __builtin_amdgcn_make_buffer_rsrc(a.rowscale + ((long)(k & 1) * nsplit + q) * B + rb * 32, 0,
+                                                               128, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, sb), rrs, br * 4, 0, 16);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+          __hip_atomic_fetch_add((gu32*)(cntB + ib(k, rb / 4, q)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  // gave up at step k: this workgroup's dG slices of the remaining steps are NaN (never plausible)
+  if (!ok && b_task) {
+    for (int kk = k; kk < T; ++kk) {
+      const int st = T - 1 - kk;
+      const int t = a.reverse ? T - 1 - st : st;
+      float* go = a.dg + ((long)t * B + b_row) * G4 + kq;
+      for (int e = 0; e < 16; ++e) go[e] = __builtin_nanf("");
+    }
+  }
+}
+
+size_t bptt_lds(int nch) { return (size_t)4 * nch * 2048 + 32 * 4 + 16; }
+
+const void* bptt_fn(int nch, int ns) {
+  if (nch == 16 && ns == 16) return (const void*)bptt_persist_kernel<16, 16>;
+  if (nch == 8 && ns == 32) return (const void*)bptt_persist_kernel<8, 32>;
+  if (nch == 4 && ns == 32) return (const void*)bptt_persist_kernel<4, 32>;
+  return nullptr;
+}
+
+// the tiling of a (B, H) problem: 128 x 128 tiles x nsplit K-slices = 256 workgroups
+bool bptt_plan(int B, int H, int& nrt, int& ntn, int& ns, int& nch) {
+  if (B % 128 || H % 128 || B > 256) return false;
+  nrt = B / 128;
+  ntn = H / 128;
+  if (256 % (nrt * ntn)) return false;
+  ns = 256 / (nrt * ntn);
+  if ((4 * H) % (16 * ns)) return false;
+  nch = 4 * H / 16 / ns;
+  return bptt_fn(nch, ns) != nullptr;
+}
+
 }  // namespace
 
 unsigned* host_flags(avc_context* ctx) {
@@ -1081,6 +1398,92 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   return AVC_OK;
 }
 
+int g_bptt_persist = 1;  // avc_bptt_persist(): the persistent BPTT where eligible
+int g_bptt_diag = 0;     // avc_debug_bptt_diag(): timing experiments (results invalid when set)
+
+bool bptt_persist_eligible(int T, int B, int H) {
+  int nrt, ntn, ns, nch;
+  if (!g_bptt_persist || T < 2 || !bptt_plan(B, H, nrt, ntn, ns, nch)) return false;
+  struct Entry { const void* fn; int dev; int cap; };
+  static std::vector<Entry> cache;
+  const void* fn = bptt_fn(nch, ns);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  int cap = -1;
+  for (const auto& e : cache)
+    if (e.fn == fn && e.dev == dev) cap = e.cap;
+  if (cap < 0) {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bptt_lds(nch));
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 512, bptt_lds(nch)) != hipSuccess) {
+      (void)hipGetLastError();
+      per_cu = 0;
+    }
+    cap = per_cu * device_cus();
+    cache.push_back({fn, dev, cap});
+  }
+  return cap >= 256;  // every workgroup co-resident
+}
+
+size_t bptt_persist_scratch(int B, int H) {
+  int nrt, ntn, ns, nch;
+  if (!bptt_plan(B, H, nrt, ntn, ns, nch)) return 0;
+  return al((size_t)2 * ns * B * H * sizeof(float)) + al((size_t)2 * ns * B * sizeof(float)) +
+         al((size_t)2 * (B / 32) * (4 * H / 16) * 2048) + al((size_t)B * H * sizeof(float)) + 4096;
+}
+
+// BPTT of one LSTM layer direction over all T steps as one launch (see bptt_persist_kernel).
+// whhT_s / amax_w: W_hh^T permuted and split (lstm.hip); d_y [T][B] rows (ldy), gates / c the
+// forward's saved activations, dg [T][B][4H] output.
+int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _Float16* whhT_s,
+                     const unsigned* amax_w, const float* d_y, long ldy, const float* gates, const float* c,
+                     float* dg, hipStream_t s) {
+  int nrt, ntn, ns, nch;
+  AVC_CHECK_ARG(bptt_persist_eligible(T, B, H) && bptt_plan(B, H, nrt, ntn, ns, nch),
+                "persistent BPTT: not eligible for this shape");
+  AVC_TRY(persist_guard(ctx));
+  Scratch sc(ctx);
+  AVC_TAKE(slab, float, (size_t)2 * ns * B * H, sc);
+  AVC_TAKE(rowscale, float, (size_t)2 * ns * B, sc);
+  AVC_TAKE(dgs, _Float16, (size_t)2 * (B / 32) * (4 * H / 16) * 1024, sc);
+  AVC_TAKE(dc, float, (size_t)B * H, sc);
+  AVC_TRY(zero_async(dc, sizeof(float) * B * H, s));
+  unsigned* region = nullptr;
+  const size_t words = ((size_t)T * nrt * ntn + (size_t)T * nrt * ns) * 32;
+  AVC_TRY(persist_region(ctx, 3, T, nrt, ntn, 256, words, s, &region));
+  BpttPArgs a{};
+  a.B = B; a.H = H; a.T = T; a.reverse = reverse; a.nsplit = ns; a.nrt = nrt; a.ntn = ntn;
+  a.whhT_s = whhT_s; a.amax_w = amax_w; a.slab = slab; a.rowscale = rowscale; a.dgs = dgs; a.dc = dc;
+  a.dy = d_y; a.lddy = ldy; a.gates = gates; a.c = c; a.dg = dg;
+  a.tickets = reinterpret_cast<unsigned long long*>(region);
+  a.tmo = region + 32;
+  a.cnt = region + kRegionHeaderWords;
+  a.fail_host = ctx->fail_host;
+  a.nwg = 256;
+  a.spin_limit = kSpinLimit;
+  a.diag = g_bptt_diag;
+  if (g_persist_inject > 0) {
+    --g_persist_inject;
+    a.spin_limit = 0;
+  }
+  const void* fn = bptt_fn(nch, ns);
+  void* args[] = {&a};
+  hipEvent_t ev = timing_begin(TC_LSTM_STEP_BWD, s);
+  if (g_persist_coop)
+    AVC_HIP(hipLaunchCooperativeKernel(fn, dim3(256), dim3(512), args, (unsigned)bptt_lds(nch), s));
+  else
+    AVC_HIP(hipLaunchKernel(fn, dim3(256), dim3(512), args, bptt_lds(nch), s));
+  if (ev) {
+    // the recurrent products of T - 1 steps; algorithmic bytes: the split dG read and the
+    // partials written and read per step, the epilogue operands, dG written
+    const double flops = (double)(T - 1) * 2.0 * B * H * 4.0 * H;
+    const double bytes = (double)(T - 1) * (4.0 * B * 4.0 * H * 256 / (nrt * ntn * ns) * nrt * ntn +
+                                            2.0 * 4.0 * ns * B * H) + (double)T * 4.0 * B * H * 12.0;
+    timing_end(TC_LSTM_STEP_BWD, ev, s, flops, bytes);
+  }
+  return AVC_OK;
+}
+
 }  // namespace avc
 
 #ifdef AVC_STAMPS
@@ -1131,6 +1534,17 @@ extern "C" int avc_lstm_persist_inproj(int on) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_inproj = on;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_debug_bptt_diag(int bits) {
+  avc::g_bptt_diag = bits;
+  return AVC_OK;
+}
+
+extern "C" int avc_bptt_persist(int on) {
+  avc::g_bptt_persist = on ? 1 : 0;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -271,6 +271,12 @@ int avc_lstm_persist_inproj(int on);
 /* Tuning hook for the encoder BiLSTM (H = 32) recurrence: 1 (default) = hardware exp/reciprocal
  * gate math and an 8-step prefetch of the input projection; 0 = libm gate math, 3-step prefetch. */
 int avc_lstm32_tune(int mode);
+/* Tuning hook: the BPTT of LSTM layers with B = 128 / 256 and H a multiple of 128 as one
+ * persistent launch (1, default; lstm_persist.hip: bptt_persist_kernel) or launch per step (0). */
+int avc_bptt_persist(int on);
+/* Diagnostic hook (timing experiments only; results are NOT valid while set): bit 0 skips the
+ * persistent BPTT's dG operand loads, bit 1 its partial loads, bit 2 its waits. */
+int avc_debug_bptt_diag(int bits);
 /* Test hook: the next `launches` persistent launches give up at their first unsatisfied wait (as
  * if a peer workgroup never became resident); eager launches only (captured graphs are dropped). */
 int avc_debug_persist_inject(int launches);

@@ -1,0 +1,36 @@
+"""Time of the BPTT recurrence alone (timing class lstm_step_bwd: the persistent launch, or the sum
+of the per-step launches) for one LSTM layer backward at B = 256, T = 128."""
+import sys
+
+import torch
+
+sys.path.insert(0, __file__.rsplit("/", 2)[0])
+from autovc_amd import _lib, ops  # noqa: E402
+
+dev = torch.device("cuda:0")
+B, T = 256, 128
+for H, din in ((1024, 1024), (512, 320)):
+    g = torch.Generator().manual_seed(H)
+    k = 1.0 / H ** 0.5
+    ws = [((torch.rand(*s, generator=g) * 2 - 1) * k).to(dev).requires_grad_(True)
+          for s in [(4 * H, din), (4 * H, H), (4 * H,), (4 * H,)]]
+    x = (torch.randn(T * B, din, generator=g) * 0.5).to(dev).requires_grad_(True)
+    dy = torch.randn(T * B, H, generator=g).to(dev)
+    for persist in (1, 0):
+        _lib.call("avc_bptt_persist", persist)
+        for rep in range(4):
+            y = ops.LSTMLayer.apply(x, *ws, T, B, True)
+            torch.cuda.synchronize()
+            if rep == 3:
+                _lib.timing_enable(["lstm_step_bwd"])
+                _lib.timing_reset()
+            y.backward(dy)
+            torch.cuda.synchronize()
+            x.grad = None
+            for w in ws:
+                w.grad = None
+        r = _lib.timing_read("lstm_step_bwd")
+        _lib.timing_enable([])
+        print(f"H={H} persist={persist}: BPTT {r['ms']:.3f} ms over {r['launches']} launches "
+              f"({1e3 * r['ms'] / T:.1f} us per step)", flush=True)
+_lib.call("avc_bptt_persist", 1)

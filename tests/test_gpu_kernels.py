@@ -2,6 +2,8 @@
 
 fp32 tolerances: products are exact-fp32 MFMA with a different summation order than the CPU, so
 errors are a few ulp of the accumulated magnitudes (|err| <= 1e-5 * scale unless stated)."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -408,12 +410,15 @@ def test_linear_backward_split_path(cuda_device):
     assert rel(xg.grad, xr.grad) < 2e-6 and rel(wgt.grad, wr.grad) < 2e-6
 
 
-@pytest.mark.parametrize("B,T,din,H,scale", [(64, 12, 512, 1024, 1.0), (48, 9, 320, 512, 1e-9), (256, 4, 512, 1024, 1e5)])
+@pytest.mark.parametrize("B,T,din,H,scale", [(64, 12, 512, 1024, 1.0), (48, 9, 320, 512, 1e-9),
+                                             (256, 4, 512, 1024, 1e5), (256, 16, 320, 512, 1.0),
+                                             (128, 10, 512, 1024, 1e-9), (256, 33, 1024, 1024, 1.0)])
 def test_bptt_split_products_match_fp64(cuda_device, B, T, din, H, scale):
-    """The BPTT recurrence as split-K 3xf16 products with per-row power-of-two scales of dG
-    (avc_bptt_mode(2): wherever eligible; the default uses it for H = 1024) and the fp32 step
-    kernel (mode 0) against fp64 autograd; gradient magnitudes from 1e-9 to 1e5 (the scales
-    follow each row's max |dG|)."""
+    """The BPTT recurrence three ways against fp64 autograd: the persistent launch
+    (lstm_persist.hip: bptt_persist_kernel, B = 128 / 256), the split-K 3xf16 products with
+    per-row power-of-two scales of dG (avc_bptt_mode(2), persistent form off) and the fp32 step
+    kernel (mode 0); gradient magnitudes from 1e-9 to 1e5 (the scales follow each row's max
+    |dG|, per K-slice in the persistent form)."""
     g = torch.Generator().manual_seed(B * 7 + H)
     x = torch.randn(B, T, din, generator=g) * 0.5
     k = 1.0 / np.sqrt(H)
@@ -426,20 +431,26 @@ def test_bptt_split_products_match_fp64(cuda_device, B, T, din, H, scale):
     yr.backward(dy.double())
     rel = lambda a, r: (a - r).abs().max().item() / r.abs().max().item()
     grads = {}
+    forms = {"persistent": (2, 1), "split-K": (2, 0), "step": (0, 0)}
     try:
-        for mode in (2, 0):
+        for name, (mode, persist) in forms.items():
             _lib.call("avc_bptt_mode", mode)
+            _lib.call("avc_bptt_persist", persist)
             xg = _t(x.transpose(0, 1).reshape(T * B, din), cuda_device).requires_grad_(True)
             wg = [_t(w, cuda_device).requires_grad_(True) for w in ws]
             yg = ops.LSTMLayer.apply(xg, *wg, T, B, True)
             yg.backward(_t(dy.transpose(0, 1).reshape(T * B, H), cuda_device))
             torch.cuda.synchronize()
-            grads[mode] = [xg.grad.cpu().reshape(T, B, din).transpose(0, 1).double()] + \
+            grads[name] = [xg.grad.cpu().reshape(T, B, din).transpose(0, 1).double()] + \
                           [w.grad.cpu().double() for w in wg]
     finally:
         _lib.call("avc_bptt_mode", 1)
+        _lib.call("avc_bptt_persist", 1)
+    giveups = ctypes.c_long(0)
+    _lib.call("avc_lstm_persist_status", ctypes.byref(giveups))
+    assert giveups.value == 0
     refs = [xr.grad] + [w.grad for w in flat]
-    for mode in (2, 0):
-        errs = [rel(a, r) for a, r in zip(grads[mode], refs)]
-        print(f"bptt mode {mode} B={B} H={H} scale={scale:g}: max rel err vs fp64 {max(errs):.2e}")
+    for name in forms:
+        errs = [rel(a, r) for a, r in zip(grads[name], refs)]
+        print(f"bptt {name} B={B} T={T} H={H} scale={scale:g}: max rel err vs fp64 {max(errs):.2e}")
         assert max(errs) < 5e-5
