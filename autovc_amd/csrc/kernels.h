@@ -80,7 +80,7 @@ bool bptt_persist_eligible(int T, int B, int H);
 size_t bptt_persist_scratch(int B, int H);
 int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _Float16* whhT_s,
                      const unsigned* amax_w, const float* d_y, long ldy, const float* gates, const float* c,
-                     float* dg, hipStream_t s);
+                     float* dg, float* colpart, unsigned* amax_dg, hipStream_t s);
 // rows of a [4H][D] gate matrix into the permuted gate order p = blk*16 + gate*4 + u (lstm.hip)
 int permute_rows(const float* src, float* dst, int H, int D, hipStream_t s);
 

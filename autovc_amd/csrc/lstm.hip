@@ -1129,6 +1129,13 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   const bool persist_bptt = !small && g_bptt_mode != 0 && saved_gates && saved_c && bptt_persist_eligible(T, B, H);
   const bool gemm_bptt = persist_bptt || (!small && B >= 32 && (H == 512 || H == 1024) &&
                                           (g_bptt_mode == 2 || (g_bptt_mode == 1 && H == 1024)));
+  // the persistent BPTT also produces max |dG| and the bias gradients' column partials
+  AVC_TAKE(amax_dg, unsigned, 64, sc);  // one max|dG| shared by the three products below
+  float* colpart = nullptr;
+  if (persist_bptt) {
+    AVC_TAKE(cp, float, (size_t)(B / 32) * 4 * H, sc);
+    colpart = cp;
+  }
   if (small) {
     lstm32_bwd_kernel<8><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
     AVC_LAUNCH_CHECK();
@@ -1161,7 +1168,8 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TRY(zero_async(dgs, gemm_afrag_bytes(arows, 4 * H), s));  // padding rows stay zero
     AVC_LAUNCH_CHECK();
     if (persist_bptt)
-      AVC_TRY(bptt_persist_run(ctx, T, B, H, reverse, whhT_s, amax_w, d_y, ldy, saved_gates, saved_c, dg, s));
+      AVC_TRY(bptt_persist_run(ctx, T, B, H, reverse, whhT_s, amax_w, d_y, ldy, saved_gates, saved_c, dg, colpart,
+                               amax_dg, s));
     for (int st = persist_bptt ? -1 : T - 1; st >= 0; --st) {
       const int t = reverse ? T - 1 - st : st;
       const int tp = reverse ? t + 1 : t - 1;
@@ -1238,8 +1246,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   }
 
   // weight gradients: dW_ih = dG^T x ; dW_hh = dG^T h_prev (h_prev = y shifted one step)
-  AVC_TAKE(amax_dg, unsigned, 64, sc);  // one max|dG| scan shared by the three products
-  AVC_TRY(gemm_absmax(dg, TB, 4L * H, 4L * H, amax_dg, s));
+  if (!persist_bptt) AVC_TRY(gemm_absmax(dg, TB, 4L * H, 4L * H, amax_dg, s));
   GemmDesc g1;
   g1.M = 4 * H; g1.N = din; g1.Kc = (int)TB;
   g1.A = dg; g1.a_trans = 1; g1.lda = 4 * H;
@@ -1257,7 +1264,8 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, d_b_ih, accumulate_dw, s, d_b_hh));  // d_b_ih = d_b_hh
   } else {
     AVC_TAKE(db_p, float, (size_t)4 * H, sc);
-    AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, db_p, 0, s));
+    if (persist_bptt) AVC_TRY(colsum(ctx, B / 32, 4 * H, colpart, 4 * H, db_p, 0, s));  // 32-row block partials
+    else AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, db_p, 0, s));
     unpermute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(dwih_dst, d_w_ih, H, din, accumulate_dw);
     unpermute_rows_kernel<<<ew_blocks(4L * H * H), 256, 0, s>>>(dwhh_dst, d_w_hh, H, H, accumulate_dw);
     unpermute_vec2_kernel<<<(4 * H + 255) / 256, 256, 0, s>>>(db_p, d_b_ih, d_b_hh, H, accumulate_dw);

@@ -921,6 +921,8 @@ struct BpttPArgs {
   int nwg;
   unsigned spin_limit;
   int diag;                 // timing experiments (avc_debug_bptt_diag), 0 in production
+  float* colpart;           // [B/32][4H] per-row-block column sums of dG over all steps (bias grads)
+  unsigned* amax_dg;        // max |dG| over all steps (float bits; zeroed before the launch)
 };
 
 // NCH: 16-deep chunks per K-slice (4H / nsplit / 16); U = H / nsplit hidden units per phase-B
@@ -975,6 +977,18 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   const int j0 = q * U + bg * 4;           // first hidden unit of the task
   const int kq = q * KS + bg * 16;         // first (permuted) gate column of the task
 
+  // this task's column sums of dG over all steps (registers, or LDS where the W slice leaves room:
+  // the narrower-slice instances are at the VGPR limit) and its max |dG|
+  constexpr bool CS_LDS = NCH < 16;
+  float* csl = reinterpret_cast<float*>(flag + 4);  // [16][512] when CS_LDS
+  float csum[CS_LDS ? 1 : 16], dmax = 0.f;
+  if constexpr (CS_LDS) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) csl[e * 512 + tid] = 0.f;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) csum[e] = 0.f;
+  }
   int k = 0;
   bool ok = true;
   for (; k < T && ok; ++k) {
@@ -1084,7 +1098,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
         if (k > 0) {
           const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)(k & 1) * nsplit * B * H, 0,
                                                              nsplit * B * H * 4, 0x00020000);
-          constexpr int SB = NS < 16 ? NS : 16;  // partials in flight per batch (registers)
+          constexpr int SB = NS < 8 ? NS : 8;  // partials in flight per batch (registers)
 #pragma unroll
           for (int s0 = 0; s0 < NS; s0 += SB) {
             f32x4 pv[SB];
@@ -1113,7 +1127,12 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<f32x4*>(go + 4 * g) = f32x4{d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]};
 #pragma unroll
-        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, fabsf(d[e]));
+        for (int e = 0; e < 16; ++e) {
+          mx = fmaxf(mx, fabsf(d[e]));
+          if constexpr (CS_LDS) csl[e * 512 + tid] += d[e];
+          else csum[e] += d[e];
+        }
+        dmax = fmaxf(dmax, mx);
         atomicMax(rmax + br, __float_as_uint(mx));
       }
       __syncthreads();
@@ -1149,6 +1168,25 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
       }
     }
   }
+  // the bias gradients' column sums (32 rows of this block: lanes 0-31 / 32-63 of a wave are the
+  // rows of two unit groups) and max |dG| for the weight-gradient products' operand scale
+  if (ok && has_b) {
+    float cs[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      if constexpr (CS_LDS) cs[e] = csl[e * 512 + tid];
+      else cs[e] = csum[e];
+      for (int o = 16; o > 0; o >>= 1) cs[e] += __shfl_xor(cs[e], o);
+    }
+    if (b_task && br == 0) {
+      float* cp = a.colpart + (long)rb * G4 + kq;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(cp + 4 * g) = f32x4{cs[4 * g], cs[4 * g + 1], cs[4 * g + 2], cs[4 * g + 3]};
+    }
+    for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o));
+    if (lane == 0) atomicMax(a.amax_dg, __float_as_uint(dmax));
+  }
   // gave up at step k: this workgroup's dG slices of the remaining steps are NaN (never plausible)
   if (!ok && b_task) {
     for (int kk = k; kk < T; ++kk) {
@@ -1160,7 +1198,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   }
 }
 
-size_t bptt_lds(int nch) { return (size_t)4 * nch * 2048 + 32 * 4 + 16; }
+size_t bptt_lds(int nch) { return (size_t)4 * nch * 2048 + 32 * 4 + 16 + (nch < 16 ? 16 * 512 * 4 : 0); }
 
 const void* bptt_fn(int nch, int ns) {
   if (nch == 16 && ns == 16) return (const void*)bptt_persist_kernel<16, 16>;
@@ -1434,10 +1472,11 @@ size_t bptt_persist_scratch(int B, int H) {
 
 // BPTT of one LSTM layer direction over all T steps as one launch (see bptt_persist_kernel).
 // whhT_s / amax_w: W_hh^T permuted and split (lstm.hip); d_y [T][B] rows (ldy), gates / c the
-// forward's saved activations, dg [T][B][4H] output.
+// forward's saved activations, dg [T][B][4H] output; colpart [B/32][4H] the column sums of dG per
+// 32-row block (the bias gradients' partials), *amax_dg = max |dG| (both over all steps).
 int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _Float16* whhT_s,
                      const unsigned* amax_w, const float* d_y, long ldy, const float* gates, const float* c,
-                     float* dg, hipStream_t s) {
+                     float* dg, float* colpart, unsigned* amax_dg, hipStream_t s) {
   int nrt, ntn, ns, nch;
   AVC_CHECK_ARG(bptt_persist_eligible(T, B, H) && bptt_plan(B, H, nrt, ntn, ns, nch),
                 "persistent BPTT: not eligible for this shape");
@@ -1455,6 +1494,8 @@ int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _
   a.B = B; a.H = H; a.T = T; a.reverse = reverse; a.nsplit = ns; a.nrt = nrt; a.ntn = ntn;
   a.whhT_s = whhT_s; a.amax_w = amax_w; a.slab = slab; a.rowscale = rowscale; a.dgs = dgs; a.dc = dc;
   a.dy = d_y; a.lddy = ldy; a.gates = gates; a.c = c; a.dg = dg;
+  a.colpart = colpart; a.amax_dg = amax_dg;
+  AVC_TRY(zero_async(amax_dg, sizeof(unsigned), s));
   a.tickets = reinterpret_cast<unsigned long long*>(region);
   a.tmo = region + 32;
   a.cnt = region + kRegionHeaderWords;
