@@ -131,7 +131,7 @@ size_t conv_bn_backward_scratch(int T, int B, int cin, int cout) {
   GemmDesc dg;
   dg.M = (int)TB; dg.N = cin; dg.Kc = cout; dg.ntaps = 5; dg.a_rows = TB;
   dg.prec16 = 1; dg.split_scale = 1;
-  return (TB * cout + 5UL * cin * cout) * sizeof(float) + bn_backward_scratch((int)TB, cout) +
+  return (TB * cout + 5UL * cin * cout) * sizeof(float) + 2 * bn_backward_scratch((int)TB, cout) +
          colsum_scratch((int)TB, cout) + std::max(gemm_scratch_bytes(w), gemm_scratch_bytes(dg)) + 2048;
 }
 
@@ -150,11 +150,14 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
   const int acc_x = accumulate == 1, acc_p = accumulate != 0;
   Scratch sc(ctx);
   AVC_TAKE(dy, float, (size_t)TB * cout, sc);
+  // the pass that writes dY also yields the conv bias gradient's column partials and max |dY|
+  // (one max shared by dgrad and wgrad)
+  AVC_TAKE(amax_dy, unsigned, 64, sc);
+  const int R = bn_backward_rows((int)TB, cout);
+  AVC_TAKE(bpart, float, (size_t)R * cout, sc);
   AVC_TRY(bn_backward(ctx, (int)TB, cout, d_out, y_pre, mean, invstd, gamma, beta, act, training,
-                      d_gamma, d_beta, acc_p, dy, s));
-  if (d_bias) AVC_TRY(colsum(ctx, (int)TB, cout, dy, cout, d_bias, acc_p, s));
-  AVC_TAKE(amax_dy, unsigned, 64, sc);  // one max|dY| scan shared by dgrad and wgrad
-  AVC_TRY(gemm_absmax(dy, TB, cout, cout, amax_dy, s));
+                      d_gamma, d_beta, acc_p, dy, s, d_bias ? bpart : nullptr, amax_dy));
+  if (d_bias) AVC_TRY(colsum_finish(R, cout, bpart, d_bias, acc_p, s));
   if (d_x) {
     AVC_TAKE(wd, float, 5UL * cin * cout, sc);
     conv_weight_dgrad_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wd, cin, cout);

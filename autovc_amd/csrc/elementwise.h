@@ -17,7 +17,11 @@ size_t bn_backward_scratch(int M, int C);
 int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* y,
                 const float* mean, const float* invstd, const float* gamma, const float* beta,
                 int act, int training, float* d_gamma, float* d_beta, int accumulate, float* dy,
-                hipStream_t s);
+                hipStream_t s, float* dy_colpart = nullptr, unsigned* dy_amax = nullptr);
+// with dy_colpart ([bn_backward_rows(M, C)][C]) / dy_amax: dy's column partial sums (finish with
+// colsum_finish) and max |dy| come out of the same pass that writes dy
+int bn_backward_rows(int M, int C);
+int colsum_finish(int R, int N, const float* part, float* out, int accumulate, hipStream_t s);
 int frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* emb, float* out,
                     hipStream_t s);
 int frames_from_mel_backward(int T, int B, int cm, int ce, const float* df, int ld, float* dx,

@@ -239,6 +239,7 @@ __global__ void bn_bwd_reduce_kernel(int M, int C, const float* __restrict__ dou
   const int m0 = blockIdx.y * rows_per, m1 = min(M, m0 + rows_per);
   const float mu = mean[c], is = invstd[c], g = gamma[c], bt = beta[c];
   float s1 = 0.f, s2 = 0.f;
+#pragma unroll 4
   for (int m = m0; m < m1; ++m) {
     const long i = (long)m * C + c;
     const float xh = (y[i] - mu) * is;
@@ -252,9 +253,11 @@ __global__ void bn_bwd_reduce_kernel(int M, int C, const float* __restrict__ dou
 
 __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const float* __restrict__ part,
                                                             float* __restrict__ sums, float* __restrict__ d_gamma,
-                                                            float* __restrict__ d_beta, int accumulate) {
+                                                            float* __restrict__ d_beta, int accumulate,
+                                                            unsigned* __restrict__ amax) {
   __shared__ double red[2][16][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  if (amax && blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;  // bn_bwd_apply_cols_kernel raises it
   const int c = blockIdx.x * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
   if (c < C)
@@ -295,6 +298,46 @@ __global__ void bn_bwd_apply_kernel(long M, int C, const float* __restrict__ dou
     if (training) v = g * is * (dA - sums[c] * inv_count - xh * sums[C + c] * inv_count);
     else v = g * is * dA;
     dy[i] = v;
+  }
+}
+
+// bn_bwd_apply_kernel by columns: thread = channel c walking a row range (per-channel constants in
+// registers, coalesced along channels), also producing the column partial sums of dy (the conv
+// bias gradient, part[blockIdx.y][c]) and max |dy| (the backward products' operand scale) so no
+// separate pass re-reads dy for them.
+__global__ __launch_bounds__(256) void bn_bwd_apply_cols_kernel(int M, int C, const float* __restrict__ dout,
+                                                                const float* __restrict__ y,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, int act,
+                                                                int training, const float* __restrict__ sums,
+                                                                float inv_count, int rows_per, float* __restrict__ dy,
+                                                                float* __restrict__ part, unsigned* __restrict__ amax) {
+  __shared__ float red[4];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  float cs = 0.f, mx = 0.f;
+  if (c < C) {
+    const int m0 = blockIdx.y * rows_per, m1 = min(M, m0 + rows_per);
+    const float is = invstd[c], g = gamma[c], mu = mean[c], bt = beta[c];
+    const float k1 = training ? sums[c] * inv_count : 0.f, k2 = training ? sums[C + c] * inv_count : 0.f;
+#pragma unroll 4
+    for (int m = m0; m < m1; ++m) {
+      const long i = (long)m * C + c;
+      const float xh = (y[i] - mu) * is;
+      const float dA = dout[i] * act_bwd(xh * g + bt, act);
+      const float v = training ? g * is * (dA - k1 - xh * k2) : g * is * dA;
+      dy[i] = v;
+      cs += v;
+      mx = fmaxf(mx, fabsf(v));
+    }
+    if (part) part[(long)blockIdx.y * C + c] = cs;
+  }
+  if (amax) {
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
   }
 }
 
@@ -606,7 +649,7 @@ size_t bn_backward_scratch(int M, int C) {
 int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* y,
                 const float* mean, const float* invstd, const float* gamma, const float* beta,
                 int act, int training, float* d_gamma, float* d_beta, int accumulate, float* dy,
-                hipStream_t s) {
+                hipStream_t s, float* dy_colpart, unsigned* dy_amax) {
   int R, rp;
   colsum_geometry(M, C, R, rp);
   Scratch sc(ctx);
@@ -614,10 +657,28 @@ int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* 
   AVC_TAKE(sums, float, (size_t)2 * C, sc);
   bn_bwd_reduce_kernel<<<dim3((C + 255) / 256, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
                                                                 beta, act, rp, part);
-  bn_bwd_final_kernel<<<(C + 63) / 64, 1024, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate);
-  bn_bwd_apply_kernel<<<ew_blocks((long)M * C), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
-                                                              beta, act, training, sums,
-                                                              1.f / (float)M, dy);
+  bn_bwd_final_kernel<<<(C + 63) / 64, 1024, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate, dy_amax);
+  if (dy_colpart || dy_amax) {
+    bn_bwd_apply_cols_kernel<<<dim3((C + 255) / 256, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta,
+                                                                      act, training, sums, 1.f / (float)M, rp, dy,
+                                                                      dy_colpart, dy_amax);
+  } else {
+    bn_bwd_apply_kernel<<<ew_blocks((long)M * C), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
+                                                                beta, act, training, sums,
+                                                                1.f / (float)M, dy);
+  }
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int bn_backward_rows(int M, int C) {
+  int R, rp;
+  colsum_geometry(M, C, R, rp);
+  return R;
+}
+
+int colsum_finish(int R, int N, const float* part, float* out, int accumulate, hipStream_t s) {
+  colsum_final_kernel<<<(N + 63) / 64, 1024, 0, s>>>(R, N, part, out, accumulate, nullptr);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
