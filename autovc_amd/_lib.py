@@ -66,6 +66,7 @@ _SIGS = {
     "avc_lstm_persist_inproj": [_I],
     "avc_lstm32_tune": [_I],
     "avc_bptt_persist": [_I],
+    "avc_debug_bptt_diag": [_I],
     "avc_debug_persist_inject": [_I],
     "avc_graph_mode": [_I],
     "avc_timing_reset": [],

@@ -78,6 +78,7 @@ int inproj_kpad(int din);
 // BPTT of one LSTM layer direction as one persistent launch (lstm_persist.hip)
 bool bptt_persist_eligible(int T, int B, int H);
 size_t bptt_persist_scratch(int B, int H);
+int bptt_colpart_rows(int B, int H);  // rows of bptt_persist_run's colpart
 int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _Float16* whhT_s,
                      const unsigned* amax_w, const float* d_y, long ldy, const float* gates, const float* c,
                      float* dg, float* colpart, unsigned* amax_dg, hipStream_t s);

@@ -1133,7 +1133,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   AVC_TAKE(amax_dg, unsigned, 64, sc);  // one max|dG| shared by the three products below
   float* colpart = nullptr;
   if (persist_bptt) {
-    AVC_TAKE(cp, float, (size_t)(B / 32) * 4 * H, sc);
+    AVC_TAKE(cp, float, (size_t)bptt_colpart_rows(B, H) * 4 * H, sc);
     colpart = cp;
   }
   if (small) {
@@ -1264,7 +1264,8 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, d_b_ih, accumulate_dw, s, d_b_hh));  // d_b_ih = d_b_hh
   } else {
     AVC_TAKE(db_p, float, (size_t)4 * H, sc);
-    if (persist_bptt) AVC_TRY(colsum(ctx, B / 32, 4 * H, colpart, 4 * H, db_p, 0, s));  // 32-row block partials
+    if (persist_bptt)  // the BPTT's per-row-block partials
+      AVC_TRY(colsum(ctx, bptt_colpart_rows(B, H), 4 * H, colpart, 4 * H, db_p, 0, s));
     else AVC_TRY(colsum(ctx, (int)TB, 4 * H, dg, 4 * H, db_p, 0, s));
     unpermute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(dwih_dst, d_w_ih, H, din, accumulate_dw);
     unpermute_rows_kernel<<<ew_blocks(4L * H * H), 256, 0, s>>>(dwhh_dst, d_w_hh, H, H, accumulate_dw);

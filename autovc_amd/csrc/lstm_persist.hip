@@ -921,7 +921,7 @@ struct BpttPArgs {
   int nwg;
   unsigned spin_limit;
   int diag;                 // timing experiments (avc_debug_bptt_diag), 0 in production
-  float* colpart;           // [B/32][4H] per-row-block column sums of dG over all steps (bias grads)
+  float* colpart;           // [B/RB][4H] per-row-block column sums of dG over all steps (bias grads)
   unsigned* amax_dg;        // max |dG| over all steps (float bits; zeroed before the launch)
 };
 
@@ -930,7 +930,7 @@ struct BpttPArgs {
 // a buffer written at step k is rewritten at step k + 2 only, and the counter chain in between
 // (B(k+1) waits on every K-slice of a tile, A(k+2) on B(k+1)) orders every reader of step k
 // before that.
-template <int NCH, int NS>
+template <int NCH, int NS, int RB>  // RB: batch rows per phase-B workgroup (16 or 32)
 __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   constexpr int U = 4 * NCH;
   constexpr int KS = 16 * NCH;               // gate columns per K-slice
@@ -948,9 +948,10 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   const int sp = wg % nsplit, tile = wg / nsplit, rt = tile / a.ntn, ct = tile % a.ntn;
   const int wm = w >> 1, wn = w & 1;         // 4 x 2 waves over the 128 x 128 tile (32 x 64 each)
   // phase B role (workgroups beyond the (row block, K-slice) pairs have none)
-  const int nrb = B / 32;
+  const int nrb = B / RB;
   const bool has_b = wg < nrb * nsplit;
   const int rb = wg / nsplit, q = wg % nsplit;
+  const int brt = rb * RB / 128;  // the 128-row tile of this workgroup's rows
   unsigned* cntA = a.cnt;
   unsigned* cntB = a.cnt + (long)T * a.nrt * a.ntn * 32;
   auto ia = [&](int k, int r, int c) { return (((long)k * a.nrt + r) * a.ntn + c) * 32; };
@@ -970,10 +971,11 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   __syncthreads();
   const unsigned E = (unsigned)flag[2];
   const float sw_inv = 1.f / pow2_scale(__uint_as_float(*a.amax_w));
-  // phase B thread task: row r (of 32), unit group g4 (4 units = one 16-deep k chunk of the slice)
-  const int br = tid & 31, bg = tid >> 5;   // 32 rows x 16 groups per pass (U / 4 groups)
+  // phase B thread task: row r (of RB), unit group g4 (4 units = one 16-deep k chunk of the slice)
+  const int br = tid & (RB - 1), bg = tid / RB;
   const bool b_task = has_b && bg < U / 4;
-  const int b_row = rb * 32 + br;
+  const int b_row = rb * RB + br;
+  const int fr = b_row & 31;      // the row's lane in its 32-row fragment block
   const int j0 = q * U + bg * 4;           // first hidden unit of the task
   const int kq = q * KS + bg * 16;         // first (permuted) gate column of the task
 
@@ -997,7 +999,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
     const int tp = a.reverse ? t + 1 : t - 1;
     // ---------------- phase A: slab[sp] = (dG_{t+1} . W_hh)[tile, K-slice sp] ----------------
     if (k > 0) {
-      if (tid == 0) flag[0] = (a.diag & 4) ? 1 : wait_ge_ctl(cntB + ib(k - 1, rt, sp), E * 4u, a.tmo, a.fail_host, a.spin_limit, E);
+      if (tid == 0) flag[0] = (a.diag & 4) ? 1 : wait_ge_ctl(cntB + ib(k - 1, rt, sp), E * (unsigned)(128 / RB), a.tmo, a.fail_host, a.spin_limit, E);
       __syncthreads();
       if (!flag[0]) { ok = false; break; }
       const int rblk = rt * 4 + wm;  // this wave's 32-row block
@@ -1082,7 +1084,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
       }
       if (k > 0) {
         if (tid == 0)
-          flag[1] = (a.diag & 4) ? 1 : wait_ge_ctl(cntA + ia(k, rb / 4, (q * U) / 128), E * (unsigned)nsplit, a.tmo, a.fail_host,
+          flag[1] = (a.diag & 4) ? 1 : wait_ge_ctl(cntA + ia(k, brt, (q * U) / 128), E * (unsigned)nsplit, a.tmo, a.fail_host,
                                 a.spin_limit, E);
         if (tid < 32) rmax[tid] = 0u;
         __syncthreads();
@@ -1149,22 +1151,22 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
             hi0[e] = h0; lo0[e] = (_Float16)((v0 - (float)h0) * 2048.0f);
             hi1[e] = h1; lo1[e] = (_Float16)((v1 - (float)h1) * 2048.0f);
           }
-          const auto drs = __builtin_amdgcn_make_buffer_rsrc(a.dgs + (k & 1) * dgs_buf + ((long)rb * nkc + kq / 16) * 1024,
-                                                             0, 2048, 0x00020000);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi0), drs, br * 16, 0, 16);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi1), drs, (br + 32) * 16, 0, 16);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo0), drs, 1024 + br * 16, 0, 16);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo1), drs, 1024 + (br + 32) * 16, 0, 16);
+          const auto drs = __builtin_amdgcn_make_buffer_rsrc(
+              a.dgs + (k & 1) * dgs_buf + ((long)(b_row >> 5) * nkc + kq / 16) * 1024, 0, 2048, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi0), drs, fr * 16, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi1), drs, (fr + 32) * 16, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo0), drs, 1024 + fr * 16, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo1), drs, 1024 + (fr + 32) * 16, 0, 16);
           if (bg == 0) {
-            const auto rrs = __builtin_amdgcn_make_buffer_rsrc(a.rowscale + ((long)(k & 1) * nsplit + q) * B + rb * 32, 0,
-                                                               128, 0x00020000);
+            const auto rrs = __builtin_amdgcn_make_buffer_rsrc(a.rowscale + ((long)(k & 1) * nsplit + q) * B + rb * RB, 0,
+                                                               RB * 4, 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, sb), rrs, br * 4, 0, 16);
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0)
-          __hip_atomic_fetch_add((gu32*)(cntB + ib(k, rb / 4, q)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add((gu32*)(cntB + ib(k, brt, q)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -1176,7 +1178,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
     for (int e = 0; e < 16; ++e) {
       if constexpr (CS_LDS) cs[e] = csl[e * 512 + tid];
       else cs[e] = csum[e];
-      for (int o = 16; o > 0; o >>= 1) cs[e] += __shfl_xor(cs[e], o);
+      for (int o = RB / 2; o > 0; o >>= 1) cs[e] += __shfl_xor(cs[e], o);
     }
     if (b_task && br == 0) {
       float* cp = a.colpart + (long)rb * G4 + kq;
@@ -1200,10 +1202,14 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
 
 size_t bptt_lds(int nch) { return (size_t)4 * nch * 2048 + 32 * 4 + 16 + (nch < 16 ? 16 * 512 * 4 : 0); }
 
+// epilogue rows per workgroup: 16 where 32-row blocks would leave half the workgroups without an
+// epilogue (nsplit = 16), else 32
+int bptt_rb(int ns) { return ns == 16 ? 16 : 32; }
+
 const void* bptt_fn(int nch, int ns) {
-  if (nch == 16 && ns == 16) return (const void*)bptt_persist_kernel<16, 16>;
-  if (nch == 8 && ns == 32) return (const void*)bptt_persist_kernel<8, 32>;
-  if (nch == 4 && ns == 32) return (const void*)bptt_persist_kernel<4, 32>;
+  if (nch == 16 && ns == 16) return (const void*)bptt_persist_kernel<16, 16, 16>;
+  if (nch == 8 && ns == 32) return (const void*)bptt_persist_kernel<8, 32, 32>;
+  if (nch == 4 && ns == 32) return (const void*)bptt_persist_kernel<4, 32, 32>;
   return nullptr;
 }
 
@@ -1463,6 +1469,11 @@ bool bptt_persist_eligible(int T, int B, int H) {
   return cap >= 256;  // every workgroup co-resident
 }
 
+int bptt_colpart_rows(int B, int H) {
+  int nrt, ntn, ns, nch;
+  return bptt_plan(B, H, nrt, ntn, ns, nch) ? B / bptt_rb(ns) : 0;
+}
+
 size_t bptt_persist_scratch(int B, int H) {
   int nrt, ntn, ns, nch;
   if (!bptt_plan(B, H, nrt, ntn, ns, nch)) return 0;
@@ -1472,8 +1483,9 @@ size_t bptt_persist_scratch(int B, int H) {
 
 // BPTT of one LSTM layer direction over all T steps as one launch (see bptt_persist_kernel).
 // whhT_s / amax_w: W_hh^T permuted and split (lstm.hip); d_y [T][B] rows (ldy), gates / c the
-// forward's saved activations, dg [T][B][4H] output; colpart [B/32][4H] the column sums of dG per
-// 32-row block (the bias gradients' partials), *amax_dg = max |dG| (both over all steps).
+// forward's saved activations, dg [T][B][4H] output; colpart [bptt_colpart_rows(B, H)][4H] the
+// column sums of dG per epilogue row block (the bias gradients' partials), *amax_dg = max |dG|
+// (both over all steps).
 int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _Float16* whhT_s,
                      const unsigned* amax_w, const float* d_y, long ldy, const float* gates, const float* c,
                      float* dg, float* colpart, unsigned* amax_dg, hipStream_t s) {

@@ -1,7 +1,6 @@
 """Timing experiments on the persistent BPTT (avc_debug_bptt_diag; results are not valid while a
 bit is set): 1 = no dG operand loads in the product phase, 2 = no partial loads in the epilogue
 phase, 4 = no waits between the phases."""
-import ctypes
 import sys
 
 import torch
@@ -9,8 +8,6 @@ import torch
 sys.path.insert(0, __file__.rsplit("/", 2)[0])
 from autovc_amd import _lib, ops  # noqa: E402
 
-lib = _lib.load()
-lib.avc_debug_bptt_diag.argtypes = [ctypes.c_int]
 dev = torch.device("cuda:0")
 B, T = 256, 128
 for H, din in ((1024, 1024), (512, 320)):
@@ -21,7 +18,7 @@ for H, din in ((1024, 1024), (512, 320)):
     x = (torch.randn(T * B, din, generator=g) * 0.5).to(dev).requires_grad_(True)
     dy = torch.randn(T * B, H, generator=g).to(dev)
     for bits in (0, 1, 2, 4, 3, 7):
-        lib.avc_debug_bptt_diag(bits)
+        _lib.call("avc_debug_bptt_diag", bits)
         for rep in range(3):
             y = ops.LSTMLayer.apply(x, *ws, T, B, True)
             torch.cuda.synchronize()
@@ -36,4 +33,4 @@ for H, din in ((1024, 1024), (512, 320)):
         r = _lib.timing_read("lstm_step_bwd")
         _lib.timing_enable([])
         print(f"H={H} diag={bits}: {1e3 * r['ms'] / T:.1f} us per step", flush=True)
-lib.avc_debug_bptt_diag(0)
+_lib.call("avc_debug_bptt_diag", 0)
