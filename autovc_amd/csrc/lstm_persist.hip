@@ -984,9 +984,9 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   constexpr bool CS_LDS = NCH < 16;
   float* csl = reinterpret_cast<float*>(flag + 4);  // [16][512] when CS_LDS
   float csum[CS_LDS ? 1 : 16], dmax = 0.f;
-  if constexpr (CS_LDS) {
+  if constexpr (CS_LDS) {  // [512 threads][16] as 4 x 16-B vectors per thread
 #pragma unroll
-    for (int e = 0; e < 16; ++e) csl[e * 512 + tid] = 0.f;
+    for (int g = 0; g < 4; ++g) reinterpret_cast<f32x4*>(csl)[tid * 4 + g] = f32x4{0.f, 0.f, 0.f, 0.f};
   } else {
 #pragma unroll
     for (int e = 0; e < 16; ++e) csum[e] = 0.f;
@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
         if (k > 0) {
           const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)(k & 1) * nsplit * B * H, 0,
                                                              nsplit * B * H * 4, 0x00020000);
-          constexpr int SB = NS < 8 ? NS : 8;  // partials in flight per batch (registers)
+          constexpr int SB = NS < 16 ? NS : 16;  // partials in flight per batch (registers)
 #pragma unroll
           for (int s0 = 0; s0 < NS; s0 += SB) {
             f32x4 pv[SB];
@@ -1131,8 +1131,14 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           mx = fmaxf(mx, fabsf(d[e]));
-          if constexpr (CS_LDS) csl[e * 512 + tid] += d[e];
-          else csum[e] += d[e];
+          if constexpr (!CS_LDS) csum[e] += d[e];
+        }
+        if constexpr (CS_LDS) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            f32x4* p4 = reinterpret_cast<f32x4*>(csl) + tid * 4 + g;
+            *p4 += f32x4{d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]};
+          }
         }
         dmax = fmaxf(dmax, mx);
         atomicMax(rmax + br, __float_as_uint(mx));
@@ -1176,7 +1182,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
     float cs[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      if constexpr (CS_LDS) cs[e] = csl[e * 512 + tid];
+      if constexpr (CS_LDS) cs[e] = csl[tid * 16 + e];
       else cs[e] = csum[e];
       for (int o = RB / 2; o > 0; o >>= 1) cs[e] += __shfl_xor(cs[e], o);
     }
