@@ -134,3 +134,34 @@ def test_alternating_launch_layouts(cuda_device):
                 y = ops.LSTMLayer.apply(x, *w, T, B, save)
                 assert float((y - ref).abs().max()) <= 1e-6
     assert _giveups() == before
+
+
+def test_persistent_bptt_timeout_is_nan_and_next_call_raises(cuda_device):
+    """The persistent BPTT (bptt_persist_kernel, B = 128) under the same safety net: an injected
+    give-up leaves NaN gradients (never plausible numbers), and the next persistent launch on the
+    context raises after resetting the counter state; then the layer runs normally again."""
+    from autovc_amd import ops
+    B, T, H, din = 128, 8, 1024, 512
+    g = torch.Generator().manual_seed(9)
+    k = 1.0 / H ** 0.5
+    ws = [((torch.rand(*s, generator=g) * 2 - 1) * k).to(cuda_device).requires_grad_(True)
+          for s in [(4 * H, din), (4 * H, H), (4 * H,), (4 * H,)]]
+    x = (torch.randn(T * B, din, generator=g) * 0.5).to(cuda_device).requires_grad_(True)
+    dy = torch.randn(T * B, H, generator=g).to(cuda_device)
+    y = ops.LSTMLayer.apply(x, *ws, T, B, True)
+    torch.cuda.synchronize()
+    before = _giveups()
+    _lib.call("avc_debug_persist_inject", 1)  # the next persistent launch: the BPTT
+    y.backward(dy)
+    torch.cuda.synchronize()
+    assert _giveups() > before, "the injected BPTT launch did not give up"
+    assert torch.isnan(ws[1].grad).any() and torch.isnan(x.grad).any()
+    with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+        ops.LSTMLayer.apply(x, *ws, T, B, True)
+    for w in ws:
+        w.grad = None
+    x.grad = None
+    y = ops.LSTMLayer.apply(x, *ws, T, B, True)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(w.grad).all() for w in ws) and torch.isfinite(x.grad).all()
