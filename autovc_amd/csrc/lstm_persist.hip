@@ -620,18 +620,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         fu wiv[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) wiv[g] = *reinterpret_cast<const fu*>(cpar + blk * 16 + 4 * g + u0);
-        const fu zi = sum[0] * wiv[0] + gxv[0];
-        const fu zf = sum[1] * wiv[1] + gxv[1];
-        const fu zg = sum[2] * wiv[2] + gxv[2];
-        const fu zo = sum[3] * wiv[3] + gxv[3];
 #pragma unroll
-        for (int u = 0; u < UPT; ++u) {
-          ig[u] = sigmoidf_(zi[u]);
-          fg[u] = sigmoidf_(zf[u]);
-          gg[u] = tanhf(zg[u]);
-          og[u] = sigmoidf_(zo[u]);
-          cst[u] = fg[u] * cst[u] + ig[u] * gg[u];
-          hv[u] = og[u] * tanhf(cst[u]);
+        for (int u = 0; u < UPT; ++u) {  // explicit fmas: the launch-per-step kernel forms the same values
+          ig[u] = gate_sigmoid(fmaf(sum[0][u], wiv[0][u], gxv[0][u]));
+          fg[u] = gate_sigmoid(fmaf(sum[1][u], wiv[1][u], gxv[1][u]));
+          gg[u] = gate_tanh(fmaf(sum[2][u], wiv[2][u], gxv[2][u]));
+          og[u] = gate_sigmoid(fmaf(sum[3][u], wiv[3][u], gxv[3][u]));
+          cst[u] = fmaf(fg[u], cst[u], ig[u] * gg[u]);
+          hv[u] = og[u] * gate_tanh(cst[u]);
           const float v = hv[u] * kHScale;
           const _Float16 hi = (_Float16)v;
           const _Float16 lo = (_Float16)(v - (float)hi);
@@ -1115,7 +1111,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float dh = dyv[u] + rec[u];
-          const float tc = tanhf(cc[u]);
+          const float tc = gate_tanh(cc[u]);  // as the forward epilogue formed it
           const float dct = dh * og[u] * (1.f - tc * tc) + dcv[u];
           dcv[u] = dct * fg[u];
           d[u] = dct * gg[u] * ig[u] * (1.f - ig[u]);

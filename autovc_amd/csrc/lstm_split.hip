@@ -306,13 +306,13 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
       float v = part[row * RP + 4 * g + u];
 #pragma unroll
       for (int ww = 1; ww < NW; ++ww) v += part[ww * MB * RP + row * RP + 4 * g + u];
-      z[g] = v * wis[g] + gxs[g];
+      z[g] = fmaf(v, wis[g], gxs[g]);  // explicit fmas: the persistent kernel forms the same values
     }
     AVC_STAMP(5);
     if (live && b < B) {
-      const float ig = sigmoidf_(z[0]), fg = sigmoidf_(z[1]), gg = tanhf(z[2]), og = sigmoidf_(z[3]);
-      const float cn = fg * cp + ig * gg;
-      const float hv = og * tanhf(cn);
+      const float ig = gate_sigmoid(z[0]), fg = gate_sigmoid(z[1]), gg = gate_tanh(z[2]), og = gate_sigmoid(z[3]);
+      const float cn = fmaf(fg, cp, ig * gg);
+      const float hv = og * gate_tanh(cn);
       S.c_out[(long)b * H + j] = cn;
       S.h_out[(long)b * S.ldh + j] = hv;
       if (S.hs_out) {
@@ -435,21 +435,18 @@ __global__ __launch_bounds__(NW * 64, 2) void lstm_split_step_kernel(SplitArgs a
     const int b = rb * MB + row;
     if (pr >= NPAIR || b >= B) continue;
     const int j0 = cb * 4 * NC + blk * 4;
-    const f32x4 zi = sum[i][0] * wiv[i][0] + gxv[i][0];
-    const f32x4 zf = sum[i][1] * wiv[i][1] + gxv[i][1];
-    const f32x4 zg = sum[i][2] * wiv[i][2] + gxv[i][2];
-    const f32x4 zo = sum[i][3] * wiv[i][3] + gxv[i][3];
     f32x4 cn, hv, ig, fg, gg, og;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      // library tanhf/expf on purpose: hardware exp/rcp forms (~1e-7 absolute) doubled the
-      // end-to-end mel error — the train-mode postnet amplifies it past the 1e-4 bar
-      ig[u] = sigmoidf_(zi[u]);
-      fg[u] = sigmoidf_(zf[u]);
-      gg[u] = tanhf(zg[u]);
-      og[u] = sigmoidf_(zo[u]);
-      cn[u] = fg[u] * cpv[i][u] + ig[u] * gg[u];
-      hv[u] = og[u] * tanhf(cn[u]);
+      // hardware exp/rcp gate math with a polynomial tanh near 0 (common.h: gate_tanh): the plain
+      // 1 - 2 / (e^2x + 1) form lost ~1e-7 absolute there, which the train-mode postnet amplified
+      // past the 1e-4 mel bar.  Explicit fmas so the persistent kernel forms identical values.
+      ig[u] = gate_sigmoid(fmaf(sum[i][0][u], wiv[i][0][u], gxv[i][0][u]));
+      fg[u] = gate_sigmoid(fmaf(sum[i][1][u], wiv[i][1][u], gxv[i][1][u]));
+      gg[u] = gate_tanh(fmaf(sum[i][2][u], wiv[i][2][u], gxv[i][2][u]));
+      og[u] = gate_sigmoid(fmaf(sum[i][3][u], wiv[i][3][u], gxv[i][3][u]));
+      cn[u] = fmaf(fg[u], cpv[i][u], ig[u] * gg[u]);
+      hv[u] = og[u] * gate_tanh(cn[u]);
     }
     *reinterpret_cast<f32x4*>(S.c_out + (long)b * H + j0) = cn;
     *reinterpret_cast<f32x4*>(S.h_out + (long)b * S.ldh + j0) = hv;

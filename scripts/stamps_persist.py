@@ -9,7 +9,7 @@ import os
 import sys
 
 REPO = __file__.rsplit("/", 2)[0]
-os.environ["AUTOVC_HIP_LIB"] = os.path.join(REPO, "diag", "libautovc_hip_stamps.so")
+os.environ["AUTOVC_HIP_LIB"] = os.environ.get("AVC_STAMPS_LIB", os.path.join(REPO, "diag", "libautovc_hip_stamps.so"))
 sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
