@@ -89,6 +89,17 @@ struct avc_gen_graph {
   hipGraphExec_t exec = nullptr;
   float* stage = nullptr;       // x | c_org | c_trg | mel | mel_post | codes
   size_t stage_bytes = 0;
+  // graphs captured on the caller's own I/O pointers (no staging copies), for pointer sets that
+  // recur (a serving loop alternates a few output buffers); least recently used dropped first
+  struct direct_graph {
+    const void* io[6];
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    unsigned long last = 0;
+  };
+  std::vector<direct_graph> direct;
+  std::vector<std::vector<const void*>> recent;  // pointer sets seen once (candidates)
+  unsigned long clock = 0;
 };
 
 // Counter region of a persistent recurrence (lstm_persist.hip): arrival counters that are never

@@ -368,6 +368,40 @@ def test_back_to_back_forwards_match(cuda_device):
             assert torch.equal(a, b), f"call {i} {name}: max|d| {(a - b).abs().max().item():.3e}"
 
 
+def test_direct_graphs_on_rotating_buffers(cuda_device):
+    """avc_generator_forward_cached keeps up to 4 graphs captured on the caller's own I/O pointers
+    (a pointer set seen twice gets one; the least recently used is dropped).  Six output buffer
+    sets and two inputs rotated over 30 back-to-back calls (captures, replays and evictions
+    interleaved, no host sync): every output bit-identical to the eager result of its input."""
+    from autovc_amd import _lib
+    from autovc_amd.weights import synthetic_embedding, synthetic_mel
+    ae = make_model(cuda_device, False)  # eval: the running statistics stay fixed across calls
+    B, T = 16, 64
+    xs = [_t(synthetic_mel(s, B, T), cuda_device) for s in (71, 72)]
+    co, ct = _t(synthetic_embedding(73, B), cuda_device), _t(synthetic_embedding(74, B), cuda_device)
+    with torch.no_grad():
+        _lib.call("avc_graph_mode", 0)
+        try:
+            refs = [[o.clone() for o in ae(x, co, ct)] for x in xs]
+        finally:
+            _lib.call("avc_graph_mode", 1)
+        params, version = ae._gen_params()
+        sets = [[torch.full_like(r, float("nan")) for r in refs[0]] for _ in range(6)]
+        order = [0, 1, 0, 1, 2, 3, 2, 3, 4, 5, 4, 5, 0, 1, 2, 3, 4, 5, 5, 4, 3, 2, 1, 0, 0, 2, 4, 1, 3, 5]
+        keep = []
+        for i, k in enumerate(order):
+            x = xs[(i + k) % 2]
+            mel, post, codes = sets[k]
+            _lib.call("avc_generator_forward_cached", _lib.context(x.device), T, B, params, version,
+                      _lib.ptr(x), _lib.ptr(co), _lib.ptr(ct), 0, _lib.ptr(mel), _lib.ptr(post),
+                      _lib.ptr(codes), _lib.stream(x.device))
+            keep.append(((i + k) % 2, [o.clone() for o in sets[k]]))
+        torch.cuda.synchronize()
+    for i, (which, outs) in enumerate(keep):
+        for name, a, b in zip(("mel", "mel_post", "codes"), outs, refs[which]):
+            assert torch.equal(a, b), f"call {i} {name}: max|d| {(a - b).abs().max().item():.3e}"
+
+
 @pytest.mark.parametrize("mode", ["train", "eval"])
 def test_c1_real_mel_end_to_end(cuda_device, mode):
     """BASELINE config 1 on the GPU end to end: the GPU mel frontend on the committed head of
