@@ -38,6 +38,10 @@ struct GemmDesc {
   const _Float16* a_frag = nullptr;  // optional A already split (row-major A, unscaled forward
                                      // products only): gemm_afrag_bytes(a_rows, Kc) bytes in the
                                      // layout split_frag32_kernel writes (e.g. by bn_apply's frag)
+  _Float16* a_frag_out = nullptr;  // optional: gemm_run writes its split of A here (instead of
+                                   // scratch; a_trans: gemm_afrag_bytes(M, Kc) bytes) ...
+  int a_frag_scaled = 0;    // ... and a later product with the same A and amax_a passes it back as
+                            // a_frag with a_frag_scaled = 1 (gradient products sharing dY^T / dG^T)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
   int stats_bm = 0;         // filled by gemm_run: rows per stats partial
 };

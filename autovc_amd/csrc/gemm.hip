@@ -1386,8 +1386,10 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     const long b_krows = frag16_b_krows(d);
     const int b_nkc = frag_nkc((int)b_krows);
     const _Float16* as = d.a_frag;
-    if (!as || scaled_product || d.a_trans) {
-      _Float16* at = sc.take<_Float16>(frag_bytes(a_src_rows, d.Kc) / 2);
+    // an A split by an earlier product with the same scale (a_frag_out -> a_frag_scaled) is reused
+    const bool reuse_a = as && d.a_frag_scaled && scaled_product && d.amax_a;
+    if (!reuse_a && (!as || scaled_product || d.a_trans)) {
+      _Float16* at = d.a_frag_out ? d.a_frag_out : sc.take<_Float16>(frag_bytes(a_src_rows, d.Kc) / 2);
       if (!at) return AVC_ERR_WORKSPACE;
       const long ta = a_ntile * 32 * nkc * 2;
       split_frag32_kernel<<<(int)std::min<long>((ta + 255) / 256, 8192), 256, 0, stream>>>(

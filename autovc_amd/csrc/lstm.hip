@@ -1095,6 +1095,7 @@ size_t lstm_backward_scratch(int T, int B, int din, int H) {
   // split-K BPTT (bptt_row_kernel): split W_hh^T, split dG rows, <= 32 partial slabs, row scales
   s += gemm_afrag_bytes(H, 4 * H) + gemm_afrag_bytes(B + 31, 4 * H) + 32 * (size_t)B * H * f + (size_t)B * f + 2048;
   s += bptt_persist_scratch(B, H);  // the persistent BPTT's double-buffered slabs, split dG, dc
+  s += gemm_afrag_bytes(4L * H, (int)TB) + 256;  // dG^T split once for dW_ih and dW_hh
   GemmDesc d1;  // dW_ih
   d1.M = 4 * H; d1.N = din; d1.Kc = (int)TB; d1.a_trans = 1; d1.b_rows = TB;
   d1.prec16 = 1; d1.split_scale = 1;
@@ -1253,11 +1254,22 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   g1.B = x; g1.ldb = ldx; g1.b_rows = TB;
   g1.C = dwih_dst; g1.ldc = din; g1.accumulate = acc_w;
   g1.prec16 = 1; g1.split_scale = 1; g1.amax_a = amax_dg;
+  // dG^T is split once (the larger operand of both products: TB x 4H against TB x din / H)
+  const bool share = gemm_frag_eligible(g1);
+  if (share) {
+    AVC_TAKE(dgT_s, _Float16, gemm_afrag_bytes(4L * H, (int)TB) / 2, sc);
+    g1.a_frag_out = dgT_s;
+  }
   AVC_TRY(gemm_run(ctx, g1, s));
   GemmDesc g2 = g1;
   g2.N = H;
   g2.B = y; g2.ldb = ldy; g2.b_shift0 = reverse ? B : -B;
   g2.C = dwhh_dst; g2.ldc = H;
+  if (share && gemm_frag_eligible(g2)) {
+    g2.a_frag = g1.a_frag_out;
+    g2.a_frag_scaled = 1;
+  }
+  g2.a_frag_out = nullptr;
   AVC_TRY(gemm_run(ctx, g2, s));
 
   if (small) {
