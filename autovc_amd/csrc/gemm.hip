@@ -596,7 +596,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
 __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restrict__ src, long rs,
                                                            long ks, int R, int K, int ntile, int nkc,
                                                            _Float16* __restrict__ dst,
-                                                           const unsigned* __restrict__ amax = nullptr) {
+                                                           const unsigned* __restrict__ amax = nullptr,
+                                                           long src_tap = 0, long dst_tap = 0) {
+  // grid y enumerates the taps of a multi-tap operand (one launch for all of them)
+  src += blockIdx.y * src_tap;
+  dst += blockIdx.y * dst_tap;
   const int G8 = nkc * 2;  // 8-element groups per row (a multiple of 4)
   const float sc = split_scale_of(amax);
   const long total = (long)ntile * 32 * G8;
@@ -989,6 +993,51 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmDesc d, int nsp
   }
 }
 
+// The same reduction for few output rows (weight gradients of narrow layers: M = 4H = 128): one
+// row chunk per block (rpb rows x N/4 float4 = tasks <= 256/G), and G thread groups sum
+// interleaved K-splits, combined through LDS in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void splitk_reduce4g_kernel(GemmDesc d, int nsplit, const float* __restrict__ slab,
+                                                              int rows_per_block, int G) {
+  __shared__ float4 part[256];
+  const int n4 = d.N >> 2;
+  const long MN = (long)d.M * d.N;
+  const int tasks = rows_per_block * n4;
+  const int g = threadIdx.x / tasks;
+  const int i = threadIdx.x - g * tasks;
+  const int m = blockIdx.y * rows_per_block + i / n4, c4 = i - (i / n4) * n4;
+  const long off = (long)m * d.N + 4 * c4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g < G && m < d.M) {
+    for (int sp = g; sp < nsplit; sp += G) {
+      const float4 b = *reinterpret_cast<const float4*>(slab + sp * MN + off);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+  }
+  part[threadIdx.x] = a;
+  __syncthreads();
+  if (g != 0 || m >= d.M) return;
+  for (int gg = 1; gg < G; ++gg) {
+    const float4 b = part[gg * tasks + i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  const float us = d.split_scale ? split_unscale(d.amax_a, d.amax_b) : 1.f;
+  float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int n = 4 * c4 + e;
+    float t = v[e] * us;
+    if (d.bias0) t += d.bias0[n];
+    if (d.bias1) t += d.bias1[n];
+    v[e] = act_apply(t, d.act);
+  }
+  float* p = d.C + (long)m * d.ldc + 4 * c4;
+  if (d.accumulate) {
+    const float4 o = *reinterpret_cast<const float4*>(p);
+    v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+  }
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 __global__ void splitk_reduce_kernel(GemmDesc d, int nsplit, const float* __restrict__ slab) {
   const long total = (long)d.nz * d.M * d.N;
   const long MN = (long)d.M * d.N;
@@ -1161,13 +1210,22 @@ unsigned* bfrag_guard_word(const GemmDesc& d, const _Float16* bf) {
 }
 
 // max |B| over all taps of a forward product's B operand into a guard word
+// max |x| over the taps of a multi-tap operand (rows x cols each, row stride ld, taps tapoff
+// apart): one scan when the taps tile one dense block, else one per tap
+void absmax_taps(const float* src, int ntaps, long tapoff, long rows, long cols, long ld, unsigned* out,
+                 hipStream_t s) {
+  if (ntaps > 1 && ld == cols && tapoff == rows * cols) {
+    absmax2d(src, rows * ntaps, cols, ld, out, s);
+    return;
+  }
+  for (int tau = 0; tau < ntaps; ++tau) absmax2d(src + (long)tau * tapoff, rows, cols, ld, out, s);
+}
+
 void absmax_b(const GemmDesc& d, unsigned* w, hipStream_t s) {
   const long b_rows = d.b_rows ? d.b_rows : (d.b_trans ? d.N : d.Kc);
   const long kb = d.b_trans ? d.Kc : std::min<long>(d.Kc, b_rows);
-  for (int tau = 0; tau < d.ntaps; ++tau) {
-    if (d.b_trans) absmax2d(d.B + (long)tau * d.b_tapoff, d.N, kb, d.ldb, w, s);
-    else absmax2d(d.B + (long)tau * d.b_tapoff, kb, d.N, d.ldb, w, s);
-  }
+  if (d.b_trans) absmax_taps(d.B, d.ntaps, d.b_tapoff, d.N, kb, d.ldb, w, s);
+  else absmax_taps(d.B, d.ntaps, d.b_tapoff, kb, d.N, d.ldb, w, s);
 }
 }  // namespace
 
@@ -1230,10 +1288,9 @@ int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
   unsigned* guard = bfrag_guard_word(d, dst);
   guard_init_kernel<<<1, 64, 0, stream>>>(guard, 1);
   absmax_b(d, guard, stream);
-  for (int tau = 0; tau < d.ntaps; ++tau)
-    split_frag32_kernel<<<(int)std::min<long>((tb + 255) / 256, 8192), 256, 0, stream>>>(
-        d.B + (long)tau * d.b_tapoff, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N,
-        d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows), (int)b_ntile, nkc, dst + tau * tapstride, guard);
+  split_frag32_kernel<<<dim3((int)std::min<long>((tb + 255) / 256, 8192), d.ntaps), 256, 0, stream>>>(
+      d.B, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N, d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows),
+      (int)b_ntile, nkc, dst, guard, d.b_tapoff, tapstride);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
@@ -1373,10 +1430,8 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
         d.amax_a = amax;
       }
       const long kb = frag16_b_krows(d);
-      for (int tau = 0; tau < d.ntaps; ++tau) {
-        if (d.b_trans) absmax2d(d.B + (long)tau * d.b_tapoff, d.N, d.Kc, d.ldb, amax + 1, stream);
-        else absmax2d(d.B + (long)tau * d.b_tapoff, kb, d.N, d.ldb, amax + 1, stream);
-      }
+      if (d.b_trans) absmax_taps(d.B, d.ntaps, d.b_tapoff, d.N, d.Kc, d.ldb, amax + 1, stream);
+      else absmax_taps(d.B, d.ntaps, d.b_tapoff, kb, d.N, d.ldb, amax + 1, stream);
       d.amax_b = amax + 1;
     }
     const long a_src_rows = d.a_trans ? d.M : d.a_rows;
@@ -1402,10 +1457,9 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
       _Float16* tmp = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, (int)b_krows) / 2);
       if (!tmp) return AVC_ERR_WORKSPACE;
       const long tb = b_ntile * 32 * b_nkc * 2;
-      for (int tau = 0; tau < d.ntaps; ++tau)
-        split_frag32_kernel<<<(int)std::min<long>((tb + 255) / 256, 8192), 256, 0, stream>>>(
-            d.B + (long)tau * d.b_tapoff, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N, (int)b_krows,
-            (int)b_ntile, b_nkc, tmp + tau * tapstride, d.amax_b);
+      split_frag32_kernel<<<dim3((int)std::min<long>((tb + 255) / 256, 8192), d.ntaps), 256, 0, stream>>>(
+          d.B, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N, (int)b_krows, (int)b_ntile, b_nkc, tmp,
+          d.amax_b, d.b_tapoff, tapstride);
       bs = tmp;
     }
     AVC_LAUNCH_CHECK();
@@ -1451,8 +1505,17 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     const long total = (long)d.nz * d.M * d.N;
     const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
     if (d.nz == 1 && d.ldc_col == 1 && d.N % 4 == 0 && d.ldc % 4 == 0 && aligned16(d.C)) {
-      const int rpb = std::max(1, 1024 / (d.N / 4));  // ~4 float4 per thread
-      splitk_reduce4_kernel<<<dim3(1, (d.M + rpb - 1) / rpb), 256, 0, stream>>>(d, p.nsplit, slab, rpb);
+      const int n4 = d.N / 4;
+      int rpb = std::max(1, 1024 / n4);  // ~4 float4 per thread
+      if ((d.M + rpb - 1) / rpb < 256 && n4 <= 128) {
+        // too few row chunks to fill the chip: one row chunk per block, K-splits across threads
+        rpb = std::max(1, std::min(256 / n4, d.M / 256));
+        int G = 1;
+        while (2 * G * rpb * n4 <= 256 && 2 * G <= p.nsplit) G *= 2;
+        splitk_reduce4g_kernel<<<dim3(1, (d.M + rpb - 1) / rpb), 256, 0, stream>>>(d, p.nsplit, slab, rpb, G);
+      } else {
+        splitk_reduce4_kernel<<<dim3(1, (d.M + rpb - 1) / rpb), 256, 0, stream>>>(d, p.nsplit, slab, rpb);
+      }
     } else {
       splitk_reduce_kernel<<<blocks, 256, 0, stream>>>(d, p.nsplit, slab);
     }

@@ -1,6 +1,9 @@
+# A/B of the C3 step time: the library named by $1 (default ablib/prev.so) against the in-tree
+# build, alternating processes, two rounds each
 set -e
+prev=${1:-ablib/prev.so}
 for i in 1 2; do
-  AUTOVC_HIP_LIB=ablib/prev.so timeout -k 10 120 python scripts/train_time.py >> gpurun_out/abt.log 2>&1
+  AUTOVC_HIP_LIB=$prev timeout -k 10 120 python scripts/train_time.py >> gpurun_out/abt.log 2>&1
   timeout -k 10 120 python scripts/train_time.py >> gpurun_out/abt.log 2>&1
 done
-cat gpurun_out/abt.log | grep median
+grep median gpurun_out/abt.log
