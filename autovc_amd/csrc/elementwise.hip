@@ -530,10 +530,17 @@ __global__ void loss_grad_kernel(int kind, long n, const float* __restrict__ a,
 }
 
 // ---- optimizer ---------------------------------------------------------------------------
-__global__ void sumsq_partial_kernel(long n, const float* __restrict__ g, double* __restrict__ part) {
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(long n, const float* __restrict__ g,
+                                                            double* __restrict__ part) {
   __shared__ double red[256];
   double s = 0.0;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+  const long n4 = (reinterpret_cast<uintptr_t>(g) & 15) == 0 ? n / 4 : 0;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = g4[i];
+    s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+  for (long i = 4 * n4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const double v = g[i];
     s += v * v;
   }
@@ -546,12 +553,20 @@ __global__ void sumsq_partial_kernel(long n, const float* __restrict__ g, double
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
-__global__ void clip_coef_kernel(int nparts, const double* __restrict__ part, float max_norm,
-                                 float* __restrict__ norm_out, float* __restrict__ coef) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// one block of 256: strided partial sums, then a fixed-order tree (deterministic)
+__global__ __launch_bounds__(256) void clip_coef_kernel(int nparts, const double* __restrict__ part, float max_norm,
+                                                        float* __restrict__ norm_out, float* __restrict__ coef) {
+  __shared__ double red[256];
   double s = 0.0;
-  for (int p = 0; p < nparts; ++p) s += part[p];
-  const float norm = (float)sqrt(s);
+  for (int p = threadIdx.x; p < nparts; p += 256) s += part[p];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const float norm = (float)sqrt(red[0]);
   if (norm_out) norm_out[0] = norm;
   float c = 1.f;
   if (max_norm > 0.f) {
@@ -561,30 +576,55 @@ __global__ void clip_coef_kernel(int nparts, const double* __restrict__ part, fl
   coef[0] = c;
 }
 
-__global__ void adam_ema_kernel(long n, float* __restrict__ p, float* __restrict__ g,
-                                float* __restrict__ m, float* __restrict__ v, float* __restrict__ ema,
-                                const float* __restrict__ coef, float lr, float b1, float b2,
-                                float eps, float wd, float step_size, float bc2_sqrt, float ema_decay,
-                                float ema_keep, int clip) {
-  const float c = clip ? coef[0] : 1.f;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float gi = g[i];
-    if (clip) {
-      gi *= c;
-      g[i] = gi;
-    }
-    float pi = p[i];
-    if (wd != 0.f) gi += wd * pi;
-    const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // torch foreach Adam: exp_avg.lerp_(g, 1-b1)
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+struct AdamArgs {
+  float c, lr, b1, b2, eps, wd, step_size, bc2_sqrt, ema_decay, ema_keep;
+  int clip;
+};
+
+// one element of the fused clip + Adam + EMA update (torch.optim.Adam's foreach arithmetic)
+__device__ __forceinline__ void adam_elem(const AdamArgs& a, float& pi, float& gi, float& mi, float& vi,
+                                          float* ei) {
+  if (a.clip) gi *= a.c;
+  float gw = gi;
+  if (a.wd != 0.f) gw += a.wd * pi;
+  mi = mi + (1.f - a.b1) * (gw - mi);  // torch foreach Adam: exp_avg.lerp_(g, 1-b1)
+  vi = a.b2 * vi + (1.f - a.b2) * gw * gw;
+  const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
+  pi -= a.step_size * (mi / denom);
+  // torch: ema_decay * avg + (1 - ema_decay) * flat  (two rounded products, one rounded sum;
+  // 1 - ema_decay formed in double on the host like the Python scalar)
+  if (ei) *ei = __fadd_rn(__fmul_rn(a.ema_decay, *ei), __fmul_rn(a.ema_keep, pi));
+}
+
+// float4 form over the first n4 * 4 elements (all five arrays 16-byte aligned), scalar tail
+__global__ __launch_bounds__(256) void adam_ema_kernel(long n, long n4, float* __restrict__ p, float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       float* __restrict__ ema, const float* __restrict__ coef,
+                                                       AdamArgs a) {
+  a.c = a.clip ? coef[0] : 1.f;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 p4 = reinterpret_cast<float4*>(p)[i], g4 = reinterpret_cast<float4*>(g)[i];
+    float4 m4 = reinterpret_cast<float4*>(m)[i], v4 = reinterpret_cast<float4*>(v)[i];
+    float4 e4 = ema ? reinterpret_cast<float4*>(ema)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float* e = ema ? &e4.x : nullptr;
+    adam_elem(a, p4.x, g4.x, m4.x, v4.x, e ? e + 0 : nullptr);
+    adam_elem(a, p4.y, g4.y, m4.y, v4.y, e ? e + 1 : nullptr);
+    adam_elem(a, p4.z, g4.z, m4.z, v4.z, e ? e + 2 : nullptr);
+    adam_elem(a, p4.w, g4.w, m4.w, v4.w, e ? e + 3 : nullptr);
+    if (a.clip) reinterpret_cast<float4*>(g)[i] = g4;
+    reinterpret_cast<float4*>(m)[i] = m4;
+    reinterpret_cast<float4*>(v)[i] = v4;
+    reinterpret_cast<float4*>(p)[i] = p4;
+    if (ema) reinterpret_cast<float4*>(ema)[i] = e4;
+  }
+  for (long i = 4 * n4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pi = p[i], gi = g[i], mi = m[i], vi = v[i];
+    adam_elem(a, pi, gi, mi, vi, ema ? ema + i : nullptr);
+    if (a.clip) g[i] = gi;
     m[i] = mi;
     v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    pi -= step_size * (mi / denom);
     p[i] = pi;
-    // torch: ema_decay * avg + (1 - ema_decay) * flat  (two rounded products, one rounded sum;
-    // 1 - ema_decay formed in double on the host like the Python scalar)
-    if (ema) ema[i] = __fadd_rn(__fmul_rn(ema_decay, ema[i]), __fmul_rn(ema_keep, pi));
   }
 }
 
@@ -809,14 +849,20 @@ int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, floa
   const bool need_norm = max_norm > 0.f || norm_out != nullptr;
   if (need_norm) {
     sumsq_partial_kernel<<<nb, 256, 0, s>>>((long)n, g, part);
-    clip_coef_kernel<<<1, 64, 0, s>>>(nb, part, max_norm, norm_out, coef);
+    clip_coef_kernel<<<1, 256, 0, s>>>(nb, part, max_norm, norm_out, coef);
   }
   const double bc1 = 1.0 - std::pow((double)b1, step);
   const double bc2 = 1.0 - std::pow((double)b2, step);
-  adam_ema_kernel<<<ew_blocks((long)n), 256, 0, s>>>((long)n, p, g, m, v, ema, coef, lr, b1, b2, eps,
-                                                     wd, (float)(lr / bc1), (float)std::sqrt(bc2),
-                                                     (float)ema_decay, (float)(1.0 - ema_decay),
-                                                     max_norm > 0.f ? 1 : 0);
+  AdamArgs a{};
+  a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
+  a.step_size = (float)(lr / bc1);
+  a.bc2_sqrt = (float)std::sqrt(bc2);
+  a.ema_decay = (float)ema_decay;
+  a.ema_keep = (float)(1.0 - ema_decay);
+  a.clip = max_norm > 0.f ? 1 : 0;
+  const bool al = aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v) && (!ema || aligned16(ema));
+  const long n4 = al ? (long)n / 4 : 0;
+  adam_ema_kernel<<<ew_blocks(std::max<long>(n4, (long)n - 4 * n4)), 256, 0, s>>>((long)n, n4, p, g, m, v, ema, coef, a);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

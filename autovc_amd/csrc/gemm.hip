@@ -674,8 +674,21 @@ __global__ __launch_bounds__(256) void absmax_rows_kernel(const float* __restric
                                                           long ld, unsigned* __restrict__ out) {
   __shared__ float red[4];
   float m = 0.f;
-  for (long r = blockIdx.x; r < rows; r += gridDim.x)
-    for (int c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, fabsf(src[r * ld + c]));
+  if ((cols & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    // flattened (row, float4 column) index: narrow regions (cols = 32 of a 64-wide row) still
+    // keep every lane busy
+    const int c4n = cols >> 2;
+    const long n = rows * c4n;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += gridDim.x * 256L) {
+      const long r = i / c4n;
+      const int c = (int)(i - r * c4n);
+      const float4 v = *reinterpret_cast<const float4*>(src + r * ld + 4 * c);
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  } else {
+    for (long r = blockIdx.x; r < rows; r += gridDim.x)
+      for (int c = threadIdx.x; c < cols; c += 256) m = fmaxf(m, fabsf(src[r * ld + c]));
+  }
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
@@ -688,8 +701,9 @@ inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* 
     absmax_vec_kernel<<<(int)std::max<long>(1, std::min<long>((n4 + 255) / 256, 1024)), 256, 0, s>>>(
         reinterpret_cast<const float4*>(src), n4, src + 4 * n4, (int)(n - 4 * n4), out);
   } else {
-    absmax_rows_kernel<<<(int)std::max<long>(1, std::min<long>(rows, 2048)), 256, 0, s>>>(src, rows, (int)cols, ld,
-                                                                                          out);
+    const long blocks = (cols % 4 == 0 && ld % 4 == 0) ? (rows * (cols / 4) + 1023) / 1024 : rows;
+    absmax_rows_kernel<<<(int)std::max<long>(1, std::min<long>(blocks, 2048)), 256, 0, s>>>(src, rows, (int)cols,
+                                                                                            ld, out);
   }
 }
 
