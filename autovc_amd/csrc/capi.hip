@@ -204,6 +204,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   return AVC_OK;
 }
 
+void drop_graph(avc_context* ctx);  // captured Generator graphs (defined below)
 }  // namespace
 }  // namespace avc
 
@@ -231,9 +232,9 @@ int avc_context_destroy(avc_context* ctx) {
   persist_release(ctx);
   for (void* p : ctx->retired) (void)hipFree(p);
   for (auto& e : ctx->prep) (void)hipFree(e.buf);
-  if (ctx->gen.exec) (void)hipGraphExecDestroy(ctx->gen.exec);
-  if (ctx->gen.graph) (void)hipGraphDestroy(ctx->gen.graph);
+  drop_graph(ctx);  // the staging graph and every direct graph
   if (ctx->gen.stage) (void)hipFree(ctx->gen.stage);
+  if (ctx->zpool) (void)hipFree(ctx->zpool);
   if (ctx->capture_stream) (void)hipStreamDestroy(ctx->capture_stream);
   if (ctx->base) (void)hipFree(ctx->base);
   delete ctx;

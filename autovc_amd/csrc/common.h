@@ -126,6 +126,10 @@ struct avc_context {
   bool track_ranges = false;
   std::vector<const void*> range_ok;
   unsigned fail_seen = 0;         // value of *fail_host already reported to the caller
+  // pool of device words handed out already zeroed (max-scan accumulators of gradient products):
+  // one zeroing launch per kZeroPool words instead of one per product (zeroed_words)
+  unsigned* zpool = nullptr;
+  int zpool_next = 0;
   std::vector<avc_prep_entry> prep;
   avc_gen_graph gen;
   hipStream_t capture_stream = nullptr;
@@ -141,6 +145,11 @@ namespace avc {
 // zero `bytes` at p (16-B aligned) on stream s with a kernel (elementwise.hip); used instead of
 // hipMemsetAsync everywhere (see there)
 int zero_async(void* p, size_t bytes, hipStream_t s);
+// n (<= 64) device words that read as zero in stream order on s: taken from the context's pool,
+// which is re-zeroed by one launch when it wraps (every earlier use of the pool precedes that
+// launch on the stream).  While s is capturing a graph the words are zeroed by their own node
+// instead (a replay must not depend on the pool's host-side position).  nullptr + error on failure.
+unsigned* zeroed_words(avc_context* ctx, int n, hipStream_t s);
 
 // Device-side failures reported through the context's pinned host words (host_flags):
 //   [0] number of the last persistent-recurrence launch that abandoned a bounded wait;

@@ -762,6 +762,34 @@ int zero_async(void* p, size_t bytes, hipStream_t s) {
   return AVC_OK;
 }
 
+constexpr int kZeroPool = 16384;  // words (64 KiB)
+
+unsigned* zeroed_words(avc_context* ctx, int n, hipStream_t s) {
+  if (n <= 0 || n > 64) {
+    set_error("zeroed_words: 1..64 words");
+    return nullptr;
+  }
+  const int take = (n + 15) / 16 * 16;  // 64-byte granules
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess) cs = hipStreamCaptureStatusActive;
+  if (!ctx->zpool) {
+    if (hipMalloc(&ctx->zpool, kZeroPool * sizeof(unsigned)) != hipSuccess) {
+      ctx->zpool = nullptr;
+      set_error("zeroed_words: hipMalloc failed");
+      return nullptr;
+    }
+    ctx->zpool_next = kZeroPool;  // forces the first zeroing below
+  }
+  if (ctx->zpool_next + take > kZeroPool) {
+    if (zero_async(ctx->zpool, kZeroPool * sizeof(unsigned), s) != AVC_OK) return nullptr;
+    ctx->zpool_next = 0;
+  }
+  unsigned* p = ctx->zpool + ctx->zpool_next;
+  ctx->zpool_next += take;
+  if (cs != hipStreamCaptureStatusNone && zero_async(p, take * sizeof(unsigned), s) != AVC_OK) return nullptr;
+  return p;
+}
+
 int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s) {
   mel_from_frames_kernel<<<ew_blocks((long)B * cm * T), 256, 0, s>>>(T, B, cm, fr, mel);
   AVC_LAUNCH_CHECK();

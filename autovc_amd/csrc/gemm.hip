@@ -659,7 +659,18 @@ __global__ __launch_bounds__(256) void absmax_vec_kernel(const float4* __restric
                                                          unsigned* __restrict__ out) {
   __shared__ float red[4];
   float m = 0.f;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+  // four independent loads in flight per thread per iteration
+  const long stride = (long)gridDim.x * 256;
+  long i = blockIdx.x * 256L + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+  }
+  for (; i < n4; i += stride) {
     const float4 v = src[i];
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
   }
@@ -698,7 +709,7 @@ __global__ __launch_bounds__(256) void absmax_rows_kernel(const float* __restric
 inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t s) {
   if (ld == cols && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
     const long n = rows * cols, n4 = n / 4;
-    absmax_vec_kernel<<<(int)std::max<long>(1, std::min<long>((n4 + 255) / 256, 1024)), 256, 0, s>>>(
+    absmax_vec_kernel<<<(int)std::max<long>(1, std::min<long>((n4 + 1023) / 1024, 2048)), 256, 0, s>>>(
         reinterpret_cast<const float4*>(src), n4, src + 4 * n4, (int)(n - 4 * n4), out);
   } else {
     const long blocks = (cols % 4 == 0 && ld % 4 == 0) ? (rows * (cols / 4) + 1023) / 1024 : rows;
@@ -1435,9 +1446,8 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
   if (frag) {
     // split both operands once into the fragment-major layout gemm16f_kernel streams
     if (scaled_product) {  // power-of-two operand scales from max |A|, max |B| (device side)
-      unsigned* amax = sc.take<unsigned>(64);
+      unsigned* amax = zeroed_words(ctx, 2, stream);
       if (!amax) return AVC_ERR_WORKSPACE;
-      AVC_TRY(zero_async(amax, 2 * sizeof(unsigned), stream));
       if (!d.amax_a) {
         if (d.a_trans) absmax2d(d.A, d.Kc, d.M, d.lda, amax, stream);
         else absmax2d(d.A, d.a_rows, d.Kc, d.lda, amax, stream);

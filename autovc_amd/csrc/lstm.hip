@@ -1162,8 +1162,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TAKE(slab, float, (size_t)nsplit * B * H, sc);
     permute_rows_kernel<<<ew_blocks(4L * H * din), 256, 0, s>>>(w_ih, wih_p, H, din);
     transpose_permute_kernel<<<dim3(4 * H / 32, H / 32), 256, 0, s>>>(w_hh, whhT, H);
-    AVC_TRY(zero_async(amax_w, 64 * sizeof(unsigned), s));
-    AVC_TRY(gemm_absmax(w_hh, 4L * H, H, H, amax_w, s));
+    AVC_TRY(gemm_absmax(w_hh, 4L * H, H, H, amax_w, s));  // (zeroes *amax_w first)
     AVC_TRY(gemm_split_frag(whhT, 4L * H, H, 4 * H, amax_w, whhT_s, s));
     AVC_TRY(zero_async(dc, sizeof(float) * B * H, s));
     AVC_TRY(zero_async(dgs, gemm_afrag_bytes(arows, 4 * H), s));  // padding rows stay zero
