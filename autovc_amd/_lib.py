@@ -34,6 +34,10 @@ _SIGS = {
                                 _P, _P, _P, _P, _P, _P],
     "avc_conv_bn_act_backward": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P,
                                  _P, _P, _P, _P, _I, _P],
+    "avc_conv_bn_act_forward_ex": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _I,
+                                   _P, _P, _P, _P, _P, _P, _P, _P],
+    "avc_conv_bn_act_backward_ex": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P,
+                                    _P, _P, _P, _P, _I, _P, _P],
     "avc_lstm_forward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P],
     "avc_bilstm_forward": [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P],
     "avc_lstm_backward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P,

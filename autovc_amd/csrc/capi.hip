@@ -271,6 +271,33 @@ int avc_conv_bn_act_forward(avc_context* ctx, int T, int B, int cin, int cout, c
                                   mean, invstd, S(stream));
 }
 
+int avc_conv_bn_act_forward_ex(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                               const float* weight, const float* bias, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var,
+                               int training, float momentum, float eps, int act,
+                               const float* residual, float* y_pre, float* out, float* mean,
+                               float* invstd, const unsigned* x_amax, unsigned* out_amax, void* stream) {
+  AVC_CHECK_ARG(ctx && x && weight && gamma && beta && y_pre && out && mean && invstd, "NULL pointer");
+  AVC_CHECK_ARG(aligned16(x_amax) && aligned16(out_amax), "amax words must be 16-byte aligned");
+  AVC_TRY(ensure_arena(ctx, conv_bn_forward_scratch(T, B, cin, cout)));
+  return conv_bn_act_forward_impl(ctx, T, B, cin, cout, x, weight, bias, gamma, beta, running_mean,
+                                  running_var, training, momentum, eps, act, residual, y_pre, out,
+                                  mean, invstd, S(stream), nullptr, nullptr, x_amax, out_amax);
+}
+
+int avc_conv_bn_act_backward_ex(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                                const float* weight, const float* gamma, const float* beta,
+                                const float* y_pre, const float* mean, const float* invstd,
+                                int training, int act, const float* d_out, float* d_x,
+                                float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
+                                int accumulate, const unsigned* x_amax, void* stream) {
+  AVC_CHECK_ARG(ctx && x && weight && gamma && beta && y_pre && mean && invstd && d_out, "NULL pointer");
+  AVC_TRY(ensure_arena(ctx, conv_bn_backward_scratch(T, B, cin, cout)));
+  return conv_bn_act_backward_impl(ctx, T, B, cin, cout, x, weight, gamma, beta, y_pre, mean, invstd,
+                                   training, act, d_out, d_x, d_weight, d_bias, d_gamma, d_beta,
+                                   accumulate, S(stream), x_amax);
+}
+
 int avc_conv_bn_act_backward(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
                              const float* weight, const float* gamma, const float* beta,
                              const float* y_pre, const float* mean, const float* invstd,

@@ -73,9 +73,11 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
                              int training, float momentum, float eps, int act,
                              const float* residual, float* y_pre, float* out, float* mean,
                              float* invstd, hipStream_t s, const _Float16* x_frag,
-                             _Float16* out_frag) {
+                             _Float16* out_frag, const unsigned* x_amax, unsigned* out_amax) {
   // x_frag: x already split (the previous layer's bn_apply wrote it); out_frag: also emit the
-  // output split for the next layer (out may then be NULL: the fp32 output is not stored)
+  // output split for the next layer (out may then be NULL: the fp32 output is not stored).
+  // x_amax: x's max words from its producer (see bn_apply's amax_out): the range scan of x is
+  // skipped; out_amax: record out's max words for the next layer (fp32 output path only)
   AVC_CHECK_ARG(T > 0 && B > 0, "conv: empty input");
   AVC_CHECK_ARG(cin % 4 == 0 && cout % 4 == 0, "conv: channel counts must be multiples of 4");
   AVC_CHECK_ARG(training || (running_mean && running_var), "conv: eval mode needs running stats");
@@ -90,6 +92,8 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   }
   GemmDesc g = conv_fwd_desc(T, B, cin, cout, x, wt, bias, y_pre);
   g.a_frag = x_frag;
+  if (x_amax) g.a_guard = x_amax + 1;
+  if (out_frag || !out) out_amax = nullptr;
   if (ctx->prep_version >= 0) {  // cache the split-f16 copy of the taps as well
     bool fb = true;
     auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_CONV_BFRAG, weight, nullptr, gemm_bfrag_bytes(g), &fb));
@@ -109,7 +113,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   }
   AVC_TRY(gemm_run(ctx, g, s));
   AVC_TRY(bn_finalize(cout, nparts, stats, (double)T * B, training, momentum, eps, running_mean,
-                      running_var, mean, invstd, s));
+                      running_var, mean, invstd, s, out_amax));
   // inside the whole-Generator forward the output's range is checked here (its consumer then
   // skips the scan); a value the next split could not hold is reported to the host.  The layer
   // with a residual (postnet's last, model.py:131-132) produces the final mel_post, which no
@@ -118,7 +122,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   unsigned* flags = check ? host_flags(ctx) : nullptr;
   if (check && !flags) return AVC_ERR_HIP;
   AVC_TRY(bn_apply((long)T * B, cout, y_pre, mean, invstd, gamma, beta, act, residual, out, s, out_frag,
-                   flags ? flags + 1 : nullptr));
+                   flags ? flags + 1 : nullptr, out_amax));
   if (check && out) mark_range_checked(ctx, out);
   return AVC_OK;
 }
@@ -140,7 +144,9 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
                               const float* y_pre, const float* mean, const float* invstd,
                               int training, int act, const float* d_out, float* d_x,
                               float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
-                              int accumulate, hipStream_t s) {
+                              int accumulate, hipStream_t s, const unsigned* x_amax) {
+  // x_amax: max |x| recorded by x's producer (bn_apply's amax_out): the weight gradient's scan
+  // of x is skipped
   AVC_CHECK_ARG(T > 0 && B > 0, "conv_backward: empty input");
   AVC_CHECK_ARG(cin % 4 == 0 && cout % 4 == 0, "conv_backward: channels must be multiples of 4");
   AVC_CHECK_ARG(accumulate >= 0 && accumulate <= 2, "conv_backward: accumulate must be 0, 1 or 2");
@@ -179,6 +185,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
     g.nz = 5; g.c_zoff = 1;
     g.C = d_weight; g.ldc = 5L * cin; g.ldc_col = 5; g.accumulate = acc_p;
     g.prec16 = 1; g.split_scale = 1; g.amax_a = amax_dy;
+    g.amax_b = x_amax;
     AVC_TRY(gemm_run(ctx, g, s));
   }
   return AVC_OK;

@@ -4,15 +4,20 @@
 
 namespace avc {
 
+// amax_init != NULL: also set amax_init[0] = 0, amax_init[1] = 2^14 (bn_apply's amax_out words)
 int bn_finalize(int C, int nparts, const float* stats, double count, int training, float momentum,
-                float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s);
+                float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s,
+                unsigned* amax_init = nullptr);
 // frag != NULL: also write the output split into the GEMM's fragment-major A layout
 // (gemm_afrag_bytes(M, C) bytes, for GemmDesc::a_frag); out may then be NULL (not stored).
 // range_flag (pinned host word): set when a finite output exceeds the f16 split's range (the
 // output is then range-checked: mark_range_checked lets its consumer skip the scan)
 int bn_apply(long M, int C, const float* y, const float* mean, const float* invstd,
              const float* gamma, const float* beta, int act, const float* residual, float* out,
-             hipStream_t s, _Float16* frag = nullptr, unsigned* range_flag = nullptr);
+             hipStream_t s, _Float16* frag = nullptr, unsigned* range_flag = nullptr,
+             unsigned* amax_out = nullptr);
+// amax_out (fp32 output only; words initialised by bn_finalize's amax_init): [0] = max |out|,
+// [1] = max(|out|, 2^14) -- the range-guard word a forward contraction of out would compute
 size_t bn_backward_scratch(int M, int C);
 int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* y,
                 const float* mean, const float* invstd, const float* gamma, const float* beta,

@@ -75,8 +75,10 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, con
                                                           float eps, float* __restrict__ rmean,
                                                           float* __restrict__ rvar,
                                                           float* __restrict__ mean_out,
-                                                          float* __restrict__ invstd_out) {
+                                                          float* __restrict__ invstd_out,
+                                                          unsigned* __restrict__ amax_init) {
   __shared__ double red[2][4][64];
+  if (amax_init && blockIdx.x == 0 && threadIdx.x < 2) amax_init[threadIdx.x] = threadIdx.x ? 0x46800000u : 0u;
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   if (training) {
@@ -119,14 +121,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
                                                        const float* __restrict__ beta, int act,
                                                        const float* __restrict__ residual,
                                                        float* __restrict__ out,
-                                                       unsigned* __restrict__ range_flag) {
+                                                       unsigned* __restrict__ range_flag,
+                                                       unsigned* __restrict__ amax_out) {
   const int Q = C / 4;
   const long nthreads = (long)gridDim.x * blockDim.x;
   const long gt = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const long rows_per_pass = nthreads / Q;
   const int q = (int)(gt % Q);
-  const long r0 = gt / Q;
-  if (r0 >= rows_per_pass) return;  // leftover threads would revisit rows (out may alias y)
+  // leftover threads would revisit rows (out may alias y): they skip the loop (but take part in
+  // the block's max reduction)
+  const long r0 = gt / Q < rows_per_pass ? gt / Q : M;
+  float amax = 0.f;
   float sc[4], sh[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -151,6 +156,18 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
       if (over) __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     reinterpret_cast<float4*>(out)[i4] = make_float4(o[0], o[1], o[2], o[3]);
+    if (amax_out) amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+  }
+  if (amax_out) {
+    __shared__ float red[4];
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      atomicMax(amax_out, __float_as_uint(m));
+      atomicMax(amax_out + 1, __float_as_uint(fmaxf(m, 16384.f)));
+    }
   }
 }
 
@@ -505,12 +522,20 @@ __global__ void loss_partial_kernel(int kind, long n, const float* __restrict__ 
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
-__global__ void loss_final_kernel(int nparts, const double* __restrict__ part, double inv_n,
-                                  float* __restrict__ out, int accumulate) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// one block of 256: strided partial sums, then a fixed-order tree (deterministic)
+__global__ __launch_bounds__(256) void loss_final_kernel(int nparts, const double* __restrict__ part, double inv_n,
+                                                         float* __restrict__ out, int accumulate) {
+  __shared__ double red[256];
   double s = 0.0;
-  for (int p = 0; p < nparts; ++p) s += part[p];
-  const float v = (float)(s * inv_n);
+  for (int p = threadIdx.x; p < nparts; p += 256) s += part[p];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const float v = (float)(red[0] * inv_n);
   out[0] = accumulate ? out[0] + v : v;
 }
 
@@ -650,16 +675,17 @@ int colsum(avc_context* ctx, int M, int N, const float* X, long ld, float* out, 
 }
 
 int bn_finalize(int C, int nparts, const float* stats, double count, int training, float momentum,
-                float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s) {
+                float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s,
+                unsigned* amax_init) {
   bn_finalize_kernel<<<(C + 63) / 64, 256, 0, s>>>(C, nparts, stats, count, training, momentum,
-                                                   eps, rmean, rvar, mean, invstd);
+                                                   eps, rmean, rvar, mean, invstd, amax_init);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
 
 int bn_apply(long M, int C, const float* y, const float* mean, const float* invstd,
              const float* gamma, const float* beta, int act, const float* residual, float* out,
-             hipStream_t s, _Float16* frag, unsigned* range_flag) {
+             hipStream_t s, _Float16* frag, unsigned* range_flag, unsigned* amax_out) {
   AVC_CHECK_ARG(C % 4 == 0, "bn_apply: channels must be a multiple of 4");
   if (frag) {
     AVC_CHECK_ARG(C % 8 == 0, "bn_apply: the split output needs channels in multiples of 8");
@@ -675,7 +701,8 @@ int bn_apply(long M, int C, const float* y, const float* mean, const float* invs
   const long Q = C / 4;
   const long threads = std::max<long>(256, std::min<long>(M * Q / 4, 2048L * 256));
   const long blocks = (threads + 255) / 256;
-  bn_apply_kernel<<<(int)blocks, 256, 0, s>>>(M, C, y, mean, invstd, gamma, beta, act, residual, out, range_flag);
+  bn_apply_kernel<<<(int)blocks, 256, 0, s>>>(M, C, y, mean, invstd, gamma, beta, act, residual, out, range_flag,
+                                              amax_out);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
@@ -850,7 +877,7 @@ int loss_forward(avc_context* ctx, int kind, size_t n, const float* a, const flo
   const int nb = (int)std::min<size_t>(1024, (n + 255) / 256);
   AVC_TAKE(part, double, (size_t)nb, sc);
   loss_partial_kernel<<<nb, 256, 0, s>>>(kind, (long)n, a, b, part);
-  loss_final_kernel<<<1, 64, 0, s>>>(nb, part, 1.0 / (double)n, out, accumulate);
+  loss_final_kernel<<<1, 256, 0, s>>>(nb, part, 1.0 / (double)n, out, accumulate);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

@@ -32,7 +32,10 @@ struct GemmDesc {
                             // max |x| before splitting (gradients: any magnitude), unscale exactly
   const unsigned* amax_a = nullptr;  // max |A| as float bits (device); preset by the caller to
                                      // share one scan between products, else filled by gemm_run
-  const unsigned* amax_b = nullptr;  // max |B| (filled by gemm_run)
+  const unsigned* amax_b = nullptr;  // max |B|: filled by gemm_run, or preset by the caller for a
+                                     // scaled (gradient) product whose B's producer recorded it
+  const unsigned* a_guard = nullptr; // forward products: A's range-guard word max(|A|, 2^14) from
+                                     // its producer (bn_apply's amax_out + 1); skips the scan
   const _Float16* b_frag = nullptr;  // optional B already split by gemm_prepare_bfrag (prec16 only;
                                      // carries its range-guard word, see gemm_prepare_bfrag)
   const _Float16* a_frag = nullptr;  // optional A already split (row-major A, unscaled forward

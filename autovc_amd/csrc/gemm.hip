@@ -1430,7 +1430,9 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     float* part = sc.take<float>(kGuardBlocks);
     if (!gw || !part) return AVC_ERR_WORKSPACE;
     d.amax_a = nullptr;
-    if (!d.a_frag && !(d.a_bound > 0.f && d.a_bound < 32768.f) && !range_checked(ctx, d.A)) {
+    if (d.a_guard && !d.a_frag) {
+      d.amax_a = d.a_guard;
+    } else if (!d.a_frag && !(d.a_bound > 0.f && d.a_bound < 32768.f) && !range_checked(ctx, d.A)) {
       AVC_TRY(guard_scan(ctx, d.A, d.a_rows, d.Kc, d.lda, part, gw, stream));
       d.amax_a = gw;
     }
@@ -1453,10 +1455,12 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
         else absmax2d(d.A, d.a_rows, d.Kc, d.lda, amax, stream);
         d.amax_a = amax;
       }
-      const long kb = frag16_b_krows(d);
-      if (d.b_trans) absmax_taps(d.B, d.ntaps, d.b_tapoff, d.N, d.Kc, d.ldb, amax + 1, stream);
-      else absmax_taps(d.B, d.ntaps, d.b_tapoff, kb, d.N, d.ldb, amax + 1, stream);
-      d.amax_b = amax + 1;
+      if (!d.amax_b) {
+        const long kb = frag16_b_krows(d);
+        if (d.b_trans) absmax_taps(d.B, d.ntaps, d.b_tapoff, d.N, d.Kc, d.ldb, amax + 1, stream);
+        else absmax_taps(d.B, d.ntaps, d.b_tapoff, kb, d.N, d.ldb, amax + 1, stream);
+        d.amax_b = amax + 1;
+      }
     }
     const long a_src_rows = d.a_trans ? d.M : d.a_rows;
     const long a_ntile = frag_ntile(a_src_rows);
@@ -1498,7 +1502,9 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     float* part = sc.take<float>(kGuardBlocks);
     if (!gw || !part) return AVC_ERR_WORKSPACE;
     d.amax_a = nullptr;
-    if (!(d.a_bound > 0.f && d.a_bound < 32768.f) && !range_checked(ctx, d.A)) {
+    if (d.a_guard) {
+      d.amax_a = d.a_guard;
+    } else if (!(d.a_bound > 0.f && d.a_bound < 32768.f) && !range_checked(ctx, d.A)) {
       AVC_TRY(guard_scan(ctx, d.A, d.a_rows, d.Kc, d.lda, part, gw, stream));
       d.amax_a = gw;
     }

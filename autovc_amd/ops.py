@@ -8,6 +8,7 @@ CPU or through PyTorch kernels except autograd's own gradient bookkeeping.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -145,6 +146,24 @@ class MelFromFrames(torch.autograd.Function):
         return dfr, None, None
 
 
+# AUTOVC_AMAX_CHAIN=0: consumers ignore the recorded words (A/B measurements)
+_AMAX_CHAIN = os.environ.get("AUTOVC_AMAX_CHAIN", "1") != "0"
+
+
+def _wptr(t):
+    """Device pointer of a device-word tensor (int32), None -> NULL."""
+    return None if t is None else t.data_ptr()
+
+
+def _amax_of(x):
+    """The max words a ConvBNAct forward recorded for x (its output), if x is that very tensor
+    and unmodified since (same version counter); else None (the consumer scans x itself)."""
+    rec = getattr(x, "_avc_amax", None)
+    if rec is None or rec[1] != x._version or not _AMAX_CHAIN:
+        return None
+    return rec[0]
+
+
 class ConvBNAct(torch.autograd.Function):
     """ConvNorm(k=5,p=2) -> BatchNorm1d -> act [+ residual]  (net_layers.py:39-49,
     encoder.py:69-70, decoder.py:69-70, postnet.py:54-61, model.py:131-132)."""
@@ -158,13 +177,19 @@ class ConvBNAct(torch.autograd.Function):
         out = _empty((T * B, cout), x)
         mean = _empty((cout,), x)
         invstd = _empty((cout,), x)
-        call("avc_conv_bn_act_forward", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
+        # max words of the activation, carried from layer to layer (conv -> conv chains): the
+        # producer records them while writing; the consumer skips its own scans of x
+        x_amax = _amax_of(x)
+        out_amax = torch.empty(4, dtype=torch.int32, device=x.device)
+        call("avc_conv_bn_act_forward_ex", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
              ptr(_c(bias)), ptr(gamma), ptr(beta), ptr(running_mean), ptr(running_var),
              int(training), float(momentum), float(eps), act, ptr(_c(residual)), ptr(y_pre), ptr(out),
-             ptr(mean), ptr(invstd), _stream(x))
+             ptr(mean), ptr(invstd), _wptr(x_amax), _wptr(out_amax), _stream(x))
+        out._avc_amax = (out_amax, out._version)
         _use(weight, bias, gamma, beta)
         ctx.save_for_backward(x, weight, gamma, beta, y_pre, mean, invstd)
         ctx.bias = bias
+        ctx.x_amax = x_amax
         ctx.cfg = (T, B, cin, cout, int(training), act, residual is not None, bias is not None)
         return out
 
@@ -177,9 +202,9 @@ class ConvBNAct(torch.autograd.Function):
         dx = _empty(x.shape, x) if ng[0] else None
         params = (weight, ctx.bias if has_bias else None, gamma, beta)
         (dw, db, dg, dbt), direct = _param_grads(params, ng[1:5])
-        call("avc_conv_bn_act_backward", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
+        call("avc_conv_bn_act_backward_ex", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
              ptr(gamma), ptr(beta), ptr(y_pre), ptr(mean), ptr(invstd), training, act, ptr(d_out),
-             ptr(dx), ptr(dw), ptr(db), ptr(dg), ptr(dbt), 2 if direct else 0, _stream(x))
+             ptr(dx), ptr(dw), ptr(db), ptr(dg), ptr(dbt), 2 if direct else 0, _wptr(ctx.x_amax), _stream(x))
         d_res = d_out if (has_res and ng[11]) else None
         dw, db, dg, dbt = _param_done(params, (dw, db, dg, dbt), direct)
         return dx, dw, db, dg, dbt, None, None, None, None, None, None, d_res, None, None

@@ -89,6 +89,25 @@ int avc_conv_bn_act_backward(avc_context* ctx, int T, int B, int cin, int cout, 
  * into its buffer, 2 = only the parameter gradients add (d_x overwritten) -- parameter
  * gradients accumulated in place across the uses of a layer (the encoder runs twice per loss). */
 
+/* The same two calls carrying the activations' max words between layers (the per-layer training
+ * path's conv -> conv chains, encoder.py:69-70 and postnet.py:54-61).  out_amax (2 device words,
+ * 16-byte aligned, may be NULL) receives [0] = max |out| and [1] = max(|out|, 2^14), computed
+ * while `out` is written; passing them back as the next layer's x_amax (forward: skips the range
+ * scan of its input; backward: skips the max scan of x in the weight gradient) gives results
+ * bit-identical to the calls above.  x_amax must describe exactly the current contents of x. */
+int avc_conv_bn_act_forward_ex(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                               const float* weight, const float* bias, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var,
+                               int training, float momentum, float eps, int act,
+                               const float* residual, float* y_pre, float* out, float* mean,
+                               float* invstd, const unsigned* x_amax, unsigned* out_amax, void* stream);
+int avc_conv_bn_act_backward_ex(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                                const float* weight, const float* gamma, const float* beta,
+                                const float* y_pre, const float* mean, const float* invstd,
+                                int training, int act, const float* d_out, float* d_x,
+                                float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
+                                int accumulate, const unsigned* x_amax, void* stream);
+
 /* ---- LSTM layer (one direction) -----------------------------------------------------------
  * Replaces one layer-direction of nn.LSTM (gates i,f,g,o; zero initial state) as used at
  * encoder.py:51,75 (H=32, bidirectional), decoder.py:37,65 (H=512) and decoder.py:53,74

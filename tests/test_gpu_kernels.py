@@ -454,3 +454,41 @@ def test_bptt_split_products_match_fp64(cuda_device, B, T, din, H, scale):
         errs = [rel(a, r) for a, r in zip(grads[name], refs)]
         print(f"bptt {name} B={B} T={T} H={H} scale={scale:g}: max rel err vs fp64 {max(errs):.2e}")
         assert max(errs) < 5e-5
+
+
+@pytest.mark.parametrize("B,T,act", [(32, 16, 1), (64, 8, 2), (3, 33, 1)])
+def test_conv_chain_max_words_bit_identical(cuda_device, B, T, act):
+    """Per-layer conv -> conv chain (encoder.py:69-70, postnet.py:54-61): the first layer records
+    its output's max words while writing it (avc_conv_bn_act_forward_ex), the second layer takes
+    them instead of scanning its input (forward range guard, weight-gradient max).  Outputs and
+    every gradient must be bit-identical to the same chain with the words withheld."""
+    g = torch.Generator().manual_seed(B * T + act)
+    C = 512
+    x = (torch.randn(T * B, C, generator=g)).to(cuda_device)
+    layers = []
+    for _ in range(2):
+        layers.append([(torch.randn(C, C, 5, generator=g) / np.sqrt(5 * C)).to(cuda_device),
+                       (torch.randn(C, generator=g) * 0.1).to(cuda_device),
+                       (1 + 0.1 * torch.randn(C, generator=g)).to(cuda_device),
+                       (0.1 * torch.randn(C, generator=g)).to(cuda_device)])
+    dy = torch.randn(T * B, C, generator=g).to(cuda_device)
+
+    def run(carry):
+        ps = [[t.clone().requires_grad_(True) for t in lay] for lay in layers]
+        h = x
+        for i, (w, b, gm, bt) in enumerate(ps):
+            if i > 0 and not carry:
+                h = h.view_as(h)  # a new tensor object: the recorded words are not found
+                assert ops._amax_of(h) is None
+            elif i > 0:
+                assert ops._amax_of(h) is not None
+            rm, rv = torch.zeros(C, device=cuda_device), torch.ones(C, device=cuda_device)
+            h = ops.ConvBNAct.apply(h, w, b, gm, bt, rm, rv, True, 0.1, 1e-5, act, None, T, B)
+        (h * dy).sum().backward()
+        return h.detach(), [t.grad for lay in ps for t in lay]
+
+    ya, ga = run(True)
+    yb, gb = run(False)
+    assert torch.equal(ya, yb)
+    for i, (a, b) in enumerate(zip(ga, gb)):
+        assert torch.equal(a, b), f"grad {i}: max|d| {(a - b).abs().max().item():.3e}"
