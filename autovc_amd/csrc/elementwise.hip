@@ -358,6 +358,128 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_cols_kernel(int M, int C, co
   }
 }
 
+// The two BN-backward passes with float4 streams: thread = (row phase, channel quad); the
+// P = 256 / (C/4) phases interleave the rows of the block's range and are combined through LDS
+// in a fixed order.  Needs C % 4 == 0, C <= 1024 and 16-byte aligned dout / y / dy.
+struct BnQuad {
+  float mu[4], is[4], g[4], bt[4];
+};
+__device__ __forceinline__ void bn_quad_load(BnQuad& k, int c0, const float* mean, const float* invstd,
+                                             const float* gamma, const float* beta) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    k.mu[e] = mean[c0 + e];
+    k.is[e] = invstd[c0 + e];
+    k.g[e] = gamma[c0 + e];
+    k.bt[e] = beta[c0 + e];
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(int M, int C, const float* __restrict__ dout,
+                                                             const float* __restrict__ y, const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, int act, int rows_per,
+                                                             float* __restrict__ part) {
+  __shared__ float4 red[2][256];
+  const int Q = C >> 2, P = 256 / Q;
+  const int ph = threadIdx.x / Q, q = threadIdx.x - ph * Q;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ph < P) {
+    BnQuad k;
+    bn_quad_load(k, 4 * q, mean, invstd, gamma, beta);
+    const int m0 = blockIdx.y * rows_per, m1 = min(M, m0 + rows_per);
+#pragma unroll 4
+    for (int m = m0 + ph; m < m1; m += P) {
+      const long i4 = (long)m * Q + q;
+      const float4 yv = reinterpret_cast<const float4*>(y)[i4];
+      const float4 dv = reinterpret_cast<const float4*>(dout)[i4];
+      const float yy[4] = {yv.x, yv.y, yv.z, yv.w}, dd[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = (yy[e] - k.mu[e]) * k.is[e];
+        const float dA = dd[e] * act_bwd(xh * k.g[e] + k.bt[e], act);
+        s1[e] += dA;
+        s2[e] += dA * xh;
+      }
+    }
+  }
+  red[0][threadIdx.x] = make_float4(s1[0], s1[1], s1[2], s1[3]);
+  red[1][threadIdx.x] = make_float4(s2[0], s2[1], s2[2], s2[3]);
+  __syncthreads();
+  if (ph != 0) return;
+  float4 a = red[0][q], b = red[1][q];
+  for (int p = 1; p < P; ++p) {
+    const float4 u = red[0][p * Q + q], v = red[1][p * Q + q];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+  }
+  reinterpret_cast<float4*>(part + ((long)blockIdx.y * 2 + 0) * C)[q] = a;
+  reinterpret_cast<float4*>(part + ((long)blockIdx.y * 2 + 1) * C)[q] = b;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(int M, int C, const float* __restrict__ dout,
+                                                            const float* __restrict__ y, const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, int act, int training,
+                                                            const float* __restrict__ sums, float inv_count,
+                                                            int rows_per, float* __restrict__ dy,
+                                                            float* __restrict__ part, unsigned* __restrict__ amax) {
+  __shared__ float4 red[256];
+  __shared__ float redm[4];
+  const int Q = C >> 2, P = 256 / Q;
+  const int ph = threadIdx.x / Q, q = threadIdx.x - ph * Q;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  float mx = 0.f;
+  if (ph < P) {
+    BnQuad k;
+    bn_quad_load(k, 4 * q, mean, invstd, gamma, beta);
+    float k1[4], k2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      k1[e] = training ? sums[4 * q + e] * inv_count : 0.f;
+      k2[e] = training ? sums[C + 4 * q + e] * inv_count : 0.f;
+    }
+    const int m0 = blockIdx.y * rows_per, m1 = min(M, m0 + rows_per);
+#pragma unroll 4
+    for (int m = m0 + ph; m < m1; m += P) {
+      const long i4 = (long)m * Q + q;
+      const float4 yv = reinterpret_cast<const float4*>(y)[i4];
+      const float4 dv = reinterpret_cast<const float4*>(dout)[i4];
+      const float yy[4] = {yv.x, yv.y, yv.z, yv.w}, dd[4] = {dv.x, dv.y, dv.z, dv.w};
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = (yy[e] - k.mu[e]) * k.is[e];
+        const float dA = dd[e] * act_bwd(xh * k.g[e] + k.bt[e], act);
+        o[e] = training ? k.g[e] * k.is[e] * (dA - k1[e] - xh * k2[e]) : k.g[e] * k.is[e] * dA;
+        cs[e] += o[e];
+        mx = fmaxf(mx, fabsf(o[e]));
+      }
+      reinterpret_cast<float4*>(dy)[i4] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if (part) {
+    red[threadIdx.x] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+    __syncthreads();
+    if (ph == 0) {
+      float4 a = red[q];
+      for (int p = 1; p < P; ++p) {
+        const float4 u = red[p * Q + q];
+        a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+      }
+      reinterpret_cast<float4*>(part + (long)blockIdx.y * C)[q] = a;
+    }
+  }
+  if (amax) {
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if ((threadIdx.x & 63) == 0) redm[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]))));
+  }
+}
+
 // ---- layout glue -------------------------------------------------------------------------
 __global__ void frames_from_mel_kernel(int T, int B, int cm, const float* __restrict__ x, int ce,
                                        const float* __restrict__ emb, float* __restrict__ out) {
@@ -707,25 +829,51 @@ int bn_apply(long M, int C, const float* y, const float* mean, const float* invs
   return AVC_OK;
 }
 
+namespace {
+// row blocks of the BN backward (a function of the shape only: callers size the bias partials
+// with bn_backward_rows): ~64 rows per block
+bool bn_vec_ok(int C, const float* dout, const float* y, const float* dy) {
+  return C % 4 == 0 && C <= 1024 && aligned16(dout) && aligned16(y) && aligned16(dy);
+}
+void bn_geometry(int M, int C, int& R, int& rows_per) {
+  if (C % 4 != 0 || C > 1024) {
+    colsum_geometry(M, C, R, rows_per);
+    return;
+  }
+  R = std::max(1, std::min(512, (M + 63) / 64));
+  rows_per = (M + R - 1) / R;
+  R = (M + rows_per - 1) / rows_per;
+}
+}  // namespace
+
 size_t bn_backward_scratch(int M, int C) {
   int R, rp;
-  colsum_geometry(M, C, R, rp);
+  bn_geometry(M, C, R, rp);
   return (size_t)R * 2 * C * sizeof(float) + 2 * C * sizeof(float) + 512;
 }
+
 
 int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* y,
                 const float* mean, const float* invstd, const float* gamma, const float* beta,
                 int act, int training, float* d_gamma, float* d_beta, int accumulate, float* dy,
                 hipStream_t s, float* dy_colpart, unsigned* dy_amax) {
+  const bool vec = bn_vec_ok(C, dout, y, dy);
   int R, rp;
-  colsum_geometry(M, C, R, rp);
+  bn_geometry(M, C, R, rp);
   Scratch sc(ctx);
   AVC_TAKE(part, float, (size_t)R * 2 * C, sc);
   AVC_TAKE(sums, float, (size_t)2 * C, sc);
-  bn_bwd_reduce_kernel<<<dim3((C + 255) / 256, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
-                                                                beta, act, rp, part);
+  if (vec) {
+    bn_bwd_reduce4_kernel<<<dim3(1, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta, act, rp, part);
+  } else {
+    bn_bwd_reduce_kernel<<<dim3((C + 255) / 256, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
+                                                                  beta, act, rp, part);
+  }
   bn_bwd_final_kernel<<<(C + 63) / 64, 1024, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate, dy_amax);
-  if (dy_colpart || dy_amax) {
+  if (vec) {
+    bn_bwd_apply4_kernel<<<dim3(1, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta, act, training, sums,
+                                                    1.f / (float)M, rp, dy, dy_colpart, dy_amax);
+  } else if (dy_colpart || dy_amax) {
     bn_bwd_apply_cols_kernel<<<dim3((C + 255) / 256, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta,
                                                                       act, training, sums, 1.f / (float)M, rp, dy,
                                                                       dy_colpart, dy_amax);
@@ -740,7 +888,7 @@ int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* 
 
 int bn_backward_rows(int M, int C) {
   int R, rp;
-  colsum_geometry(M, C, R, rp);
+  bn_geometry(M, C, R, rp);
   return R;
 }
 
