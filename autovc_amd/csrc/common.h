@@ -225,6 +225,14 @@ T* prep_or_scratch(avc_context* ctx, Scratch& sc, int kind, const void* key0, co
   return sc.template take<T>(count);
 }
 
+// running max |x| as float bits (atomicMax of non-negative floats), skipped when the word
+// already holds at least v: within a launch the word only grows, so a stale read costs at most
+// an unneeded atomic -- thousands of blocks otherwise serialise on one L2 line
+__device__ __forceinline__ void amax_update(unsigned* w, float v) {
+  const unsigned u = __float_as_uint(v);
+  if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < u) atomicMax(w, u);
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 // Gate nonlinearities of the recurrences' step epilogues (the dependent chain of every time step):
 // hardware exp (v_exp_f32) and reciprocal (v_rcp_f32), ~1e-7 relative of the libm forms, a few

@@ -165,8 +165,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
     __syncthreads();
     if (threadIdx.x == 0) {
       const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      atomicMax(amax_out, __float_as_uint(m));
-      atomicMax(amax_out + 1, __float_as_uint(fmaxf(m, 16384.f)));
+      amax_update(amax_out, m);
+      amax_update(amax_out + 1, fmaxf(m, 16384.f));
     }
   }
 }
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_cols_kernel(int M, int C, co
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
     __syncthreads();
-    if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    if (threadIdx.x == 0) amax_update(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
   }
 }
 
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(int M, int C, const 
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     if ((threadIdx.x & 63) == 0) redm[threadIdx.x >> 6] = mx;
     __syncthreads();
-    if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]))));
+    if (threadIdx.x == 0) amax_update(amax, fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3])));
   }
 }
 

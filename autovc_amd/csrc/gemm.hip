@@ -678,7 +678,7 @@ __global__ __launch_bounds__(256) void absmax_vec_kernel(const float4* __restric
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  if (threadIdx.x == 0) amax_update(out, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
 __global__ __launch_bounds__(256) void absmax_rows_kernel(const float* __restrict__ src, long rows, int cols,
@@ -703,7 +703,7 @@ __global__ __launch_bounds__(256) void absmax_rows_kernel(const float* __restric
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  if (threadIdx.x == 0) amax_update(out, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
 inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t s) {
