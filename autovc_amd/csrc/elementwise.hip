@@ -176,6 +176,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
 // same arithmetic as bn_apply_kernel, same hi / lo split (lo scaled by 2^11); padding rows and
 // channels (to 32-row tiles and 32-deep K) are written as zeros.
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+constexpr int kBnFragLdsC = 1024;
 __global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int nkc, long ntile,
                                                             const float* __restrict__ y,
                                                             const float* __restrict__ mean,
@@ -188,14 +189,28 @@ __global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int n
                                                             unsigned* __restrict__ range_flag) {
   const int G8 = nkc * 2;
   const long total = ntile * 32 * G8;
+  // per-channel scale / shift formed once per workgroup in LDS (same expressions as
+  // bn_apply_kernel), so the element loop issues two float4 loads instead of 32 parameter loads
+  __shared__ float s_sc[kBnFragLdsC], s_sh[kBnFragLdsC];
+  const bool lds = C <= kBnFragLdsC;
+  if (lds) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const float sc = invstd[c] * gamma[c];
+      s_sc[c] = sc;
+      s_sh[c] = beta[c] - mean[c] * sc;
+    }
+    __syncthreads();
+  }
+  const unsigned q4 = (unsigned)(G8 >> 2);
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
     const int gq = (int)(idx & 3);
     const long rest = idx >> 2;
     const int rr = (int)(rest & 31);
     const long tq = rest >> 5;
-    const long t = tq / (G8 >> 2);
-    const int quad = (int)(tq - t * (G8 >> 2));
+    // 32-bit division where the tile-quad index fits (always, below 2^32 quads)
+    const long t = tq < 0xffffffffL ? (long)((unsigned)tq / q4) : tq / (long)q4;
+    const int quad = (int)(tq - t * (long)q4);
     const long r = t * 32 + rr;
     const int g8 = quad * 4 + gq, k0 = 8 * g8;
     float o[8];
@@ -203,12 +218,17 @@ __global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int n
       const float4* q = reinterpret_cast<const float4*>(y + r * C + k0);
       const float4 a = q[0], b = q[1];
       o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+      if (lds) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = k0 + e;
-        const float sc = invstd[c] * gamma[c];
-        const float sh = beta[c] - mean[c] * sc;
-        o[e] = act_fwd(o[e] * sc + sh, act);
+        for (int e = 0; e < 8; ++e) o[e] = act_fwd(o[e] * s_sc[k0 + e] + s_sh[k0 + e], act);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = k0 + e;
+          const float sc = invstd[c] * gamma[c];
+          const float sh = beta[c] - mean[c] * sc;
+          o[e] = act_fwd(o[e] * sc + sh, act);
+        }
       }
       if (residual) {
         const float4* rq = reinterpret_cast<const float4*>(residual + r * C + k0);

@@ -616,13 +616,15 @@ __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restri
       const long rest = idx >> 2;
       const int rr = (int)(rest & 31);
       const long tq = rest >> 5;  // tile * (G8/4) + quad
-      const long t = tq / (G8 >> 2);
-      const int quad = (int)(tq - t * (G8 >> 2));
+      // 32-bit divisions whenever the indices fit (a 64-bit division is a long software sequence)
+      const unsigned q4 = (unsigned)(G8 >> 2);
+      const long t = tq < 0xffffffffL ? (long)((unsigned)tq / q4) : tq / (long)q4;
+      const int quad = (int)(tq - t * (long)q4);
       r = t * 32 + rr;
       g8 = quad * 4 + gq;
     } else {        // transposed source (column stride 1): consecutive threads take consecutive rows
       const long rows = (long)ntile * 32;
-      g8 = (int)(idx / rows);
+      g8 = idx < 0xffffffffL && rows < 0xffffffffL ? (int)((unsigned)idx / (unsigned)rows) : (int)(idx / rows);
       r = idx - (long)g8 * rows;
     }
     float v[8];
