@@ -199,8 +199,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TRY(cba(P_POST + 12, 512, 512, bb, ba, AVC_ACT_TANH, nullptr, fb, fa));
   AVC_TRY(cba(P_POST + 18, 512, 512, ba, bb, AVC_ACT_TANH, nullptr, fa, fb));
   AVC_TRY(cba(P_POST + 24, 512, 80, bb, postf, AVC_ACT_NONE, melf, fb));
-  AVC_TRY(mel_from_frames(T, B, 80, melf, mel, s));
-  AVC_TRY(mel_from_frames(T, B, 80, postf, mel_post, s));
+  AVC_TRY(mel_from_frames(T, B, 80, melf, mel, s, postf, mel_post));  // both outputs, one launch
   return AVC_OK;
 }
 

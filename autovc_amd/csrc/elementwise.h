@@ -31,7 +31,8 @@ int frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* e
                     hipStream_t s);
 int frames_from_mel_backward(int T, int B, int cm, int ce, const float* df, int ld, float* dx,
                              float* demb, int accumulate, hipStream_t s);
-int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s);
+int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s,
+                    const float* fr1 = nullptr, float* mel1 = nullptr);
 int codes_from_encoder(int T, int B, const float* enc, float* codes, hipStream_t s);
 int codes_from_encoder_backward(int T, int B, const float* dcodes, float* denc, int accumulate,
                                 hipStream_t s);

@@ -507,9 +507,17 @@ __global__ void frames_from_mel_kernel(int T, int B, int cm, const float* __rest
   const long total = (long)T * B * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long r = i / C;
-    const int b = (int)(r % B), t = (int)(r / B);
+    int c, b, t;
+    if (total <= 0x7fffffffL) {  // 32-bit divisions (a 64-bit one is a long software sequence)
+      const unsigned u = (unsigned)i, r = u / (unsigned)C;
+      c = (int)(u - r * (unsigned)C);
+      t = (int)(r / (unsigned)B);
+      b = (int)(r - (unsigned)t * (unsigned)B);
+    } else {
+      c = (int)(i % C);
+      const long r = i / C;
+      b = (int)(r % B), t = (int)(r / B);
+    }
     out[i] = c < cm ? x[((long)b * cm + c) * T + t] : emb[(long)b * ce + (c - cm)];
   }
 }
@@ -538,14 +546,25 @@ __global__ void emb_grad_kernel(int T, int B, int cm, int ce, const float* __res
   demb[i] = accumulate ? demb[i] + (float)s : (float)s;
 }
 
+// grid y = 1 or 2: a second (frames, mel) pair in the same launch (the Generator's mel and mel_post)
 __global__ void mel_from_frames_kernel(int T, int B, int cm, const float* __restrict__ fr,
-                                       float* __restrict__ mel) {
+                                       float* __restrict__ mel, const float* __restrict__ fr1,
+                                       float* __restrict__ mel1) {
+  if (blockIdx.y) fr = fr1, mel = mel1;
   const long total = (long)B * cm * T;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int t = (int)(i % T);
-    const long bc = i / T;
-    const int c = (int)(bc % cm), b = (int)(bc / cm);
+    int t, c, b;
+    if (total <= 0x7fffffffL) {  // 32-bit divisions
+      const unsigned u = (unsigned)i, bc = u / (unsigned)T;
+      t = (int)(u - bc * (unsigned)T);
+      b = (int)(bc / (unsigned)cm);
+      c = (int)(bc - (unsigned)b * (unsigned)cm);
+    } else {
+      t = (int)(i % T);
+      const long bc = i / T;
+      c = (int)(bc % cm), b = (int)(bc / cm);
+    }
     mel[i] = fr[((long)t * B + b) * cm + c];
   }
 }
@@ -574,9 +593,17 @@ __global__ void decoder_input_kernel(int T, int B, const float* __restrict__ enc
   const long total = (long)T * B * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const long r = i / C;
-    const int b = (int)(r % B), t = (int)(r / B);
+    int c, b, t;
+    if (total <= 0x7fffffffL) {  // 32-bit divisions
+      const unsigned u = (unsigned)i, r = u / (unsigned)C;
+      c = (int)(u - r * (unsigned)C);
+      t = (int)(r / (unsigned)B);
+      b = (int)(r - (unsigned)t * (unsigned)B);
+    } else {
+      c = (int)(i % C);
+      const long r = i / C;
+      b = (int)(r % B), t = (int)(r / B);
+    }
     float v;
     if (c < 32) {
       const int blk = min(t / 32, nA - 1);
@@ -985,8 +1012,9 @@ unsigned* zeroed_words(avc_context* ctx, int n, hipStream_t s) {
   return p;
 }
 
-int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s) {
-  mel_from_frames_kernel<<<ew_blocks((long)B * cm * T), 256, 0, s>>>(T, B, cm, fr, mel);
+int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s, const float* fr1,
+                    float* mel1) {
+  mel_from_frames_kernel<<<dim3(ew_blocks((long)B * cm * T), fr1 ? 2 : 1), 256, 0, s>>>(T, B, cm, fr, mel, fr1, mel1);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

@@ -1267,7 +1267,7 @@ __global__ void guard_init_kernel(unsigned* w, int n) {
 // The same guard word in ONE launch (no initialisation kernel): every block writes its maximum
 // to partial[blockIdx], and the last block to take a ticket (atomicInc wraps the per-context
 // ticket back to 0, so it is ready for the next scan) writes max(all, 2^14) to *out.
-constexpr int kGuardBlocks = 256;
+constexpr int kGuardBlocks = 1024;  // partial words of the guard scan (one per workgroup)
 __global__ __launch_bounds__(256) void guard_scan_kernel(const float* __restrict__ src, long rows, int cols,
                                                          long ld, float* __restrict__ partial,
                                                          unsigned* __restrict__ ticket, unsigned* __restrict__ out) {
@@ -1277,7 +1277,17 @@ __global__ __launch_bounds__(256) void guard_scan_kernel(const float* __restrict
   if (ld == cols && (reinterpret_cast<uintptr_t>(src) & 15) == 0 && (cols & 3) == 0) {
     const long n4 = rows * cols / 4;
     const float4* s4 = reinterpret_cast<const float4*>(src);
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const long stride = (long)gridDim.x * 256;
+    long i = blockIdx.x * 256L + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {  // four loads in flight
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = s4[i + u * stride];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+    }
+    for (; i < n4; i += stride) {
       const float4 v = s4[i];
       m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
