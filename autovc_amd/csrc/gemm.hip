@@ -1267,7 +1267,7 @@ __global__ void guard_init_kernel(unsigned* w, int n) {
 // The same guard word in ONE launch (no initialisation kernel): every block writes its maximum
 // to partial[blockIdx], and the last block to take a ticket (atomicInc wraps the per-context
 // ticket back to 0, so it is ready for the next scan) writes max(all, 2^14) to *out.
-constexpr int kGuardBlocks = 1024;  // partial words of the guard scan (one per workgroup)
+constexpr int kGuardBlocks = 256;  // partial words of the guard scan (one per workgroup; each takes a ticket atomic, 1024 measured slower)
 __global__ __launch_bounds__(256) void guard_scan_kernel(const float* __restrict__ src, long rows, int cols,
                                                          long ld, float* __restrict__ partial,
                                                          unsigned* __restrict__ ticket, unsigned* __restrict__ out) {
