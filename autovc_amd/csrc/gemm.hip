@@ -708,14 +708,19 @@ __global__ __launch_bounds__(256) void absmax_rows_kernel(const float* __restric
   if (threadIdx.x == 0) amax_update(out, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
+// Every workgroup of a max scan ends in one atomic max on the same word, and workgroups that finish
+// together all take it (the running max has not risen yet): the grid is capped at kMaxScanBlocks
+// (2048 workgroups made a 64 MB scan take ~37 us, mostly serialised atomics); the loop keeps four
+// loads in flight per thread instead.
+constexpr long kMaxScanBlocks = 256;
 inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t s) {
   if (ld == cols && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
     const long n = rows * cols, n4 = n / 4;
-    absmax_vec_kernel<<<(int)std::max<long>(1, std::min<long>((n4 + 1023) / 1024, 2048)), 256, 0, s>>>(
+    absmax_vec_kernel<<<(int)std::max<long>(1, std::min<long>((n4 + 1023) / 1024, kMaxScanBlocks)), 256, 0, s>>>(
         reinterpret_cast<const float4*>(src), n4, src + 4 * n4, (int)(n - 4 * n4), out);
   } else {
     const long blocks = (cols % 4 == 0 && ld % 4 == 0) ? (rows * (cols / 4) + 1023) / 1024 : rows;
-    absmax_rows_kernel<<<(int)std::max<long>(1, std::min<long>(blocks, 2048)), 256, 0, s>>>(src, rows, (int)cols,
+    absmax_rows_kernel<<<(int)std::max<long>(1, std::min<long>(blocks, kMaxScanBlocks)), 256, 0, s>>>(src, rows, (int)cols,
                                                                                             ld, out);
   }
 }
