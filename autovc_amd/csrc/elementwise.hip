@@ -139,24 +139,38 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
     sc[e] = invstd[c] * gamma[c];
     sh[e] = beta[c] - mean[c] * sc[e];
   }
-  for (long r = r0; r < M; r += rows_per_pass) {
-    const long i4 = r * Q + q;
-    const float4 v = reinterpret_cast<const float4*>(y)[i4];
-    float o[4] = {v.x, v.y, v.z, v.w};
+  // kRows rows per pass, all loads issued before any store (out may alias y: every element is
+  // read and written by the same thread, so loading ahead is safe), so the loads overlap
+  constexpr int kRows = 4;
+  for (long rb = r0; rb < M; rb += kRows * rows_per_pass) {
+    float4 v[kRows], rr[kRows];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = act_fwd(o[e] * sc[e] + sh[e], act);
-    if (residual) {
-      const float4 rr = reinterpret_cast<const float4*>(residual)[i4];
-      o[0] += rr.x; o[1] += rr.y; o[2] += rr.z; o[3] += rr.w;
+    for (int u = 0; u < kRows; ++u) {
+      const long r = rb + u * rows_per_pass;
+      if (r < M) {
+        v[u] = reinterpret_cast<const float4*>(y)[r * Q + q];
+        if (residual) rr[u] = reinterpret_cast<const float4*>(residual)[r * Q + q];
+      }
     }
-    if (range_flag) {  // the consumer contraction skips its range scan (see bn_apply_frag_kernel)
-      bool over = false;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) over |= fabsf(o[e]) >= 65504.f && fabsf(o[e]) < __builtin_inff();
-      if (over) __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int u = 0; u < kRows; ++u) {
+      const long r = rb + u * rows_per_pass;
+      if (r >= M) break;
+      float o[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = act_fwd(o[e] * sc[e] + sh[e], act);
+      if (residual) {
+        o[0] += rr[u].x; o[1] += rr[u].y; o[2] += rr[u].z; o[3] += rr[u].w;
+      }
+      if (range_flag) {  // the consumer contraction skips its range scan (see bn_apply_frag_kernel)
+        bool over = false;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) over |= fabsf(o[e]) >= 65504.f && fabsf(o[e]) < __builtin_inff();
+        if (over) __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      reinterpret_cast<float4*>(out)[r * Q + q] = make_float4(o[0], o[1], o[2], o[3]);
+      if (amax_out) amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
     }
-    reinterpret_cast<float4*>(out)[i4] = make_float4(o[0], o[1], o[2], o[3]);
-    if (amax_out) amax = fmaxf(amax, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
   }
   if (amax_out) {
     __shared__ float red[4];
@@ -868,7 +882,8 @@ int bn_apply(long M, int C, const float* y, const float* mean, const float* invs
   }
   // ~4 float4 per thread; every thread owns one channel quad for the whole launch
   const long Q = C / 4;
-  const long threads = std::max<long>(256, std::min<long>(M * Q / 4, 2048L * 256));
+  // with max words every workgroup ends in an atomic max on one word: fewer, longer workgroups
+  const long threads = std::max<long>(256, std::min<long>(M * Q / 4, (amax_out ? 512L : 2048L) * 256));
   const long blocks = (threads + 255) / 256;
   bn_apply_kernel<<<(int)blocks, 256, 0, s>>>(M, C, y, mean, invstd, gamma, beta, act, residual, out, range_flag,
                                               amax_out);
