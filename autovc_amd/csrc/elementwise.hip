@@ -49,8 +49,16 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(int R, int N, const 
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + cl;
   double s = 0.0;
-  if (n < N)
-    for (int r = grp; r < R; r += 16) s += part[(long)r * N + n];
+  if (n < N) {
+    // four partial rows loaded ahead of their adds (same addition order: bit-identical sums)
+    int r = grp;
+    for (; r + 48 < R; r += 64) {
+      const float a = part[(long)r * N + n], b = part[(long)(r + 16) * N + n];
+      const float c = part[(long)(r + 32) * N + n], e = part[(long)(r + 48) * N + n];
+      s += a; s += b; s += c; s += e;
+    }
+    for (; r < R; r += 16) s += part[(long)r * N + n];
+  }
   red[grp][cl] = s;
   __syncthreads();
   if (grp != 0 || n >= N) return;
