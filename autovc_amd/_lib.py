@@ -52,6 +52,7 @@ _SIGS = {
     "avc_decoder_input": [_I, _I, _P, _I, _P, _P, _P],
     "avc_decoder_input_backward": [_I, _I, _I, _P, _P, _I, _P],
     "avc_overlap_average": [_I, _I, _I, _I, _P, _P, _P],
+    "avc_overlap_average_backward": [_I, _I, _I, _I, _P, _P, _P, _P],
     "avc_loss_forward": [_P, _I, _Z, _P, _P, _P, _I, _P],
     "avc_loss_backward": [_I, _Z, _P, _P, _P, _P, _P, _I, _P],
     "avc_clip_adam_ema": [_P, _Z, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, ctypes.c_double, _P, _P],
@@ -72,6 +73,12 @@ _SIGS = {
     "avc_bptt_persist": [_I],
     "avc_debug_bptt_diag": [_I],
     "avc_debug_persist_inject": [_I],
+    "avc_persist_notify": [_P, _P],
+    "avc_persist_launches": [_P, ctypes.POINTER(ctypes.c_long)],
+    "avc_bptt_persist_eligible": [_I, _I, _I],
+    "avc_debug_persist_spin_limit": [ctypes.c_uint],
+    "avc_debug_hog": [_P, _I, _I, ctypes.c_long, _P],
+    "avc_debug_hog_resident": [_P, ctypes.POINTER(_I)],
     "avc_graph_mode": [_I],
     "avc_timing_reset": [],
     "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -155,6 +162,13 @@ def context(device: torch.device) -> int:
 
 def stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def persist_launches(device: torch.device) -> int:
+    """Persistent launches enqueued on the device's context so far (avc_persist_launches)."""
+    n = ctypes.c_long()
+    call("avc_persist_launches", context(device), ctypes.byref(n))
+    return n.value
 
 
 def ptr(t) -> int | None:

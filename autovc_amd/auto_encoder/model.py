@@ -385,9 +385,11 @@ class AutoEncoder(nn.Module):
         self._check(X, None, "X")
         # parameter gradients are accumulated in place into the flat gradient by the layers'
         # backward kernels (ops.GradSink), not returned and added by autograd
-        red = self._grad_buckets() if dp.world() > 1 else None
+        red = self._grad_buckets() if (dp.world() > 1 or self.grad_comm is not None) else None
+        sink = None
         if self.inplace_grads:
-            ops.set_grad_sink(ops.GradSink(notify=red.param_ready if red is not None else None))
+            sink = ops.GradSink(notify=red.param_ready if red is not None else None, comm=red)
+            ops.set_grad_sink(sink)
         try:
             out_decoder, out_postnet, content_codes = self._forward_layers(X, c_org, c_org)
             loss = self._loss(X=X, c_org=c_org, out_decoder=out_decoder, out_postnet=out_postnet,
@@ -395,8 +397,9 @@ class AutoEncoder(nn.Module):
             self.optimiser.zero_grad()
             if red is not None:
                 # data parallel: bucketed RCCL all-reduce of the flat gradient, issued while
-                # backward still runs (dp.GradBuckets), then /world
-                with red.armed():
+                # backward still runs but never beside a persistent launch's dispatch
+                # (dp.GradBuckets, co-residency rule), then /world
+                with red.armed(sink.recurrences if sink is not None else 0):
                     loss.backward()
                 red.finish()
             else:
@@ -404,18 +407,25 @@ class AutoEncoder(nn.Module):
         finally:
             ops.set_grad_sink(None)
         self.optimiser.step(max_norm=max_norm, ema=self.avg_params, ema_decay=ema_decay)
+        self._last_out_postnet = out_postnet.detach()  # for _log's conversion figure
         return loss.detach(), self.optimiser.last_grad_norm
 
     def _grad_buckets(self):
         red = getattr(self, "_reducer", None)
-        if red is None or red.flat is not self._flat_grad:
+        if red is None or red.flat is not self._flat_grad or red.comm_key != self.grad_comm:
             if red is not None:
                 red.remove()
-            red = self._reducer = dp.GradBuckets(self.parameters(), self._flat_grad, self.bucket_bytes)
+            kw = dict(self.grad_comm or {})
+            red = self._reducer = dp.GradBuckets(self.parameters(), self._flat_grad, self.bucket_bytes, **kw)
+            red.comm_key = self.grad_comm
         return red
 
     bucket_bytes = 16 << 20  # data-parallel all-reduce bucket (≈7 buckets over the 113.7 MB gradient)
     inplace_grads = True     # train_step: layers accumulate parameter gradients in place (ops.GradSink)
+    # keyword arguments of dp.GradBuckets (all_reduce, world_size, co_residency) for tests that drive
+    # the bucketed exchange with a stand-in collective; None = torch.distributed when world > 1
+    grad_comm = None
+    _last_out_postnet = None  # train_step's postnet output, for _log's conversion figure
 
     def learn(self, trainloader, n_epochs=AutoEncoderParams["learn"]["n_epochs"],
               log_freq=AutoEncoderParams["learn"]["log_freq"],
@@ -458,7 +468,7 @@ class AutoEncoder(nn.Module):
                     print(f"\rstep {self.logging['step']}/{N_iterations} | loss {float(loss):.5f}", end="")
                 if (self.logging["step"] % log_freq == 0 or self.logging["step"] == N_iterations) \
                         and wandb_run is not None:
-                    self._log(wandb_run, X, None)
+                    self._log(wandb_run, X, self._last_out_postnet)
             if self.logging["epoch"] % save_freq == 0 or self.logging["epoch"] == n_epochs:
                 self.save(model_name, save_dir, wandb_run)
             if voice_converter is not None and dp.rank() == 0:
@@ -473,9 +483,15 @@ class AutoEncoder(nn.Module):
             print("\n")
 
     def _log(self, wandb_run, X, out_postnet):
+        """model.py:363-376: the running loss, then the conversion figure of the batch's first
+        utterance (input vs postnet output of the step just taken)."""
         wandb_run.log({"loss": float(self.logging["running_loss"]) / self.logging["log_steps"],
                        "epoch": self.logging["epoch"], "batch": self.logging["batch"],
                        "step": self.logging["step"], "learning rate": self.logging["lr"]})
+        if out_postnet is not None:
+            import matplotlib.pyplot as plt  # only when logging to wandb, like the reference's use
+            wandb_run.log({"Conversion": self.plot_conversion(X[0], out_postnet[0])})
+            plt.close()
         self.logging["running_loss"] = 0.0
         self.logging["log_steps"] = 0
 
@@ -485,7 +501,8 @@ class AutoEncoder(nn.Module):
         c_trg = c_trg.expand(batch.size(0), -1)
         _, output, _ = self(batch, c_org, c_trg)
         N = batch.size(-1)
-        return ops.overlap_average(output.detach(), int(N * (1 - overlap)))
+        # differentiable like the reference's pad + stack + nanmean (the graph is kept)
+        return ops.overlap_average(output, int(N * (1 - overlap)))
 
     def plot_conversion(self, original, converted):
         import matplotlib.pyplot as plt

@@ -435,6 +435,12 @@ int avc_overlap_average(int M, int C, int N, int step, const float* frames, floa
   return overlap_average(M, C, N, step, frames, out, S(stream));
 }
 
+int avc_overlap_average_backward(int M, int C, int N, int step, const float* frames, const float* d_out,
+                                 float* d_frames, void* stream) {
+  AVC_CHECK_ARG(frames && d_out && d_frames, "NULL pointer");
+  return overlap_average_backward(M, C, N, step, frames, d_out, d_frames, S(stream));
+}
+
 int avc_loss_forward(avc_context* ctx, int kind, size_t n, const float* a, const float* b,
                      float* loss_out, int accumulate, void* stream) {
   AVC_CHECK_ARG(ctx && a && b && loss_out, "NULL pointer");

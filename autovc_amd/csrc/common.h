@@ -126,6 +126,10 @@ struct avc_context {
   bool track_ranges = false;
   std::vector<const void*> range_ok;
   unsigned fail_seen = 0;         // value of *fail_host already reported to the caller
+  // co-residency hooks (lstm_persist.hip: persist_dispatch): an event recorded right after every
+  // persistent launch (avc_persist_notify), and the number of persistent launches so far
+  void* persist_event = nullptr;
+  long persist_launches = 0;
   // pool of device words handed out already zeroed (max-scan accumulators of gradient products):
   // one zeroing launch per kZeroPool words instead of one per product (zeroed_words)
   unsigned* zpool = nullptr;

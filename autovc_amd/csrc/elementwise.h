@@ -41,6 +41,8 @@ int decoder_input(int T, int B, const float* enc, int ce, const float* ctrg, flo
 int decoder_input_backward(int T, int B, int ce, const float* dd, float* denc, int accumulate,
                            hipStream_t s);
 int overlap_average(int M, int C, int N, int step, const float* fr, float* out, hipStream_t s);
+int overlap_average_backward(int M, int C, int N, int step, const float* fr, const float* dout, float* dfr,
+                             hipStream_t s);
 size_t loss_scratch();
 int loss_forward(avc_context* ctx, int kind, size_t n, const float* a, const float* b, float* out,
                  int accumulate, hipStream_t s);

@@ -695,6 +695,33 @@ __global__ void overlap_average_kernel(int M, int C, int N, int step, const floa
   }
 }
 
+// d fr[i][c][k] = d_out[c][i*step + k] / (non-NaN slices covering that column), 0 for a NaN
+// entry: torch's nanmean backward (nansum / count) for the paste of model.py:428-437
+__global__ void overlap_average_backward_kernel(int M, int C, int N, int step, const float* __restrict__ fr,
+                                                const float* __restrict__ dout, float* __restrict__ dfr) {
+  const int L = (M - 1) * step + N;
+  const long total = (long)M * C * N;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int i = (int)(idx / ((long)C * N));
+    const int c = (int)((idx / N) % C);
+    const int tau = i * step + (int)(idx % N);
+    const float v = fr[idx];
+    if (v != v) {
+      dfr[idx] = 0.f;
+      continue;
+    }
+    int cnt = 0;
+    for (int j = 0; j < M; ++j) {
+      const int k = tau - j * step;
+      if (k < 0 || k >= N) continue;
+      const float w = fr[((long)j * C + c) * N + k];
+      if (w == w) ++cnt;
+    }
+    dfr[idx] = dout[(long)c * L + tau] / (float)cnt;
+  }
+}
+
 // ---- losses ------------------------------------------------------------------------------
 __global__ void loss_partial_kernel(int kind, long n, const float* __restrict__ a,
                                     const float* __restrict__ b, double* __restrict__ part) {
@@ -790,11 +817,15 @@ __global__ __launch_bounds__(256) void clip_coef_kernel(int nparts, const double
     if (c > 1.f) c = 1.f;
   }
   coef[0] = c;
+  // a non-finite norm (a persistent recurrence that gave up writes NaN; in data-parallel training
+  // the NaN reaches every rank through the all-reduce): the update below is skipped
+  coef[1] = isfinite(norm) ? 0.f : 1.f;
 }
 
 struct AdamArgs {
   float c, lr, b1, b2, eps, wd, step_size, bc2_sqrt, ema_decay, ema_keep;
   int clip;
+  int guard;  // coef[1] holds the skip flag of clip_coef_kernel
 };
 
 // one element of the fused clip + Adam + EMA update (torch.optim.Adam's foreach arithmetic)
@@ -817,6 +848,7 @@ __global__ __launch_bounds__(256) void adam_ema_kernel(long n, long n4, float* _
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        float* __restrict__ ema, const float* __restrict__ coef,
                                                        AdamArgs a) {
+  if (a.guard && coef[1] != 0.f) return;  // non-finite gradient norm: parameters, moments, EMA kept
   a.c = a.clip ? coef[0] : 1.f;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -1086,6 +1118,15 @@ int overlap_average(int M, int C, int N, int step, const float* fr, float* out, 
   return AVC_OK;
 }
 
+int overlap_average_backward(int M, int C, int N, int step, const float* fr, const float* dout, float* dfr,
+                             hipStream_t s) {
+  AVC_CHECK_ARG(M >= 1 && C >= 1 && N >= 1 && step >= 0, "overlap_average_backward: bad shape");
+  const long total = (long)M * C * N;
+  overlap_average_backward_kernel<<<ew_blocks(total), 256, 0, s>>>(M, C, N, step, fr, dout, dfr);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
 size_t loss_scratch() { return 1024 * sizeof(double) + 256; }
 
 int loss_forward(avc_context* ctx, int kind, size_t n, const float* a, const float* b,
@@ -1134,6 +1175,7 @@ int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, floa
   a.ema_decay = (float)ema_decay;
   a.ema_keep = (float)(1.0 - ema_decay);
   a.clip = max_norm > 0.f ? 1 : 0;
+  a.guard = need_norm ? 1 : 0;
   const bool al = aligned16(p) && aligned16(g) && aligned16(m) && aligned16(v) && (!ema || aligned16(ema));
   const long n4 = al ? (long)n / 4 : 0;
   adam_ema_kernel<<<ew_blocks(std::max<long>(n4, (long)n - 4 * n4)), 256, 0, s>>>((long)n, n4, p, g, m, v, ema, coef, a);

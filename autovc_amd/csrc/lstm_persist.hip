@@ -53,7 +53,15 @@
 // Arithmetic is identical to lstm_split_step_kernel's NC = 4 tiles: the same 3xf16 products
 // (hi.lo, lo.hi, hi.hi per 32-deep chunk, in that order), the same K split over 4 waves and
 // the same fixed-order LDS reduction, so the two paths agree bit for bit.
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "kernels.h"
@@ -799,27 +807,104 @@ int persist_capacity(int H, int RT) {
 
 int g_persist_coop = 0;          // avc_lstm_persist_coop()
 int g_persist_inject = 0;        // avc_debug_persist_inject(): launches left that give up at once
+unsigned g_spin_limit = kSpinLimit;  // avc_debug_persist_spin_limit()
+
+// ---- Co-residency of persistent launches ---------------------------------------
+// A persistent launch needs every workgroup resident at once; the occupancy check above only
+// sees an idle device.  Two things can hold CUs while a persistent grid dispatches:
+//  * kernels of this process's other streams that wait on something outside the GPU: an RCCL
+//    collective waiting for a lagging peer rank.  The host layer keeps them out (dp.GradBuckets:
+//    no collective is in flight while a persistent launch dispatches; the buckets that become
+//    ready meanwhile are issued behind the event avc_persist_notify records right after the
+//    launch, so they run beside the rest of the backward, never beside a dispatch);
+//  * persistent launches of another process on the same GPU (several ranks per device: the
+//    world-2 DP test on a one-GPU box).  AVC_PERSIST_XPROC_LOCK=<file> serialises them: the
+//    launching thread holds an exclusive flock on the file from before the launch until a host
+//    function enqueued behind it runs (the kernel has finished).  Nothing is waited on while the
+//    lock is held except this process's own queued work, so the lock cannot deadlock.
+struct XprocLock {
+  std::mutex m;
+  int fd = -2;    // -2: environment not read yet; -1: off
+  int held = 0;   // launches enqueued and not yet finished
+};
+XprocLock g_xl;
+
+bool xproc_lock_on() {
+  std::lock_guard<std::mutex> g(g_xl.m);
+  if (g_xl.fd == -2) {
+    const char* path = getenv("AVC_PERSIST_XPROC_LOCK");
+    g_xl.fd = (path && *path) ? open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0666) : -1;
+  }
+  return g_xl.fd >= 0;
+}
+
+int xproc_acquire() {
+  std::lock_guard<std::mutex> g(g_xl.m);
+  if (g_xl.held == 0) {
+    int rc;
+    do rc = flock(g_xl.fd, LOCK_EX); while (rc != 0 && errno == EINTR);
+    if (rc != 0) {
+      set_error(std::string("AVC_PERSIST_XPROC_LOCK: flock failed: ") + strerror(errno));
+      return AVC_ERR_HIP;
+    }
+  }
+  ++g_xl.held;
+  return AVC_OK;
+}
+
+void xproc_release() {
+  std::lock_guard<std::mutex> g(g_xl.m);
+  if (g_xl.held > 0 && --g_xl.held == 0) (void)flock(g_xl.fd, LOCK_UN);
+}
+
+void xproc_release_cb(void*) { xproc_release(); }
+
+// Every persistent launch goes through here: the cross-process lock, the launch itself (plain or
+// cooperative), the context's notify event and launch count.
+int persist_dispatch(avc_context* ctx, const void* fn, dim3 grid, dim3 block, void** args, size_t lds,
+                     hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  AVC_HIP(hipStreamIsCapturing(s, &cs));
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  const bool xl = xproc_lock_on();
+  if (xl) {
+    if (capturing) {  // the lock is taken at launch time, which a graph replay does not revisit
+      set_error("persistent recurrence: not captured into a graph while AVC_PERSIST_XPROC_LOCK is set");
+      return AVC_ERR_WORKSPACE;  // the capturing caller falls back to eager calls
+    }
+    AVC_TRY(xproc_acquire());
+  }
+  const hipError_t e = g_persist_coop ? hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)lds, s)
+                                      : hipLaunchKernel(fn, grid, block, args, lds, s);
+  if (xl) {
+    if (e != hipSuccess || hipLaunchHostFunc(s, xproc_release_cb, nullptr) != hipSuccess) {
+      (void)hipStreamSynchronize(s);
+      xproc_release();
+    }
+  }
+  AVC_HIP(e);
+  if (ctx->persist_event && !capturing)
+    AVC_HIP(hipEventRecord(static_cast<hipEvent_t>(ctx->persist_event), s));
+  ++ctx->persist_launches;
+  return AVC_OK;
+}
 
 // Launch: grid (nslot * ncb, ngrp); co-residency was checked by the eligibility test.
-int persist_launch(PersistArgs a, int RT, int ngrp, hipStream_t s) {
+int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_t s) {
   const dim3 grid(a.nslot * a.ncb, ngrp);
   a.nwg = (int)(grid.x * grid.y);
   for (int L = 0; L < a.nslot; ++L)
     AVC_CHECK_ARG(a.W[L] && a.winv[L], "persistent recurrence: a slot's split weights are missing");
   AVC_CHECK_ARG(a.in_slot == 0 || (a.in_slot == a.nslot - 1 && a.xs && a.b0 && a.gx0 && (a.din == 384 || a.din == 512)),
                 "persistent recurrence: input slot operands are missing");
-  a.spin_limit = kSpinLimit;
+  a.spin_limit = g_spin_limit;
   if (g_persist_inject > 0) {
     --g_persist_inject;
     a.spin_limit = 0;
   }
   const void* fn = persist_fn(a.H, RT);
   void* args[] = {&a};
-  if (g_persist_coop)
-    AVC_HIP(hipLaunchCooperativeKernel(fn, grid, dim3(256), args, (unsigned)persist_lds(a.H, RT), s));
-  else
-    AVC_HIP(hipLaunchKernel(fn, grid, dim3(256), args, persist_lds(a.H, RT), s));
-  return AVC_OK;
+  return persist_dispatch(ctx, fn, grid, dim3(256), args, persist_lds(a.H, RT), s);
 }
 
 // The counter region of launch layout (kind, T, ngrp, ncb, nwg) on this context: created zeroed (stream-ordered, before
@@ -1365,7 +1450,7 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   a.diag = g_persist_diag;
   set_region_args(a, ctx, region);
   hipEvent_t ev = timing_begin(TC_LSTM1_PERSIST, s);
-  AVC_TRY(persist_launch(a, RT, ngrp, s));
+  AVC_TRY(persist_launch(ctx, a, RT, ngrp, s));
   if (ev) {
     // split W_hh read once; per step the split h operand of every workgroup's group, gx, h, c
     const double flops = (double)T * 2.0 * B * H * 4.0 * H + (ip ? (double)T * 2.0 * B * ip->din * 4.0 * H : 0.0);
@@ -1431,7 +1516,7 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   set_region_args(a, ctx, region);
   const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
   hipEvent_t ev = timing_begin(TC_LSTM2_PERSIST, s);
-  AVC_TRY(persist_launch(a, RT, 1, s));
+  AVC_TRY(persist_launch(ctx, a, RT, 1, s));
   if (ev) {
     // one launch = the whole 2-layer recurrence: 3 products of [B x H] . [H x 4H] per time step;
     // algorithmic bytes = the split weights read once + per step the split h operands and the
@@ -1515,7 +1600,7 @@ int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _
   a.cnt = region + kRegionHeaderWords;
   a.fail_host = ctx->fail_host;
   a.nwg = 256;
-  a.spin_limit = kSpinLimit;
+  a.spin_limit = g_spin_limit;
   a.diag = g_bptt_diag;
   if (g_persist_inject > 0) {
     --g_persist_inject;
@@ -1524,10 +1609,7 @@ int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _
   const void* fn = bptt_fn(nch, ns);
   void* args[] = {&a};
   hipEvent_t ev = timing_begin(TC_LSTM_STEP_BWD, s);
-  if (g_persist_coop)
-    AVC_HIP(hipLaunchCooperativeKernel(fn, dim3(256), dim3(512), args, (unsigned)bptt_lds(nch), s));
-  else
-    AVC_HIP(hipLaunchKernel(fn, dim3(256), dim3(512), args, bptt_lds(nch), s));
+  AVC_TRY(persist_dispatch(ctx, fn, dim3(256), dim3(512), args, bptt_lds(nch), s));
   if (ev) {
     // the recurrent products of T - 1 steps; algorithmic bytes: the split dG read and the
     // partials written and read per step, the epilogue operands, dG written
@@ -1626,6 +1708,79 @@ extern "C" int avc_persist_check(avc_context* ctx, void* stream, int* failed) {
   const int rc = avc::persist_guard(ctx);
   if (failed) *failed = rc == AVC_ERR_DEVICE ? 1 : 0;
   return rc;
+}
+
+extern "C" int avc_persist_notify(avc_context* ctx, void* event) {
+  AVC_CHECK_ARG(ctx != nullptr, "ctx is NULL");
+  ctx->persist_event = event;
+  return AVC_OK;
+}
+
+extern "C" int avc_persist_launches(avc_context* ctx, long* count) {
+  AVC_CHECK_ARG(ctx != nullptr && count != nullptr, "NULL pointer");
+  *count = ctx->persist_launches;
+  return AVC_OK;
+}
+
+extern "C" int avc_bptt_persist_eligible(int T, int B, int H) {
+  return avc::bptt_persist_eligible(T, B, H) ? 1 : 0;
+}
+
+extern "C" int avc_debug_persist_spin_limit(unsigned polls) {
+  avc::g_spin_limit = polls ? polls : avc::kSpinLimit;
+  ++avc::g_config_epoch;  // drop a captured graph: the limit is a launch argument
+  return AVC_OK;
+}
+
+namespace avc {
+namespace {
+// Test load for the co-residency tests: n_wg workgroups that each hold lds_bytes of LDS (a whole
+// CU at the maximum) for `ticks` of the constant 100 MHz wall clock, counting themselves resident
+// in a pinned host word of its own first.  Bounded by construction (no waits on anything but the clock).
+__global__ void __launch_bounds__(64) hog_kernel(unsigned long long ticks, unsigned* resident) {
+  extern __shared__ unsigned hog_lds[];
+  if (threadIdx.x == 0) {
+    hog_lds[0] = 1u;
+    __hip_atomic_store(resident + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+  }
+  __syncthreads();
+}
+}  // namespace
+}  // namespace avc
+
+static unsigned* g_hog_words = nullptr;  // pinned: one "started" word per hog workgroup
+static int g_hog_n = 0;
+
+extern "C" int avc_debug_hog(avc_context* ctx, int n_wg, int lds_bytes, long usec, void* stream) {
+  AVC_CHECK_ARG(ctx != nullptr, "ctx is NULL");
+  AVC_CHECK_ARG(n_wg > 0 && n_wg <= 4096, "avc_debug_hog: n_wg must be 1..4096");
+  AVC_CHECK_ARG(lds_bytes >= 4 && lds_bytes <= 160 * 1024, "avc_debug_hog: lds_bytes must be 4..163840");
+  AVC_CHECK_ARG(usec > 0 && usec <= 10000000L, "avc_debug_hog: usec must be 1..10^7");
+  if (!g_hog_words) AVC_HIP(hipHostMalloc((void**)&g_hog_words, 4096 * sizeof(unsigned), hipHostMallocDefault));
+  int dev = 0, khz = 0;
+  AVC_HIP(hipGetDevice(&dev));
+  AVC_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0) khz = 100000;
+  AVC_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));  // an earlier hog is done
+  memset(g_hog_words, 0, 4096 * sizeof(unsigned));
+  g_hog_n = n_wg;
+  const void* fn = (const void*)avc::hog_kernel;
+  AVC_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
+  unsigned long long ticks = (unsigned long long)usec * (unsigned long long)khz / 1000ull;
+  unsigned* resident = g_hog_words;
+  void* args[] = {&ticks, &resident};
+  AVC_HIP(hipLaunchKernel(fn, dim3(n_wg), dim3(64), args, (size_t)lds_bytes, reinterpret_cast<hipStream_t>(stream)));
+  return AVC_OK;
+}
+
+extern "C" int avc_debug_hog_resident(avc_context* ctx, int* n) {
+  AVC_CHECK_ARG(ctx != nullptr && n != nullptr, "NULL pointer");
+  int k = 0;
+  for (int i = 0; g_hog_words && i < g_hog_n; ++i) k += __atomic_load_n(g_hog_words + i, __ATOMIC_ACQUIRE) != 0;
+  *n = k;
+  return AVC_OK;
 }
 
 extern "C" int avc_lstm_persist_status(long* giveups) {

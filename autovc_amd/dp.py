@@ -53,11 +53,34 @@ class GradBuckets:
     stream wait, not a host sync, with the nccl/RCCL backend) and divides by the world size.
 
     Outside `armed()` the hooks do nothing, so other backward passes (tests, user code) never
-    start a collective."""
+    start a collective.
 
-    def __init__(self, params, flat_grad: torch.Tensor, bucket_bytes: int = 16 << 20):
+    Co-residency rule.  The decoder LSTMs' backward runs as persistent launches that
+    need every CU at once (lstm_persist.hip: bptt_persist_kernel); an RCCL kernel waiting for a
+    lagging peer must never hold CUs while one dispatches, or the launch's resident workgroups
+    spin until their bounded wait gives up.  So (ops._lstm_bwd calls the two hooks):
+      * `before_recurrence`: the compute stream waits for every collective issued so far (a
+        stream wait with RCCL; no host sync), so none is in flight when the persistent grid
+        dispatches;
+      * while a decoder LSTM's backward is still to come, complete buckets are held back; the ones
+        whose gradients were final before a recurrence are issued right after it, on a side
+        stream behind the event the library records after the persistent launch
+        (avc_persist_notify), so they run beside that layer's dX/dW GEMMs and the rest of the
+        backward -- never beside a dispatch;
+      * after the last recurrence, buckets are issued as soon as they are complete.
+    `all_reduce` / `world` replace dist.all_reduce / the process group's size (tests: a collective
+    stand-in that holds CUs, world 1); `co_residency=False` turns the rule off (tests only)."""
+
+    def __init__(self, params, flat_grad: torch.Tensor, bucket_bytes: int = 16 << 20, all_reduce=None,
+                 world_size: int | None = None, co_residency: bool = True):
         params = list(params)
         self.flat = flat_grad
+        self._all_reduce = all_reduce if all_reduce is not None else (
+            lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True))
+        self._world = world_size
+        self.co_residency = co_residency
+        self._side = None
+        self._event = None
         base = flat_grad.data_ptr()
         spans = []
         for p in params:
@@ -91,12 +114,16 @@ class GradBuckets:
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
         self.reset()
 
-    def reset(self):
+    def reset(self, recurrences: int = 0):
         self.pending = list(self.sizes)
         self.next = 0
         self.handles = []
+        self.fenced = 0             # handles the compute stream already waits for
         self.seen = set()
         self.launch_log = []        # (bucket, parameters still pending overall) per issue
+        self.recurrences_left = recurrences if self.co_residency else 0
+        self._behind = 0
+        self._launches0 = 0
 
     def _ready(self, i):
         if not self._armed or i in self.seen:
@@ -117,24 +144,80 @@ class GradBuckets:
         if i is not None:
             self._ready(i)
 
-    def _issue(self, ready_only):
-        while self.next < len(self.buckets) and (not ready_only or self.pending[self.next] <= 0):
+    def _complete_run(self):
+        """Complete buckets from `next` on, in issue order."""
+        n = 0
+        while self.next + n < len(self.buckets) and self.pending[self.next + n] <= 0:
+            n += 1
+        return n
+
+    def _issue_n(self, n):
+        for _ in range(n):
             lo, hi = self.buckets[self.next]
             self.launch_log.append((self.next, sum(max(0, c) for c in self.pending)))
-            self.handles.append(dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+            self.handles.append(self._all_reduce(self.flat[lo:hi]))
             self.next += 1
 
-    def armed(self):
+    def _issue(self, ready_only):
+        if not ready_only:
+            self._issue_n(len(self.buckets) - self.next)
+        elif self.recurrences_left <= 0:  # held back while a persistent backward is still to come
+            self._issue_n(self._complete_run())
+
+    def before_recurrence(self):
+        """A decoder LSTM backward (possibly a persistent launch) is about to be enqueued."""
+        if not self._armed or not self.co_residency:
+            return
+        for h in self.handles[self.fenced:]:
+            h.wait()
+        self.fenced = len(self.handles)
+        self._behind = self._complete_run()  # final before the recurrence starts
+        dev = self.flat.device
+        if dev.type == "cuda":
+            from . import _lib
+            if self._event is None:
+                self._side = torch.cuda.Stream(device=dev)
+                self._event = torch.cuda.Event()
+                self._event.record(torch.cuda.current_stream(dev))  # creates the HIP event
+            _lib.call("avc_persist_notify", _lib.context(dev), self._event.cuda_event)
+            self._launches0 = _lib.persist_launches(dev)
+
+    def after_recurrence(self, left: int):
+        """The decoder LSTM backward is enqueued; `left` of them are still to come."""
+        if not self._armed or not self.co_residency:
+            return
+        self.recurrences_left = left
+        dev = self.flat.device
+        fired = False
+        if dev.type == "cuda":
+            from . import _lib
+            fired = _lib.persist_launches(dev) > self._launches0
+            _lib.call("avc_persist_notify", _lib.context(dev), None)
+        if self._behind and fired:
+            # behind the persistent launch: beside the layer's dX / dW products, not its dispatch
+            self._side.wait_event(self._event)
+            with torch.cuda.stream(self._side):
+                self._issue_n(self._behind)
+        else:
+            self._issue_n(self._behind)
+        self._behind = 0
+        self._issue(ready_only=True)
+
+    def armed(self, recurrences: int = 0):
+        """Context for one backward; `recurrences` = decoder LSTM backwards it will run."""
         outer = self
 
         class _Arm:
             def __enter__(self):
-                outer.reset()
+                outer.reset(recurrences)
                 outer._armed = True
                 return outer
 
             def __exit__(self, *exc):
                 outer._armed = False
+                if outer.flat.device.type == "cuda":
+                    from . import _lib
+                    _lib.call("avc_persist_notify", _lib.context(outer.flat.device), None)
                 return False
         return _Arm()
 
@@ -143,7 +226,7 @@ class GradBuckets:
         for h in self.handles:
             h.wait()
         self.handles = []
-        self.flat.div_(world())
+        self.flat.div_(self._world if self._world is not None else world())
         return self.flat
 
     def remove(self):
@@ -164,17 +247,26 @@ def params_in_sync(flat_param: torch.Tensor) -> bool:
     if world() == 1:
         return True
     v = flat_param.detach().double()
-    ck = torch.stack([v.sum(), (v * v).sum(), v.abs().max()])
+    ck = torch.stack([v.sum(), (v * v).sum(), v.abs().max()]).to(collective_device())
     lo, hi = ck.clone(), ck.clone()
     dist.all_reduce(lo, op=dist.ReduceOp.MIN)
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
     return bool(torch.equal(lo, hi))
 
 
+def collective_device() -> torch.device:
+    """Where the default process group's tensors must live: the current GPU for nccl (RCCL has
+    no CPU backend), the CPU for gloo."""
+    if world() > 1 and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def broadcast_seed(src: int = 0) -> int:
     """A 63-bit seed drawn from rank `src`'s torch RNG, the same on every rank."""
     seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
     if world() > 1:
+        seed = seed.to(collective_device())
         dist.broadcast(seed, src)
     return int(seed.item())
 
@@ -195,9 +287,14 @@ def shard_loader(loader, seed: int | None = None):
     seed = broadcast_seed() if seed is None else seed
     sampler = DistributedSampler(loader.dataset, num_replicas=world(), rank=rank(),
                                  shuffle=isinstance(loader.sampler, RandomSampler), seed=seed, drop_last=True)
+    # everything but the sampler as the caller built it
+    extra = dict(worker_init_fn=loader.worker_init_fn, generator=loader.generator, timeout=loader.timeout,
+                 multiprocessing_context=loader.multiprocessing_context)
+    if loader.num_workers > 0:
+        extra.update(persistent_workers=loader.persistent_workers, prefetch_factor=loader.prefetch_factor)
     return DataLoader(loader.dataset, batch_size=loader.batch_size, sampler=sampler,
                       collate_fn=loader.collate_fn, num_workers=loader.num_workers,
-                      pin_memory=loader.pin_memory, drop_last=loader.drop_last)
+                      pin_memory=loader.pin_memory, drop_last=loader.drop_last, **extra)
 
 
 def set_epoch(loader, epoch: int) -> None:

@@ -49,9 +49,20 @@ class GradSink:
     model.py:201); when the last use's backward has written, `notify(p)` fires -- the data-parallel
     bucketed all-reduce (dp.GradBuckets.param_ready) hangs off it."""
 
-    def __init__(self, notify=None):
+    def __init__(self, notify=None, comm=None):
         self.notify = notify
+        self.comm = comm            # dp.GradBuckets (data parallel): the co-residency hooks
         self.uses = {}
+        self.recurrences = 0        # decoder LSTM layers run forward whose backward is still to come
+
+    def recurrence_begin(self):
+        if self.comm is not None:
+            self.comm.before_recurrence()
+
+    def recurrence_end(self):
+        self.recurrences -= 1
+        if self.comm is not None:
+            self.comm.after_recurrence(self.recurrences)
 
     def use(self, *params):
         for p in params:
@@ -218,6 +229,8 @@ def _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, reverse, save, T, B):
     call("avc_lstm_forward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
          ptr(w_hh.contiguous()), ptr(b_ih), ptr(b_hh), y.data_ptr() + col * F32, ldy, ptr(gates),
          ptr(cst), _stream(x))
+    if save and _sink is not None and H != 32:
+        _sink.recurrences += 1
     return gates, cst
 
 
@@ -228,11 +241,19 @@ def _lstm_bwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, gates, cst, d_y, d_x, reve
     (dwi, dwh, dbi, dbh), direct = _param_grads(params, needs)
     # the kernels write all four: fill the ones autograd does not want with scratch
     scratch = [torch.empty_like(p) if b is None else b for p, b in zip(params, (dwi, dwh, dbi, dbh))]
+    # decoder LSTMs: the BPTT may be a persistent launch; the data-parallel all-reduce keeps its
+    # collectives away from its dispatch (dp.GradBuckets, co-residency rule)
+    sink = _sink if H != 32 else None
+    if sink is not None:
+        sink.recurrence_begin()
     call("avc_lstm_backward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
          ptr(w_hh.contiguous()), y.data_ptr() + col * F32, ldy, ptr(gates), ptr(cst),
          d_y.data_ptr() + col * F32, ptr(d_x), *[ptr(t) for t in scratch], int(acc), int(direct),
          _stream(x))
-    return tuple(_param_done(params, (dwi, dwh, dbi, dbh), direct))
+    done = tuple(_param_done(params, (dwi, dwh, dbi, dbh), direct))
+    if sink is not None:
+        sink.recurrence_end()
+    return done
 
 
 class LSTMLayer(torch.autograd.Function):
@@ -410,13 +431,33 @@ def l1_loss(a, b):
     return Loss.apply(a, b, 1)
 
 
+class OverlapAverage(torch.autograd.Function):
+    """(M, C, N) slices -> (C, (M-1)*step + N) NaN-padded nanmean paste (model.py:428-437); the
+    backward is torch's nanmean backward (d_out / count, 0 at NaN entries)."""
+
+    @staticmethod
+    def forward(ctx, frames, step):
+        frames = frames.contiguous()
+        M, C, N = frames.shape
+        out = _empty((C, (M - 1) * step + N), frames)
+        call("avc_overlap_average", M, C, N, step, ptr(frames), ptr(out), _stream(frames))
+        ctx.save_for_backward(frames)
+        ctx.step = step
+        return out
+
+    @staticmethod
+    def backward(ctx, d):
+        (frames,) = ctx.saved_tensors
+        M, C, N = frames.shape
+        d = d.contiguous()
+        dfr = torch.empty_like(frames)
+        call("avc_overlap_average_backward", M, C, N, ctx.step, ptr(frames), ptr(d), ptr(dfr), _stream(d))
+        return dfr, None
+
+
 def overlap_average(frames: torch.Tensor, step: int) -> torch.Tensor:
     """(M, C, N) slices -> (C, (M-1)*step + N) NaN-padded nanmean paste (model.py:428-437)."""
-    frames = frames.contiguous()
-    M, C, N = frames.shape
-    out = _empty((C, (M - 1) * step + N), frames)
-    call("avc_overlap_average", M, C, N, step, ptr(frames), ptr(out), _stream(frames))
-    return out
+    return OverlapAverage.apply(frames, step)
 
 
 def gemm(a, b, bias=None, a_trans=False, b_trans=False):

@@ -176,6 +176,10 @@ int avc_decoder_input_backward(int T, int B, int ce, const float* d_dec_in, floa
  * out (C, (M-1)*step + N). */
 int avc_overlap_average(int M, int C, int N, int step, const float* frames, float* out,
                         void* stream);
+/* Its backward (torch's nanmean backward: d_out / count of non-NaN slices at the column, 0 for NaN
+ * entries), so batch_forward keeps the autograd graph like the reference: d_frames (M, C, N). */
+int avc_overlap_average_backward(int M, int C, int N, int step, const float* frames, const float* d_out,
+                                 float* d_frames, void* stream);
 
 /* ---- losses (model.py:184-215; criteria at model.py:286-288) -----------------------------
  * kind 0 = nn.MSELoss (mean of (a-b)^2), kind 1 = nn.L1Loss (mean of |a-b|).
@@ -193,7 +197,10 @@ int avc_loss_backward(int kind, size_t n, const float* a, const float* b, const 
  *   Adam(lr, beta1, beta2, eps, weight_decay, step) with the clipped gradient (torch.optim.Adam
  *   semantics, amsgrad=False), then ema = ema_decay*ema + (1-ema_decay)*param (ema may be NULL),
  *   rounded like the reference's fp32 tensor expression with Python-double scalars.
- * max_norm <= 0 disables clipping. */
+ * max_norm <= 0 disables clipping.  A non-finite total_norm (a persistent recurrence that gave
+ * up writes NaN gradients) skips the update: param, exp_avg, exp_avg_sq and ema are left as they
+ * were (torch would write NaN into all of them).  Needs the norm: max_norm > 0 or
+ * norm_out != NULL. */
 int avc_clip_adam_ema(avc_context* ctx, size_t n, float* param, float* grad, float* exp_avg,
                       float* exp_avg_sq, float* ema, float lr, float beta1, float beta2,
                       float eps, float weight_decay, int step, float max_norm, double ema_decay,
@@ -299,6 +306,26 @@ int avc_debug_bptt_diag(int bits);
 /* Test hook: the next `launches` persistent launches give up at their first unsatisfied wait (as
  * if a peer workgroup never became resident); eager launches only (captured graphs are dropped). */
 int avc_debug_persist_inject(int launches);
+/* Co-residency hooks (replaces nothing in the reference: its training step,
+ * autovc/auto_encoder/model.py:312-318, has no persistent kernels).  A persistent launch needs
+ * every workgroup resident; a kernel of another stream that waits on something outside the GPU
+ * (an RCCL collective waiting for a peer rank) must not hold CUs while one dispatches.
+ * avc_persist_notify: record `event` (a hipEvent_t; NULL = none) on the launch stream right after
+ *   every later persistent launch on ctx, so a caller can start collectives behind the recurrence
+ *   (autovc_amd/dp.py GradBuckets).
+ * avc_persist_launches: persistent launches enqueued on ctx so far.
+ * avc_bptt_persist_eligible: 1 if avc_lstm_backward at (T, B, H) runs the persistent BPTT.
+ * The environment variable AVC_PERSIST_XPROC_LOCK=<file> serialises persistent launches across
+ * processes that share one GPU (flock held from the launch until the kernel has finished). */
+int avc_persist_notify(avc_context* ctx, void* event);
+int avc_persist_launches(avc_context* ctx, long* count);
+int avc_bptt_persist_eligible(int T, int B, int H);
+/* Test hooks for the co-residency tests: the spin limit of the persistent kernels' bounded waits in
+ * polls (0 = the default, 2^21); a load of n_wg workgroups holding lds_bytes of LDS each (a whole
+ * CU at 163840) for `usec` microseconds on `stream`, and how many of them have started. */
+int avc_debug_persist_spin_limit(unsigned polls);
+int avc_debug_hog(avc_context* ctx, int n_wg, int lds_bytes, long usec, void* stream);
+int avc_debug_hog_resident(avc_context* ctx, int* n);
 /* Forward-graph policy of avc_generator_forward_cached: 1 = capture on the second call with the
  * same key and replay (default); 0 = always eager (tests that need eager reference outputs). */
 int avc_graph_mode(int on);

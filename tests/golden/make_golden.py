@@ -177,6 +177,64 @@ def train_case(AE, hparams, steps=3, B=4, T=128):
     return d
 
 
+def curve_case(AE, hparams, steps=12, B=256, T=128):
+    """The training-loss curve of BASELINE config 3 (B = 256, T = 128) from the reference's own
+    learn() (model.py:218-361), one epoch over `steps` seeded batches: per-step loss and pre-clip
+    gradient norm, recorded by wrapping the instance's _loss and torch.nn.utils.clip_grad_norm_
+    (the values the loop computes; nothing else changes).  Only the batch seeds and the two curves
+    are stored.  The same steps are also run through the oracle's Trainer in float64 (exact
+    arithmetic up to 1e-16): its distance from the fp32 reference is the run-to-run spread any
+    correct fp32 implementation has, which the GPU test's tolerance is built from."""
+    seeds = [500 + s for s in range(steps)]
+
+    def batch(s):
+        return (torch.from_numpy(synthetic_mel(seeds[s], B, T)), torch.from_numpy(onehot_embedding(B, offset=s)))
+
+    ae, ck = make_ae(AE)
+    losses, norms = [], []
+    inner_loss = ae._loss
+
+    def loss_rec(*a, **k):
+        out = inner_loss(*a, **k)
+        losses.append(float(out.detach()))
+        return out
+    ae._loss = loss_rec
+    clip = torch.nn.utils.clip_grad_norm_
+
+    def clip_rec(*a, **k):
+        n = clip(*a, **k)
+        norms.append(float(n))
+        return n
+    hp_opt = hparams["optimizer"]
+    saved = dict(hp_opt)
+    torch.nn.utils.clip_grad_norm_ = clip_rec
+    with tempfile.TemporaryDirectory() as tmp:
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        os.makedirs("ckpt")
+        try:
+            ae.learn([batch(s) for s in range(steps)], n_epochs=1, save_dir="ckpt", model_name="m.pt")
+        finally:
+            torch.nn.utils.clip_grad_norm_ = clip
+            os.chdir(cwd)
+            hp_opt.clear()
+            hp_opt.update(saved)
+    assert len(losses) == steps and len(norms) == steps
+
+    from oracle import autovc_oracle as orc
+    sd64 = {k: v.double() if v.is_floating_point() else v for k, v in torch_state_dict(0).items()}
+    tr = orc.Trainer(sd64)
+    l64, n64 = [], []
+    for s in range(steps):
+        X, c = batch(s)
+        l, g = tr.grads(X.double(), c.double(), tr.bufs)
+        l64.append(l)
+        n64.append(tr._apply(list(g)))
+    return dict(seeds=np.array(seeds), onehot_offsets=np.arange(steps), B=np.array(B), T=np.array(T),
+                losses=np.array(losses), grad_norms=np.array(norms), losses_f64=np.array(l64),
+                grad_norms_f64=np.array(n64), weights_checksum=np.array(ck), lr=np.array(saved.get("lr", 1e-3)))
+
+
 def checkpoint_layout_case(AE, hparams, B=2, T=64):
     """The checkpoint dict the reference's learn() writes through save() (model.py:158-176): one
     training step, then the file's structure (model_state keys/shapes/dtypes, optimizer_state's
@@ -234,6 +292,7 @@ def main():
         "batch_forward_m5_n128": lambda: batch_forward_case(AE),
         "c1_mette_183_b1_t128": lambda: c1_case(AE),
         "train_b4_t128_3steps": lambda: train_case(AE, hparams),
+        "train_b256_t128_curve": lambda: curve_case(AE, hparams),
     }
     only = sys.argv[1:]
     for name, fn in cases.items():

@@ -1,10 +1,15 @@
 """Data-parallel training step on the GPU (BASELINE config 4's path at world size 2): two ranks on
-the box's one MI355X, gloo carrying the gradient all-reduce (RCCL does not run two ranks on one
-device; the product path is the same dp.average_gradients call).  Each rank runs
-AutoEncoder.train_step on its own half of the batch; the ordering under test is forward + loss +
-backward per rank -> all-reduce mean -> clip_grad_norm_(1) -> Adam -> EMA on every rank, checked
-against the oracle's step_dp (oracle/autovc_oracle.py), and the ranks' parameters must stay
-bit-identical."""
+the box's one MI355X, gloo carrying the bucketed gradient all-reduce (RCCL does not run two ranks
+on one device; the product path is the same dp.GradBuckets exchange).  Each rank runs
+AutoEncoder.train_step on its own shard; the ordering under test is forward + loss + backward per
+rank -> all-reduce mean -> clip_grad_norm_(1) -> Adam -> EMA on every rank, checked against the
+oracle's step_dp (oracle/autovc_oracle.py), and the ranks' parameters must stay bit-identical.
+
+B_RANK = 256, T = 128 is config 4's per-rank plan: the decoder LSTMs' backward runs as persistent
+launches (bptt_persist_kernel) while earlier buckets are in flight, under the co-residency rule
+of dp.GradBuckets.  Two ranks share the one GPU here, so their persistent launches are also
+serialised across the processes (AVC_PERSIST_XPROC_LOCK, lstm_persist.hip: persist_dispatch) --
+with one GPU per rank (the real config) that lock is not needed."""
 import os
 import socket
 
@@ -16,7 +21,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-B_RANK, T = 16, 64
+CASES = [(16, 64), (256, 128)]  # (batch per rank, frames): fallback plan; config 4's persistent plan
 
 
 def _free_port():
@@ -27,18 +32,19 @@ def _free_port():
     return p
 
 
-def _shard(rank):
+def _shard(rank, B_RANK, T):
     from autovc_amd.weights import onehot_embedding, synthetic_mel
     X = synthetic_mel(81, 2 * B_RANK, T)[rank * B_RANK:(rank + 1) * B_RANK]
     c = onehot_embedding(2 * B_RANK)[rank * B_RANK:(rank + 1) * B_RANK]
     return torch.from_numpy(np.ascontiguousarray(X)), torch.from_numpy(np.ascontiguousarray(c))
 
 
-def _worker(rank, ws, port, q, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, ws, port, q, out_dir, B_RANK, T):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      AVC_PERSIST_XPROC_LOCK=os.path.join(out_dir, "persist.lock"))
     try:
         dist.init_process_group("gloo", rank=rank, world_size=ws)
-        from autovc_amd import dp
+        from autovc_amd import _lib, dp
         from autovc_amd.auto_encoder import AutoEncoder
         from autovc_amd.weights import torch_state_dict
         dev = torch.device("cuda:0")
@@ -46,9 +52,12 @@ def _worker(rank, ws, port, q, out_dir):
         ae.load_state_dict(torch_state_dict(0))
         ae.to(dev).train()
         ae.configure_optimizer()
-        X, c = _shard(rank)
+        X, c = _shard(rank, B_RANK, T)
+        launches = _lib.persist_launches(dev)
         loss, norm = ae.train_step(X.to(dev), c.to(dev))
-        rec = {"loss": loss.item(), "norm": norm.item(), "sync1": dp.params_in_sync(ae._flat_param)}
+        rec = {"loss": loss.item(), "norm": norm.item(), "sync1": dp.params_in_sync(ae._flat_param),
+               "persist": _lib.persist_launches(dev) - launches,
+               "order": [b for b, _ in ae._reducer.launch_log]}
         if rank == 0:
             torch.save({"flat": ae._flat_param.cpu(), "ema_sum": float(ae.avg_params.double().sum())},
                        os.path.join(out_dir, "rank0.pt"))
@@ -64,17 +73,19 @@ def _worker(rank, ws, port, q, out_dir):
         raise
 
 
-def test_dp_train_step_world2_against_oracle(tmp_path):
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("B_RANK,T", CASES)
+def test_dp_train_step_world2_against_oracle(tmp_path, B_RANK, T):
     from oracle import autovc_oracle as orc
     from autovc_amd.weights import torch_state_dict
     ws = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, ws, port, q, str(tmp_path))) for r in range(ws)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, q, str(tmp_path), B_RANK, T)) for r in range(ws)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(ws))
+    res = dict(q.get(timeout=420) for _ in range(ws))
     for p in procs:
         p.join(timeout=60)
     assert all("error" not in r for r in res.values()), res
@@ -83,9 +94,12 @@ def test_dp_train_step_world2_against_oracle(tmp_path):
     sd = torch_state_dict(0)
     tr = orc.Trainer(sd)
     bufs = [{k: v.clone() for k, v in sd.items() if k not in tr.p} for _ in range(ws)]
-    losses, norm = tr.step_dp([_shard(r) for r in range(ws)], bufs)
+    losses, norm = tr.step_dp([_shard(r, B_RANK, T) for r in range(ws)], bufs)
     print(f"DP world 2: losses {[res[r]['loss'] for r in range(ws)]} (oracle {losses}); "
           f"norm {[res[r]['norm'] for r in range(ws)]} (oracle {norm:.6f})")
+    assert res[0]["order"] == res[1]["order"]  # the same collectives in the same order
+    if B_RANK == 256:  # config 4's plan: lstm1 forward + three BPTTs persistent
+        assert all(res[r]["persist"] >= 4 for r in range(ws)), [res[r]["persist"] for r in range(ws)]
     for r in range(ws):
         assert res[r]["sync1"] and res[r]["sync2"], "ranks' parameters diverged"
         assert res[r]["loss"] == pytest.approx(losses[r], rel=1e-5)

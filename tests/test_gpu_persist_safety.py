@@ -81,9 +81,15 @@ def test_train_step_after_timeout_raises(cuda_device):
     c = torch.from_numpy(onehot_embedding(B)).to(cuda_device)
     ae.configure_optimizer()
     ae.train_step(X, c)
+    keep = [t.detach().clone() for t in (ae._flat_param, ae.optimiser.exp_avg, ae.optimiser.exp_avg_sq,
+                                          ae.avg_params)]
     _lib.call("avc_debug_persist_inject", 1)
-    loss, _ = ae.train_step(X, c)
+    loss, norm = ae.train_step(X, c)
     assert not torch.isfinite(loss).item()
+    assert not torch.isfinite(norm).item()
+    # the fused clip/Adam/EMA skipped the update: nothing was poisoned with NaN
+    for a, b in zip(keep, (ae._flat_param, ae.optimiser.exp_avg, ae.optimiser.exp_avg_sq, ae.avg_params)):
+        assert torch.equal(a, b)
     with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
         ae.train_step(X, c)
 
