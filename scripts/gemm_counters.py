@@ -19,14 +19,22 @@ def main():
     d, out = sys.argv[1:3]
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        # pass directories are named <mode>_<first counter> (gpu_check.sh gpmc3): the mode of
+        # gemm_micro.py that ran (c2 / c3fwd / c3bwd)
+        mode = next((m for m in ("c3fwd", "c3bwd", "c2") if f"/{m}_" in f), "")
         for r in csv.DictReader(open(f)):
             n = r["Kernel_Name"]
             if "gemm16f" not in n:
                 continue
             g = r.get("Grid_Size", "")
-            shape = {"131072": "conv 512->512 k5, M=8192 N=512 K=2560",
-                     "1048576": "lstm2 input projection, M=8192 N=4096 K=512"}.get(g, "")
-            key = f"gemm16f grid={g} {shape}".strip()
+            shape = {("c2", "131072"): "conv 512->512 k5 fwd, M=8192 N=512 K=2560",
+                     ("", "131072"): "conv 512->512 k5 fwd, M=8192 N=512 K=2560",
+                     ("c2", "1048576"): "lstm2 input projection, M=8192 N=4096 K=512",
+                     ("", "1048576"): "lstm2 input projection, M=8192 N=4096 K=512",
+                     ("c3fwd", "524288"): "conv 512->512 k5 fwd, M=32768 N=512 K=2560",
+                     ("c3bwd", "524288"): "conv 512->512 k5 dgrad (5 of 6 launches; 1 fwd), M=32768 N=512 K=2560",
+                     }.get((mode, g), "wgrad (split-K / tap-batched)" if mode == "c3bwd" else "")
+            key = f"{mode} gemm16f grid={g} {shape}".strip()
             vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
     res = {}
     for k, c in vals.items():
