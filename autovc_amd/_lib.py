@@ -69,6 +69,7 @@ _SIGS = {
     "avc_persist_check": [_P, _P, ctypes.POINTER(_I)],
     "avc_lstm_persist_coop": [_I],
     "avc_lstm_persist_inproj": [_I],
+    "avc_lstm_persist_qwait": [_I],
     "avc_lstm32_tune": [_I],
     "avc_bptt_persist": [_I],
     "avc_debug_bptt_diag": [_I],

@@ -93,6 +93,19 @@ constexpr int kRep = 8, kLine = 32;  // replicas; unsigned words per 128-B line
 __host__ __device__ __forceinline__ long cnt_index(int L, int T, int t, int r) {
   return (((long)L * T + t) * kRep + r) * kLine;
 }
+// Quarter counters (round 3, `avc_lstm_persist_qwait`): wave w of a consumer multiplies the K
+// chunks [w*NCH, (w+1)*NCH) of h, i.e. hidden units [w*H/4, (w+1)*H/4), which exactly the
+// workgroups [w*ncb/4, (w+1)*ncb/4) of the producing slot write.  Every producer also counts itself
+// in on the counter of its quarter (after the nslot*T full lines), so each wave waits for its own
+// 16 producers instead of the whole slot behind one workgroup barrier.
+constexpr int kQuarters = 4;
+__host__ __device__ __forceinline__ long qcnt_index(int nslot, int L, int T, int t, int q, int r) {
+  return (long)nslot * T * kRep * kLine + ((((long)L * T + t) * kQuarters + q) * kRep + r) * kLine;
+}
+// counter words of one group: the full lines, and with quarter counters four more per (slot, step)
+__host__ __device__ __forceinline__ long cnt_words(int nslot, int T, bool quarters) {
+  return (long)nslot * T * kRep * kLine * (quarters ? 1 + kQuarters : 1);
+}
 // gx1 hand-off: a ring of kGxRing steps of per-column-block slabs [64 rows][64 columns] fp32, so
 // each (step, column block) pair exchanges one contiguous 16 KB; slot 1 re-fills a ring entry
 // only after every slot-2 workgroup has finished the step that read it (back-pressure wait)
@@ -167,6 +180,9 @@ struct PersistArgs {
   int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
 };
 int g_persist_diag = 0;
+// avc_lstm_persist_qwait(): per-wave waits on quarter counters, bit 0 = two-layer form (lstm2:
+// 1141 -> 1073 us at C2), bit 1 = one-layer form (lstm1: 384 -> 400 us at C2, so off)
+int g_persist_qwait = 1;
 
 // One lane waits until *p reaches target (wrap-safe; relaxed agent-scope polls).  false = gave
 // up, or another workgroup of this launch (epoch E) did: the give-up word is checked every 64
@@ -194,6 +210,32 @@ __device__ bool wait_ge_ctl(unsigned* p, unsigned target, unsigned* tmo, unsigne
 
 __device__ __forceinline__ bool wait_ge(unsigned* p, unsigned target, const PersistArgs& a, unsigned E) {
   return wait_ge_ctl(p, target, a.tmo, a.fail_host, a.spin_limit, E);
+}
+
+// One lane waits until *p_i >= t_i for every enabled i (e_i): each poll loads all of them back to
+// back (one round trip for the lot), then compares; bounded and giving up like wait_ge_ctl.
+__device__ bool wait3(unsigned* p0, unsigned t0, bool e0, unsigned* p1, unsigned t1, bool e1, unsigned* p2,
+                      unsigned t2, bool e2, const PersistArgs& a, unsigned E) {
+  if (!e0 && !e1 && !e2) return true;
+  gu32* gt = (gu32*)(a.tmo);
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned v0 = e0 ? __hip_atomic_load((gu32*)p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const unsigned v1 = e1 ? __hip_atomic_load((gu32*)p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const unsigned v2 = e2 ? __hip_atomic_load((gu32*)p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    if ((!e0 || (int)(v0 - t0) >= 0) && (!e1 || (int)(v1 - t1) >= 0) && (!e2 || (int)(v2 - t2) >= 0)) return true;
+    if ((spins & 63) == 63 && __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E)
+      return false;
+    if (spins >= a.spin_limit) {
+      const unsigned old = __hip_atomic_fetch_max(gt, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old != E) {
+        const unsigned nf = atomicAdd(&g_persist_giveups, 1u) + 1u;
+        if (a.fail_host)
+          __hip_atomic_store(a.fail_host, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
 }
 
 // power of two the x split was scaled by (split_steps16_kernel): max |x| -> [2^14, 2^15)
@@ -324,7 +366,9 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
 // loads; 1 = no invalidate, EVERY load of handed-off bytes (split h, gx1) an sc1 load
 // (cdna_hip_programming.md Guideline 16, "Valid forms": producer stores sc1 + drained).
 // PD = h chunks loaded ahead of the chunk being multiplied (register buffers PD + 1).
-template <int NCH, int RT, int HO, int PD>
+// QW = 1: per-wave waits on quarter counters (see qcnt_index) instead of three polling lanes and a
+// workgroup barrier at the top of every step.
+template <int NCH, int RT, int HO, int PD, int QW>
 __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   constexpr int NW = 4, NC = 4;
   constexpr int MB = 16 * RT;        // batch rows computed (B <= MB)
@@ -335,10 +379,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   extern __shared__ float lds[];
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds);
   float* part = lds + NW * NCH * 512;
-  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);  // [4]: polling lanes' results (0, 1, 3), epoch (2)
+  // [8]: polling lanes' results (0, 1, 3), epoch (2); QW: each wave's wait result (4 + w)
+  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);
   // [TW] per-row unscale of this block's gate rows, then [TW] b_ih1 + b_hh1 (slot 1): read from
   // LDS in the epilogue instead of living in registers through the MFMA loop
-  float* cpar = reinterpret_cast<float*>(flag + 4);
+  float* cpar = reinterpret_cast<float*>(flag + 8);
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
@@ -417,6 +462,36 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   for (; t < T; ++t) {
     // ---- wait for this step's operands ----------------------------------------------------
     AVC_PSTAMP(0);
+    if constexpr (QW) {
+      // Lane 0 of every wave waits for what THIS wave reads, all in one multi-counter poll: the
+      // quarter of the h source its K chunks come from; slot 2: the slot-1 quarter that wrote its
+      // gx1 slab (the one of workgroup cb); slot 0 with the input slot, every 4th step: gx0 for 4
+      // steps (as below).  Wave 1 also takes the back-pressure wait; it gates nothing but the
+      // stores after the reduction barrier (slot 1's gx1 ring entry), which every wave passes after
+      // wave 1's wait.  No workgroup barrier: each wave starts its loads as soon as its own
+      // producers are in.  A failed wait is acted on after the reduction barrier (all waves leave).
+      if (lane == 0) {
+        const unsigned qtarget = E * (unsigned)(a.ncb / kQuarters);
+        const int hsl = L == 1 ? 0 : L;      // slot whose h this slot reads (0: h0, 2: h1)
+        const int ht = L == 1 ? t : t - 1;   // and its step
+        // 0: the h quarter; 1: the gx operand; 2: back-pressure (wave 1)
+        const bool e0 = ht >= 0;
+        unsigned* p0 = cnt + qcnt_index(a.nslot, hsl, T, e0 ? ht : 0, w, rep);
+        const bool e1 = L == 2 || (L == 0 && a.in_slot > 0 && (t & 3) == 0);
+        unsigned* p1 = L == 2 ? cnt + qcnt_index(a.nslot, 1, T, t, cb / (a.ncb / kQuarters), rep)
+                              : cnt + cnt_index(a.in_slot, T, min(t + 3, T - 1), rep);
+        const unsigned t1 = L == 2 ? qtarget : target;
+        const bool e2 = w == 1 && ((L == 0 && t >= kLead && a.nslot >= 3) || (L == 1 && t >= kGxRing));
+        unsigned* p2 = cnt + cnt_index(2, T, e2 ? t - (L == 0 ? kLead : kGxRing) : 0, rep);
+        flag[4 + w] = wait3(p0, qtarget, e0, p1, t1, e1, p2, target, e2, a, E) ? 1 : 0;
+      }
+      // the polled values are in (the loop compared them); nothing below moves above this point
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      AVC_PSTAMP(1);
+      AVC_PRSTAMP(7);
+      AVC_PSTAMP(2);
+    } else {
     // Two lanes poll in parallel (lane 0 of waves 0 and 1): the data this step reads, and the
     // back-pressure that keeps slots 0 and 1 at most kLead / kGxRing steps ahead of slot 2 (a
     // slot running far ahead streams gx0 / writes h0 through the Infinity Cache and starves the
@@ -450,6 +525,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     __syncthreads();
     if (flag[0] == 0 || flag[1] == 0 || flag[3] == 0) break;
     AVC_PSTAMP(2);
+    }
 
     // ---- recurrent / input product over this wave's K quarter ----------------------------
     // The epilogue operands (gx0 / b1 / the gx1 hand-off) are loaded right after the LAST h
@@ -590,6 +666,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e];
     __syncthreads();
+    if constexpr (QW) {
+      if (flag[4] == 0 || flag[5] == 0 || flag[6] == 0 || flag[7] == 0) break;
+    }
     fu hv, ig, fg, gg, og;
     if (L == 1) {
       // projection slot: the same fixed-order sum, scale and bias per 4 columns, stored to this
@@ -669,9 +748,13 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     __syncthreads();
     AVC_PSTAMP(5);
     AVC_PRSTAMP(6);
-    if (tid < kRep)
-      __hip_atomic_fetch_add((gu32*)(cnt + cnt_index(L, T, t, tid)), 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+    // lanes 8..15 count in on this workgroup's quarter -- in both wait forms, so every launch adds
+    // ncb / 4 to every quarter word and the epoch targets hold whichever form the next launch takes
+    if (tid < 2 * kRep) {
+      const long ci = tid < kRep ? cnt_index(L, T, t, tid)
+                                 : qcnt_index(a.nslot, L, T, t, cb / (a.ncb / kQuarters), tid - kRep);
+      __hip_atomic_fetch_add((gu32*)(cnt + ci), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // outputs nobody reads inside this launch: stored after publishing (off the hand-off path)
     if (L != 1 && live) {
       *reinterpret_cast<fu*>(y_out + ((long)t * B + b) * H + j0 + u0) = hv;
@@ -767,16 +850,18 @@ int lstm1_rows_per_group(int B, int H) {
 
 size_t persist_lds(int H, int RT) {
   const int nch = H / 32 / 4;
-  return (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 16 + 2 * 64 * sizeof(float);
+  return (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 32 + 2 * 64 * sizeof(float);
 }
 
 // The template instance a launch of (H, RT) runs under the current tuning.
-const void* persist_fn(int H, int RT) {
+const void* persist_fn(int H, int RT, bool two_layer = true) {
+  const bool qw = (g_persist_qwait & (two_layer ? 1 : 2)) != 0;
   const int nch = H / 32 / 4;
 #define AVC_PERSIST_FN(NCHV, RTV)                                                                 \
-  return g_persist_mode == 1 ? (const void*)lstm_persist_kernel<NCHV, RTV, 0, 1>                  \
-       : g_persist_pd == 1   ? (const void*)lstm_persist_kernel<NCHV, RTV, 1, 1>                  \
-                             : (const void*)lstm_persist_kernel<NCHV, RTV, 1, 2>;
+  return g_persist_mode == 1 ? (const void*)lstm_persist_kernel<NCHV, RTV, 0, 1, 0>               \
+       : g_persist_pd == 1   ? (const void*)lstm_persist_kernel<NCHV, RTV, 1, 1, 0>               \
+       : qw                  ? (const void*)lstm_persist_kernel<NCHV, RTV, 1, 2, 1>               \
+                             : (const void*)lstm_persist_kernel<NCHV, RTV, 1, 2, 0>;
   if (nch == 8) {
     if (RT == 1) { AVC_PERSIST_FN(8, 1) } else if (RT == 2) { AVC_PERSIST_FN(8, 2) } else { AVC_PERSIST_FN(8, 4) }
   } else {
@@ -902,7 +987,7 @@ int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_
     --g_persist_inject;
     a.spin_limit = 0;
   }
-  const void* fn = persist_fn(a.H, RT);
+  const void* fn = persist_fn(a.H, RT, a.nslot >= 3);
   void* args[] = {&a};
   return persist_dispatch(ctx, fn, grid, dim3(256), args, persist_lds(a.H, RT), s);
 }
@@ -1433,7 +1518,7 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   const long hsz = (long)ntile * 16 * H * 2 * 2;
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
   const int nslot = ip ? 2 : 1;
-  const long gstride = (long)nslot * T * kRep * kLine;  // counter words per group: [nslot][T][kRep] lines
+  const long gstride = cnt_words(nslot, T, true);  // counter words per group: full + quarter lines
   AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
   unsigned* region = nullptr;
   AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), (size_t)ngrp * gstride, s,
@@ -1497,9 +1582,10 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   AVC_TAKE(hs1, unsigned char, (size_t)2 * hsz, sc);                      // ring of 2
   AVC_TAKE(gx1, float, (size_t)kGxRing * (4 * H / 64) * 64 * 64, sc);     // slab ring
   const int nslot = ip ? 4 : 3;
-  // counters [nslot][T][kRep] (one 128-B line each) in the persistent region of this layout
+  // counters [nslot][T][kRep] (one 128-B line each) and the quarter counters in the persistent
+  // region of this layout
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), (size_t)nslot * T * kRep * kLine, s,
+  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), (size_t)cnt_words(nslot, T, true), s,
                          &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
@@ -1661,6 +1747,16 @@ extern "C" int avc_lstm_persist_layers(int mask) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_layers = mask;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_qwait(int mask) {
+  if (mask < 0 || mask > 3) {
+    avc::set_error("avc_lstm_persist_qwait: mask must be 0..3");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_qwait = mask;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -272,6 +272,11 @@ int avc_lstm_persist_tune(int mode);
 /* Tuning hook: split-h chunks the persistent recurrence keeps in flight ahead of the chunk being
  * multiplied (1 or 2 = default); same arithmetic either way. */
 int avc_lstm_persist_depth(int chunks);
+/* Tuning hook: the persistent recurrences' per-step waits.  Bit set = every wave waits for the
+ * quarter of the producing slot whose h it multiplies (quarter counters, no workgroup barrier);
+ * clear = one polling lane per operand and a workgroup barrier.  Bit 0: two-layer form (lstm2),
+ * bit 1: one-layer form (lstm1); default 1.  Same arithmetic either way (bit-identical). */
+int avc_lstm_persist_qwait(int mask);
 /* Tuning hook: which recurrences may take the persistent form (bit 0 = one layer, e.g. decoder
  * lstm1; bit 1 = two stacked layers, decoder lstm2; default 3 = both). */
 int avc_lstm_persist_layers(int mask);
