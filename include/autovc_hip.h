@@ -258,10 +258,10 @@ int avc_lstm_split_tune(int kslice, int col_blocks, int rows64);
  * scaled-split (default); 3 = as 2 but backward products on the fp32 kernel. */
 int avc_gemm_tune(int prec16);
 /* Tuning hook: variant of the pre-split split-f16 GEMM for 128x128 tiles (8 waves each):
- * 0 = 4x2 waves, 4-stage ring of 32-deep K-tiles; 1 = 4x2, 2 stages of 64-deep K-tiles (default);
- * 2 = 4x2, 3 stages x 48; 3 = 2x4, 4 x 32; 4 = 2x4, 2 x 64; 5 = 4x2, 3 x 32; 6 / 7 = 4x2,
- * 2 x 32 / 2 x 64 with plain (not Kahan-compensated) 128-k partial folds, 128 VGPRs (two
- * workgroups per CU for 6). */
+ * 0 = 4x2 waves, 4-stage ring of 32-deep K-tiles; 1 = 4x2, 2 stages of 64-deep K-tiles, Kahan
+ * fold of the 128-k partials; 2 = 4x2, 3 stages x 48; 3 = 2x4, 4 x 32; 4 = 2x4, 2 x 64; 5 = 4x2,
+ * 3 x 32; 6 / 7 = 4x2, 2 x 32 / 2 x 64 with plain (not Kahan-compensated) 128-k partial folds,
+ * 128 VGPRs (two workgroups per CU for 6); 8 (default) = 1 with the plain fold. */
 int avc_gemm_config(int cfg);
 /* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) and decoder lstm1 (one layer,
  * batch <= 256) as ONE weight-stationary launch each (lstm_persist.hip) instead of one launch per
