@@ -540,9 +540,14 @@ def pmc_traffic(cls, args):
     (profiles/rNN_pmc_traffic.json, written by scripts/pmc_traffic.py); counters cannot be read
     from inside the process, so the number is the profiled run's, not this run's."""
     import glob
-    if args.mode != "fwd" or args.batch not in (None, 64) or args.frames != 128:
+    # default commands only: C2 forward (profiles/rNN_pmc_traffic.json), C3 training step
+    # (profiles/rNN_pmc_traffic_train.json)
+    if args.frames != 128 or args.mode not in ("fwd", "train"):
         return None
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")))
+    if args.batch not in (None, 64 if args.mode == "fwd" else 256):
+        return None
+    pat = "r*_pmc_traffic.json" if args.mode == "fwd" else "r*_pmc_traffic_train.json"
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", pat)))
     if not files:
         return None
     with open(files[-1]) as fh:

@@ -26,6 +26,8 @@ for step in "$@"; do
     prof)  run prof 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o fwd -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-timing ;;
     pmcf)  run pmcf 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcF -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
     pmcw)  run pmcw 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcW -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
+    pmcft) run pmcft 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcFT -o train -- python3 bench.py --mode train --steps 2 --warmup 1 --no-cpu --no-timing ;;
+    pmcwt) run pmcwt 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcWT -o train -- python3 bench.py --mode train --steps 2 --warmup 1 --no-cpu --no-timing ;;
     sweep) run sweep 600 python scripts/sweep_lstm.py ;;
     proftrain) run proftrain 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/proftrain -o train -- python3 bench.py --mode train --steps 3 --warmup 1 --no-cpu --no-timing ;;
     ssplit) run ssplit 400 python scripts/sweep_split.py ;;
