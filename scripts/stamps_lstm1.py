@@ -6,7 +6,7 @@ import os
 import sys
 
 REPO = __file__.rsplit("/", 2)[0]
-os.environ["AUTOVC_HIP_LIB"] = os.path.join(REPO, "diag", "libautovc_hip_stamps.so")
+os.environ["AUTOVC_HIP_LIB"] = os.environ.get("AVC_STAMPS_LIB", os.path.join(REPO, "diag", "libautovc_hip_stamps.so"))
 sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -42,3 +42,18 @@ step = np.median(np.diff(st[:, 4:T - 4, 5], axis=1))
 d = np.diff(st[:, 4:T - 4, 6], axis=1) * 10.0
 print("lstm1 per-step median ticks: " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, ph)) +
       f"; step-to-step {step:.0f} ticks, realtime {np.median(d):.0f} ns")
+if len(sys.argv) > 1:  # second measurement with the given avc_lstm_persist_qwait mask
+    _lib.call("avc_lstm_persist_qwait", int(sys.argv[1]))
+    buf.zero_()
+    lib.avc_debug_stamps_persist(ctypes.c_void_p(buf.data_ptr()))
+    with torch.no_grad():
+        ae(x, c, c)
+    torch.cuda.synchronize()
+    lib.avc_debug_stamps_persist(ctypes.c_void_p(0))
+    st = buf.view(NCB, T, 8).cpu().numpy().astype(np.int64)
+    s = st[:, 4:T - 4, :]
+    ph = [np.median(s[:, :, i + 1] - s[:, :, i]) for i in range(5)]
+    step = np.median(np.diff(st[:, 4:T - 4, 5], axis=1))
+    d = np.diff(st[:, 4:T - 4, 6], axis=1) * 10.0
+    print(f"qwait {sys.argv[1]}: lstm1 per-step median ticks: " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, ph)) +
+          f"; step-to-step {step:.0f} ticks, realtime {np.median(d):.0f} ns")
