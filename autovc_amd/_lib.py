@@ -70,6 +70,7 @@ _SIGS = {
     "avc_lstm_persist_coop": [_I],
     "avc_lstm_persist_inproj": [_I],
     "avc_lstm_persist_qwait": [_I],
+    "avc_lstm_persist_granules": [_I],
     "avc_lstm32_tune": [_I],
     "avc_bptt_persist": [_I],
     "avc_debug_bptt_diag": [_I],

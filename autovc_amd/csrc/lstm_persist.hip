@@ -175,6 +175,8 @@ struct PersistArgs {
   unsigned* tmo;              // give-up word: epoch of the last launch that gave up
   unsigned long long* tickets;  // one per workgroup per launch
   unsigned* fail_host;        // pinned host word (avc_context::fail_host): last failure number
+  unsigned char* hg;          // GR: granule ring [grp][kGrRing][hg_step] (in the counter region)
+  long hg_step, hg_gstride;   // GR: bytes per (group, step) / per group
   int nwg;                    // workgroups in the grid
   unsigned spin_limit;        // polls before giving up (0 = test injection: give up at once)
   int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
@@ -183,6 +185,38 @@ int g_persist_diag = 0;
 // avc_lstm_persist_qwait(): per-wave waits on quarter counters, bit 0 = two-layer form (lstm2:
 // 1141 -> 1073 us at C2), bit 1 = one-layer form (lstm1: 384 -> 400 us at C2, so off)
 int g_persist_qwait = 1;
+// avc_lstm_persist_granules(): the one-layer form hands split h over as data-tagged granules
+int g_persist_gran = 1;
+
+// Granule hand-off (GR, one-layer form, H = 512): split h_t goes out as 8-B granules
+// {f16 hi | f16 lo << 16, tag}, one per (batch row, hidden unit), each written by ONE sc1 store
+// (cdna_hip_programming.md Guideline 16, R2: the data is the flag).  A consumer wave loads its K
+// quarter of h_{t-1} and re-loads until every tag it holds is this (launch, step)'s tag: no
+// drain, no workgroup barrier and no counter between the producer's epilogue and the consumer's
+// MFMAs.  Layout per (group, step): [RT tiles][nck chunks][4 j][64 lanes][16 B], lane l of chunk
+// kc holding row l & 15, units kc*32 + 8*(l >> 4) + 2j, +1 -- the lane's 8 units of the split-h
+// fragment in 4 b128 loads, each wave instruction reading 1 KB contiguous.  A ring of kGrRing
+// steps: a producer at step t has seen h_{t-1} of every workgroup of its group, so every reader
+// of step t - 2 is done (ring >= 2 suffices); the tag carries t & 7 so the step t - 4 left in the
+// same entry never matches, and E so an earlier launch's granules never do.
+constexpr int kGrRing = 4;
+__host__ __device__ __forceinline__ unsigned gr_tag(unsigned E, int t) { return (E << 3) | (unsigned)(t & 7); }
+
+// One wave, every lane: leave a spin?  The give-up word is read every 64 passes; past the limit
+// the launch gives up (the first wave to do so reports it, as wait_ge_ctl).  spins is uniform.
+__device__ bool spin_give_up(unsigned spins, const PersistArgs& a, unsigned E, int lane) {
+  if ((spins & 63) == 63 && __hip_atomic_load((gu32*)a.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E)
+    return true;
+  if (spins < a.spin_limit) return false;
+  if (lane == 0) {
+    const unsigned old = __hip_atomic_fetch_max((gu32*)a.tmo, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old != E) {
+      const unsigned nf = atomicAdd(&g_persist_giveups, 1u) + 1u;
+      if (a.fail_host) __hip_atomic_store(a.fail_host, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  return true;
+}
 
 // One lane waits until *p reaches target (wrap-safe; relaxed agent-scope polls).  false = gave
 // up, or another workgroup of this launch (epoch E) did: the give-up word is checked every 64
@@ -368,8 +402,10 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
 // PD = h chunks loaded ahead of the chunk being multiplied (register buffers PD + 1).
 // QW = 1: per-wave waits on quarter counters (see qcnt_index) instead of three polling lanes and a
 // workgroup barrier at the top of every step.
-template <int NCH, int RT, int HO, int PD, int QW>
+// GR = 1: granule hand-off of split h (one-layer form, NCH = 4, RT = 1; see gr_tag).
+template <int NCH, int RT, int HO, int PD, int QW, int GR = 0>
 __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
+  static_assert(!GR || (NCH == 4 && RT == 1 && HO == 1 && !QW), "granule hand-off: one-layer form, H = 512, RT = 1");
   constexpr int NW = 4, NC = 4;
   constexpr int MB = 16 * RT;        // batch rows computed (B <= MB)
   constexpr int TW = 16 * NC;        // 64 gate rows
@@ -384,6 +420,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   // [TW] per-row unscale of this block's gate rows, then [TW] b_ih1 + b_hh1 (slot 1): read from
   // LDS in the epilogue instead of living in registers through the MFMA loop
   float* cpar = reinterpret_cast<float*>(flag + 8);
+  // GR: [MB][16] split h of this workgroup's 16 hidden units, staged for the granule stores
+  unsigned* hst = reinterpret_cast<unsigned*>(cpar + 2 * 64);
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
@@ -457,12 +495,26 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   float* y_out = L == 0 ? a.y0 : a.y1;
   auto gx1_slab = [&](int tt, int c) -> long { return ((long)(tt % kGxRing) * a.ncb + c) * (64 * TW); };
   const int rep = blockIdx.x & (kRep - 1);
+  // outputs nobody reads inside this launch: h, and for training c and the activated gates
+  auto store_out = [&](int tt, const fu& h, const fu& c, const fu& i, const fu& f, const fu& g, const fu& o) {
+    *reinterpret_cast<fu*>(y_out + ((long)tt * B + b) * H + j0 + u0) = h;
+    if (c_save) *reinterpret_cast<fu*>(c_save + ((long)tt * B + b) * H + j0 + u0) = c;
+    if (g_save) {
+      float* go = g_save + ((long)tt * B + b) * G4 + p0 + u0;
+      *reinterpret_cast<fu*>(go) = i;
+      *reinterpret_cast<fu*>(go + 4) = f;
+      *reinterpret_cast<fu*>(go + 8) = g;
+      *reinterpret_cast<fu*>(go + 12) = o;
+    }
+  };
+  fu pend_h = {}, pend_c = {}, pend_i = {}, pend_f = {}, pend_g = {}, pend_o = {};  // GR: step t - 1's outputs
 
   int t = 0;
   for (; t < T; ++t) {
     // ---- wait for this step's operands ----------------------------------------------------
     AVC_PSTAMP(0);
-    if constexpr (QW) {
+    if constexpr (QW || GR) {
+      // GR: only the input slot's gx0 is waited on here (h comes with its tags, below).
       // Lane 0 of every wave waits for what THIS wave reads, all in one multi-counter poll: the
       // quarter of the h source its K chunks come from; slot 2: the slot-1 quarter that wrote its
       // gx1 slab (the one of workgroup cb); slot 0 with the input slot, every 4th step: gx0 for 4
@@ -475,22 +527,23 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         const int hsl = L == 1 ? 0 : L;      // slot whose h this slot reads (0: h0, 2: h1)
         const int ht = L == 1 ? t : t - 1;   // and its step
         // 0: the h quarter; 1: the gx operand; 2: back-pressure (wave 1)
-        const bool e0 = ht >= 0;
+        const bool e0 = !GR && ht >= 0;
         unsigned* p0 = cnt + qcnt_index(a.nslot, hsl, T, e0 ? ht : 0, w, rep);
         const bool e1 = L == 2 || (L == 0 && a.in_slot > 0 && (t & 3) == 0);
         unsigned* p1 = L == 2 ? cnt + qcnt_index(a.nslot, 1, T, t, cb / (a.ncb / kQuarters), rep)
                               : cnt + cnt_index(a.in_slot, T, min(t + 3, T - 1), rep);
         const unsigned t1 = L == 2 ? qtarget : target;
-        const bool e2 = w == 1 && ((L == 0 && t >= kLead && a.nslot >= 3) || (L == 1 && t >= kGxRing));
+        const bool e2 = !GR && w == 1 && ((L == 0 && t >= kLead && a.nslot >= 3) || (L == 1 && t >= kGxRing));
         unsigned* p2 = cnt + cnt_index(2, T, e2 ? t - (L == 0 ? kLead : kGxRing) : 0, rep);
         flag[4 + w] = wait3(p0, qtarget, e0, p1, t1, e1, p2, target, e2, a, E) ? 1 : 0;
       }
       // the polled values are in (the loop compared them); nothing below moves above this point
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (GR: no wait here -- it would drain the previous step's granule and output stores)
+      if constexpr (!GR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       AVC_PSTAMP(1);
       AVC_PRSTAMP(7);
-      AVC_PSTAMP(2);
+      if constexpr (!GR) AVC_PSTAMP(2);  // (GR: once the granules' tags match)
     } else {
     // Two lanes poll in parallel (lane 0 of waves 0 and 1): the data this step reads, and the
     // back-pressure that keeps slots 0 and 1 at most kLead / kGxRing steps ahead of slot 2 (a
@@ -584,7 +637,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     const unsigned char* src = L == 0 ? (t > 0 ? a.hs0 + (long)(t - 1) * a.hsz : nullptr)
                                       : (L == 1 ? a.hs0 + (long)t * a.hsz
                                                 : (t > 0 ? a.hs1 + (long)((t - 1) & 1) * a.hsz : nullptr));
-    if (src == nullptr) {
+    if (GR ? t == 0 : src == nullptr) {  // (GR: h_{t-1} comes from the granule ring, hs0 is unused)
       load_gx();
     } else {
       const int hrow16 = nck * 2048;
@@ -638,6 +691,65 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[0], acc[r][3], 0, 0, 0);      \
   }
 #endif
+      if constexpr (GR) {
+        // granules of step t - 1: this wave's K quarter (chunks kc0 ..) of every row tile,
+        // re-loaded until every tag is this step's (see gr_tag); gx0 goes out behind the first
+        // round (its producer was waited on above), so one vmcnt covers both
+        const unsigned tg = gr_tag(E, t - 1);
+        const auto grs = __builtin_amdgcn_make_buffer_rsrc(
+            a.hg + grp * a.hg_gstride + (long)((t - 1) % kGrRing) * a.hg_step, 0, (int)a.hg_step, 0x00020000);
+        const int gvo = kc0 * 4096 + lane * 16;
+        u32x4 gv[NCH][RT][4];
+        auto gload = [&]() {
+#pragma unroll
+          for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int r = 0; r < RT; ++r)
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                gv[c][r][j] = __builtin_amdgcn_raw_buffer_load_b128(grs, gvo, (r * nck + c) * 4096 + j * 1024, 16 /*sc1*/);
+        };
+        gload();
+        load_gx();
+        if (live) store_out(t - 1, pend_h, pend_c, pend_i, pend_f, pend_g, pend_o);
+        bool good = true;
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
+#pragma unroll
+          for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int r = 0; r < RT; ++r)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) ok = ok & (gv[c][r][j][1] == tg) & (gv[c][r][j][3] == tg);
+          if (__all(ok)) break;
+          if (spin_give_up(spins, a, E, lane)) {
+            good = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          gload();
+        }
+        if (!good && lane == 0) flag[4 + w] = 0;
+        AVC_PSTAMP(2);
+        // repack: granule 2j / 2j+1 of a lane -> element 2j / 2j+1 of the hi and lo f16x8
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          f16x8 hv8[RT][2];
+#pragma unroll
+          for (int r = 0; r < RT; ++r) {
+            u32x4 hi4, lo4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const unsigned d0 = gv[c][r][j][0], d1 = gv[c][r][j][2];
+              hi4[j] = (d0 & 0xffffu) | (d1 << 16);
+              lo4[j] = (d0 >> 16) | (d1 & 0xffff0000u);
+            }
+            hv8[r][0] = __builtin_bit_cast(f16x8, hi4);
+            hv8[r][1] = __builtin_bit_cast(f16x8, lo4);
+          }
+          AVC_PMFMA(hv8, c)
+        }
+      } else {
 #pragma unroll
       for (int c = 0; c < PDX && c < NCH; ++c) { AVC_PLD(hb[c], c) }
       if constexpr (NCH <= PDX) load_gx();
@@ -650,6 +762,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         AVC_PMFMA(hb[c % NB], c)
         __builtin_amdgcn_sched_barrier(0);
+      }
       }
 #undef AVC_PMFMA
 #undef AVC_PLD
@@ -666,7 +779,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e];
     __syncthreads();
-    if constexpr (QW) {
+    if constexpr (QW || GR) {
       if (flag[4] == 0 || flag[5] == 0 || flag[6] == 0 || flag[7] == 0) break;
     }
     fu hv, ig, fg, gg, og;
@@ -722,7 +835,27 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
                   ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
         }
       }
-      if (t + 1 < T || L == 0) {
+      if constexpr (GR) {
+        if (t + 1 < T) {
+          // stage the workgroup's [MB rows][16 units], then every thread stores RT granules: per
+          // (tile, j) one wave instruction writes 512 contiguous bytes (lanes 32(cb&1) .. +31 of
+          // chunk cb >> 1; layout at gr_tag), i.e. 4 whole lines
+#pragma unroll
+          for (int u = 0; u < UPT; ++u) hst[row * 16 + blk * 4 + u0 + u] = hl[u];
+          __syncthreads();
+          const unsigned tg = gr_tag(E, t);
+          const auto ors = __builtin_amdgcn_make_buffer_rsrc(
+              a.hg + grp * a.hg_gstride + (long)(t % kGrRing) * a.hg_step, 0, (int)a.hg_step, 0x00020000);
+          const int j = tid >> 6, lp = (tid & 63) >> 1, hh = tid & 1;
+          const int lu = 8 * (lp >> 4) + 2 * j + hh;
+#pragma unroll
+          for (int r = 0; r < RT; ++r) {
+            const u32x2 gr = {hst[(r * 16 + (lp & 15)) * 16 + lu], tg};
+            const int off = (((r * nck + (cb >> 1)) * 4 + j) * 64 + 32 * (cb & 1) + lp) * 16 + hh * 8;
+            __builtin_amdgcn_raw_buffer_store_b64(gr, ors, off, 0, 16 /*sc1*/);
+          }
+        }
+      } else if (t + 1 < T || L == 0) {
         // the pair's 4 units go out as one 8-B hi and one 8-B lo store (whole fragment rows) from
         // its first thread; the other SUB - 1 threads hand their units over by lane shuffles
         unsigned q[4];
@@ -743,6 +876,18 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         }
       }
     }
+    if constexpr (GR) {
+      // no publish: the granules carry their own tags, and slot 0's counters are not used (a GR
+      // launch has a region of its own -- its size differs -- and no input-slot back-pressure).
+      // This step's outputs are stored next step, behind its granule loads: vmcnt retires in
+      // issue order, so stores issued here would hold those loads' data until they complete.
+      AVC_PSTAMP(5);
+      AVC_PRSTAMP(6);
+      if (L == 0) {
+        pend_h = hv; pend_c = cst; pend_i = ig; pend_f = fg; pend_g = gg; pend_o = og;
+      }
+      continue;
+    }
     // ---- publish: every storing wave drains, barrier, the workgroup counts itself in ------
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -756,17 +901,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       __hip_atomic_fetch_add((gu32*)(cnt + ci), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // outputs nobody reads inside this launch: stored after publishing (off the hand-off path)
-    if (L != 1 && live) {
-      *reinterpret_cast<fu*>(y_out + ((long)t * B + b) * H + j0 + u0) = hv;
-      if (c_save) *reinterpret_cast<fu*>(c_save + ((long)t * B + b) * H + j0 + u0) = cst;
-      if (g_save) {
-        float* go = g_save + ((long)t * B + b) * G4 + p0 + u0;
-        *reinterpret_cast<fu*>(go) = ig;
-        *reinterpret_cast<fu*>(go + 4) = fg;
-        *reinterpret_cast<fu*>(go + 8) = gg;
-        *reinterpret_cast<fu*>(go + 12) = og;
-      }
-    }
+    if (L != 1 && live) store_out(t, hv, cst, ig, fg, gg, og);
+  }
+  if constexpr (GR) {
+    if (t == T && T > 0 && live) store_out(T - 1, pend_h, pend_c, pend_i, pend_f, pend_g, pend_o);
   }
   // gave up at step t: the rows this workgroup owns for steps t..T-1 are written as NaN, so a
   // timed-out launch never hands plausible numbers downstream (the host reports it, see above)
@@ -850,13 +988,23 @@ int lstm1_rows_per_group(int B, int H) {
 
 size_t persist_lds(int H, int RT) {
   const int nch = H / 32 / 4;
-  return (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 32 + 2 * 64 * sizeof(float);
+  return (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 32 + 2 * 64 * sizeof(float) +
+         (size_t)16 * RT * 16 * sizeof(unsigned);
+}
+
+// Does a one-layer launch of (H, RT) hand split h over as granules under the current tuning?
+// One 16-row tile per group only: a granule carries 4 B of tag per 4 B of h, and what a step costs
+// tracks the bytes each consumer wave ingests (MI355X_MICROARCH.md, handoff-payload).  Measured:
+// C5 lstm1 (RT 1) 2930 -> 2862 us, C2 lstm1 (RT 1) unchanged, C3 lstm1 (RT 2) 542 -> 721 us.
+bool persist_gran(int H, int RT) {
+  return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd == 2 && !(g_persist_qwait & 2);
 }
 
 // The template instance a launch of (H, RT) runs under the current tuning.
 const void* persist_fn(int H, int RT, bool two_layer = true) {
   const bool qw = (g_persist_qwait & (two_layer ? 1 : 2)) != 0;
   const int nch = H / 32 / 4;
+  if (!two_layer && persist_gran(H, RT)) return (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 1>;
 #define AVC_PERSIST_FN(NCHV, RTV)                                                                 \
   return g_persist_mode == 1 ? (const void*)lstm_persist_kernel<NCHV, RTV, 0, 1, 0>               \
        : g_persist_pd == 1   ? (const void*)lstm_persist_kernel<NCHV, RTV, 1, 1, 0>               \
@@ -872,10 +1020,10 @@ const void* persist_fn(int H, int RT, bool two_layer = true) {
 
 // Workgroups of instance (H, RT) the device can hold at once: the occupancy API's resident
 // workgroups per CU (LDS, VGPRs, waves) x CUs.  Cached per instance.
-int persist_capacity(int H, int RT) {
+int persist_capacity(int H, int RT, bool two_layer = true) {
   struct Entry { const void* fn; int dev; int cap; };
   static std::vector<Entry> cache;
-  const void* fn = persist_fn(H, RT);
+  const void* fn = persist_fn(H, RT, two_layer);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   for (const auto& e : cache)
@@ -1451,7 +1599,7 @@ bool lstm2_persist_eligible(int T, int B, int H) {
 bool lstm1_persist_eligible(int T, int B, int H) {
   if (g_persist_mode == 0 || !(g_persist_layers & 1) || T < 1 || B < 1 || B > 256 || !(H == 1024 || H == 512)) return false;
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
-  return ngrp * (4 * H / 64) <= persist_capacity(H, RT);
+  return ngrp * (4 * H / 64) <= persist_capacity(H, RT, false);
 }
 
 int g_persist_inproj = 1;  // avc_lstm_persist_inproj(): an input slot computes layer 0's input projection
@@ -1494,7 +1642,7 @@ size_t inproj_scratch(int T, int B, int H, int din) {
 bool lstm1_inproj_eligible(int T, int B, int H, int din) {
   if (!g_persist_inproj || din <= 256 || din > 512 || din % 8 || !lstm1_persist_eligible(T, B, H)) return false;
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
-  return 2 * ngrp * (4 * H / 64) <= persist_capacity(H, RT);
+  return 2 * ngrp * (4 * H / 64) <= persist_capacity(H, RT, false);
 }
 
 size_t lstm1_persist_scratch(int T, int B, int H, int din) {
@@ -1519,14 +1667,29 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
   const int nslot = ip ? 2 : 1;
   const long gstride = cnt_words(nslot, T, true);  // counter words per group: full + quarter lines
-  AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
+  // granule hand-off: a kGrRing-step ring per group behind the counters (zeroed with them; the
+  // tags make stale entries harmless, see gr_tag)
+  const bool gran = persist_gran(H, RT);
+  const long hg_step = (long)RT * (H / 32) * 4096;
+  const size_t cwords = ((size_t)ngrp * gstride + 63) & ~size_t(63);
+  const size_t gwords = gran ? (size_t)ngrp * kGrRing * hg_step / sizeof(unsigned) : 0;
+  unsigned char* hs0 = nullptr;
+  if (!gran) {
+    hs0 = sc.template take<unsigned char>((size_t)T * hsz);
+    if (hs0 == nullptr) return AVC_ERR_WORKSPACE;
+  }
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), (size_t)ngrp * gstride, s,
-                         &region));
+  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), cwords + gwords, s, &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = nslot; a.cnt_gstride = gstride;
+  if (gran) {
+    a.hg = reinterpret_cast<unsigned char*>(region + kRegionHeaderWords + cwords);
+    a.hg_step = hg_step;
+    a.hg_gstride = kGrRing * hg_step;
+  }
   if (ip) AVC_TRY(attach_inproj(ctx, sc, *ip, T, B, 1, a, s));
+  if (gran) a.in_lead = 1;  // (back-pressure polls slot 0's counters, which a GR launch does not add to)
   a.W[0] = reinterpret_cast<const unsigned char*>(whh_s);
   a.winv[0] = winv;
   a.gx0 = gx;
@@ -1757,6 +1920,16 @@ extern "C" int avc_lstm_persist_qwait(int mask) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_qwait = mask;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_granules(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_lstm_persist_granules: 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_gran = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

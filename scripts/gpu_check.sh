@@ -53,6 +53,7 @@ for step in "$@"; do
              for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" "TA_BUSY_avr TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
                n=$(echo $grp | cut -d' ' -f1); run gpmc3_${mode}_$n 120 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/gpmc3/${mode}_$n -o g -- python3 scripts/gemm_micro.py $mode; done; done ;;
     stamps) run stamps 300 python scripts/stamps_lstm.py ;;
+    pgran) run pgran 300 python scripts/persist_gran_ab.py ;;
     audio) run audio 600 python -m pytest tests/test_gpu_audio.py -v -m gpu -s --timeout 200 -p no:cacheprovider ;;
     benchtrain) run benchtrain 400 python bench.py --mode train --steps 5 --warmup 2 --no-cpu ;;
     benchtraincpu) run benchtraincpu 500 python bench.py --mode train --steps 5 --warmup 2 ;;

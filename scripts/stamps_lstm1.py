@@ -29,21 +29,10 @@ with torch.no_grad():
     ae(x, c, c)
 torch.cuda.synchronize()
 buf = torch.zeros(NCB * T * 8, dtype=torch.int64, device=dev)
-lib.avc_debug_stamps_persist(ctypes.c_void_p(buf.data_ptr()))
-with torch.no_grad():
-    ae(x, c, c)
-torch.cuda.synchronize()
-lib.avc_debug_stamps_persist(ctypes.c_void_p(0))
-st = buf.view(NCB, T, 8).cpu().numpy().astype(np.int64)
-names = ["poll wait", "acquire+barrier", "mfma loop", "lds reduce", "epilogue+drain"]
-s = st[:, 4:T - 4, :]
-ph = [np.median(s[:, :, i + 1] - s[:, :, i]) for i in range(5)]
-step = np.median(np.diff(st[:, 4:T - 4, 5], axis=1))
-d = np.diff(st[:, 4:T - 4, 6], axis=1) * 10.0
-print("lstm1 per-step median ticks: " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, ph)) +
-      f"; step-to-step {step:.0f} ticks, realtime {np.median(d):.0f} ns")
-if len(sys.argv) > 1:  # second measurement with the given avc_lstm_persist_qwait mask
-    _lib.call("avc_lstm_persist_qwait", int(sys.argv[1]))
+names = ["poll wait", "acquire+barrier (GR: granule wait)", "mfma loop", "lds reduce", "epilogue+drain"]
+
+
+def measure(label):
     buf.zero_()
     lib.avc_debug_stamps_persist(ctypes.c_void_p(buf.data_ptr()))
     with torch.no_grad():
@@ -55,5 +44,14 @@ if len(sys.argv) > 1:  # second measurement with the given avc_lstm_persist_qwai
     ph = [np.median(s[:, :, i + 1] - s[:, :, i]) for i in range(5)]
     step = np.median(np.diff(st[:, 4:T - 4, 5], axis=1))
     d = np.diff(st[:, 4:T - 4, 6], axis=1) * 10.0
-    print(f"qwait {sys.argv[1]}: lstm1 per-step median ticks: " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, ph)) +
-          f"; step-to-step {step:.0f} ticks, realtime {np.median(d):.0f} ns")
+    print(f"{label}: lstm1 per-step median ticks: " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, ph)) +
+          f"; step-to-step {step:.0f} ticks, realtime {np.median(d):.0f} ns", flush=True)
+
+
+measure("default")
+# further measurements after each tuning call: "granules=0" -> avc_lstm_persist_granules(0); a
+# bare integer is an avc_lstm_persist_qwait mask
+for arg in sys.argv[1:]:
+    name, val = arg.split("=") if "=" in arg else ("qwait", arg)
+    _lib.call(f"avc_lstm_persist_{name}", int(val))
+    measure(arg)
