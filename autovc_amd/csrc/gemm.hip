@@ -725,6 +725,43 @@ inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* 
   }
 }
 
+// The same stats partials from a 256-row tile: two per tile (the 128-row granularity make_plan
+// reports), each the sum of the WM / 2 waves whose rows it covers.
+template <int BM, int BN, int WM, int WTN, int TN>
+__device__ __forceinline__ void stats_256(const GemmDesc& d, unsigned char* lds, const float* csum, const float* csq,
+                                          int tm, int tn, int wm, int wn, int lane, int tid, int NT) {
+  static_assert(BM == 256 && WM % 2 == 0, "two 128-row partials per tile");
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const float s = csum[j] + __shfl_xor(csum[j], 32);
+    const float s2 = csq[j] + __shfl_xor(csq[j], 32);
+    if (lane < 32) {
+      const int cl = wn * WTN + 32 * j + lane;
+      red[(wm * 2 + 0) * BN + cl] = s;
+      red[(wm * 2 + 1) * BN + cl] = s2;
+    }
+  }
+  __syncthreads();
+  for (int cl = tid; cl < BN; cl += NT) {
+    const int col = tn * BN + cl;
+    if (col >= d.N) continue;
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      if ((tm * 2L + sp) * 128 >= d.M) break;
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = sp * (WM / 2); r < (sp + 1) * (WM / 2); ++r) {
+        s += red[(r * 2 + 0) * BN + cl];
+        s2 += red[(r * 2 + 1) * BN + cl];
+      }
+      d.stats[((tm * 2L + sp) * 2 + 0) * d.N + col] = s;
+      d.stats[((tm * 2L + sp) * 2 + 1) * d.N + col] = s2;
+    }
+  }
+}
+
 struct Frag16Args {
   const _Float16* As; int a_ntile, a_nkc; long a_shift0, a_tapshift;  // shifts in rows (x32)
   const _Float16* Bs; int b_ntile, b_nkc; long b_tapstride;            // halves per tap
@@ -867,7 +904,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbh[cb][j], part[i][j], 0, 0, 0);
+          if constexpr (KH == 2) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbh[cb][j], acc[i][j], 0, 0, 0);
+          else part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbh[cb][j], part[i][j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -881,14 +919,14 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
       __builtin_amdgcn_sched_barrier(0);
     }
 #undef AVC16F_FRAGS
-    if ((kt - kt0) % KB == KB - 1 || kt + 1 == kt1) {
+    if (KH != 2 && ((kt - kt0) % KB == KB - 1 || kt + 1 == kt1)) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
-            if constexpr (KH && OCC == 1 && !AVC_GEMM_DIAG_NOKAHAN) {
+            if constexpr (KH == 1 && OCC == 1 && !AVC_GEMM_DIAG_NOKAHAN) {
               const float y = part[i][j][e] - cmp[i][j][e];
               const float t = acc[i][j][e] + y;
               cmp[i][j][e] = (t - acc[i][j][e]) - y;
@@ -907,7 +945,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e)
-        acc[i][j][e] = (KH && OCC == 1 ? acc[i][j][e] - cmp[i][j][e] : acc[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
+        acc[i][j][e] = (KH == 1 && OCC == 1 ? acc[i][j][e] - cmp[i][j][e] : acc[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
 #undef AVC16F_ISSUE
   if (d.split_scale && nsplit == 1) {  // split-K partials stay scaled; splitk_reduce_kernel unscales
     const float us = split_unscale(d.amax_a, d.amax_b);
@@ -964,7 +1002,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
         csq[j] += v * v;
       }
   }
-  if (d.stats) {
+  if constexpr (BM == 256) {
+    if (d.stats) stats_256<BM, BN, WM, WTN, TN>(d, lds, csum, csq, tm, tn, wm, wn, lane, tid, NT);
+  } else if (d.stats) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
 #pragma unroll
@@ -1166,8 +1206,11 @@ size_t frag16_scratch(const GemmDesc& d) {
   return frag_bytes(a_rows, d.Kc) + (size_t)d.ntaps * frag_bytes(d.N, (int)frag16_b_krows(d)) + 2048;
 }
 
-// avc_gemm_config(): tile/ring variant of gemm16f for 128x128 tiles; 8 (= 1 with the plain fold of
-// the 128-k partials) measured best in round 3, 1 in rounds 1-2
+// avc_gemm_config(): tile/ring variant of gemm16f; 8 (= 1 with the plain fold of the 128-k
+// partials) is the default since round 3 (1 in rounds 1-2).  Late round 3: 9 / 10 (256 x 128 tiles)
+// and 11 (8 with the hi.hi products in one MFMA chain over K) were 0-3 % faster on single GEMMs but
+// moved the C3 step by < 0.1 ms (34.68 vs 34.72 ms) while 10 / 11 double the product's error
+// against float64 (1.9e-7 -> 3.9e-7 on the 8192 x 4096 x 512 product), so 8 stays
 int g_gemm_cfg = 8;
 
 template <int BM, int BN, int WM, int WN, int NS, int KC, int OCC = 1, int KH = 1>
@@ -1185,8 +1228,11 @@ void launch16f_cfg(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
   const int kt_per_tap = (f.a_nkc + KC - 1) / KC;
   const int ktotal = d.ntaps * kt_per_tap;
   const int kps = (ktotal + p.nsplit - 1) / p.nsplit;
-  dim3 grid(p.tilesM * p.tilesN, d.nz * p.nsplit);
-  gemm16f_kernel<BM, BN, WM, WN, NS, KC, OCC, KH><<<grid, 64 * WM * WN, lds, s>>>(d, f, p.tilesM, p.tilesN, kt_per_tap,
+  // tiles of this instance (the plan's are 128 x 128 for every big product; a 256-row instance
+  // halves tilesM and keeps the plan's split-K count)
+  const int tilesM = (d.M + BM - 1) / BM, tilesN = (d.N + BN - 1) / BN;
+  dim3 grid(tilesM * tilesN, d.nz * p.nsplit);
+  gemm16f_kernel<BM, BN, WM, WN, NS, KC, OCC, KH><<<grid, 64 * WM * WN, lds, s>>>(d, f, tilesM, tilesN, kt_per_tap,
                                                                         kps, p.nsplit, slab);
 }
 
@@ -1200,6 +1246,9 @@ void launch16f_128(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
     case 6: launch16f_cfg<128, 128, 4, 2, 2, 2, 2>(d, f, p, slab, s); break;
     case 7: launch16f_cfg<128, 128, 4, 2, 2, 4, 2>(d, f, p, slab, s); break;
     case 8: launch16f_cfg<128, 128, 4, 2, 2, 4, 1, 0>(d, f, p, slab, s); break;  // cfg 1, plain fold
+    case 9: launch16f_cfg<256, 128, 4, 2, 3, 2, 1, 0>(d, f, p, slab, s); break;  // 256-row tiles
+    case 10: launch16f_cfg<256, 128, 4, 2, 3, 2, 1, 2>(d, f, p, slab, s); break;  // ... hi.hi into one chain
+    case 11: launch16f_cfg<128, 128, 4, 2, 2, 4, 1, 2>(d, f, p, slab, s); break;  // 8 with hi.hi into one chain
     default: launch16f_cfg<128, 128, 4, 2, 4, 2>(d, f, p, slab, s); break;
   }
 }
@@ -1591,8 +1640,8 @@ extern "C" int avc_gemm_tune(int mode) {
 }
 
 extern "C" int avc_gemm_config(int cfg) {
-  if (cfg < 0 || cfg > 8) {
-    avc::set_error("avc_gemm_config: cfg must be 0..8");
+  if (cfg < 0 || cfg > 11) {
+    avc::set_error("avc_gemm_config: cfg must be 0..11");
     return AVC_ERR_INVALID;
   }
   avc::g_gemm_cfg = cfg;

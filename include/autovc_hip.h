@@ -261,7 +261,9 @@ int avc_gemm_tune(int prec16);
  * 0 = 4x2 waves, 4-stage ring of 32-deep K-tiles; 1 = 4x2, 2 stages of 64-deep K-tiles, Kahan
  * fold of the 128-k partials; 2 = 4x2, 3 stages x 48; 3 = 2x4, 4 x 32; 4 = 2x4, 2 x 64; 5 = 4x2,
  * 3 x 32; 6 / 7 = 4x2, 2 x 32 / 2 x 64 with plain (not Kahan-compensated) 128-k partial folds,
- * 128 VGPRs (two workgroups per CU for 6); 8 (default) = 1 with the plain fold. */
+ * 128 VGPRs (two workgroups per CU for 6); 8 (default) = 1 with the plain fold; 9 / 10 = 256 x 128 tiles,
+ * 3 stages x 32, plain fold / hi.hi products in one MFMA chain over K; 11 = 8 with the hi.hi
+ * products in one chain (no 128-k partials).  Default 8. */
 int avc_gemm_config(int cfg);
 /* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) and decoder lstm1 (one layer,
  * batch <= 256) as ONE weight-stationary launch each (lstm_persist.hip) instead of one launch per

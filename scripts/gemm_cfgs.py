@@ -54,4 +54,4 @@ with torch.no_grad():
         same = all(torch.equal(p, q) for p, q in zip(outs, ref))
         print(f"cfg {cfg:2d}: conv+BN {tc:7.1f} us  lstm2-proj {tl:7.1f} us  C2 forward {tf / 1e3:6.3f} ms  "
               f"bit-identical {same}", flush=True)
-_lib.call("avc_gemm_config", 1)
+_lib.call("avc_gemm_config", 8)

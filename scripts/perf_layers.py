@@ -27,7 +27,7 @@ def main():
     for c in cfgs:
         _lib.call("avc_gemm_config", c)
         run(f"cfg{c}")
-    _lib.call("avc_gemm_config", 1)
+    _lib.call("avc_gemm_config", 8)
 
 
 def run(tag):

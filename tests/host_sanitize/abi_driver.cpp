@@ -46,8 +46,10 @@ static void host_only() {
   CHECK(avc_wavernn_fold_shape(8800, 0, 0, 0, &rows, &steps) == AVC_OK && rows == 1 && steps == 8800);
   CHECK(avc_wavernn_fold_shape(0, 1, 1, 1, &rows, &steps) == AVC_ERR_INVALID);
   // tuning hooks: valid values accepted, invalid ones rejected with a message
-  CHECK(avc_gemm_config(9) == AVC_ERR_INVALID);
-  CHECK(avc_gemm_config(1) == AVC_OK);
+  CHECK(avc_gemm_config(12) == AVC_ERR_INVALID);
+  CHECK(avc_gemm_config(8) == AVC_OK);
+  CHECK(avc_lstm_persist_granules(2) == AVC_ERR_INVALID);
+  CHECK(avc_lstm_persist_granules(1) == AVC_OK);
   CHECK(avc_lstm_tune(17, 0) == AVC_ERR_INVALID);
   CHECK(avc_lstm_tune(0, 0) == AVC_OK);
   CHECK(avc_lstm_persist_tune(3) == AVC_ERR_INVALID);

@@ -294,9 +294,9 @@ def test_conv_fragment_path(cuda_device, B, T, cin, cout):
     assert (out_cf - y).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 def test_gemm16f_configs(cuda_device, cfg):
-    """Every 128x128 variant of the pre-split split-f16 GEMM (avc_gemm_config): a Linear with
+    """Every variant of the pre-split split-f16 GEMM (avc_gemm_config; 9 / 10: 256-row tiles): a Linear with
     a ragged K (336: the 64-deep K-tiles end half out of range) and N (1040: a partial column
     tile), and a 512->512 Conv1d k5 + BN whose taps are 32-row tile shifts, against fp64."""
     g = torch.Generator().manual_seed(1000 + cfg)
@@ -322,7 +322,7 @@ def test_gemm16f_configs(cuda_device, cfg):
                                       1e-5, ops.ACT_NONE, None, T, B)
         torch.cuda.synchronize()
     finally:
-        _lib.call("avc_gemm_config", 1)
+        _lib.call("avc_gemm_config", 8)  # the library default
     err = (y.cpu().double() - ref).abs().max().item()
     assert err < 2e-6 * max(1.0, ref.abs().max().item()), err
     out_cf = out.cpu().reshape(T, B, cout).permute(1, 2, 0).double()
