@@ -25,8 +25,8 @@ class Decoder(nn.Module):
     def frames(self, x, T, B, save):
         """x [T*B][320] time-major frames -> decoder output frames [T*B][80]."""
         h = ops.LSTMLayer.apply(x, *self.lstm1.layer(0), T, B, save)
-        for conv in self.convolutions:
-            h = conv_bn(conv, h, T, B, ops.ACT_RELU)
+        for i, conv in enumerate(self.convolutions):
+            h = conv_bn(conv, h, T, B, ops.ACT_RELU, emit_frag=i + 1 < len(self.convolutions))
         for l in range(2):
             h = ops.LSTMLayer.apply(h, *self.lstm2.layer(l), T, B, save)
         lin = self.linear_projection.linear_layer

@@ -5,15 +5,16 @@ from .. import ops
 from .net_layers import ConvNorm, LSTMParams
 
 
-def conv_bn(seq, x, T, B, act, residual=None):
-    """Sequential(ConvNorm, BatchNorm1d) + act on time-major frames, honouring bn.training."""
+def conv_bn(seq, x, T, B, act, residual=None, emit_frag=False):
+    """Sequential(ConvNorm, BatchNorm1d) + act on time-major frames, honouring bn.training.
+    emit_frag: the next op is another conv (its input also handed over as a split image)."""
     conv, bn = seq[0].conv, seq[1]
     training = bn.training or bn.running_mean is None
     if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
         bn.num_batches_tracked.add_(1)
     momentum = 0.1 if bn.momentum is None else bn.momentum
     return ops.ConvBNAct.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean,
-                               bn.running_var, training, momentum, bn.eps, act, residual, T, B)
+                               bn.running_var, training, momentum, bn.eps, act, residual, T, B, emit_frag)
 
 
 class Encoder(nn.Module):
@@ -38,8 +39,8 @@ class Encoder(nn.Module):
         """x (B,80,T), c_org (B,256) -> BiLSTM outputs [T*B][64] (fwd || bwd)."""
         B, _, T = x.shape
         h = ops.FramesFromMel.apply(x, c_org)
-        for conv in self.convolutions:
-            h = conv_bn(conv, h, T, B, ops.ACT_RELU)
+        for i, conv in enumerate(self.convolutions):
+            h = conv_bn(conv, h, T, B, ops.ACT_RELU, emit_frag=i + 1 < len(self.convolutions))
         for l in range(2):
             h = ops.BiLSTMLayer.apply(h, *self.lstm.layer(l), *self.lstm.layer(l, True), T, B, save)
         return h

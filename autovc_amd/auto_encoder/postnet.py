@@ -26,7 +26,7 @@ class Postnet(nn.Module):
     def frames(self, x, T, B, residual=None):
         """x [T*B][80] -> postnet(x) (+ residual) frames [T*B][80]."""
         for i in range(len(self.convolutions) - 1):
-            x = conv_bn(self.convolutions[i], x, T, B, ops.ACT_TANH)
+            x = conv_bn(self.convolutions[i], x, T, B, ops.ACT_TANH, emit_frag=True)
         return conv_bn(self.convolutions[-1], x, T, B, ops.ACT_NONE, residual)
 
     def forward(self, x):

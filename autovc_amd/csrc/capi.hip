@@ -284,6 +284,33 @@ int avc_conv_bn_act_forward_ex(avc_context* ctx, int T, int B, int cin, int cout
                                   mean, invstd, S(stream), nullptr, nullptr, x_amax, out_amax);
 }
 
+int avc_conv_bn_act_forward_frag(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                                 const void* x_frag, const float* weight, const float* bias, const float* gamma,
+                                 const float* beta, float* running_mean, float* running_var, int training,
+                                 float momentum, float eps, int act, const float* residual, float* y_pre,
+                                 float* out, void* out_frag, float* mean, float* invstd, const unsigned* x_amax,
+                                 unsigned* out_amax, void* stream) {
+  AVC_CHECK_ARG(ctx && x && weight && gamma && beta && y_pre && out && mean && invstd, "NULL pointer");
+  AVC_CHECK_ARG(aligned16(x_amax) && aligned16(out_amax), "amax words must be 16-byte aligned");
+  AVC_CHECK_ARG(aligned16(x_frag) && aligned16(out_frag), "split images must be 16-byte aligned");
+  AVC_CHECK_ARG(!x_frag || conv_frag_chain_ok(T, B, cin, cout),
+                "conv forward: a split input needs B % 32 == 0 and cin % 8 == 0 (avc_conv_frag_chain_ok)");
+  AVC_CHECK_ARG(!out_frag || cout % 8 == 0, "conv forward: a split output needs cout % 8 == 0");
+  AVC_TRY(ensure_arena(ctx, conv_bn_forward_scratch(T, B, cin, cout)));
+  return conv_bn_act_forward_impl(ctx, T, B, cin, cout, x, weight, bias, gamma, beta, running_mean,
+                                  running_var, training, momentum, eps, act, residual, y_pre, out,
+                                  mean, invstd, S(stream), static_cast<const _Float16*>(x_frag),
+                                  static_cast<_Float16*>(out_frag), x_amax, out_amax);
+}
+
+int avc_conv_frag_chain_ok(int T, int B, int cin, int cout) {
+  return T > 0 && B > 0 && cin > 0 && cout > 0 && conv_frag_chain_ok(T, B, cin, cout) ? 1 : 0;
+}
+
+size_t avc_act_frag_bytes(long rows, int channels) {
+  return rows > 0 && channels > 0 ? gemm_afrag_bytes(rows, channels) : 0;
+}
+
 int avc_conv_bn_act_backward_ex(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
                                 const float* weight, const float* gamma, const float* beta,
                                 const float* y_pre, const float* mean, const float* invstd,

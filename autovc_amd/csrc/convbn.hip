@@ -77,7 +77,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   // x_frag: x already split (the previous layer's bn_apply wrote it); out_frag: also emit the
   // output split for the next layer (out may then be NULL: the fp32 output is not stored).
   // x_amax: x's max words from its producer (see bn_apply's amax_out): the range scan of x is
-  // skipped; out_amax: record out's max words for the next layer (fp32 output path only)
+  // skipped; out_amax: record out's max words for the next layer (with or without out_frag)
   AVC_CHECK_ARG(T > 0 && B > 0, "conv: empty input");
   AVC_CHECK_ARG(cin % 4 == 0 && cout % 4 == 0, "conv: channel counts must be multiples of 4");
   AVC_CHECK_ARG(training || (running_mean && running_var), "conv: eval mode needs running stats");
@@ -93,7 +93,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   GemmDesc g = conv_fwd_desc(T, B, cin, cout, x, wt, bias, y_pre);
   g.a_frag = x_frag;
   if (x_amax) g.a_guard = x_amax + 1;
-  if (out_frag || !out) out_amax = nullptr;
+  if (!out && !out_frag) out_amax = nullptr;
   if (ctx->prep_version >= 0) {  // cache the split-f16 copy of the taps as well
     bool fb = true;
     auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_CONV_BFRAG, weight, nullptr, gemm_bfrag_bytes(g), &fb));

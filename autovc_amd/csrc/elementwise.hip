@@ -208,8 +208,10 @@ __global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int n
                                                             const float* __restrict__ residual,
                                                             float* __restrict__ out,
                                                             _Float16* __restrict__ frag,
-                                                            unsigned* __restrict__ range_flag) {
+                                                            unsigned* __restrict__ range_flag,
+                                                            unsigned* __restrict__ amax_out) {
   const int G8 = nkc * 2;
+  float amax = 0.f;  // max |out| of this thread's elements (amax_out: see bn_apply_kernel)
   const long total = ntile * 32 * G8;
   // per-channel scale / shift formed once per workgroup in LDS (same expressions as
   // bn_apply_kernel), so the element loop issues two float4 loads instead of 32 parameter loads
@@ -224,8 +226,8 @@ __global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int n
     __syncthreads();
   }
   const unsigned q4 = (unsigned)(G8 >> 2);
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x) {
+  // item idx -> (row r, 8-channel group g8): tile-quad major, then row, then group (4 per quad)
+  auto coords = [&](long idx, long& r, int& g8) {
     const int gq = (int)(idx & 3);
     const long rest = idx >> 2;
     const int rr = (int)(rest & 31);
@@ -233,57 +235,101 @@ __global__ __launch_bounds__(256) void bn_apply_frag_kernel(long M, int C, int n
     // 32-bit division where the tile-quad index fits (always, below 2^32 quads)
     const long t = tq < 0xffffffffL ? (long)((unsigned)tq / q4) : tq / (long)q4;
     const int quad = (int)(tq - t * (long)q4);
-    const long r = t * 32 + rr;
-    const int g8 = quad * 4 + gq, k0 = 8 * g8;
-    float o[8];
-    if (r < M && k0 < C) {  // C % 8 == 0: a group is all in or all out
-      const float4* q = reinterpret_cast<const float4*>(y + r * C + k0);
-      const float4 a = q[0], b = q[1];
-      o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
-      if (lds) {
+    r = t * 32 + rr;
+    g8 = quad * 4 + gq;
+  };
+  // IT items per thread per pass, all loads issued before any store (the grid is capped when max
+  // words are recorded, so each thread walks several items: without this they go one round trip
+  // at a time)
+  constexpr int IT = 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long base = blockIdx.x * (long)blockDim.x + threadIdx.x; base < total; base += IT * stride) {
+    float4 ya[IT], yb[IT], ra[IT], rb[IT];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = act_fwd(o[e] * s_sc[k0 + e] + s_sh[k0 + e], act);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int c = k0 + e;
-          const float sc = invstd[c] * gamma[c];
-          const float sh = beta[c] - mean[c] * sc;
-          o[e] = act_fwd(o[e] * sc + sh, act);
+    for (int u = 0; u < IT; ++u) {
+      const long idx = base + u * stride;
+      long r;
+      int g8;
+      coords(idx, r, g8);
+      const int k0 = 8 * g8;
+      if (idx < total && r < M && k0 < C) {  // C % 8 == 0: a group is all in or all out
+        const float4* q = reinterpret_cast<const float4*>(y + r * C + k0);
+        ya[u] = q[0];
+        yb[u] = q[1];
+        if (residual) {
+          const float4* rq = reinterpret_cast<const float4*>(residual + r * C + k0);
+          ra[u] = rq[0];
+          rb[u] = rq[1];
         }
       }
-      if (residual) {
-        const float4* rq = reinterpret_cast<const float4*>(residual + r * C + k0);
-        const float4 ra = rq[0], rb = rq[1];
-        o[0] += ra.x; o[1] += ra.y; o[2] += ra.z; o[3] += ra.w;
-        o[4] += rb.x; o[5] += rb.y; o[6] += rb.z; o[7] += rb.w;
-      }
-      if (out) {
-        float4* oq = reinterpret_cast<float4*>(out + r * C + k0);
-        oq[0] = make_float4(o[0], o[1], o[2], o[3]);
-        oq[1] = make_float4(o[4], o[5], o[6], o[7]);
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = 0.f;
     }
-    h16x8 hi, lo;
-    bool over = false;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const _Float16 h = (_Float16)o[j];
-      hi[j] = h;
-      lo[j] = (_Float16)((o[j] - (float)h) * 2048.0f);
-      over |= fabsf(o[j]) >= 65504.f && fabsf(o[j]) < __builtin_inff();
+    for (int u = 0; u < IT; ++u) {
+      const long idx = base + u * stride;
+      if (idx >= total) break;
+      long r;
+      int g8;
+      coords(idx, r, g8);
+      const int k0 = 8 * g8;
+      float o[8];
+      if (r < M && k0 < C) {
+        o[0] = ya[u].x; o[1] = ya[u].y; o[2] = ya[u].z; o[3] = ya[u].w;
+        o[4] = yb[u].x; o[5] = yb[u].y; o[6] = yb[u].z; o[7] = yb[u].w;
+        if (lds) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = act_fwd(o[e] * s_sc[k0 + e] + s_sh[k0 + e], act);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int c = k0 + e;
+            const float sc = invstd[c] * gamma[c];
+            const float sh = beta[c] - mean[c] * sc;
+            o[e] = act_fwd(o[e] * sc + sh, act);
+          }
+        }
+        if (residual) {
+          o[0] += ra[u].x; o[1] += ra[u].y; o[2] += ra[u].z; o[3] += ra[u].w;
+          o[4] += rb[u].x; o[5] += rb[u].y; o[6] += rb[u].z; o[7] += rb[u].w;
+        }
+        if (out) {
+          float4* oq = reinterpret_cast<float4*>(out + r * C + k0);
+          oq[0] = make_float4(o[0], o[1], o[2], o[3]);
+          oq[1] = make_float4(o[4], o[5], o[6], o[7]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = 0.f;
+      }
+      h16x8 hi, lo;
+      bool over = false;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        amax = fmaxf(amax, fabsf(o[j]));
+        const _Float16 h = (_Float16)o[j];
+        hi[j] = h;
+        lo[j] = (_Float16)((o[j] - (float)h) * 2048.0f);
+        over |= fabsf(o[j]) >= 65504.f && fabsf(o[j]) < __builtin_inff();
+      }
+      // range guard of the conv -> conv hand-over: a finite activation the f16 split cannot hold
+      // (a BatchNorm affine far outside any trained range) is reported to the host (pinned word),
+      // and the next call on the context fails with AVC_ERR_DEVICE
+      if (over && range_flag) __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const long blk = ((r >> 5) * nkc + (g8 >> 1)) * 2;
+      const int lane = (int)(r & 31) + 32 * (g8 & 1);
+      *reinterpret_cast<h16x8*>(frag + blk * 512 + lane * 8) = hi;
+      *reinterpret_cast<h16x8*>(frag + (blk + 1) * 512 + lane * 8) = lo;
     }
-    // range guard of the conv -> conv hand-over: a finite activation the f16 split cannot hold
-    // (a BatchNorm affine far outside any trained range) is reported to the host (pinned word),
-    // and the next call on the context fails with AVC_ERR_DEVICE
-    if (over && range_flag) __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const long blk = ((r >> 5) * nkc + (g8 >> 1)) * 2;
-    const int lane = (int)(r & 31) + 32 * (g8 & 1);
-    *reinterpret_cast<h16x8*>(frag + blk * 512 + lane * 8) = hi;
-    *reinterpret_cast<h16x8*>(frag + (blk + 1) * 512 + lane * 8) = lo;
+  }
+  if (amax_out) {
+    __shared__ float red[4];
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      amax_update(amax_out, m);
+      amax_update(amax_out + 1, fmaxf(m, 16384.f));
+    }
   }
 }
 
@@ -915,8 +961,9 @@ int bn_apply(long M, int C, const float* y, const float* mean, const float* invs
     const int nkc = (C + 31) / 32 * 2;
     const long ntile = (M + 31) / 32;
     const long total = ntile * 32 * nkc * 2;
-    bn_apply_frag_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(
-        M, C, nkc, ntile, y, mean, invstd, gamma, beta, act, residual, out, frag, range_flag);
+    // with max words every workgroup ends in an atomic max on one word: fewer, longer workgroups
+    bn_apply_frag_kernel<<<(int)std::min<long>((total + 255) / 256, amax_out ? 512 : 8192), 256, 0, s>>>(
+        M, C, nkc, ntile, y, mean, invstd, gamma, beta, act, residual, out, frag, range_flag, amax_out);
     AVC_LAUNCH_CHECK();
     return AVC_OK;
   }

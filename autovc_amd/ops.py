@@ -175,13 +175,41 @@ def _amax_of(x):
     return rec[0]
 
 
+# AUTOVC_FRAG_CHAIN=0: conv -> conv chains hand over fp32 only (A/B measurements)
+_FRAG_CHAIN = os.environ.get("AUTOVC_FRAG_CHAIN", "1") != "0"
+_frag_ok_cache = {}
+
+
+def frag_chain_ok(T, B, cin):
+    """Can a conv over [T*B][cin] frames take its input as a split image (avc_conv_frag_chain_ok)?"""
+    key = (T, B, cin)
+    ok = _frag_ok_cache.get(key)
+    if ok is None:
+        ok = _frag_ok_cache[key] = bool(_lib.load().avc_conv_frag_chain_ok(T, B, cin, 8))
+    return ok and _FRAG_CHAIN
+
+
+def _take_frag(x):
+    """The split image a ConvBNAct forward emitted for x (its output), if x is that very tensor and
+    unmodified since; the record is dropped once taken (one consumer per activation)."""
+    rec = x.__dict__.pop("_avc_frag", None)
+    if rec is None or rec[1] != x._version or not _FRAG_CHAIN:
+        return None
+    return rec[0]
+
+
 class ConvBNAct(torch.autograd.Function):
     """ConvNorm(k=5,p=2) -> BatchNorm1d -> act [+ residual]  (net_layers.py:39-49,
-    encoder.py:69-70, decoder.py:69-70, postnet.py:54-61, model.py:131-132)."""
+    encoder.py:69-70, decoder.py:69-70, postnet.py:54-61, model.py:131-132).
+
+    emit_frag: the caller's next op is a conv of the same frames (a conv -> conv chain): the
+    output is also written as the split-f16 image that conv's product streams, so the consumer
+    skips its range scan and its split of x (avc_conv_bn_act_forward_frag; bit-identical)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, running_mean, running_var, training, momentum,
-                eps, act, residual, T, B):
+                eps, act, residual, T, B, emit_frag=False):
+        x_frag = _take_frag(x)
         x = x.contiguous()
         cout, cin, _ = weight.shape
         y_pre = _empty((T * B, cout), x)
@@ -192,11 +220,20 @@ class ConvBNAct(torch.autograd.Function):
         # producer records them while writing; the consumer skips its own scans of x
         x_amax = _amax_of(x)
         out_amax = torch.empty(4, dtype=torch.int32, device=x.device)
-        call("avc_conv_bn_act_forward_ex", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
-             ptr(_c(bias)), ptr(gamma), ptr(beta), ptr(running_mean), ptr(running_var),
-             int(training), float(momentum), float(eps), act, ptr(_c(residual)), ptr(y_pre), ptr(out),
-             ptr(mean), ptr(invstd), _wptr(x_amax), _wptr(out_amax), _stream(x))
+        if x_frag is not None and not frag_chain_ok(T, B, cin):
+            x_frag = None
+        out_frag = None
+        if emit_frag and frag_chain_ok(T, B, cout):
+            out_frag = torch.empty(int(_lib.load().avc_act_frag_bytes(T * B, cout)), dtype=torch.uint8,
+                                   device=x.device)
+        call("avc_conv_bn_act_forward_frag", _ctx(x), T, B, cin, cout, ptr(x), _wptr(x_frag),
+             ptr(weight.contiguous()), ptr(_c(bias)), ptr(gamma), ptr(beta), ptr(running_mean),
+             ptr(running_var), int(training), float(momentum), float(eps), act, ptr(_c(residual)),
+             ptr(y_pre), ptr(out), _wptr(out_frag), ptr(mean), ptr(invstd), _wptr(x_amax),
+             _wptr(out_amax), _stream(x))
         out._avc_amax = (out_amax, out._version)
+        if out_frag is not None:
+            out._avc_frag = (out_frag, out._version)
         _use(weight, bias, gamma, beta)
         ctx.save_for_backward(x, weight, gamma, beta, y_pre, mean, invstd)
         ctx.bias = bias
@@ -218,7 +255,7 @@ class ConvBNAct(torch.autograd.Function):
              ptr(dx), ptr(dw), ptr(db), ptr(dg), ptr(dbt), 2 if direct else 0, _wptr(ctx.x_amax), _stream(x))
         d_res = d_out if (has_res and ng[11]) else None
         dw, db, dg, dbt = _param_done(params, (dw, db, dg, dbt), direct)
-        return dx, dw, db, dg, dbt, None, None, None, None, None, None, d_res, None, None
+        return dx, dw, db, dg, dbt, None, None, None, None, None, None, d_res, None, None, None
 
 
 def _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, reverse, save, T, B):

@@ -107,6 +107,23 @@ int avc_conv_bn_act_backward_ex(avc_context* ctx, int T, int B, int cin, int cou
                                 int training, int act, const float* d_out, float* d_x,
                                 float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
                                 int accumulate, const unsigned* x_amax, void* stream);
+/* The forward of _ex handing the activation over ALSO as the split-f16 fragment image the next
+ * conv's product streams (the training path's conv -> conv chains: encoder.py:69-70,
+ * decoder.py:69-70, postnet.py:54-61).  out_frag (avc_act_frag_bytes(T*B, cout) bytes, 16-byte
+ * aligned, may be NULL) receives act(BN(y_pre)) split hi/lo while `out` is written, range-checked
+ * as the fused forward's hand-over is; x_frag (NULL, or the previous layer's out_frag for exactly
+ * the current contents of x) replaces the range scan and the split of x.  Requires
+ * avc_conv_frag_chain_ok(T, B, cin, cout) for x_frag.  Results are bit-identical to _ex. */
+int avc_conv_bn_act_forward_frag(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                                 const void* x_frag, const float* weight, const float* bias, const float* gamma,
+                                 const float* beta, float* running_mean, float* running_var, int training,
+                                 float momentum, float eps, int act, const float* residual, float* y_pre,
+                                 float* out, void* out_frag, float* mean, float* invstd, const unsigned* x_amax,
+                                 unsigned* out_amax, void* stream);
+/* 1 if a conv of this shape can take its input as a split image (B % 32 == 0, cin % 8 == 0) */
+int avc_conv_frag_chain_ok(int T, int B, int cin, int cout);
+/* bytes of the split image of a [rows][channels] activation (0 for an empty one) */
+size_t avc_act_frag_bytes(long rows, int channels);
 
 /* ---- LSTM layer (one direction) -----------------------------------------------------------
  * Replaces one layer-direction of nn.LSTM (gates i,f,g,o; zero initial state) as used at

@@ -294,7 +294,7 @@ def test_conv_fragment_path(cuda_device, B, T, cin, cout):
     assert (out_cf - y).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("cfg", list(range(12)))
 def test_gemm16f_configs(cuda_device, cfg):
     """Every variant of the pre-split split-f16 GEMM (avc_gemm_config; 9 / 10: 256-row tiles): a Linear with
     a ragged K (336: the 64-deep K-tiles end half out of range) and N (1040: a partial column
