@@ -854,11 +854,72 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = cmp[i][j] = part[i][j] = crs[i][j] = zero16;
 
+  // Fast issue (round 3).  The macro above spends ~300 scalar instructions of index math per
+  // K-tile per wave, and the CU's one scalar unit issues at most one per cycle for all 8 waves:
+  // 2 x 348 per SIMD per K-tile against 1536 cycles of MFMA work was the kernel's bound.  Here
+  // every piece's VGPR offset (tile row / column, hi / lo, lane, and the conv tap's shift) is
+  // formed once per tap, and a K-tile adds one SGPR offset (its 16-deep chunk index; buffer
+  // bounds checks see the VGPR part only, so out-of-range pieces stay at kOut).  Same bytes,
+  // same LDS image: bit-identical.  Waves whose pieces straddle A and B, and K-tiles that run
+  // past K, keep the macro.
+  const bool wave_a = (w + 1) * DPW <= ABLK, wave_b = w * DPW >= ABLK;
+  unsigned voff[DPW];
+  int itau = kt0 / kt_per_tap, ikin = kt0 - itau * kt_per_tap;  // the next K-tile to issue
+  int vtau = -1;                                                 // the tap voff was formed for
+  // (macros, not lambdas: a lambda here left the kernel's host-side handle undefined)
+#define AVC16F_SETTAP(TAU)                                                                        \
+  {                                                                                               \
+    _Pragma("unroll") for (int i = 0; i < DPW; ++i) {                                             \
+      const int b = w * DPW + i;                                                                  \
+      if (wave_a) {                                                                               \
+        const int rt = b / (2 * KC), kc = (b >> 1) % KC, hl = b & 1;                              \
+        const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)(TAU) * a_tapshift) / 32; \
+        voff[i] = src_tile >= 0 && src_tile < a_ntile                                             \
+                      ? (unsigned)(((src_tile * a_nkc + kc) * 2 + hl) * 1024) + lane * 16 : kOut; \
+      } else {                                                                                    \
+        const int bb = b - ABLK;                                                                  \
+        const int ct = bb / (2 * KC), kc = (bb >> 1) % KC, hl = bb & 1;                           \
+        const int src_tile = tn * (BN / 32) + ct;                                                 \
+        voff[i] = src_tile < b_ntile                                                              \
+                      ? (unsigned)((TAU) * b_tapstride * 2 + ((long)(src_tile * b_nkc + kc) * 2 + hl) * 1024) + lane * 16 \
+                      : kOut;                                                                     \
+      }                                                                                           \
+    }                                                                                             \
+    vtau = (TAU);                                                                                 \
+  }
+#define AVC16F_FAST_ISSUE(KT, ST)                                                                 \
+  {                                                                                               \
+    const int kc0f = ikin * KC;                                                                   \
+    const bool inside = wave_a ? kc0f + KC <= a_nkc : (wave_b && kc0f + bzs >= 0 && kc0f + KC + bzs <= b_nkc); \
+    if (!inside) {                                                                                \
+      AVC16F_ISSUE(KT, ST)                                                                        \
+    } else {                                                                                      \
+      if (itau != vtau) AVC16F_SETTAP(itau)                                                       \
+      unsigned char* const fbase = lds + (ST) * STAGE;                                            \
+      const int so = (wave_a ? kc0f : kc0f + bzs) * 2048;                                         \
+      _Pragma("unroll") for (int i = 0; i < DPW; ++i) {                                           \
+        unsigned char* dst = fbase + (w * DPW + i) * 1024;                                        \
+        const unsigned vo = voff[i]; /* (an array element as the builtin's argument drops the  \
+                                        kernel's host-side handle: ROCm 7.2 hipcc) */             \
+        if (AVC_GEMM_NOLOAD) {                                                                    \
+        } else if (wave_a) {                                                                      \
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)dst, 16, vo, so, 0, 0); \
+        } else {                                                                                  \
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16, vo, so, 0, 0); \
+        }                                                                                         \
+      }                                                                                           \
+    }                                                                                             \
+    if (++ikin == kt_per_tap) {                                                                   \
+      ikin = 0;                                                                                   \
+      ++itau;                                                                                     \
+    }                                                                                             \
+  }
+
   constexpr int KB = 8 / KC;  // K-tiles (128 k) per compensated partial
   // NS-stage ring: NS-1 K-tiles in flight ahead of the one being consumed
 #pragma unroll
   for (int pre = 0; pre < NS - 1; ++pre)  // (not `i`: the macro's own loop variable)
-    if (kt0 + pre < kt1) AVC16F_ISSUE(kt0 + pre, pre);
+    if (kt0 + pre < kt1) AVC16F_FAST_ISSUE(kt0 + pre, pre);
   for (int kt = kt0; kt < kt1; ++kt) {
     const int st = (kt - kt0) % NS;
     // this wave's blocks of tile kt have landed once at most the later tiles' DPW each are pending
@@ -873,7 +934,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + NS - 1 < kt1) AVC16F_ISSUE(kt + NS - 1, (kt + NS - 1 - kt0) % NS);
+    if (kt + NS - 1 < kt1) AVC16F_FAST_ISSUE(kt + NS - 1, (kt + NS - 1 - kt0) % NS);
     const unsigned char* Ai = lds + st * STAGE;
     const unsigned char* Bi = Ai + ABLK * 1024;
     // Fragments of chunk s + 1 are read while chunk s's MFMAs issue (two register buffers), and
@@ -947,6 +1008,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
       for (int e = 0; e < 16; ++e)
         acc[i][j][e] = (KH == 1 && OCC == 1 ? acc[i][j][e] - cmp[i][j][e] : acc[i][j][e]) + crs[i][j][e] * (1.0f / 2048.0f);
 #undef AVC16F_ISSUE
+#undef AVC16F_SETTAP
+#undef AVC16F_FAST_ISSUE
   if (d.split_scale && nsplit == 1) {  // split-K partials stay scaled; splitk_reduce_kernel unscales
     const float us = split_unscale(d.amax_a, d.amax_b);
 #pragma unroll
