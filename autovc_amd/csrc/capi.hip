@@ -609,6 +609,13 @@ int avc_generator_forward_cached(avc_context* ctx, int T, int B, const float* co
                     g.params.size() == (size_t)P_COUNT &&
                     std::equal(g.params.begin(), g.params.end(), params);
   ctx->prep_version = weights_version;
+  // the derived-weight cache is live only inside this call: every exit (the graph replays return
+  // early) drops it again, or a later per-layer call (training between conversions) would take
+  // derived weights cached for an older version of the same tensors
+  struct PrepScope {
+    avc_context* c;
+    ~PrepScope() { c->prep_version = -1; }
+  } prep_scope{ctx};
   int rc = AVC_OK;
   if (same && !timing && g_graph_mode && (g.exec || g.seen >= 1)) {
     if (!g.exec) {

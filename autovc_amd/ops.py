@@ -175,8 +175,10 @@ def _amax_of(x):
     return rec[0]
 
 
-# AUTOVC_FRAG_CHAIN=0: conv -> conv chains hand over fp32 only (A/B measurements)
-_FRAG_CHAIN = os.environ.get("AUTOVC_FRAG_CHAIN", "1") != "0"
+# AUTOVC_FRAG_CHAIN=1: conv -> conv chains of the per-layer path also hand over the split image
+# (off by default: it measured no C3 gain, and a handed-over image cannot hold |x| >= 65504, which
+# the fp32 hand-over's guard-scaled split of the consumer handles)
+_FRAG_CHAIN = os.environ.get("AUTOVC_FRAG_CHAIN", "0") == "1"
 _frag_ok_cache = {}
 
 

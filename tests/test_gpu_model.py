@@ -422,3 +422,38 @@ def test_c1_real_mel_end_to_end(cuda_device, mode):
         err = np.abs(got.cpu().numpy() - g[f"{name}_{mode}"]).max()
         print(f"C1 {mode} {name}: max|d| = {err:.2e}")
         assert err <= TOL_MEL, name
+
+
+def test_per_layer_calls_after_cached_graph_replays_see_new_weights(cuda_device):
+    """The derived-weight cache of avc_generator_forward_cached is live only inside that call.
+    Regression (round 3): a replay of a graph captured on the caller's own I/O pointers returned
+    with the cache still live, so a later per-layer forward (training between conversions) took
+    conv layouts derived for the older weights of the same tensors.  Here: conversions replayed
+    from direct graphs, then the weights change in place, then a per-layer forward must equal the
+    same forward of a fresh model holding the new weights."""
+    from autovc_amd import _lib
+    from autovc_amd.weights import synthetic_embedding, synthetic_mel
+    B, T = 16, 64
+    x = _t(synthetic_mel(91, B, T), cuda_device)
+    co, ct = _t(synthetic_embedding(92, B), cuda_device), _t(synthetic_embedding(93, B), cuda_device)
+    ae = make_model(cuda_device, False)
+    params, version = ae._gen_params()
+    outs = [torch.empty_like(x), torch.empty_like(x), torch.empty(B, 32 * (T // 32 + (T + 31) // 32), device=cuda_device)]
+    with torch.no_grad():
+        for _ in range(4):  # eager, staging-graph capture, then direct-graph capture and replay
+            _lib.call("avc_generator_forward_cached", _lib.context(x.device), T, B, params, version,
+                      _lib.ptr(x), _lib.ptr(co), _lib.ptr(ct), 0, *[_lib.ptr(o) for o in outs],
+                      _lib.stream(x.device))
+        torch.cuda.synchronize()
+        for name, p in ae.named_parameters():
+            if "convolutions" in name and name.endswith("conv.weight"):
+                p.mul_(1.5)
+    sd = {k: v.detach().clone() for k, v in ae.state_dict().items()}
+    ae.fused_autograd = False
+    got = ae._forward_layers(x, co, ct)
+    fresh = AutoEncoder(device=cuda_device, verbose=False)
+    fresh.load_state_dict(sd)
+    fresh.to(cuda_device).eval()
+    ref = fresh._forward_layers(x, co, ct)
+    for a, b in zip(got, ref):
+        assert torch.equal(a.detach(), b.detach())

@@ -84,14 +84,48 @@ def test_train_step_after_timeout_raises(cuda_device):
     keep = [t.detach().clone() for t in (ae._flat_param, ae.optimiser.exp_avg, ae.optimiser.exp_avg_sq,
                                           ae.avg_params)]
     _lib.call("avc_debug_persist_inject", 1)
-    loss, norm = ae.train_step(X, c)
-    assert not torch.isfinite(loss).item()
-    assert not torch.isfinite(norm).item()
-    # the fused clip/Adam/EMA skipped the update: nothing was poisoned with NaN
+    # The give-up reaches the host word asynchronously: a later persistent call of the SAME step
+    # may already see it and raise (the step stops before its update), or the step completes with
+    # a non-finite loss and norm and the fused clip/Adam/EMA skips the update; the next call raises.
+    # Either way nothing was updated or poisoned with NaN.
+    try:
+        loss, norm = ae.train_step(X, c)
+    except RuntimeError as e:
+        assert "abandoned a bounded wait" in str(e)
+    else:
+        assert not torch.isfinite(loss).item()
+        assert not torch.isfinite(norm).item()
+        with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+            ae.train_step(X, c)
     for a, b in zip(keep, (ae._flat_param, ae.optimiser.exp_avg, ae.optimiser.exp_avg_sq, ae.avg_params)):
         assert torch.equal(a, b)
-    with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
-        ae.train_step(X, c)
+
+
+def test_non_finite_gradient_skips_the_update(cuda_device):
+    """What a give-up leaves behind, made deterministic: a NaN in the flat gradient makes the
+    fused clip/Adam/EMA skip the whole update (parameters, both moments and the EMA unchanged) and
+    report a non-finite norm; a finite gradient afterwards updates normally."""
+    ae = _model(cuda_device)
+    B, T = 32, 64
+    X = torch.from_numpy(synthetic_mel(75, B, T)).to(cuda_device)
+    c = torch.from_numpy(onehot_embedding(B)).to(cuda_device)
+    ae.configure_optimizer()
+    ae.train_step(X, c)
+    bufs = lambda: (ae._flat_param, ae.optimiser.exp_avg, ae.optimiser.exp_avg_sq, ae.avg_params)  # noqa: E731
+    keep = [t.detach().clone() for t in bufs()]
+    g = torch.randn_like(ae._flat_grad) * 1e-3
+    ae._flat_grad.copy_(g)
+    ae._flat_grad[12345] = float("nan")
+    ae.optimiser.step(max_norm=1.0, ema=ae.avg_params)
+    torch.cuda.synchronize()
+    assert not torch.isfinite(ae.optimiser.last_grad_norm).item()
+    for a, b in zip(keep, bufs()):
+        assert torch.equal(a, b)
+    ae._flat_grad.copy_(g)
+    ae.optimiser.step(max_norm=1.0, ema=ae.avg_params)
+    torch.cuda.synchronize()
+    assert torch.isfinite(ae.optimiser.last_grad_norm).item()
+    assert not torch.equal(keep[0], ae._flat_param)
 
 
 def test_cooperative_launch_matches(cuda_device):
