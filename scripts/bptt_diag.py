@@ -1,6 +1,7 @@
 """Timing experiments on the persistent BPTT (avc_debug_bptt_diag; results are not valid while a
 bit is set): 1 = no dG operand loads in the product phase, 2 = no partial loads in the epilogue
-phase, 4 = no waits between the phases."""
+phase, 4 = no waits between the phases, 8 = no partial stores in the product phase, 16 = no dG / dc
+stores in the epilogue phase, 32 = no drains before the counter adds."""
 import sys
 
 import torch
@@ -17,7 +18,7 @@ for H, din in ((1024, 1024), (512, 320)):
           for s in [(4 * H, din), (4 * H, H), (4 * H,), (4 * H,)]]
     x = (torch.randn(T * B, din, generator=g) * 0.5).to(dev).requires_grad_(True)
     dy = torch.randn(T * B, H, generator=g).to(dev)
-    for bits in (0, 1, 2, 4, 3, 7):
+    for bits in [int(b) for b in sys.argv[1:]] or (0, 1, 2, 4, 3, 7):
         _lib.call("avc_debug_bptt_diag", bits)
         for rep in range(3):
             y = ops.LSTMLayer.apply(x, *ws, T, B, True)
