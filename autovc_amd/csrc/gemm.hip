@@ -19,6 +19,12 @@ constexpr int BK = 32;
 #ifndef AVC_GEMM_NOLOAD
 #define AVC_GEMM_NOLOAD 0  // diagnostic build only (-DAVC_GEMM_NOLOAD=1): gemm16f skips its LDS-DMA
 #endif
+#ifndef AVC_GEMM_DIAG_NOREAD
+#define AVC_GEMM_DIAG_NOREAD 0  // diagnostic: gemm16f reads its fragments from LDS once, not per K-tile
+#endif
+#ifndef AVC_GEMM_DIAG_NOBAR
+#define AVC_GEMM_DIAG_NOBAR 0  // diagnostic (wrong results): gemm16f skips its per-K-tile barrier
+#endif
 #ifndef AVC_GEMM_DIAG_NOKAHAN
 #define AVC_GEMM_DIAG_NOKAHAN 0  // diagnostic: gemm16f folds 128-k partials with a plain add
 #endif
@@ -916,6 +922,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   }
 
   constexpr int KB = 8 / KC;  // K-tiles (128 k) per compensated partial
+  f16x8 fah[2][TM], fal[2][TM], fbh[2][TN], fbl[2][TN];  // fragment double buffer
   // NS-stage ring: NS-1 K-tiles in flight ahead of the one being consumed
 #pragma unroll
   for (int pre = 0; pre < NS - 1; ++pre)  // (not `i`: the macro's own loop variable)
@@ -933,7 +940,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (AVC_GEMM_DIAG_NOBAR) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (kt + NS - 1 < kt1) AVC16F_FAST_ISSUE(kt + NS - 1, (kt + NS - 1 - kt0) % NS);
     const unsigned char* Ai = lds + st * STAGE;
     const unsigned char* Bi = Ai + ABLK * 1024;
@@ -941,7 +949,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
     // the MFMAs go in passes over the accumulators (hi.hi for every tile, then hi.lo, then
     // lo.hi): no MFMA waits on a just-issued LDS read or on the MFMA right before it.  Each
     // accumulator still sees hi.hi, hi.lo, lo.hi per chunk in the same order (bit-identical).
-    f16x8 fah[2][TM], fal[2][TM], fbh[2][TN], fbl[2][TN];
 #define AVC16F_FRAGS(S, BUF)                                                                      \
     _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                              \
       const unsigned char* p = Ai + (((wm * TM + i) * KC + (S)) * 2) * 1024 + lane * 16;          \
@@ -953,10 +960,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
       fbh[BUF][j] = *reinterpret_cast<const f16x8*>(p);                                           \
       fbl[BUF][j] = *reinterpret_cast<const f16x8*>(p + 1024);                                    \
     }
-    AVC16F_FRAGS(0, 0)
+    if (!AVC_GEMM_DIAG_NOREAD || kt == kt0) { AVC16F_FRAGS(0, 0) }
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
-      if (s + 1 < KC) { AVC16F_FRAGS(s + 1, (s + 1) & 1) }
+      if (s + 1 < KC && (!AVC_GEMM_DIAG_NOREAD || kt == kt0)) { AVC16F_FRAGS(s + 1, (s + 1) & 1) }
       // pin the order: without it the scheduler sinks the next chunk's reads back under these
       // MFMAs and every pass waits on lgkmcnt(0) again
       __builtin_amdgcn_sched_barrier(0);
