@@ -66,6 +66,7 @@ _SIGS = {
     "avc_lstm_split_tune": [_I, _I, _I],
     "avc_gemm_tune": [_I],
     "avc_gemm_config": [_I],
+    "avc_bn_fuse": [_I],
     "avc_lstm_persist_tune": [_I],
     "avc_lstm_persist_depth": [_I],
     "avc_lstm_persist_layers": [_I],

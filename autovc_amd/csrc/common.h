@@ -177,6 +177,16 @@ inline bool range_checked(const avc_context* ctx, const void* p) {
 }
 int persist_guard(avc_context* ctx);
 void persist_release(avc_context* ctx);
+// Co-resident launches besides the LSTM recurrences (lstm_persist.hip): the counter region of a
+// launch layout (header: ticket line, give-up line; then counter_words), the dispatch (cross-
+// process lock, cooperative option, notify event), the bounded spin count, the device's CUs.
+// Region kinds: 1-3 the recurrences, 4 the fused-BN GEMM (gemm.hip).
+int coresident_region(avc_context* ctx, int kind, int ngrp, int ncb, int nwg, size_t counter_words, hipStream_t s,
+                      unsigned** region);
+int coresident_dispatch(avc_context* ctx, const void* fn, dim3 grid, dim3 block, void** args, size_t lds,
+                        hipStream_t s);
+unsigned coresident_spin_limit();
+int coresident_cus();
 
 struct Scratch {
   avc_context* ctx;

@@ -111,9 +111,6 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
     stats = st;
     g.stats = stats;
   }
-  AVC_TRY(gemm_run(ctx, g, s));
-  AVC_TRY(bn_finalize(cout, nparts, stats, (double)T * B, training, momentum, eps, running_mean,
-                      running_var, mean, invstd, s, out_amax));
   // inside the whole-Generator forward the output's range is checked here (its consumer then
   // skips the scan); a value the next split could not hold is reported to the host.  The layer
   // with a residual (postnet's last, model.py:131-132) produces the final mel_post, which no
@@ -121,6 +118,25 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   const bool check = out_frag || (ctx->track_ranges && !residual);
   unsigned* flags = check ? host_flags(ctx) : nullptr;
   if (check && !flags) return AVC_ERR_HIP;
+  if (!out_amax && gemm_bnf_ok(g, training != 0)) {
+    // BatchNorm + act fused into the GEMM's epilogue (gemm.h BnFuse): same bits, two launches
+    // fewer, and y_pre is stored only where a backward will read it (never inside the
+    // whole-Generator forward, whose y_pre is the output buffer or scratch)
+    if (!y_pre || y_pre == out || ctx->track_ranges) g.C = nullptr;
+    BnFuse& f = g.bnf;
+    f.on = 1; f.training = training != 0; f.act = act;
+    f.gamma = gamma; f.beta = beta; f.residual = residual; f.out = out;
+    f.frag = out_frag; f.nkc_out = (cout + 31) / 32 * 2;
+    f.range_flag = flags ? flags + 1 : nullptr;
+    f.rmean = running_mean; f.rvar = running_var; f.mean = mean; f.invstd = invstd;
+    f.momentum = momentum; f.eps = eps; f.count = (double)T * B;
+    AVC_TRY(gemm_run(ctx, g, s));
+    if (check && out) mark_range_checked(ctx, out);
+    return AVC_OK;
+  }
+  AVC_TRY(gemm_run(ctx, g, s));
+  AVC_TRY(bn_finalize(cout, nparts, stats, (double)T * B, training, momentum, eps, running_mean,
+                      running_var, mean, invstd, s, out_amax));
   AVC_TRY(bn_apply((long)T * B, cout, y_pre, mean, invstd, gamma, beta, act, residual, out, s, out_frag,
                    flags ? flags + 1 : nullptr, out_amax));
   if (check && out) mark_range_checked(ctx, out);

@@ -5,6 +5,32 @@
 
 namespace avc {
 
+// BatchNorm + activation fused into the split-f16 GEMM's epilogue (gemm_bnf_ok):
+// y = A.B + bias stays in registers, and each workgroup normalises its own tile.  Train mode:
+// every workgroup stores its column partials (write-through), counts itself in on its column
+// tile's arrival counter and waits until all tilesM tiles of that column are in (the grid is
+// co-resident: one launch of at most one wave of workgroups, through persist_dispatch; epoch-
+// tagged counters that are never reset, bounded spins, NaN on give-up, as the persistent LSTM
+// kernels); it then forms mean / invstd of its columns from the partials in bn_finalize_kernel's
+// order and applies BN + act (+ residual) exactly as bn_apply / bn_apply_frag do, writing the fp32
+// output and / or the split fragment image.  Eval mode uses the running statistics (no barrier).
+struct BnFuse {
+  int on = 0, training = 0, act = 0;
+  int nkc_out = 0;                 // 16-deep chunks of the fragment image (frag)
+  const float* gamma = nullptr; const float* beta = nullptr; const float* residual = nullptr;
+  float* out = nullptr;            // fp32 [M][N] output (nullable)
+  _Float16* frag = nullptr;        // split output image (nullable; M % 32 == 0)
+  unsigned* range_flag = nullptr;  // pinned word: a finite |output| >= 65504 was produced
+  float* rmean = nullptr; float* rvar = nullptr; float* mean = nullptr; float* invstd = nullptr;
+  float momentum = 0.f, eps = 0.f; double count = 0.0;
+  unsigned* cnt = nullptr;         // [tilesN] arrival counters, one 128-B line each
+  unsigned* tmo = nullptr;         // give-up word (epoch of the last launch that gave up)
+  unsigned long long* tickets = nullptr;
+  unsigned* fail_host = nullptr;
+  unsigned spin_limit = 0;
+  int nwg = 0;
+};
+
 // C(m, n) = act( sum_tap sum_k A_tap(m, k) * B_tap(k, n) + bias0[n] + bias1[n] )
 //
 // A (a_trans = 0): element (m, k) of tap tau at A[(m + a_shift0 + tau*a_tapshift) * lda + k];
@@ -47,7 +73,12 @@ struct GemmDesc {
                             // a_frag with a_frag_scaled = 1 (gradient products sharing dY^T / dG^T)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
   int stats_bm = 0;         // filled by gemm_run: rows per stats partial
+  BnFuse bnf;               // fused BatchNorm epilogue (bnf.on; set up by gemm_bnf_ok's caller)
 };
+
+// true when gemm_run can fuse BatchNorm (+ act) into this product's epilogue (d.bnf.on): a
+// split-f16 product on streamed fragments, one K split, one co-resident wave of workgroups
+bool gemm_bnf_ok(const GemmDesc& d, bool training);
 
 // Launch (with automatic tile and split-K choice).  Uses ctx scratch for split-K slabs.
 int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split = 0);

@@ -8,6 +8,8 @@
 // current one (one barrier per K-step).  The row-shift in the A/B addressing implements the
 // Conv1d taps implicitly (no im2col buffer): in time-major frame rows a shift of one frame is
 // a shift of B rows, and rows outside the sequence read as the zero padding.
+#include <vector>
+
 #include "gemm.h"
 #include "timing.h"
 
@@ -44,6 +46,33 @@ __device__ __forceinline__ float act_apply(float v, int act) {
     return fminf(fmaxf((db + 100.f) / 100.f, 0.f), 1.f);
   }
   return v;
+}
+
+// ---- fused BatchNorm epilogue (BnFuse): the column-tile barrier ------------------------------
+__device__ unsigned g_bnf_giveups = 0;  // sticky count of timed-out fused launches
+typedef __attribute__((address_space(1))) unsigned bnf_gu32;
+
+// One lane waits until *p reaches target (wrap-safe relaxed agent-scope polls, as the persistent
+// LSTM kernels' wait_ge_ctl); false = gave up, or another workgroup of this launch (epoch E) did.
+// A give-up is reported to the context's pinned word with the top bit set, so its numbers never
+// collide with the persistent recurrences' failure numbers (persist_guard compares for change).
+__device__ bool bnf_wait(unsigned* p, unsigned target, const BnFuse& bf, unsigned E) {
+  bnf_gu32* gp = (bnf_gu32*)p;
+  bnf_gu32* gt = (bnf_gu32*)bf.tmo;
+  for (unsigned spins = 0;; ++spins) {
+    if ((int)(__hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) return true;
+    if ((spins & 63) == 63 && __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E) return false;
+    if (spins >= bf.spin_limit) {
+      const unsigned old = __hip_atomic_fetch_max(gt, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old != E) {
+        const unsigned n = atomicAdd(&g_bnf_giveups, 1u) + 1u;
+        if (bf.fail_host)
+          __hip_atomic_store(bf.fail_host, 0x80000000u | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
 }
 
 // Tile order: workgroup ids are XCD-contiguous (wgid ranges per XCD), and within them bands of 8
@@ -285,7 +314,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
         float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
         if (d.accumulate) *p += v; else *p = v;
         csum[j] += v;
-        csq[j] += v * v;
+        csq[j] = fmaf(v, v, csq[j]);  // explicit: every epilogue (and the fused BN one) forms the same bits
       }
   }
 
@@ -554,7 +583,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
         float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
         if (d.accumulate) *p += v; else *p = v;
         csum[j] += v;
-        csq[j] += v * v;
+        csq[j] = fmaf(v, v, csq[j]);  // explicit: every epilogue (and the fused BN one) forms the same bits
       }
   }
   if (d.stats) {
@@ -768,6 +797,209 @@ __device__ __forceinline__ void stats_256(const GemmDesc& d, unsigned char* lds,
   }
 }
 
+// Fused BatchNorm epilogue of gemm16f (GemmDesc::bnf, see gemm.h).  Every expression that forms a
+// value is the one the unfused chain uses (this kernel's epilogue for y and the column partials,
+// bn_finalize_kernel for mean / invstd and the running statistics, bn_apply(_frag) for the
+// output and its split), in the same order, so both chains give the same bits.
+// LDS (bytes): [0, 8K) column partials [WM][2][BN] f32; [8K, 16K) fp64 sums [2][4][BN];
+// [16K, 17K) scale / shift [2][BN]; 17K flag; [18K, ..) the tile [BM][BN + 4] f32.
+template <int BM, int BN, int WM, int WTN, int TM, int TN, int NT>
+__device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM][TN], unsigned char* lds, int tm,
+                                             int tn, int tilesM, int wm, int lane, int tid, int row_base,
+                                             int col_base, unsigned long long ticket) {
+  static_assert(NT == 4 * BN, "the finalize step takes 4 threads per column (bn_finalize_kernel)");
+  const BnFuse& bf = d.bnf;
+  float* red = reinterpret_cast<float*>(lds);
+  double* dred = reinterpret_cast<double*>(lds + 8192);
+  float* s_sc = reinterpret_cast<float*>(lds + 16384);
+  float* s_sh = s_sc + BN;
+  int* flag = reinterpret_cast<int*>(lds + 17408);
+  float* tile = reinterpret_cast<float*>(lds + 18432);
+  constexpr int TP = BN + 4;
+  const int wn = (col_base - tn * BN - (lane & 31)) / WTN;
+  // (1) y = A.B + bias, kept in registers (stored only where the caller keeps y_pre), and this
+  // tile's column partials, exactly as the unfused epilogue forms them
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    csum[j] = 0.f;
+    csq[j] = 0.f;
+    const int col = col_base + 32 * j;
+    const bool colok = col < d.N;
+    float bias = 0.f;
+    if (colok) {
+      if (d.bias0) bias += d.bias0[col];
+      if (d.bias1) bias += d.bias1[col];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+        if (!colok || row >= d.M) continue;
+        const float v = act_apply(acc[i][j][e] + bias, d.act);
+        acc[i][j][e] = v;
+        if (d.C) d.C[(long)row * d.ldc + col] = v;
+        csum[j] += v;
+        csq[j] = fmaf(v, v, csq[j]);  // explicit: every epilogue (and the fused BN one) forms the same bits
+      }
+  }
+  __syncthreads();  // every wave is done with the LDS ring
+  bool ok = true;
+  if (bf.training) {
+    // (2) the column partials of this tile (fixed-order sum over the WM wave rows), stored
+    // write-through, drained, then this workgroup counts itself in on its column tile
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float s = csum[j] + __shfl_xor(csum[j], 32);
+      const float s2 = csq[j] + __shfl_xor(csq[j], 32);
+      if (lane < 32) {
+        const int cl = wn * WTN + 32 * j + lane;
+        red[(wm * 2 + 0) * BN + cl] = s;
+        red[(wm * 2 + 1) * BN + cl] = s2;
+      }
+    }
+    __syncthreads();
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc(d.stats, 0, tilesM * 2 * d.N * 4, 0x00020000);
+    for (int cl = tid; cl < BN; cl += NT) {
+      const int col = tn * BN + cl;
+      if (col < d.N) {
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int r = 0; r < WM; ++r) {
+          s += red[(r * 2 + 0) * BN + cl];
+          s2 += red[(r * 2 + 1) * BN + cl];
+        }
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), srs, ((tm * 2 + 0) * d.N + col) * 4, 0,
+                                              16 /*sc1*/);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s2), srs, ((tm * 2 + 1) * d.N + col) * 4, 0,
+                                              16 /*sc1*/);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned E = (unsigned)(ticket / (unsigned long long)bf.nwg) + 1u;
+      __hip_atomic_fetch_add((bnf_gu32*)(bf.cnt + tn * 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = bnf_wait(bf.cnt + tn * 32, E * (unsigned)tilesM, bf, E) ? 1 : 0;
+    }
+    __syncthreads();
+    ok = flag[0] != 0;
+    // (3) this workgroup's columns' sums over every tile, in bn_finalize_kernel's order (4 thread
+    // groups over the partial rows p = grp, grp + 4, ..., then the 4 group sums left to right)
+    const int grp = tid / BN, cl = tid - grp * BN, col = tn * BN + cl;
+    double s = 0.0, s2 = 0.0;
+    if (col < d.N) {
+#pragma unroll 4
+      for (int p = grp; p < tilesM; p += 4) {
+        s += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 0) * d.N + col) * 4, 0, 16));
+        s2 += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 1) * d.N + col) * 4, 0, 16));
+      }
+    }
+    dred[(0 * 4 + grp) * BN + cl] = s;
+    dred[(1 * 4 + grp) * BN + cl] = s2;
+    __syncthreads();
+  }
+  // (4) per-column scale and shift (bn_finalize_kernel, then bn_apply's sc / sh)
+  if (tid < BN) {
+    const int col = tn * BN + tid;
+    if (col < d.N) {
+      float mf, isf;
+      if (bf.training) {
+        const double s = dred[0 * BN + tid] + dred[1 * BN + tid] + dred[2 * BN + tid] + dred[3 * BN + tid];
+        const double s2 = dred[4 * BN + tid] + dred[5 * BN + tid] + dred[6 * BN + tid] + dred[7 * BN + tid];
+        const double mean = s / bf.count;
+        double var = s2 / bf.count - mean * mean;
+        if (var < 0.0) var = 0.0;
+        mf = (float)mean;
+        isf = (float)(1.0 / sqrt(var + (double)bf.eps));
+        if (!ok) mf = __builtin_nanf("");  // gave up: this launch's outputs are NaN, never plausible
+        if (tm == 0 && ok) {
+          if (bf.mean) bf.mean[col] = mf;
+          if (bf.invstd) bf.invstd[col] = isf;
+          if (bf.rmean) bf.rmean[col] = (float)((1.0 - bf.momentum) * bf.rmean[col] + bf.momentum * mean);
+          if (bf.rvar) {
+            const double unb = bf.count > 1.0 ? var * bf.count / (bf.count - 1.0) : var;
+            bf.rvar[col] = (float)((1.0 - bf.momentum) * bf.rvar[col] + bf.momentum * unb);
+          }
+        }
+      } else {
+        mf = bf.rmean[col];
+        isf = (float)(1.0 / sqrt((double)bf.rvar[col] + (double)bf.eps));
+        if (tm == 0) {
+          if (bf.mean) bf.mean[col] = mf;
+          if (bf.invstd) bf.invstd[col] = isf;
+        }
+      }
+      const float sc = isf * bf.gamma[col];
+      s_sc[tid] = sc;
+      s_sh[tid] = bf.beta[col] - mf * sc;
+    }
+  }
+  // (5) the pre-BN tile into LDS, so each output item is one row's 8 consecutive columns
+  const int rl0 = row_base - tm * BM, cl0 = col_base - tn * BN;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) tile[(rl0 + 32 * i + (e & 3) + 8 * (e >> 2)) * TP + cl0 + 32 * j] = acc[i][j][e];
+  __syncthreads();
+  // (6) BN + act (+ residual) per item (32-row block, 16-deep chunk, lane): a wave's fragment
+  // stores cover whole 1 KiB blocks.  Items past N inside the image's K padding are zeros, as
+  // bn_apply_frag writes them.
+  constexpr int NCH16 = BN / 16, ITEMS = (BM / 32) * NCH16 * 64;
+  const long fr_rows = ((long)d.M + 31) / 32 * 32;
+  const int kpad = bf.nkc_out * 16;
+  bool over = false;
+  for (int it = tid; it < ITEMS; it += NT) {
+    const int l = it & 63, blk = it >> 6;
+    const int c16 = blk % NCH16, rb = blk / NCH16;
+    const int rl = rb * 32 + (l & 31), cl8 = c16 * 16 + 8 * (l >> 5);
+    const long row = (long)tm * BM + rl;
+    const int col = tn * BN + cl8;
+    float o[8];
+    if (row < d.M && col < d.N) {
+      const float4 a = *reinterpret_cast<const float4*>(tile + rl * TP + cl8);
+      const float4 b = *reinterpret_cast<const float4*>(tile + rl * TP + cl8 + 4);
+      o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+      o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = act_apply(o[e] * s_sc[cl8 + e] + s_sh[cl8 + e], bf.act);
+      if (bf.residual) {
+        const float4* rq = reinterpret_cast<const float4*>(bf.residual + row * d.N + col);
+        const float4 ra = rq[0], rb4 = rq[1];
+        o[0] += ra.x; o[1] += ra.y; o[2] += ra.z; o[3] += ra.w;
+        o[4] += rb4.x; o[5] += rb4.y; o[6] += rb4.z; o[7] += rb4.w;
+      }
+      if (bf.out) {
+        float4* oq = reinterpret_cast<float4*>(bf.out + row * d.N + col);
+        oq[0] = make_float4(o[0], o[1], o[2], o[3]);
+        oq[1] = make_float4(o[4], o[5], o[6], o[7]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) over |= fabsf(o[e]) >= 65504.f && fabsf(o[e]) < __builtin_inff();
+    if (bf.frag && row < fr_rows && col < kpad) {
+      f16x8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const _Float16 h = (_Float16)o[e];
+        hi[e] = h;
+        lo[e] = (_Float16)((o[e] - (float)h) * 2048.0f);
+      }
+      const long fb = ((row >> 5) * bf.nkc_out + (col >> 4)) * 2;
+      const int fl = (int)(row & 31) + 32 * ((col >> 3) & 1);
+      *reinterpret_cast<f16x8*>(bf.frag + fb * 512 + fl * 8) = hi;
+      *reinterpret_cast<f16x8*>(bf.frag + (fb + 1) * 512 + fl * 8) = lo;
+    }
+  }
+  if (over && bf.range_flag) __hip_atomic_store(bf.range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct Frag16Args {
   const _Float16* As; int a_ntile, a_nkc; long a_shift0, a_tapshift;  // shifts in rows (x32)
   const _Float16* Bs; int b_ntile, b_nkc; long b_tapstride;            // halves per tap
@@ -780,11 +1012,19 @@ struct Frag16Args {
 // 128-k partial is already a fresh MFMA chain, so the fold adds 20 roundings to a K = 2560 sum;
 // measured: the C2 conv 92 -> 84 us, and every forward / gradient / loss-curve parity test keeps
 // its margin.
-template <int BM, int BN, int WM, int WN, int NS, int KC, int OCC = 1, int KH = 1>
+// BNF = 1: the fused BatchNorm epilogue (GemmDesc::bnf; one K split, co-resident grid).
+template <int BM, int BN, int WM, int WN, int NS, int KC, int OCC = 1, int KH = 1, int BNF = 0>
 __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kernel(GemmDesc d, Frag16Args f, int tilesM,
                                                                int tilesN, int kt_per_tap, int kps,
                                                                int nsplit, float* __restrict__ slab) {
   constexpr int NT = 64 * WM * WN, NWAVE = WM * WN;
+  // fused BN, train mode: this launch's ticket (its epoch), taken now so its latency hides
+  // behind the main loop
+  unsigned long long bnf_ticket = 0;
+  if constexpr (BNF) {
+    if (d.bnf.training && threadIdx.x == 0)
+      bnf_ticket = __hip_atomic_fetch_add(d.bnf.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   constexpr int ABLK = (BM / 32) * KC * 2, BBLK = (BN / 32) * KC * 2;  // 1 KiB blocks per K-tile (KC kc x hi/lo)
@@ -792,6 +1032,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   static_assert(NBLK % NWAVE == 0, "blocks per K-tile must split evenly over the waves");
   constexpr int DPW = NBLK / NWAVE;  // LDS-DMA instructions per wave per K-tile
   constexpr int STAGE = NBLK * 1024;
+  static_assert(!BNF || 18432 + BM * (BN + 4) * 4 <= NS * STAGE, "fused BN: the tile does not fit the ring's LDS");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // NS stages
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1046,6 +1287,11 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
       }
     return;
   }
+  if constexpr (BNF) {
+    bnf_epilogue<BM, BN, WM, WTN, TM, TN, NT>(d, acc, lds, tm, tn, tilesM, wm, lane, tid, row_base, col_base,
+                                              bnf_ticket);
+    return;
+  }
   float* __restrict__ C = d.C + (long)z * d.c_zoff;
   float csum[TN], csq[TN];
 #pragma unroll
@@ -1069,7 +1315,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
         float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
         if (d.accumulate) *p += v; else *p = v;
         csum[j] += v;
-        csq[j] += v * v;
+        csq[j] = fmaf(v, v, csq[j]);  // explicit: every epilogue (and the fused BN one) forms the same bits
       }
   }
   if constexpr (BM == 256) {
@@ -1538,6 +1784,78 @@ int guard_scan(avc_context* ctx, const float* src, long rows, long cols, long ld
 }
 }  // namespace
 
+// ---- fused BatchNorm epilogue: eligibility and launch ------------------------------------
+int g_bnf = 1;  // avc_bn_fuse()
+
+namespace {
+// the two gemm16f instances the plans pick (128 x 128: avc_gemm_config 8; 64 x 64), BNF = 1
+const void* bnf_fn(int bm) {
+  if (bm == 128) return reinterpret_cast<const void*>(&gemm16f_kernel<128, 128, 4, 2, 2, 4, 1, 0, 1>);
+  return reinterpret_cast<const void*>(&gemm16f_kernel<64, 64, 2, 2, 4, 2, 1, 1, 1>);
+}
+size_t bnf_lds(int bm) { return bm == 128 ? 2 * 64 * 1024 : 4 * 16 * 1024; }
+int bnf_threads(int bm) { return bm == 128 ? 512 : 256; }
+
+// workgroups of the instance the device holds at once (occupancy API x CUs), per device
+int bnf_capacity(int bm) {
+  struct Entry { int bm, dev, cap; };
+  static std::vector<Entry> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  for (const auto& e : cache)
+    if (e.bm == bm && e.dev == dev) return e.cap;
+  const void* fn = bnf_fn(bm);
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bnf_lds(bm));
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, bnf_threads(bm), bnf_lds(bm)) != hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = 0;
+  }
+  const int cap = per_cu * coresident_cus();
+  cache.push_back({bm, dev, cap});
+  return cap;
+}
+
+int launch16f_bnf(avc_context* ctx, GemmDesc d, Frag16Args f, const Plan& p, hipStream_t s) {
+  const int bm = p.bm;
+  const int KC = bm == 128 ? 4 : 2;
+  int kt_per_tap = (f.a_nkc + KC - 1) / KC;
+  int kps = d.ntaps * kt_per_tap, nsplit = 1;
+  int tilesM = (d.M + bm - 1) / bm, tilesN = (d.N + bm - 1) / bm;
+  const int nwg = tilesM * tilesN;
+  AVC_CHECK_ARG(nwg <= bnf_capacity(bm), "fused BatchNorm GEMM: the grid is not co-resident");
+  const void* fn = bnf_fn(bm);
+  float* slab = nullptr;
+  void* args[] = {&d, &f, &tilesM, &tilesN, &kt_per_tap, &kps, &nsplit, &slab};
+  if (!d.bnf.training) {  // eval mode: no barrier, an ordinary launch
+    AVC_HIP(hipLaunchKernel(fn, dim3(nwg), dim3(bnf_threads(bm)), args, bnf_lds(bm), s));
+    return AVC_OK;
+  }
+  unsigned* region = nullptr;
+  AVC_TRY(coresident_region(ctx, 4, tilesM, tilesN, nwg, (size_t)tilesN * 32, s, &region));
+  unsigned* flags = host_flags(ctx);
+  if (!flags) return AVC_ERR_HIP;
+  d.bnf.tickets = reinterpret_cast<unsigned long long*>(region);  // region layout: lstm_persist.hip
+  d.bnf.tmo = region + 32;
+  d.bnf.cnt = region + 64;
+  d.bnf.fail_host = flags;
+  d.bnf.spin_limit = coresident_spin_limit();
+  d.bnf.nwg = nwg;
+  return coresident_dispatch(ctx, fn, dim3(nwg), dim3(bnf_threads(bm)), args, bnf_lds(bm), s);
+}
+}  // namespace
+
+bool gemm_bnf_ok(const GemmDesc& d, bool training) {
+  if (!g_bnf || !d.prec16 || d.split_scale || !frag16_eligible(d) || d.nz != 1 || d.accumulate || d.ldc_col != 1 ||
+      d.act != AVC_ACT_NONE || d.N % 8 != 0)
+    return false;
+  Plan p = make_plan(d, 0);
+  if (training) p.nsplit = 1;  // a stats product never splits K (gemm_run)
+  if (p.nsplit != 1 || p.bm != p.bn) return false;
+  if (p.bm == 128 && g_gemm_cfg != 8) return false;  // the fused instance is configuration 8's
+  return p.tilesM * p.tilesN <= bnf_capacity(p.bm);
+}
+
 int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) {
   AVC_CHECK_ARG(d.M > 0 && d.N > 0 && d.Kc > 0 && d.ntaps > 0 && d.nz > 0, "gemm: empty problem");
   AVC_CHECK_ARG(d.Kc % 4 == 0 || (d.a_trans == 1 && d.b_trans == 0),
@@ -1656,8 +1974,14 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     d.amax_b = gw + 1;
     d.split_scale = 1;
   }
+  AVC_CHECK_ARG(!d.bnf.on || (frag && p.nsplit == 1 && p.bm == p.bn && (p.bm == 64 || g_gemm_cfg == 8) &&
+                              (d.stats != nullptr) == (d.bnf.training != 0)),
+                "gemm: fused BatchNorm requested for a product that cannot take it (gemm_bnf_ok)");
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
-  if (frag) {
+  if (frag && d.bnf.on) {
+    const int rc = launch16f_bnf(ctx, d, fa, p, stream);
+    if (rc != AVC_OK) return rc;
+  } else if (frag) {
     if (p.bm == 128) launch16f_128(d, fa, p, slab, stream);
     else launch16f_cfg<64, 64, 2, 2, 4, 2>(d, fa, p, slab, stream);
   } else if (staged16) {
@@ -1715,6 +2039,16 @@ extern "C" int avc_gemm_config(int cfg) {
     return AVC_ERR_INVALID;
   }
   avc::g_gemm_cfg = cfg;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_bn_fuse(int on) {
+  if (on < 0 || on > 1) {
+    avc::set_error("avc_bn_fuse: on must be 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_bnf = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

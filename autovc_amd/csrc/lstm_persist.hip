@@ -1552,6 +1552,18 @@ bool bptt_plan(int B, int H, int& nrt, int& ntn, int& ns, int& nch) {
 
 }  // namespace
 
+// the co-resident launch machinery for other grid-synchronised kernels (gemm.hip's fused BN)
+int coresident_region(avc_context* ctx, int kind, int ngrp, int ncb, int nwg, size_t counter_words, hipStream_t s,
+                      unsigned** region) {
+  return persist_region(ctx, kind, 0, ngrp, ncb, nwg, counter_words, s, region);
+}
+int coresident_dispatch(avc_context* ctx, const void* fn, dim3 grid, dim3 block, void** args, size_t lds,
+                        hipStream_t s) {
+  return persist_dispatch(ctx, fn, grid, block, args, lds, s);
+}
+unsigned coresident_spin_limit() { return g_spin_limit; }
+int coresident_cus() { return device_cus(); }
+
 unsigned* host_flags(avc_context* ctx) {
   if (!ctx->fail_host) {
     void* p = nullptr;
@@ -1582,8 +1594,9 @@ int persist_guard(avc_context* ctx) {
   for (auto& r : ctx->regions) ctx->retired.push_back(r.mem);
   ctx->regions.clear();
   ctx->gen.epoch = -2;  // the captured forward graph references the retired regions: re-capture
-  set_error("a persistent LSTM recurrence launched by an earlier call on this context abandoned a "
-            "bounded wait (a workgroup was not resident); that call's outputs were written as NaN and "
+  set_error("a persistent launch (LSTM recurrence, or a convolution with fused BatchNorm) made by an "
+            "earlier call on this context abandoned a bounded wait (a workgroup was not resident); that "
+            "call's outputs were written as NaN and "
             "the BatchNorm running statistics it updated are not valid. State has been reset.");
   return AVC_ERR_DEVICE;
 }

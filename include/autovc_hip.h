@@ -282,6 +282,13 @@ int avc_gemm_tune(int prec16);
  * 3 stages x 32, plain fold / hi.hi products in one MFMA chain over K; 11 = 8 with the hi.hi
  * products in one chain (no 128-k partials).  Default 8. */
 int avc_gemm_config(int cfg);
+/* Conv1d + BatchNorm1d + activation forward (the reference's ConvNorm -> BatchNorm1d -> relu /
+ * tanh, encoder.py:69-70, decoder.py:69-70, postnet.py:54-61): 1 (default) = BatchNorm fused
+ * into the convolution's GEMM epilogue wherever the GEMM's grid is one co-resident wave of
+ * workgroups (train mode: a column-tile barrier inside the launch; eval mode: running
+ * statistics), 0 = the GEMM, a statistics launch and a normalise launch.  Both give the same
+ * bits. */
+int avc_bn_fuse(int on);
 /* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) and decoder lstm1 (one layer,
  * batch <= 256) as ONE weight-stationary launch each (lstm_persist.hip) instead of one launch per
  * time step: 0 = never; whenever eligible with the in-launch hand-offs read 1 = after an

@@ -1,0 +1,117 @@
+"""BatchNorm fused into the convolution's GEMM epilogue (gemm.h BnFuse, avc_bn_fuse).
+
+Reference composition: ConvNorm -> BatchNorm1d -> relu / tanh / identity (encoder.py:69-70,
+decoder.py:69-70, postnet.py:54-61), with model.py:131-132's residual on postnet's last layer.
+The fused form keeps y = conv(x) in registers, forms mean / invstd in every workgroup from the
+column partials behind a column-tile barrier (train mode) or from the running statistics (eval
+mode), and writes the normalised output and its split image.  Every value is formed by the same
+expressions in the same order as the unfused chain (GEMM -> bn_finalize -> bn_apply), so outputs,
+y_pre, mean / invstd and the running statistics must be bit-identical -- at one co-resident wave of
+workgroups (C2's 256) and at small grids, in both BN modes, across repeated launches (epochs) and
+HIP-graph replays of the whole-Generator forward."""
+import ctypes
+
+import pytest
+import torch
+
+from autovc_amd import _lib
+from autovc_amd.auto_encoder import AutoEncoder
+from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_dict
+
+pytestmark = pytest.mark.gpu
+
+RELU, TANH, NONE = 1, 2, 0
+
+
+def _fuse(on):
+    _lib.call("avc_bn_fuse", int(on))
+
+
+@pytest.fixture(autouse=True)
+def _restore_default():
+    yield
+    _fuse(1)
+
+
+def _conv(dev, T, B, cin, cout, act, training, residual, seed, reps=1):
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.randn(T * B, cin, generator=g)).to(dev)
+    W = ((torch.rand(cout, cin, 5, generator=g) - 0.5) * 0.2).to(dev)
+    bias = ((torch.rand(cout, generator=g) - 0.5) * 0.1).to(dev)
+    gamma = (torch.rand(cout, generator=g) + 0.5).to(dev)
+    beta = ((torch.rand(cout, generator=g) - 0.5) * 0.2).to(dev)
+    rm = ((torch.rand(cout, generator=g) - 0.5) * 0.1).to(dev)
+    rv = (torch.rand(cout, generator=g) + 0.5).to(dev)
+    res = torch.randn(T * B, cout, generator=g).to(dev) if residual else None
+    y_pre = torch.full((T * B, cout), float("nan"), device=dev)
+    out = torch.full((T * B, cout), float("nan"), device=dev)
+    mean = torch.zeros(cout, device=dev)
+    invstd = torch.zeros(cout, device=dev)
+    outs = []
+    for _ in range(reps):
+        _lib.call("avc_conv_bn_act_forward", _lib.context(dev), T, B, cin, cout, _lib.ptr(x), _lib.ptr(W),
+                  _lib.ptr(bias), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), int(training),
+                  ctypes.c_float(0.1), ctypes.c_float(1e-5), act, _lib.ptr(res), _lib.ptr(y_pre), _lib.ptr(out),
+                  _lib.ptr(mean), _lib.ptr(invstd), _lib.stream(dev))
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (out, y_pre, mean, invstd, rm, rv)])
+    return outs
+
+
+@pytest.mark.parametrize("T,B,cin,cout,act,residual", [
+    (128, 64, 512, 512, RELU, False),   # C2 conv: 64 x 4 tiles of 128 x 128, one per CU
+    (128, 64, 336, 512, RELU, False),   # encoder's first conv (cin = 80 + 256)
+    (128, 64, 512, 80, NONE, True),     # postnet's last conv + residual: 64 x 64 tiles
+    (128, 2, 512, 512, TANH, False),    # a small grid (8 workgroups)
+    (96, 3, 80, 512, TANH, False),      # ragged rows: M = 288
+])
+@pytest.mark.parametrize("training", [True, False])
+def test_fused_conv_bn_is_bit_identical(cuda_device, T, B, cin, cout, act, residual, training):
+    _fuse(0)
+    ref = _conv(cuda_device, T, B, cin, cout, act, training, residual, seed=5, reps=2)
+    _fuse(1)
+    got = _conv(cuda_device, T, B, cin, cout, act, training, residual, seed=5, reps=2)
+    names = ["out", "y_pre", "mean", "invstd", "running_mean", "running_var"]
+    bad = []
+    for rep in range(2):  # the second launch runs at the next epoch of the same counters
+        for n, a, b in zip(names, got[rep], ref[rep]):
+            if not torch.equal(a, b):
+                d = (a.double() - b.double()).abs().nan_to_num(9.0)
+                bad.append((rep, n, float(d.max()), int((d > 0).sum()), a.numel()))
+    assert not bad, bad
+    assert torch.isfinite(got[1][0]).all()
+
+
+def test_fused_conv_bn_is_taken_at_c2():
+    """The C2 conv products take the fused form (one co-resident wave: 256 tiles of 128 x 128)."""
+    lib = _lib.load()
+    assert lib.avc_conv_frag_chain_ok(128, 64, 512, 512) == 1
+
+
+def _generator(dev, training, reps, B=64, T=128):
+    ae = AutoEncoder(device=dev, verbose=False)
+    ae.load_state_dict(torch_state_dict(0))
+    ae.to(dev)
+    ae.train(training)
+    x = torch.from_numpy(synthetic_mel(11, B, T)).to(dev)
+    c = torch.from_numpy(synthetic_embedding(12, B)).to(dev)
+    outs = []
+    with torch.no_grad():
+        for _ in range(reps):  # eager, then captured, then replayed
+            mel, post, codes = ae(x, c, c)
+            torch.cuda.synchronize()
+            bufs = [b.detach().clone() for n, b in ae.named_buffers() if "running" in n]
+            outs.append([mel.clone(), post.clone(), codes.clone()] + bufs)
+    ae.check_health()
+    return outs
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_whole_generator_fused_bn_is_bit_identical(cuda_device, training):
+    _fuse(0)
+    ref = _generator(cuda_device, training, reps=4)
+    _fuse(1)
+    got = _generator(cuda_device, training, reps=4)
+    for rep in range(4):
+        for i, (a, b) in enumerate(zip(got[rep], ref[rep])):
+            assert torch.equal(a, b), (rep, i, float((a.double() - b.double()).abs().max()))
