@@ -89,7 +89,7 @@ struct GenBufs {
 size_t gen_scratch(int T, int B) {
   const size_t TB = (size_t)T * B, f = sizeof(float);
   size_t own = TB * (336 + 512 + 512 + 64 + 64 + 320 + 1024 + 1024 + 80 + 80) * f + 4 * 512 * f + 64 * 256 +
-               2 * gemm_afrag_bytes((long)TB, 512) + 512;
+               2 * gemm_afrag_bytes((long)TB, 512) + gemm_afrag_bytes((long)TB, 1024) + 1024;
   size_t nested = 0;
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 336, 512));
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 512, 512));
@@ -127,6 +127,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   // fragment output): no fp32 store, no separate split pass
   AVC_TAKE(fa, _Float16, gemm_afrag_bytes(TB, 512) / 2, sc);
   AVC_TAKE(fb, _Float16, gemm_afrag_bytes(TB, 512) / 2, sc);
+  AVC_TAKE(fl, _Float16, gemm_afrag_bytes(TB, 1024) / 2, sc);  // lstm2's output split for the Linear
   float* mean = stat;
   float* invstd = stat + 512;
   const float eps = 1e-5f, mom = 0.1f;
@@ -148,10 +149,12 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TRY(frames_from_mel(T, B, 80, x, 256, c_org, x0, s));
   AVC_TRY(cba(P_ENC_CONV + 0, 336, 512, x0, ba, AVC_ACT_RELU, nullptr, nullptr, fa));
   AVC_TRY(cba(P_ENC_CONV + 6, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, fa, fb));
-  AVC_TRY(cba(P_ENC_CONV + 12, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fb));
+  // the third conv hands its output to the BiLSTM's input projection as a split image only
+  const bool to_bilstm = chain && bilstm_takes_frag(T, B, 512);
+  AVC_TRY(cba(P_ENC_CONV + 12, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fb, to_bilstm ? fa : nullptr));
   const int EL = P_ENC_LSTM;
   AVC_TRY(bilstm_forward_impl(ctx, T, B, 512, 32, ba, 512, P + EL, P + EL + 4, e1, 64, nullptr, nullptr,
-                              nullptr, nullptr, s));
+                              nullptr, nullptr, s, to_bilstm ? fa : nullptr));
   mark_range_checked(ctx, e1);  // an LSTM's h: |h| < 1
   AVC_TRY(bilstm_forward_impl(ctx, T, B, 64, 32, e1, 64, P + EL + 8, P + EL + 12, e2, 64, nullptr, nullptr,
                               nullptr, nullptr, s));
@@ -165,16 +168,17 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
     mark_range_checked(ctx, din);
   }
   const int D1 = P_DEC_LSTM1;
+  // lstm1 also writes its h as the split image the first decoder conv streams (its epilogue, or a
+  // split pass where the recurrence is not persistent)
   AVC_TRY(lstm_forward_impl(ctx, T, B, 320, 512, 0, din, 320, P[D1], P[D1 + 1], P[D1 + 2], P[D1 + 3],
-                            ba, 512, nullptr, nullptr, s));
+                            ba, 512, nullptr, nullptr, s, chain ? fb : nullptr));
   mark_range_checked(ctx, ba);  // lstm1's h
-  AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, nullptr, fa));
+  AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, chain ? fb : nullptr, fa));
   AVC_TRY(cba(P_DEC_CONV + 6, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fa, fb));
   AVC_TRY(cba(P_DEC_CONV + 12, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, fb));
   const int D2 = P_DEC_LSTM2;
   // decoder.lstm2: both layers advanced as one wavefront (lstm.hip: lstm2_forward_impl)
-  AVC_TRY(lstm2_forward_impl(ctx, T, B, 512, 1024, bb, 512, P + D2, P + D2 + 4, l1, l2, nullptr,
-                             nullptr, nullptr, nullptr, s));
+  // (l2 also as the split image the Linear streams when its product takes fragments)
   GemmDesc lin;
   lin.M = (int)TB; lin.N = 80; lin.Kc = 1024;
   lin.A = l2; lin.lda = 1024;
@@ -183,6 +187,10 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   lin.C = melf; lin.ldc = 80;
   lin.prec16 = 1;
   lin.a_bound = 1.f;  // |h| < 1 (lstm2's output): no range scan needed
+  const bool lin_frag = TB % 32 == 0 && gemm_frag_eligible(lin);
+  AVC_TRY(lstm2_forward_impl(ctx, T, B, 512, 1024, bb, 512, P + D2, P + D2 + 4, l1, l2, nullptr,
+                             nullptr, nullptr, nullptr, s, lin_frag ? fl : nullptr));
+  if (lin_frag) lin.a_frag = fl;
   if (ctx->prep_version >= 0) {
     bool fb = true;
     auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_GEMM_BFRAG, P[P_LIN], nullptr, gemm_bfrag_bytes(lin), &fb));

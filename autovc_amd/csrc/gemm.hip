@@ -888,6 +888,8 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
     // (3) this workgroup's columns' sums over every tile, in bn_finalize_kernel's order (4 thread
     // groups over the partial rows p = grp, grp + 4, ..., then the 4 group sums left to right)
     const int grp = tid / BN, cl = tid - grp * BN, col = tn * BN + cl;
+    // (4 rows of loads in flight per thread: a variant that requested all 16 rows of a thread
+    // before its first add measured 0.08 ms slower per C2 forward)
     double s = 0.0, s2 = 0.0;
     if (col < d.N) {
 #pragma unroll 4

@@ -15,7 +15,8 @@ size_t colsum_scratch(int M, int N);
 int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
                       const float* x, int ldx, const float* w_ih, const float* w_hh,
                       const float* b_ih, const float* b_hh, float* y, int ldy,
-                      float* saved_gates, float* saved_c, hipStream_t s);
+                      float* saved_gates, float* saved_c, hipStream_t s,
+                      _Float16* y_frag = nullptr);  // y also as the split image a GEMM streams (a_frag)
 size_t lstm_forward_scratch(int T, int B, int din, int H, bool training);
 int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
                        const float* x, int ldx, const float* w_ih, const float* w_hh,
@@ -27,13 +28,16 @@ size_t lstm_backward_scratch(int T, int B, int din, int H);
 // two stacked layers as a wavefront (w0/w1 = {w_ih, w_hh, b_ih, b_hh}); saved buffers optional
 int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                        const float* const* w0, const float* const* w1, float* y0, float* y1,
-                       float* g0, float* c0, float* g1, float* c1, hipStream_t s);
+                       float* g0, float* c0, float* g1, float* c1, hipStream_t s,
+                       _Float16* y1_frag = nullptr);  // y1 also as a split image (a_frag)
 size_t lstm2_forward_scratch(int T, int B, int din, int H, bool training);
 
 // bidirectional layer (wf/wr = {w_ih, w_hh, b_ih, b_hh}); H = 32 runs both directions in one launch
 int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                         const float* const* wf, const float* const* wr, float* y, int ldy,
-                        float* g_f, float* c_f, float* g_r, float* c_r, hipStream_t s);
+                        float* g_f, float* c_f, float* g_r, float* c_r, hipStream_t s,
+                        const _Float16* x_frag = nullptr);  // x given only as a split image (GemmDesc::a_frag)
+bool bilstm_takes_frag(int T, int B, int din);  // H = 32: its input projection streams a split x
 size_t bilstm_forward_scratch(int T, int B, int din, int H, bool training);
 
 // ---- split-fp16 LSTM forward recurrence (lstm_split.hip), used by the two above when supported
@@ -42,10 +46,11 @@ size_t lstm_split_forward_scratch(int T, int B, int din, int H, int nlayers);
 int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
                             const float* x, int ldx, const float* w_ih, const float* w_hh,
                             const float* b_ih, const float* b_hh, float* y, int ldy,
-                            float* saved_gates, float* saved_c, hipStream_t s);
+                            float* saved_gates, float* saved_c, hipStream_t s, _Float16* y_frag = nullptr);
 int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                              const float* const* w0, const float* const* w1, float* y0, float* y1,
-                             float* g0, float* c0, float* g1, float* c1, hipStream_t s);
+                             float* g0, float* c0, float* g1, float* c1, hipStream_t s,
+                             _Float16* y1_frag = nullptr);
 // decoder.lstm2 as one weight-stationary launch (lstm_persist.hip); gx0 = layer 0's input
 // projection, w*_s = split weights (each followed by its per-row unscale), b1_p = permuted
 // b_ih1 + b_hh1
@@ -64,7 +69,7 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
                           const _Float16* w0_s, const float* winv0, const _Float16* w1i_s,
                           const float* winv1i, const _Float16* w1h_s, const float* winv1h,
                           const float* b1_p, float* y0, float* y1, float* g0, float* c0, float* g1,
-                          float* c1, hipStream_t s, const InProj* ip = nullptr);
+                          float* c1, hipStream_t s, const InProj* ip = nullptr, _Float16* y1_frag = nullptr);
 // one forward layer (decoder.lstm1) as one weight-stationary launch, batch split into
 // independent groups; gx = input projection + biases, whh_s = split W_hh followed by winv
 bool lstm1_persist_eligible(int T, int B, int H);
@@ -72,7 +77,7 @@ bool lstm1_inproj_eligible(int T, int B, int H, int din);
 size_t lstm1_persist_scratch(int T, int B, int H, int din);
 int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, const _Float16* whh_s,
                           const float* winv, float* y, float* g, float* c, hipStream_t s,
-                          const InProj* ip = nullptr);
+                          const InProj* ip = nullptr, _Float16* y_frag = nullptr);
 // K of an input slot's split operands: din padded with zeros to 128 * (3 or 4) columns
 int inproj_kpad(int din);
 // BPTT of one LSTM layer direction as one persistent launch (lstm_persist.hip)

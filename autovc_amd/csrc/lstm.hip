@@ -849,7 +849,17 @@ int permute_rows(const float* src, float* dst, int H, int D, hipStream_t s) {
 int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
                       const float* x, int ldx, const float* w_ih, const float* w_hh,
                       const float* b_ih, const float* b_hh, float* y, int ldy,
-                      float* saved_gates, float* saved_c, hipStream_t s) {
+                      float* saved_gates, float* saved_c, hipStream_t s, _Float16* y_frag) {
+  if (y_frag) {
+    // the persistent recurrence writes the split image in its epilogue; any other path splits y
+    // afterwards (split_frag32_kernel's unscaled split: |h| < 1)
+    if (lstm_split_supported(H, din) && !reverse && ldy == H && lstm1_persist_eligible(T, B, H))
+      return lstm_split_forward_impl(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, b_ih, b_hh, y, ldy,
+                                     saved_gates, saved_c, s, y_frag);
+    AVC_TRY(lstm_forward_impl(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, b_ih, b_hh, y, ldy, saved_gates,
+                              saved_c, s));
+    return gemm_split_frag(y, ldy, T * B, H, nullptr, y_frag, s);
+  }
   AVC_CHECK_ARG(T > 0 && B > 0 && din > 0, "lstm: empty problem");
   AVC_CHECK_ARG(H == 32 || (H % 64 == 0), "lstm: H must be 32 or a multiple of 64");
   AVC_CHECK_ARG(din % 4 == 0 && ldx % 4 == 0, "lstm: din/ldx must be multiples of 4");
@@ -932,11 +942,22 @@ size_t bilstm_forward_scratch(int T, int B, int din, int H, bool training) {
          gemm_scratch_bytes(d) + 1024;
 }
 
+namespace {
+GemmDesc bilstm_proj_desc(int T, int B, int din) {
+  GemmDesc g;
+  g.M = T * B; g.N = 256; g.Kc = din; g.a_rows = (long)T * B;
+  g.b_trans = 1; g.ldb = din; g.prec16 = 1;
+  return g;
+}
+}  // namespace
+
+bool bilstm_takes_frag(int T, int B, int din) { return gemm_frag_eligible(bilstm_proj_desc(T, B, din)); }
+
 // Bidirectional layer (encoder.py:51): y[:, 0:H] forward, y[:, H:2H] reverse.  H = 32: both input
 // projections into one [T*B][256] buffer, then ONE recurrence launch for both directions.
 int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                         const float* const* wf, const float* const* wr, float* y, int ldy,
-                        float* g_f, float* c_f, float* g_r, float* c_r, hipStream_t s) {
+                        float* g_f, float* c_f, float* g_r, float* c_r, hipStream_t s, const _Float16* x_frag) {
   if (H != 32) {
     AVC_TRY(lstm_forward_impl(ctx, T, B, din, H, 0, x, ldx, wf[0], wf[1], wf[2], wf[3], y, ldy, g_f, c_f, s));
     return lstm_forward_impl(ctx, T, B, din, H, 1, x, ldx, wr[0], wr[1], wr[2], wr[3], y + H, ldy, g_r, c_r, s);
@@ -961,6 +982,10 @@ int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const fl
   g.b_trans = 1; g.ldb = din; g.B = wcat; g.bias0 = wcat + 256L * din;
   g.C = gx; g.ldc = 256;
   g.prec16 = 1;
+  if (x_frag) {  // x handed over split by its producer (bilstm_takes_frag said yes; x itself is not read)
+    AVC_CHECK_ARG(ldx == din && gemm_frag_eligible(g), "bilstm: a split input needs a fragment-streaming product");
+    g.a_frag = x_frag;
+  }
   if (ctx->prep_version >= 0) {
     bool fb = true;
     auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_GEMM_BFRAG, wcat, nullptr, gemm_bfrag_bytes(g), &fb));
@@ -995,7 +1020,13 @@ size_t lstm2_forward_scratch(int T, int B, int din, int H, bool training) {
 // [h0_t | h1_{t-1}] . [W_ih1 | W_hh1]^T + (b_ih1 + b_hh1) with K = 2H.
 int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                        const float* const* w0, const float* const* w1, float* y0, float* y1,
-                       float* g0, float* c0, float* g1, float* c1, hipStream_t s) {
+                       float* g0, float* c0, float* g1, float* c1, hipStream_t s, _Float16* y1_frag) {
+  if (y1_frag) {  // as lstm_forward_impl's y_frag, for the second layer's output
+    if (lstm_split_supported(H, din) && lstm2_persist_eligible(T, B, H))
+      return lstm2_split_forward_impl(ctx, T, B, din, H, x, ldx, w0, w1, y0, y1, g0, c0, g1, c1, s, y1_frag);
+    AVC_TRY(lstm2_forward_impl(ctx, T, B, din, H, x, ldx, w0, w1, y0, y1, g0, c0, g1, c1, s));
+    return gemm_split_frag(y1, H, T * B, H, nullptr, y1_frag, s);
+  }
   AVC_CHECK_ARG(T > 0 && B > 0 && din % 4 == 0 && ldx % 4 == 0, "lstm2: bad shape");
   AVC_CHECK_ARG(H % 64 == 0, "lstm2: H must be a multiple of 64");
   AVC_CHECK_ARG((g0 == nullptr) == (c0 == nullptr) && (g1 == nullptr) == (c1 == nullptr) &&

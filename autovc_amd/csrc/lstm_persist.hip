@@ -169,6 +169,8 @@ struct PersistArgs {
   unsigned char* hs1;         // [2][hsz] ring (only slot 2 reads it, one step later)
   long hsz;                   // bytes per time step of a split-h buffer
   float* y0; float* y1;       // [T][B][H] fp32 h
+  _Float16* yfrag;            // optional: slot yf_slot's h_t also as the split image the next
+  int yf_slot, yf_nkc;        // contraction streams (GemmDesc::a_frag, rows t*B + b, nkc chunks)
   float* g0; float* g1;       // optional [T][B][4H] activated gates (training)
   float* c0; float* c1;       // optional [T][B][H] cell state (training)
   unsigned* cnt;              // [nslot][T] arrivals (never reset; see the epoch above)
@@ -496,8 +498,25 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   auto gx1_slab = [&](int tt, int c) -> long { return ((long)(tt % kGxRing) * a.ncb + c) * (64 * TW); };
   const int rep = blockIdx.x & (kRep - 1);
   // outputs nobody reads inside this launch: h, and for training c and the activated gates
+  _Float16* const yfrag = L == a.yf_slot ? a.yfrag : nullptr;
   auto store_out = [&](int tt, const fu& h, const fu& c, const fu& i, const fu& f, const fu& g, const fu& o) {
     *reinterpret_cast<fu*>(y_out + ((long)tt * B + b) * H + j0 + u0) = h;
+    if (yfrag) {  // split_frag32_kernel's unscaled split (|h| < 1), at its fragment position
+      const long r = (long)tt * B + b;
+      const int k = j0 + u0;
+      const long blk = ((r >> 5) * a.yf_nkc + (k >> 4)) * 2;
+      const long off = blk * 512 + ((r & 31) + 32 * ((k >> 3) & 1)) * 8 + (k & 7);
+      typedef _Float16 hu __attribute__((ext_vector_type(UPT)));
+      hu hi, lo;
+#pragma unroll
+      for (int u = 0; u < UPT; ++u) {
+        const _Float16 hh = (_Float16)h[u];
+        hi[u] = hh;
+        lo[u] = (_Float16)((h[u] - (float)hh) * 2048.0f);
+      }
+      *reinterpret_cast<hu*>(yfrag + off) = hi;
+      *reinterpret_cast<hu*>(yfrag + off + 512) = lo;
+    }
     if (c_save) *reinterpret_cast<fu*>(c_save + ((long)tt * B + b) * H + j0 + u0) = c;
     if (g_save) {
       float* go = g_save + ((long)tt * B + b) * G4 + p0 + u0;
@@ -1675,7 +1694,8 @@ size_t lstm1_persist_scratch(int T, int B, int H, int din) {
 // y / c [T][B][H], g [T][B][4H] (permuted, optional: training).  Bit-identical to the
 // launch-per-step form (same products, same K split, same reduction order).
 int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, const _Float16* whh_s,
-                          const float* winv, float* y, float* g, float* c, hipStream_t s, const InProj* ip) {
+                          const float* winv, float* y, float* g, float* c, hipStream_t s, const InProj* ip,
+                          _Float16* y_frag) {
   AVC_CHECK_ARG(lstm1_persist_eligible(T, B, H), "lstm1 persistent path: not eligible for this shape");
   AVC_CHECK_ARG(!ip || lstm1_inproj_eligible(T, B, H, ip->din), "lstm1 input-projection slot: not eligible");
   AVC_TRY(persist_guard(ctx));
@@ -1713,6 +1733,7 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   a.gx0 = gx;
   a.hs0 = hs0; a.hsz = hsz;
   a.y0 = y; a.g0 = g; a.c0 = c;
+  a.yfrag = y_frag; a.yf_slot = 0; a.yf_nkc = (H + 31) / 32 * 2;
   a.diag = g_persist_diag;
   set_region_args(a, ctx, region);
   hipEvent_t ev = timing_begin(TC_LSTM1_PERSIST, s);
@@ -1752,7 +1773,7 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
                           const _Float16* w0_s, const float* winv0, const _Float16* w1i_s,
                           const float* winv1i, const _Float16* w1h_s, const float* winv1h,
                           const float* b1_p, float* y0, float* y1, float* g0, float* c0, float* g1,
-                          float* c1, hipStream_t s, const InProj* ip) {
+                          float* c1, hipStream_t s, const InProj* ip, _Float16* y1_frag) {
   AVC_CHECK_ARG(lstm2_persist_eligible(T, B, H), "lstm2 persistent path: not eligible for this shape");
   AVC_CHECK_ARG(!ip || lstm2_inproj_eligible(T, B, H, ip->din), "lstm2 input-projection slot: not eligible");
   AVC_TRY(persist_guard(ctx));
@@ -1779,6 +1800,7 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   a.gx0 = gx0; a.b1 = b1_p; a.gx1 = gx1;
   a.hs0 = hs0; a.hs1 = hs1; a.hsz = hsz;
   a.y0 = y0; a.y1 = y1; a.g0 = g0; a.g1 = g1; a.c0 = c0; a.c1 = c1;
+  a.yfrag = y1_frag; a.yf_slot = 2; a.yf_nkc = (H + 31) / 32 * 2;
   a.diag = g_persist_diag;
   set_region_args(a, ctx, region);
   const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);

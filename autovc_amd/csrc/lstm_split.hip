@@ -632,7 +632,7 @@ int split_wih(avc_context* ctx, Scratch& sc, const float* w_ih, int H, int din, 
 int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
                             const float* x, int ldx, const float* w_ih, const float* w_hh,
                             const float* b_ih, const float* b_hh, float* y, int ldy,
-                            float* saved_gates, float* saved_c, hipStream_t s) {
+                            float* saved_gates, float* saved_c, hipStream_t s, _Float16* y_frag) {
   AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm split path: H must be a multiple of 32, >= 64");
   Scratch sc(ctx);
   const long TB = (long)T * B;
@@ -664,7 +664,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
     // idle) as one weight-stationary launch
     InProj ip{x, (long)ldx, din, nullptr, nullptr, b_p};
     AVC_TRY(split_wih(ctx, sc, w_ih, H, din, ip, s));
-    return lstm1_persist_forward(ctx, T, B, H, gx, whh_s, winv, y, saved_gates, saved_c, s, &ip);
+    return lstm1_persist_forward(ctx, T, B, H, gx, whh_s, winv, y, saved_gates, saved_c, s, &ip, y_frag);
   }
   GemmDesc g;
   g.M = (int)TB; g.N = 4 * H; g.Kc = din;
@@ -675,7 +675,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
   AVC_TRY(attach_bfrag(ctx, g, w_ih, f_wih, s));
   AVC_TRY(gemm_run(ctx, g, s));
   if (!reverse && ldy == H && lstm1_persist_eligible(T, B, H))  // the recurrence as one launch
-    return lstm1_persist_forward(ctx, T, B, H, gx, whh_s, winv, y, saved_gates, saved_c, s);
+    return lstm1_persist_forward(ctx, T, B, H, gx, whh_s, winv, y, saved_gates, saved_c, s, nullptr, y_frag);
 
   const int NW = pick_nw(H);
   // narrow full-K tiles when they alone fill the chip (no slab hand-off: one memory round trip
@@ -748,7 +748,7 @@ int lstm_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, int 
 // (no cross-workgroup slab hand-off).
 int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                              const float* const* w0, const float* const* w1, float* y0, float* y1,
-                             float* g0, float* c0, float* g1, float* c1, hipStream_t s) {
+                             float* g0, float* c0, float* g1, float* c1, hipStream_t s, _Float16* y1_frag) {
   AVC_CHECK_ARG(lstm_split_supported(H, din), "lstm2 split path: H must be a multiple of 64");
   Scratch sc(ctx);
   const long TB = (long)T * B;
@@ -785,7 +785,7 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
     InProj ip{x, (long)ldx, din, nullptr, nullptr, b0_p};
     AVC_TRY(split_wih(ctx, sc, w0[0], H, din, ip, s));
     return lstm2_persist_forward(ctx, T, B, H, gx, w0_s, winv0, w1i_s, winv1i, w1h_s, winv1h, b1_p,
-                                 y0, y1, g0, c0, g1, c1, s, &ip);
+                                 y0, y1, g0, c0, g1, c1, s, &ip, y1_frag);
   }
   GemmDesc g;
   g.M = (int)TB; g.N = 4 * H; g.Kc = din;
@@ -797,7 +797,7 @@ int lstm2_split_forward_impl(avc_context* ctx, int T, int B, int din, int H, con
   AVC_TRY(gemm_run(ctx, g, s));
   if (lstm2_persist_eligible(T, B, H))  // the whole recurrence as one weight-stationary launch
     return lstm2_persist_forward(ctx, T, B, H, gx, w0_s, winv0, w1i_s, winv1i, w1h_s, winv1h, b1_p,
-                                 y0, y1, g0, c0, g1, c1, s);
+                                 y0, y1, g0, c0, g1, c1, s, nullptr, y1_frag);
 
   float* cpp0 = nullptr;
   float* cpp1 = nullptr;
