@@ -67,6 +67,7 @@ _SIGS = {
     "avc_gemm_tune": [_I],
     "avc_gemm_config": [_I],
     "avc_bn_fuse": [_I],
+    "avc_split_handover": [_I],
     "avc_lstm_persist_tune": [_I],
     "avc_lstm_persist_depth": [_I],
     "avc_lstm_persist_layers": [_I],
@@ -128,7 +129,11 @@ def load():
                 raise HipLibraryError(
                     f"HIP library not found at {LIB_PATH}; build it with `make` (hipcc --offload-arch=gfx950)")
             lib = ctypes.CDLL(LIB_PATH)
+            # an A/B build named by AUTOVC_HIP_LIB may predate a symbol; the in-tree build has them all
+            ab = "AUTOVC_HIP_LIB" in os.environ
             for name, args in _SIGS.items():
+                if ab and not hasattr(lib, name):
+                    continue
                 fn = getattr(lib, name)
                 fn.argtypes = args
                 fn.restype = _RESTYPES.get(name, ctypes.c_int)

@@ -104,6 +104,10 @@ size_t gen_scratch(int T, int B) {
   return own + nested + (1 << 20);
 }
 
+// avc_split_handover(): the split-image hand-overs of the whole-Generator forward that do not
+// come from a conv (encoder conv 3 -> BiLSTM projection, lstm1 -> decoder conv 1, lstm2 -> Linear)
+int g_handover = 1;
+
 int generator_forward(avc_context* ctx, int T, int B, const float* const* P, const float* x,
                       const float* c_org, const float* c_trg, int training, float* mel,
                       float* mel_post, float* codes, hipStream_t s) {
@@ -150,7 +154,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TRY(cba(P_ENC_CONV + 0, 336, 512, x0, ba, AVC_ACT_RELU, nullptr, nullptr, fa));
   AVC_TRY(cba(P_ENC_CONV + 6, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, fa, fb));
   // the third conv hands its output to the BiLSTM's input projection as a split image only
-  const bool to_bilstm = chain && bilstm_takes_frag(T, B, 512);
+  const bool to_bilstm = chain && g_handover && bilstm_takes_frag(T, B, 512);
   AVC_TRY(cba(P_ENC_CONV + 12, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fb, to_bilstm ? fa : nullptr));
   const int EL = P_ENC_LSTM;
   AVC_TRY(bilstm_forward_impl(ctx, T, B, 512, 32, ba, 512, P + EL, P + EL + 4, e1, 64, nullptr, nullptr,
@@ -171,9 +175,9 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   // lstm1 also writes its h as the split image the first decoder conv streams (its epilogue, or a
   // split pass where the recurrence is not persistent)
   AVC_TRY(lstm_forward_impl(ctx, T, B, 320, 512, 0, din, 320, P[D1], P[D1 + 1], P[D1 + 2], P[D1 + 3],
-                            ba, 512, nullptr, nullptr, s, chain ? fb : nullptr));
+                            ba, 512, nullptr, nullptr, s, chain && g_handover ? fb : nullptr));
   mark_range_checked(ctx, ba);  // lstm1's h
-  AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, chain ? fb : nullptr, fa));
+  AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, chain && g_handover ? fb : nullptr, fa));
   AVC_TRY(cba(P_DEC_CONV + 6, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fa, fb));
   AVC_TRY(cba(P_DEC_CONV + 12, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, fb));
   const int D2 = P_DEC_LSTM2;
@@ -187,7 +191,7 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   lin.C = melf; lin.ldc = 80;
   lin.prec16 = 1;
   lin.a_bound = 1.f;  // |h| < 1 (lstm2's output): no range scan needed
-  const bool lin_frag = TB % 32 == 0 && gemm_frag_eligible(lin);
+  const bool lin_frag = g_handover && TB % 32 == 0 && gemm_frag_eligible(lin);
   AVC_TRY(lstm2_forward_impl(ctx, T, B, 512, 1024, bb, 512, P + D2, P + D2 + 4, l1, l2, nullptr,
                              nullptr, nullptr, nullptr, s, lin_frag ? fl : nullptr));
   if (lin_frag) lin.a_frag = fl;
@@ -719,3 +723,13 @@ int avc_prepared_release(avc_context* ctx) {
 }
 
 }  // extern "C"
+
+extern "C" int avc_split_handover(int on) {
+  if (on < 0 || on > 1) {
+    avc::set_error("avc_split_handover: on must be 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_handover = on;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}

@@ -289,6 +289,11 @@ int avc_gemm_config(int cfg);
  * statistics), 0 = the GEMM, a statistics launch and a normalise launch.  Both give the same
  * bits. */
 int avc_bn_fuse(int on);
+/* Whole-Generator forward: 1 (default) = the encoder's last conv, decoder lstm1 and decoder lstm2
+ * hand their outputs to the next contraction (BiLSTM projection, first decoder conv, Linear) as
+ * the split image that contraction streams, written by their own epilogues; 0 = fp32 outputs and
+ * a split pass in front of each consumer.  Both give the same bits. */
+int avc_split_handover(int on);
 /* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) and decoder lstm1 (one layer,
  * batch <= 256) as ONE weight-stationary launch each (lstm_persist.hip) instead of one launch per
  * time step: 0 = never; whenever eligible with the in-launch hand-offs read 1 = after an

@@ -115,3 +115,24 @@ def test_whole_generator_fused_bn_is_bit_identical(cuda_device, training):
     for rep in range(4):
         for i, (a, b) in enumerate(zip(got[rep], ref[rep])):
             assert torch.equal(a, b), (rep, i, float((a.double() - b.double()).abs().max()))
+
+
+def _set_handover(on):
+    _lib.call("avc_split_handover", int(on))
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_split_handovers_are_bit_identical(cuda_device, training):
+    """The encoder's last conv -> BiLSTM projection, lstm1 -> first decoder conv and lstm2 -> Linear
+    hand-overs as split images written by the producers (avc_split_handover) give the bits of the
+    fp32 hand-over + split pass, at C2 (B = 64: every hand-over active)."""
+    try:
+        _set_handover(0)
+        ref = _generator(cuda_device, training, reps=3)
+        _set_handover(1)
+        got = _generator(cuda_device, training, reps=3)
+    finally:
+        _set_handover(1)
+    for rep in range(3):
+        for i, (a, b) in enumerate(zip(got[rep], ref[rep])):
+            assert torch.equal(a, b), (rep, i, float((a.double() - b.double()).abs().max()))
