@@ -60,8 +60,12 @@ __device__ bool bnf_wait(unsigned* p, unsigned target, const BnFuse& bf, unsigne
   bnf_gu32* gp = (bnf_gu32*)p;
   bnf_gu32* gt = (bnf_gu32*)bf.tmo;
   for (unsigned spins = 0;; ++spins) {
-    if ((int)(__hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) return true;
-    if ((spins & 63) == 63 && __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E) return false;
+    // the give-up word is read beside every poll (one round trip for both): a workgroup that
+    // arrives after another one gave up never takes the barrier as passed
+    const unsigned v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned g = __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (g == E) return false;
+    if ((int)(v - target) >= 0) return true;
     if (spins >= bf.spin_limit) {
       const unsigned old = __hip_atomic_fetch_max(gt, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old != E) {

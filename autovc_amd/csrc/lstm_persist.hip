@@ -926,20 +926,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     if (t == T && T > 0 && live) store_out(T - 1, pend_h, pend_c, pend_i, pend_f, pend_g, pend_o);
   }
   // gave up at step t: the rows this workgroup owns for steps t..T-1 are written as NaN, so a
-  // timed-out launch never hands plausible numbers downstream (the host reports it, see above)
+  // timed-out launch never hands plausible numbers downstream (the host reports it, see above) --
+  // through every output, the split image included.  The granule form stores a step's outputs
+  // one step late, so its step t - 1 is written as NaN as well.
   if (t < T && L != 1 && live) {
     fu nv;
 #pragma unroll
     for (int u = 0; u < UPT; ++u) nv[u] = __builtin_nanf("");
-    for (int tt = t; tt < T; ++tt) {
-      *reinterpret_cast<fu*>(y_out + ((long)tt * B + b) * H + j0 + u0) = nv;
-      if (c_save) *reinterpret_cast<fu*>(c_save + ((long)tt * B + b) * H + j0 + u0) = nv;
-      if (g_save) {
-        float* go = g_save + ((long)tt * B + b) * G4 + p0 + u0;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) *reinterpret_cast<fu*>(go + 4 * g) = nv;
-      }
-    }
+    for (int tt = GR && t > 0 ? t - 1 : t; tt < T; ++tt) store_out(tt, nv, nv, nv, nv, nv, nv);
   }
 }
 

@@ -10,6 +10,7 @@ y_pre, mean / invstd and the running statistics must be bit-identical -- at one 
 workgroups (C2's 256) and at small grids, in both BN modes, across repeated launches (epochs) and
 HIP-graph replays of the whole-Generator forward."""
 import ctypes
+import time
 
 import pytest
 import torch
@@ -33,7 +34,7 @@ def _restore_default():
     _fuse(1)
 
 
-def _conv(dev, T, B, cin, cout, act, training, residual, seed, reps=1):
+def _conv_inputs(dev, T, B, cin, cout, residual, seed):
     g = torch.Generator().manual_seed(seed)
     x = (torch.randn(T * B, cin, generator=g)).to(dev)
     W = ((torch.rand(cout, cin, 5, generator=g) - 0.5) * 0.2).to(dev)
@@ -47,14 +48,25 @@ def _conv(dev, T, B, cin, cout, act, training, residual, seed, reps=1):
     out = torch.full((T * B, cout), float("nan"), device=dev)
     mean = torch.zeros(cout, device=dev)
     invstd = torch.zeros(cout, device=dev)
+    return x, W, bias, gamma, beta, rm, rv, res, y_pre, out, mean, invstd
+
+
+def _conv_call(dev, T, B, cin, cout, act, training, t):
+    x, W, bias, gamma, beta, rm, rv, res, y_pre, out, mean, invstd = t
+    _lib.call("avc_conv_bn_act_forward", _lib.context(dev), T, B, cin, cout, _lib.ptr(x), _lib.ptr(W),
+              _lib.ptr(bias), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), int(training),
+              ctypes.c_float(0.1), ctypes.c_float(1e-5), act, _lib.ptr(res), _lib.ptr(y_pre), _lib.ptr(out),
+              _lib.ptr(mean), _lib.ptr(invstd), _lib.stream(dev))
+
+
+def _conv(dev, T, B, cin, cout, act, training, residual, seed, reps=1):
+    t = _conv_inputs(dev, T, B, cin, cout, residual, seed)
     outs = []
     for _ in range(reps):
-        _lib.call("avc_conv_bn_act_forward", _lib.context(dev), T, B, cin, cout, _lib.ptr(x), _lib.ptr(W),
-                  _lib.ptr(bias), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), int(training),
-                  ctypes.c_float(0.1), ctypes.c_float(1e-5), act, _lib.ptr(res), _lib.ptr(y_pre), _lib.ptr(out),
-                  _lib.ptr(mean), _lib.ptr(invstd), _lib.stream(dev))
+        _conv_call(dev, T, B, cin, cout, act, training, t)
         torch.cuda.synchronize()
-        outs.append([t.clone() for t in (out, y_pre, mean, invstd, rm, rv)])
+        x, W, bias, gamma, beta, rm, rv, res, y_pre, out, mean, invstd = t
+        outs.append([v.clone() for v in (out, y_pre, mean, invstd, rm, rv)])
     return outs
 
 
@@ -136,3 +148,36 @@ def test_split_handovers_are_bit_identical(cuda_device, training):
     for rep in range(3):
         for i, (a, b) in enumerate(zip(got[rep], ref[rep])):
             assert torch.equal(a, b), (rep, i, float((a.double() - b.double()).abs().max()))
+
+
+def test_fused_conv_bn_beside_held_cus_gives_up_safely(cuda_device):
+    """The column-tile barrier's bounded wait: with 192 of the 256 CUs held by a long kernel on
+    another stream while the fused C2 conv (256 workgroups, one per CU) dispatches, the resident
+    workgroups give up instead of hanging, every output is NaN, and the next check on the context
+    raises (then state is reset and the same call gives the reference bits again)."""
+    dev = cuda_device
+    ref = _conv(dev, 128, 64, 512, 512, RELU, True, False, seed=9)[0]
+    t = _conv_inputs(dev, 128, 64, 512, 512, False, seed=9)  # everything ready before the CUs are held
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(device=dev)
+    _lib.call("avc_debug_persist_spin_limit", 1 << 13)
+    try:
+        side.wait_stream(torch.cuda.current_stream(dev))
+        _lib.call("avc_debug_hog", _lib.context(dev), 192, 160 * 1024, 600_000, side.cuda_stream)
+        n, t0 = ctypes.c_int(0), time.time()
+        while n.value < 192 and time.time() - t0 < 20:
+            _lib.call("avc_debug_hog_resident", _lib.context(dev), ctypes.byref(n))
+            time.sleep(0.001)
+        assert n.value == 192
+        _conv_call(dev, 128, 64, 512, 512, RELU, True, t)  # dispatches while 192 CUs are held
+        torch.cuda.synchronize()
+        bad = [t[9].clone()]
+    finally:
+        _lib.call("avc_debug_persist_spin_limit", 0)
+    # (workgroups that passed the barrier before the first give-up may still have written numbers)
+    assert torch.isnan(bad[0]).any(), "a fused conv that gave up returned only numbers"
+    with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+        _lib.call("avc_persist_check", _lib.context(dev), _lib.stream(dev), None)
+    again = _conv(dev, 128, 64, 512, 512, RELU, True, False, seed=9)[0]
+    for a, b in zip(again, ref):
+        assert torch.equal(a, b)
