@@ -68,6 +68,7 @@ _SIGS = {
     "avc_gemm_config": [_I],
     "avc_bn_fuse": [_I],
     "avc_split_handover": [_I],
+    "avc_debug_bnf_inject": [_I],
     "avc_lstm_persist_tune": [_I],
     "avc_lstm_persist_depth": [_I],
     "avc_lstm_persist_layers": [_I],

@@ -1792,6 +1792,7 @@ int guard_scan(avc_context* ctx, const float* src, long rows, long cols, long ld
 
 // ---- fused BatchNorm epilogue: eligibility and launch ------------------------------------
 int g_bnf = 1;  // avc_bn_fuse()
+int g_bnf_inject = 0;  // avc_debug_bnf_inject(): train-mode fused launches left that give up at once
 
 namespace {
 // the two gemm16f instances the plans pick (128 x 128: avc_gemm_config 8; 64 x 64), BNF = 1
@@ -1846,6 +1847,10 @@ int launch16f_bnf(avc_context* ctx, GemmDesc d, Frag16Args f, const Plan& p, hip
   d.bnf.cnt = region + 64;
   d.bnf.fail_host = flags;
   d.bnf.spin_limit = coresident_spin_limit();
+  if (g_bnf_inject > 0) {  // test hook: this launch's barrier gives up at its first unmet poll
+    --g_bnf_inject;
+    d.bnf.spin_limit = 0;
+  }
   d.bnf.nwg = nwg;
   return coresident_dispatch(ctx, fn, dim3(nwg), dim3(bnf_threads(bm)), args, bnf_lds(bm), s);
 }
@@ -2056,5 +2061,14 @@ extern "C" int avc_bn_fuse(int on) {
   }
   avc::g_bnf = on;
   ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_debug_bnf_inject(int launches) {
+  if (launches < 0) {
+    avc::set_error("avc_debug_bnf_inject: launches must be >= 0");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_bnf_inject = launches;
   return AVC_OK;
 }

@@ -294,6 +294,10 @@ int avc_bn_fuse(int on);
  * the split image that contraction streams, written by their own epilogues; 0 = fp32 outputs and
  * a split pass in front of each consumer.  Both give the same bits. */
 int avc_split_handover(int on);
+/* Test hook: the next `launches` train-mode fused-BatchNorm conv launches give up at their
+ * barrier's first unmet poll (NaN outputs; the next call or avc_persist_check reports it, as for
+ * avc_debug_persist_inject). */
+int avc_debug_bnf_inject(int launches);
 /* Decoder lstm2 (two stacked layers, H = 512 or 1024, batch <= 64) and decoder lstm1 (one layer,
  * batch <= 256) as ONE weight-stationary launch each (lstm_persist.hip) instead of one launch per
  * time step: 0 = never; whenever eligible with the in-launch hand-offs read 1 = after an

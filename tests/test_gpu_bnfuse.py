@@ -193,3 +193,22 @@ def test_fused_conv_bn_beside_held_cus_completes(cuda_device):
     else:
         for a, b in zip(got, ref):
             assert torch.equal(a, b)
+
+
+def test_fused_conv_bn_give_up_is_nan_and_reported(cuda_device):
+    """The barrier's bounded wait, forced (avc_debug_bnf_inject): the launch gives up instead of
+    waiting, its output carries NaN, the next check on the context raises, and after that reset
+    the same call gives the reference bits again (a fresh counter region)."""
+    dev = cuda_device
+    ref = _conv(dev, 128, 64, 512, 512, RELU, True, False, seed=13)[0]
+    _lib.call("avc_debug_bnf_inject", 1)
+    try:
+        bad = _conv(dev, 128, 64, 512, 512, RELU, True, False, seed=13)[0]
+    finally:
+        _lib.call("avc_debug_bnf_inject", 0)
+    assert torch.isnan(bad[0]).any(), "a fused conv that gave up returned only numbers"
+    with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+        _lib.call("avc_persist_check", _lib.context(dev), _lib.stream(dev), None)
+    again = _conv(dev, 128, 64, 512, 512, RELU, True, False, seed=13)[0]
+    for a, b in zip(again, ref):
+        assert torch.equal(a, b)
