@@ -88,6 +88,7 @@ _SIGS = {
     "avc_debug_persist_spin_limit": [ctypes.c_uint],
     "avc_debug_hog": [_P, _I, _I, ctypes.c_long, _P],
     "avc_debug_hog_resident": [_P, ctypes.POINTER(_I)],
+    "avc_debug_hog_xcds": [_P, ctypes.POINTER(_I)],
     "avc_graph_mode": [_I],
     "avc_timing_reset": [],
     "avc_timing_read": [_I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),

@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import itertools
 import inspect
+import math
 import time
 
 import torch
@@ -54,6 +55,10 @@ class FusedAdam(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros_like(model._flat_param)
         self._step = 0
         self._step_t = torch.tensor(0.0)
+        # the previous update's gradient norm, copied to pinned host memory behind the update, and
+        # the event after that copy: a non-finite norm means the device skipped that update
+        self._pending = None
+        self._norm_host = torch.empty(1, dtype=torch.float32, pin_memory=torch.cuda.is_available())
         for p, (off, n) in zip(params, model._flat_slices):
             self.state[p] = {"step": self._step_t, "exp_avg": self.exp_avg[off:off + n].view_as(p),
                              "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p)}
@@ -70,6 +75,7 @@ class FusedAdam(torch.optim.Optimizer):
         if not m._flat_valid():
             raise RuntimeError("parameters were re-allocated after the optimizer was built")
         g = self.param_groups[0]
+        self._settle()
         self._step += 1
         self._step_t.fill_(float(self._step))
         norm = torch.empty((), dtype=torch.float32, device=m._flat_param.device)
@@ -81,7 +87,28 @@ class FusedAdam(torch.optim.Optimizer):
                   float(max_norm), float(ema_decay), norm.data_ptr(), _lib.stream(norm.device))
         m._param_epoch += 1  # parameters changed outside torch's version counters
         self.last_grad_norm = norm
+        # (the norm is always formed here, so the kernel's skip guard is always armed)
+        self._norm_host.copy_(norm.reshape(1), non_blocking=True)
+        self._pending = torch.cuda.Event()
+        self._pending.record(torch.cuda.current_stream(norm.device))
         return loss
+
+    def _settle(self):
+        """Account for the last update: when its gradient norm was not finite the device kept
+        parameters, moments and EMA (adam_ema_kernel), so that step did not happen and the count
+        (Adam's bias correction, the checkpoint's step) goes back.  The event has normally long
+        completed by the next step (a forward and backward were enqueued behind it)."""
+        ev, self._pending = self._pending, None
+        if ev is None:
+            return
+        ev.synchronize()
+        if not math.isfinite(float(self._norm_host[0])):
+            self._step -= 1
+            self._step_t.fill_(float(self._step))
+
+    def state_dict(self):
+        self._settle()
+        return super().state_dict()
 
     def load_state_dict(self, state_dict):
         """torch.optim.Adam's state_dict (the reference checkpoint's optimizer_state, model.py:175):
@@ -100,6 +127,7 @@ class FusedAdam(torch.optim.Optimizer):
                 steps.add(int(float(st[i]["step"])))
         if len(steps) > 1:
             raise ValueError("per-parameter Adam step counts differ; the fused update keeps one")
+        self._pending = None
         self._step = steps.pop() if steps else 0
         self._step_t.fill_(float(self._step))
         for g, sg in zip(self.param_groups, state_dict["param_groups"]):
@@ -387,8 +415,11 @@ class AutoEncoder(nn.Module):
         # backward kernels (ops.GradSink), not returned and added by autograd
         red = self._grad_buckets() if (dp.world() > 1 or self.grad_comm is not None) else None
         sink = None
-        if self.inplace_grads:
-            sink = ops.GradSink(notify=red.param_ready if red is not None else None, comm=red)
+        if self.inplace_grads or red is not None:
+            # without in-place gradients the sink still carries the co-residency hooks of the
+            # data-parallel exchange (autograd's accumulate hooks then count the parameters)
+            notify = red.param_ready if red is not None and self.inplace_grads else None
+            sink = ops.GradSink(notify=notify, comm=red, inplace=self.inplace_grads)
             ops.set_grad_sink(sink)
         try:
             out_decoder, out_postnet, content_codes = self._forward_layers(X, c_org, c_org)

@@ -1049,7 +1049,18 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
   int tm, tn;
-  tile_of(wgid, tilesM, tilesN, tm, tn);
+  if constexpr (BNF) {
+    // fused BN: the barrier group of column tile tn (its tilesM row tiles) is the contiguous
+    // dispatch range [tn * tilesM, (tn + 1) * tilesM), dealt evenly over the XCDs, so a group needs
+    // only its own tilesM workgroups resident, never the whole grid (bnf_epilogue).
+    // Per XCD the row tiles are tm = x mod 8 under all tilesN column tiles: the same L2 reuse as
+    // tile_of's bands.
+    tn = bid / tilesM;
+    tm = bid - tn * tilesM;
+    (void)wgid;
+  } else {
+    tile_of(wgid, tilesM, tilesN, tm, tn);
+  }
   const int split = blockIdx.y % nsplit, z = blockIdx.y / nsplit;
   const int ktotal = d.ntaps * kt_per_tap;
   const int kt0 = split * kps;
@@ -1830,7 +1841,7 @@ int launch16f_bnf(avc_context* ctx, GemmDesc d, Frag16Args f, const Plan& p, hip
   int kps = d.ntaps * kt_per_tap, nsplit = 1;
   int tilesM = (d.M + bm - 1) / bm, tilesN = (d.N + bm - 1) / bm;
   const int nwg = tilesM * tilesN;
-  AVC_CHECK_ARG(nwg <= bnf_capacity(bm), "fused BatchNorm GEMM: the grid is not co-resident");
+  AVC_CHECK_ARG(tilesM <= bnf_capacity(bm), "fused BatchNorm GEMM: a column tile's workgroups are not co-resident");
   const void* fn = bnf_fn(bm);
   float* slab = nullptr;
   void* args[] = {&d, &f, &tilesM, &tilesN, &kt_per_tap, &kps, &nsplit, &slab};
@@ -1864,7 +1875,12 @@ bool gemm_bnf_ok(const GemmDesc& d, bool training) {
   if (training) p.nsplit = 1;  // a stats product never splits K (gemm_run)
   if (p.nsplit != 1 || p.bm != p.bn) return false;
   if (p.bm == 128 && g_gemm_cfg != 8) return false;  // the fused instance is configuration 8's
-  return p.tilesM * p.tilesN <= bnf_capacity(p.bm);
+  // The invariant the barrier needs: one column tile's tilesM workgroups (a contiguous dispatch
+  // range) resident at once.  avc_bn_fuse(1) also keeps the fused form to grids that are one
+  // co-resident wave; 2 takes it wherever a single group fits (multi-wave grids, e.g. C3's 1024).
+  const int cap = bnf_capacity(p.bm);
+  if (p.tilesM > cap) return false;
+  return g_bnf == 2 || p.tilesM * p.tilesN <= cap;
 }
 
 int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) {
@@ -2055,8 +2071,8 @@ extern "C" int avc_gemm_config(int cfg) {
 }
 
 extern "C" int avc_bn_fuse(int on) {
-  if (on < 0 || on > 1) {
-    avc::set_error("avc_bn_fuse: on must be 0 or 1");
+  if (on < 0 || on > 2) {
+    avc::set_error("avc_bn_fuse: on must be 0, 1 or 2");
     return AVC_ERR_INVALID;
   }
   avc::g_bnf = on;

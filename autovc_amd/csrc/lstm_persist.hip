@@ -201,6 +201,13 @@ int g_persist_gran = 1;
 // steps: a producer at step t has seen h_{t-1} of every workgroup of its group, so every reader
 // of step t - 2 is done (ring >= 2 suffices); the tag carries t & 7 so the step t - 4 left in the
 // same entry never matches, and E so an earlier launch's granules never do.
+// Torn reads: the memory model does not promise that a 16-B load sees an 8-B store whole, so the
+// stored tag word is gr_tag ^ data and a consumer accepts a granule only when tag ^ data equals
+// this step's gr_tag.  With data and tag from different stores: a new tag with an old data word
+// passes only if the two data words are equal, and an old tag with the new data word only ever
+// hands over the new data -- either way the accepted data is this step's, so a tear can delay a
+// consumer (it re-loads) but never feed it stale h.  (Old tag with old data never passes: tags of
+// different steps or launches differ, and a zeroed entry's 0 is no tag, E >= 1.)
 constexpr int kGrRing = 4;
 __host__ __device__ __forceinline__ unsigned gr_tag(unsigned E, int t) { return (E << 3) | (unsigned)(t & 7); }
 
@@ -739,7 +746,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
             for (int r = 0; r < RT; ++r)
 #pragma unroll
-              for (int j = 0; j < 4; ++j) ok = ok & (gv[c][r][j][1] == tg) & (gv[c][r][j][3] == tg);
+              for (int j = 0; j < 4; ++j)
+                ok = ok & ((gv[c][r][j][1] ^ gv[c][r][j][0]) == tg) & ((gv[c][r][j][3] ^ gv[c][r][j][2]) == tg);
           if (__all(ok)) break;
           if (spin_give_up(spins, a, E, lane)) {
             good = false;
@@ -869,7 +877,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           const int lu = 8 * (lp >> 4) + 2 * j + hh;
 #pragma unroll
           for (int r = 0; r < RT; ++r) {
-            const u32x2 gr = {hst[(r * 16 + (lp & 15)) * 16 + lu], tg};
+            const unsigned hd = hst[(r * 16 + (lp & 15)) * 16 + lu];
+            const u32x2 gr = {hd, tg ^ hd};  // the tag word covers the data word (torn reads: gr_tag)
             const int off = (((r * nck + (cb >> 1)) * 4 + j) * 64 + 32 * (cb & 1) + lp) * 16 + hh * 8;
             __builtin_amdgcn_raw_buffer_store_b64(gr, ors, off, 0, 16 /*sc1*/);
           }
@@ -2039,12 +2048,16 @@ namespace avc {
 namespace {
 // Test load for the co-residency tests: n_wg workgroups that each hold lds_bytes of LDS (a whole
 // CU at the maximum) for `ticks` of the constant 100 MHz wall clock, counting themselves resident
-// in a pinned host word of its own first.  Bounded by construction (no waits on anything but the clock).
+// in a pinned host word of its own first (1 + the XCD the workgroup runs on, HW_REG_XCC_ID, so a
+// test can see how many CUs each XCD has left).  Bounded by construction (no waits on anything but
+// the clock).
 __global__ void __launch_bounds__(64) hog_kernel(unsigned long long ticks, unsigned* resident) {
   extern __shared__ unsigned hog_lds[];
   if (threadIdx.x == 0) {
     hog_lds[0] = 1u;
-    __hip_atomic_store(resident + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    __hip_atomic_store(resident + blockIdx.x, 1u + (xcc & 7u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned long long t0 = wall_clock64();
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
   }
@@ -2083,6 +2096,16 @@ extern "C" int avc_debug_hog_resident(avc_context* ctx, int* n) {
   int k = 0;
   for (int i = 0; g_hog_words && i < g_hog_n; ++i) k += __atomic_load_n(g_hog_words + i, __ATOMIC_ACQUIRE) != 0;
   *n = k;
+  return AVC_OK;
+}
+
+extern "C" int avc_debug_hog_xcds(avc_context* ctx, int* per_xcd) {
+  AVC_CHECK_ARG(ctx != nullptr && per_xcd != nullptr, "NULL pointer");
+  for (int x = 0; x < 8; ++x) per_xcd[x] = 0;
+  for (int i = 0; g_hog_words && i < g_hog_n; ++i) {
+    const unsigned v = __atomic_load_n(g_hog_words + i, __ATOMIC_ACQUIRE);
+    if (v) ++per_xcd[(v - 1) & 7];
+  }
   return AVC_OK;
 }
 

@@ -49,11 +49,12 @@ class GradSink:
     model.py:201); when the last use's backward has written, `notify(p)` fires -- the data-parallel
     bucketed all-reduce (dp.GradBuckets.param_ready) hangs off it."""
 
-    def __init__(self, notify=None, comm=None):
+    def __init__(self, notify=None, comm=None, inplace=True):
         self.notify = notify
         self.comm = comm            # dp.GradBuckets (data parallel): the co-residency hooks
+        self.inplace = inplace      # False: only the co-residency hooks (autograd accumulates gradients)
         self.uses = {}
-        self.recurrences = 0        # decoder LSTM layers run forward whose backward is still to come
+        self.recurrences = 0        # persistent LSTM backwards still to come (their forwards ran)
 
     def recurrence_begin(self):
         if self.comm is not None:
@@ -89,10 +90,18 @@ def _use(*params):
         _sink.use(*params)
 
 
+def _persistent_bptt(T, B, H):
+    """Will avc_lstm_backward at (T, B, H) be a persistent launch (avc_bptt_persist_eligible, a
+    cached lookup in the library; asked at both ends, so a toggle in between is seen)?  Only those
+    need the co-residency hooks: the other backwards are ordinary launches a collective may run
+    beside."""
+    return H != 32 and bool(_lib.load().avc_bptt_persist_eligible(T, B, H))
+
+
 def _param_grads(params, needs):
     """Gradient buffers for a layer's parameters: their own `.grad` (in place, accumulating) when
     a sink is active and every needed one exists, else fresh tensors.  Returns (buffers, direct)."""
-    if _sink is not None and all(p.grad is not None and p.grad.is_contiguous() and p.grad.shape == p.shape
+    if _sink is not None and _sink.inplace and all(p.grad is not None and p.grad.is_contiguous() and p.grad.shape == p.shape
                                  for p, n in zip(params, needs) if n and p is not None):
         return [p.grad if (n and p is not None) else None for p, n in zip(params, needs)], True
     return [torch.empty_like(p) if (n and p is not None) else None for p, n in zip(params, needs)], False
@@ -268,7 +277,7 @@ def _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, reverse, save, T, B):
     call("avc_lstm_forward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
          ptr(w_hh.contiguous()), ptr(b_ih), ptr(b_hh), y.data_ptr() + col * F32, ldy, ptr(gates),
          ptr(cst), _stream(x))
-    if save and _sink is not None and H != 32:
+    if save and _sink is not None and _persistent_bptt(T, B, H):
         _sink.recurrences += 1
     return gates, cst
 
@@ -280,9 +289,10 @@ def _lstm_bwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, gates, cst, d_y, d_x, reve
     (dwi, dwh, dbi, dbh), direct = _param_grads(params, needs)
     # the kernels write all four: fill the ones autograd does not want with scratch
     scratch = [torch.empty_like(p) if b is None else b for p, b in zip(params, (dwi, dwh, dbi, dbh))]
-    # decoder LSTMs: the BPTT may be a persistent launch; the data-parallel all-reduce keeps its
-    # collectives away from its dispatch (dp.GradBuckets, co-residency rule)
-    sink = _sink if H != 32 else None
+    # a persistent BPTT launch (decoder LSTMs at B = 128 / 256): the data-parallel all-reduce keeps
+    # its collectives away from its dispatch (dp.GradBuckets, co-residency rule); other shapes are
+    # ordinary launches and take no fence
+    sink = _sink if _sink is not None and _persistent_bptt(T, B, H) else None
     if sink is not None:
         sink.recurrence_begin()
     call("avc_lstm_backward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),

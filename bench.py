@@ -320,7 +320,7 @@ def setup_generator(args, dev, rank):
             "algorithmic_gflop_per_step": round((56.77e6 if fwd else 192.2e6) * B * T / 1e9, 1),
         },
         "cpu": ((lambda out: _with_dmel(cpu_baseline(args, sd, x_np, out, B, T, rank))) if fwd else
-                (lambda out: (cpu_train_baseline(args, sd, T), {}))),
+                (lambda out: (cpu_train_baseline(args, sd, T, B), {}))),
         "extra": eval_bn if fwd else None,
     }
 
@@ -356,7 +356,7 @@ def setup_long(args, dev, rank):
 
     def cpu(out):
         from oracle import autovc_oracle as orc
-        cores = min(16, len(os.sched_getaffinity(0)))
+        cores, cpu_desc = _cpu_share()
         torch.set_num_threads(cores)
         # bounded sample: the first 4 utterances of the batch (same lengths, same padding)
         n = min(4, B)
@@ -377,7 +377,7 @@ def setup_long(args, dev, rank):
                  "kind": "port",
                  "sample": f"{len(times)} timed reps of the first {n} utterances of the C5 batch (padded to {T}) "
                            f"through the oracle forward, median; unpadded frames counted; "
-                           f"{torch.get_num_threads()} torch threads"}, {})
+                           f"{torch.get_num_threads()} torch threads; {cpu_desc}"}, {})
 
     return {
         "step": step, "units_per_step": valid, "unit": "mel-frames/s", "dtype": DTYPE,
@@ -394,6 +394,27 @@ def setup_long(args, dev, rank):
             "algorithmic_gflop_per_step": round(56.77e6 * B * T / 1e9, 1)},
         "cpu": cpu,
     }
+
+
+def _cpu_share():
+    """Threads for a CPU baseline: every core of this process's affinity set, except that a box
+    which grants this job a share of a larger machine says so in OMP_NUM_THREADS (the GPU boxes
+    here: 16 per GPU, of the whole machine's cores) -- the share is then used.  Returns (threads,
+    a description naming the CPU model and both counts)."""
+    aff = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    n = min(aff, int(share)) if share.isdigit() and int(share) > 0 else aff
+    model = "unknown CPU"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    why = f" (the job's CPU share, OMP_NUM_THREADS={share})" if n < aff else " (the whole affinity set)"
+    return n, f"{n} threads of {aff} in the affinity set{why}, {model}"
 
 
 def _with_dmel(r):
@@ -425,9 +446,11 @@ def setup_mel(args, dev, rank):
         times.sort()
         med = times[len(times) // 2]
         d = float((out.float().cpu() - ref).abs().max())
+        _, cpu_desc = _cpu_share()
         return ({"value": round(F / med, 1), "unit": "mel-frames/s", "cores": 1, "kind": "port",
                  "sample": f"{len(times)} timed reps of the same 60 s utterance through the float64 numpy "
-                           f"restatement (oracle/audio_oracle.py; numpy rfft, single thread), median"},
+                           f"restatement (oracle/audio_oracle.py; numpy rfft, single thread: numpy's FFT "
+                           f"does not thread), median; CPU: {cpu_desc}"},
                 {"max_abs_dmel_vs_cpu": d})
 
     return {
@@ -458,7 +481,7 @@ def setup_se(args, dev, rank):
 
     def cpu(out):
         from oracle import audio_oracle as ao
-        cores = min(16, len(os.sched_getaffinity(0)))
+        cores, cpu_desc = _cpu_share()
         torch.set_num_threads(cores)
         ref = ao.embed_utterance(sd, wav_np)
         times = []
@@ -472,7 +495,7 @@ def setup_se(args, dev, rank):
         d = float(abs(out.numpy() - ref).max())
         return ({"value": round(SE_SECONDS / med, 2), "unit": "audio-seconds/s", "cores": cores, "kind": "port",
                  "sample": f"{len(times)} timed reps of the same 10 s utterance through the oracle (numpy float64 "
-                           f"mel + torch-CPU LSTM, {torch.get_num_threads()} threads), median"},
+                           f"mel + torch-CPU LSTM, {torch.get_num_threads()} threads), median; {cpu_desc}"},
                 {"max_abs_dembed_vs_cpu": d})
 
     return {
@@ -507,7 +530,7 @@ def setup_vocoder(args, dev, rank):
 
     def cpu(out):
         from oracle import wavernn_oracle as wo
-        cores = min(16, len(os.sched_getaffinity(0)))
+        cores, cpu_desc = _cpu_share()
         torch.set_num_threads(cores)
         n = 60
         wo.generate(sd, torch.from_numpy(mel_np), steps=4)  # warm
@@ -519,7 +542,7 @@ def setup_vocoder(args, dev, rank):
         return ({"value": round(audio_s / per_call, 3), "unit": "audio-seconds/s", "cores": cores, "kind": "port",
                  "sample": f"the first {n} of the {L} sequential steps (all {part.shape[0]} fold rows) of the same "
                            f"generate() through the oracle (torch-CPU, {torch.get_num_threads()} threads), "
-                           f"extrapolated linearly to the whole loop (every step is the same work)"},
+                           f"extrapolated linearly to the whole loop (every step is the same work); {cpu_desc}"},
                 {"fold_rows": int(part.shape[0]), "sequential_steps": L})
 
     return {
@@ -557,38 +580,37 @@ def pmc_traffic(cls, args):
     return {"traffic_bytes": c["traffic_bytes"], "source": os.path.relpath(files[-1], HERE)}
 
 
-def cpu_train_baseline(args, sd, T):
+def cpu_train_baseline(args, sd, T, B=256):
     """Oracle training step (oracle/autovc_oracle.py Trainer: fwd, _loss with the second encoder
-    pass, autograd backward, clip 1.0, Adam, EMA — model.py:303-321) on this host's cores.  A full
-    B = 256 step takes tens of seconds on CPU, so the sample is a bounded B = 32 batch (frames/s
-    is per-frame work; BN statistics are per batch either way)."""
+    pass, autograd backward, clip 1.0, Adam, EMA -- model.py:303-321) on this host's cores, at the
+    bench's own batch (B = 256: ~6 s per step on 16 threads): one warm step, then timed steps until
+    --cpu-seconds have passed (at least one)."""
     from oracle import autovc_oracle as orc
     from autovc_amd.weights import onehot_embedding, synthetic_mel
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores, cpu_desc = _cpu_share()
     torch.set_num_threads(cores)
-    Bs = 32
-    X = torch.from_numpy(synthetic_mel(1, Bs, T))
-    c = torch.from_numpy(onehot_embedding(Bs))
+    X = torch.from_numpy(synthetic_mel(1, B, T))
+    c = torch.from_numpy(onehot_embedding(B))
     tr = orc.Trainer(sd)
     tr.step(X, c)  # warm
     times = []
     t_start = time.perf_counter()
-    while len(times) < 2 or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 10):
+    while not times or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 10):
         t1 = time.perf_counter()
         tr.step(X, c)
         times.append(time.perf_counter() - t1)
     times.sort()
     med = times[len(times) // 2]
-    return {"value": round(Bs * T / med, 1), "unit": "mel-frames/s", "cores": cores, "kind": "port",
-            "sample": f"{len(times)} timed training steps (+1 warm) of a B={Bs}, T={T} one-hot batch through the "
-                      f"oracle Trainer, median; {torch.get_num_threads()} torch threads"}
+    return {"value": round(B * T / med, 1), "unit": "mel-frames/s", "cores": cores, "kind": "port",
+            "sample": f"{len(times)} timed training steps (+1 warm) of the bench's B={B}, T={T} one-hot batch "
+                      f"through the oracle Trainer, median; {torch.get_num_threads()} torch threads; {cpu_desc}"}
 
 
 def cpu_baseline(args, sd, x_np, gpu_out, B, T, rank):
     """Oracle forward (torch-CPU restatement, `port`) on this host's cores, same batch."""
     from oracle import autovc_oracle as orc
     from autovc_amd.weights import synthetic_embedding
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores, cpu_desc = _cpu_share()
     torch.set_num_threads(cores)
     x = torch.from_numpy(x_np)
     c_org = torch.from_numpy(synthetic_embedding(101 + rank, B))
@@ -608,7 +630,7 @@ def cpu_baseline(args, sd, x_np, gpu_out, B, T, rank):
     dmel = float((gpu_out[1].float().cpu() - ref[1]).abs().max())
     return ({"value": round(B * T / med, 1), "unit": "mel-frames/s", "cores": cores, "kind": "port",
              "sample": f"{len(times)} timed reps (+1 warm) of the C2 batch (B={B}, T={T}) through the oracle "
-                       f"forward, median; {torch.get_num_threads()} torch threads"}, dmel)
+                       f"forward, median; {torch.get_num_threads()} torch threads; {cpu_desc}"}, dmel)
 
 
 if __name__ == "__main__":

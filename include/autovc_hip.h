@@ -285,9 +285,10 @@ int avc_gemm_config(int cfg);
 /* Conv1d + BatchNorm1d + activation forward (the reference's ConvNorm -> BatchNorm1d -> relu /
  * tanh, encoder.py:69-70, decoder.py:69-70, postnet.py:54-61): 1 (default) = BatchNorm fused
  * into the convolution's GEMM epilogue wherever the GEMM's grid is one co-resident wave of
- * workgroups (train mode: a column-tile barrier inside the launch; eval mode: running
- * statistics), 0 = the GEMM, a statistics launch and a normalise launch.  Both give the same
- * bits. */
+ * workgroups (train mode: a column-tile barrier inside the launch, whose group -- one column
+ * tile's row tiles, a contiguous dispatch range -- must be resident at once; eval mode: running
+ * statistics); 2 = fused wherever one such group fits the device (grids of several waves);
+ * 0 = the GEMM, a statistics launch and a normalise launch.  All give the same bits. */
 int avc_bn_fuse(int on);
 /* Whole-Generator forward: 1 (default) = the encoder's last conv, decoder lstm1 and decoder lstm2
  * hand their outputs to the next contraction (BiLSTM projection, first decoder conv, Linear) as
@@ -371,6 +372,9 @@ int avc_bptt_persist_eligible(int T, int B, int H);
 int avc_debug_persist_spin_limit(unsigned polls);
 int avc_debug_hog(avc_context* ctx, int n_wg, int lds_bytes, long usec, void* stream);
 int avc_debug_hog_resident(avc_context* ctx, int* n);
+/* Test hook: per_xcd[8] = how many of the current hog's started workgroups run on each XCD
+ * (HW_REG_XCC_ID), so a co-residency test can state the CUs each XCD has left. */
+int avc_debug_hog_xcds(avc_context* ctx, int* per_xcd);
 /* Forward-graph policy of avc_generator_forward_cached: 1 = capture on the second call with the
  * same key and replay (default); 0 = always eager (tests that need eager reference outputs). */
 int avc_graph_mode(int on);

@@ -16,6 +16,9 @@ run() {
 for step in "$@"; do
   case $step in
     persist) run persist 300 python -u -m pytest tests/test_gpu_model.py -x -v -s -k persistent --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    bnf)   run bnf 300 python -u -m pytest tests/test_gpu_bnfuse.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    gran)  run gran 300 python -u -m pytest tests/test_gpu_granules.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    safety) run safety 300 python -u -m pytest tests/test_gpu_persist_safety.py tests/test_gpu_coresidency.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kern)  run kern 600 python -m pytest tests/test_gpu_kernels.py -v -m gpu -x --timeout 120 -p no:cacheprovider ;;
     model) run model 600 python -m pytest tests/test_gpu_model.py -v -m gpu -s --timeout 200 -p no:cacheprovider ;;

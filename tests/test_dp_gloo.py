@@ -223,3 +223,28 @@ def test_grad_buckets_overlap_world2():
         assert [b for b, _ in log] == list(range(len(log)))   # strictly in bucket order
         assert log[0][1] > 0, "first bucket was only issued after backward finished"
     assert res[0][3] == res[1][3]  # same issue order on both ranks
+
+
+def test_nccl_branch_places_collective_tensors_on_the_gpu(monkeypatch):
+    """The nccl (RCCL) branch, forced on CPU: RCCL has no CPU backend, so collective_device() must
+    name the current GPU, and broadcast_seed / params_in_sync must hand the collectives tensors on
+    that device (the round-2 fix of the seed broadcast).  The GPU itself is stood in for
+    by a recorder: the collectives record the device of what they are given."""
+    monkeypatch.setattr(dp, "world", lambda: 2)
+    monkeypatch.setattr(dist, "get_backend", lambda *a, **k: "nccl")
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 5)
+    assert dp.collective_device() == torch.device("cuda", 5)
+
+    # the helpers must route through collective_device(); a CPU-only box cannot hold a CUDA
+    # tensor, so the recorder hands out a stand-in device and checks every collective sees it
+    stand_in = torch.device("cpu")
+    asked, seen = [], []
+    monkeypatch.setattr(dp, "collective_device", lambda: asked.append(1) or stand_in)
+    monkeypatch.setattr(dist, "broadcast", lambda t, src, *a, **k: seen.append(("broadcast", t.device)))
+    monkeypatch.setattr(dist, "all_reduce", lambda t, *a, **k: seen.append(("all_reduce", t.device)))
+    seed = dp.broadcast_seed()
+    assert isinstance(seed, int) and 0 <= seed < 2 ** 62
+    assert dp.params_in_sync(torch.randn(64))
+    assert len(asked) == 2
+    assert [s[0] for s in seen] == ["broadcast", "all_reduce", "all_reduce"]
+    assert all(d == stand_in for _, d in seen)

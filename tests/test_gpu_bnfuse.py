@@ -94,6 +94,27 @@ def test_fused_conv_bn_is_bit_identical(cuda_device, T, B, cin, cout, act, resid
     assert torch.isfinite(got[1][0]).all()
 
 
+@pytest.mark.parametrize("training", [True, False])
+def test_fused_conv_bn_multi_wave_is_bit_identical(cuda_device, training):
+    """avc_bn_fuse(2): the fused form on a grid of several waves (C3's conv, B = 256: 1024
+    workgroups, 4 column groups of 256 that pass their barriers one after another) gives the
+    unfused chain's bits, across two launches (epochs)."""
+    shape = (128, 256, 512, 512, RELU, False)
+    try:
+        _fuse(0)
+        ref = _conv(cuda_device, *shape[:5], training, shape[5], seed=6, reps=2)
+        _fuse(2)
+        launches = _lib.persist_launches(cuda_device)
+        got = _conv(cuda_device, *shape[:5], training, shape[5], seed=6, reps=2)
+        if training:
+            assert _lib.persist_launches(cuda_device) - launches == 2  # the fused form ran
+    finally:
+        _fuse(1)
+    for rep in range(2):
+        for a, b in zip(got[rep], ref[rep]):
+            assert torch.equal(a, b)
+
+
 def test_fused_conv_bn_is_taken_at_c2():
     """The C2 conv products take the fused form (one co-resident wave: 256 tiles of 128 x 128)."""
     lib = _lib.load()
@@ -150,30 +171,42 @@ def test_split_handovers_are_bit_identical(cuda_device, training):
             assert torch.equal(a, b), (rep, i, float((a.double() - b.double()).abs().max()))
 
 
-def test_fused_conv_bn_beside_held_cus_completes(cuda_device):
-    """The column-tile barrier beside a long kernel that holds 192 CUs on another stream (the
-    co-residency hazard of DESIGN §7) with the bounded wait cut to 2^13 polls: the call never
-    hangs, and its outcome is consistent -- either the grid got its CUs and the result equals the
-    reference bit for bit, or the barrier gave up, the output carries NaN and the next check on
-    the context raises (after which the same call gives the reference bits again).  (On the
-    round-3 test box the grid completed in 0.35 ms beside the held CUs, so the give-up branch was
-    not reached here.)"""
-    dev = cuda_device
-    ref = _conv(dev, 128, 64, 512, 512, RELU, True, False, seed=9)[0]
-    t = _conv_inputs(dev, 128, 64, 512, 512, False, seed=9)  # everything ready before the CUs are held
+# The two fused instances at C2 shapes: 128 x 128 tiles (tilesM = 64 row tiles per column tile,
+# one workgroup per CU) and postnet's last conv on 64 x 64 tiles (tilesM = 128, two per CU).  Either
+# way one barrier group needs 64 CUs: 8 on each XCD, since a group is a contiguous dispatch range
+# dealt round-robin over the 8 XCDs.
+HELD_SHAPES = [(128, 64, 512, 512, RELU, False), (128, 64, 512, 80, NONE, True)]
+
+
+def _hold_cus(dev, n_hold, stream):
+    """Start avc_debug_hog with n_hold workgroups of 160 KB LDS (one per CU) for 0.6 s on `stream`
+    and wait until all of them run; returns how many it holds on each XCD."""
+    _lib.call("avc_debug_hog", _lib.context(dev), n_hold, 160 * 1024, 600_000, stream.cuda_stream)
+    n, t0 = ctypes.c_int(0), time.time()
+    while n.value < n_hold and time.time() - t0 < 20:
+        _lib.call("avc_debug_hog_resident", _lib.context(dev), ctypes.byref(n))
+        time.sleep(0.001)
+    assert n.value == n_hold
+    per = (ctypes.c_int * 8)()
+    _lib.call("avc_debug_hog_xcds", _lib.context(dev), per)
+    return list(per)
+
+
+def _fused_conv_beside_hog(dev, shape, n_hold, seed):
+    """One train-mode fused conv dispatched while n_hold CUs are held by a kernel on another
+    stream, with the barrier's bounded wait cut to 2^13 polls.  Returns (reference outputs, outputs,
+    gave_up, held per XCD)."""
+    T, B, cin, cout, act, residual = shape
+    ref = _conv(dev, T, B, cin, cout, act, True, residual, seed=seed)[0]
+    t = _conv_inputs(dev, T, B, cin, cout, residual, seed=seed)  # everything ready before the CUs are held
     torch.cuda.synchronize()
     side = torch.cuda.Stream(device=dev)
     _lib.call("avc_debug_persist_spin_limit", 1 << 13)
     try:
         side.wait_stream(torch.cuda.current_stream(dev))
-        _lib.call("avc_debug_hog", _lib.context(dev), 192, 160 * 1024, 600_000, side.cuda_stream)
-        n, t0 = ctypes.c_int(0), time.time()
-        while n.value < 192 and time.time() - t0 < 20:
-            _lib.call("avc_debug_hog_resident", _lib.context(dev), ctypes.byref(n))
-            time.sleep(0.001)
-        assert n.value == 192
+        per = _hold_cus(dev, n_hold, side)
         launches = _lib.persist_launches(dev)
-        _conv_call(dev, 128, 64, 512, 512, RELU, True, t)  # dispatches while 192 CUs are held
+        _conv_call(dev, T, B, cin, cout, act, True, t)  # dispatches while the CUs are held
         torch.cuda.synchronize()
         assert _lib.persist_launches(dev) - launches == 1  # the fused, co-resident form ran
     finally:
@@ -185,14 +218,44 @@ def test_fused_conv_bn_beside_held_cus_completes(cuda_device):
     except RuntimeError as e:
         assert "abandoned a bounded wait" in str(e)
         gave_up = True
-    if gave_up:
-        assert torch.isnan(got[0]).any(), "a fused conv that gave up returned only numbers"
-        again = _conv(dev, 128, 64, 512, 512, RELU, True, False, seed=9)[0]
-        for a, b in zip(again, ref):
-            assert torch.equal(a, b)
-    else:
-        for a, b in zip(got, ref):
-            assert torch.equal(a, b)
+    return ref, got, gave_up, per
+
+
+@pytest.mark.parametrize("shape", HELD_SHAPES, ids=["128x128", "64x64"])
+def test_fused_conv_bn_needs_only_one_column_group(cuda_device, shape):
+    """Positive control of the co-residency invariant: with every CU but 8 per XCD
+    held, the 256-workgroup grid is far from co-resident, but each column tile's group (a
+    contiguous dispatch range, 8 per XCD) is; the groups pass their barriers one after another and
+    the result equals the unfused chain bit for bit."""
+    cus = torch.cuda.get_device_properties(cuda_device).multi_processor_count
+    if cus % 8:
+        pytest.skip(f"{cus} CUs: not 8 equal XCDs")
+    ref, got, gave_up, per = _fused_conv_beside_hog(cuda_device, shape, cus - 64, seed=9)
+    free = [cus // 8 - p for p in per]
+    print("held per XCD", per, "free", free)
+    if min(free) < 8:
+        pytest.skip(f"the hog was not dealt evenly over the XCDs ({per}): no control")
+    assert not gave_up, f"a group of 8 per XCD had 8 free CUs per XCD and still gave up ({per})"
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("shape", HELD_SHAPES, ids=["128x128", "64x64"])
+def test_fused_conv_bn_gives_up_beside_held_cus(cuda_device, shape):
+    """Negative control under real contention: hold all but 56 CUs (at least one XCD keeps at
+    most 7 free, fewer than the 8 one column group places there; 56 free in total is fewer than
+    the group's 64 on any placement).  The first group can never be resident at once, so its
+    barrier must give up within the bounded wait: NaN outputs, a raise on the next check, and after
+    that reset the same call gives the reference bits again."""
+    cus = torch.cuda.get_device_properties(cuda_device).multi_processor_count
+    ref, got, gave_up, per = _fused_conv_beside_hog(cuda_device, shape, cus - 56, seed=10)
+    print("held per XCD", per, "free", [cus // 8 - p for p in per])
+    assert gave_up, f"the barrier passed with only 56 CUs free ({per})"
+    assert torch.isnan(got[0]).any(), "a fused conv that gave up returned only numbers"
+    T, B, cin, cout, act, residual = shape
+    again = _conv(cuda_device, T, B, cin, cout, act, True, residual, seed=10)[0]
+    for a, b in zip(again, ref):
+        assert torch.equal(a, b)
 
 
 def test_fused_conv_bn_give_up_is_nan_and_reported(cuda_device):

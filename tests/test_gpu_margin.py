@@ -10,8 +10,8 @@ For each set three distances are reported on mel / mel_post / codes:
   * the fp32 reference itself vs float64.
 The reference's own distance from exact arithmetic is part of every GPU-vs-reference number (the
 train-mode postnet BNs amplify input noise ~60x), so the GPU-vs-float64 column is what
-says how good the HIP arithmetic is.  The test writes gpurun_out/r03_margin.json (copied to
-profiles/r03_margin.json)."""
+says how good the HIP arithmetic is.  The test writes gpurun_out/r04_margin.json (copied to
+profiles/r04_margin.json)."""
 import json
 import os
 
@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 
 TOL_MEL = 1e-4
 B, T = 64, 128
-OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "r03_margin.json")
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "r04_margin.json")
 
 
 def _scaled(sd, f):
@@ -58,26 +58,27 @@ def results():
         json.dump(res, fh, indent=1)
 
 
-@pytest.mark.parametrize("name", WEIGHT_SETS)
-def test_c2_forward_margin(cuda_device, results, name):
+def _weights(dev, name):
+    if name.startswith("seed") and "_x" not in name:
+        return torch_state_dict(int(name[4:]))
+    if name == "seed0_x4":
+        return _scaled(torch_state_dict(0), 4.0)
+    if name == "seed0_x0.25":
+        return _scaled(torch_state_dict(0), 0.25)
+    return _trained(dev)
+
+
+def _margin(dev, results, key, sd, B, T, xseed=1):
+    """GPU forward vs the oracle in fp32 and float64 (see the module docstring); records and checks."""
     from oracle import autovc_oracle as orc
     torch.set_num_threads(min(16, torch.get_num_threads()))
-    if name.startswith("seed") and "_x" not in name:
-        sd = torch_state_dict(int(name[4:]))
-    elif name == "seed0_x4":
-        sd = _scaled(torch_state_dict(0), 4.0)
-    elif name == "seed0_x0.25":
-        sd = _scaled(torch_state_dict(0), 0.25)
-    else:
-        sd = _trained(cuda_device)
-    x = synthetic_mel(1, B, T)
+    x = synthetic_mel(xseed, B, T)
     co, ct = synthetic_embedding(101, B), synthetic_embedding(201, B)
-
-    ae = AutoEncoder(device=cuda_device, verbose=False)
+    ae = AutoEncoder(device=dev, verbose=False)
     ae.load_state_dict(sd)
-    ae.to(cuda_device).train()
+    ae.to(dev).train()
     with torch.no_grad():
-        outs = [o.cpu() for o in ae(*(torch.from_numpy(a).to(cuda_device) for a in (x, co, ct)))]
+        outs = [o.cpu() for o in ae(*(torch.from_numpy(a).to(dev) for a in (x, co, ct)))]
     ae.check_health()
 
     def oracle(dtype):
@@ -86,16 +87,16 @@ def test_c2_forward_margin(cuda_device, results, name):
         with torch.no_grad():
             return orc.forward(s, *(torch.from_numpy(a).to(dtype) for a in (x, co, ct)), True, bufs)
     r32, r64 = oracle(torch.float32), oracle(torch.float64)
-    rec = {}
-    for i, key in enumerate(("mel", "mel_post", "codes")):
+    rec = {"B": B, "T": T}
+    for i, k in enumerate(("mel", "mel_post", "codes")):
         g, a, e = outs[i].double(), r32[i].double(), r64[i]
-        rec[key] = {"gpu_vs_ref": float((g - a).abs().max()), "gpu_vs_f64": float((g - e).abs().max()),
-                    "ref_vs_f64": float((a - e).abs().max()), "max_abs": float(e.abs().max())}
-    worst = max(rec[k]["gpu_vs_ref"] for k in rec)
+        rec[k] = {"gpu_vs_ref": float((g - a).abs().max()), "gpu_vs_f64": float((g - e).abs().max()),
+                  "ref_vs_f64": float((a - e).abs().max()), "max_abs": float(e.abs().max())}
+    worst = max(rec[k]["gpu_vs_ref"] for k in ("mel", "mel_post", "codes"))
     rec["margin"] = TOL_MEL / worst if worst > 0 else float("inf")
-    results[name] = rec
-    print(f"{name}: " + "; ".join(f"{k} gpu-ref {v['gpu_vs_ref']:.2e} gpu-f64 {v['gpu_vs_f64']:.2e} "
-                                  f"ref-f64 {v['ref_vs_f64']:.2e}" for k, v in rec.items() if k != "margin")
+    results[key] = rec
+    print(f"{key}: " + "; ".join(f"{k} gpu-ref {v['gpu_vs_ref']:.2e} gpu-f64 {v['gpu_vs_f64']:.2e} "
+                                 f"ref-f64 {v['ref_vs_f64']:.2e}" for k, v in rec.items() if isinstance(v, dict))
           + f"; margin {rec['margin']:.2f}x")
     assert np.isfinite(worst)
     for k in ("mel", "mel_post", "codes"):
@@ -103,8 +104,26 @@ def test_c2_forward_margin(cuda_device, results, name):
         # the HIP arithmetic is not further from exact than the fp32 reference's own (factor 2 and
         # a 1e-7 floor: both are sums of many roundings of either sign)
         assert r["gpu_vs_f64"] <= 2 * r["ref_vs_f64"] + 1e-7, (k, r)
-        # the absolute bar where it is meaningful: weight sets on which the fp32 reference itself
-        # stays within half of it from exact arithmetic (x4 / x0.25 push the reference's own error
-        # to 1.5e-3 / 1.5e-4: no fp32 implementation can be held to 1e-4 there)
+        # north_star's 1e-4 bar is asserted where the fp32 reference itself stays within half of it
+        # from exact arithmetic.  Where it does not (the x4 / x0.25 sets: ref - f64 1.5e-3 / 1.5e-4)
+        # the bar is NOT met (GPU - ref 2.5e-3 / 1.6e-4), and only the line above is checked: the GPU
+        # is closer to float64 than the reference there, so the distance is the reference's own
+        # rounding, which an implementation with a different summation order cannot reproduce.
         if r["ref_vs_f64"] < TOL_MEL / 2:
             assert r["gpu_vs_ref"] <= TOL_MEL, (k, r)
+    return rec
+
+
+# the batch sizes convert() actually runs (voice_converter.py:171-175: one utterance, B = 1, with
+# cut=False; batch_forward's slices otherwise) and the smoke test's B = 2, T = 64
+SMALL = [(0, 1, 128), (1, 1, 128), (2, 1, 128), (0, 1, 300), (0, 2, 64), (1, 2, 64), (0, 2, 128), (2, 3, 96)]
+
+
+@pytest.mark.parametrize("seed,B,T", SMALL, ids=[f"seed{s}_B{b}_T{t}" for s, b, t in SMALL])
+def test_small_batch_margin(cuda_device, results, seed, B, T):
+    _margin(cuda_device, results, f"seed{seed}_B{B}_T{T}", torch_state_dict(seed), B, T, xseed=5 + seed)
+
+
+@pytest.mark.parametrize("name", WEIGHT_SETS)
+def test_c2_forward_margin(cuda_device, results, name):
+    _margin(cuda_device, results, name, _weights(cuda_device, name), B, T)

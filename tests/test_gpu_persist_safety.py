@@ -128,6 +128,31 @@ def test_non_finite_gradient_skips_the_update(cuda_device):
     assert not torch.equal(keep[0], ae._flat_param)
 
 
+def test_skipped_update_does_not_count_as_a_step(cuda_device):
+    """A NaN-gradient step followed by a finite one gives exactly the parameters, moments, EMA and
+    step count of the finite step alone (Adam's bias correction sees the updates actually applied;
+    ADVICE r03)."""
+    runs = []
+    for with_nan in (False, True):
+        ae = _model(cuda_device)
+        ae.configure_optimizer()
+        g = torch.randn(ae._flat_grad.shape, generator=torch.Generator().manual_seed(3)).to(cuda_device) * 1e-3
+        if with_nan:
+            ae._flat_grad.copy_(g)
+            ae._flat_grad[777] = float("nan")
+            ae.optimiser.step(max_norm=1.0, ema=ae.avg_params)
+        ae._flat_grad.copy_(g)
+        ae.optimiser.step(max_norm=1.0, ema=ae.avg_params)
+        torch.cuda.synchronize()
+        st = ae.optimiser.state_dict()
+        runs.append(([t.detach().clone() for t in (ae._flat_param, ae.optimiser.exp_avg, ae.optimiser.exp_avg_sq,
+                                                  ae.avg_params)], float(st["state"][0]["step"])))
+    (ref, ref_step), (got, got_step) = runs
+    assert ref_step == got_step == 1.0
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
 def test_cooperative_launch_matches(cuda_device):
     """avc_lstm_persist_coop(1): the same kernels under hipLaunchCooperativeKernel (runtime
     co-residency guarantee), eager and graph-replayed, bit-identical to the default launch."""
