@@ -68,6 +68,7 @@ _SIGS = {
     "avc_gemm_config": [_I],
     "avc_bn_fuse": [_I],
     "avc_split_handover": [_I],
+    "avc_dead_h_stores": [_I],
     "avc_debug_bnf_inject": [_I],
     "avc_lstm_persist_tune": [_I],
     "avc_lstm_persist_depth": [_I],
@@ -78,6 +79,7 @@ _SIGS = {
     "avc_lstm_persist_inproj": [_I],
     "avc_lstm_persist_qwait": [_I],
     "avc_lstm_persist_granules": [_I],
+    "avc_lstm_persist_halves": [_I],
     "avc_lstm32_tune": [_I],
     "avc_bptt_persist": [_I],
     "avc_debug_bptt_diag": [_I],

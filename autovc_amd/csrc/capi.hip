@@ -107,6 +107,7 @@ size_t gen_scratch(int T, int B) {
 // avc_split_handover(): the split-image hand-overs of the whole-Generator forward that do not
 // come from a conv (encoder conv 3 -> BiLSTM projection, lstm1 -> decoder conv 1, lstm2 -> Linear)
 int g_handover = 1;
+int g_dead_y = 1;  // avc_dead_h_stores(): skip the recurrences' fp32 h stores nothing reads (avc_context::dead_y)
 
 int generator_forward(avc_context* ctx, int T, int B, const float* const* P, const float* x,
                       const float* c_org, const float* c_trg, int training, float* mel,
@@ -174,8 +175,16 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   const int D1 = P_DEC_LSTM1;
   // lstm1 also writes its h as the split image the first decoder conv streams (its epilogue, or a
   // split pass where the recurrence is not persistent)
-  AVC_TRY(lstm_forward_impl(ctx, T, B, 320, 512, 0, din, 320, P[D1], P[D1 + 1], P[D1 + 2], P[D1 + 3],
-                            ba, 512, nullptr, nullptr, s, chain && g_handover ? fb : nullptr));
+  struct DeadY {  // the fp32 h of a recurrence is not stored where only its split image is read
+    avc_context* c;
+    DeadY(avc_context* c_, int bits) : c(c_) { c->dead_y = bits; }
+    ~DeadY() { c->dead_y = 0; }
+  };
+  {
+    DeadY dy(ctx, g_dead_y && chain && g_handover ? 1 : 0);  // the first decoder conv streams fb only
+    AVC_TRY(lstm_forward_impl(ctx, T, B, 320, 512, 0, din, 320, P[D1], P[D1 + 1], P[D1 + 2], P[D1 + 3],
+                              ba, 512, nullptr, nullptr, s, chain && g_handover ? fb : nullptr));
+  }
   mark_range_checked(ctx, ba);  // lstm1's h
   AVC_TRY(cba(P_DEC_CONV + 0, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, chain && g_handover ? fb : nullptr, fa));
   AVC_TRY(cba(P_DEC_CONV + 6, 512, 512, bb, ba, AVC_ACT_RELU, nullptr, fa, fb));
@@ -192,8 +201,11 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   lin.prec16 = 1;
   lin.a_bound = 1.f;  // |h| < 1 (lstm2's output): no range scan needed
   const bool lin_frag = g_handover && TB % 32 == 0 && gemm_frag_eligible(lin);
-  AVC_TRY(lstm2_forward_impl(ctx, T, B, 512, 1024, bb, 512, P + D2, P + D2 + 4, l1, l2, nullptr,
-                             nullptr, nullptr, nullptr, s, lin_frag ? fl : nullptr));
+  {
+    DeadY dy(ctx, g_dead_y ? (lin_frag ? 3 : 2) : 0);  // layer 0's h is read split only; l2 too with lin_frag
+    AVC_TRY(lstm2_forward_impl(ctx, T, B, 512, 1024, bb, 512, P + D2, P + D2 + 4, l1, l2, nullptr,
+                               nullptr, nullptr, nullptr, s, lin_frag ? fl : nullptr));
+  }
   if (lin_frag) lin.a_frag = fl;
   if (ctx->prep_version >= 0) {
     bool fb = true;
@@ -723,6 +735,16 @@ int avc_prepared_release(avc_context* ctx) {
 }
 
 }  // extern "C"
+
+extern "C" int avc_dead_h_stores(int on) {
+  if (on < 0 || on > 1) {
+    avc::set_error("avc_dead_h_stores: on must be 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_dead_y = on;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
 
 extern "C" int avc_split_handover(int on) {
   if (on < 0 || on > 1) {

@@ -125,6 +125,11 @@ struct avc_context {
   // inside the current whole-Generator forward; their contractions skip the range scan
   bool track_ranges = false;
   std::vector<const void*> range_ok;
+  // inside the whole-Generator forward: fp32 outputs of the persistent recurrences that nothing
+  // reads (bit 0: the h whose split image y_frag the next contraction streams instead -- lstm1's,
+  // lstm2's layer 1; bit 1: lstm2's layer-0 h, which slot 1 takes from the split hand-off); the
+  // kernels then skip those stores
+  int dead_y = 0;
   unsigned fail_seen = 0;         // value of *fail_host already reported to the caller
   // co-residency hooks (lstm_persist.hip: persist_dispatch): an event recorded right after every
   // persistent launch (avc_persist_notify), and the number of persistent launches so far

@@ -303,13 +303,15 @@ constexpr int kLead3 = 12;  // with back-pressure (in_lead 2 / 3) the input slot
 // bn_apply_frag's split), reduces the 4 waves' K quarters in a fixed order and stores
 // gx0_t = sum * unscale + b0 with whole-line write-through stores, then counts itself in on
 // cnt[3][t].  Slot 0 waits for that counter and reads gx0_t with sc1 loads (the gx1 hand-off form).
-template <int RT, int NCH3>
+// NHI: the recurrence's batch halves (counters per (step, half), see lstm_persist_kernel): this
+// slot computes every row of a step at once and counts in on the step's last half.
+template <int RT, int NCH3, int NHI>
 __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* part, int* flag, unsigned E,
                            unsigned target, int cb) {
   constexpr int NW = 4, NC = 4, MB = 16 * RT, TW = 16 * NC, RP = TW + 4;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
-  const int B = a.B, T = a.T;
+  const int B = a.B, T = a.T, TT = T * NHI;
   const int nck3 = 4 * NCH3;  // a.din == 128 * NCH3
   const long G4 = 4L * a.H;
   const int rep = blockIdx.x & (kRep - 1);
@@ -342,7 +344,7 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
     // back-pressure: at most kLead3 steps ahead of slot 0
     if (tid == 0) {
       const bool check = t >= kLead3 && (a.in_lead == 3 || (a.in_lead == 2 && (t & 3) == 0));
-      const bool ok = !check || wait_ge(cnt + cnt_index(0, T, t - kLead3, rep), target, a, E);
+      const bool ok = !check || wait_ge(cnt + cnt_index(0, TT, (t - kLead3) * NHI + NHI - 1, rep), target, a, E);
       flag[0] = ok ? 1 : 0;
     }
     __syncthreads();
@@ -400,7 +402,7 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid < kRep)
-      __hip_atomic_fetch_add((gu32*)(cnt + cnt_index(a.in_slot, T, t, tid)), 1u, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add((gu32*)(cnt + cnt_index(a.in_slot, TT, t * NHI + NHI - 1, tid)), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -412,25 +414,35 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
 // QW = 1: per-wave waits on quarter counters (see qcnt_index) instead of three polling lanes and a
 // workgroup barrier at the top of every step.
 // GR = 1: granule hand-off of split h (one-layer form, NCH = 4, RT = 1; see gr_tag).
-template <int NCH, int RT, int HO, int PD, int QW, int GR = 0>
+// NH = 2: batch halves (two-layer form with quarter waits; round 4).  The workgroup's rows are two
+// independent halves of 16 * RT rows (LSTM batch rows never interact), walked alternately: step t
+// of half 0, then step t of half 1, each with its own wait, product, reduction, epilogue and
+// publish, on counters per (step, half).  A half's hand-off (drain, counter, the consumers' poll
+// and first loads) then runs while every workgroup computes the other half, instead of on the
+// critical path of the whole step.  Same products, same order per row: bit-identical to NH = 1.
+template <int NCH, int RT, int HO, int PD, int QW, int GR = 0, int NH = 1>
 __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   static_assert(!GR || (NCH == 4 && RT == 1 && HO == 1 && !QW), "granule hand-off: one-layer form, H = 512, RT = 1");
+  static_assert(NH == 1 || (NH == 2 && QW && !GR && HO == 1), "batch halves: two-layer quarter-wait form");
   constexpr int NW = 4, NC = 4;
-  constexpr int MB = 16 * RT;        // batch rows computed (B <= MB)
+  constexpr int MB = 16 * RT;        // batch rows computed per half (B <= MB * NH)
   constexpr int TW = 16 * NC;        // 64 gate rows
   constexpr int RP = TW + 4;
   constexpr int NPAIR = MB * NC;     // (row, 16-column block) epilogue pairs, <= 256
   // LDS: gate tile 3's weights for every wave (NW x NCH x 2 KiB), then the reduction partials
+  // (sized for all NH halves: the input slot reduces every row at once)
   extern __shared__ float lds[];
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds);
   float* part = lds + NW * NCH * 512;
   // [8]: polling lanes' results (0, 1, 3), epoch (2); QW: each wave's wait result (4 + w)
-  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);
+  int* flag = reinterpret_cast<int*>(part + NW * MB * NH * RP);
   // [TW] per-row unscale of this block's gate rows, then [TW] b_ih1 + b_hh1 (slot 1): read from
   // LDS in the epilogue instead of living in registers through the MFMA loop
   float* cpar = reinterpret_cast<float*>(flag + 8);
-  // GR: [MB][16] split h of this workgroup's 16 hidden units, staged for the granule stores
+  // GR: [MB][16] split h of this workgroup's 16 hidden units, staged for the granule stores; then
+  // [MB][16] the unscaled split of the same h for the y_frag image (whole fragment rows, below)
   unsigned* hst = reinterpret_cast<unsigned*>(cpar + 2 * 64);
+  unsigned* yst = hst + MB * NH * 16;
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
@@ -442,6 +454,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   unsigned* const cnt = a.cnt + (long)grp * a.cnt_gstride;
   const int nck = H >> 5;            // 32-deep chunks per row
   const long G4 = 4L * H;
+  const int TT = T * NH;             // counter steps: one per (time step, half)
 
   // this launch's epoch (see the header): every workgroup takes one ticket
   if (tid == 0) {
@@ -453,8 +466,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   const unsigned target = E * (unsigned)a.ncb;
 
   if (a.in_slot > 0 && L == a.in_slot) {  // layer 0's input projection
-    if (a.din == 512) input_slot<RT, 4>(a, cnt, grp, part, flag, E, target, cb);
-    else input_slot<RT, 3>(a, cnt, grp, part, flag, E, target, cb);
+    if (a.din == 512) input_slot<RT * NH, 4, NH>(a, cnt, grp, part, flag, E, target, cb);
+    else input_slot<RT * NH, 3, NH>(a, cnt, grp, part, flag, E, target, cb);
     return;
   }
 
@@ -486,9 +499,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   static_assert(NPAIR * SUB == 256, "one epilogue slot per thread");
   const int pair = tid / SUB, sub = tid % SUB, u0 = sub * UPT;
   const int row = pair / NC, blk = pair % NC;
-  const int b = grp * MB + row;
-  const bool live = b < B;
-  const int bc = min(b, B - 1);
+  const int row0 = grp * MB * NH + row;  // this thread's batch row in half 0 (half hf: + hf * MB)
+  int b = row0;
+  bool live = b < B;
+  int bc = min(b, B - 1);
   const int p0 = cb * TW + blk * 16;       // first permuted gate column of the pair
   const int j0 = cb * 4 * NC + blk * 4;    // first hidden unit of the pair
   typedef float fu __attribute__((ext_vector_type(UPT)));
@@ -496,7 +510,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     cpar[tid] = a.winv[L][cb * TW + tid];
     if (L == 1) cpar[TW + tid] = a.b1[cb * TW + tid];
   }
-  fu cst = fu{};
+  fu cst = fu{}, cst_other = fu{};  // cell state of the current half, and of the other one (NH = 2)
   // slot 1 stores gx1 in whole lines: lane -> (row 4i + lane/16 of the wave's 16, columns 4*pc..)
   const int pc = lane & 15;
   float* c_save = L == 0 ? a.c0 : a.c1;
@@ -506,9 +520,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   const int rep = blockIdx.x & (kRep - 1);
   // outputs nobody reads inside this launch: h, and for training c and the activated gates
   _Float16* const yfrag = L == a.yf_slot ? a.yfrag : nullptr;
-  auto store_out = [&](int tt, const fu& h, const fu& c, const fu& i, const fu& f, const fu& g, const fu& o) {
-    *reinterpret_cast<fu*>(y_out + ((long)tt * B + b) * H + j0 + u0) = h;
-    if (yfrag) {  // split_frag32_kernel's unscaled split (|h| < 1), at its fragment position
+  // frag: also this thread's units of y_frag (the give-up NaN fill; normally yfrag_rows writes it)
+  auto store_out = [&](int tt, const fu& h, const fu& c, const fu& i, const fu& f, const fu& g, const fu& o,
+                       bool frag = false) {
+    if (y_out) *reinterpret_cast<fu*>(y_out + ((long)tt * B + b) * H + j0 + u0) = h;
+    if (yfrag && frag) {  // split_frag32_kernel's unscaled split (|h| < 1), at its fragment position
       const long r = (long)tt * B + b;
       const int k = j0 + u0;
       const long blk = ((r >> 5) * a.yf_nkc + (k >> 4)) * 2;
@@ -534,9 +550,34 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     }
   };
   fu pend_h = {}, pend_c = {}, pend_i = {}, pend_f = {}, pend_g = {}, pend_o = {};  // GR: step t - 1's outputs
+  // y_frag as whole fragment rows (round 4): the MB rows staged in yst (batch rows rb0 ..) of step
+  // tt go out as 16-B pieces, 32 consecutive fragment lanes of one (hi / lo, k half) per 512 B.
+  // This workgroup's 16 units are exactly the 16-k chunk cb of the image.  (Per-thread stores of
+  // 2-8 B pieces left partly written lines on several XCDs; every thread takes part here.)
+  auto yfrag_rows = [&](int tt, int rb0) {
+    for (int p = tid; p < MB * 4; p += 256) {
+      const int r = p % MB, kh = (p / MB) & 1, hl2 = p / (2 * MB);
+      const int bb = rb0 + r;
+      if (bb >= B) continue;
+      const long rr = (long)tt * B + bb;
+      const long blk2 = ((rr >> 5) * a.yf_nkc + cb) * 2 + hl2;
+      const u32x4 q0 = *reinterpret_cast<const u32x4*>(yst + r * 16 + kh * 8);
+      const u32x4 q1 = *reinterpret_cast<const u32x4*>(yst + r * 16 + kh * 8 + 4);
+      auto half = [&](unsigned q) { return hl2 ? q >> 16 : q & 0xffffu; };
+      const u32x4 v = {half(q0[0]) | (half(q0[1]) << 16), half(q0[2]) | (half(q0[3]) << 16),
+                       half(q1[0]) | (half(q1[1]) << 16), half(q1[2]) | (half(q1[3]) << 16)};
+      *reinterpret_cast<u32x4*>(yfrag + blk2 * 512 + ((rr & 31) + 32 * kh) * 8) = v;
+    }
+  };
 
-  int t = 0;
-  for (; t < T; ++t) {
+  int s = 0;
+  for (; s < TT; ++s) {
+    const int t = NH == 1 ? s : s / NH, hf = NH == 1 ? 0 : s % NH;
+    if constexpr (NH > 1) {
+      b = row0 + hf * MB;
+      live = b < B;
+      bc = min(b, B - 1);
+    }
     // ---- wait for this step's operands ----------------------------------------------------
     AVC_PSTAMP(0);
     if constexpr (QW || GR) {
@@ -553,14 +594,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         const int hsl = L == 1 ? 0 : L;      // slot whose h this slot reads (0: h0, 2: h1)
         const int ht = L == 1 ? t : t - 1;   // and its step
         // 0: the h quarter; 1: the gx operand; 2: back-pressure (wave 1)
+        // (NH = 2: h and gx1 per (step, half); the input slot's gx0 and the back-pressure per step,
+        // taken at half 0 on the last half's counters -- a workgroup publishes its halves in order)
         const bool e0 = !GR && ht >= 0;
-        unsigned* p0 = cnt + qcnt_index(a.nslot, hsl, T, e0 ? ht : 0, w, rep);
-        const bool e1 = L == 2 || (L == 0 && a.in_slot > 0 && (t & 3) == 0);
-        unsigned* p1 = L == 2 ? cnt + qcnt_index(a.nslot, 1, T, t, cb / (a.ncb / kQuarters), rep)
-                              : cnt + cnt_index(a.in_slot, T, min(t + 3, T - 1), rep);
+        unsigned* p0 = cnt + qcnt_index(a.nslot, hsl, TT, e0 ? ht * NH + hf : 0, w, rep);
+        const bool e1 = L == 2 || (L == 0 && a.in_slot > 0 && (t & 3) == 0 && hf == 0);
+        unsigned* p1 = L == 2 ? cnt + qcnt_index(a.nslot, 1, TT, t * NH + hf, cb / (a.ncb / kQuarters), rep)
+                              : cnt + cnt_index(a.in_slot, TT, min(t + 3, T - 1) * NH + NH - 1, rep);
         const unsigned t1 = L == 2 ? qtarget : target;
-        const bool e2 = !GR && w == 1 && ((L == 0 && t >= kLead && a.nslot >= 3) || (L == 1 && t >= kGxRing));
-        unsigned* p2 = cnt + cnt_index(2, T, e2 ? t - (L == 0 ? kLead : kGxRing) : 0, rep);
+        const bool e2 = !GR && w == 1 && hf == 0 && ((L == 0 && t >= kLead && a.nslot >= 3) || (L == 1 && t >= kGxRing));
+        unsigned* p2 = cnt + cnt_index(2, TT, e2 ? (t - (L == 0 ? kLead : kGxRing)) * NH + NH - 1 : 0, rep);
         flag[4 + w] = wait3(p0, qtarget, e0, p1, t1, e1, p2, target, e2, a, E) ? 1 : 0;
       }
       // the polled values are in (the loop compared them); nothing below moves above this point
@@ -582,12 +625,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       // the input slot runs ahead (up to kLead3 steps), so its progress is checked every 4th step
       // for 4 steps at once: its workgroups finish steps in order, so all of them counting in on
       // step t + 3 implies steps t .. t + 2 are complete (and drained) as well
-      if (tid == 128) idx = L == 0 && a.in_slot > 0 && (t & 3) == 0 ? cnt_index(a.in_slot, T, min(t + 3, T - 1), rep) : -1;
-      else if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, T, t - 1, rep) : -1)
-                                     : (t >= kLead && a.nslot >= 3 ? cnt_index(2, T, t - kLead, rep) : -1);
-      else if (L == 1) idx = primary ? cnt_index(0, T, t, rep)
-                                     : (t >= kGxRing ? cnt_index(2, T, t - kGxRing, rep) : -1);
-      else idx = primary ? (t > 0 ? cnt_index(2, T, t - 1, rep) : -1) : cnt_index(1, T, t, rep);
+      if (tid == 128) idx = L == 0 && a.in_slot > 0 && (t & 3) == 0 ? cnt_index(a.in_slot, TT, min(t + 3, T - 1), rep) : -1;
+      else if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, TT, t - 1, rep) : -1)
+                                     : (t >= kLead && a.nslot >= 3 ? cnt_index(2, TT, t - kLead, rep) : -1);
+      else if (L == 1) idx = primary ? cnt_index(0, TT, t, rep)
+                                     : (t >= kGxRing ? cnt_index(2, TT, t - kGxRing, rep) : -1);
+      else idx = primary ? (t > 0 ? cnt_index(2, TT, t - 1, rep) : -1) : cnt_index(1, TT, t, rep);
       const bool ok = idx < 0 || wait_ge(cnt + idx, target, a, E);
       if (primary) {
         AVC_PSTAMP(1);
@@ -667,7 +710,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       load_gx();
     } else {
       const int hrow16 = nck * 2048;
-      const long hbase = (long)grp * RT * hrow16 + (long)kc0 * 2048;
+      const long hbase = ((long)grp * NH + hf) * RT * hrow16 + (long)kc0 * 2048;
       const auto hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(src) + hbase, 0,
                                                          (int)((long)a.ntile * nck * 2048 - hbase), 0x00020000);
       // h chunk buffers: PDX chunks in flight ahead of the MFMAs.  With one 16-row tile (the
@@ -738,6 +781,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         gload();
         load_gx();
         if (live) store_out(t - 1, pend_h, pend_c, pend_i, pend_f, pend_g, pend_o);
+        if (yfrag) yfrag_rows(t - 1, grp * MB);
         bool good = true;
         for (unsigned spins = 0;; ++spins) {
           bool ok = true;
@@ -819,7 +863,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = w * 16 + i * 4 + (lane >> 4);
-        if (r < MB && r < B) {
+        if (r < MB && hf * MB + r < B) {
           const int off = r * RP + 4 * pc;
           f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
 #pragma unroll
@@ -827,7 +871,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           const f32x4 wiv1 = *reinterpret_cast<const f32x4*>(cpar + 4 * pc);
           const f32x4 b1v = *reinterpret_cast<const f32x4*>(cpar + TW + 4 * pc);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v * wiv1 + b1v), ors,
-                                                 (r * TW + 4 * pc) * 4, 0, 16 /*sc1*/);
+                                                 ((hf * MB + r) * TW + 4 * pc) * 4, 0, 16 /*sc1*/);
         }
       }
     } else {
@@ -860,6 +904,12 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           const _Float16 lo = (_Float16)(v - (float)hi);
           hl[u] = (unsigned)__builtin_bit_cast(unsigned short, hi) |
                   ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
+          if (yfrag) {  // the unscaled split of the y_frag image (store_out's expressions)
+            const _Float16 yh = (_Float16)hv[u];
+            const _Float16 yl = (_Float16)((hv[u] - (float)yh) * 2048.0f);
+            yst[row * 16 + blk * 4 + u0 + u] = (unsigned)__builtin_bit_cast(unsigned short, yh) |
+                                               ((unsigned)__builtin_bit_cast(unsigned short, yl) << 16);
+          }
         }
       }
       if constexpr (GR) {
@@ -924,25 +974,41 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     // lanes 8..15 count in on this workgroup's quarter -- in both wait forms, so every launch adds
     // ncb / 4 to every quarter word and the epoch targets hold whichever form the next launch takes
     if (tid < 2 * kRep) {
-      const long ci = tid < kRep ? cnt_index(L, T, t, tid)
-                                 : qcnt_index(a.nslot, L, T, t, cb / (a.ncb / kQuarters), tid - kRep);
+      const long ci = tid < kRep ? cnt_index(L, TT, s, tid)
+                                 : qcnt_index(a.nslot, L, TT, s, cb / (a.ncb / kQuarters), tid - kRep);
       __hip_atomic_fetch_add((gu32*)(cnt + ci), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // outputs nobody reads inside this launch: stored after publishing (off the hand-off path)
+    // outputs nobody reads inside this launch: stored after publishing (off the hand-off path);
+    // the publish barrier above orders every thread's yst writes before yfrag_rows reads them
     if (L != 1 && live) store_out(t, hv, cst, ig, fg, gg, og);
+    if (yfrag) yfrag_rows(t, row0 - row + hf * MB);
+    if constexpr (NH > 1) {  // the other half's cell state becomes the current one
+      const fu tmp = cst;
+      cst = cst_other;
+      cst_other = tmp;
+    }
   }
+  const int t = NH == 1 ? s : s / NH;  // the step the loop stopped at (T: completed)
   if constexpr (GR) {
     if (t == T && T > 0 && live) store_out(T - 1, pend_h, pend_c, pend_i, pend_f, pend_g, pend_o);
+    if (t == T && T > 0 && yfrag) {  // (the last step staged yst without the granules' barrier)
+      __syncthreads();
+      yfrag_rows(T - 1, grp * MB);
+    }
   }
   // gave up at step t: the rows this workgroup owns for steps t..T-1 are written as NaN, so a
   // timed-out launch never hands plausible numbers downstream (the host reports it, see above) --
   // through every output, the split image included.  The granule form stores a step's outputs
   // one step late, so its step t - 1 is written as NaN as well.
-  if (t < T && L != 1 && live) {
+  if (t < T && L != 1) {
     fu nv;
 #pragma unroll
     for (int u = 0; u < UPT; ++u) nv[u] = __builtin_nanf("");
-    for (int tt = GR && t > 0 ? t - 1 : t; tt < T; ++tt) store_out(tt, nv, nv, nv, nv, nv, nv);
+    for (int h2 = 0; h2 < NH; ++h2) {  // every half's rows (NH = 2: from the step that gave up)
+      b = row0 + h2 * MB;
+      if (b < B)
+        for (int tt = GR && t > 0 ? t - 1 : t; tt < T; ++tt) store_out(tt, nv, nv, nv, nv, nv, nv, true);
+    }
   }
 }
 
@@ -1011,7 +1077,7 @@ int lstm1_rows_per_group(int B, int H) {
 size_t persist_lds(int H, int RT) {
   const int nch = H / 32 / 4;
   return (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 32 + 2 * 64 * sizeof(float) +
-         (size_t)16 * RT * 16 * sizeof(unsigned);
+         (size_t)2 * 16 * RT * 16 * sizeof(unsigned);  // hst + yst
 }
 
 // Does a one-layer launch of (H, RT) hand split h over as granules under the current tuning?
@@ -1022,11 +1088,28 @@ bool persist_gran(int H, int RT) {
   return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd == 2 && !(g_persist_qwait & 2);
 }
 
+int g_persist_halves = 1;  // avc_lstm_persist_halves(): the two-layer form walks two batch halves
+
+// Batch halves (lstm_persist_kernel's NH) a launch of (RT 16-row tiles) takes under the current
+// tuning: 2 for the two-layer form in its default hand-off with at least two tiles, else 1.
+int persist_nh(int RT, bool two_layer) {
+  return two_layer && RT >= 2 && g_persist_halves && (g_persist_qwait & 1) && g_persist_mode == 2 &&
+                 g_persist_pd == 2
+             ? 2
+             : 1;
+}
+
 // The template instance a launch of (H, RT) runs under the current tuning.
 const void* persist_fn(int H, int RT, bool two_layer = true) {
   const bool qw = (g_persist_qwait & (two_layer ? 1 : 2)) != 0;
   const int nch = H / 32 / 4;
   if (!two_layer && persist_gran(H, RT)) return (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 1>;
+  if (persist_nh(RT, two_layer) == 2) {  // RT / 2 tiles per half
+    if (nch == 8) return RT == 2 ? (const void*)lstm_persist_kernel<8, 1, 1, 2, 1, 0, 2>
+                                 : (const void*)lstm_persist_kernel<8, 2, 1, 2, 1, 0, 2>;
+    return RT == 2 ? (const void*)lstm_persist_kernel<4, 1, 1, 2, 1, 0, 2>
+                   : (const void*)lstm_persist_kernel<4, 2, 1, 2, 1, 0, 2>;
+  }
 #define AVC_PERSIST_FN(NCHV, RTV)                                                                 \
   return g_persist_mode == 1 ? (const void*)lstm_persist_kernel<NCHV, RTV, 0, 1, 0>               \
        : g_persist_pd == 1   ? (const void*)lstm_persist_kernel<NCHV, RTV, 1, 1, 0>               \
@@ -1735,7 +1818,8 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   a.winv[0] = winv;
   a.gx0 = gx;
   a.hs0 = hs0; a.hsz = hsz;
-  a.y0 = y; a.g0 = g; a.c0 = c;
+  a.y0 = y_frag && (ctx->dead_y & 1) ? nullptr : y;  // only the split image is read (avc_context::dead_y)
+  a.g0 = g; a.c0 = c;
   a.yfrag = y_frag; a.yf_slot = 0; a.yf_nkc = (H + 31) / 32 * 2;
   a.diag = g_persist_diag;
   set_region_args(a, ctx, region);
@@ -1787,10 +1871,12 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   AVC_TAKE(hs1, unsigned char, (size_t)2 * hsz, sc);                      // ring of 2
   AVC_TAKE(gx1, float, (size_t)kGxRing * (4 * H / 64) * 64 * 64, sc);     // slab ring
   const int nslot = ip ? 4 : 3;
-  // counters [nslot][T][kRep] (one 128-B line each) and the quarter counters in the persistent
-  // region of this layout
+  const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
+  const int NH = persist_nh(RT, true);
+  // counters [nslot][T * NH][kRep] (one 128-B line each, per time step and batch half) and the
+  // quarter counters in the persistent region of this layout
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), (size_t)cnt_words(nslot, T, true), s,
+  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), (size_t)cnt_words(nslot, T * NH, true), s,
                          &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
@@ -1802,11 +1888,12 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   a.winv[0] = winv0; a.winv[1] = winv1i; a.winv[2] = winv1h;
   a.gx0 = gx0; a.b1 = b1_p; a.gx1 = gx1;
   a.hs0 = hs0; a.hs1 = hs1; a.hsz = hsz;
-  a.y0 = y0; a.y1 = y1; a.g0 = g0; a.g1 = g1; a.c0 = c0; a.c1 = c1;
+  a.y0 = (ctx->dead_y & 2) ? nullptr : y0;             // (avc_context::dead_y)
+  a.y1 = y1_frag && (ctx->dead_y & 1) ? nullptr : y1;
+  a.g0 = g0; a.g1 = g1; a.c0 = c0; a.c1 = c1;
   a.yfrag = y1_frag; a.yf_slot = 2; a.yf_nkc = (H + 31) / 32 * 2;
   a.diag = g_persist_diag;
   set_region_args(a, ctx, region);
-  const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
   hipEvent_t ev = timing_begin(TC_LSTM2_PERSIST, s);
   AVC_TRY(persist_launch(ctx, a, RT, 1, s));
   if (ev) {
@@ -1973,6 +2060,16 @@ extern "C" int avc_lstm_persist_granules(int on) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_gran = on;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_halves(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_lstm_persist_halves: 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_halves = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -295,6 +295,10 @@ int avc_bn_fuse(int on);
  * the split image that contraction streams, written by their own epilogues; 0 = fp32 outputs and
  * a split pass in front of each consumer.  Both give the same bits. */
 int avc_split_handover(int on);
+/* Whole-Generator forward: 1 (default) = the persistent recurrences skip the fp32 h stores nothing
+ * reads (lstm2's layer 0, handed to layer 1 as the split hand-off; lstm1's and lstm2's last layer
+ * where the next contraction streams their split image); 0 = store them.  Same outputs either way. */
+int avc_dead_h_stores(int on);
 /* Test hook: the next `launches` train-mode fused-BatchNorm conv launches give up at their
  * barrier's first unmet poll (NaN outputs; the next call or avc_persist_check reports it, as for
  * avc_debug_persist_inject). */
@@ -318,6 +322,11 @@ int avc_lstm_persist_qwait(int mask);
  * critical path); 0 = the counter hand-off.  Applies when bit 1 of the qwait mask is clear and
  * the default hand-off form and depth are set.  Same arithmetic either way (bit-identical). */
 int avc_lstm_persist_granules(int on);
+/* Tuning hook: 1 (default) = the two-layer persistent form (decoder lstm2, batch > 16) walks its
+ * workgroup's rows as two independent batch halves, step t of one half while the other half's
+ * hand-off is in flight (counters per step and half); 0 = all rows at once.  Same arithmetic either
+ * way (bit-identical). */
+int avc_lstm_persist_halves(int on);
 /* Tuning hook: which recurrences may take the persistent form (bit 0 = one layer, e.g. decoder
  * lstm1; bit 1 = two stacked layers, decoder lstm2; default 3 = both). */
 int avc_lstm_persist_layers(int mask);

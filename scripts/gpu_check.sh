@@ -17,6 +17,9 @@ for step in "$@"; do
   case $step in
     persist) run persist 300 python -u -m pytest tests/test_gpu_model.py -x -v -s -k persistent --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     bnf)   run bnf 300 python -u -m pytest tests/test_gpu_bnfuse.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    halves) run halves 300 python -u -m pytest tests/test_gpu_halves.py tests/test_gpu_model.py -k "halves or persistent or back_to_back or c5" -x -v --timeout 150 --timeout-method thread -p no:cacheprovider ;;
+    halvesab) run halvesab 300 python scripts/persist_hook_ab.py avc_lstm_persist_halves 0 1 0 1 0 1 ;;
+    deadab) run deadab 300 python scripts/persist_hook_ab.py avc_dead_h_stores 0 1 0 1 0 1 ;;
     gran)  run gran 300 python -u -m pytest tests/test_gpu_granules.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     safety) run safety 300 python -u -m pytest tests/test_gpu_persist_safety.py tests/test_gpu_coresidency.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
