@@ -1088,7 +1088,8 @@ bool persist_gran(int H, int RT) {
   return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd == 2 && !(g_persist_qwait & 2);
 }
 
-int g_persist_halves = 1;  // avc_lstm_persist_halves(): the two-layer form walks two batch halves
+int g_persist_halves = 0;  // avc_lstm_persist_halves(): the two-layer form walks two batch halves
+                           // (measured slower: C2 lstm2 1062 -> 1335 us, C5 6120 -> 8090 us)
 
 // Batch halves (lstm_persist_kernel's NH) a launch of (RT 16-row tiles) takes under the current
 // tuning: 2 for the two-layer form in its default hand-off with at least two tiles, else 1.

@@ -322,10 +322,10 @@ int avc_lstm_persist_qwait(int mask);
  * critical path); 0 = the counter hand-off.  Applies when bit 1 of the qwait mask is clear and
  * the default hand-off form and depth are set.  Same arithmetic either way (bit-identical). */
 int avc_lstm_persist_granules(int on);
-/* Tuning hook: 1 (default) = the two-layer persistent form (decoder lstm2, batch > 16) walks its
+/* Tuning hook: 1 = the two-layer persistent form (decoder lstm2, batch > 16) walks its
  * workgroup's rows as two independent batch halves, step t of one half while the other half's
- * hand-off is in flight (counters per step and half); 0 = all rows at once.  Same arithmetic either
- * way (bit-identical). */
+ * hand-off is in flight (counters per step and half); 0 (default, measured faster) = all rows at
+ * once.  Same arithmetic either way (bit-identical). */
 int avc_lstm_persist_halves(int on);
 /* Tuning hook: which recurrences may take the persistent form (bit 0 = one layer, e.g. decoder
  * lstm1; bit 1 = two stacked layers, decoder lstm2; default 3 = both). */
