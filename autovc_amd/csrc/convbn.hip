@@ -14,6 +14,9 @@
 #include "kernels.h"
 
 namespace avc {
+
+int g_bnb_frag = 0;  // avc_bn_bwd_frag(): the BN backward writes dY already split
+
 namespace {
 
 // Wt[(tau*cin + ci)*cout + co] = W[(co*cin + ci)*5 + tau]   (forward B operand, [K][N])
@@ -151,7 +154,9 @@ size_t conv_bn_backward_scratch(int T, int B, int cin, int cout) {
   GemmDesc dg;
   dg.M = (int)TB; dg.N = cin; dg.Kc = cout; dg.ntaps = 5; dg.a_rows = TB;
   dg.prec16 = 1; dg.split_scale = 1;
-  return (TB * cout + 5UL * cin * cout) * sizeof(float) + 2 * bn_backward_scratch((int)TB, cout) +
+  // (+ the dY / dY^T fragment images of the split-writing BN backward, avc_bn_bwd_frag)
+  return (TB * cout + 5UL * cin * cout) * sizeof(float) + 2 * bn_backward_frag_scratch((int)TB, cout) +
+         gemm_afrag_bytes(TB, cout) + gemm_afrag_bytes(cout, (int)TB) + 4096 +
          colsum_scratch((int)TB, cout) + std::max(gemm_scratch_bytes(w), gemm_scratch_bytes(dg)) + 2048;
 }
 
@@ -171,40 +176,71 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
   // (d_x overwritten: the caller accumulates parameter gradients in place across uses)
   const int acc_x = accumulate == 1, acc_p = accumulate != 0;
   Scratch sc(ctx);
-  AVC_TAKE(dy, float, (size_t)TB * cout, sc);
-  // the pass that writes dY also yields the conv bias gradient's column partials and max |dY|
-  // (one max shared by dgrad and wgrad)
+  // the two products of dY: dgrad (dX = dY * W, taps as row shifts) and wgrad (dW = dY^T x)
+  GemmDesc gd;
+  gd.M = (int)TB; gd.N = cin; gd.Kc = cout; gd.ntaps = 5;
+  gd.lda = cout; gd.a_rows = TB; gd.a_shift0 = -2L * B; gd.a_tapshift = B;
+  gd.ldb = cin; gd.b_rows = cout; gd.b_tapoff = (long)cout * cin;
+  gd.C = d_x; gd.ldc = cin; gd.accumulate = acc_x;
+  gd.prec16 = 1; gd.split_scale = 1;
+  // dW[co][ci][tau] = sum_r dY[r][co] * x[r + (tau-2)B][ci]
+  GemmDesc gw;
+  gw.M = cout; gw.N = cin; gw.Kc = (int)TB;
+  gw.a_trans = 1; gw.lda = cout;
+  gw.B = x; gw.ldb = cin; gw.b_rows = TB; gw.b_shift0 = -2L * B; gw.b_zshift = B;
+  gw.nz = 5; gw.c_zoff = 1;
+  gw.C = d_weight; gw.ldc = 5L * cin; gw.ldc_col = 5; gw.accumulate = acc_p;
+  gw.prec16 = 1; gw.split_scale = 1;
+  gw.amax_b = x_amax;
+  // round 4 (avc_bn_bwd_frag): the BN backward writes dY already split for both
+  // products -- dY and dY^T fragment images scaled by a proven bound on max |dY| -- so neither the
+  // fp32 dY nor its max scan and two split passes exist
+  const bool fb = g_bnb_frag && (d_x || d_weight) && bn_backward_frag_ok((int)TB, cout, d_out, y_pre) &&
+                  (!d_x || gemm_frag_eligible(gd)) && (!d_weight || gemm_frag_eligible(gw));
   AVC_TAKE(amax_dy, unsigned, 64, sc);
-  const int R = bn_backward_rows((int)TB, cout);
-  AVC_TAKE(bpart, float, (size_t)R * cout, sc);
-  AVC_TRY(bn_backward(ctx, (int)TB, cout, d_out, y_pre, mean, invstd, gamma, beta, act, training,
-                      d_gamma, d_beta, acc_p, dy, s, d_bias ? bpart : nullptr, amax_dy));
-  if (d_bias) AVC_TRY(colsum_finish(R, cout, bpart, d_bias, acc_p, s));
+  float* dy = nullptr;
+  if (fb) {
+    const int R = bn_backward_frag_rows((int)TB);
+    AVC_TAKE(bpart, float, (size_t)R * cout, sc);
+    AVC_TAKE(imgA, _Float16, gemm_afrag_bytes(TB, cout) / 2, sc);
+    AVC_TAKE(imgT, _Float16, gemm_afrag_bytes(cout, (int)TB) / 2, sc);
+    AVC_TRY(bn_backward_frag(ctx, (int)TB, cout, d_out, y_pre, mean, invstd, gamma, beta, act, training, d_gamma,
+                             d_beta, acc_p, imgA, imgT, amax_dy, s, d_bias ? bpart : nullptr));
+    if (d_bias) AVC_TRY(colsum_finish(R, cout, bpart, d_bias, acc_p, s));
+    gd.a_frag = imgA; gd.a_frag_scaled = 1;
+    gw.a_frag = imgT; gw.a_frag_scaled = 1;
+  } else {
+    // the pass that writes dY also yields the conv bias gradient's column partials and max |dY|
+    // (one max shared by dgrad and wgrad)
+    AVC_TAKE(dyb, float, (size_t)TB * cout, sc);
+    dy = dyb;
+    const int R = bn_backward_rows((int)TB, cout);
+    AVC_TAKE(bpart, float, (size_t)R * cout, sc);
+    AVC_TRY(bn_backward(ctx, (int)TB, cout, d_out, y_pre, mean, invstd, gamma, beta, act, training,
+                        d_gamma, d_beta, acc_p, dy, s, d_bias ? bpart : nullptr, amax_dy));
+    if (d_bias) AVC_TRY(colsum_finish(R, cout, bpart, d_bias, acc_p, s));
+  }
+  gd.A = dy; gd.amax_a = amax_dy;
+  gw.A = dy; gw.amax_a = amax_dy;
   if (d_x) {
     AVC_TAKE(wd, float, 5UL * cin * cout, sc);
     conv_weight_dgrad_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wd, cin, cout);
     AVC_LAUNCH_CHECK();
-    GemmDesc g;
-    g.M = (int)TB; g.N = cin; g.Kc = cout; g.ntaps = 5;
-    g.A = dy; g.lda = cout; g.a_rows = TB; g.a_shift0 = -2L * B; g.a_tapshift = B;
-    g.B = wd; g.ldb = cin; g.b_rows = cout; g.b_tapoff = (long)cout * cin;
-    g.C = d_x; g.ldc = cin; g.accumulate = acc_x;
-    g.prec16 = 1; g.split_scale = 1; g.amax_a = amax_dy;
-    AVC_TRY(gemm_run(ctx, g, s));
+    gd.B = wd;
+    AVC_TRY(gemm_run(ctx, gd, s));
   }
-  if (d_weight) {
-    // dW[co][ci][tau] = sum_r dY[r][co] * x[r + (tau-2)B][ci]
-    GemmDesc g;
-    g.M = cout; g.N = cin; g.Kc = (int)TB;
-    g.A = dy; g.a_trans = 1; g.lda = cout;
-    g.B = x; g.ldb = cin; g.b_rows = TB; g.b_shift0 = -2L * B; g.b_zshift = B;
-    g.nz = 5; g.c_zoff = 1;
-    g.C = d_weight; g.ldc = 5L * cin; g.ldc_col = 5; g.accumulate = acc_p;
-    g.prec16 = 1; g.split_scale = 1; g.amax_a = amax_dy;
-    g.amax_b = x_amax;
-    AVC_TRY(gemm_run(ctx, g, s));
-  }
+  if (d_weight) AVC_TRY(gemm_run(ctx, gw, s));
   return AVC_OK;
 }
 
 }  // namespace avc
+
+extern "C" int avc_bn_bwd_frag(int on) {
+  if (on < 0 || on > 1) {
+    avc::set_error("avc_bn_bwd_frag: on must be 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_bnb_frag = on;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}

@@ -26,6 +26,17 @@ int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* 
 // with dy_colpart ([bn_backward_rows(M, C)][C]) / dy_amax: dy's column partial sums (finish with
 // colsum_finish) and max |dy| come out of the same pass that writes dy
 int bn_backward_rows(int M, int C);
+// bn_backward with dy written already split (round 4): imgA = dy as a row-major A
+// operand (gemm_afrag_bytes(M, C)), imgT = dy^T (gemm_afrag_bytes(C, M)), both scaled by the power
+// of two of *bound (zeroed by the caller; a proven upper bound on max |dy|, so GemmDesc::amax_a =
+// bound with a_frag_scaled reuses the images); no fp32 dy.  dy_colpart: [bn_backward_frag_rows(M)][C].
+bool bn_backward_frag_ok(int M, int C, const float* dout, const float* y);
+int bn_backward_frag(avc_context* ctx, int M, int C, const float* dout, const float* y, const float* mean,
+                     const float* invstd, const float* gamma, const float* beta, int act, int training,
+                     float* d_gamma, float* d_beta, int accumulate, _Float16* imgA, _Float16* imgT,
+                     unsigned* bound, hipStream_t s, float* dy_colpart = nullptr);
+int bn_backward_frag_rows(int M);
+size_t bn_backward_frag_scratch(int M, int C);
 int colsum_finish(int R, int N, const float* part, float* out, int accumulate, hipStream_t s);
 int frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* emb, float* out,
                     hipStream_t s);

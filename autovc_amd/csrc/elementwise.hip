@@ -356,22 +356,46 @@ __global__ void bn_bwd_reduce_kernel(int M, int C, const float* __restrict__ dou
   part[((long)blockIdx.y * 2 + 1) * C + c] = s2;
 }
 
+// BnBound (bn_backward_frag): also bound max |dy| before dy exists, so the pass that writes dy can
+// write it already split.  From the reduce pass's per-channel max |dA| and max |x^| (mpart):
+//   |dy_c| = |g_c is_c (dA - k1_c - x^ k2_c)| <= |g_c is_c| (max|dA|_c + |k1_c| + max|x^|_c |k2_c|),
+// maximised over the channels into *bound (pre-zeroed).  The split's power-of-two scale then
+// comes from the bound instead of the exact max: a bound above the max by 2^k only moves the
+// operand k binades down inside f16's range, which leaves hi / lo (and so the product, unscaled
+// exactly) unchanged for every element above 2^-13 of the scaled max.
+struct BnBound {
+  const float* mpart = nullptr;  // [R][2][C] per-block max |dA|, max |x^|
+  const float* gamma = nullptr;
+  const float* invstd = nullptr;
+  float inv_count = 0.f;
+  int training = 0;
+  unsigned* bound = nullptr;     // max over c of the bound above (float bits)
+};
+
 __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const float* __restrict__ part,
                                                             float* __restrict__ sums, float* __restrict__ d_gamma,
                                                             float* __restrict__ d_beta, int accumulate,
-                                                            unsigned* __restrict__ amax) {
+                                                            unsigned* __restrict__ amax, BnBound bb) {
   __shared__ double red[2][16][64];
+  __shared__ float redm[2][16][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   if (amax && blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;  // bn_bwd_apply_cols_kernel raises it
   const int c = blockIdx.x * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
+  float m1 = 0.f, m2 = 0.f;
   if (c < C)
     for (int r = grp; r < R; r += 16) {
       s1 += part[((long)r * 2 + 0) * C + c];
       s2 += part[((long)r * 2 + 1) * C + c];
+      if (bb.bound) {
+        m1 = fmaxf(m1, bb.mpart[((long)r * 2 + 0) * C + c]);
+        m2 = fmaxf(m2, bb.mpart[((long)r * 2 + 1) * C + c]);
+      }
     }
   red[0][grp][cl] = s1;
   red[1][grp][cl] = s2;
+  redm[0][grp][cl] = m1;
+  redm[1][grp][cl] = m2;
   __syncthreads();
   if (grp != 0 || c >= C) return;
   double t1 = 0.0, t2 = 0.0;
@@ -379,11 +403,20 @@ __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const 
   for (int g = 0; g < 16; ++g) {
     t1 += red[0][g][cl];
     t2 += red[1][g][cl];
+    m1 = fmaxf(m1, redm[0][g][cl]);
+    m2 = fmaxf(m2, redm[1][g][cl]);
   }
   sums[c] = (float)t1;
   sums[C + c] = (float)t2;
   if (d_beta) d_beta[c] = accumulate ? d_beta[c] + (float)t1 : (float)t1;
   if (d_gamma) d_gamma[c] = accumulate ? d_gamma[c] + (float)t2 : (float)t2;
+  if (bb.bound) {
+    // the apply pass's own k1 / k2 (sums as float, times 1 / M); a few ulps of slack for the
+    // rounding of the apply's expression
+    const float k1 = bb.training ? (float)t1 * bb.inv_count : 0.f, k2 = bb.training ? (float)t2 * bb.inv_count : 0.f;
+    const float b = fabsf(bb.gamma[c] * bb.invstd[c]) * (m1 + fabsf(k1) + m2 * fabsf(k2)) * 1.0001f;
+    atomicMax(bb.bound, __float_as_uint(b));  // non-negative floats order as their bits
+  }
 }
 
 __global__ void bn_bwd_apply_kernel(long M, int C, const float* __restrict__ dout,
@@ -468,11 +501,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(int M, int C, const
                                                              const float* __restrict__ invstd,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int act, int rows_per,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part, float* __restrict__ mpart,
+                                                             unsigned* __restrict__ zero_word) {
   __shared__ float4 red[2][256];
+  // (bn_backward_frag: the bound word the final kernel raises, zeroed here, a launch before)
+  if (zero_word && blockIdx.y == 0 && threadIdx.x == 0) *zero_word = 0u;
   const int Q = C >> 2, P = 256 / Q;
   const int ph = threadIdx.x / Q, q = threadIdx.x - ph * Q;
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  float mx1[4] = {0.f, 0.f, 0.f, 0.f}, mx2[4] = {0.f, 0.f, 0.f, 0.f};  // max |dA|, max |xh| (mpart)
   if (ph < P) {
     BnQuad k;
     bn_quad_load(k, 4 * q, mean, invstd, gamma, beta);
@@ -489,21 +526,38 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(int M, int C, const
         const float dA = dd[e] * act_bwd(xh * k.g[e] + k.bt[e], act);
         s1[e] += dA;
         s2[e] += dA * xh;
+        mx1[e] = fmaxf(mx1[e], fabsf(dA));
+        mx2[e] = fmaxf(mx2[e], fabsf(xh));
       }
     }
   }
   red[0][threadIdx.x] = make_float4(s1[0], s1[1], s1[2], s1[3]);
   red[1][threadIdx.x] = make_float4(s2[0], s2[1], s2[2], s2[3]);
   __syncthreads();
+  if (ph == 0) {
+    float4 a = red[0][q], b = red[1][q];
+    for (int p = 1; p < P; ++p) {
+      const float4 u = red[0][p * Q + q], v = red[1][p * Q + q];
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+      b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+    }
+    reinterpret_cast<float4*>(part + ((long)blockIdx.y * 2 + 0) * C)[q] = a;
+    reinterpret_cast<float4*>(part + ((long)blockIdx.y * 2 + 1) * C)[q] = b;
+  }
+  if (!mpart) return;
+  __syncthreads();
+  red[0][threadIdx.x] = make_float4(mx1[0], mx1[1], mx1[2], mx1[3]);
+  red[1][threadIdx.x] = make_float4(mx2[0], mx2[1], mx2[2], mx2[3]);
+  __syncthreads();
   if (ph != 0) return;
   float4 a = red[0][q], b = red[1][q];
   for (int p = 1; p < P; ++p) {
     const float4 u = red[0][p * Q + q], v = red[1][p * Q + q];
-    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
-    b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+    a.x = fmaxf(a.x, u.x); a.y = fmaxf(a.y, u.y); a.z = fmaxf(a.z, u.z); a.w = fmaxf(a.w, u.w);
+    b.x = fmaxf(b.x, v.x); b.y = fmaxf(b.y, v.y); b.z = fmaxf(b.z, v.z); b.w = fmaxf(b.w, v.w);
   }
-  reinterpret_cast<float4*>(part + ((long)blockIdx.y * 2 + 0) * C)[q] = a;
-  reinterpret_cast<float4*>(part + ((long)blockIdx.y * 2 + 1) * C)[q] = b;
+  reinterpret_cast<float4*>(mpart + ((long)blockIdx.y * 2 + 0) * C)[q] = a;
+  reinterpret_cast<float4*>(mpart + ((long)blockIdx.y * 2 + 1) * C)[q] = b;
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(int M, int C, const float* __restrict__ dout,
@@ -565,6 +619,130 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(int M, int C, const 
     if ((threadIdx.x & 63) == 0) redm[threadIdx.x >> 6] = mx;
     __syncthreads();
     if (threadIdx.x == 0) amax_update(amax, fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3])));
+  }
+}
+
+// bn_bwd_apply4_kernel writing dy already split (bn_backward_frag; round 4): the two fragment
+// images the conv backward's products stream -- dy as the dgrad product's A (rows = frames, k =
+// channels) and dy^T as the weight gradient's A (rows = channels, k = frames), both in
+// split_frag32_kernel's layout and scaled by the power of two of the bound from
+// bn_bwd_final_kernel (BnBound) -- instead of an fp32 dy that a max scan and two split passes
+// re-read.  Workgroup = 32 frames x 128 channels: dy (same expressions as bn_bwd_apply4_kernel)
+// into an LDS tile, its column sums (the conv bias gradient's partials, one row per 32 frames),
+// then the tile's blocks of both images.  Needs C % 4 == 0.
+__device__ __forceinline__ void bwd_split8(const float* v, h16x8& hi, h16x8& lo) {  // split8 (gemm.hip)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = (_Float16)v[j];
+    hi[j] = h;
+    lo[j] = (_Float16)((v[j] - (float)h) * 2048.0f);
+  }
+}
+__device__ __forceinline__ float pow2_of_bound(const unsigned* w) {  // split_scale_of (gemm.hip)
+  const float m = __uint_as_float(*w);
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, 15 - e);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_frag_kernel(int M, int C, const float* __restrict__ dout,
+                                                                const float* __restrict__ y,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, int act, int training,
+                                                                const float* __restrict__ sums, float inv_count,
+                                                                const unsigned* __restrict__ bound,
+                                                                _Float16* __restrict__ imgA, int nkcA,
+                                                                _Float16* __restrict__ imgT, int nkcT,
+                                                                float* __restrict__ part) {
+  constexpr int TR = 32, TC = 128, LD = TC + 4;
+  __shared__ __attribute__((aligned(16))) float tile[TR][LD];
+  __shared__ float4 csr[4][32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cg = blockIdx.x, rt = blockIdx.y;
+  const int c0 = cg * TC, r0 = rt * TR;
+  const int q = tid & 31, ph = tid >> 5;  // channel quad of the group, row phase (8)
+  const int c = c0 + 4 * q;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    BnQuad k;
+    bn_quad_load(k, c, mean, invstd, gamma, beta);
+    float k1[4], k2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      k1[e] = training ? sums[c + e] * inv_count : 0.f;
+      k2[e] = training ? sums[C + c + e] * inv_count : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TR / 8; ++i) {
+      const int r = ph + 8 * i, m = r0 + r;
+      float o[4] = {0.f, 0.f, 0.f, 0.f};
+      if (m < M) {
+        const long i4 = ((long)m * C + c) >> 2;
+        const float4 yv = reinterpret_cast<const float4*>(y)[i4];
+        const float4 dv = reinterpret_cast<const float4*>(dout)[i4];
+        const float yy[4] = {yv.x, yv.y, yv.z, yv.w}, dd[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (yy[e] - k.mu[e]) * k.is[e];
+          const float dA = dd[e] * act_bwd(xh * k.g[e] + k.bt[e], act);
+          o[e] = training ? k.g[e] * k.is[e] * (dA - k1[e] - xh * k2[e]) : k.g[e] * k.is[e] * dA;
+          cs[e] += o[e];
+        }
+      }
+      *reinterpret_cast<float4*>(&tile[r][4 * q]) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TR / 8; ++i) *reinterpret_cast<float4*>(&tile[ph + 8 * i][4 * q]) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // column sums over the 32 frames in a fixed order: the two phases of a wave, then the 4 waves
+#pragma unroll
+  for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], 32);
+  if (lane < 32) csr[w][q] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+  __syncthreads();
+  if (part && tid < 32 && c < C) {
+    float4 a = csr[0][q];
+#pragma unroll
+    for (int ww = 1; ww < 4; ++ww) {
+      const float4 u = csr[ww][q];
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    }
+    *reinterpret_cast<float4*>(part + (long)rt * C + c) = a;
+  }
+  const float sc = pow2_of_bound(bound);
+  // dy as the dgrad product's A: block (row tile rt, 16-channel chunk kc), lane l = row l & 31,
+  // channels 8 (l >> 5) .. + 7 of the chunk
+  for (int it = tid; it < (TC / 16) * 64; it += 256) {
+    const int kcl = it >> 6, kc = cg * (TC / 16) + kcl;
+    if (kc >= nkcA) continue;
+    const int l = it & 63, r = l & 31, k0 = kcl * 16 + 8 * (l >> 5);
+    const float4 a = *reinterpret_cast<const float4*>(&tile[r][k0]);
+    const float4 b = *reinterpret_cast<const float4*>(&tile[r][k0 + 4]);
+    const float v[8] = {a.x * sc, a.y * sc, a.z * sc, a.w * sc, b.x * sc, b.y * sc, b.z * sc, b.w * sc};
+    h16x8 hi, lo;
+    bwd_split8(v, hi, lo);
+    const long blk = ((long)rt * nkcA + kc) * 2;
+    *reinterpret_cast<h16x8*>(imgA + blk * 512 + l * 8) = hi;
+    *reinterpret_cast<h16x8*>(imgA + (blk + 1) * 512 + l * 8) = lo;
+  }
+  // dy^T as the weight gradient's A: block (channel tile ct, 16-frame chunk 2 rt + j), lane l =
+  // channel l & 31 of the tile, frames 8 (l >> 5) .. + 7 of the chunk
+  const int ntc = (C + 31) / 32;
+  for (int it = tid; it < (TC / 32) * 2 * 64; it += 256) {
+    const int ctl = it >> 7, j = (it >> 6) & 1, ct = cg * (TC / 32) + ctl;
+    if (ct >= ntc) continue;
+    const int l = it & 63, cl = ctl * 32 + (l & 31), rb = j * 16 + 8 * (l >> 5);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = tile[rb + e][cl] * sc;
+    h16x8 hi, lo;
+    bwd_split8(v, hi, lo);
+    const long blk = ((long)ct * nkcT + 2 * rt + j) * 2;
+    *reinterpret_cast<h16x8*>(imgT + blk * 512 + l * 8) = hi;
+    *reinterpret_cast<h16x8*>(imgT + (blk + 1) * 512 + l * 8) = lo;
   }
 }
 
@@ -1013,12 +1191,12 @@ int bn_backward(avc_context* ctx, int M, int C, const float* dout, const float* 
   AVC_TAKE(part, float, (size_t)R * 2 * C, sc);
   AVC_TAKE(sums, float, (size_t)2 * C, sc);
   if (vec) {
-    bn_bwd_reduce4_kernel<<<dim3(1, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta, act, rp, part);
+    bn_bwd_reduce4_kernel<<<dim3(1, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta, act, rp, part, nullptr, nullptr);
   } else {
     bn_bwd_reduce_kernel<<<dim3((C + 255) / 256, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma,
                                                                   beta, act, rp, part);
   }
-  bn_bwd_final_kernel<<<(C + 63) / 64, 1024, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate, dy_amax);
+  bn_bwd_final_kernel<<<(C + 63) / 64, 1024, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate, dy_amax, BnBound{});
   if (vec) {
     bn_bwd_apply4_kernel<<<dim3(1, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta, act, training, sums,
                                                     1.f / (float)M, rp, dy, dy_colpart, dy_amax);
@@ -1040,6 +1218,38 @@ int bn_backward_rows(int M, int C) {
   bn_geometry(M, C, R, rp);
   return R;
 }
+
+bool bn_backward_frag_ok(int M, int C, const float* dout, const float* y) {
+  return C % 4 == 0 && C <= 1024 && aligned16(dout) && aligned16(y) && M > 0;
+}
+
+int bn_backward_frag(avc_context* ctx, int M, int C, const float* dout, const float* y, const float* mean,
+                     const float* invstd, const float* gamma, const float* beta, int act, int training,
+                     float* d_gamma, float* d_beta, int accumulate, _Float16* imgA, _Float16* imgT,
+                     unsigned* bound, hipStream_t s, float* dy_colpart) {
+  AVC_CHECK_ARG(bn_backward_frag_ok(M, C, dout, y), "bn_backward_frag: C must be a multiple of 4 (<= 1024), rows 16-B aligned");
+  int R, rp;
+  bn_geometry(M, C, R, rp);
+  Scratch sc(ctx);
+  AVC_TAKE(part, float, (size_t)R * 2 * C, sc);
+  AVC_TAKE(mpart, float, (size_t)R * 2 * C, sc);
+  AVC_TAKE(sums, float, (size_t)2 * C, sc);
+  bn_bwd_reduce4_kernel<<<dim3(1, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta, act, rp, part, mpart, bound);
+  BnBound bb;
+  bb.mpart = mpart; bb.gamma = gamma; bb.invstd = invstd; bb.inv_count = 1.f / (float)M;
+  bb.training = training; bb.bound = bound;
+  bn_bwd_final_kernel<<<(C + 63) / 64, 1024, 0, s>>>(R, C, part, sums, d_gamma, d_beta, accumulate, nullptr, bb);
+  const int nkcA = (C + 31) / 32 * 2, nkcT = (M + 31) / 32 * 2;
+  bn_bwd_apply_frag_kernel<<<dim3((C + 127) / 128, (M + 31) / 32), 256, 0, s>>>(
+      M, C, dout, y, mean, invstd, gamma, beta, act, training, sums, 1.f / (float)M, bound, imgA, nkcA, imgT, nkcT,
+      dy_colpart);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int bn_backward_frag_rows(int M) { return (M + 31) / 32; }
+
+size_t bn_backward_frag_scratch(int M, int C) { return bn_backward_scratch(M, C) + (size_t)bn_backward_rows(M, C) * 2 * C * sizeof(float) + 256; }
 
 int colsum_finish(int R, int N, const float* part, float* out, int accumulate, hipStream_t s) {
   colsum_final_kernel<<<(N + 63) / 64, 1024, 0, s>>>(R, N, part, out, accumulate, nullptr);

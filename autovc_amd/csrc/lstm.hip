@@ -721,7 +721,11 @@ void launch_lstm32(int nblk, int T, int B, long ldgx, long ldy, const L32Dir& d0
 // register ring refilled PF steps ahead (loop unrolled by PF: static slots; refills are
 // unconditional and clamped so no join waits on them), and the dG broadcast through LDS needs
 // no barrier: one wave's LDS operations complete in issue order (see lstm32_fwd_kernel).
-template <int PF>
+// FAST (round 4, avc_lstm32_tune(1), the default): the 64-term dot product as two packed-FMA
+// chains (v_pk_fma_f32, 16 instructions deep each, instead of one 64-deep scalar chain), and
+// tanh(c_t) in the forward FAST kernel's own form, so the derivative uses the very tanh(c) value
+// the forward multiplied by o_t (libm tanhf was also the longest piece of the step's chain).
+template <int PF, bool FAST = false>
 __global__ __launch_bounds__(64) void lstm32_bwd_kernel(int T, int B, int reverse,
                                                         const float* __restrict__ whh,
                                                         const float* __restrict__ gates,
@@ -772,17 +776,31 @@ __global__ __launch_bounds__(64) void lstm32_bwd_kernel(int T, int B, int revers
         const int t = reverse ? T - 1 - s : s;
         const long row = (long)t * B + b;
         float part = 0.f;
+        if constexpr (FAST) {
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          f2 q[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
-        for (int q4 = 0; q4 < 16; ++q4) {
-          const float4 g4 = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
-          part += wc[4 * q4] * g4.x + wc[4 * q4 + 1] * g4.y + wc[4 * q4 + 2] * g4.z + wc[4 * q4 + 3] * g4.w;
+          for (int q4 = 0; q4 < 16; ++q4) {
+            const float4 g4 = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
+            q[0] = __builtin_elementwise_fma(f2{wc[4 * q4], wc[4 * q4 + 1]}, f2{g4.x, g4.y}, q[0]);
+            q[1] = __builtin_elementwise_fma(f2{wc[4 * q4 + 2], wc[4 * q4 + 3]}, f2{g4.z, g4.w}, q[1]);
+          }
+          const f2 sq = q[0] + q[1];
+          part = sq.x + sq.y;
+        } else {
+#pragma unroll
+          for (int q4 = 0; q4 < 16; ++q4) {
+            const float4 g4 = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
+            part += wc[4 * q4] * g4.x + wc[4 * q4 + 1] * g4.y + wc[4 * q4 + 2] * g4.z + wc[4 * q4 + 3] * g4.w;
+          }
         }
         part += __shfl_xor(part, 32);
         float dzi = 0.f, dzf = 0.f, dzg = 0.f, dzo = 0.f;
         if (lane < 32) {
           const float dh = dyv + part;
           const float cp = s > 0 ? cpv : 0.f;
-          const float tc = tanhf(c);
+          // (FAST: lstm32_fwd_kernel<8, true>'s th(c))
+          const float tc = FAST ? 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * c)) - 1.f : tanhf(c);
           const float dct = dh * og * (1.f - tc * tc) + dc;
           dc = dct * fg;
           dzi = dct * gg * ig * (1.f - ig);
@@ -1169,7 +1187,8 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     colpart = cp;
   }
   if (small) {
-    lstm32_bwd_kernel<8><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
+    if (g_lstm32_mode == 0) lstm32_bwd_kernel<8, false><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
+    else lstm32_bwd_kernel<8, true><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
     AVC_LAUNCH_CHECK();
   } else if (gemm_bptt) {
     // W_hh^T permuted ([H][4H]: row j = hidden unit, k = permuted gate row), split once with the

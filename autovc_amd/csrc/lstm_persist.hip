@@ -71,7 +71,7 @@ namespace avc {
 
 int g_persist_mode = 2;  // avc_lstm_persist_tune(): 0 = never; 1 / 2 = when eligible (hand-off form)
 int g_persist_layers = 3;  // avc_lstm_persist_layers(): bit 0 = one-layer form, bit 1 = two-layer form
-int g_persist_pd = 2;    // avc_lstm_persist_depth(): h chunks in flight ahead of the MFMAs (1 or 2)
+int g_persist_pd = 2;    // avc_lstm_persist_depth(): h chunks in flight ahead of the MFMAs (1..4; 3 / 4: halves only)
 
 namespace {
 
@@ -1085,7 +1085,7 @@ size_t persist_lds(int H, int RT) {
 // tracks the bytes each consumer wave ingests (MI355X_MICROARCH.md, handoff-payload).  Measured:
 // C5 lstm1 (RT 1) 2930 -> 2862 us, C2 lstm1 (RT 1) unchanged, C3 lstm1 (RT 2) 542 -> 721 us.
 bool persist_gran(int H, int RT) {
-  return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd == 2 && !(g_persist_qwait & 2);
+  return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd >= 2 && !(g_persist_qwait & 2);
 }
 
 int g_persist_halves = 0;  // avc_lstm_persist_halves(): the two-layer form walks two batch halves
@@ -1095,7 +1095,7 @@ int g_persist_halves = 0;  // avc_lstm_persist_halves(): the two-layer form walk
 // tuning: 2 for the two-layer form in its default hand-off with at least two tiles, else 1.
 int persist_nh(int RT, bool two_layer) {
   return two_layer && RT >= 2 && g_persist_halves && (g_persist_qwait & 1) && g_persist_mode == 2 &&
-                 g_persist_pd == 2
+                 g_persist_pd >= 2
              ? 2
              : 1;
 }
@@ -1106,8 +1106,13 @@ const void* persist_fn(int H, int RT, bool two_layer = true) {
   const int nch = H / 32 / 4;
   if (!two_layer && persist_gran(H, RT)) return (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 1>;
   if (persist_nh(RT, two_layer) == 2) {  // RT / 2 tiles per half
-    if (nch == 8) return RT == 2 ? (const void*)lstm_persist_kernel<8, 1, 1, 2, 1, 0, 2>
+    // a half's h chunks are half as large, so depth 3 / 4 keeps the bytes in flight of depth 2
+    // at RT rows (avc_lstm_persist_depth; the RT = 1 halves already take every chunk at once)
+    if (nch == 8 && RT > 2)
+      return g_persist_pd == 4   ? (const void*)lstm_persist_kernel<8, 2, 1, 4, 1, 0, 2>
+             : g_persist_pd == 3 ? (const void*)lstm_persist_kernel<8, 2, 1, 3, 1, 0, 2>
                                  : (const void*)lstm_persist_kernel<8, 2, 1, 2, 1, 0, 2>;
+    if (nch == 8) return (const void*)lstm_persist_kernel<8, 1, 1, 2, 1, 0, 2>;
     return RT == 2 ? (const void*)lstm_persist_kernel<4, 1, 1, 2, 1, 0, 2>
                    : (const void*)lstm_persist_kernel<4, 2, 1, 2, 1, 0, 2>;
   }
@@ -2026,8 +2031,8 @@ extern "C" int avc_lstm_persist_tune(int mode) {
 }
 
 extern "C" int avc_lstm_persist_depth(int chunks) {
-  if (chunks < 1 || chunks > 2) {
-    avc::set_error("avc_lstm_persist_depth: chunks must be 1 or 2");
+  if (chunks < 1 || chunks > 4) {
+    avc::set_error("avc_lstm_persist_depth: chunks must be 1..4 (3 and 4 apply to the batch-halves form only)");
     return AVC_ERR_INVALID;
   }
   avc::g_persist_pd = chunks;

@@ -310,7 +310,8 @@ int avc_debug_bnf_inject(int launches);
  * Every path computes the same arithmetic in the same order (bit-identical outputs). */
 int avc_lstm_persist_tune(int mode);
 /* Tuning hook: split-h chunks the persistent recurrence keeps in flight ahead of the chunk being
- * multiplied (1 or 2 = default); same arithmetic either way. */
+ * multiplied (1 or 2 = default; 3 or 4 select deeper instances of the batch-halves form only,
+ * avc_lstm_persist_halves, whose chunks are half as large); same arithmetic either way. */
 int avc_lstm_persist_depth(int chunks);
 /* Tuning hook: the persistent recurrences' per-step waits.  Bit set = every wave waits for the
  * quarter of the producing slot whose h it multiplies (quarter counters, no workgroup barrier);
@@ -327,6 +328,12 @@ int avc_lstm_persist_granules(int on);
  * hand-off is in flight (counters per step and half); 0 (default, measured faster) = all rows at
  * once.  Same arithmetic either way (bit-identical). */
 int avc_lstm_persist_halves(int on);
+/* Tuning hook: 1 (default) = the backward of Conv1d + BatchNorm (avc_conv_bn_act_backward*) has its
+ * BatchNorm backward write dY already split for both products (the dgrad operand dY and the weight
+ * gradient's dY^T, fragment images scaled by a proven upper bound on max |dY|), instead of an fp32
+ * dY that a max scan and two split passes re-read; 0 = the fp32 dY path.  The products agree to the
+ * last bit except where an element lies 2^-27 below the operand's max. */
+int avc_bn_bwd_frag(int on);
 /* Tuning hook: which recurrences may take the persistent form (bit 0 = one layer, e.g. decoder
  * lstm1; bit 1 = two stacked layers, decoder lstm2; default 3 = both). */
 int avc_lstm_persist_layers(int mask);

@@ -71,6 +71,15 @@ for step in "$@"; do
     profvoc) run profvoc 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profvoc -o voc -- python3 bench.py --mode vocoder --steps 2 --warmup 1 --no-cpu --no-timing ;;
     profmel) run profmel 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profmel -o mel -- python3 bench.py --mode mel --steps 10 --warmup 2 --no-cpu --no-timing ;;
     profse) run profse 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/profse -o se -- python3 bench.py --mode se --steps 10 --warmup 2 --no-cpu --no-timing ;;
+    bnfab) run bnfab 300 python scripts/persist_hook_ab.py avc_bn_fuse 1 2 1 2 1 2 ;;
+    bnftrain) run bnftrain 400 python scripts/train_hook_ab.py avc_bn_fuse 1 2 ;;
+    ebudget) run ebudget 400 python scripts/error_budget.py 2 1 128 && run ebudget0 400 python scripts/error_budget.py 0 1 128 && run ebudget64 600 python scripts/error_budget.py 0 64 128 ;;
+    hpd) run hpd 400 python scripts/persist_cfg_ab.py "avc_lstm_persist_halves=0,avc_lstm_persist_depth=2" "avc_lstm_persist_halves=1,avc_lstm_persist_depth=2" "avc_lstm_persist_halves=1,avc_lstm_persist_depth=3" "avc_lstm_persist_halves=1,avc_lstm_persist_depth=4" ;;
+    rccl) run rccl 400 python -u -m pytest tests/test_gpu_rccl.py -x -v -s --timeout 600 -p no:cacheprovider ;;
+    pmcgran) for g in 0 1; do run pmcgranF$g 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcgranF$g -o fwd -- python3 scripts/fwd_hooks.py avc_lstm_persist_granules=$g 4 && run pmcgranW$g 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcgranW$g -o fwd -- python3 scripts/fwd_hooks.py avc_lstm_persist_granules=$g 4; done ;;
+    granab) run granab 300 python scripts/persist_cfg_ab.py "avc_lstm_persist_granules=1" "avc_lstm_persist_granules=0" ;;
+    bnbwd) run bnbwd 400 python -u -m pytest tests/test_gpu_bnbwd.py tests/test_gpu_kernels.py -x -v -s --timeout 200 -p no:cacheprovider ;;
+    bnbwdab) run bnbwdab 400 python scripts/train_hook_ab.py avc_bn_bwd_frag 0 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
