@@ -15,7 +15,7 @@
 
 namespace avc {
 
-int g_bnb_frag = 0;  // avc_bn_bwd_frag(): the BN backward writes dY already split
+int g_bnb_frag = 1;  // avc_bn_bwd_frag(): the BN backward writes dY already split
 
 namespace {
 

@@ -22,12 +22,30 @@ __device__ __forceinline__ float act_fwd(float a, int act) {
 }
 // derivative of act at pre-activation a
 __device__ __forceinline__ float act_bwd(float a, int act) {
+#pragma clang fp contract(off)
   if (act == AVC_ACT_RELU) return a > 0.f ? 1.f : 0.f;
   if (act == AVC_ACT_TANH) {
     const float t = tanhf(a);
     return 1.f - t * t;
   }
   return 1.f;
+}
+
+// The BatchNorm backward's per-element expressions, written once with contraction off so every
+// pass that forms them (reduce, apply, the split-writing apply of round 4) gets the same bits
+// whatever the compiler would fuse in each kernel:
+//   x^ = (y - mu) * is,  dA = dout * act'(x^ g + b),  dy = g is (dA - k1 - x^ k2)  (train) | g is dA
+__device__ __forceinline__ float bnb_xhat(float y, float mu, float is) {
+#pragma clang fp contract(off)
+  return (y - mu) * is;
+}
+__device__ __forceinline__ float bnb_da(float d, float xh, float g, float bt, int act) {
+#pragma clang fp contract(off)
+  return d * act_bwd(xh * g + bt, act);
+}
+__device__ __forceinline__ float bnb_dy(float dA, float xh, float g, float is, float k1, float k2, int training) {
+#pragma clang fp contract(off)
+  return training ? g * is * (dA - k1 - xh * k2) : g * is * dA;
 }
 
 // ---- column sums -------------------------------------------------------------------------
@@ -347,8 +365,8 @@ __global__ void bn_bwd_reduce_kernel(int M, int C, const float* __restrict__ dou
 #pragma unroll 4
   for (int m = m0; m < m1; ++m) {
     const long i = (long)m * C + c;
-    const float xh = (y[i] - mu) * is;
-    const float dA = dout[i] * act_bwd(xh * g + bt, act);
+    const float xh = bnb_xhat(y[i], mu, is);
+    const float dA = bnb_da(dout[i], xh, g, bt, act);
     s1 += dA;
     s2 += dA * xh;
   }
@@ -430,11 +448,10 @@ __global__ void bn_bwd_apply_kernel(long M, int C, const float* __restrict__ dou
        i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
     const float is = invstd[c], g = gamma[c];
-    const float xh = (y[i] - mean[c]) * is;
-    const float dA = dout[i] * act_bwd(xh * g + beta[c], act);
-    float v;
-    if (training) v = g * is * (dA - sums[c] * inv_count - xh * sums[C + c] * inv_count);
-    else v = g * is * dA;
+    const float xh = bnb_xhat(y[i], mean[c], is);
+    const float dA = bnb_da(dout[i], xh, g, beta[c], act);
+    const float v = bnb_dy(dA, xh, g, is, training ? sums[c] * inv_count : 0.f,
+                           training ? sums[C + c] * inv_count : 0.f, training);
     dy[i] = v;
   }
 }
@@ -462,9 +479,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_cols_kernel(int M, int C, co
 #pragma unroll 4
     for (int m = m0; m < m1; ++m) {
       const long i = (long)m * C + c;
-      const float xh = (y[i] - mu) * is;
-      const float dA = dout[i] * act_bwd(xh * g + bt, act);
-      const float v = training ? g * is * (dA - k1 - xh * k2) : g * is * dA;
+      const float xh = bnb_xhat(y[i], mu, is);
+      const float dA = bnb_da(dout[i], xh, g, bt, act);
+      const float v = bnb_dy(dA, xh, g, is, k1, k2, training);
       dy[i] = v;
       cs += v;
       mx = fmaxf(mx, fabsf(v));
@@ -522,8 +539,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(int M, int C, const
       const float yy[4] = {yv.x, yv.y, yv.z, yv.w}, dd[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float xh = (yy[e] - k.mu[e]) * k.is[e];
-        const float dA = dd[e] * act_bwd(xh * k.g[e] + k.bt[e], act);
+        const float xh = bnb_xhat(yy[e], k.mu[e], k.is[e]);
+        const float dA = bnb_da(dd[e], xh, k.g[e], k.bt[e], act);
         s1[e] += dA;
         s2[e] += dA * xh;
         mx1[e] = fmaxf(mx1[e], fabsf(dA));
@@ -593,9 +610,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(int M, int C, const 
       float o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float xh = (yy[e] - k.mu[e]) * k.is[e];
-        const float dA = dd[e] * act_bwd(xh * k.g[e] + k.bt[e], act);
-        o[e] = training ? k.g[e] * k.is[e] * (dA - k1[e] - xh * k2[e]) : k.g[e] * k.is[e] * dA;
+        const float xh = bnb_xhat(yy[e], k.mu[e], k.is[e]);
+        const float dA = bnb_da(dd[e], xh, k.g[e], k.bt[e], act);
+        o[e] = bnb_dy(dA, xh, k.g[e], k.is[e], k1[e], k2[e], training);
         cs[e] += o[e];
         mx = fmaxf(mx, fabsf(o[e]));
       }
@@ -686,9 +703,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_frag_kernel(int M, int C, co
         const float yy[4] = {yv.x, yv.y, yv.z, yv.w}, dd[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float xh = (yy[e] - k.mu[e]) * k.is[e];
-          const float dA = dd[e] * act_bwd(xh * k.g[e] + k.bt[e], act);
-          o[e] = training ? k.g[e] * k.is[e] * (dA - k1[e] - xh * k2[e]) : k.g[e] * k.is[e] * dA;
+          const float xh = bnb_xhat(yy[e], k.mu[e], k.is[e]);
+          const float dA = bnb_da(dd[e], xh, k.g[e], k.bt[e], act);
+          o[e] = bnb_dy(dA, xh, k.g[e], k.is[e], k1[e], k2[e], training);
           cs[e] += o[e];
         }
       }

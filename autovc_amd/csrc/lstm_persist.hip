@@ -188,7 +188,7 @@ int g_persist_diag = 0;
 // 1141 -> 1073 us at C2), bit 1 = one-layer form (lstm1: 384 -> 400 us at C2, so off)
 int g_persist_qwait = 1;
 // avc_lstm_persist_granules(): the one-layer form hands split h over as data-tagged granules
-int g_persist_gran = 1;
+int g_persist_gran = 0;  // (round 4: the counter form measured 20 us faster at C2, equal at C5)
 
 // Granule hand-off (GR, one-layer form, H = 512): split h_t goes out as 8-B granules
 // {f16 hi | f16 lo << 16, tag}, one per (batch row, hidden unit), each written by ONE sc1 store

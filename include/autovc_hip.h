@@ -318,9 +318,10 @@ int avc_lstm_persist_depth(int chunks);
  * clear = one polling lane per operand and a workgroup barrier.  Bit 0: two-layer form (lstm2),
  * bit 1: one-layer form (lstm1); default 1.  Same arithmetic either way (bit-identical). */
 int avc_lstm_persist_qwait(int mask);
-/* Tuning hook: 1 (default) = the one-layer persistent form at H = 512 (decoder lstm1) hands split
- * h from step to step as data-tagged 8-B granules (no counter, drain or barrier on the step's
- * critical path); 0 = the counter hand-off.  Applies when bit 1 of the qwait mask is clear and
+/* Tuning hook: 1 = the one-layer persistent form at H = 512 (decoder lstm1) hands split h from
+ * step to step as data-tagged 8-B granules (no counter, drain or barrier on the step's critical
+ * path); 0 (default since round 4: 20 us faster at C2, equal at C5, half the h bytes) = the counter
+ * hand-off.  Applies when bit 1 of the qwait mask is clear and
  * the default hand-off form and depth are set.  Same arithmetic either way (bit-identical). */
 int avc_lstm_persist_granules(int on);
 /* Tuning hook: 1 = the two-layer persistent form (decoder lstm2, batch > 16) walks its

@@ -80,6 +80,7 @@ for step in "$@"; do
     granab) run granab 300 python scripts/persist_cfg_ab.py "avc_lstm_persist_granules=1" "avc_lstm_persist_granules=0" ;;
     bnbwd) run bnbwd 400 python -u -m pytest tests/test_gpu_bnbwd.py tests/test_gpu_kernels.py -x -v -s --timeout 200 -p no:cacheprovider ;;
     bnbwdab) run bnbwdab 400 python scripts/train_hook_ab.py avc_bn_bwd_frag 0 1 ;;
+    prodcurve) run prodcurve 500 python -u -m pytest tests/test_gpu_production.py tests/test_gpu_curve.py -x -v -s --timeout 300 -p no:cacheprovider ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -18,7 +18,7 @@ from autovc_amd import _lib, ops
 
 pytestmark = pytest.mark.gpu
 
-DEFAULT = 0  # the library's default (avc_bn_bwd_frag)
+DEFAULT = 1  # the library's default (avc_bn_bwd_frag)
 CASES = [(16, 64, 336, 512, ops.ACT_RELU, True, False), (32, 40, 512, 512, ops.ACT_TANH, True, False),
          (16, 48, 512, 80, ops.ACT_NONE, True, True), (16, 64, 80, 512, ops.ACT_TANH, False, False)]
 

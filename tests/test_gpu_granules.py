@@ -44,30 +44,36 @@ def _run(ws, x, dy, T, B, save):
 def test_granules_match_counter_form(cuda_device, T, B, save):
     ws, x, dy = _layer(cuda_device, T, B)
     before = _giveups()
-    _lib.call("avc_lstm_persist_granules", 0)
+    _lib.call("avc_lstm_persist_granules", 0)  # (the library default since round 4)
+    ref = _run(ws, x, dy, T, B, save)
+    _lib.call("avc_lstm_persist_granules", 1)
     try:
-        ref = _run(ws, x, dy, T, B, save)
+        for _ in range(3):  # repeated launches on one counter region: epochs and ring tags advance
+            got = _run(ws, x, dy, T, B, save)
+            for a, b in zip(got, ref):
+                assert torch.equal(a, b)
+        torch.cuda.synchronize()
     finally:
-        _lib.call("avc_lstm_persist_granules", 1)
-    for _ in range(3):  # repeated launches on one counter region: epochs and ring tags advance
-        got = _run(ws, x, dy, T, B, save)
-        for a, b in zip(got, ref):
-            assert torch.equal(a, b)
-    torch.cuda.synchronize()
+        _lib.call("avc_lstm_persist_granules", 0)
     assert _giveups() == before
 
 
 def test_granule_give_up_is_nan_and_next_call_raises(cuda_device):
     T, B = 64, 32
     ws, x, dy = _layer(cuda_device, T, B)
-    ref = _run(ws, x, dy, T, B, False)[0]
-    torch.cuda.synchronize()
-    before = _giveups()
-    _lib.call("avc_debug_persist_inject", 1)
-    bad = ops.LSTMLayer.apply(x, *ws, T, B, False)
-    torch.cuda.synchronize()
-    assert _giveups() > before
-    assert torch.isnan(bad).any(), "timed-out launch returned numbers"
-    with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
-        ops.LSTMLayer.apply(x, *ws, T, B, False)
-    assert torch.equal(_run(ws, x, dy, T, B, False)[0], ref)
+    _lib.call("avc_lstm_persist_granules", 1)
+    try:
+        ref = _run(ws, x, dy, T, B, False)[0]
+        torch.cuda.synchronize()
+        before = _giveups()
+        _lib.call("avc_debug_persist_inject", 1)
+        bad = ops.LSTMLayer.apply(x, *ws, T, B, False)
+        torch.cuda.synchronize()
+        assert _giveups() > before
+        assert torch.isnan(bad).any(), "timed-out launch returned numbers"
+        with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+            ops.LSTMLayer.apply(x, *ws, T, B, False)
+        assert torch.equal(_run(ws, x, dy, T, B, False)[0], ref)
+    finally:
+        _lib.call("avc_debug_persist_inject", 0)
+        _lib.call("avc_lstm_persist_granules", 0)
