@@ -94,7 +94,7 @@ STAGES.append(("dec.linear", o_linear(sd64), o_linear(sd32), g_linear(dec.linear
 for i in range(5):
     p, act = f"postnet.convolutions.{i}", ("tanh" if i < 4 else None)
     STAGES.append((f"post.conv{i}", o_conv(sd64, p, act), o_conv(sd32, p, act), g_conv(post.convolutions[i], act)))
-MEL = 7    # index of the stage whose output is mel (the residual of the last one)
+MEL = 6    # index of the stage whose output is mel (dec.linear; the residual of the last one)
 LAST = len(STAGES) - 1
 
 
@@ -161,7 +161,7 @@ with torch.no_grad():
         def carried(y):  # the stage's own error carried to mel_post in float64
             if k == LAST:
                 return mx(y, post64)
-            return mx(chain(o64, y, k + 1, mel64 if k > MEL else None)[LAST], post64)
+            return mx(chain(o64, y, k + 1, mel64 if k > MEL else (y if k == MEL else None))[LAST], post64)
         rows.append({"stage": name, "local_gpu": mx(yg, ref[k]), "local_ref": mx(y3, ref[k]),
                      "post_gpu": carried(yg), "post_ref": carried(y3),
                      "chain_gpu": mx(g[k], ref[k]), "chain_ref": mx(r32[k], ref[k]), "max_abs": float(ref[k].abs().max())})
