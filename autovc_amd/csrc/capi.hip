@@ -89,7 +89,8 @@ struct GenBufs {
 size_t gen_scratch(int T, int B) {
   const size_t TB = (size_t)T * B, f = sizeof(float);
   size_t own = TB * (336 + 512 + 512 + 64 + 64 + 320 + 1024 + 1024 + 80 + 80) * f + 4 * 512 * f + 64 * 256 +
-               2 * gemm_afrag_bytes((long)TB, 512) + gemm_afrag_bytes((long)TB, 1024) + 1024;
+               2 * gemm_afrag_bytes((long)TB, 512) + gemm_afrag_bytes((long)TB, 1024) + gemm_afrag_bytes((long)TB, 336) +
+               2048 + 1024;  // (+ the frames' split image and their range-guard words)
   size_t nested = 0;
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 336, 512));
   nested = std::max(nested, conv_bn_forward_scratch(T, B, 512, 512));
@@ -133,6 +134,8 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   AVC_TAKE(fa, _Float16, gemm_afrag_bytes(TB, 512) / 2, sc);
   AVC_TAKE(fb, _Float16, gemm_afrag_bytes(TB, 512) / 2, sc);
   AVC_TAKE(fl, _Float16, gemm_afrag_bytes(TB, 1024) / 2, sc);  // lstm2's output split for the Linear
+  AVC_TAKE(fx, _Float16, gemm_afrag_bytes(TB, 336) / 2, sc);   // the frames as encoder conv 1's split operand
+  AVC_TAKE(xguard, unsigned, 64, sc);                           // and their range-guard words
   float* mean = stat;
   float* invstd = stat + 512;
   const float eps = 1e-5f, mom = 0.1f;
@@ -142,17 +145,25 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   // (its only reader is the next conv's GEMM); off when that GEMM would not stream fragments
   const bool chain = conv_frag_chain_ok(T, B, 512, 512) && conv_frag_chain_ok(T, B, 512, 80);
   auto cba = [&](int base, int cin, int cout, const float* in, float* out, int act,
-                 const float* residual, const _Float16* in_frag = nullptr, _Float16* out_frag = nullptr) {
+                 const float* residual, const _Float16* in_frag = nullptr, _Float16* out_frag = nullptr,
+                 const unsigned* in_guard = nullptr) {
     if (!chain) in_frag = nullptr, out_frag = nullptr;
     return conv_bn_act_forward_impl(ctx, T, B, cin, cout, in, P[base], P[base + 1], P[base + 2],
                                     P[base + 3], M(base + 4), M(base + 5), training, mom, eps, act,
                                     residual, out, out_frag ? nullptr : out, mean, invstd, s, in_frag,
-                                    out_frag);
+                                    out_frag, nullptr, nullptr, in_frag ? in_guard : nullptr);
   };
 
-  // Encoder (encoder.py:53-97)
-  AVC_TRY(frames_from_mel(T, B, 80, x, 256, c_org, x0, s));
-  AVC_TRY(cba(P_ENC_CONV + 0, 336, 512, x0, ba, AVC_ACT_RELU, nullptr, nullptr, fa));
+  // Encoder (encoder.py:53-97).  Round 4: the frames go straight into the first conv's split
+  // operand, scaled by the range guard of the mel and embedding themselves (frames_from_mel_frag;
+  // the same bits as frames -> guard scan -> split)
+  if (chain && g_handover && conv_frag_chain_ok(T, B, 336, 512)) {
+    AVC_TRY(frames_from_mel_frag(ctx, T, B, 80, x, 256, c_org, fx, xguard, s));
+    AVC_TRY(cba(P_ENC_CONV + 0, 336, 512, x0, ba, AVC_ACT_RELU, nullptr, fx, fa, xguard + 1));
+  } else {
+    AVC_TRY(frames_from_mel(T, B, 80, x, 256, c_org, x0, s));
+    AVC_TRY(cba(P_ENC_CONV + 0, 336, 512, x0, ba, AVC_ACT_RELU, nullptr, nullptr, fa));
+  }
   AVC_TRY(cba(P_ENC_CONV + 6, 512, 512, ba, bb, AVC_ACT_RELU, nullptr, fa, fb));
   // the third conv hands its output to the BiLSTM's input projection as a split image only
   const bool to_bilstm = chain && g_handover && bilstm_takes_frag(T, B, 512);

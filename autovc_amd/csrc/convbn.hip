@@ -76,7 +76,8 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
                              int training, float momentum, float eps, int act,
                              const float* residual, float* y_pre, float* out, float* mean,
                              float* invstd, hipStream_t s, const _Float16* x_frag,
-                             _Float16* out_frag, const unsigned* x_amax, unsigned* out_amax) {
+                             _Float16* out_frag, const unsigned* x_amax, unsigned* out_amax,
+                             const unsigned* x_frag_guard) {
   // x_frag: x already split (the previous layer's bn_apply wrote it); out_frag: also emit the
   // output split for the next layer (out may then be NULL: the fp32 output is not stored).
   // x_amax: x's max words from its producer (see bn_apply's amax_out): the range scan of x is
@@ -95,6 +96,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   }
   GemmDesc g = conv_fwd_desc(T, B, cin, cout, x, wt, bias, y_pre);
   g.a_frag = x_frag;
+  g.a_frag_guard = x_frag ? x_frag_guard : nullptr;  // x_frag split with that guard's scale (frames_frag)
   if (x_amax) g.a_guard = x_amax + 1;
   if (!out && !out_frag) out_amax = nullptr;
   if (ctx->prep_version >= 0) {  // cache the split-f16 copy of the taps as well

@@ -40,6 +40,11 @@ size_t bn_backward_frag_scratch(int M, int C);
 int colsum_finish(int R, int N, const float* part, float* out, int accumulate, hipStream_t s);
 int frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* emb, float* out,
                     hipStream_t s);
+// frames_from_mel written directly as the first conv's split operand (gemm_afrag_bytes(T*B, cm+ce)),
+// scaled by the range guard of x / emb it takes first: guard[0..1] = {max, max(max, 2^14)} (two
+// device words; GemmDesc::a_frag_guard = guard + 1); the fp32 frames are not stored
+int frames_from_mel_frag(avc_context* ctx, int T, int B, int cm, const float* x, int ce, const float* emb,
+                         _Float16* frag, unsigned* guard, hipStream_t s);
 int frames_from_mel_backward(int T, int B, int cm, int ce, const float* df, int ld, float* dx,
                              float* demb, int accumulate, hipStream_t s);
 int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream_t s,

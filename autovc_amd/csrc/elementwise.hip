@@ -785,6 +785,82 @@ __global__ void frames_from_mel_kernel(int T, int B, int cm, const float* __rest
   }
 }
 
+// frames_from_mel straight into the first encoder conv's split operand (round 4):
+// frames_guard_kernel takes the range guard of the input itself (max |x| over the mel and the
+// embedding: a quarter of the frames' bytes) into w[0] = max, w[1] = max(max, 2^14) (pre-zeroed);
+// frames_frag_kernel then writes the [T*B][cm+ce] frames directly as the fragment image
+// split_frag32_kernel would make of them with that guard's scale (GemmDesc::a_frag_guard): the
+// frames' fp32 store, their range scan and the split pass are gone, and the bits are the same.
+__global__ __launch_bounds__(256) void frames_guard_kernel(const float* __restrict__ x, long nx,
+                                                           const float* __restrict__ emb, long ne,
+                                                           float* __restrict__ partial, unsigned* __restrict__ ticket,
+                                                           unsigned* __restrict__ w) {
+  // (guard_scan_kernel's one-launch form over two sources: every block writes its maximum to
+  // partial[blockIdx]; the last block to take a ticket writes the words -- no zeroing launch)
+  __shared__ float red[4];
+  __shared__ bool last;
+  float m = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nx + ne; i += (long)gridDim.x * 256)
+    m = fmaxf(m, fabsf(i < nx ? x[i] : emb[i - nx]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(partial + blockIdx.x, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    last = atomicInc(ticket, gridDim.x - 1) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  float v = 0.f;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += 256)
+    v = fmaxf(v, __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    v = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    w[0] = __float_as_uint(v);
+    w[1] = __float_as_uint(fmaxf(v, 16384.f));
+  }
+}
+
+__global__ __launch_bounds__(256) void frames_frag_kernel(int T, int B, int cm, const float* __restrict__ x, int ce,
+                                                          const float* __restrict__ emb, int nkc, long ntile,
+                                                          const unsigned* __restrict__ guard,
+                                                          _Float16* __restrict__ frag) {
+  const int C = cm + ce, G8 = nkc * 2;
+  const float sc = pow2_of_bound(guard);  // split_scale_of: 1 below 2^15
+  const long total = ntile * 32 * G8, M = (long)T * B;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    // item -> (row r, 8-channel group g8), rows fastest within a tile: a wave writes 64 lanes of
+    // one fragment block pair
+    const long tile = idx / (32L * G8);
+    const int rem = (int)(idx - tile * 32L * G8), g8 = rem >> 5, rr = rem & 31;
+    const long r = tile * 32 + rr;
+    float v[8];
+    if (r < M) {
+      const int t = (int)(r / B), b = (int)(r - (long)t * B);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 8 * g8 + e;
+        v[e] = (c < cm ? x[((long)b * cm + c) * T + t] : c < C ? emb[(long)b * ce + (c - cm)] : 0.f) * sc;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+    }
+    h16x8 hi, lo;
+    bwd_split8(v, hi, lo);
+    const long blk = (tile * nkc + (g8 >> 1)) * 2;
+    const int lane = rr + 32 * (g8 & 1);
+    *reinterpret_cast<h16x8*>(frag + blk * 512 + lane * 8) = hi;
+    *reinterpret_cast<h16x8*>(frag + (blk + 1) * 512 + lane * 8) = lo;
+  }
+}
+
 // d_x[b][c][t] (+)= d_frames[(t*B+b)*ld + c]
 __global__ void mel_grad_kernel(int T, int B, int cm, const float* __restrict__ df, int ld,
                                 float* __restrict__ dx, int accumulate) {
@@ -1277,6 +1353,32 @@ int colsum_finish(int R, int N, const float* part, float* out, int accumulate, h
 int frames_from_mel(int T, int B, int cm, const float* x, int ce, const float* emb, float* out,
                     hipStream_t s) {
   frames_from_mel_kernel<<<ew_blocks((long)T * B * (cm + ce)), 256, 0, s>>>(T, B, cm, x, ce, emb, out);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
+int frames_from_mel_frag(avc_context* ctx, int T, int B, int cm, const float* x, int ce, const float* emb,
+                         _Float16* frag, unsigned* guard, hipStream_t s) {
+  if (!ctx->guard_ticket) {  // (as guard_scan: the first use happens eagerly, before any capture)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    AVC_HIP(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone) {
+      set_error("frames range guard: ticket not allocated before graph capture");
+      return AVC_ERR_WORKSPACE;
+    }
+    AVC_HIP(hipMalloc(&ctx->guard_ticket, 256));
+    AVC_HIP(hipMemsetAsync(ctx->guard_ticket, 0, 256, s));
+    AVC_HIP(hipStreamSynchronize(s));
+  }
+  Scratch sc(ctx);
+  AVC_TAKE(part, float, 256, sc);
+  const long nx = (long)B * cm * T, ne = (long)B * ce;
+  frames_guard_kernel<<<(int)std::max<long>(1, std::min<long>((nx + ne + 1023) / 1024, 256)), 256, 0, s>>>(
+      x, nx, emb, ne, part, ctx->guard_ticket, guard);
+  const int nkc = (cm + ce + 31) / 32 * 2;
+  const long ntile = ((long)T * B + 31) / 32, total = ntile * 32 * nkc * 2;
+  frames_frag_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(T, B, cm, x, ce, emb, nkc, ntile,
+                                                                                   guard + 1, frag);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

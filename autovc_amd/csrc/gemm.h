@@ -71,6 +71,8 @@ struct GemmDesc {
                                    // scratch; a_trans: gemm_afrag_bytes(M, Kc) bytes) ...
   int a_frag_scaled = 0;    // ... and a later product with the same A and amax_a passes it back as
                             // a_frag with a_frag_scaled = 1 (gradient products sharing dY^T / dG^T)
+  const unsigned* a_frag_guard = nullptr;  // forward products: a_frag was split scaled by the power of
+                                           // two of this range-guard word (max(|A|, 2^14); frames_frag)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
   int stats_bm = 0;         // filled by gemm_run: rows per stats partial
   BnFuse bnf;               // fused BatchNorm epilogue (bnf.on; set up by gemm_bnf_ok's caller)

@@ -1918,7 +1918,9 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     float* part = sc.take<float>(kGuardBlocks);
     if (!gw || !part) return AVC_ERR_WORKSPACE;
     d.amax_a = nullptr;
-    if (d.a_guard && !d.a_frag) {
+    if (d.a_frag && d.a_frag_guard) {
+      d.amax_a = d.a_frag_guard;  // the image's own scale (its producer range-checked A)
+    } else if (d.a_guard && !d.a_frag) {
       d.amax_a = d.a_guard;
     } else if (!d.a_frag && !(d.a_bound > 0.f && d.a_bound < 32768.f) && !range_checked(ctx, d.A)) {
       AVC_TRY(guard_scan(ctx, d.A, d.a_rows, d.Kc, d.lda, part, gw, stream));

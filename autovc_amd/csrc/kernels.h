@@ -98,7 +98,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
                              const float* residual, float* y_pre, float* out, float* mean,
                              float* invstd, hipStream_t s, const _Float16* x_frag = nullptr,
                              _Float16* out_frag = nullptr, const unsigned* x_amax = nullptr,
-                             unsigned* out_amax = nullptr);
+                             unsigned* out_amax = nullptr, const unsigned* x_frag_guard = nullptr);
 size_t conv_bn_forward_scratch(int T, int B, int cin, int cout);
 // true when a conv with cin input channels takes its input as split fragments (x_frag honoured)
 bool conv_frag_chain_ok(int T, int B, int cin, int cout);
