@@ -1355,9 +1355,17 @@ struct BpttPArgs {
 // a buffer written at step k is rewritten at step k + 2 only, and the counter chain in between
 // (B(k+1) waits on every K-slice of a tile, A(k+2) on B(k+1)) orders every reader of step k
 // before that.
-template <int NCH, int NS, int RB>  // RB: batch rows per phase-B workgroup (16 or 32)
+// BGF (round 4, avc_bptt_coalesce(1), the default): phase B's threads take the unit group as the
+// fast index (tid = row * U/4 + group) instead of the row, so one wave instruction of the partial
+// reads covers 64 / (U/4) rows x U*4 contiguous bytes -- whole 128-B lines -- where row-fastest
+// lanes put every 16-B piece on a line of its own (4 KB apart) and each sc1 load fetched half a
+// line.  The split dG for the next step, whose fragment layout is row-fastest, is then staged in
+// LDS and stored as whole 256-B / 1-KB runs, and the bias column sums are combined over the rows
+// through LDS once after the last step (a fixed row order).
+template <int NCH, int NS, int RB, bool BGF = false>  // RB: batch rows per phase-B workgroup (16 or 32)
 __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   constexpr int U = 4 * NCH;
+  constexpr int UG = U / 4;                  // 4-unit groups of a phase-B workgroup's slice
   constexpr int KS = 16 * NCH;               // gate columns per K-slice
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_b[];
   unsigned char* wl = lds_b;                 // [4 col tiles][NCH][hi, lo] 1 KiB blocks
@@ -1397,8 +1405,8 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   const unsigned E = (unsigned)flag[2];
   const float sw_inv = 1.f / pow2_scale(__uint_as_float(*a.amax_w));
   // phase B thread task: row r (of RB), unit group g4 (4 units = one 16-deep k chunk of the slice)
-  const int br = tid & (RB - 1), bg = tid / RB;
-  const bool b_task = has_b && bg < U / 4;
+  const int br = BGF ? tid / UG : tid & (RB - 1), bg = BGF ? tid % UG : tid / RB;
+  const bool b_task = has_b && (BGF ? br < RB : bg < UG);
   const int b_row = rb * RB + br;
   const int fr = b_row & 31;      // the row's lane in its 32-row fragment block
   const int j0 = q * U + bg * 4;           // first hidden unit of the task
@@ -1408,6 +1416,8 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   // the narrower-slice instances are at the VGPR limit) and its max |dG|
   constexpr bool CS_LDS = NCH < 16;
   float* csl = reinterpret_cast<float*>(flag + 4);  // [16][512] when CS_LDS
+  // BGF: the split dG staging, [UG chunks][hi, lo][2 RB slots][16 B] (slot = k-half * RB + row)
+  unsigned char* stg = reinterpret_cast<unsigned char*>(csl) + (CS_LDS ? 16 * 512 * 4 : 0);
   float csum[CS_LDS ? 1 : 16], dmax = 0.f;
   if constexpr (CS_LDS) {  // [512 threads][16] as 4 x 16-B vectors per thread
 #pragma unroll
@@ -1587,16 +1597,38 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
             hi0[e] = h0; lo0[e] = (_Float16)((v0 - (float)h0) * 2048.0f);
             hi1[e] = h1; lo1[e] = (_Float16)((v1 - (float)h1) * 2048.0f);
           }
+          if constexpr (BGF) {  // into the staging image; stored below as whole runs
+            unsigned char* sp = stg + (long)bg * 2 * (2 * RB) * 16;
+            *reinterpret_cast<h8*>(sp + (0 * RB + br) * 16) = hi0;
+            *reinterpret_cast<h8*>(sp + (1 * RB + br) * 16) = hi1;
+            *reinterpret_cast<h8*>(sp + (2 * RB + br) * 16) = lo0;
+            *reinterpret_cast<h8*>(sp + (3 * RB + br) * 16) = lo1;
+          } else {
           const auto drs = __builtin_amdgcn_make_buffer_rsrc(
               a.dgs + (k & 1) * dgs_buf + ((long)(b_row >> 5) * nkc + kq / 16) * 1024, 0, 2048, 0x00020000);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi0), drs, fr * 16, 0, 16);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi1), drs, (fr + 32) * 16, 0, 16);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo0), drs, 1024 + fr * 16, 0, 16);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo1), drs, 1024 + (fr + 32) * 16, 0, 16);
+          }
           if (bg == 0) {
             const auto rrs = __builtin_amdgcn_make_buffer_rsrc(a.rowscale + ((long)(k & 1) * nsplit + q) * B + rb * RB, 0,
                                                                RB * 4, 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, sb), rrs, br * 4, 0, 16);
+          }
+        }
+        if constexpr (BGF) {
+          // the staged split dG as whole runs: piece p -> (chunk, hi/lo, slot); slot s = half * RB + r
+          // lands at fragment lane half * 32 + ((rb * RB) & 31) + r of block (row block, chunk)
+          __syncthreads();
+          constexpr int PIECES = UG * 2 * 2 * RB;
+          for (int p = tid; p < PIECES; p += 512) {
+            const int sl = p % (2 * RB), hl = (p / (2 * RB)) & 1, c = p / (4 * RB);
+            const int lane_g = (sl / RB) * 32 + ((rb * RB) & 31) + sl % RB;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(stg + (long)p * 16);
+            const auto drs = __builtin_amdgcn_make_buffer_rsrc(
+                a.dgs + (k & 1) * dgs_buf + ((long)((rb * RB) >> 5) * nkc + q * NCH + c) * 1024, 0, 2048, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(v, drs, hl * 1024 + lane_g * 16, 0, 16);
           }
         }
         if (!(a.diag & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1609,6 +1641,26 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   // the bias gradients' column sums (32 rows of this block: lanes 0-31 / 32-63 of a wave are the
   // rows of two unit groups) and max |dG| for the weight-gradient products' operand scale
   if (ok && has_b) {
+    if constexpr (BGF) {
+      // rows are spread over waves: every task's 16 sums into LDS (the W slice is free now), then
+      // thread (group, e) adds its column over the RB rows in row order
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(wl);  // [512][16]
+      if (b_task) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          if constexpr (CS_LDS) red[tid * 16 + e] = csl[tid * 16 + e];
+          else red[tid * 16 + e] = csum[e];
+        }
+      }
+      __syncthreads();
+      if (tid < UG * 16) {
+        const int g = tid / 16, e = tid % 16;
+        float v = 0.f;
+        for (int r = 0; r < RB; ++r) v += red[(r * UG + g) * 16 + e];
+        a.colpart[(long)rb * G4 + q * KS + g * 16 + e] = v;
+      }
+    } else {
     float cs[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -1621,6 +1673,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<f32x4*>(cp + 4 * g) = f32x4{cs[4 * g], cs[4 * g + 1], cs[4 * g + 2], cs[4 * g + 3]};
+    }
     }
     for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o));
     if (lane == 0) atomicMax(a.amax_dg, __float_as_uint(dmax));
@@ -1636,13 +1689,22 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
   }
 }
 
-size_t bptt_lds(int nch) { return (size_t)4 * nch * 2048 + 32 * 4 + 16 + (nch < 16 ? 16 * 512 * 4 : 0); }
+// (+ the BGF staging of the split dG: UG x 2 x 2 RB x 16 B = 16 KB at every instance)
+size_t bptt_lds(int nch) { return (size_t)4 * nch * 2048 + 32 * 4 + 16 + (nch < 16 ? 16 * 512 * 4 : 0) + 16 * 1024; }
+
+int g_bptt_bgf = 0;  // avc_bptt_coalesce(): phase B unit-group-fastest (coalesced partial reads)
 
 // epilogue rows per workgroup: 16 where 32-row blocks would leave half the workgroups without an
 // epilogue (nsplit = 16), else 32
 int bptt_rb(int ns) { return ns == 16 ? 16 : 32; }
 
 const void* bptt_fn(int nch, int ns) {
+  if (g_bptt_bgf) {
+    if (nch == 16 && ns == 16) return (const void*)bptt_persist_kernel<16, 16, 16, true>;
+    if (nch == 8 && ns == 32) return (const void*)bptt_persist_kernel<8, 32, 32, true>;
+    if (nch == 4 && ns == 32) return (const void*)bptt_persist_kernel<4, 32, 32, true>;
+    return nullptr;
+  }
   if (nch == 16 && ns == 16) return (const void*)bptt_persist_kernel<16, 16, 16>;
   if (nch == 8 && ns == 32) return (const void*)bptt_persist_kernel<8, 32, 32>;
   if (nch == 4 && ns == 32) return (const void*)bptt_persist_kernel<4, 32, 32>;
@@ -2221,5 +2283,15 @@ extern "C" int avc_lstm_persist_status(long* giveups) {
   AVC_HIP(hipDeviceSynchronize());
   AVC_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(avc::g_persist_giveups), sizeof(unsigned), 0, hipMemcpyDeviceToHost));
   *giveups = (long)v;
+  return AVC_OK;
+}
+
+extern "C" int avc_bptt_coalesce(int on) {
+  if (on < 0 || on > 1) {
+    avc::set_error("avc_bptt_coalesce: on must be 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_bptt_bgf = on;
+  ++avc::g_config_epoch;
   return AVC_OK;
 }

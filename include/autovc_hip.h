@@ -335,6 +335,11 @@ int avc_lstm_persist_halves(int on);
  * dY that a max scan and two split passes re-read; 0 = the fp32 dY path.  The products agree to the
  * last bit except where an element lies 2^-27 below the operand's max. */
 int avc_bn_bwd_frag(int on);
+/* Tuning hook: 1 (default) = the persistent BPTT's epilogue phase maps its threads unit-group-fast,
+ * so its reads of the split-K partials are whole cache lines, and stages the split dG it writes for
+ * the next step in LDS (whole-run stores); 0 = the round-3 row-fast mapping.  Same dG, dc and split
+ * dG bits; the bias gradients' column sums are combined in a different (fixed) order. */
+int avc_bptt_coalesce(int on);
 /* Tuning hook: which recurrences may take the persistent form (bit 0 = one layer, e.g. decoder
  * lstm1; bit 1 = two stacked layers, decoder lstm2; default 3 = both). */
 int avc_lstm_persist_layers(int mask);
