@@ -108,6 +108,9 @@ _SIGS = {
     "avc_speaker_encoder_forward": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _P],
     "avc_embedding_mean_normalize": [_I, _I, _P, _P, _P],
     "avc_wavernn_param_count": [_I],
+    "avc_wavernn_persist": [_I],
+    "avc_wavernn_persist_eligible": [_I, _I, _I],
+    "avc_debug_wavernn_inject": [_I],
     "avc_wavernn_upsample": [_P, _P, _I, _P, _P, _P, _P, _P],
     "avc_wavernn_generate": [_P, _P, _I, _P, _P, _I, _I, _I, _I, ctypes.c_ulonglong, _P, _P, _P, _P, _P],
     "avc_wavernn_fold_shape": [ctypes.c_long, _I, _I, _I, ctypes.POINTER(ctypes.c_long),

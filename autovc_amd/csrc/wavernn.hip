@@ -202,7 +202,7 @@ __device__ __forceinline__ void stage_load(const WrStep& a, int which, int i, in
           const float4 pi = *reinterpret_cast<const float4*>(a.pI + ((long)src * (a.Ltot + 1) + q) * H + k);
           const float4 w0 = *reinterpret_cast<const float4*>(a.wi0 + k);
           const float xp = xprev_at(a, r, i);
-          x = make_float4(pi.x + w0.x * xp, pi.y + w0.y * xp, pi.z + w0.z * xp, pi.w + w0.w * xp);
+          x = make_float4(fmaf(w0.x, xp, pi.x), fmaf(w0.y, xp, pi.y), fmaf(w0.z, xp, pi.z), fmaf(w0.w, xp, pi.w));
           break;
         }
         case IN_H1: p = a.h1 + ((long)cur * a.R + r) * H + k; break;
@@ -289,6 +289,19 @@ __device__ __forceinline__ void reduce_lanes(const float (&acc)[NG][kRC], int w,
   __syncthreads();
 }
 
+// torch's GRUCell epilogue for one (unit, row) from the summed gate products (gi / gh without
+// biases): the new h; shared by the per-step kernel and the persistent loop (contraction off, so
+// both form the same bits)
+__device__ __forceinline__ float gru_cell(const float* gi, const float* gh, const float (&ebi)[3], const float (&ebh)[3],
+                                          float ehp) {
+#pragma clang fp contract(off)
+  const float gi_r = gi[0] + ebi[0], gi_z = gi[kRC] + ebi[1], gi_n = gi[2 * kRC] + ebi[2];
+  const float gh_r = gh[0] + ebh[0], gh_z = gh[kRC] + ebh[1], gh_n = gh[2 * kRC] + ebh[2];
+  const float rg = sigmoidf_(gh_r + gi_r), zg = sigmoidf_(gh_z + gi_z);
+  const float ng = tanhf(gi_n + gh_n * rg);
+  return (ehp - ng) * zg + ng;
+}
+
 // GRU layer WHICH (1: rnn1 on xI; 2: rnn2 on [t1, a2]) for two hidden units per workgroup.
 // Waves 0/1: the input gates (r, z, n rows) of units u0 / u0+1, waves 2/3: their hidden gates.
 // torch's GRU cell order (aten RNN.cpp GRUCell): r = σ(gh_r + gi_r), z = σ(gh_z + gi_z),
@@ -336,7 +349,7 @@ __global__ __launch_bounds__(256) void wr_gru_kernel(WrStep a) {
         int src;
         long q;
         fold_pos(a, r0, i, src, q);
-        ex = a.pI[((long)src * (a.Ltot + 1) + q) * H + un] + a.wi0[un] * xprev_at(a, r0, i);
+        ex = fmaf(a.wi0[un], xprev_at(a, r0, i), a.pI[((long)src * (a.Ltot + 1) + q) * H + un]);
       } else {
         ex = a.t1[(long)r0 * H + un];
       }
@@ -356,11 +369,7 @@ __global__ __launch_bounds__(256) void wr_gru_kernel(WrStep a) {
     if (ep) {
       const float* gi = sums + (uu * 3) * kRC + rr0;        // wave uu: input gates
       const float* gh = sums + ((2 + uu) * 3) * kRC + rr0;  // wave 2 + uu: hidden gates
-      const float gi_r = gi[0] + ebi[0], gi_z = gi[kRC] + ebi[1], gi_n = gi[2 * kRC] + ebi[2];
-      const float gh_r = gh[0] + ebh[0], gh_z = gh[kRC] + ebh[1], gh_n = gh[2 * kRC] + ebh[2];
-      const float rg = sigmoidf_(gh_r + gi_r), zg = sigmoidf_(gh_z + gi_z);
-      const float ng = tanhf(gi_n + gh_n * rg);
-      const float hn = (ehp - ng) * zg + ng;
+      const float hn = gru_cell(gi, gh, ebi, ebh, ehp);
       hb[((long)(cur ^ 1) * R + r0) * H + un] = hn;
       // x = I(...) + h1 (model.py:269) after rnn1, x + h2 (model.py:273) after rnn2
       (WHICH == 1 ? a.t1 : a.t2)[(long)r0 * H + un] = ex + hn;
@@ -422,6 +431,46 @@ __device__ __forceinline__ float uniform_draw(unsigned long long seed, int r, in
   return __fadd_rn(1e-5f, __fmul_rn(0.99998f, u));
 }
 
+// the sample of fold row r at step i from its logits lg (model.py:279-315, distribution.py:87-123);
+// teacher-forced calls store the logits and return the given sample.  Shared by the per-step
+// kernel and the persistent loop (contraction off).
+__device__ __forceinline__ float wr_sample(const WrStep& a, int r, int i, const float* lg) {
+#pragma clang fp contract(off)
+  const int NC = a.NC;
+  const long o = (long)r * a.L + i;
+  float x;
+  if (a.teacher) {
+    for (int c = 0; c < NC; ++c) a.logits[o * NC + c] = lg[c];
+    x = a.x_tf[o];  // (unused by the next step, which reads x_tf itself)
+  } else if (a.mol) {
+    const int nr = NC / 3;
+    int best = 0;
+    float bv = 0.f;
+    for (int k = 0; k < nr; ++k) {  // Gumbel-max mixture choice; first maximum wins (torch.max)
+      const float u = uniform_draw(a.seed, r, i, k);
+      const float t = lg[k] - logf(-logf(u));
+      if (k == 0 || t > bv) { bv = t; best = k; }
+    }
+    const float mean = lg[nr + best];
+    const float ls = fmaxf(lg[2 * nr + best], -32.236191301916641f);  // log(1e-14)
+    const float u = uniform_draw(a.seed, r, i, nr);
+    x = mean + expf(ls) * (logf(u) - logf(1.0f - u));
+    x = fminf(fmaxf(x, -1.f), 1.f);
+  } else {  // RAW: Categorical(softmax) by inverse CDF, 2k / (n_classes - 1) - 1
+    float mx = lg[0];
+    for (int c = 1; c < NC; ++c) mx = fmaxf(mx, lg[c]);
+    float sum = 0.f;  // (each exp is formed twice, the same bits both times: no indexed array)
+    for (int c = 0; c < NC; ++c) sum += expf(lg[c] - mx);
+    const float u = uniform_draw(a.seed, r, i, 0);
+    float cdf = 0.f;
+    int k = 0;
+    for (int c = 0; c < NC; ++c) { cdf += expf(lg[c] - mx) / sum; if (cdf < u) k = c + 1; }
+    k = min(k, NC - 1);
+    x = 2.f * (float)k / ((float)NC - 1.f) - 1.f;
+  }
+  return x;
+}
+
 // fc3 + sampling (model.py:279-315; distribution.py:87-123), one workgroup per fold row; the last
 // workgroup to finish advances the step counter for the next launch.
 __global__ __launch_bounds__(256) void wr_out_kernel(WrStep a) {
@@ -466,36 +515,7 @@ __global__ __launch_bounds__(256) void wr_out_kernel(WrStep a) {
   __syncthreads();
   if (tid == 0) {
     const long o = (long)r * a.L + i;
-    float x;
-    if (a.teacher) {
-      for (int c = 0; c < NC; ++c) a.logits[o * NC + c] = lg[c];
-      x = a.x_tf[o];  // (unused by the next step, which reads x_tf itself)
-    } else if (a.mol) {
-      const int nr = NC / 3;
-      int best = 0;
-      float bv = 0.f;
-      for (int k = 0; k < nr; ++k) {  // Gumbel-max mixture choice; first maximum wins (torch.max)
-        const float u = uniform_draw(a.seed, r, i, k);
-        const float t = lg[k] - logf(-logf(u));
-        if (k == 0 || t > bv) { bv = t; best = k; }
-      }
-      const float mean = lg[nr + best];
-      const float ls = fmaxf(lg[2 * nr + best], -32.236191301916641f);  // log(1e-14)
-      const float u = uniform_draw(a.seed, r, i, nr);
-      x = mean + expf(ls) * (logf(u) - logf(1.0f - u));
-      x = fminf(fmaxf(x, -1.f), 1.f);
-    } else {  // RAW: Categorical(softmax) by inverse CDF, 2k / (n_classes - 1) - 1
-      float mx = lg[0];
-      for (int c = 1; c < NC; ++c) mx = fmaxf(mx, lg[c]);
-      float e[64], sum = 0.f;
-      for (int c = 0; c < NC; ++c) { e[c] = expf(lg[c] - mx); sum += e[c]; }
-      const float u = uniform_draw(a.seed, r, i, 0);
-      float cdf = 0.f;
-      int k = 0;
-      for (int c = 0; c < NC; ++c) { cdf += e[c] / sum; if (cdf < u) k = c + 1; }
-      k = min(k, NC - 1);
-      x = 2.f * (float)k / ((float)NC - 1.f) - 1.f;
-    }
+    const float x = wr_sample(a, r, i, lg);
     a.out[o] = x;
     a.x_prev[r] = x;
     if (atomicAdd(a.done, 1) == a.R - 1) {  // every workgroup has read this step: advance it
@@ -504,7 +524,6 @@ __global__ __launch_bounds__(256) void wr_out_kernel(WrStep a) {
     }
   }
 }
-
 __global__ void wr_column_kernel(int n, long ld, const float* __restrict__ W, float* __restrict__ col) {
   for (int k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) col[k] = W[(long)k * ld];
 }
@@ -520,6 +539,521 @@ __global__ void wr_init_state_kernel(int R, int H, int Fc, int* step, int* done,
     *step = 0;
     *done = 0;
   }
+}
+
+// ---- the persistent sample loop (avc_wavernn_persist) ---------------------------------------
+//
+// All L steps in ONE launch of G = H / 2 workgroups (one per CU; every one resident, checked on
+// the host) instead of five launches per step.  Workgroup w does what blockIdx w does in the
+// per-step kernels, with the same arithmetic, so the two paths agree bit for bit:
+//   every w:              GRU1 and GRU2 for hidden units 2w, 2w + 1;
+//   w < nfc:              fc1 rows [8w, 8w + 8)                  (role FC1)
+//   nfc <= w < 2 nfc:     fc2 rows [8(w - nfc), 8(w - nfc) + 8)  (role FC2)
+//   2 nfc <= w < 2nfc+R:  fc3 + sampling of fold row w - 2 nfc  (role OUT)
+// A GRU's hidden-gate products W_hh h_{i-1} do not depend on the sample just drawn: they are
+// formed early (the 'hid' phase: step i+1's sums, kept in LDS) while fc1 / fc2 / fc3 of step i
+// run, each role placing them where it waits anyway.  The chain of a step is then GRU1's input
+// gates -> GRU2's input gates -> fc1 -> fc2 -> fc3 + sampling: five in-launch hand-offs.
+// Hand-offs follow the LSTM recurrences' counter form (cdna_hip_programming.md Guideline 16):
+// payload stored write-through (sc1), every storing wave drains, barrier, one 8-lane add to the
+// stage's 8 counter replicas; a consumer polls its replica relaxed, barrier, and EVERY load of
+// handed-off bytes is an sc1 load.  Counters are a ring of kWrRing steps per stage that is never
+// reset: launch E's target for step i (ring slot k = i % kWrRing) is ((E - 1) n_k + i / kWrRing
+// + 1) P, n_k the steps of slot k per launch, P the stage's producers; E comes from a ticket each
+// workgroup takes at start, as in the recurrences.  Write-after-read: each buffer rewritten at
+// step i + 1 was read at step i by workgroups that counted in on a counter the writer has waited
+// for.  Every spin is bounded; a launch that gives up writes its remaining samples
+// as NaN and the call reports AVC_ERR_DEVICE.
+constexpr int kWrRing = 16, kWrStages = 5, kWrRep = 8, kWrLine = 32;
+constexpr int kWrMaxChunks = 4;  // fold rows <= kWrMaxChunks * kRC
+constexpr long kWrCntWords = (long)kWrStages * kWrRing * kWrRep * kWrLine;
+enum : int { WR_NONE = 0, WR_FC1 = 1, WR_FC2 = 2, WR_OUT = 3 };
+enum : int { S_GRU1 = 0, S_GRU2 = 1, S_FC1 = 2, S_FC2 = 3, S_OUT = 4 };
+// LDS (floats): staging | partial transpose | hidden sums [2][chunks][6 kRC] | input / fc sums |
+// previous h [2][chunks][2 kRC] | own t1 [chunks][2 kRC] | logits | flags
+constexpr int kWrXs = 0, kWrRed = kWrXs + kRC * 576, kWrShid = kWrRed + 8 * kRC * kRP;
+constexpr int kWrSin = kWrShid + 2 * kWrMaxChunks * 6 * kRC, kWrHprev = kWrSin + 8 * kRC;
+constexpr int kWrT1 = kWrHprev + 2 * kWrMaxChunks * 2 * kRC, kWrLg = kWrT1 + kWrMaxChunks * 2 * kRC;
+constexpr int kWrFlags = kWrLg + 64, kWrLdsFloats = kWrFlags + 8;
+
+struct WrLoop {
+  WrStep a;
+  int G, nfc, nchk;
+  unsigned* cnt;                  // [stage][ring][replica] lines (never reset)
+  unsigned* tmo;                  // give-up word: epoch of the last launch that gave up
+  unsigned long long* tickets;    // one per workgroup per launch
+  unsigned* fail_host;            // the context's pinned failure word
+  unsigned spin_limit;
+};
+
+typedef __attribute__((address_space(1))) unsigned wr_gu32;
+typedef unsigned wr_u32x4 __attribute__((ext_vector_type(4)));
+__device__ unsigned g_wr_giveups = 0;
+
+// sc1 (write-through / L2-bypassing) accesses of handed-off bytes: base is uniform, off in floats
+__device__ __forceinline__ float4 ld4_sc1(const float* base, long off) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+  const wr_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off * 4), 0, 16 /*sc1*/);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ float ld_sc1(const float* base, long off) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off * 4), 0, 16 /*sc1*/));
+}
+__device__ __forceinline__ void st_sc1(float* base, long off, float v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)(off * 4), 0, 16 /*sc1*/);
+}
+
+__device__ __forceinline__ long wr_cidx(int S, int i, int rep) {
+  return (((long)S * kWrRing + i % kWrRing) * kWrRep + rep) * kWrLine;
+}
+__device__ __forceinline__ unsigned wr_target(const WrLoop& p, int S, int i, unsigned E) {
+  const int k = i % kWrRing;
+  const unsigned nk = (unsigned)((p.a.L - k + kWrRing - 1) / kWrRing);
+  const unsigned P = S <= S_GRU2 ? (unsigned)p.G : S <= S_FC2 ? (unsigned)p.nfc : (unsigned)p.a.R;
+  return ((E - 1u) * nk + (unsigned)(i / kWrRing) + 1u) * P;
+}
+
+// One lane waits for stage S of step i (wrap-safe relaxed agent-scope polls of its replica);
+// false = gave up, or another workgroup of this launch did (the give-up word, every 64 polls).
+__device__ __forceinline__ bool wr_poll(const WrLoop& p, int S, int i, unsigned E) {
+  wr_gu32* c = (wr_gu32*)(p.cnt + wr_cidx(S, i, blockIdx.x % kWrRep));
+  wr_gu32* t = (wr_gu32*)p.tmo;
+  const unsigned target = wr_target(p, S, i, E);
+  for (unsigned spins = 0;; ++spins) {
+    if ((int)(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) return true;
+    if ((spins & 63) == 63 && __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E) return false;
+    if (spins >= p.spin_limit) {
+      const unsigned old = __hip_atomic_fetch_max(t, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old != E) {  // first to give up in this launch (tag 0x40000000: the vocoder loop)
+        const unsigned n = atomicAdd(&g_wr_giveups, 1u) + 1u;
+        if (p.fail_host)
+          __hip_atomic_store(p.fail_host, 0x40000000u | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// the whole workgroup waits (thread 0 polls; the verdict goes through one of 4 LDS words in turn,
+// so a word is rewritten only after barriers every reader has passed)
+__device__ __forceinline__ bool wr_wait(const WrLoop& p, int S, int i, unsigned E, int* flags, int& nw) {
+  int* f = flags + (nw++ & 3);
+  if (threadIdx.x == 0) *f = wr_poll(p, S, i, E) ? 1 : 0;
+  __syncthreads();
+  return *f != 0;
+}
+
+// every storing wave drains its sc1 stores, barrier, one 8-lane add to the stage's replicas
+__device__ __forceinline__ void wr_publish(const WrLoop& p, int S, int i) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < kWrRep)
+    __hip_atomic_fetch_add((wr_gu32*)(p.cnt + wr_cidx(S, i, threadIdx.x)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Loop staging of rows [rb, rb + kRC) of input `which` (stage_load's layout and values): _pre
+// issues the loads of bytes no workgroup of the launch writes (pI, the aux slices) before the
+// wait, _post the handed-off part (sc1) after it; IN_XI forms pI + W_I[:, 0] x_prev as stage_load.
+__device__ __forceinline__ void lstage_pre(const WrStep& a, int which, int i, int rb, int K, int tid, float4 (&v)[kStage4]) {
+  const int K4 = K >> 2, H = a.H;
+#pragma unroll
+  for (int m = 0; m < kStage4; ++m) {
+    const int e = tid + 256 * m;
+    const int rr = e / K4, k = 4 * (e - rr * K4), r = rb + rr;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rr < kRC && r < a.R) {
+      int src;
+      long q;
+      fold_pos(a, r, i, src, q);
+      if (which == IN_XI) {
+        x = *reinterpret_cast<const float4*>(a.pI + ((long)src * (a.Ltot + 1) + q) * H + k);
+      } else if (which != IN_H1 && which != IN_H2) {
+        const int kv = which == IN_Y1A4 ? a.Fc : H;
+        if (k >= kv && q < a.Ltot) {
+          const int off = (which == IN_T1A2 ? 1 : which == IN_T2A3 ? 2 : 3) * a.A + (k - kv);
+          x = *reinterpret_cast<const float4*>(a.auxf + ((long)src * a.Tf + q / a.hop) * a.auxd + off);
+        }
+      }
+    }
+    v[m] = x;
+  }
+}
+__device__ __forceinline__ void lstage_post(const WrStep& a, int which, int i, int rb, int K, int tid, float4 (&v)[kStage4]) {
+  const int K4 = K >> 2, H = a.H, cur = i & 1;
+#pragma unroll
+  for (int m = 0; m < kStage4; ++m) {
+    const int e = tid + 256 * m;
+    const int rr = e / K4, k = 4 * (e - rr * K4), r = rb + rr;
+    if (rr < kRC && r < a.R) {
+      switch (which) {
+        case IN_XI: {
+          const float4 pi = v[m];
+          const float4 w0 = *reinterpret_cast<const float4*>(a.wi0 + k);
+          const float xp = a.teacher ? a.x_tf[(long)r * a.L + i] : ld_sc1(a.x_prev, r);
+          v[m] = make_float4(fmaf(w0.x, xp, pi.x), fmaf(w0.y, xp, pi.y), fmaf(w0.z, xp, pi.z), fmaf(w0.w, xp, pi.w));
+          break;
+        }
+        case IN_H1: v[m] = ld4_sc1(a.h1, ((long)cur * a.R + r) * H + k); break;
+        case IN_H2: v[m] = ld4_sc1(a.h2, ((long)cur * a.R + r) * H + k); break;
+        case IN_T1A2: if (k < H) v[m] = ld4_sc1(a.t1, (long)r * H + k); break;
+        case IN_T2A3: if (k < H) v[m] = ld4_sc1(a.t2, (long)r * H + k); break;
+        default: if (k < a.Fc) v[m] = ld4_sc1(a.y1, (long)r * a.Fc + k); break;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void lstage_store(int K, int tid, const float4 (&v)[kStage4], float* xs) {
+  const int K4 = K >> 2;
+#pragma unroll
+  for (int m = 0; m < kStage4; ++m) {
+    const int e = tid + 256 * m;
+    if (e < kRC * K4) reinterpret_cast<float4*>(xs)[e] = v[m];
+  }
+}
+
+// rows_dot over the NR staged rows [rr0, rr0 + NR): each (output row, staged row) partial is formed
+// in rows_dot's order (j ascending, x y z w), so the sums are the per-step kernels' bits
+template <int NG, int NR>
+__device__ __forceinline__ void rows_dot_part(const float4 (&wv)[NG][kJ4], const float* xs, int K, int lane, int rr0,
+                                              float (&acc)[NG][NR]) {
+  const int K4 = K >> 2;
+  const float4* xs4 = reinterpret_cast<const float4*>(xs);
+#pragma unroll
+  for (int g = 0; g < NG; ++g)
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) acc[g][rr] = 0.f;
+#pragma unroll
+  for (int j = 0; j < kJ4; ++j) {
+    const int k4 = lane + 64 * j;
+    if (k4 < K4) {
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) {
+        const float4 x = xs4[(rr0 + rr) * K4 + k4];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          float t = acc[g][rr];
+          t = fmaf(wv[g][j].x, x.x, t);
+          t = fmaf(wv[g][j].y, x.y, t);
+          t = fmaf(wv[g][j].z, x.z, t);
+          acc[g][rr] = fmaf(wv[g][j].w, x.w, t);
+        }
+      }
+    }
+  }
+}
+
+// One GRU phase of step i for units u0, u0 + 1: HID = the hidden gates (W_hh h_{i-1}; sums kept
+// for the input phase), else the input gates, the cell and the hand-off of h_i and t1 / t2.
+// Wave w multiplies unit w >> 1's three gate rows against staged rows [12 (w & 1), + 12).
+template <int WHICH, bool HID>
+__device__ __forceinline__ bool gru_phase(const WrLoop& p, int i, unsigned E, float* sm, int& nw, const float (&ebi)[3],
+                          const float (&ebh)[3]) {
+  const WrStep& a = p.a;
+  // (the thread index goes through an empty asm per phase, so the lane-dependent index math of
+  // every phase is formed inside it instead of being hoisted out of the step loop into scratch)
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, w = tid >> 6;
+  const int H = a.H, R = a.R, u0 = blockIdx.x * 2;
+  const int K = HID ? H : (WHICH == 1 ? H : H + a.A);
+  const int which = HID ? (WHICH == 1 ? IN_H1 : IN_H2) : (WHICH == 1 ? IN_XI : IN_T1A2);
+  const float* W = HID ? (WHICH == 1 ? a.Whh1 : a.Whh2) : (WHICH == 1 ? a.Wih1 : a.Wih2);
+  float* xs = sm + kWrXs;
+  float* red = sm + kWrRed;
+  float* sin_ = sm + kWrSin;
+  int* flags = reinterpret_cast<int*>(sm + kWrFlags);
+  float4 wv[3][kJ4];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int j = 0; j < kJ4; ++j) wv[g][j] = wrow4(W, (long)g * H + u0 + (w >> 1), K, lane + 64 * j);
+  float4 v[kStage4];
+  lstage_pre(a, which, i, 0, K, tid, v);
+  // producers: HID waits for h_{i-1} of its own layer; GRU1's input gates for the sample of step
+  // i - 1, GRU2's for t1 of step i
+  const int wS = HID ? (WHICH == 1 ? S_GRU1 : S_GRU2) : (WHICH == 1 ? S_OUT : S_GRU1);
+  const int wi = (HID || WHICH == 1) ? i - 1 : i;
+  if (wi >= 0 && !wr_wait(p, wS, wi, E, flags, nw)) return false;
+  for (int c = 0; c < p.nchk; ++c) {
+    const int rb = c * kRC;
+    if (c > 0) lstage_pre(a, which, i, rb, K, tid, v);
+    lstage_post(a, which, i, rb, K, tid, v);
+    lstage_store(K, tid, v, xs);
+    __syncthreads();
+    float acc[3][12];
+    rows_dot_part<3, 12>(wv, xs, K, lane, 12 * (w & 1), acc);
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int rr = 0; rr < 12; ++rr) red[(((w >> 1) * 3 + g) * kRC + 12 * (w & 1) + rr) * kRP + lane] = acc[g][rr];
+    __syncthreads();
+    float* dst = HID ? sm + kWrShid + ((WHICH - 1) * kWrMaxChunks + c) * 6 * kRC : sin_;
+    if (tid < 6 * kRC) {
+      const float* row = red + tid * kRP;
+      float s = 0.f;
+#pragma unroll 8
+      for (int l = 0; l < 64; ++l) s += row[l];
+      dst[tid] = s;
+    }
+    __syncthreads();
+    if (!HID) {
+      const int nr = min(kRC, R - rb);
+      if (tid < 2 * nr) {
+        const int uu = tid & 1, rr0 = tid >> 1, un = u0 + uu, r0 = rb + rr0;
+        const float* sh = sm + kWrShid + ((WHICH - 1) * kWrMaxChunks + c) * 6 * kRC;
+        float* hp = sm + kWrHprev + ((WHICH - 1) * kWrMaxChunks + c) * 2 * kRC + tid;
+        float* t1o = sm + kWrT1 + c * 2 * kRC + tid;
+        const float hn = gru_cell(sin_ + uu * 3 * kRC + rr0, sh + uu * 3 * kRC + rr0, ebi, ebh, *hp);
+        *hp = hn;
+        float ex;
+        if (WHICH == 1) {
+          int src;
+          long q;
+          fold_pos(a, r0, i, src, q);
+          const float xp = a.teacher ? a.x_tf[(long)r0 * a.L + i] : ld_sc1(a.x_prev, r0);
+          ex = fmaf(a.wi0[un], xp, a.pI[((long)src * (a.Ltot + 1) + q) * H + un]);
+        } else {
+          ex = *t1o;
+        }
+        const float tv = ex + hn;
+        if (WHICH == 1) *t1o = tv;
+        st_sc1(WHICH == 1 ? a.h1 : a.h2, ((long)((i & 1) ^ 1) * R + r0) * H + un, hn);
+        st_sc1(WHICH == 1 ? a.t1 : a.t2, (long)r0 * H + un, tv);
+      }
+    }
+  }
+  if (!HID) wr_publish(p, WHICH == 1 ? S_GRU1 : S_GRU2, i);
+  return true;
+}
+
+// fc1 / fc2 of step i for rows [8f, 8f + 8) (wr_fc_kernel's arithmetic)
+template <int WHICH>
+__device__ __forceinline__ bool fc_phase(const WrLoop& p, int f, int i, unsigned E, float* sm, int& nw) {
+  const WrStep& a = p.a;
+  int tid = threadIdx.x;  // (opaque per phase: see gru_phase)
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, w = tid >> 6;
+  const int Kv = WHICH == 1 ? a.H : a.Fc, K = Kv + a.A;
+  const float* W = WHICH == 1 ? a.W1 : a.W2;
+  const float* bias = WHICH == 1 ? a.b1 : a.b2;
+  float* y = WHICH == 1 ? a.y1 : a.y2;
+  float* xs = sm + kWrXs;
+  float* sums = sm + kWrSin;
+  int* flags = reinterpret_cast<int*>(sm + kWrFlags);
+  const int n0 = f * 8 + 2 * w;
+  float4 wv[2][kJ4];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < kJ4; ++j) wv[g][j] = wrow4(W, min(n0 + g, a.Fc - 1), K, lane + 64 * j);
+  const int which = WHICH == 1 ? IN_T2A3 : IN_Y1A4;
+  float4 v[kStage4];
+  lstage_pre(a, which, i, 0, K, tid, v);
+  if (!wr_wait(p, WHICH == 1 ? S_GRU2 : S_FC1, i, E, flags, nw)) return false;
+  for (int c = 0; c < p.nchk; ++c) {
+    const int rb = c * kRC;
+    if (c > 0) lstage_pre(a, which, i, rb, K, tid, v);
+    lstage_post(a, which, i, rb, K, tid, v);
+    lstage_store(K, tid, v, xs);
+    __syncthreads();
+    float acc[2][kRC];
+    rows_dot<2>(wv, xs, K, lane, acc);
+    reduce_lanes<2>(acc, w, lane, sm + kWrRed, sums);
+    const int nr = min(kRC, a.R - rb);
+    for (int t = tid; t < 8 * nr; t += 256) {
+      const int o = t / nr, rr = t - o * nr, n = f * 8 + o;
+      if (n < a.Fc) st_sc1(y, (long)(rb + rr) * a.Fc + n, fmaxf(sums[o * kRC + rr] + bias[n], 0.f));
+    }
+    __syncthreads();
+  }
+  wr_publish(p, WHICH == 1 ? S_FC1 : S_FC2, i);
+  return true;
+}
+
+// fc3 + sampling of fold row r at step i (wr_out_kernel's arithmetic)
+__device__ __forceinline__ bool out_phase(const WrLoop& p, int r, int i, unsigned E, float* sm, int& nw) {
+  const WrStep& a = p.a;
+  int tid = threadIdx.x;  // (opaque per phase: see gru_phase)
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, w = tid >> 6;
+  const int Fc = a.Fc, NC = a.NC;
+  float* red = sm + kWrRed;
+  float* lg = sm + kWrLg;
+  int* flags = reinterpret_cast<int*>(sm + kWrFlags);
+  float4 w3[8][kJ4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int j = 0; j < kJ4; ++j)
+      w3[m][j] = reinterpret_cast<const float4*>(a.W3 + (long)min(w + 4 * m, NC - 1) * Fc)[min(lane + 64 * j, (Fc >> 2) - 1)];
+  if (!wr_wait(p, S_FC2, i, E, flags, nw)) return false;
+  float4 yv[kJ4];
+#pragma unroll
+  for (int j = 0; j < kJ4; ++j)
+    yv[j] = lane + 64 * j < (Fc >> 2) ? ld4_sc1(a.y2, (long)r * Fc + 4 * (lane + 64 * j)) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float acc[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kJ4; ++j) {
+      s = fmaf(w3[m][j].x, yv[j].x, s);
+      s = fmaf(w3[m][j].y, yv[j].y, s);
+      s = fmaf(w3[m][j].z, yv[j].z, s);
+      s = fmaf(w3[m][j].w, yv[j].w, s);
+    }
+    acc[m] = s;
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) red[(w * 8 + m) * kRP + lane] = acc[m];
+  __syncthreads();
+  if (tid < 32) {
+    const int ww = tid & 3, m = tid >> 2, c = ww + 4 * m;
+    if (c < NC) {
+      const float* row = red + (ww * 8 + m) * kRP;
+      float s = 0.f;
+#pragma unroll 8
+      for (int l = 0; l < 64; ++l) s += row[l];
+      lg[c] = s + a.b3[c];
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float x = wr_sample(a, r, i, lg);
+    a.out[(long)r * a.L + i] = x;
+    st_sc1(a.x_prev, r, x);
+  }
+  wr_publish(p, S_OUT, i);
+  return true;
+}
+
+__global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
+  extern __shared__ float wr_sm[];
+  const WrStep& a = p.a;
+  const int tid = threadIdx.x, L = a.L;
+  int* flags = reinterpret_cast<int*>(wr_sm + kWrFlags);
+  if (tid == 0) {  // this launch's epoch
+    const unsigned long long tk = __hip_atomic_fetch_add(p.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flags[4] = (int)(unsigned)(tk / (unsigned long long)p.G + 1ull);
+  }
+  for (int t = tid; t < kWrLg - kWrHprev; t += 256) wr_sm[kWrHprev + t] = 0.f;  // h_{-1} = 0
+  __syncthreads();
+  const unsigned E = (unsigned)flags[4];
+  int nw = 0;
+  const int wg = blockIdx.x, nfc = p.nfc;
+  const int role = wg < nfc ? WR_FC1 : wg < 2 * nfc ? WR_FC2 : wg < 2 * nfc + a.R ? WR_OUT : WR_NONE;
+  // the epilogue thread's biases (unit u0 + (tid & 1)), fixed for the launch
+  const int un = 2 * wg + (tid & 1);
+  float ebi1[3], ebh1[3], ebi2[3], ebh2[3];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    ebi1[g] = a.bih1[g * a.H + un];
+    ebh1[g] = a.bhh1[g * a.H + un];
+    ebi2[g] = a.bih2[g * a.H + un];
+    ebh2[g] = a.bhh2[g * a.H + un];
+  }
+  // per step: GRU1 and GRU2 input phases of step i, then the role's ops; HID ops form step i + 1's
+  // hidden sums (skipped after the last step).  One op list walked by one switch, so every phase
+  // is instantiated once.
+  enum : int { OP_HID1, OP_HID2, OP_IN1, OP_IN2, OP_FC1, OP_FC2, OP_OUT };
+  // the role's op list, packed 4 bits per op (no indexed array: it would live in scratch)
+  const unsigned seq = role == WR_FC1   ? (OP_IN1 | OP_IN2 << 4 | OP_FC1 << 8 | OP_HID1 << 12 | OP_HID2 << 16)
+                       : role == WR_FC2 ? (OP_IN1 | OP_IN2 << 4 | OP_HID2 << 8 | OP_FC2 << 12 | OP_HID1 << 16)
+                       : role == WR_OUT ? (OP_IN1 | OP_IN2 << 4 | OP_HID1 << 8 | OP_HID2 << 12 | OP_OUT << 16)
+                                        : (OP_IN1 | OP_IN2 << 4 | OP_HID1 << 8 | OP_HID2 << 12);
+  const int nops = role == WR_NONE ? 4 : 5;
+  bool ok = true;
+  int i = -1;  // step -1: only the hidden sums of step 0 (h_{-1} = 0)
+  for (; ok && i < L; ++i) {
+    for (int o = 0; o < nops && ok; ++o) {
+      const int op = (int)((seq >> (4 * o)) & 15u);
+      const bool hid = op == OP_HID1 || op == OP_HID2;
+      if (hid ? i + 1 >= L : i < 0) continue;
+      switch (op) {
+        case OP_HID1: ok = gru_phase<1, true>(p, i + 1, E, wr_sm, nw, ebi1, ebh1); break;
+        case OP_HID2: ok = gru_phase<2, true>(p, i + 1, E, wr_sm, nw, ebi2, ebh2); break;
+        case OP_IN1: ok = gru_phase<1, false>(p, i, E, wr_sm, nw, ebi1, ebh1); break;
+        case OP_IN2: ok = gru_phase<2, false>(p, i, E, wr_sm, nw, ebi2, ebh2); break;
+        case OP_FC1: ok = fc_phase<1>(p, wg, i, E, wr_sm, nw); break;
+        case OP_FC2: ok = fc_phase<2>(p, wg - nfc, i, E, wr_sm, nw); break;
+        default: ok = out_phase(p, wg - 2 * nfc, i, E, wr_sm, nw); break;
+      }
+    }
+    if (!ok) break;
+  }
+  // gave up at step i: the row's remaining samples (and teacher-forced logits) are NaN, so a
+  // timed-out launch never returns plausible audio (the call reports it)
+  if (!ok && role == WR_OUT && tid == 0) {
+    const int r = wg - 2 * nfc;
+    const float nan = __builtin_nanf("");
+    for (int k = max(i, 0); k < L; ++k) {
+      a.out[(long)r * L + k] = nan;
+      if (a.teacher)
+        for (int c = 0; c < a.NC; ++c) a.logits[((long)r * L + k) * a.NC + c] = nan;
+    }
+  }
+}
+
+int g_wr_persist = 0;  // avc_wavernn_persist(): 1 = the persistent sample loop where eligible
+int g_wr_inject = 0;   // avc_debug_wavernn_inject(): loop launches left that give up at once
+
+// workgroups of wr_loop_kernel the device holds at once (occupancy x CUs), cached per device
+int wr_loop_capacity() {
+  static int cap = -1, cap_dev = -1;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (cap >= 0 && dev == cap_dev) return cap;
+  const void* fn = (const void*)wr_loop_kernel;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kWrLdsFloats * 4);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, kWrLdsFloats * 4) != hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = 0;
+  }
+  cap = per_cu * coresident_cus();
+  cap_dev = dev;
+  return cap;
+}
+
+// the loop's shape limits: fold rows in <= kWrMaxChunks staging chunks, one workgroup per role
+// (fc1, fc2, each fold row's sampling) besides the GRU units, every workgroup resident
+bool wr_loop_eligible(const WrStep& a) {
+  const int G = a.H / 2, nfc = (a.Fc + 7) / 8;
+  return g_wr_persist && a.R <= kWrMaxChunks * kRC && 2 * nfc + a.R <= G && a.L >= 1 && G <= wr_loop_capacity();
+}
+
+int wr_loop_run(avc_context* ctx, const WrStep& a, hipStream_t s, double macs) {
+  AVC_TRY(persist_guard(ctx));
+  const int G = a.H / 2;
+  unsigned* region = nullptr;
+  // counter layout key: (L, G) -- the targets depend on the steps per launch
+  AVC_TRY(coresident_region(ctx, 5, a.L, G, G, (size_t)kWrCntWords, s, &region));
+  WrLoop p{};
+  p.a = a;
+  p.G = G;
+  p.nfc = (a.Fc + 7) / 8;
+  p.nchk = (a.R + kRC - 1) / kRC;
+  p.tickets = reinterpret_cast<unsigned long long*>(region);  // region layout: lstm_persist.hip
+  p.tmo = region + 32;
+  p.cnt = region + 64;
+  p.fail_host = host_flags(ctx);
+  if (!p.fail_host) return AVC_ERR_HIP;
+  p.spin_limit = coresident_spin_limit();
+  if (g_wr_inject > 0) {  // test hook: this launch gives up at its first unmet poll
+    --g_wr_inject;
+    p.spin_limit = 0;
+  }
+  void* args[] = {&p};
+  hipEvent_t ev = timing_begin(TC_WAVERNN, s);
+  AVC_TRY(coresident_dispatch(ctx, (const void*)wr_loop_kernel, dim3(G), dim3(256), args, kWrLdsFloats * 4, s));
+  if (ev) timing_end(TC_WAVERNN, ev, s, (double)a.L * 2.0 * macs * a.R, (double)a.L * 4.0 * macs);
+  AVC_HIP(hipStreamSynchronize(s));
+  return persist_guard(ctx);  // this launch gave up: its samples are NaN, report it now
 }
 
 // numpy.linspace(a, b, n)[k] in float64: a + k·(b - a)/(n - 1), the last point exactly b
@@ -749,7 +1283,14 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
   const long chunks = (L + kChunk - 1) / kChunk;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
-  if (chunks > 1) {
+  // per-step algorithmic work of every fold row (timing class "wavernn"): GRU1 6·H·H, GRU2
+  // 3·H·(H + A) + 3·H·H, fc1 Fc·(H + A), fc2 Fc·(Fc + A), fc3 NC·Fc MACs, every weight read once
+  // per step
+  const double macs = 6.0 * H * H + 3.0 * H * (H + A) + 3.0 * H * H + (double)d.Fc * (H + A) +
+                      (double)d.Fc * (d.Fc + A) + (double)d.NC * d.Fc;
+  if (wr_loop_eligible(a)) {
+    AVC_TRY(wr_loop_run(ctx, a, s, macs));
+  } else if (chunks > 1) {
     AVC_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
     int rc = AVC_OK;
     for (int k = 0; k < kChunk && rc == AVC_OK; ++k) rc = launch_step(a, cs);
@@ -764,11 +1305,6 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
       (void)hipGraphDestroy(graph);
       AVC_HIP(ei);
     }
-    // per-step algorithmic work of every fold row (timing class "wavernn", one record per chunk):
-    // GRU1 6·H·H, GRU2 3·H·(H + A) + 3·H·H, fc1 Fc·(H + A), fc2 Fc·(Fc + A), fc3 NC·Fc MACs,
-    // every weight read once per step
-    const double macs = 6.0 * H * H + 3.0 * H * (H + A) + 3.0 * H * H + (double)d.Fc * (H + A) +
-                        (double)d.Fc * (d.Fc + A) + (double)d.NC * d.Fc;
     for (long c = 0; c < chunks; ++c) {
       hipEvent_t ev = timing_begin(TC_WAVERNN, s);
       const hipError_t el = hipGraphLaunch(exec, s);
@@ -795,6 +1331,28 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
     AVC_LAUNCH_CHECK();
   }
   return AVC_OK;
+}
+
+int avc_wavernn_persist(int on) {
+  AVC_CHECK_ARG(on == 0 || on == 1, "avc_wavernn_persist: on must be 0 or 1");
+  avc::g_wr_persist = on;
+  return AVC_OK;
+}
+
+int avc_debug_wavernn_inject(int launches) {
+  AVC_CHECK_ARG(launches >= 0, "avc_debug_wavernn_inject: launches must be >= 0");
+  avc::g_wr_inject = launches;
+  return AVC_OK;
+}
+
+int avc_wavernn_persist_eligible(int rows, int rnn_dims, int fc_dims) {
+  avc::WrStep a{};
+  a.R = rows; a.H = rnn_dims; a.Fc = fc_dims; a.L = 1;
+  const int on = avc::g_wr_persist;
+  avc::g_wr_persist = 1;
+  const bool ok = avc::wr_loop_eligible(a);
+  avc::g_wr_persist = on;
+  return ok ? 1 : 0;
 }
 
 // Rows and steps of a generate() call (so the caller can size `samples` [rows][steps]).

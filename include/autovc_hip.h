@@ -462,6 +462,16 @@ int avc_wavernn_upsample(avc_context* ctx, const int* dims, int T, const float* 
 int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* const* params, const float* mel,
                          int batched, int target, int overlap, int mol, unsigned long long seed,
                          const float* x_teacher, float* logits, float* samples, float* wave, void* stream);
+/* Tuning hook: 1 = avc_wavernn_generate runs the whole sample loop as ONE persistent launch of
+ * rnn_dims / 2 workgroups with in-launch hand-offs where eligible
+ * (avc_wavernn_persist_eligible: <= 96 fold rows, 2 * ceil(fc_dims / 8) + rows <= rnn_dims / 2,
+ * every workgroup resident); 0 = five graph-captured launches per sample step.  Same arithmetic,
+ * bit-identical samples, logits and waveform.  A loop launch that abandons a bounded wait writes
+ * its remaining samples as NaN and the call fails with AVC_ERR_DEVICE. */
+int avc_wavernn_persist(int on);
+int avc_wavernn_persist_eligible(int rows, int rnn_dims, int fc_dims);
+/* Test hook: the next `launches` loop launches give up at their first unmet wait. */
+int avc_debug_wavernn_inject(int launches);
 
 #ifdef __cplusplus
 }

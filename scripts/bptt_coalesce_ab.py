@@ -38,4 +38,4 @@ for H, din in ((1024, 1024), (512, 320)):
         v = res[mode][1:]
         print(f"H={H} coalesce={mode}: BPTT launch median {np.median(v):.1f} us ({', '.join(f'{t:.0f}' for t in v)})",
               flush=True)
-_lib.call("avc_bptt_coalesce", 0)
+_lib.call("avc_bptt_coalesce", 1)

@@ -132,7 +132,8 @@ with torch.no_grad():
     ref = chain(o64, din64, 0)           # float64 chain
     r32 = chain(o32, din32, 0)           # fp32 reference chain
     g = chain(gpu, dinG.to(dev), 0)      # GPU per-layer chain
-    fused = [v.cpu().double() for v in ae(x.to(dev), co.to(dev), ct.to(dev))]
+    # the fused forward returns (B, 80, T) mels: to frames [T*B][80] like the chains
+    fused = [v.cpu().double().permute(2, 0, 1).reshape(T * B, -1) for v in ae(x.to(dev), co.to(dev), ct.to(dev))[:2]]
     ae.check_health()
 
 

@@ -13,7 +13,7 @@ import torch
 from autovc_amd import _lib, ops
 
 pytestmark = pytest.mark.gpu
-DEFAULT = 0  # the library's default (avc_bptt_coalesce)
+DEFAULT = 1  # the library's default (avc_bptt_coalesce)
 
 
 def _bwd(dev, B, T, din, H, mode):
