@@ -111,6 +111,7 @@ _SIGS = {
     "avc_wavernn_persist": [_I],
     "avc_wavernn_persist_eligible": [_I, _I, _I],
     "avc_debug_wavernn_inject": [_I],
+    "avc_debug_wavernn_stamps": [_P, _I],
     "avc_wavernn_upsample": [_P, _P, _I, _P, _P, _P, _P, _P],
     "avc_wavernn_generate": [_P, _P, _I, _P, _P, _I, _I, _I, _I, ctypes.c_ulonglong, _P, _P, _P, _P, _P],
     "avc_wavernn_fold_shape": [ctypes.c_long, _I, _I, _I, ctypes.POINTER(ctypes.c_long),

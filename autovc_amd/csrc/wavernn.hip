@@ -584,6 +584,8 @@ struct WrLoop {
   unsigned long long* tickets;    // one per workgroup per launch
   unsigned* fail_host;            // the context's pinned failure word
   unsigned spin_limit;
+  unsigned long long* stamps;     // diagnostics (avc_debug_wavernn_stamps): [G][nstamp][16] realtime
+  int nstamp;                     // steps stamped
 };
 
 typedef __attribute__((address_space(1))) unsigned wr_gu32;
@@ -641,7 +643,12 @@ __device__ __forceinline__ bool wr_poll(const WrLoop& p, int S, int i, unsigned 
 // so a word is rewritten only after barriers every reader has passed)
 __device__ __forceinline__ bool wr_wait(const WrLoop& p, int S, int i, unsigned E, int* flags, int& nw) {
   int* f = flags + (nw++ & 3);
-  if (threadIdx.x == 0) *f = wr_poll(p, S, i, E) ? 1 : 0;
+  if (threadIdx.x == 0) {
+    *f = wr_poll(p, S, i, E) ? 1 : 0;
+    // diagnostics: when the wait ended (slot 3 op + 1 of the loop step; flags[6] / [7] = op, step)
+    if (p.stamps && flags[7] >= 0 && flags[7] < p.nstamp)
+      p.stamps[((long)blockIdx.x * p.nstamp + flags[7]) * 24 + 3 * flags[6] + 1] = __builtin_amdgcn_s_memrealtime();
+  }
   __syncthreads();
   return *f != 0;
 }
@@ -940,6 +947,7 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
   if (tid == 0) {  // this launch's epoch
     const unsigned long long tk = __hip_atomic_fetch_add(p.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     flags[4] = (int)(unsigned)(tk / (unsigned long long)p.G + 1ull);
+    flags[7] = -1;
   }
   for (int t = tid; t < kWrLg - kWrHprev; t += 256) wr_sm[kWrHprev + t] = 0.f;  // h_{-1} = 0
   __syncthreads();
@@ -974,6 +982,12 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
       const int op = (int)((seq >> (4 * o)) & 15u);
       const bool hid = op == OP_HID1 || op == OP_HID2;
       if (hid ? i + 1 >= L : i < 0) continue;
+      const bool stamp = p.stamps && i >= 0 && i < p.nstamp && tid == 0;
+      if (tid == 0) {  // (read by wr_wait's stamp, same thread)
+        flags[6] = op;
+        flags[7] = i;
+      }
+      if (stamp) p.stamps[((long)wg * p.nstamp + i) * 24 + 3 * op] = __builtin_amdgcn_s_memrealtime();
       switch (op) {
         case OP_HID1: ok = gru_phase<1, true>(p, i + 1, E, wr_sm, nw, ebi1, ebh1); break;
         case OP_HID2: ok = gru_phase<2, true>(p, i + 1, E, wr_sm, nw, ebi2, ebh2); break;
@@ -983,6 +997,7 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
         case OP_FC2: ok = fc_phase<2>(p, wg - nfc, i, E, wr_sm, nw); break;
         default: ok = out_phase(p, wg - 2 * nfc, i, E, wr_sm, nw); break;
       }
+      if (stamp) p.stamps[((long)wg * p.nstamp + i) * 24 + 3 * op + 2] = __builtin_amdgcn_s_memrealtime();
     }
     if (!ok) break;
   }
@@ -1001,6 +1016,8 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
 
 int g_wr_persist = 0;  // avc_wavernn_persist(): 1 = the persistent sample loop where eligible
 int g_wr_inject = 0;   // avc_debug_wavernn_inject(): loop launches left that give up at once
+unsigned long long* g_wr_stamps = nullptr;  // avc_debug_wavernn_stamps(): next loop launch's stamps
+int g_wr_nstamp = 0;
 
 // workgroups of wr_loop_kernel the device holds at once (occupancy x CUs), cached per device
 int wr_loop_capacity() {
@@ -1048,6 +1065,9 @@ int wr_loop_run(avc_context* ctx, const WrStep& a, hipStream_t s, double macs) {
     --g_wr_inject;
     p.spin_limit = 0;
   }
+  p.stamps = g_wr_stamps;
+  p.nstamp = g_wr_stamps ? g_wr_nstamp : 0;
+  g_wr_stamps = nullptr;
   void* args[] = {&p};
   hipEvent_t ev = timing_begin(TC_WAVERNN, s);
   AVC_TRY(coresident_dispatch(ctx, (const void*)wr_loop_kernel, dim3(G), dim3(256), args, kWrLdsFloats * 4, s));
@@ -1342,6 +1362,15 @@ int avc_wavernn_persist(int on) {
 int avc_debug_wavernn_inject(int launches) {
   AVC_CHECK_ARG(launches >= 0, "avc_debug_wavernn_inject: launches must be >= 0");
   avc::g_wr_inject = launches;
+  return AVC_OK;
+}
+
+// Diagnostics: the next loop launch writes s_memrealtime stamps (100 MHz) of its first `steps`
+// steps into buf [rnn_dims / 2][steps][24] (u64; per op: start, wait done, end).
+int avc_debug_wavernn_stamps(void* buf, int steps) {
+  AVC_CHECK_ARG(steps >= 0 && (buf || steps == 0), "avc_debug_wavernn_stamps: bad arguments");
+  avc::g_wr_stamps = static_cast<unsigned long long*>(buf);
+  avc::g_wr_nstamp = steps;
   return AVC_OK;
 }
 

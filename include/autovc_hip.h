@@ -472,6 +472,9 @@ int avc_wavernn_persist(int on);
 int avc_wavernn_persist_eligible(int rows, int rnn_dims, int fc_dims);
 /* Test hook: the next `launches` loop launches give up at their first unmet wait. */
 int avc_debug_wavernn_inject(int launches);
+/* Diagnostics: the next loop launch stamps its first `steps` steps (s_memrealtime, 100 MHz) into
+ * buf [rnn_dims / 2][steps][24] (u64; per op of the loop: start, wait done, end). */
+int avc_debug_wavernn_stamps(void* buf, int steps);
 
 #ifdef __cplusplus
 }

@@ -49,7 +49,7 @@ def _both(dev, fn):
 
 
 @pytest.mark.parametrize("mode", ["MOL", "RAW"])
-@pytest.mark.parametrize("T,batched,target,overlap", [(8, False, 0, 0), (24, True, 1000, 100), (120, True, 1000, 100)])
+@pytest.mark.parametrize("T,batched,target,overlap", [(24, False, 0, 0), (24, True, 1000, 100), (120, True, 1000, 100)])
 def test_loop_is_bit_identical(cuda_device, sd, mode, T, batched, target, overlap):
     if mode == "RAW":
         sd = dict(sd)
