@@ -253,6 +253,21 @@ __device__ __forceinline__ void amax_update(unsigned* w, float v) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// One BatchNorm statistics partial (S = column sum of its n rows, Q = sum of squares about its own
+// mean S / n; gemm.hip bn_tile_stats) folded into fp64 accumulators about the common shift K:
+// s += S, a1 += n (m - K), a2 += Q + n (m - K)^2.  Then mean = s / count and
+// var = a2 / count - (a1 / count)^2 -- exact for any K, and with K = the first partial's mean the
+// subtraction cancels nothing that fp32 rounding put there.  Shared by bn_finalize_kernel and the
+// fused BN epilogue (contraction off: both form the same bits).
+__device__ __forceinline__ void bn_combine(float S, float Q, long n, double K, double& s, double& a1, double& a2) {
+#pragma clang fp contract(off)
+  const double dn = (double)n;
+  const double dm = (double)S / dn - K;
+  s += (double)S;
+  a1 += dn * dm;
+  a2 += (double)Q + dn * dm * dm;
+}
 // Gate nonlinearities of the recurrences' step epilogues (the dependent chain of every time step):
 // hardware exp (v_exp_f32) and reciprocal (v_rcp_f32), ~1e-7 relative of the libm forms, a few
 // instructions instead of ~30 each.  tanh(x) = 2 sigmoid(2x) - 1 (saturates to +-1 correctly).

@@ -108,9 +108,10 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
     }
   }
   float* stats = nullptr;
-  int nparts = 0;
+  int nparts = 0, part_rows = 0;
   if (training) {
     const int bm = gemm_stats_rows(T * B, cout);
+    part_rows = bm;
     nparts = (T * B + bm - 1) / bm;
     AVC_TAKE(st, float, (size_t)nparts * 2 * cout, sc);
     stats = st;
@@ -140,7 +141,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
     return AVC_OK;
   }
   AVC_TRY(gemm_run(ctx, g, s));
-  AVC_TRY(bn_finalize(cout, nparts, stats, (double)T * B, training, momentum, eps, running_mean,
+  AVC_TRY(bn_finalize(cout, nparts, part_rows, stats, (double)T * B, training, momentum, eps, running_mean,
                       running_var, mean, invstd, s, out_amax));
   AVC_TRY(bn_apply((long)T * B, cout, y_pre, mean, invstd, gamma, beta, act, residual, out, s, out_frag,
                    flags ? flags + 1 : nullptr, out_amax));

@@ -5,7 +5,7 @@
 namespace avc {
 
 // amax_init != NULL: also set amax_init[0] = 0, amax_init[1] = 2^14 (bn_apply's amax_out words)
-int bn_finalize(int C, int nparts, const float* stats, double count, int training, float momentum,
+int bn_finalize(int C, int nparts, int part_rows, const float* stats, double count, int training, float momentum,
                 float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s,
                 unsigned* amax_init = nullptr);
 // frag != NULL: also write the output split into the GEMM's fragment-major A layout

@@ -96,34 +96,39 @@ void colsum_geometry(int M, int N, int& R, int& rows_per) {
 
 // ---- BatchNorm ---------------------------------------------------------------------------
 // 64 channels per block; the 4 waves split the partial-sum slabs, combine in fp64 through LDS.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, const float* __restrict__ stats,
+__global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int part_rows, const float* __restrict__ stats,
                                                           double count, int training, float momentum,
                                                           float eps, float* __restrict__ rmean,
                                                           float* __restrict__ rvar,
                                                           float* __restrict__ mean_out,
                                                           float* __restrict__ invstd_out,
                                                           unsigned* __restrict__ amax_init) {
-  __shared__ double red[2][4][64];
+  __shared__ double red[3][4][64];
   if (amax_init && blockIdx.x == 0 && threadIdx.x < 2) amax_init[threadIdx.x] = threadIdx.x ? 0x46800000u : 0u;
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   if (training) {
-    double s = 0.0, s2 = 0.0;
+    // partial p covers rows [p * part_rows, min(M, (p + 1) * part_rows)) (gemm.hip bn_tile_stats)
+    const long M = (long)count;
+    double s = 0.0, a1 = 0.0, a2 = 0.0;
     if (c < C) {
+      const double K = (double)stats[c] / (double)min((long)part_rows, M);
 #pragma unroll 4
-      for (int p = grp; p < nparts; p += 4) {
-        s += stats[((long)p * 2 + 0) * C + c];
-        s2 += stats[((long)p * 2 + 1) * C + c];
-      }
+      for (int p = grp; p < nparts; p += 4)
+        bn_combine(stats[((long)p * 2 + 0) * C + c], stats[((long)p * 2 + 1) * C + c],
+                   min((long)part_rows, M - (long)p * part_rows), K, s, a1, a2);
     }
     red[0][grp][cl] = s;
-    red[1][grp][cl] = s2;
+    red[1][grp][cl] = a1;
+    red[2][grp][cl] = a2;
     __syncthreads();
     if (grp != 0 || c >= C) return;
     s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-    s2 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+    a1 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+    a2 = red[2][0][cl] + red[2][1][cl] + red[2][2][cl] + red[2][3][cl];
     const double mean = s / count;
-    double var = s2 / count - mean * mean;
+    const double e1 = a1 / count;
+    double var = a2 / count - e1 * e1;
     if (var < 0.0) var = 0.0;
     mean_out[c] = (float)mean;
     invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
@@ -1214,10 +1219,10 @@ int colsum(avc_context* ctx, int M, int N, const float* X, long ld, float* out, 
   return AVC_OK;
 }
 
-int bn_finalize(int C, int nparts, const float* stats, double count, int training, float momentum,
+int bn_finalize(int C, int nparts, int part_rows, const float* stats, double count, int training, float momentum,
                 float eps, float* rmean, float* rvar, float* mean, float* invstd, hipStream_t s,
                 unsigned* amax_init) {
-  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, s>>>(C, nparts, stats, count, training, momentum,
+  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, s>>>(C, nparts, part_rows, stats, count, training, momentum,
                                                    eps, rmean, rvar, mean, invstd, amax_init);
   AVC_LAUNCH_CHECK();
   return AVC_OK;

@@ -108,6 +108,102 @@ __device__ __forceinline__ float split_unscale(const unsigned* amax_a, const uns
   return 1.f / (split_scale_of(amax_a) * split_scale_of(amax_b));
 }
 
+// BatchNorm column partials of one output tile (train mode).  Per column and partial (PARTS = 1:
+// the tile's rows; 2: the two 128-row halves of a 256-row tile, make_plan's stats granularity):
+// stats[part][0][col] = S, the sum of the column's valid rows, and stats[part][1][col] = the sum
+// of squares about the partial's own mean S / n, from a second pass over the same values.  So the
+// variance never comes out of E[x^2] - E[x]^2 with fp32 sums: at B = 1 a decoder conv channel's
+// mean is ~17 standard deviations, and that difference cost ~2^-12 relative in the variance
+// (dec.conv0 5.9e-5 local error against fp32 CPU's 6.9e-6); bn_finalize_kernel combines
+// the partials in fp64 about a common shift.  val(i, j, e) = act(acc + bias) as the epilogue
+// stored it (RAW: acc already holds it).  Every producer (the three GEMM epilogues, the fused BN
+// one) goes through here, so fused and unfused chains form the same bits.  SC1: write-through
+// stores (the fused BN's in-launch hand-off).  red: >= (WM + PARTS) * BN floats of LDS, free.
+template <int BM, int BN, int WM, int WTN, int TM, int TN, int PARTS, bool RAW, bool SC1>
+__device__ __forceinline__ void bn_tile_stats(const GemmDesc& d, const f32x16 (&acc)[TM][TN], const float (&bias)[TN],
+                                              float* red, int tm, int tn, int wm, int wn, int lane, int tid, int NT,
+                                              int row_base, int col_base) {
+  static_assert(PARTS == 1 || (BM == 256 && WM % 2 == 0), "two 128-row partials per 256-row tile");
+  constexpr int PR = BM / PARTS, WPP = WM / PARTS;  // rows and wave rows per partial
+  const int M = d.M, N = d.N, act = d.act;
+  float* tmean = red + WM * BN;  // [PARTS][BN]
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc(d.stats, 0, 0x7fffffff, 0x00020000);
+  auto put = [&](long idx, float v) {
+    if (SC1) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), srs, (int)(idx * 4), 0, 16 /*sc1*/);
+    else d.stats[idx] = v;
+  };
+  float cs[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {  // pass 1: the column sums
+    cs[j] = 0.f;
+    const int col = col_base + 32 * j;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+        if (col >= N || row >= M) continue;
+        cs[j] += RAW ? acc[i][j][e] : act_apply(acc[i][j][e] + bias[j], act);
+      }
+  }
+  __syncthreads();  // (the LDS operand ring is dead)
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const float v = cs[j] + __shfl_xor(cs[j], 32);
+    if (lane < 32) red[wm * BN + wn * WTN + 32 * j + lane] = v;
+  }
+  __syncthreads();
+  for (int cl = tid; cl < BN; cl += NT) {
+    const int col = tn * BN + cl;
+    if (col >= N) continue;
+#pragma unroll
+    for (int sp = 0; sp < PARTS; ++sp) {
+      const long part = (long)tm * PARTS + sp;
+      if (part * PR >= M) break;
+      float v = 0.f;
+#pragma unroll
+      for (int r = sp * WPP; r < (sp + 1) * WPP; ++r) v += red[r * BN + cl];
+      put((part * 2 + 0) * N + col, v);
+      tmean[sp * BN + cl] = v / (float)min((long)PR, (long)M - part * PR);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {  // pass 2: squares about the partial's mean
+    const int col = col_base + 32 * j;
+    const float m = tmean[(wm / WPP) * BN + wn * WTN + 32 * j + (lane & 31)];
+    cs[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+        if (col >= N || row >= M) continue;
+        const float dv = (RAW ? acc[i][j][e] : act_apply(acc[i][j][e] + bias[j], act)) - m;
+        cs[j] = fmaf(dv, dv, cs[j]);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const float v = cs[j] + __shfl_xor(cs[j], 32);
+    if (lane < 32) red[wm * BN + wn * WTN + 32 * j + lane] = v;  // (pass 1's reads are behind the barrier)
+  }
+  __syncthreads();
+  for (int cl = tid; cl < BN; cl += NT) {
+    const int col = tn * BN + cl;
+    if (col >= N) continue;
+#pragma unroll
+    for (int sp = 0; sp < PARTS; ++sp) {
+      const long part = (long)tm * PARTS + sp;
+      if (part * PR >= M) break;
+      float v = 0.f;
+#pragma unroll
+      for (int r = sp * WPP; r < (sp + 1) * WPP; ++r) v += red[r * BN + cl];
+      put((part * 2 + 1) * N + col, v);
+    }
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int AT, int BT>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tilesM, int tilesN,
                                                             int kt_per_tap, int kps, int nsplit,
@@ -296,11 +392,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
   }
 
   float* __restrict__ C = d.C + (long)z * d.c_zoff;
-  float csum[TN], csq[TN];
+  float biasv[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    csum[j] = 0.f;
-    csq[j] = 0.f;
     const int col = col_base + 32 * j;
     const bool colok = col < d.N;
     float bias = 0.f;
@@ -308,6 +402,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
       if (d.bias0) bias += d.bias0[col];
       if (d.bias1) bias += d.bias1[col];
     }
+    biasv[j] = bias;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -317,39 +412,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
         const float v = act_apply(acc[i][j][e] + bias, d.act);
         float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
         if (d.accumulate) *p += v; else *p = v;
-        csum[j] += v;
-        csq[j] = fmaf(v, v, csq[j]);  // explicit: every epilogue (and the fused BN one) forms the same bits
       }
   }
 
-  if (d.stats) {
-    __syncthreads();  // LDS operand tiles are dead now; reuse them for the column reduction
-    float* red = lds;  // [WM][2 (sum,sq)][BN]
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float s = csum[j] + __shfl_xor(csum[j], 32);
-      float s2 = csq[j] + __shfl_xor(csq[j], 32);
-      if (lane < 32) {
-        const int cl = wn * WTN + 32 * j + lane;
-        red[(wm * 2 + 0) * BN + cl] = s;
-        red[(wm * 2 + 1) * BN + cl] = s2;
-      }
-    }
-    __syncthreads();
-    for (int cl = tid; cl < BN; cl += NT) {
-      const int col = tn * BN + cl;
-      if (col < d.N) {
-        float s = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int r = 0; r < WM; ++r) {
-          s += red[(r * 2 + 0) * BN + cl];
-          s2 += red[(r * 2 + 1) * BN + cl];
-        }
-        d.stats[((long)tm * 2 + 0) * d.N + col] = s;
-        d.stats[((long)tm * 2 + 1) * d.N + col] = s2;
-      }
-    }
-  }
+  if (d.stats)  // (the LDS operand tiles are dead now: the column reduction reuses them)
+    bn_tile_stats<BM, BN, WM, WTN, TM, TN, 1, false, false>(d, acc, biasv, lds, tm, tn, wm, wn, lane, tid, NT,
+                                                            row_base, col_base);
 }
 
 // ---- split-fp16 ("3xf16") GEMM for forward products ------------------------------------
@@ -565,11 +633,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
     return;
   }
   float* __restrict__ C = d.C + (long)z * d.c_zoff;
-  float csum[TN], csq[TN];
+  float biasv[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    csum[j] = 0.f;
-    csq[j] = 0.f;
     const int col = col_base + 32 * j;
     const bool colok = col < d.N;
     float bias = 0.f;
@@ -577,6 +643,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
       if (d.bias0) bias += d.bias0[col];
       if (d.bias1) bias += d.bias1[col];
     }
+    biasv[j] = bias;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -586,38 +653,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
         const float v = act_apply(acc[i][j][e] + bias, d.act);
         float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
         if (d.accumulate) *p += v; else *p = v;
-        csum[j] += v;
-        csq[j] = fmaf(v, v, csq[j]);  // explicit: every epilogue (and the fused BN one) forms the same bits
       }
   }
-  if (d.stats) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float s = csum[j] + __shfl_xor(csum[j], 32);
-      const float s2 = csq[j] + __shfl_xor(csq[j], 32);
-      if (lane < 32) {
-        const int cl = wn * WTN + 32 * j + lane;
-        red[(wm * 2 + 0) * BN + cl] = s;
-        red[(wm * 2 + 1) * BN + cl] = s2;
-      }
-    }
-    __syncthreads();
-    for (int cl = tid; cl < BN; cl += NT) {
-      const int col = tn * BN + cl;
-      if (col < d.N) {
-        float s = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int r = 0; r < WM; ++r) {
-          s += red[(r * 2 + 0) * BN + cl];
-          s2 += red[(r * 2 + 1) * BN + cl];
-        }
-        d.stats[((long)tm * 2 + 0) * d.N + col] = s;
-        d.stats[((long)tm * 2 + 1) * d.N + col] = s2;
-      }
-    }
-  }
+  if (d.stats)
+    bn_tile_stats<BM, BN, WM, WTN, TM, TN, 1, false, false>(d, acc, biasv, reinterpret_cast<float*>(lds), tm, tn, wm,
+                                                            wn, lane, tid, NT, row_base, col_base);
 }
 
 // ---- split-f16 GEMM on pre-split fragment-major operands ("gemm16f") ---------------------
@@ -764,49 +804,12 @@ inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* 
   }
 }
 
-// The same stats partials from a 256-row tile: two per tile (the 128-row granularity make_plan
-// reports), each the sum of the WM / 2 waves whose rows it covers.
-template <int BM, int BN, int WM, int WTN, int TN>
-__device__ __forceinline__ void stats_256(const GemmDesc& d, unsigned char* lds, const float* csum, const float* csq,
-                                          int tm, int tn, int wm, int wn, int lane, int tid, int NT) {
-  static_assert(BM == 256 && WM % 2 == 0, "two 128-row partials per tile");
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const float s = csum[j] + __shfl_xor(csum[j], 32);
-    const float s2 = csq[j] + __shfl_xor(csq[j], 32);
-    if (lane < 32) {
-      const int cl = wn * WTN + 32 * j + lane;
-      red[(wm * 2 + 0) * BN + cl] = s;
-      red[(wm * 2 + 1) * BN + cl] = s2;
-    }
-  }
-  __syncthreads();
-  for (int cl = tid; cl < BN; cl += NT) {
-    const int col = tn * BN + cl;
-    if (col >= d.N) continue;
-#pragma unroll
-    for (int sp = 0; sp < 2; ++sp) {
-      if ((tm * 2L + sp) * 128 >= d.M) break;
-      float s = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int r = sp * (WM / 2); r < (sp + 1) * (WM / 2); ++r) {
-        s += red[(r * 2 + 0) * BN + cl];
-        s2 += red[(r * 2 + 1) * BN + cl];
-      }
-      d.stats[((tm * 2L + sp) * 2 + 0) * d.N + col] = s;
-      d.stats[((tm * 2L + sp) * 2 + 1) * d.N + col] = s2;
-    }
-  }
-}
-
 // Fused BatchNorm epilogue of gemm16f (GemmDesc::bnf, see gemm.h).  Every expression that forms a
 // value is the one the unfused chain uses (this kernel's epilogue for y and the column partials,
 // bn_finalize_kernel for mean / invstd and the running statistics, bn_apply(_frag) for the
 // output and its split), in the same order, so both chains give the same bits.
-// LDS (bytes): [0, 8K) column partials [WM][2][BN] f32; [8K, 16K) fp64 sums [2][4][BN];
-// [16K, 17K) scale / shift [2][BN]; 17K flag; [18K, ..) the tile [BM][BN + 4] f32.
+// LDS (bytes): [0, 8K) column partials [WM + 1][BN] f32; [8K, 20K) fp64 sums [3][4][BN];
+// [20K, 21K) scale / shift [2][BN]; 21K flag; [22K, ..) the tile [BM][BN + 4] f32.
 template <int BM, int BN, int WM, int WTN, int TM, int TN, int NT>
 __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM][TN], unsigned char* lds, int tm,
                                              int tn, int tilesM, int wm, int lane, int tid, int row_base,
@@ -815,19 +818,15 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
   const BnFuse& bf = d.bnf;
   float* red = reinterpret_cast<float*>(lds);
   double* dred = reinterpret_cast<double*>(lds + 8192);
-  float* s_sc = reinterpret_cast<float*>(lds + 16384);
+  float* s_sc = reinterpret_cast<float*>(lds + 20480);
   float* s_sh = s_sc + BN;
-  int* flag = reinterpret_cast<int*>(lds + 17408);
-  float* tile = reinterpret_cast<float*>(lds + 18432);
+  int* flag = reinterpret_cast<int*>(lds + 21504);
+  float* tile = reinterpret_cast<float*>(lds + 22528);
   constexpr int TP = BN + 4;
   const int wn = (col_base - tn * BN - (lane & 31)) / WTN;
-  // (1) y = A.B + bias, kept in registers (stored only where the caller keeps y_pre), and this
-  // tile's column partials, exactly as the unfused epilogue forms them
-  float csum[TN], csq[TN];
+  // (1) y = A.B + bias, kept in registers (stored only where the caller keeps y_pre)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    csum[j] = 0.f;
-    csq[j] = 0.f;
     const int col = col_base + 32 * j;
     const bool colok = col < d.N;
     float bias = 0.f;
@@ -844,42 +843,16 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
         const float v = act_apply(acc[i][j][e] + bias, d.act);
         acc[i][j][e] = v;
         if (d.C) d.C[(long)row * d.ldc + col] = v;
-        csum[j] += v;
-        csq[j] = fmaf(v, v, csq[j]);  // explicit: every epilogue (and the fused BN one) forms the same bits
       }
   }
-  __syncthreads();  // every wave is done with the LDS ring
   bool ok = true;
   if (bf.training) {
-    // (2) the column partials of this tile (fixed-order sum over the WM wave rows), stored
-    // write-through, drained, then this workgroup counts itself in on its column tile
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float s = csum[j] + __shfl_xor(csum[j], 32);
-      const float s2 = csq[j] + __shfl_xor(csq[j], 32);
-      if (lane < 32) {
-        const int cl = wn * WTN + 32 * j + lane;
-        red[(wm * 2 + 0) * BN + cl] = s;
-        red[(wm * 2 + 1) * BN + cl] = s2;
-      }
-    }
-    __syncthreads();
-    const auto srs = __builtin_amdgcn_make_buffer_rsrc(d.stats, 0, tilesM * 2 * d.N * 4, 0x00020000);
-    for (int cl = tid; cl < BN; cl += NT) {
-      const int col = tn * BN + cl;
-      if (col < d.N) {
-        float s = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int r = 0; r < WM; ++r) {
-          s += red[(r * 2 + 0) * BN + cl];
-          s2 += red[(r * 2 + 1) * BN + cl];
-        }
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), srs, ((tm * 2 + 0) * d.N + col) * 4, 0,
-                                              16 /*sc1*/);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s2), srs, ((tm * 2 + 1) * d.N + col) * 4, 0,
-                                              16 /*sc1*/);
-      }
-    }
+    // (2) this tile's column partials exactly as the unfused epilogue forms them (bn_tile_stats),
+    // stored write-through, drained, then this workgroup counts itself in on its column tile
+    const float nob[TN] = {};
+    const int wm_ = wm, wn_ = wn;
+    bn_tile_stats<BM, BN, WM, WTN, TM, TN, 1, true, true>(d, acc, nob, red, tm, tn, wm_, wn_, lane, tid, NT, row_base,
+                                                          col_base);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -889,21 +862,27 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
     }
     __syncthreads();
     ok = flag[0] != 0;
-    // (3) this workgroup's columns' sums over every tile, in bn_finalize_kernel's order (4 thread
-    // groups over the partial rows p = grp, grp + 4, ..., then the 4 group sums left to right)
+    // (3) this workgroup's columns' partials over every tile, combined in bn_finalize_kernel's
+    // order (4 thread groups over the partial rows p = grp, grp + 4, ..., then the 4 group sums
+    // left to right) and form (bn_combine)
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc(d.stats, 0, tilesM * 2 * d.N * 4, 0x00020000);
     const int grp = tid / BN, cl = tid - grp * BN, col = tn * BN + cl;
     // (4 rows of loads in flight per thread: a variant that requested all 16 rows of a thread
     // before its first add measured 0.08 ms slower per C2 forward)
-    double s = 0.0, s2 = 0.0;
+    double s = 0.0, a1 = 0.0, a2 = 0.0;
     if (col < d.N) {
+      const double K = (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, col * 4, 0, 16)) /
+                       (double)min(BM, d.M);
 #pragma unroll 4
       for (int p = grp; p < tilesM; p += 4) {
-        s += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 0) * d.N + col) * 4, 0, 16));
-        s2 += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 1) * d.N + col) * 4, 0, 16));
+        const float S = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 0) * d.N + col) * 4, 0, 16));
+        const float Q = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 1) * d.N + col) * 4, 0, 16));
+        bn_combine(S, Q, min(BM, d.M - p * BM), K, s, a1, a2);
       }
     }
     dred[(0 * 4 + grp) * BN + cl] = s;
-    dred[(1 * 4 + grp) * BN + cl] = s2;
+    dred[(1 * 4 + grp) * BN + cl] = a1;
+    dred[(2 * 4 + grp) * BN + cl] = a2;
     __syncthreads();
   }
   // (4) per-column scale and shift (bn_finalize_kernel, then bn_apply's sc / sh)
@@ -913,9 +892,11 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
       float mf, isf;
       if (bf.training) {
         const double s = dred[0 * BN + tid] + dred[1 * BN + tid] + dred[2 * BN + tid] + dred[3 * BN + tid];
-        const double s2 = dred[4 * BN + tid] + dred[5 * BN + tid] + dred[6 * BN + tid] + dred[7 * BN + tid];
+        const double a1 = dred[4 * BN + tid] + dred[5 * BN + tid] + dred[6 * BN + tid] + dred[7 * BN + tid];
+        const double a2 = dred[8 * BN + tid] + dred[9 * BN + tid] + dred[10 * BN + tid] + dred[11 * BN + tid];
         const double mean = s / bf.count;
-        double var = s2 / bf.count - mean * mean;
+        const double e1 = a1 / bf.count;
+        double var = a2 / bf.count - e1 * e1;
         if (var < 0.0) var = 0.0;
         mf = (float)mean;
         isf = (float)(1.0 / sqrt(var + (double)bf.eps));
@@ -1310,11 +1291,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
     return;
   }
   float* __restrict__ C = d.C + (long)z * d.c_zoff;
-  float csum[TN], csq[TN];
+  float biasv[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    csum[j] = 0.f;
-    csq[j] = 0.f;
     const int col = col_base + 32 * j;
     const bool colok = col < d.N;
     float bias = 0.f;
@@ -1322,6 +1301,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
       if (d.bias0) bias += d.bias0[col];
       if (d.bias1) bias += d.bias1[col];
     }
+    biasv[j] = bias;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1331,40 +1311,11 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
         const float v = act_apply(acc[i][j][e] + bias, d.act);
         float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
         if (d.accumulate) *p += v; else *p = v;
-        csum[j] += v;
-        csq[j] = fmaf(v, v, csq[j]);  // explicit: every epilogue (and the fused BN one) forms the same bits
       }
   }
-  if constexpr (BM == 256) {
-    if (d.stats) stats_256<BM, BN, WM, WTN, TN>(d, lds, csum, csq, tm, tn, wm, wn, lane, tid, NT);
-  } else if (d.stats) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(lds);  // [WM][2][BN]
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float s = csum[j] + __shfl_xor(csum[j], 32);
-      const float s2 = csq[j] + __shfl_xor(csq[j], 32);
-      if (lane < 32) {
-        const int cl = wn * WTN + 32 * j + lane;
-        red[(wm * 2 + 0) * BN + cl] = s;
-        red[(wm * 2 + 1) * BN + cl] = s2;
-      }
-    }
-    __syncthreads();
-    for (int cl = tid; cl < BN; cl += NT) {
-      const int col = tn * BN + cl;
-      if (col < d.N) {
-        float s = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int r = 0; r < WM; ++r) {
-          s += red[(r * 2 + 0) * BN + cl];
-          s2 += red[(r * 2 + 1) * BN + cl];
-        }
-        d.stats[((long)tm * 2 + 0) * d.N + col] = s;
-        d.stats[((long)tm * 2 + 1) * d.N + col] = s2;
-      }
-    }
-  }
+  if (d.stats)
+    bn_tile_stats<BM, BN, WM, WTN, TM, TN, BM == 256 ? 2 : 1, false, false>(
+        d, acc, biasv, reinterpret_cast<float*>(lds), tm, tn, wm, wn, lane, tid, NT, row_base, col_base);
 }
 
 // splitk_reduce_kernel for the common case (one product, row-major C, N % 4 == 0): a thread sums
