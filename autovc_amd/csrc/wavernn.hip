@@ -431,32 +431,46 @@ __device__ __forceinline__ float uniform_draw(unsigned long long seed, int r, in
   return __fadd_rn(1e-5f, __fmul_rn(0.99998f, u));
 }
 
-// the sample of fold row r at step i from its logits lg (model.py:279-315, distribution.py:87-123);
-// teacher-forced calls store the logits and return the given sample.  Shared by the per-step
-// kernel and the persistent loop (contraction off).
-__device__ __forceinline__ float wr_sample(const WrStep& a, int r, int i, const float* lg) {
+// The sample of fold row r at step i from its logits lg (model.py:279-315, distribution.py:87-123),
+// called by every thread of the workgroup; thread 0 returns it.  Teacher-forced calls store the
+// logits and return the given sample.  MOL: lanes k < nr form the Gumbel-perturbed mixture logits
+// and lane nr the logistic draw's log-odds side by side (LDS tk[0..nr]); thread 0 then takes the
+// first maximum (torch.max) and forms the sample -- each value by the expression the serial form
+// used, so the bits are unchanged.  Shared by the per-step kernel and the persistent loop
+// (contraction off).  tk: >= 32 floats of LDS.
+__device__ __forceinline__ float wr_sample(const WrStep& a, int r, int i, const float* lg, float* tk) {
 #pragma clang fp contract(off)
-  const int NC = a.NC;
+  const int NC = a.NC, tid = threadIdx.x;
   const long o = (long)r * a.L + i;
-  float x;
+  float x = 0.f;
   if (a.teacher) {
-    for (int c = 0; c < NC; ++c) a.logits[o * NC + c] = lg[c];
-    x = a.x_tf[o];  // (unused by the next step, which reads x_tf itself)
+    if (tid == 0) {
+      for (int c = 0; c < NC; ++c) a.logits[o * NC + c] = lg[c];
+      x = a.x_tf[o];  // (unused by the next step, which reads x_tf itself)
+    }
   } else if (a.mol) {
     const int nr = NC / 3;
-    int best = 0;
-    float bv = 0.f;
-    for (int k = 0; k < nr; ++k) {  // Gumbel-max mixture choice; first maximum wins (torch.max)
-      const float u = uniform_draw(a.seed, r, i, k);
-      const float t = lg[k] - logf(-logf(u));
-      if (k == 0 || t > bv) { bv = t; best = k; }
+    if (tid < nr) {
+      const float u = uniform_draw(a.seed, r, i, tid);
+      tk[tid] = lg[tid] - logf(-logf(u));
+    } else if (tid == nr) {
+      const float u = uniform_draw(a.seed, r, i, nr);
+      tk[nr] = logf(u) - logf(1.0f - u);
     }
-    const float mean = lg[nr + best];
-    const float ls = fmaxf(lg[2 * nr + best], -32.236191301916641f);  // log(1e-14)
-    const float u = uniform_draw(a.seed, r, i, nr);
-    x = mean + expf(ls) * (logf(u) - logf(1.0f - u));
-    x = fminf(fmaxf(x, -1.f), 1.f);
-  } else {  // RAW: Categorical(softmax) by inverse CDF, 2k / (n_classes - 1) - 1
+    __syncthreads();
+    if (tid == 0) {
+      int best = 0;
+      float bv = 0.f;
+      for (int k = 0; k < nr; ++k) {  // Gumbel-max mixture choice; first maximum wins (torch.max)
+        const float t = tk[k];
+        if (k == 0 || t > bv) { bv = t; best = k; }
+      }
+      const float mean = lg[nr + best];
+      const float ls = fmaxf(lg[2 * nr + best], -32.236191301916641f);  // log(1e-14)
+      x = mean + expf(ls) * tk[nr];
+      x = fminf(fmaxf(x, -1.f), 1.f);
+    }
+  } else if (tid == 0) {  // RAW: Categorical(softmax) by inverse CDF, 2k / (n_classes - 1) - 1
     float mx = lg[0];
     for (int c = 1; c < NC; ++c) mx = fmaxf(mx, lg[c]);
     float sum = 0.f;  // (each exp is formed twice, the same bits both times: no indexed array)
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(256) void wr_out_kernel(WrStep a) {
   const int i = cur_step(a);
   if (i >= a.L) return;
   __shared__ float red[4 * 8 * kRP];
-  __shared__ float lg[64];
+  __shared__ float lg[64];  // [0, 32) logits, [32, 64) wr_sample's tk
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = blockIdx.x, Fc = a.Fc, NC = a.NC;
   float4 yv[kJ4];
@@ -513,9 +527,9 @@ __global__ __launch_bounds__(256) void wr_out_kernel(WrStep a) {
     }
   }
   __syncthreads();
+  const float x = wr_sample(a, r, i, lg, lg + 32);
   if (tid == 0) {
     const long o = (long)r * a.L + i;
-    const float x = wr_sample(a, r, i, lg);
     a.out[o] = x;
     a.x_prev[r] = x;
     if (atomicAdd(a.done, 1) == a.R - 1) {  // every workgroup has read this step: advance it
@@ -930,8 +944,8 @@ __device__ __forceinline__ bool out_phase(const WrLoop& p, int r, int i, unsigne
     }
   }
   __syncthreads();
+  const float x = wr_sample(a, r, i, lg, lg + 32);
   if (tid == 0) {
-    const float x = wr_sample(a, r, i, lg);
     a.out[(long)r * a.L + i] = x;
     st_sc1(a.x_prev, r, x);
   }
