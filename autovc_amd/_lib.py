@@ -110,7 +110,6 @@ _SIGS = {
     "avc_wavernn_param_count": [_I],
     "avc_wavernn_persist": [_I],
     "avc_wavernn_persist_eligible": [_I, _I, _I],
-    "avc_wavernn_loop_counters": [_I],
     "avc_debug_wavernn_inject": [_I],
     "avc_debug_wavernn_stamps": [_P, _I],
     "avc_wavernn_upsample": [_P, _P, _I, _P, _P, _P, _P, _P],

@@ -598,8 +598,7 @@ struct WrLoop {
   unsigned long long* tickets;    // one per workgroup per launch
   unsigned* fail_host;            // the context's pinned failure word
   unsigned spin_limit;
-  int groups;                     // counter form: 0 = 8 replicas per stage, 1 = 8 group counters
-  unsigned long long* stamps;     // diagnostics (avc_debug_wavernn_stamps): [G][nstamp][24] realtime
+  unsigned long long* stamps;     // diagnostics (avc_debug_wavernn_stamps): [G][nstamp][16] realtime
   int nstamp;                     // steps stamped
 };
 
@@ -632,44 +631,6 @@ __device__ __forceinline__ unsigned wr_target(const WrLoop& p, int S, int i, uns
   return ((E - 1u) * nk + (unsigned)(i / kWrRing) + 1u) * P;
 }
 
-// Producers of stage S in counter group g (workgroups w of the stage's range with w % 8 == g)
-__device__ __forceinline__ unsigned wr_group_producers(const WrLoop& p, int S, int g) {
-  const int lo = S <= S_GRU2 ? 0 : S == S_FC1 ? 0 : S == S_FC2 ? p.nfc : 2 * p.nfc;
-  const int hi = S <= S_GRU2 ? p.G : S == S_FC1 ? p.nfc : S == S_FC2 ? 2 * p.nfc : 2 * p.nfc + p.a.R;
-  return (unsigned)((hi + 7 - g) / 8 - (lo + 7 - g) / 8);
-}
-
-// Group-counter form (p.groups): producer w adds to the line of group w % 8 only, so each line
-// takes at most G / 8 arrivals instead of every producer's (MI355X_MICROARCH.md 'fanin': ~12 ns
-// per serialised atomic, 256 arrivals ~3 us); wave 0's lanes 0..7 poll the 8 group lines side by
-// side and the wait ends when every group has reached its share.  Groups are logical (w % 8, the
-// XCD under round-robin placement): placement changes speed, never the result.
-__device__ __forceinline__ bool wr_poll_groups(const WrLoop& p, int S, int i, unsigned E) {
-  const int lane = threadIdx.x & 63, g = lane & 7;
-  const int k = i % kWrRing;
-  const unsigned nk = (unsigned)((p.a.L - k + kWrRing - 1) / kWrRing);
-  const unsigned target = ((E - 1u) * nk + (unsigned)(i / kWrRing) + 1u) * wr_group_producers(p, S, g);
-  wr_gu32* c = (wr_gu32*)(p.cnt + wr_cidx(S, i, g));
-  wr_gu32* t = (wr_gu32*)p.tmo;
-  for (unsigned spins = 0;; ++spins) {
-    const bool ok = lane >= 8 || (int)(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0;
-    if (__all(ok)) return true;
-    if ((spins & 63) == 63 && __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E) return false;
-    if (spins >= p.spin_limit) {
-      if (lane == 0) {
-        const unsigned old = __hip_atomic_fetch_max(t, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old != E) {
-          const unsigned n = atomicAdd(&g_wr_giveups, 1u) + 1u;
-          if (p.fail_host)
-            __hip_atomic_store(p.fail_host, 0x40000000u | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
 // One lane waits for stage S of step i (wrap-safe relaxed agent-scope polls of its replica);
 // false = gave up, or another workgroup of this launch did (the give-up word, every 64 polls).
 __device__ __forceinline__ bool wr_poll(const WrLoop& p, int S, int i, unsigned E) {
@@ -696,10 +657,8 @@ __device__ __forceinline__ bool wr_poll(const WrLoop& p, int S, int i, unsigned 
 // so a word is rewritten only after barriers every reader has passed)
 __device__ __forceinline__ bool wr_wait(const WrLoop& p, int S, int i, unsigned E, int* flags, int& nw) {
   int* f = flags + (nw++ & 3);
-  bool r = false;
-  if (threadIdx.x < 64) r = p.groups ? wr_poll_groups(p, S, i, E) : (threadIdx.x == 0 && wr_poll(p, S, i, E));
   if (threadIdx.x == 0) {
-    *f = r ? 1 : 0;
+    *f = wr_poll(p, S, i, E) ? 1 : 0;
     // diagnostics: when the wait ended (slot 3 op + 1 of the loop step; flags[6] / [7] = op, step)
     if (p.stamps && flags[7] >= 0 && flags[7] < p.nstamp)
       p.stamps[((long)blockIdx.x * p.nstamp + flags[7]) * 24 + 3 * flags[6] + 1] = __builtin_amdgcn_s_memrealtime();
@@ -708,14 +667,13 @@ __device__ __forceinline__ bool wr_wait(const WrLoop& p, int S, int i, unsigned 
   return *f != 0;
 }
 
-// every storing wave drains its sc1 stores, barrier, then one 8-lane add to the stage's replicas
-// (or one add to the workgroup's group counter)
+// every storing wave drains its sc1 stores, barrier, one 8-lane add to the stage's replicas
 __device__ __forceinline__ void wr_publish(const WrLoop& p, int S, int i) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (p.groups ? threadIdx.x == 0 : threadIdx.x < kWrRep)
-    __hip_atomic_fetch_add((wr_gu32*)(p.cnt + wr_cidx(S, i, p.groups ? (int)(blockIdx.x % kWrRep) : (int)threadIdx.x)),
-                           1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < kWrRep)
+    __hip_atomic_fetch_add((wr_gu32*)(p.cnt + wr_cidx(S, i, threadIdx.x)), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Loop staging of rows [rb, rb + kRC) of input `which` (stage_load's layout and values): _pre
@@ -1072,7 +1030,6 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
 
 int g_wr_persist = 0;  // avc_wavernn_persist(): 1 = the persistent sample loop where eligible
 int g_wr_inject = 0;   // avc_debug_wavernn_inject(): loop launches left that give up at once
-int g_wr_groups = 0;   // avc_wavernn_loop_counters(): 0 = replicated counters, 1 = group counters
 unsigned long long* g_wr_stamps = nullptr;  // avc_debug_wavernn_stamps(): next loop launch's stamps
 int g_wr_nstamp = 0;
 
@@ -1118,7 +1075,6 @@ int wr_loop_run(avc_context* ctx, const WrStep& a, hipStream_t s, double macs) {
   p.fail_host = host_flags(ctx);
   if (!p.fail_host) return AVC_ERR_HIP;
   p.spin_limit = coresident_spin_limit();
-  p.groups = g_wr_groups;
   if (g_wr_inject > 0) {  // test hook: this launch gives up at its first unmet poll
     --g_wr_inject;
     p.spin_limit = 0;
@@ -1414,12 +1370,6 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
 int avc_wavernn_persist(int on) {
   AVC_CHECK_ARG(on == 0 || on == 1, "avc_wavernn_persist: on must be 0 or 1");
   avc::g_wr_persist = on;
-  return AVC_OK;
-}
-
-int avc_wavernn_loop_counters(int form) {
-  AVC_CHECK_ARG(form == 0 || form == 1, "avc_wavernn_loop_counters: form must be 0 (replicas) or 1 (groups)");
-  avc::g_wr_groups = form;
   return AVC_OK;
 }
 

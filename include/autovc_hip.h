@@ -470,10 +470,6 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
  * its remaining samples as NaN and the call fails with AVC_ERR_DEVICE. */
 int avc_wavernn_persist(int on);
 int avc_wavernn_persist_eligible(int rows, int rnn_dims, int fc_dims);
-/* Tuning hook for the persistent loop's arrival counters: 0 (default) = every producer adds to 8
- * replicas of its stage's counter, a consumer polls one; 1 = a producer adds to the counter of its
- * group (workgroup % 8) only and a consumer polls all 8 (fewer serialised atomics per line). */
-int avc_wavernn_loop_counters(int form);
 /* Test hook: the next `launches` loop launches give up at their first unmet wait. */
 int avc_debug_wavernn_inject(int launches);
 /* Diagnostics: the next loop launch stamps its first `steps` steps (s_memrealtime, 100 MHz) into

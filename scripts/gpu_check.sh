@@ -83,7 +83,7 @@ for step in "$@"; do
     prodcurve) run prodcurve 500 python -u -m pytest tests/test_gpu_production.py tests/test_gpu_curve.py -x -v -s --timeout 300 -p no:cacheprovider ;;
     bpttc) run bpttc 300 python -u -m pytest tests/test_gpu_bptt_coalesce.py -x -v -s --timeout 200 -p no:cacheprovider && run bpttcab 300 python scripts/bptt_coalesce_ab.py && run bpttctrain 400 python scripts/train_hook_ab.py avc_bptt_coalesce 0 1 ;;
     wrp) run wrp 400 python -u -m pytest tests/test_gpu_wavernn_persist.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider && run wrpab 300 python scripts/vocoder_ab.py 3 ;;
-    wrstamps) run wrstamps 300 python scripts/vocoder_stamps.py 128 0 && run wrstamps1 300 python scripts/vocoder_stamps.py 128 1 ;;
+    wrstamps) run wrstamps 300 python scripts/vocoder_stamps.py 128 ;;
     bnstat) run bnstat 600 python -u -m pytest tests/test_gpu_bnfuse.py tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_margin.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

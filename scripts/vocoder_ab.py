@@ -1,9 +1,7 @@
 """A/B of the WaveRNN sample loop: per-step graph chunks (avc_wavernn_persist 0) against the
 persistent loop (1), alternating in one process on the bench's 10 s utterance (bench.py --mode
 vocoder: 801 mel frames, batched target 11000 / overlap 550 -> 20 fold rows x 12100 steps).
-Configurations: argv[2:] as persist:counters (default "0:0 1:0 1:1"; counters =
-avc_wavernn_loop_counters).  Prints the median generate() time per configuration and whether
-the waveforms are bit-identical."""
+Prints the median generate() time per mode and whether the waveforms are bit-identical."""
 import sys
 import time
 
@@ -21,29 +19,24 @@ net = WaveRNN(device=dev)
 net.load_state_dict(wavernn_state_dict(0))
 mel = torch.from_numpy(synthetic_mel(31, 1, T)).to(dev)
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-cfgs = [tuple(int(v) for v in c.split(":")) for c in (sys.argv[2:] or ["0:0", "1:0", "1:1"])]
-times, waves = {c: [] for c in cfgs}, {}
+times, waves = {0: [], 1: []}, {}
 for r in range(reps + 1):
-    for c in cfgs:
-        _lib.call("avc_wavernn_persist", c[0])
-        _lib.call("avc_wavernn_loop_counters", c[1])
+    for mode in (0, 1):
+        _lib.call("avc_wavernn_persist", mode)
         torch.manual_seed(7)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         w = net.generate(mel)
         dt = time.perf_counter() - t0
         if r > 0:
-            times[c].append(dt)
-        waves[c] = w
-        print(f"rep {r} persist={c[0]} counters={c[1]}: {1e3 * dt:.1f} ms", flush=True)
+            times[mode].append(dt)
+        waves[mode] = w
+        print(f"rep {r} persist={mode}: {1e3 * dt:.1f} ms", flush=True)
 _lib.call("avc_wavernn_persist", 0)
-_lib.call("avc_wavernn_loop_counters", 0)
 audio_s = (T - 1) * 275 / 22050
-for c in cfgs:
-    med = float(np.median(times[c]))
-    print(f"persist={c[0]} counters={c[1]}: median {1e3 * med:.1f} ms per generate = {audio_s / med:.2f} audio-s/s, "
+for mode in (0, 1):
+    med = float(np.median(times[mode]))
+    print(f"persist={mode}: median {1e3 * med:.1f} ms per generate = {audio_s / med:.2f} audio-s/s, "
           f"{1e6 * med / 12100:.1f} us per sample step")
-w0 = waves[cfgs[0]]
-for c in cfgs[1:]:
-    print(f"waveform {c} bit-identical to {cfgs[0]}:", bool(np.array_equal(w0, waves[c])),
-          "max |d|", float(np.abs(w0 - waves[c]).max()))
+print("waveforms bit-identical:", bool(np.array_equal(waves[0], waves[1])),
+      "max |d|", float(np.abs(waves[0] - waves[1]).max()))

@@ -16,7 +16,6 @@ from autovc_amd.wavernn import WaveRNN  # noqa: E402
 from autovc_amd.weights import synthetic_mel, wavernn_state_dict  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 128
-FORM = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # avc_wavernn_loop_counters
 dev = torch.device("cuda:0")
 T = 10 * 22050 // 275
 net = WaveRNN(device=dev)
@@ -24,15 +23,12 @@ net.load_state_dict(wavernn_state_dict(0))
 mel = torch.from_numpy(synthetic_mel(31, 1, T)).to(dev)
 G = 256
 _lib.call("avc_wavernn_persist", 1)
-_lib.call("avc_wavernn_loop_counters", FORM)
 net.generate(mel)  # warm (regions, code)
 buf = torch.zeros(G, N, 24, dtype=torch.int64, device=dev)
 _lib.call("avc_debug_wavernn_stamps", buf.data_ptr(), N)
 net.generate(mel)
 torch.cuda.synchronize()
 _lib.call("avc_wavernn_persist", 0)
-_lib.call("avc_wavernn_loop_counters", 0)
-print(f"counter form {FORM}")
 st = buf.cpu().numpy().astype(np.float64) * 10.0 / 1000.0  # -> microseconds
 HID1, HID2, IN1, IN2, FC1, FC2, OUT = range(7)
 names = ["HID1", "HID2", "IN1", "IN2", "FC1", "FC2", "OUT"]
@@ -63,4 +59,4 @@ for op, prod, di in chain:
 for op in (HID1, HID2):
     dur = np.mean([np.median(col(op, 2, i) - col(op, 0, i)) for i in steps])
     print(f"{names[op]}: start -> end median {dur:.2f} us")
-np.save(f"gpurun_out/vocoder_stamps_c{FORM}.npy", st)
+np.save("gpurun_out/vocoder_stamps.npy", st)

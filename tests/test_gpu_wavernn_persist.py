@@ -34,11 +34,10 @@ def make(dev, sd, mode="MOL"):
     return net
 
 
-def _both(dev, fn, counters=0):
+def _both(dev, fn):
     out = {}
     for mode in (0, 1):
         _lib.call("avc_wavernn_persist", mode)
-        _lib.call("avc_wavernn_loop_counters", counters)
         try:
             n0 = _lib.persist_launches(dev)
             res = fn()
@@ -46,13 +45,12 @@ def _both(dev, fn, counters=0):
             out[mode] = ([None if t is None else t.cpu().clone() for t in res], _lib.persist_launches(dev) - n0)
         finally:
             _lib.call("avc_wavernn_persist", DEFAULT)
-            _lib.call("avc_wavernn_loop_counters", 0)
     return out
 
 
-@pytest.mark.parametrize("mode,counters", [("MOL", 0), ("RAW", 0), ("MOL", 1)])
+@pytest.mark.parametrize("mode", ["MOL", "RAW"])
 @pytest.mark.parametrize("T,batched,target,overlap", [(24, False, 0, 0), (24, True, 1000, 100), (120, True, 1000, 100)])
-def test_loop_is_bit_identical(cuda_device, sd, mode, counters, T, batched, target, overlap):
+def test_loop_is_bit_identical(cuda_device, sd, mode, T, batched, target, overlap):
     if mode == "RAW":
         sd = dict(sd)
         g = torch.Generator().manual_seed(4)
@@ -60,13 +58,13 @@ def test_loop_is_bit_identical(cuda_device, sd, mode, counters, T, batched, targ
         sd["fc3.bias"] = (torch.rand(18, generator=g) - 0.5) * 0.2
     net = make(cuda_device, sd, mode)
     mel = torch.from_numpy(synthetic_mel(21, 1, T))
-    res = _both(cuda_device, lambda: net._run(mel, batched, target, overlap, 77), counters)
+    res = _both(cuda_device, lambda: net._run(mel, batched, target, overlap, 77))
     (s0, _, w0), n0 = res[0]
     (s1, _, w1), n1 = res[1]
     rows = s0.shape[0]
     assert n0 == 0, "the per-step path made a persistent launch"
     eligible = _lib.load().avc_wavernn_persist_eligible(rows, 512, 512)
-    print(f"{mode} counters={counters} T={T}: {rows} fold rows x {s0.shape[1]} steps, persistent launches {n1}, eligible {eligible}")
+    print(f"{mode} T={T}: {rows} fold rows x {s0.shape[1]} steps, persistent launches {n1}, eligible {eligible}")
     assert eligible == 1 and n1 == 1, "the persistent loop was not taken"
     assert torch.isfinite(s1).all()
     same = float((s0 == s1).double().mean())
