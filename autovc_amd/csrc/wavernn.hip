@@ -768,6 +768,61 @@ __device__ __forceinline__ void rows_dot_part(const float4 (&wv)[NG][kJ4], const
   }
 }
 
+// The six gate rows of units u0, u0 + 1 (wave w: unit w >> 1's three rows against staged rows
+// [12 (w & 1), + 12)) against one staged chunk v: sums[(uu * 3 + g) * kRC + rr] into dst
+__device__ __forceinline__ void gru_chunk_sums(const float4 (&wv)[3][kJ4], const float4 (&v)[kStage4], int K, float* xs,
+                                               float* red, float* dst, int tid, int lane, int w) {
+  lstage_store(K, tid, v, xs);
+  __syncthreads();
+  float acc[3][12];
+  rows_dot_part<3, 12>(wv, xs, K, lane, 12 * (w & 1), acc);
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int rr = 0; rr < 12; ++rr) red[(((w >> 1) * 3 + g) * kRC + 12 * (w & 1) + rr) * kRP + lane] = acc[g][rr];
+  __syncthreads();
+  if (tid < 6 * kRC) {
+    const float* row = red + tid * kRP;
+    float s = 0.f;
+#pragma unroll 8
+    for (int l = 0; l < 64; ++l) s += row[l];
+    dst[tid] = s;
+  }
+  __syncthreads();
+}
+
+// Step i's hidden-gate sums of BOTH layers (W_hh1 h1_{i-1}, W_hh2 h2_{i-1}) for units u0, u0 + 1,
+// kept in LDS for the input phases: the two layers' h rows are loaded together (one round trip),
+// then multiplied one after the other.
+__device__ __forceinline__ bool hid_phase(const WrLoop& p, int i, unsigned E, float* sm, int& nw) {
+  const WrStep& a = p.a;
+  int tid = threadIdx.x;  // (opaque per phase: see gru_phase)
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, w = tid >> 6;
+  const int H = a.H, u0 = blockIdx.x * 2;
+  int* flags = reinterpret_cast<int*>(sm + kWrFlags);
+  float4 wv1[3][kJ4], wv2[3][kJ4];
+#pragma unroll
+  for (int g = 0; g < 3; ++g)
+#pragma unroll
+    for (int j = 0; j < kJ4; ++j) {
+      wv1[g][j] = wrow4(a.Whh1, (long)g * H + u0 + (w >> 1), H, lane + 64 * j);
+      wv2[g][j] = wrow4(a.Whh2, (long)g * H + u0 + (w >> 1), H, lane + 64 * j);
+    }
+  if (i >= 1 && !(wr_wait(p, S_GRU1, i - 1, E, flags, nw) && wr_wait(p, S_GRU2, i - 1, E, flags, nw))) return false;
+  for (int c = 0; c < p.nchk; ++c) {
+    const int rb = c * kRC;
+    float4 v1[kStage4], v2[kStage4];
+    lstage_pre(a, IN_H1, i, rb, H, tid, v1);
+    lstage_pre(a, IN_H2, i, rb, H, tid, v2);
+    lstage_post(a, IN_H1, i, rb, H, tid, v1);
+    lstage_post(a, IN_H2, i, rb, H, tid, v2);
+    gru_chunk_sums(wv1, v1, H, sm + kWrXs, sm + kWrRed, sm + kWrShid + c * 6 * kRC, tid, lane, w);
+    gru_chunk_sums(wv2, v2, H, sm + kWrXs, sm + kWrRed, sm + kWrShid + (kWrMaxChunks + c) * 6 * kRC, tid, lane, w);
+  }
+  return true;
+}
+
 // One GRU phase of step i for units u0, u0 + 1: HID = the hidden gates (W_hh h_{i-1}; sums kept
 // for the input phase), else the input gates, the cell and the hand-off of h_i and t1 / t2.
 // Wave w multiplies unit w >> 1's three gate rows against staged rows [12 (w & 1), + 12).
@@ -802,28 +857,23 @@ __device__ __forceinline__ bool gru_phase(const WrLoop& p, int i, unsigned E, fl
   if (wi >= 0 && !wr_wait(p, wS, wi, E, flags, nw)) return false;
   for (int c = 0; c < p.nchk; ++c) {
     const int rb = c * kRC;
+    const int nr = min(kRC, R - rb);
     if (c > 0) lstage_pre(a, which, i, rb, K, tid, v);
-    lstage_post(a, which, i, rb, K, tid, v);
-    lstage_store(K, tid, v, xs);
-    __syncthreads();
-    float acc[3][12];
-    rows_dot_part<3, 12>(wv, xs, K, lane, 12 * (w & 1), acc);
-#pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-      for (int rr = 0; rr < 12; ++rr) red[(((w >> 1) * 3 + g) * kRC + 12 * (w & 1) + rr) * kRP + lane] = acc[g][rr];
-    __syncthreads();
-    float* dst = HID ? sm + kWrShid + ((WHICH - 1) * kWrMaxChunks + c) * 6 * kRC : sin_;
-    if (tid < 6 * kRC) {
-      const float* row = red + tid * kRP;
-      float s = 0.f;
-#pragma unroll 8
-      for (int l = 0; l < 64; ++l) s += row[l];
-      dst[tid] = s;
+    // GRU1's epilogue operands (the new sample, pI, W_I[:, 0]) issued with the staging loads
+    float xpe = 0.f, pie = 0.f, w0e = 0.f;
+    if (!HID && WHICH == 1 && tid < 2 * nr) {
+      const int r0 = rb + (tid >> 1), un = u0 + (tid & 1);
+      int src;
+      long q;
+      fold_pos(a, r0, i, src, q);
+      xpe = a.teacher ? a.x_tf[(long)r0 * a.L + i] : ld_sc1(a.x_prev, r0);
+      pie = a.pI[((long)src * (a.Ltot + 1) + q) * H + un];
+      w0e = a.wi0[un];
     }
-    __syncthreads();
+    lstage_post(a, which, i, rb, K, tid, v);
+    gru_chunk_sums(wv, v, K, xs, red, HID ? sm + kWrShid + ((WHICH - 1) * kWrMaxChunks + c) * 6 * kRC : sin_, tid,
+                   lane, w);
     if (!HID) {
-      const int nr = min(kRC, R - rb);
       if (tid < 2 * nr) {
         const int uu = tid & 1, rr0 = tid >> 1, un = u0 + uu, r0 = rb + rr0;
         const float* sh = sm + kWrShid + ((WHICH - 1) * kWrMaxChunks + c) * 6 * kRC;
@@ -831,16 +881,7 @@ __device__ __forceinline__ bool gru_phase(const WrLoop& p, int i, unsigned E, fl
         float* t1o = sm + kWrT1 + c * 2 * kRC + tid;
         const float hn = gru_cell(sin_ + uu * 3 * kRC + rr0, sh + uu * 3 * kRC + rr0, ebi, ebh, *hp);
         *hp = hn;
-        float ex;
-        if (WHICH == 1) {
-          int src;
-          long q;
-          fold_pos(a, r0, i, src, q);
-          const float xp = a.teacher ? a.x_tf[(long)r0 * a.L + i] : ld_sc1(a.x_prev, r0);
-          ex = fmaf(a.wi0[un], xp, a.pI[((long)src * (a.Ltot + 1) + q) * H + un]);
-        } else {
-          ex = *t1o;
-        }
+        const float ex = WHICH == 1 ? fmaf(w0e, xpe, pie) : *t1o;
         const float tv = ex + hn;
         if (WHICH == 1) *t1o = tv;
         st_sc1(WHICH == 1 ? a.h1 : a.h2, ((long)((i & 1) ^ 1) * R + r0) * H + un, hn);
@@ -878,17 +919,22 @@ __device__ __forceinline__ bool fc_phase(const WrLoop& p, int f, int i, unsigned
   if (!wr_wait(p, WHICH == 1 ? S_GRU2 : S_FC1, i, E, flags, nw)) return false;
   for (int c = 0; c < p.nchk; ++c) {
     const int rb = c * kRC;
+    const int nr = min(kRC, a.R - rb);
     if (c > 0) lstage_pre(a, which, i, rb, K, tid, v);
+    // the epilogue thread's bias (one (output row, fold row) per thread: 8 nr <= 192), issued with
+    // the staging loads
+    const int o = tid / nr, n = f * 8 + o;
+    const bool ep = tid < 8 * nr && n < a.Fc;
+    const float bz = ep ? bias[n] : 0.f;
     lstage_post(a, which, i, rb, K, tid, v);
     lstage_store(K, tid, v, xs);
     __syncthreads();
     float acc[2][kRC];
     rows_dot<2>(wv, xs, K, lane, acc);
     reduce_lanes<2>(acc, w, lane, sm + kWrRed, sums);
-    const int nr = min(kRC, a.R - rb);
-    for (int t = tid; t < 8 * nr; t += 256) {
-      const int o = t / nr, rr = t - o * nr, n = f * 8 + o;
-      if (n < a.Fc) st_sc1(y, (long)(rb + rr) * a.Fc + n, fmaxf(sums[o * kRC + rr] + bias[n], 0.f));
+    if (ep) {
+      const int rr = tid - o * nr;
+      st_sc1(y, (long)(rb + rr) * a.Fc + n, fmaxf(sums[o * kRC + rr] + bz, 0.f));
     }
     __syncthreads();
   }
@@ -912,6 +958,8 @@ __device__ __forceinline__ bool out_phase(const WrLoop& p, int r, int i, unsigne
 #pragma unroll
     for (int j = 0; j < kJ4; ++j)
       w3[m][j] = reinterpret_cast<const float4*>(a.W3 + (long)min(w + 4 * m, NC - 1) * Fc)[min(lane + 64 * j, (Fc >> 2) - 1)];
+  const int cb3 = (tid & 3) + 4 * (tid >> 2);
+  const float b3v = tid < 32 && cb3 < NC ? a.b3[cb3] : 0.f;
   if (!wr_wait(p, S_FC2, i, E, flags, nw)) return false;
   float4 yv[kJ4];
 #pragma unroll
@@ -940,7 +988,7 @@ __device__ __forceinline__ bool out_phase(const WrLoop& p, int r, int i, unsigne
       float s = 0.f;
 #pragma unroll 8
       for (int l = 0; l < 64; ++l) s += row[l];
-      lg[c] = s + a.b3[c];
+      lg[c] = s + b3v;
     }
   }
   __syncthreads();
@@ -979,22 +1027,23 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
     ebi2[g] = a.bih2[g * a.H + un];
     ebh2[g] = a.bhh2[g * a.H + un];
   }
-  // per step: GRU1 and GRU2 input phases of step i, then the role's ops; HID ops form step i + 1's
-  // hidden sums (skipped after the last step).  One op list walked by one switch, so every phase
-  // is instantiated once.
-  enum : int { OP_HID1, OP_HID2, OP_IN1, OP_IN2, OP_FC1, OP_FC2, OP_OUT };
+  // per step: GRU1 and GRU2 input phases of step i, then the role's ops; HID forms step i + 1's
+  // hidden sums of both layers (skipped after the last step), placed where the role would wait
+  // anyway: FC1 after its product, FC2 and OUT before waiting for theirs.  One op list walked by one
+  // switch, so every phase is instantiated once.
+  enum : int { OP_HID = 0, OP_IN1 = 2, OP_IN2 = 3, OP_FC1 = 4, OP_FC2 = 5, OP_OUT = 6 };
   // the role's op list, packed 4 bits per op (no indexed array: it would live in scratch)
-  const unsigned seq = role == WR_FC1   ? (OP_IN1 | OP_IN2 << 4 | OP_FC1 << 8 | OP_HID1 << 12 | OP_HID2 << 16)
-                       : role == WR_FC2 ? (OP_IN1 | OP_IN2 << 4 | OP_HID2 << 8 | OP_FC2 << 12 | OP_HID1 << 16)
-                       : role == WR_OUT ? (OP_IN1 | OP_IN2 << 4 | OP_HID1 << 8 | OP_HID2 << 12 | OP_OUT << 16)
-                                        : (OP_IN1 | OP_IN2 << 4 | OP_HID1 << 8 | OP_HID2 << 12);
-  const int nops = role == WR_NONE ? 4 : 5;
+  const unsigned seq = role == WR_FC1   ? (OP_IN1 | OP_IN2 << 4 | OP_FC1 << 8 | OP_HID << 12)
+                       : role == WR_FC2 ? (OP_IN1 | OP_IN2 << 4 | OP_HID << 8 | OP_FC2 << 12)
+                       : role == WR_OUT ? (OP_IN1 | OP_IN2 << 4 | OP_HID << 8 | OP_OUT << 12)
+                                        : (OP_IN1 | OP_IN2 << 4 | OP_HID << 8);
+  const int nops = role == WR_NONE ? 3 : 4;
   bool ok = true;
   int i = -1;  // step -1: only the hidden sums of step 0 (h_{-1} = 0)
   for (; ok && i < L; ++i) {
     for (int o = 0; o < nops && ok; ++o) {
       const int op = (int)((seq >> (4 * o)) & 15u);
-      const bool hid = op == OP_HID1 || op == OP_HID2;
+      const bool hid = op == OP_HID;
       if (hid ? i + 1 >= L : i < 0) continue;
       const bool stamp = p.stamps && i >= 0 && i < p.nstamp && tid == 0;
       if (tid == 0) {  // (read by wr_wait's stamp, same thread)
@@ -1003,8 +1052,7 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
       }
       if (stamp) p.stamps[((long)wg * p.nstamp + i) * 24 + 3 * op] = __builtin_amdgcn_s_memrealtime();
       switch (op) {
-        case OP_HID1: ok = gru_phase<1, true>(p, i + 1, E, wr_sm, nw, ebi1, ebh1); break;
-        case OP_HID2: ok = gru_phase<2, true>(p, i + 1, E, wr_sm, nw, ebi2, ebh2); break;
+        case OP_HID: ok = hid_phase(p, i + 1, E, wr_sm, nw); break;
         case OP_IN1: ok = gru_phase<1, false>(p, i, E, wr_sm, nw, ebi1, ebh1); break;
         case OP_IN2: ok = gru_phase<2, false>(p, i, E, wr_sm, nw, ebi2, ebh2); break;
         case OP_FC1: ok = fc_phase<1>(p, wg, i, E, wr_sm, nw); break;

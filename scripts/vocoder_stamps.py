@@ -2,7 +2,7 @@
 
 Runs generate() of the bench's 10 s utterance with the loop on and s_memrealtime stamps (100 MHz)
 of the first N steps: per workgroup and op (IN1 / IN2 = the GRUs' input phases, FC1, FC2, OUT,
-HID1 / HID2 = next step's hidden-gate phases) the op's start, the end of its wait and its end.
+HID = next step's hidden-gate phase of both layers) the op's start, the end of its wait and its end.
 Prints, averaged over steps 16..N-1, the step period and for each chain op: the wait's end
 relative to the producer's last end (hand-off latency) and the op's duration after the wait."""
 import sys
@@ -30,8 +30,8 @@ net.generate(mel)
 torch.cuda.synchronize()
 _lib.call("avc_wavernn_persist", 0)
 st = buf.cpu().numpy().astype(np.float64) * 10.0 / 1000.0  # -> microseconds
-HID1, HID2, IN1, IN2, FC1, FC2, OUT = range(7)
-names = ["HID1", "HID2", "IN1", "IN2", "FC1", "FC2", "OUT"]
+HID, _, IN1, IN2, FC1, FC2, OUT = range(7)
+names = ["HID", "-", "IN1", "IN2", "FC1", "FC2", "OUT"]
 nfc, R = 64, 20
 roles = {FC1: range(0, nfc), FC2: range(nfc, 2 * nfc), OUT: range(2 * nfc, 2 * nfc + R)}
 wgs = {op: list(roles.get(op, range(G))) for op in range(7)}
@@ -56,7 +56,7 @@ for op, prod, di in chain:
     print(f"{names[op]:4s}: hand-off from {names[prod]} last end -> median wait end {hand:6.2f} us "
           f"(spread over consumers {wait_spread:5.2f}); after the wait median {dur:5.2f} / max {dur_max:5.2f} us; "
           f"start -> wait end {pre:6.2f} us")
-for op in (HID1, HID2):
+for op in (HID,):
     dur = np.mean([np.median(col(op, 2, i) - col(op, 0, i)) for i in steps])
     print(f"{names[op]}: start -> end median {dur:.2f} us")
 np.save("gpurun_out/vocoder_stamps.npy", st)
