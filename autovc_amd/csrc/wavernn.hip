@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
   }
 }
 
-int g_wr_persist = 0;  // avc_wavernn_persist(): 1 = the persistent sample loop where eligible
+int g_wr_persist = 1;  // avc_wavernn_persist(): 1 (default) = the persistent sample loop where eligible
 int g_wr_inject = 0;   // avc_debug_wavernn_inject(): loop launches left that give up at once
 unsigned long long* g_wr_stamps = nullptr;  // avc_debug_wavernn_stamps(): next loop launch's stamps
 int g_wr_nstamp = 0;
@@ -1110,12 +1110,15 @@ int wr_loop_run(avc_context* ctx, const WrStep& a, hipStream_t s, double macs) {
   AVC_TRY(persist_guard(ctx));
   const int G = a.H / 2;
   unsigned* region = nullptr;
-  // counter layout key: (L, G) -- the targets depend on the steps per launch
-  AVC_TRY(coresident_region(ctx, 5, a.L, G, G, (size_t)kWrCntWords, s, &region));
+  // counter layout key: every quantity a wait target depends on -- the steps per launch L and each
+  // stage's producer count (G, nfc, R); a region shared by two layouts would leave one layout's
+  // arrivals under the other's epoch targets
+  const int nfc = (a.Fc + 7) / 8;
+  AVC_TRY(coresident_region(ctx, 5, a.L, a.R * 1024 + nfc, G, (size_t)kWrCntWords, s, &region));
   WrLoop p{};
   p.a = a;
   p.G = G;
-  p.nfc = (a.Fc + 7) / 8;
+  p.nfc = nfc;
   p.nchk = (a.R + kRC - 1) / kRC;
   p.tickets = reinterpret_cast<unsigned long long*>(region);  // region layout: lstm_persist.hip
   p.tmo = region + 32;

@@ -462,7 +462,7 @@ int avc_wavernn_upsample(avc_context* ctx, const int* dims, int T, const float* 
 int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* const* params, const float* mel,
                          int batched, int target, int overlap, int mol, unsigned long long seed,
                          const float* x_teacher, float* logits, float* samples, float* wave, void* stream);
-/* Tuning hook: 1 = avc_wavernn_generate runs the whole sample loop as ONE persistent launch of
+/* Tuning hook: 1 (default) = avc_wavernn_generate runs the whole sample loop as ONE persistent launch of
  * rnn_dims / 2 workgroups with in-launch hand-offs where eligible
  * (avc_wavernn_persist_eligible: <= 96 fold rows, 2 * ceil(fc_dims / 8) + rows <= rnn_dims / 2,
  * every workgroup resident); 0 = five graph-captured launches per sample step.  Same arithmetic,

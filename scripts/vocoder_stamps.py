@@ -28,7 +28,7 @@ buf = torch.zeros(G, N, 24, dtype=torch.int64, device=dev)
 _lib.call("avc_debug_wavernn_stamps", buf.data_ptr(), N)
 net.generate(mel)
 torch.cuda.synchronize()
-_lib.call("avc_wavernn_persist", 0)
+_lib.call("avc_wavernn_persist", 1)  # (the default)
 st = buf.cpu().numpy().astype(np.float64) * 10.0 / 1000.0  # -> microseconds
 HID, _, IN1, IN2, FC1, FC2, OUT = range(7)
 names = ["HID", "-", "IN1", "IN2", "FC1", "FC2", "OUT"]

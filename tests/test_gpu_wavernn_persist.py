@@ -19,7 +19,7 @@ from autovc_amd.wavernn import WaveRNN
 from tests.conftest import load_golden
 
 pytestmark = pytest.mark.gpu
-DEFAULT = 0  # the library's default (avc_wavernn_persist)
+DEFAULT = 1  # the library's default (avc_wavernn_persist)
 
 
 @pytest.fixture(scope="module")
