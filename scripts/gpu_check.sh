@@ -85,6 +85,7 @@ for step in "$@"; do
     wrp) run wrp 400 python -u -m pytest tests/test_gpu_wavernn_persist.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider && run wrpab 300 python scripts/vocoder_ab.py 3 ;;
     wrstamps) run wrstamps 300 python scripts/vocoder_stamps.py 128 ;;
     bnstat) run bnstat 600 python -u -m pytest tests/test_gpu_bnfuse.py tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_margin.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    voctest) run voctest 400 python -u -m pytest tests/test_gpu_wavernn.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
