@@ -82,6 +82,7 @@ _SIGS = {
     "avc_lstm_persist_halves": [_I],
     "avc_bn_bwd_frag": [_I],
     "avc_bptt_coalesce": [_I],
+    "avc_dg_dual_split": [_I],
     "avc_lstm32_tune": [_I],
     "avc_bptt_persist": [_I],
     "avc_debug_bptt_diag": [_I],

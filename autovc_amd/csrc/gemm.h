@@ -103,6 +103,12 @@ int gemm_frag_partials(int M, int N, int K, const _Float16* As, const _Float16* 
                        float* slab, hipStream_t s);
 // [R][K] fp32 (row stride rs) -> fragment-major split, scaled by the power of two of *amax
 int gemm_split_frag(const float* src, long rs, int R, int K, const unsigned* amax, _Float16* dst, hipStream_t s);
+// One read of row-major [R][C] src writes its scaled split as an A operand (K = C, rows R) into
+// dst_a and as an A^T operand (K = R, rows C) into dst_t, the bits split_frag32_kernel gives each
+// (R % 32 == 0, C % 64 == 0: gemm_split_dual_ok).  Consumers take them as a_frag + a_frag_scaled.
+bool gemm_split_dual_ok(long R, long C, long ld);
+int gemm_split_dual(const float* src, long ld, long R, int C, const unsigned* amax, _Float16* dst_a, _Float16* dst_t,
+                    hipStream_t s);
 // max |x| of a rows x cols region (row stride ld) into *out (float bits), for GemmDesc::amax_a
 int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t stream);
 

@@ -1712,6 +1712,74 @@ int gemm_frag_partials(int M, int N, int K, const _Float16* As, const _Float16* 
 
 // split a [R][K] row-major fp32 matrix (row stride rs) into the fragment-major layout, scaled
 // by the power of two split_scale_of(amax) (amax NULL: unscaled)
+// One read of a row-major [R][C] operand (R % 32 == 0, C % 64 == 0) writes BOTH of its scaled
+// split images: dst_a as the A operand of a product with K = C (rows R: split_frag32_kernel's
+// row-major layout) and dst_t as the A^T operand of a product with K = R (rows C: its transposed
+// layout).  Workgroup = a 32 x 64 block staged through LDS; every element is scaled and split by
+// the expressions split_frag32_kernel uses, so both images are its bits.  (The LSTM backward's dG:
+// the dX product reads it as A, the two weight-gradient products as A^T; two split passes read the
+// 512 MB operand twice.)
+__global__ __launch_bounds__(256) void split_frag32_dual_kernel(const float* __restrict__ src, long ld, int R, int C,
+                                                                const unsigned* __restrict__ amax,
+                                                                _Float16* __restrict__ dst_a,
+                                                                _Float16* __restrict__ dst_t) {
+  __shared__ float tile[32][65];
+  const int tid = threadIdx.x;
+  const long bt = blockIdx.x;        // 32-row block
+  const int bc = (int)blockIdx.y;    // 64-column block
+  const float sc = split_scale_of(amax);
+  const int nkc_a = C / 16, nkc_t = R / 16;
+  {  // A image: thread = (row rr, 8-column group g)
+    const int rr = tid >> 3, g = tid & 7;
+    const long r = bt * 32 + rr;
+    const float4* q = reinterpret_cast<const float4*>(src + r * ld + (long)bc * 64 + 8 * g);
+    const float4 a = q[0], b = q[1];
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if (amax) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= sc;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[rr][8 * g + e] = v[e];
+    f16x8 hi, lo;
+    split8(v, hi, lo);
+    const int g8 = bc * 8 + g;
+    const long blk = ((r >> 5) * nkc_a + (g8 >> 1)) * 2;
+    const int lane = (int)(r & 31) + 32 * (g8 & 1);
+    *reinterpret_cast<f16x8*>(dst_a + blk * 512 + lane * 8) = hi;
+    *reinterpret_cast<f16x8*>(dst_a + (blk + 1) * 512 + lane * 8) = lo;
+  }
+  __syncthreads();
+  {  // A^T image: thread = (column c, 8-row group q)
+    const int c = tid & 63, q = tid >> 6;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = tile[8 * q + e][c];
+    f16x8 hi, lo;
+    split8(v, hi, lo);
+    const long r = (long)bc * 64 + c;
+    const long g8 = bt * 4 + q;
+    const long blk = ((r >> 5) * nkc_t + (g8 >> 1)) * 2;
+    const int lane = (int)(r & 31) + 32 * (int)(g8 & 1);
+    *reinterpret_cast<f16x8*>(dst_t + blk * 512 + lane * 8) = hi;
+    *reinterpret_cast<f16x8*>(dst_t + (blk + 1) * 512 + lane * 8) = lo;
+  }
+}
+
+bool gemm_split_dual_ok(long R, long C, long ld) {
+  return R > 0 && C > 0 && R % 32 == 0 && C % 64 == 0 && ld % 4 == 0 && R / 32 < 0x7fffffffL && C / 64 <= 65535;
+}
+
+int gemm_split_dual(const float* src, long ld, long R, int C, const unsigned* amax, _Float16* dst_a, _Float16* dst_t,
+                    hipStream_t s) {
+  AVC_CHECK_ARG(gemm_split_dual_ok(R, C, ld) && (reinterpret_cast<uintptr_t>(src) & 15) == 0,
+                "gemm_split_dual: needs rows % 32 == 0, columns % 64 == 0 and 16-byte aligned rows");
+  split_frag32_dual_kernel<<<dim3((unsigned)(R / 32), (unsigned)(C / 64)), 256, 0, s>>>(src, ld, (int)R, C, amax,
+                                                                                       dst_a, dst_t);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
+
 int gemm_split_frag(const float* src, long rs, int R, int K, const unsigned* amax, _Float16* dst, hipStream_t s) {
   const long ntile = frag_ntile(R);
   const int nkc = frag_nkc(K);

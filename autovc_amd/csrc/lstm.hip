@@ -708,6 +708,7 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx,
   }
 }
 
+int g_dg_dual = 1;  // avc_dg_dual_split(): one pass writes both split images of dG (dX and dW products)
 int g_lstm32_mode = 1;  // avc_lstm32_tune(): 0 = libm gate math, 3-step prefetch; 1 = fast math, 8 steps
 
 void launch_lstm32(int nblk, int T, int B, long ldgx, long ldy, const L32Dir& d0, const L32Dir& d1, hipStream_t s) {
@@ -1145,6 +1146,7 @@ size_t lstm_backward_scratch(int T, int B, int din, int H) {
   s += gemm_afrag_bytes(H, 4 * H) + gemm_afrag_bytes(B + 31, 4 * H) + 32 * (size_t)B * H * f + (size_t)B * f + 2048;
   s += bptt_persist_scratch(B, H);  // the persistent BPTT's double-buffered slabs, split dG, dc
   s += gemm_afrag_bytes(4L * H, (int)TB) + 256;  // dG^T split once for dW_ih and dW_hh
+  s += gemm_afrag_bytes((long)TB, 4 * H) + 256;  // dG split by the same pass for dX (gemm_split_dual)
   GemmDesc d1;  // dW_ih
   d1.M = 4 * H; d1.N = din; d1.Kc = (int)TB; d1.a_trans = 1; d1.b_rows = TB;
   d1.prec16 = 1; d1.split_scale = 1;
@@ -1303,11 +1305,25 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   g1.B = x; g1.ldb = ldx; g1.b_rows = TB;
   g1.C = dwih_dst; g1.ldc = din; g1.accumulate = acc_w;
   g1.prec16 = 1; g1.split_scale = 1; g1.amax_a = amax_dg;
-  // dG^T is split once (the larger operand of both products: TB x 4H against TB x din / H)
+  // dG^T is split once (the larger operand of both products: TB x 4H against TB x din / H); with
+  // the dX product also streaming split dG, one pass writes both images (g_dg_dual)
   const bool share = gemm_frag_eligible(g1);
+  _Float16* dg_s = nullptr;  // dG as the dX product's A operand, when the dual pass wrote it
   if (share) {
     AVC_TAKE(dgT_s, _Float16, gemm_afrag_bytes(4L * H, (int)TB) / 2, sc);
-    g1.a_frag_out = dgT_s;
+    GemmDesc g3p;
+    g3p.M = (int)TB; g3p.N = din; g3p.Kc = 4 * H; g3p.A = dg; g3p.lda = 4 * H; g3p.a_rows = TB;
+    g3p.B = wih_use; g3p.ldb = din; g3p.C = d_x; g3p.ldc = din; g3p.prec16 = 1; g3p.split_scale = 1;
+    g3p.amax_a = amax_dg;
+    if (g_dg_dual && d_x && gemm_frag_eligible(g3p) && gemm_split_dual_ok((long)TB, 4L * H, 4L * H)) {
+      AVC_TAKE(dgs_a, _Float16, gemm_afrag_bytes((long)TB, 4 * H) / 2, sc);
+      AVC_TRY(gemm_split_dual(dg, 4L * H, (long)TB, 4 * H, amax_dg, dgs_a, dgT_s, s));
+      dg_s = dgs_a;
+      g1.a_frag = dgT_s;
+      g1.a_frag_scaled = 1;
+    } else {
+      g1.a_frag_out = dgT_s;
+    }
   }
   AVC_TRY(gemm_run(ctx, g1, s));
   GemmDesc g2 = g1;
@@ -1315,7 +1331,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   g2.B = y; g2.ldb = ldy; g2.b_shift0 = reverse ? B : -B;
   g2.C = dwhh_dst; g2.ldc = H;
   if (share && gemm_frag_eligible(g2)) {
-    g2.a_frag = g1.a_frag_out;
+    g2.a_frag = g1.a_frag_out ? g1.a_frag_out : g1.a_frag;
     g2.a_frag_scaled = 1;
   }
   g2.a_frag_out = nullptr;
@@ -1342,6 +1358,10 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     g3.b_trans = small ? 0 : 0;
     g3.C = d_x; g3.ldc = din; g3.accumulate = accumulate_dx;
     g3.prec16 = 1; g3.split_scale = 1; g3.amax_a = amax_dg;
+    if (dg_s) {  // written by the dual split pass above
+      g3.a_frag = dg_s;
+      g3.a_frag_scaled = 1;
+    }
     AVC_TRY(gemm_run(ctx, g3, s));
   }
   return AVC_OK;
@@ -1357,6 +1377,15 @@ extern "C" int avc_debug_stamps(void* buf, long target_launch) {
   return AVC_OK;
 }
 #endif
+
+extern "C" int avc_dg_dual_split(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_dg_dual_split: on must be 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_dg_dual = on;
+  return AVC_OK;
+}
 
 extern "C" int avc_bptt_mode(int mode) {
   if (mode < 0 || mode > 2) {

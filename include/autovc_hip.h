@@ -340,6 +340,10 @@ int avc_bn_bwd_frag(int on);
  * the next step in LDS (whole-run stores); 0 = the round-3 row-fast mapping.  Same dG, dc and split
  * dG bits; the bias gradients' column sums are combined in a different (fixed) order. */
 int avc_bptt_coalesce(int on);
+/* Tuning hook: 1 (default) = the LSTM backward splits dG for its dX product (A operand) and for its
+ * two weight-gradient products (A^T operand) in ONE pass over the fp32 dG (split_frag32_dual_kernel),
+ * where the shapes allow (T * B % 32 == 0, 4H % 64 == 0); 0 = two split passes.  Same bits. */
+int avc_dg_dual_split(int on);
 /* Tuning hook: which recurrences may take the persistent form (bit 0 = one layer, e.g. decoder
  * lstm1; bit 1 = two stacked layers, decoder lstm2; default 3 = both). */
 int avc_lstm_persist_layers(int mask);
