@@ -110,6 +110,7 @@ _SIGS = {
     "avc_embedding_mean_normalize": [_I, _I, _P, _P, _P],
     "avc_wavernn_param_count": [_I],
     "avc_wavernn_persist": [_I],
+    "avc_wavernn_proj_tiled": [_I],
     "avc_wavernn_persist_eligible": [_I, _I, _I],
     "avc_debug_wavernn_inject": [_I],
     "avc_debug_wavernn_stamps": [_P, _I],

@@ -473,6 +473,9 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
  * bit-identical samples, logits and waveform.  A loop launch that abandons a bounded wait writes
  * its remaining samples as NaN and the call fails with AVC_ERR_DEVICE. */
 int avc_wavernn_persist(int on);
+/* Tuning hook: 1 (default) = generate()'s input projection of every sample position (pI) as an
+ * LDS-tiled kernel; 0 = one thread per output.  Same bits. */
+int avc_wavernn_proj_tiled(int on);
 int avc_wavernn_persist_eligible(int rows, int rnn_dims, int fc_dims);
 /* Test hook: the next `launches` loop launches give up at their first unmet wait. */
 int avc_debug_wavernn_inject(int launches);

@@ -109,3 +109,22 @@ def test_eligibility_limits():
     assert _lib.load().avc_wavernn_persist_eligible(97, 512, 512) == 0
     assert _lib.load().avc_wavernn_persist_eligible(96, 512, 512) == 1
     assert _lib.load().avc_wavernn_persist_eligible(60, 256, 512) == 0
+
+
+def test_tiled_input_projection_is_bit_identical(cuda_device, sd):
+    """generate()'s per-position input projection pI (avc_wavernn_proj_tiled): the LDS-tiled kernel
+    keeps every output's FMA chain order, so the whole generation is bit-identical."""
+    net = make(cuda_device, sd)
+    mel = torch.from_numpy(synthetic_mel(23, 1, 40))
+    out = {}
+    for mode in (0, 1):
+        _lib.call("avc_wavernn_proj_tiled", mode)
+        try:
+            s, _, w = net._run(mel, True, 1000, 100, 9)
+            torch.cuda.synchronize()
+            out[mode] = (s.cpu(), w.cpu())
+        finally:
+            _lib.call("avc_wavernn_proj_tiled", 1)
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    m, aux = net.upsample_features(mel)
+    assert m.shape[0] == 40 * 275  # (the projection's rows: every position of the padded mel)
