@@ -113,10 +113,22 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int
     double s = 0.0, a1 = 0.0, a2 = 0.0;
     if (c < C) {
       const double K = (double)stats[c] / (double)min((long)part_rows, M);
-#pragma unroll 4
-      for (int p = grp; p < nparts; p += 4)
-        bn_combine(stats[((long)p * 2 + 0) * C + c], stats[((long)p * 2 + 1) * C + c],
-                   min((long)part_rows, M - (long)p * part_rows), K, s, a1, a2);
+      // partials p = grp, grp + 4, ... in order, four loads in flight (the fp64 combine does not
+      // pipeline on its own: one round trip per partial measured 27 vs 10 us per C3 call)
+      for (int p0 = grp; p0 < nparts; p0 += 16) {
+        float Sv[4], Qv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int p = p0 + 4 * u;
+          Sv[u] = p < nparts ? stats[((long)p * 2 + 0) * C + c] : 0.f;
+          Qv[u] = p < nparts ? stats[((long)p * 2 + 1) * C + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int p = p0 + 4 * u;
+          if (p < nparts) bn_combine(Sv[u], Qv[u], min((long)part_rows, M - (long)p * part_rows), K, s, a1, a2);
+        }
+      }
     }
     red[0][grp][cl] = s;
     red[1][grp][cl] = a1;

@@ -873,11 +873,19 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
     if (col < d.N) {
       const double K = (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, col * 4, 0, 16)) /
                        (double)min(BM, d.M);
-#pragma unroll 4
-      for (int p = grp; p < tilesM; p += 4) {
-        const float S = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 0) * d.N + col) * 4, 0, 16));
-        const float Q = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 1) * d.N + col) * 4, 0, 16));
-        bn_combine(S, Q, min(BM, d.M - p * BM), K, s, a1, a2);
+      for (int p0 = grp; p0 < tilesM; p0 += 16) {  // four partials' loads in flight, combined in order
+        float Sv[4], Qv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int p = p0 + 4 * u;
+          Sv[u] = p < tilesM ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 0) * d.N + col) * 4, 0, 16)) : 0.f;
+          Qv[u] = p < tilesM ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 1) * d.N + col) * 4, 0, 16)) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int p = p0 + 4 * u;
+          if (p < tilesM) bn_combine(Sv[u], Qv[u], min(BM, d.M - p * BM), K, s, a1, a2);
+        }
       }
     }
     dred[(0 * 4 + grp) * BN + cl] = s;

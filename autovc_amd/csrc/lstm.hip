@@ -1313,7 +1313,8 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     AVC_TAKE(dgT_s, _Float16, gemm_afrag_bytes(4L * H, (int)TB) / 2, sc);
     GemmDesc g3p;
     g3p.M = (int)TB; g3p.N = din; g3p.Kc = 4 * H; g3p.A = dg; g3p.lda = 4 * H; g3p.a_rows = TB;
-    g3p.B = wih_use; g3p.ldb = din; g3p.C = d_x; g3p.ldc = din; g3p.prec16 = 1; g3p.split_scale = 1;
+    g3p.B = wih_use; g3p.ldb = din; g3p.b_rows = 4L * H; g3p.C = d_x; g3p.ldc = din; g3p.prec16 = 1;
+    g3p.split_scale = 1;
     g3p.amax_a = amax_dg;
     if (g_dg_dual && d_x && gemm_frag_eligible(g3p) && gemm_split_dual_ok((long)TB, 4L * H, 4L * H)) {
       AVC_TAKE(dgs_a, _Float16, gemm_afrag_bytes((long)TB, 4 * H) / 2, sc);
