@@ -564,12 +564,13 @@ def pmc_traffic(cls, args):
     from inside the process, so the number is the profiled run's, not this run's."""
     import glob
     # default commands only: C2 forward (profiles/rNN_pmc_traffic.json), C3 training step
-    # (profiles/rNN_pmc_traffic_train.json)
-    if args.frames != 128 or args.mode not in ("fwd", "train"):
+    # (profiles/rNN_pmc_traffic_train.json), C5 long-form forward (profiles/rNN_pmc_traffic_long.json)
+    if args.frames != 128 or args.mode not in ("fwd", "train", "long"):
         return None
-    if args.batch not in (None, 64 if args.mode == "fwd" else 256):
+    if args.batch not in (None, {"fwd": 64, "train": 256, "long": 32}[args.mode]):
         return None
-    pat = "r*_pmc_traffic.json" if args.mode == "fwd" else "r*_pmc_traffic_train.json"
+    pat = {"fwd": "r*_pmc_traffic.json", "train": "r*_pmc_traffic_train.json",
+           "long": "r*_pmc_traffic_long.json"}[args.mode]
     files = sorted(glob.glob(os.path.join(HERE, "profiles", pat)))
     if not files:
         return None
