@@ -260,10 +260,13 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 // var = a2 / count - (a1 / count)^2 -- exact for any K, and with K = the first partial's mean the
 // subtraction cancels nothing that fp32 rounding put there.  Shared by bn_finalize_kernel and the
 // fused BN epilogue (contraction off: both form the same bits).
-__device__ __forceinline__ void bn_combine(float S, float Q, long n, double K, double& s, double& a1, double& a2) {
+// inv_n = 1 / n (callers pass the one reciprocal of the full partial size, and divide only for the
+// short last partial: an fp64 division per partial made the combine several times slower).
+__device__ __forceinline__ void bn_combine(float S, float Q, long n, double inv_n, double K, double& s, double& a1,
+                                           double& a2) {
 #pragma clang fp contract(off)
   const double dn = (double)n;
-  const double dm = (double)S / dn - K;
+  const double dm = (double)S * inv_n - K;
   s += (double)S;
   a1 += dn * dm;
   a2 += (double)Q + dn * dm * dm;

@@ -113,6 +113,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int
     double s = 0.0, a1 = 0.0, a2 = 0.0;
     if (c < C) {
       const double K = (double)stats[c] / (double)min((long)part_rows, M);
+      const double inv_pr = 1.0 / (double)part_rows;
+      const double inv_last = 1.0 / (double)(M - (long)(nparts - 1) * part_rows);  // the short last partial
       // partials p = grp, grp + 4, ... in order, four loads in flight (the fp64 combine does not
       // pipeline on its own: one round trip per partial measured 27 vs 10 us per C3 call)
       for (int p0 = grp; p0 < nparts; p0 += 16) {
@@ -126,7 +128,10 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int p = p0 + 4 * u;
-          if (p < nparts) bn_combine(Sv[u], Qv[u], min((long)part_rows, M - (long)p * part_rows), K, s, a1, a2);
+          if (p < nparts) {
+            const long n = min((long)part_rows, M - (long)p * part_rows);
+            bn_combine(Sv[u], Qv[u], n, p == nparts - 1 ? inv_last : inv_pr, K, s, a1, a2);
+          }
         }
       }
     }

@@ -873,6 +873,8 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
     if (col < d.N) {
       const double K = (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, col * 4, 0, 16)) /
                        (double)min(BM, d.M);
+      const double inv_pr = 1.0 / (double)BM;
+      const double inv_last = 1.0 / (double)(d.M - (tilesM - 1) * BM);  // the short last partial
       for (int p0 = grp; p0 < tilesM; p0 += 16) {  // four partials' loads in flight, combined in order
         float Sv[4], Qv[4];
 #pragma unroll
@@ -884,7 +886,10 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int p = p0 + 4 * u;
-          if (p < tilesM) bn_combine(Sv[u], Qv[u], min(BM, d.M - p * BM), K, s, a1, a2);
+          if (p < tilesM) {
+            const long n = min(BM, d.M - p * BM);
+            bn_combine(Sv[u], Qv[u], n, p == tilesM - 1 ? inv_last : inv_pr, K, s, a1, a2);
+          }
         }
       }
     }
