@@ -111,14 +111,17 @@ __device__ __forceinline__ float split_unscale(const unsigned* amax_a, const uns
 // BatchNorm column partials of one output tile (train mode).  Per column and partial (PARTS = 1:
 // the tile's rows; 2: the two 128-row halves of a 256-row tile, make_plan's stats granularity):
 // stats[part][0][col] = S, the sum of the column's valid rows, and stats[part][1][col] = the sum
-// of squares about the partial's own mean S / n, from a second pass over the same values.  So the
-// variance never comes out of E[x^2] - E[x]^2 with fp32 sums: at B = 1 a decoder conv channel's
-// mean is ~17 standard deviations, and that difference cost ~2^-12 relative in the variance
-// (dec.conv0 5.9e-5 local error against fp32 CPU's 6.9e-6); bn_finalize_kernel combines
-// the partials in fp64 about a common shift.  val(i, j, e) = act(acc + bias) as the epilogue
-// stored it (RAW: acc already holds it).  Every producer (the three GEMM epilogues, the fused BN
-// one) goes through here, so fused and unfused chains form the same bits.  SC1: write-through
-// stores (the fused BN's in-launch hand-off).  red: >= (WM + PARTS) * BN floats of LDS, free.
+// of squares about the partial's mean S / n.  Both come from ONE pass over the values shifted by
+// k, the partial's first row of that column (broadcast through LDS): S = S1 + n k and
+// Q = S2 - S1^2 / n with S1 = sum (x - k), S2 = sum (x - k)^2.  A sample of the column lies within
+// a few standard deviations of its mean, so nothing like E[x^2] - E[x]^2 with fp32 sums is ever
+// formed: at B = 1 a decoder conv channel's mean is ~17 standard deviations and that difference
+// cost ~2^-12 relative in the variance (dec.conv0 5.9e-5 local error against fp32 CPU's 6.9e-6,
+// DESIGN §3).  bn_finalize_kernel combines the partials in fp64 about a common shift.  val(i, j, e)
+// = act(acc + bias) as the epilogue stored it (RAW: acc already holds it).  Every producer (the
+// three GEMM epilogues, the fused BN one) goes through here, so fused and unfused chains form the
+// same bits.  SC1: write-through stores (the fused BN's in-launch hand-off).  red: >= (2 WM +
+// PARTS) * BN floats of LDS, free.
 template <int BM, int BN, int WM, int WTN, int TM, int TN, int PARTS, bool RAW, bool SC1>
 __device__ __forceinline__ void bn_tile_stats(const GemmDesc& d, const f32x16 (&acc)[TM][TN], const float (&bias)[TN],
                                               float* red, int tm, int tn, int wm, int wn, int lane, int tid, int NT,
@@ -126,69 +129,48 @@ __device__ __forceinline__ void bn_tile_stats(const GemmDesc& d, const f32x16 (&
   static_assert(PARTS == 1 || (BM == 256 && WM % 2 == 0), "two 128-row partials per 256-row tile");
   constexpr int PR = BM / PARTS, WPP = WM / PARTS;  // rows and wave rows per partial
   const int M = d.M, N = d.N, act = d.act;
-  float* tmean = red + WM * BN;  // [PARTS][BN]
+  float* kshift = red + 2 * WM * BN;  // [PARTS][BN]
   const auto srs = __builtin_amdgcn_make_buffer_rsrc(d.stats, 0, 0x7fffffff, 0x00020000);
   auto put = [&](long idx, float v) {
     if (SC1) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), srs, (int)(idx * 4), 0, 16 /*sc1*/);
     else d.stats[idx] = v;
   };
-  float cs[TN];
+  __syncthreads();  // (the LDS operand ring is dead)
+  // the shift: element (0, j, 0) of a lane < 32 of the partial's first wave row is its first row
+  if (wm % WPP == 0 && lane < 32) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {  // pass 1: the column sums
+    for (int j = 0; j < TN; ++j)
+      kshift[(wm / WPP) * BN + wn * WTN + 32 * j + lane] = RAW ? acc[0][j][0] : act_apply(acc[0][j][0] + bias[j], act);
+  }
+  __syncthreads();
+  float cs[TN], cq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
     cs[j] = 0.f;
+    cq[j] = 0.f;
     const int col = col_base + 32 * j;
+    const float k = kshift[(wm / WPP) * BN + wn * WTN + 32 * j + (lane & 31)];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
         if (col >= N || row >= M) continue;
-        cs[j] += RAW ? acc[i][j][e] : act_apply(acc[i][j][e] + bias[j], act);
+        const float dv = (RAW ? acc[i][j][e] : act_apply(acc[i][j][e] + bias[j], act)) - k;
+        cs[j] += dv;
+        cq[j] = fmaf(dv, dv, cq[j]);
       }
   }
-  __syncthreads();  // (the LDS operand ring is dead)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const float v = cs[j] + __shfl_xor(cs[j], 32);
-    if (lane < 32) red[wm * BN + wn * WTN + 32 * j + lane] = v;
-  }
-  __syncthreads();
-  for (int cl = tid; cl < BN; cl += NT) {
-    const int col = tn * BN + cl;
-    if (col >= N) continue;
-#pragma unroll
-    for (int sp = 0; sp < PARTS; ++sp) {
-      const long part = (long)tm * PARTS + sp;
-      if (part * PR >= M) break;
-      float v = 0.f;
-#pragma unroll
-      for (int r = sp * WPP; r < (sp + 1) * WPP; ++r) v += red[r * BN + cl];
-      put((part * 2 + 0) * N + col, v);
-      tmean[sp * BN + cl] = v / (float)min((long)PR, (long)M - part * PR);
+    const float v2 = cq[j] + __shfl_xor(cq[j], 32);
+    if (lane < 32) {
+      red[(wm * 2 + 0) * BN + wn * WTN + 32 * j + lane] = v;
+      red[(wm * 2 + 1) * BN + wn * WTN + 32 * j + lane] = v2;
     }
   }
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {  // pass 2: squares about the partial's mean
-    const int col = col_base + 32 * j;
-    const float m = tmean[(wm / WPP) * BN + wn * WTN + 32 * j + (lane & 31)];
-    cs[j] = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
-        if (col >= N || row >= M) continue;
-        const float dv = (RAW ? acc[i][j][e] : act_apply(acc[i][j][e] + bias[j], act)) - m;
-        cs[j] = fmaf(dv, dv, cs[j]);
-      }
-  }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const float v = cs[j] + __shfl_xor(cs[j], 32);
-    if (lane < 32) red[wm * BN + wn * WTN + 32 * j + lane] = v;  // (pass 1's reads are behind the barrier)
-  }
-  __syncthreads();
   for (int cl = tid; cl < BN; cl += NT) {
     const int col = tn * BN + cl;
     if (col >= N) continue;
@@ -196,10 +178,15 @@ __device__ __forceinline__ void bn_tile_stats(const GemmDesc& d, const f32x16 (&
     for (int sp = 0; sp < PARTS; ++sp) {
       const long part = (long)tm * PARTS + sp;
       if (part * PR >= M) break;
-      float v = 0.f;
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int r = sp * WPP; r < (sp + 1) * WPP; ++r) v += red[r * BN + cl];
-      put((part * 2 + 1) * N + col, v);
+      for (int r = sp * WPP; r < (sp + 1) * WPP; ++r) {
+        s1 += red[(r * 2 + 0) * BN + cl];
+        s2 += red[(r * 2 + 1) * BN + cl];
+      }
+      const float n = (float)min((long)PR, (long)M - part * PR), k = kshift[sp * BN + cl];
+      put((part * 2 + 0) * N + col, fmaf(n, k, s1));
+      put((part * 2 + 1) * N + col, fmaxf(s2 - s1 * (s1 / n), 0.f));
     }
   }
 }
@@ -808,7 +795,7 @@ inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* 
 // value is the one the unfused chain uses (this kernel's epilogue for y and the column partials,
 // bn_finalize_kernel for mean / invstd and the running statistics, bn_apply(_frag) for the
 // output and its split), in the same order, so both chains give the same bits.
-// LDS (bytes): [0, 8K) column partials [WM + 1][BN] f32; [8K, 20K) fp64 sums [3][4][BN];
+// LDS (bytes): [0, 8K) column partials [2 WM + 1][BN] f32; [8K, 20K) fp64 sums [3][4][BN];
 // [20K, 21K) scale / shift [2][BN]; 21K flag; [22K, ..) the tile [BM][BN + 4] f32.
 template <int BM, int BN, int WM, int WTN, int TM, int TN, int NT>
 __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM][TN], unsigned char* lds, int tm,
