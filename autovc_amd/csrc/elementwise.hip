@@ -112,18 +112,27 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int
     const long M = (long)count;
     double s = 0.0, a1 = 0.0, a2 = 0.0;
     if (c < C) {
-      const double K = (double)stats[c] / (double)min((long)part_rows, M);
+      // partials p = grp, grp + 4, ... combined in order; the next four partials' loads are issued
+      // before the current four are combined, and the shift K (partial 0's mean) comes with the
+      // first batch (one round trip per partial measured 27 vs 10 us per C3 call)
       const double inv_pr = 1.0 / (double)part_rows;
       const double inv_last = 1.0 / (double)(M - (long)(nparts - 1) * part_rows);  // the short last partial
-      // partials p = grp, grp + 4, ... in order, four loads in flight (the fp64 combine does not
-      // pipeline on its own: one round trip per partial measured 27 vs 10 us per C3 call)
+      const float S0 = stats[c];
+      float Sv[4], Qv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int p = grp + 4 * u;
+        Sv[u] = p < nparts ? stats[((long)p * 2 + 0) * C + c] : 0.f;
+        Qv[u] = p < nparts ? stats[((long)p * 2 + 1) * C + c] : 0.f;
+      }
+      const double K = (double)S0 * (nparts == 1 ? inv_last : inv_pr);
       for (int p0 = grp; p0 < nparts; p0 += 16) {
-        float Sv[4], Qv[4];
+        float Sn[4], Qn[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int p = p0 + 4 * u;
-          Sv[u] = p < nparts ? stats[((long)p * 2 + 0) * C + c] : 0.f;
-          Qv[u] = p < nparts ? stats[((long)p * 2 + 1) * C + c] : 0.f;
+          const int p = p0 + 16 + 4 * u;
+          Sn[u] = p < nparts ? stats[((long)p * 2 + 0) * C + c] : 0.f;
+          Qn[u] = p < nparts ? stats[((long)p * 2 + 1) * C + c] : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -132,6 +141,11 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int
             const long n = min((long)part_rows, M - (long)p * part_rows);
             bn_combine(Sv[u], Qv[u], n, p == nparts - 1 ? inv_last : inv_pr, K, s, a1, a2);
           }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          Sv[u] = Sn[u];
+          Qv[u] = Qn[u];
         }
       }
     }

@@ -110,46 +110,42 @@ __device__ __forceinline__ float split_unscale(const unsigned* amax_a, const uns
 
 // BatchNorm column partials of one output tile (train mode).  Per column and partial (PARTS = 1:
 // the tile's rows; 2: the two 128-row halves of a 256-row tile, make_plan's stats granularity):
-// stats[part][0][col] = S, the sum of the column's valid rows, and stats[part][1][col] = the sum
-// of squares about the partial's mean S / n.  Both come from ONE pass over the values shifted by
-// k, the partial's first row of that column (broadcast through LDS): S = S1 + n k and
-// Q = S2 - S1^2 / n with S1 = sum (x - k), S2 = sum (x - k)^2.  A sample of the column lies within
-// a few standard deviations of its mean, so nothing like E[x^2] - E[x]^2 with fp32 sums is ever
-// formed: at B = 1 a decoder conv channel's mean is ~17 standard deviations and that difference
-// cost ~2^-12 relative in the variance (dec.conv0 5.9e-5 local error against fp32 CPU's 6.9e-6,
-// DESIGN §3).  bn_finalize_kernel combines the partials in fp64 about a common shift.  val(i, j, e)
-// = act(acc + bias) as the epilogue stored it (RAW: acc already holds it).  Every producer (the
-// three GEMM epilogues, the fused BN one) goes through here, so fused and unfused chains form the
-// same bits.  SC1: write-through stores (the fused BN's in-launch hand-off).  red: >= (2 WM +
-// PARTS) * BN floats of LDS, free.
+// stats[part][0][col] = S, the sum of the column's valid rows, and stats[part][1][col] = Q, the sum
+// of squares about the partial's mean S / n.  One pass: each wave sums its rows of a column shifted
+// by k, the wave's first row of that column (a lane shuffle away), so S_w = S1 + n_w k and
+// Q_w = S2 - S1^2 / n_w carry no cancellation beyond ((mean - k) / std)^2 -- a sample lies within a
+// few standard deviations of its mean; the wave rows of a partial are then merged exactly (Chan:
+// Q = sum Q_w + sum n_w (S_w / n_w - S / n)^2).  So the variance never comes out of
+// E[x^2] - E[x]^2 with fp32 sums: at B = 1 a decoder conv channel's mean is ~17 standard deviations
+// and that difference cost ~2^-12 relative in the variance (dec.conv0 5.9e-5 local error against
+// fp32 CPU's 6.9e-6).  bn_finalize_kernel combines the partials in fp64 about a common
+// shift.  val(i, j, e) = act(acc + bias) as the epilogue stored it (RAW: acc already holds it).
+// Every producer (the three GEMM epilogues, the fused BN one) goes through here, so fused and
+// unfused chains form the same bits.  SC1: write-through stores (the fused BN's in-launch
+// hand-off).  red: >= 2 WM BN floats of LDS, free.
 template <int BM, int BN, int WM, int WTN, int TM, int TN, int PARTS, bool RAW, bool SC1>
 __device__ __forceinline__ void bn_tile_stats(const GemmDesc& d, const f32x16 (&acc)[TM][TN], const float (&bias)[TN],
                                               float* red, int tm, int tn, int wm, int wn, int lane, int tid, int NT,
                                               int row_base, int col_base) {
   static_assert(PARTS == 1 || (BM == 256 && WM % 2 == 0), "two 128-row partials per 256-row tile");
-  constexpr int PR = BM / PARTS, WPP = WM / PARTS;  // rows and wave rows per partial
+  constexpr int PR = BM / PARTS, WPP = WM / PARTS, WTM = BM / WM;  // rows / wave rows per partial
   const int M = d.M, N = d.N, act = d.act;
-  float* kshift = red + 2 * WM * BN;  // [PARTS][BN]
   const auto srs = __builtin_amdgcn_make_buffer_rsrc(d.stats, 0, 0x7fffffff, 0x00020000);
   auto put = [&](long idx, float v) {
     if (SC1) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), srs, (int)(idx * 4), 0, 16 /*sc1*/);
     else d.stats[idx] = v;
   };
-  __syncthreads();  // (the LDS operand ring is dead)
-  // the shift: element (0, j, 0) of a lane < 32 of the partial's first wave row is its first row
-  if (wm % WPP == 0 && lane < 32) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      kshift[(wm / WPP) * BN + wn * WTN + 32 * j + lane] = RAW ? acc[0][j][0] : act_apply(acc[0][j][0] + bias[j], act);
-  }
-  __syncthreads();
+  // this wave row's valid rows (its first row, row_base of lane 0, is tm * BM + wm * WTM)
+  const long wrow0 = (long)tm * BM + (long)wm * WTM;
+  const float nw = (float)max(0L, min((long)WTM, (long)M - wrow0));
   float cs[TN], cq[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    cs[j] = 0.f;
-    cq[j] = 0.f;
     const int col = col_base + 32 * j;
-    const float k = kshift[(wm / WPP) * BN + wn * WTN + 32 * j + (lane & 31)];
+    // the shift: element (0, j, 0) of lane (lane & 31) holds row wrow0 of this lane's column
+    const float v00 = RAW ? acc[0][j][0] : act_apply(acc[0][j][0] + bias[j], act);
+    const float k = __shfl(v00, lane & 31);
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -157,17 +153,21 @@ __device__ __forceinline__ void bn_tile_stats(const GemmDesc& d, const f32x16 (&
         const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
         if (col >= N || row >= M) continue;
         const float dv = (RAW ? acc[i][j][e] : act_apply(acc[i][j][e] + bias[j], act)) - k;
-        cs[j] += dv;
-        cq[j] = fmaf(dv, dv, cq[j]);
+        s1 += dv;
+        s2 = fmaf(dv, dv, s2);
       }
+    s1 += __shfl_xor(s1, 32);
+    s2 += __shfl_xor(s2, 32);
+    // the wave row's (S_w, Q_w) of this column
+    cs[j] = nw > 0.f ? fmaf(nw, k, s1) : 0.f;
+    cq[j] = nw > 0.f ? fmaxf(s2 - s1 * (s1 / nw), 0.f) : 0.f;
   }
+  __syncthreads();  // (the LDS operand ring is dead)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const float v = cs[j] + __shfl_xor(cs[j], 32);
-    const float v2 = cq[j] + __shfl_xor(cq[j], 32);
     if (lane < 32) {
-      red[(wm * 2 + 0) * BN + wn * WTN + 32 * j + lane] = v;
-      red[(wm * 2 + 1) * BN + wn * WTN + 32 * j + lane] = v2;
+      red[(wm * 2 + 0) * BN + wn * WTN + 32 * j + lane] = cs[j];
+      red[(wm * 2 + 1) * BN + wn * WTN + 32 * j + lane] = cq[j];
     }
   }
   __syncthreads();
@@ -178,15 +178,22 @@ __device__ __forceinline__ void bn_tile_stats(const GemmDesc& d, const f32x16 (&
     for (int sp = 0; sp < PARTS; ++sp) {
       const long part = (long)tm * PARTS + sp;
       if (part * PR >= M) break;
-      float s1 = 0.f, s2 = 0.f;
+      const float n = (float)min((long)PR, (long)M - part * PR);
+      float S = 0.f;
 #pragma unroll
-      for (int r = sp * WPP; r < (sp + 1) * WPP; ++r) {
-        s1 += red[(r * 2 + 0) * BN + cl];
-        s2 += red[(r * 2 + 1) * BN + cl];
+      for (int r = sp * WPP; r < (sp + 1) * WPP; ++r) S += red[(r * 2 + 0) * BN + cl];
+      const float m = S / n;
+      float Q = 0.f;
+#pragma unroll
+      for (int r = sp * WPP; r < (sp + 1) * WPP; ++r) {  // Chan's merge of the wave rows
+        const float nr = (float)max(0L, min((long)WTM, (long)M - ((long)tm * BM + (long)r * WTM)));
+        if (nr > 0.f) {
+          const float dm = red[(r * 2 + 0) * BN + cl] / nr - m;
+          Q += red[(r * 2 + 1) * BN + cl] + nr * dm * dm;
+        }
       }
-      const float n = (float)min((long)PR, (long)M - part * PR), k = kshift[sp * BN + cl];
-      put((part * 2 + 0) * N + col, fmaf(n, k, s1));
-      put((part * 2 + 1) * N + col, fmaxf(s2 - s1 * (s1 / n), 0.f));
+      put((part * 2 + 0) * N + col, S);
+      put((part * 2 + 1) * N + col, Q);
     }
   }
 }
@@ -795,7 +802,7 @@ inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* 
 // value is the one the unfused chain uses (this kernel's epilogue for y and the column partials,
 // bn_finalize_kernel for mean / invstd and the running statistics, bn_apply(_frag) for the
 // output and its split), in the same order, so both chains give the same bits.
-// LDS (bytes): [0, 8K) column partials [2 WM + 1][BN] f32; [8K, 20K) fp64 sums [3][4][BN];
+// LDS (bytes): [0, 8K) column partials [2 WM][BN] f32; [8K, 20K) fp64 sums [3][4][BN];
 // [20K, 21K) scale / shift [2][BN]; 21K flag; [22K, ..) the tile [BM][BN + 4] f32.
 template <int BM, int BN, int WM, int WTN, int TM, int TN, int NT>
 __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM][TN], unsigned char* lds, int tm,
@@ -858,17 +865,27 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
     // before its first add measured 0.08 ms slower per C2 forward)
     double s = 0.0, a1 = 0.0, a2 = 0.0;
     if (col < d.N) {
-      const double K = (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, col * 4, 0, 16)) /
-                       (double)min(BM, d.M);
+      // (bn_finalize_kernel's order and loads: K with the first batch, the next batch's loads issued
+      // before the current one is combined)
       const double inv_pr = 1.0 / (double)BM;
       const double inv_last = 1.0 / (double)(d.M - (tilesM - 1) * BM);  // the short last partial
-      for (int p0 = grp; p0 < tilesM; p0 += 16) {  // four partials' loads in flight, combined in order
-        float Sv[4], Qv[4];
+      auto ld = [&](int p, int h) {
+        return p < tilesM ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + h) * d.N + col) * 4, 0, 16)) : 0.f;
+      };
+      const float S0 = ld(0, 0);
+      float Sv[4], Qv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        Sv[u] = ld(grp + 4 * u, 0);
+        Qv[u] = ld(grp + 4 * u, 1);
+      }
+      const double K = (double)S0 * (tilesM == 1 ? inv_last : inv_pr);
+      for (int p0 = grp; p0 < tilesM; p0 += 16) {
+        float Sn[4], Qn[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int p = p0 + 4 * u;
-          Sv[u] = p < tilesM ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 0) * d.N + col) * 4, 0, 16)) : 0.f;
-          Qv[u] = p < tilesM ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + 1) * d.N + col) * 4, 0, 16)) : 0.f;
+          Sn[u] = ld(p0 + 16 + 4 * u, 0);
+          Qn[u] = ld(p0 + 16 + 4 * u, 1);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -877,6 +894,11 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
             const long n = min(BM, d.M - p * BM);
             bn_combine(Sv[u], Qv[u], n, p == tilesM - 1 ? inv_last : inv_pr, K, s, a1, a2);
           }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          Sv[u] = Sn[u];
+          Qv[u] = Qn[u];
         }
       }
     }
