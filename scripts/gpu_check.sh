@@ -90,6 +90,7 @@ for step in "$@"; do
     pmclong) run pmcfl 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcFL -o long -- python3 bench.py --mode long --steps 2 --warmup 1 --no-cpu --no-timing && run pmcwl 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcWL -o long -- python3 bench.py --mode long --steps 2 --warmup 1 --no-cpu --no-timing ;;
     abc2) run abc2 700 bash scripts/ab_c2.sh ab/prev_bnstats.so ;;
     dpprod) run dpprod 600 python -u -m pytest tests/test_gpu_dp.py tests/test_gpu_production.py -x -v -s --timeout 400 -p no:cacheprovider ;;
+    fragchain) rm -f gpurun_out/abe.log && run fragchain 600 bash scripts/ab_env.sh AUTOVC_FRAG_CHAIN 0 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
