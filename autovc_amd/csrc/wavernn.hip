@@ -975,12 +975,14 @@ __device__ __forceinline__ bool fc_phase(const WrLoop& p, int f, int i, unsigned
   float* xs = sm + kWrXs;
   float* sums = sm + kWrSin;
   int* flags = reinterpret_cast<int*>(sm + kWrFlags);
-  const int n0 = f * 8 + 2 * w;
-  float4 wv[2][kJ4];
+  // wave w: output rows [4 (w & 1), + 4) of the 8 against staged rows [12 (w >> 1), + 12) -- the
+  // per-step kernel's (output row, fold row) partials with half its LDS reads per wave
+  const int og = 4 * (w & 1), rh = 12 * (w >> 1);
+  float4 wv[4][kJ4];
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < 4; ++g)
 #pragma unroll
-    for (int j = 0; j < kJ4; ++j) wv[g][j] = wrow4(W, min(n0 + g, a.Fc - 1), K, lane + 64 * j);
+    for (int j = 0; j < kJ4; ++j) wv[g][j] = wrow4(W, min(f * 8 + og + g, a.Fc - 1), K, lane + 64 * j);
   const int which = WHICH == 1 ? IN_T2A3 : IN_Y1A4;
   float4 v[kStage4];
   lstage_pre(a, which, i, 0, K, tid, v);
@@ -997,9 +999,22 @@ __device__ __forceinline__ bool fc_phase(const WrLoop& p, int f, int i, unsigned
     lstage_post(a, which, i, rb, K, tid, v);
     lstage_store(K, tid, v, xs);
     __syncthreads();
-    float acc[2][kRC];
-    rows_dot<2>(wv, xs, K, lane, acc);
-    reduce_lanes<2>(acc, w, lane, sm + kWrRed, sums);
+    float acc[4][12];
+    rows_dot_part<4, 12>(wv, xs, K, lane, rh, acc);
+    float* red = sm + kWrRed;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int r = 0; r < 12; ++r) red[((og + g) * kRC + rh + r) * kRP + lane] = acc[g][r];
+    __syncthreads();
+    if (tid < 8 * kRC) {  // reduce_lanes' fixed-order 64-lane sums, sums[o * kRC + rr]
+      const float* row = red + tid * kRP;
+      float sacc = 0.f;
+#pragma unroll 8
+      for (int l = 0; l < 64; ++l) sacc += row[l];
+      sums[tid] = sacc;
+    }
+    __syncthreads();
     if (ep) {
       const int rr = tid - o * nr;
       st_sc1(y, (long)(rb + rr) * a.Fc + n, fmaxf(sums[o * kRC + rr] + bz, 0.f));
