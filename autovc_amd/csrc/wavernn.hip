@@ -1114,21 +1114,19 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
   // hidden sums of both layers (skipped after the last step), placed where the role would wait
   // anyway: FC1 after its product, FC2 and OUT before waiting for theirs.  One op list walked by one
   // switch, so every phase is instantiated once.
-  // (fc2 workgroups split the hidden sums around their phase: layer 2's before it, layer 1's after,
-  // since both together take longer than fc1 does and would delay fc2)
-  enum : int { OP_HID = 0, OP_HID1 = 1, OP_IN1 = 2, OP_IN2 = 3, OP_FC1 = 4, OP_FC2 = 5, OP_OUT = 6, OP_HID2 = 7 };
+  enum : int { OP_HID = 0, OP_IN1 = 2, OP_IN2 = 3, OP_FC1 = 4, OP_FC2 = 5, OP_OUT = 6 };
   // the role's op list, packed 4 bits per op (no indexed array: it would live in scratch)
   const unsigned seq = role == WR_FC1   ? (OP_IN1 | OP_IN2 << 4 | OP_FC1 << 8 | OP_HID << 12)
-                       : role == WR_FC2 ? (OP_IN1 | OP_IN2 << 4 | OP_HID2 << 8 | OP_FC2 << 12 | OP_HID1 << 16)
+                       : role == WR_FC2 ? (OP_IN1 | OP_IN2 << 4 | OP_HID << 8 | OP_FC2 << 12)
                        : role == WR_OUT ? (OP_IN1 | OP_IN2 << 4 | OP_HID << 8 | OP_OUT << 12)
                                         : (OP_IN1 | OP_IN2 << 4 | OP_HID << 8);
-  const int nops = role == WR_NONE ? 3 : role == WR_FC2 ? 5 : 4;
+  const int nops = role == WR_NONE ? 3 : 4;
   bool ok = true;
   int i = -1;  // step -1: only the hidden sums of step 0 (h_{-1} = 0)
   for (; ok && i < L; ++i) {
     for (int o = 0; o < nops && ok; ++o) {
       const int op = (int)((seq >> (4 * o)) & 15u);
-      const bool hid = op == OP_HID || op == OP_HID1 || op == OP_HID2;
+      const bool hid = op == OP_HID;
       if (hid ? i + 1 >= L : i < 0) continue;
       const bool stamp = p.stamps && i >= 0 && i < p.nstamp && tid == 0;
       if (tid == 0) {  // (read by wr_wait's stamp, same thread)
@@ -1138,8 +1136,6 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
       if (stamp) p.stamps[((long)wg * p.nstamp + i) * 24 + 3 * op] = __builtin_amdgcn_s_memrealtime();
       switch (op) {
         case OP_HID: ok = hid_phase(p, i + 1, E, wr_sm, nw); break;
-        case OP_HID1: ok = gru_phase<1, true>(p, i + 1, E, wr_sm, nw, ebi1, ebh1); break;
-        case OP_HID2: ok = gru_phase<2, true>(p, i + 1, E, wr_sm, nw, ebi2, ebh2); break;
         case OP_IN1: ok = gru_phase<1, false>(p, i, E, wr_sm, nw, ebi1, ebh1); break;
         case OP_IN2: ok = gru_phase<2, false>(p, i, E, wr_sm, nw, ebi2, ebh2); break;
         case OP_FC1: ok = fc_phase<1>(p, wg, i, E, wr_sm, nw); break;
