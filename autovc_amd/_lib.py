@@ -60,6 +60,7 @@ _SIGS = {
     "avc_loss_forward": [_P, _I, _Z, _P, _P, _P, _I, _P],
     "avc_loss_backward": [_I, _Z, _P, _P, _P, _P, _P, _I, _P],
     "avc_clip_adam_ema": [_P, _Z, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, ctypes.c_double, _P, _P],
+    "avc_clip_adam_ema_dev": [_P, _Z, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, ctypes.c_double, _P, _P, _P],
     "avc_timing_enable": [_I],
     "avc_lstm_tune": [_I, _I],
     "avc_bptt_mode": [_I],
@@ -110,6 +111,7 @@ _SIGS = {
     "avc_embedding_mean_normalize": [_I, _I, _P, _P, _P],
     "avc_wavernn_param_count": [_I],
     "avc_wavernn_persist": [_I],
+    "avc_wavernn_fallbacks": [],
     "avc_wavernn_proj_tiled": [_I],
     "avc_wavernn_persist_eligible": [_I, _I, _I],
     "avc_debug_wavernn_inject": [_I],

@@ -14,7 +14,6 @@ from __future__ import annotations
 import ctypes
 import itertools
 import inspect
-import math
 import time
 
 import torch
@@ -53,12 +52,12 @@ class FusedAdam(torch.optim.Optimizer):
         self.model = model
         self.exp_avg = torch.zeros_like(model._flat_param)
         self.exp_avg_sq = torch.zeros_like(model._flat_param)
-        self._step = 0
+        self._step = 0  # updates requested (step() calls) since the count was last settled
         self._step_t = torch.tensor(0.0)
-        # the previous update's gradient norm, copied to pinned host memory behind the update, and
-        # the event after that copy: a non-finite norm means the device skipped that update
-        self._pending = None
-        self._norm_host = torch.empty(1, dtype=torch.float32, pin_memory=torch.cuda.is_available())
+        # updates the device skipped for a non-finite gradient norm (adam_ema_kernel), counted on
+        # the device: the kernel's bias correction uses _step - skips, so step() never waits for
+        # the norm; the host count is settled when the state is read (state_dict)
+        self._skips = torch.zeros(1, dtype=torch.int32, device=model._flat_param.device)
         for p, (off, n) in zip(params, model._flat_slices):
             self.state[p] = {"step": self._step_t, "exp_avg": self.exp_avg[off:off + n].view_as(p),
                              "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p)}
@@ -75,36 +74,31 @@ class FusedAdam(torch.optim.Optimizer):
         if not m._flat_valid():
             raise RuntimeError("parameters were re-allocated after the optimizer was built")
         g = self.param_groups[0]
-        self._settle()
         self._step += 1
-        self._step_t.fill_(float(self._step))
+        self._step_t.fill_(float(self._step))  # (provisional until _settle: skips not subtracted)
         norm = torch.empty((), dtype=torch.float32, device=m._flat_param.device)
         b1, b2 = g["betas"]
-        _lib.call("avc_clip_adam_ema", _lib.context(norm.device), m._flat_param.numel(),
+        # (the norm is always formed here, so the kernel's skip guard is always armed)
+        _lib.call("avc_clip_adam_ema_dev", _lib.context(norm.device), m._flat_param.numel(),
                   m._flat_param.data_ptr(), m._flat_grad.data_ptr(), self.exp_avg.data_ptr(),
                   self.exp_avg_sq.data_ptr(), None if ema is None else _lib.ptr(ema), float(g["lr"]),
                   float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), self._step,
-                  float(max_norm), float(ema_decay), norm.data_ptr(), _lib.stream(norm.device))
+                  float(max_norm), float(ema_decay), norm.data_ptr(), self._skips.data_ptr(),
+                  _lib.stream(norm.device))
         m._param_epoch += 1  # parameters changed outside torch's version counters
         self.last_grad_norm = norm
-        # (the norm is always formed here, so the kernel's skip guard is always armed)
-        self._norm_host.copy_(norm.reshape(1), non_blocking=True)
-        self._pending = torch.cuda.Event()
-        self._pending.record(torch.cuda.current_stream(norm.device))
         return loss
 
     def _settle(self):
-        """Account for the last update: when its gradient norm was not finite the device kept
-        parameters, moments and EMA (adam_ema_kernel), so that step did not happen and the count
-        (Adam's bias correction, the checkpoint's step) goes back.  The event has normally long
-        completed by the next step (a forward and backward were enqueued behind it)."""
-        ev, self._pending = self._pending, None
-        if ev is None:
-            return
-        ev.synchronize()
-        if not math.isfinite(float(self._norm_host[0])):
-            self._step -= 1
-            self._step_t.fill_(float(self._step))
+        """Fold the device's count of skipped updates into the host count: an update whose
+        gradient norm was not finite kept parameters, moments and EMA (adam_ema_kernel), so it did
+        not happen for Adam's bias correction or the checkpoint's step.  Waits for the device (only
+        where the state is read)."""
+        sk = int(self._skips.item())
+        if sk:
+            self._step -= sk
+            self._skips.zero_()
+        self._step_t.fill_(float(self._step))
 
     def state_dict(self):
         self._settle()
@@ -127,7 +121,7 @@ class FusedAdam(torch.optim.Optimizer):
                 steps.add(int(float(st[i]["step"])))
         if len(steps) > 1:
             raise ValueError("per-parameter Adam step counts differ; the fused update keeps one")
-        self._pending = None
+        self._skips.zero_()
         self._step = steps.pop() if steps else 0
         self._step_t.fill_(float(self._step))
         for g, sg in zip(self.param_groups, state_dict["param_groups"]):

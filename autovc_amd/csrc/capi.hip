@@ -526,6 +526,16 @@ int avc_clip_adam_ema(avc_context* ctx, size_t n, float* param, float* grad, flo
                        weight_decay, step, max_norm, ema_decay, norm_out, S(stream));
 }
 
+int avc_clip_adam_ema_dev(avc_context* ctx, size_t n, float* param, float* grad, float* exp_avg,
+                          float* exp_avg_sq, float* ema, float lr, float beta1, float beta2,
+                          float eps, float weight_decay, int calls, float max_norm, double ema_decay,
+                          float* norm_out, unsigned* skips, void* stream) {
+  AVC_CHECK_ARG(ctx && param && grad && exp_avg && exp_avg_sq && skips, "NULL pointer");
+  AVC_TRY(ensure_arena(ctx, optimizer_scratch()));
+  return clip_adam_ema(ctx, n, param, grad, exp_avg, exp_avg_sq, ema, lr, beta1, beta2, eps,
+                       weight_decay, calls, max_norm, ema_decay, norm_out, S(stream), skips);
+}
+
 int avc_generator_param_count(void) { return P_COUNT; }
 
 int avc_generator_forward(avc_context* ctx, int T, int B, const float* const* params,

@@ -67,6 +67,6 @@ int loss_backward(int kind, size_t n, const float* a, const float* b, const floa
 size_t optimizer_scratch();
 int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, float* v, float* ema,
                   float lr, float b1, float b2, float eps, float wd, int step, float max_norm,
-                  double ema_decay, float* norm_out, hipStream_t s);
+                  double ema_decay, float* norm_out, hipStream_t s, unsigned* skips = nullptr);
 
 }  // namespace avc

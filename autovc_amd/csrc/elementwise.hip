@@ -112,30 +112,34 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int
     const long M = (long)count;
     double s = 0.0, a1 = 0.0, a2 = 0.0;
     if (c < C) {
-      // partials p = grp, grp + 4, ... combined in order; the next four partials' loads are issued
-      // before the current four are combined, and the shift K (partial 0's mean) comes with the
-      // first batch (one round trip per partial measured 27 vs 10 us per C3 call)
+      // partials p = grp, grp + 4, ... combined in order (the fused-BN epilogue's order, gemm.hip
+      // bnf_epilogue: same bits); the shift K (partial 0's mean) comes with the first batch.  The
+      // loads go out kB partials per thread at a time, the next batch's before the current one is
+      // combined: the combine is a chain of dependent fp64 adds, the loads a round trip each batch,
+      // and with 4 per batch the C3 call (256 partials x 512 channels on 8 workgroups) took 24.6 us
+      // in round trips (round 4); 16 per batch takes four.
+      constexpr int kB = 16;
       const double inv_pr = 1.0 / (double)part_rows;
       const double inv_last = 1.0 / (double)(M - (long)(nparts - 1) * part_rows);  // the short last partial
       const float S0 = stats[c];
-      float Sv[4], Qv[4];
+      float Sv[kB], Qv[kB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kB; ++u) {
         const int p = grp + 4 * u;
         Sv[u] = p < nparts ? stats[((long)p * 2 + 0) * C + c] : 0.f;
         Qv[u] = p < nparts ? stats[((long)p * 2 + 1) * C + c] : 0.f;
       }
       const double K = (double)S0 * (nparts == 1 ? inv_last : inv_pr);
-      for (int p0 = grp; p0 < nparts; p0 += 16) {
-        float Sn[4], Qn[4];
+      for (int p0 = grp; p0 < nparts; p0 += 4 * kB) {
+        float Sn[kB], Qn[kB];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int p = p0 + 16 + 4 * u;
+        for (int u = 0; u < kB; ++u) {
+          const int p = p0 + 4 * kB + 4 * u;
           Sn[u] = p < nparts ? stats[((long)p * 2 + 0) * C + c] : 0.f;
           Qn[u] = p < nparts ? stats[((long)p * 2 + 1) * C + c] : 0.f;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kB; ++u) {
           const int p = p0 + 4 * u;
           if (p < nparts) {
             const long n = min((long)part_rows, M - (long)p * part_rows);
@@ -143,7 +147,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kB; ++u) {
           Sv[u] = Sn[u];
           Qv[u] = Qn[u];
         }
@@ -411,14 +415,17 @@ __global__ void bn_bwd_reduce_kernel(int M, int C, const float* __restrict__ dou
 }
 
 // BnBound (bn_backward_frag): also bound max |dy| before dy exists, so the pass that writes dy can
-// write it already split.  From the reduce pass's per-channel max |dA| and max |x^| (mpart):
-//   |dy_c| = |g_c is_c (dA - k1_c - x^ k2_c)| <= |g_c is_c| (max|dA|_c + |k1_c| + max|x^|_c |k2_c|),
+// write it already split.  From the reduce pass's per-channel signed max / min of dA and max |x^|
+// (mpart):
+//   |dy_c| = |g_c is_c (dA - k1_c - x^ k2_c)| <= |g_c is_c| (max(maxdA_c - k1_c, k1_c - mindA_c) + max|x^|_c |k2_c|),
 // maximised over the channels into *bound (pre-zeroed).  The split's power-of-two scale then
 // comes from the bound instead of the exact max: a bound above the max by 2^k only moves the
 // operand k binades down inside f16's range, which leaves hi / lo (and so the product, unscaled
-// exactly) unchanged for every element above 2^-13 of the scaled max.
+// exactly) unchanged for every element above 2^-13 of the scaled max.  The signed range keeps the
+// bound tight when dA is mostly its channel mean k1 (round 4 used max|dA| + |k1|, which exceeds
+// the true max by |k1| / |dA - k1| there: many binades for a mean-dominated gradient).
 struct BnBound {
-  const float* mpart = nullptr;  // [R][2][C] per-block max |dA|, max |x^|
+  const float* mpart = nullptr;  // [R][3][C] per-block max dA, min dA, max |x^|
   const float* gamma = nullptr;
   const float* invstd = nullptr;
   float inv_count = 0.f;
@@ -431,25 +438,27 @@ __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const 
                                                             float* __restrict__ d_beta, int accumulate,
                                                             unsigned* __restrict__ amax, BnBound bb) {
   __shared__ double red[2][16][64];
-  __shared__ float redm[2][16][64];
+  __shared__ float redm[3][16][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   if (amax && blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;  // bn_bwd_apply_cols_kernel raises it
   const int c = blockIdx.x * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
-  float m1 = 0.f, m2 = 0.f;
+  float m1 = -INFINITY, m0 = INFINITY, m2 = 0.f;  // max dA, min dA, max |x^|
   if (c < C)
     for (int r = grp; r < R; r += 16) {
       s1 += part[((long)r * 2 + 0) * C + c];
       s2 += part[((long)r * 2 + 1) * C + c];
       if (bb.bound) {
-        m1 = fmaxf(m1, bb.mpart[((long)r * 2 + 0) * C + c]);
-        m2 = fmaxf(m2, bb.mpart[((long)r * 2 + 1) * C + c]);
+        m1 = fmaxf(m1, bb.mpart[((long)r * 3 + 0) * C + c]);
+        m0 = fminf(m0, bb.mpart[((long)r * 3 + 1) * C + c]);
+        m2 = fmaxf(m2, bb.mpart[((long)r * 3 + 2) * C + c]);
       }
     }
   red[0][grp][cl] = s1;
   red[1][grp][cl] = s2;
   redm[0][grp][cl] = m1;
   redm[1][grp][cl] = m2;
+  redm[2][grp][cl] = m0;
   __syncthreads();
   if (grp != 0 || c >= C) return;
   double t1 = 0.0, t2 = 0.0;
@@ -459,6 +468,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const 
     t2 += red[1][g][cl];
     m1 = fmaxf(m1, redm[0][g][cl]);
     m2 = fmaxf(m2, redm[1][g][cl]);
+    m0 = fminf(m0, redm[2][g][cl]);
   }
   sums[c] = (float)t1;
   sums[C + c] = (float)t2;
@@ -468,7 +478,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const 
     // the apply pass's own k1 / k2 (sums as float, times 1 / M); a few ulps of slack for the
     // rounding of the apply's expression
     const float k1 = bb.training ? (float)t1 * bb.inv_count : 0.f, k2 = bb.training ? (float)t2 * bb.inv_count : 0.f;
-    const float b = fabsf(bb.gamma[c] * bb.invstd[c]) * (m1 + fabsf(k1) + m2 * fabsf(k2)) * 1.0001f;
+    const float rng = fmaxf(fmaxf(m1 - k1, k1 - m0), 0.f);  // max |dA - k1| over the channel's rows
+    const float b = fabsf(bb.gamma[c] * bb.invstd[c]) * (rng + m2 * fabsf(k2)) * 1.0001f;
     atomicMax(bb.bound, __float_as_uint(b));  // non-negative floats order as their bits
   }
 }
@@ -562,7 +573,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(int M, int C, const
   const int Q = C >> 2, P = 256 / Q;
   const int ph = threadIdx.x / Q, q = threadIdx.x - ph * Q;
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-  float mx1[4] = {0.f, 0.f, 0.f, 0.f}, mx2[4] = {0.f, 0.f, 0.f, 0.f};  // max |dA|, max |xh| (mpart)
+  // (mpart) max dA, min dA, max |xh|
+  float mx1[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, mn1[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+  float mx2[4] = {0.f, 0.f, 0.f, 0.f};
   if (ph < P) {
     BnQuad k;
     bn_quad_load(k, 4 * q, mean, invstd, gamma, beta);
@@ -579,7 +592,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(int M, int C, const
         const float dA = bnb_da(dd[e], xh, k.g[e], k.bt[e], act);
         s1[e] += dA;
         s2[e] += dA * xh;
-        mx1[e] = fmaxf(mx1[e], fabsf(dA));
+        mx1[e] = fmaxf(mx1[e], dA);
+        mn1[e] = fminf(mn1[e], dA);
         mx2[e] = fmaxf(mx2[e], fabsf(xh));
       }
     }
@@ -602,15 +616,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(int M, int C, const
   red[0][threadIdx.x] = make_float4(mx1[0], mx1[1], mx1[2], mx1[3]);
   red[1][threadIdx.x] = make_float4(mx2[0], mx2[1], mx2[2], mx2[3]);
   __syncthreads();
-  if (ph != 0) return;
-  float4 a = red[0][q], b = red[1][q];
-  for (int p = 1; p < P; ++p) {
-    const float4 u = red[0][p * Q + q], v = red[1][p * Q + q];
-    a.x = fmaxf(a.x, u.x); a.y = fmaxf(a.y, u.y); a.z = fmaxf(a.z, u.z); a.w = fmaxf(a.w, u.w);
-    b.x = fmaxf(b.x, v.x); b.y = fmaxf(b.y, v.y); b.z = fmaxf(b.z, v.z); b.w = fmaxf(b.w, v.w);
+  if (ph == 0) {
+    float4 a = red[0][q], b = red[1][q];
+    for (int p = 1; p < P; ++p) {
+      const float4 u = red[0][p * Q + q], v = red[1][p * Q + q];
+      a.x = fmaxf(a.x, u.x); a.y = fmaxf(a.y, u.y); a.z = fmaxf(a.z, u.z); a.w = fmaxf(a.w, u.w);
+      b.x = fmaxf(b.x, v.x); b.y = fmaxf(b.y, v.y); b.z = fmaxf(b.z, v.z); b.w = fmaxf(b.w, v.w);
+    }
+    reinterpret_cast<float4*>(mpart + ((long)blockIdx.y * 3 + 0) * C)[q] = a;
+    reinterpret_cast<float4*>(mpart + ((long)blockIdx.y * 3 + 2) * C)[q] = b;
   }
-  reinterpret_cast<float4*>(mpart + ((long)blockIdx.y * 2 + 0) * C)[q] = a;
-  reinterpret_cast<float4*>(mpart + ((long)blockIdx.y * 2 + 1) * C)[q] = b;
+  __syncthreads();
+  red[0][threadIdx.x] = make_float4(mn1[0], mn1[1], mn1[2], mn1[3]);
+  __syncthreads();
+  if (ph != 0) return;
+  float4 a = red[0][q];
+  for (int p = 1; p < P; ++p) {
+    const float4 u = red[0][p * Q + q];
+    a.x = fminf(a.x, u.x); a.y = fminf(a.y, u.y); a.z = fminf(a.z, u.z); a.w = fminf(a.w, u.w);
+  }
+  reinterpret_cast<float4*>(mpart + ((long)blockIdx.y * 3 + 1) * C)[q] = a;
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply4_kernel(int M, int C, const float* __restrict__ dout,
@@ -1151,7 +1176,8 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(long n, const float*
 
 // one block of 256: strided partial sums, then a fixed-order tree (deterministic)
 __global__ __launch_bounds__(256) void clip_coef_kernel(int nparts, const double* __restrict__ part, float max_norm,
-                                                        float* __restrict__ norm_out, float* __restrict__ coef) {
+                                                        float* __restrict__ norm_out, float* __restrict__ coef,
+                                                        unsigned* __restrict__ skips) {
   __shared__ double red[256];
   double s = 0.0;
   for (int p = threadIdx.x; p < nparts; p += 256) s += part[p];
@@ -1173,12 +1199,20 @@ __global__ __launch_bounds__(256) void clip_coef_kernel(int nparts, const double
   // a non-finite norm (a persistent recurrence that gave up writes NaN; in data-parallel training
   // the NaN reaches every rank through the all-reduce): the update below is skipped
   coef[1] = isfinite(norm) ? 0.f : 1.f;
+  // device count of skipped updates (avc_clip_adam_ema_dev): Adam's bias correction of this update
+  // uses step - skips, so the host never has to wait for the norm to know the step
+  unsigned sk = skips ? *skips : 0u;
+  if (skips && !isfinite(norm)) *skips = ++sk;
+  coef[2] = __uint_as_float(sk);
 }
 
+constexpr int kAdamTab = 8;
 struct AdamArgs {
   float c, lr, b1, b2, eps, wd, step_size, bc2_sqrt, ema_decay, ema_keep;
   int clip;
   int guard;  // coef[1] holds the skip flag of clip_coef_kernel
+  int tabled;  // step_size / bc2_sqrt from the tables below, indexed by the device skip count coef[2]
+  float ss[kAdamTab], bc[kAdamTab];  // the host's values for effective steps step, step - 1, ...
 };
 
 // one element of the fused clip + Adam + EMA update (torch.optim.Adam's foreach arithmetic)
@@ -1203,6 +1237,11 @@ __global__ __launch_bounds__(256) void adam_ema_kernel(long n, long n4, float* _
                                                        AdamArgs a) {
   if (a.guard && coef[1] != 0.f) return;  // non-finite gradient norm: parameters, moments, EMA kept
   a.c = a.clip ? coef[0] : 1.f;
+  if (a.tabled) {
+    const unsigned k = min(__float_as_uint(coef[2]), (unsigned)(kAdamTab - 1));
+    a.step_size = a.ss[k];
+    a.bc2_sqrt = a.bc[k];
+  }
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 p4 = reinterpret_cast<float4*>(p)[i], g4 = reinterpret_cast<float4*>(g)[i];
@@ -1361,7 +1400,7 @@ int bn_backward_frag(avc_context* ctx, int M, int C, const float* dout, const fl
   bn_geometry(M, C, R, rp);
   Scratch sc(ctx);
   AVC_TAKE(part, float, (size_t)R * 2 * C, sc);
-  AVC_TAKE(mpart, float, (size_t)R * 2 * C, sc);
+  AVC_TAKE(mpart, float, (size_t)R * 3 * C, sc);
   AVC_TAKE(sums, float, (size_t)2 * C, sc);
   bn_bwd_reduce4_kernel<<<dim3(1, R), 256, 0, s>>>(M, C, dout, y, mean, invstd, gamma, beta, act, rp, part, mpart, bound);
   BnBound bb;
@@ -1378,7 +1417,7 @@ int bn_backward_frag(avc_context* ctx, int M, int C, const float* dout, const fl
 
 int bn_backward_frag_rows(int M) { return (M + 31) / 32; }
 
-size_t bn_backward_frag_scratch(int M, int C) { return bn_backward_scratch(M, C) + (size_t)bn_backward_rows(M, C) * 2 * C * sizeof(float) + 256; }
+size_t bn_backward_frag_scratch(int M, int C) { return bn_backward_scratch(M, C) + (size_t)bn_backward_rows(M, C) * 3 * C * sizeof(float) + 256; }
 
 int colsum_finish(int R, int N, const float* part, float* out, int accumulate, hipStream_t s) {
   colsum_final_kernel<<<(N + 63) / 64, 1024, 0, s>>>(R, N, part, out, accumulate, nullptr);
@@ -1567,8 +1606,9 @@ size_t optimizer_scratch() { return 2048 * sizeof(double) + 512; }
 
 int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, float* v, float* ema,
                   float lr, float b1, float b2, float eps, float wd, int step, float max_norm,
-                  double ema_decay, float* norm_out, hipStream_t s) {
+                  double ema_decay, float* norm_out, hipStream_t s, unsigned* skips) {
   AVC_CHECK_ARG(step >= 1, "adam step counter starts at 1");
+  AVC_CHECK_ARG(!skips || max_norm > 0.f || norm_out, "adam skip count: needs the gradient norm");
   Scratch sc(ctx);
   const int nb = (int)std::min<size_t>(2048, (n + 255) / 256);
   AVC_TAKE(part, double, (size_t)nb, sc);
@@ -1576,14 +1616,22 @@ int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, floa
   const bool need_norm = max_norm > 0.f || norm_out != nullptr;
   if (need_norm) {
     sumsq_partial_kernel<<<nb, 256, 0, s>>>((long)n, g, part);
-    clip_coef_kernel<<<1, 256, 0, s>>>(nb, part, max_norm, norm_out, coef);
+    clip_coef_kernel<<<1, 256, 0, s>>>(nb, part, max_norm, norm_out, coef, skips);
   }
-  const double bc1 = 1.0 - std::pow((double)b1, step);
-  const double bc2 = 1.0 - std::pow((double)b2, step);
   AdamArgs a{};
   a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
-  a.step_size = (float)(lr / bc1);
-  a.bc2_sqrt = (float)std::sqrt(bc2);
+  // torch.optim.Adam's bias corrections in double (Python floats), for this step and, with a
+  // device skip count, for the steps it would be after k skipped updates
+  for (int k = 0; k < kAdamTab; ++k) {
+    const int st = std::max(1, step - k);
+    const double bc1 = 1.0 - std::pow((double)b1, st);
+    const double bc2 = 1.0 - std::pow((double)b2, st);
+    a.ss[k] = (float)(lr / bc1);
+    a.bc[k] = (float)std::sqrt(bc2);
+  }
+  a.step_size = a.ss[0];
+  a.bc2_sqrt = a.bc[0];
+  a.tabled = skips ? 1 : 0;
   a.ema_decay = (float)ema_decay;
   a.ema_keep = (float)(1.0 - ema_decay);
   a.clip = max_norm > 0.f ? 1 : 0;

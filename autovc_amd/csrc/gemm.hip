@@ -1056,10 +1056,15 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
     // fused BN: the barrier group of column tile tn (its tilesM row tiles) is the contiguous
     // dispatch range [tn * tilesM, (tn + 1) * tilesM), dealt evenly over the XCDs, so a group needs
     // only its own tilesM workgroups resident, never the whole grid (bnf_epilogue).
-    // Per XCD the row tiles are tm = x mod 8 under all tilesN column tiles: the same L2 reuse as
-    // tile_of's bands.
+    // Inside the group, dispatch index l = bid - tn * tilesM lands on XCD l % 8 (round-robin), and
+    // that XCD takes the contiguous band of tilesM / 8 row tiles starting at (l % 8) * tilesM / 8,
+    // the same band under every column tile.  The conv taps shift A by +-1 / +-2 frames (+-B rows),
+    // i.e. into the neighbouring row tile, which is then in the same band and the same L2.
+    // (Round 4 mapped tm = l, which dealt row tiles x, x + 8, ... to XCD x: every tap's neighbour
+    // tile sat in another XCD's L2, +46 % fetched bytes at C2.)  Speed only: any bijection is correct.
     tn = bid / tilesM;
-    tm = bid - tn * tilesM;
+    const int l = bid - tn * tilesM;
+    tm = (tilesM & 7) ? l : (l & 7) * (tilesM >> 3) + (l >> 3);
     (void)wgid;
   } else {
     tile_of(wgid, tilesM, tilesN, tm, tn);

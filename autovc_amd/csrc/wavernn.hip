@@ -1162,6 +1162,7 @@ __global__ __launch_bounds__(256, 1) void wr_loop_kernel(WrLoop p) {
 int g_wr_proj_tiled = 1;  // avc_wavernn_proj_tiled(): the LDS-tiled input projection (same bits)
 int g_wr_persist = 1;  // avc_wavernn_persist(): 1 (default) = the persistent sample loop where eligible
 int g_wr_inject = 0;   // avc_debug_wavernn_inject(): loop launches left that give up at once
+int g_wr_fallbacks = 0;  // avc_wavernn_fallbacks(): loop launches that gave up and were re-run per step
 unsigned long long* g_wr_stamps = nullptr;  // avc_debug_wavernn_stamps(): next loop launch's stamps
 int g_wr_nstamp = 0;
 
@@ -1190,7 +1191,12 @@ bool wr_loop_eligible(const WrStep& a) {
   return g_wr_persist && a.R <= kWrMaxChunks * kRC && 2 * nfc + a.R <= G && a.L >= 1 && G <= wr_loop_capacity();
 }
 
-int wr_loop_run(avc_context* ctx, const WrStep& a, hipStream_t s, double macs) {
+// gave_up: set when THIS launch abandoned a bounded wait (a workgroup was not resident, e.g. CUs
+// held by another process); its samples are NaN and the caller re-runs the call on the per-step path.
+// A failure an earlier call left on the context is returned as before, with gave_up false.
+int wr_loop_run(avc_context* ctx, const WrStep& a, hipStream_t s, double macs, unsigned long long* stamps,
+                bool* gave_up) {
+  *gave_up = false;
   AVC_TRY(persist_guard(ctx));
   const int G = a.H / 2;
   unsigned* region = nullptr;
@@ -1214,15 +1220,16 @@ int wr_loop_run(avc_context* ctx, const WrStep& a, hipStream_t s, double macs) {
     --g_wr_inject;
     p.spin_limit = 0;
   }
-  p.stamps = g_wr_stamps;
-  p.nstamp = g_wr_stamps ? g_wr_nstamp : 0;
-  g_wr_stamps = nullptr;
+  p.stamps = stamps;
+  p.nstamp = stamps ? g_wr_nstamp : 0;
   void* args[] = {&p};
   hipEvent_t ev = timing_begin(TC_WAVERNN, s);
   AVC_TRY(coresident_dispatch(ctx, (const void*)wr_loop_kernel, dim3(G), dim3(256), args, kWrLdsFloats * 4, s));
   if (ev) timing_end(TC_WAVERNN, ev, s, (double)a.L * 2.0 * macs * a.R, (double)a.L * 4.0 * macs);
   AVC_HIP(hipStreamSynchronize(s));
-  return persist_guard(ctx);  // this launch gave up: its samples are NaN, report it now
+  const int rc = persist_guard(ctx);  // this launch gave up: its samples are NaN
+  *gave_up = rc == AVC_ERR_DEVICE;
+  return rc;
 }
 
 // numpy.linspace(a, b, n)[k] in float64: a + k·(b - a)/(n - 1), the last point exactly b
@@ -1374,6 +1381,10 @@ int avc_wavernn_upsample(avc_context* ctx, const int* dims, int T, const float* 
 int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* const* params, const float* mel,
                          int batched, int target, int overlap, int mol, unsigned long long seed,
                          const float* x_teacher, float* logits, float* samples, float* wave, void* stream) {
+  // the stamp buffer (avc_debug_wavernn_stamps) belongs to this call only, whichever path it takes:
+  // a later loop launch never writes into a buffer the caller may have freed since
+  unsigned long long* const stamps = g_wr_stamps;
+  g_wr_stamps = nullptr;
   AVC_CHECK_ARG(ctx && dims && params && mel, "NULL pointer");
   const WrDims d{dims[0], dims[1], dims[2], dims[3], dims[4], dims[5], dims[6], dims[7], dims[8], dims[9], dims[10]};
   AVC_TRY(check_dims(d));
@@ -1461,8 +1472,22 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
   // per step
   const double macs = 6.0 * H * H + 3.0 * H * (H + A) + 3.0 * H * H + (double)d.Fc * (H + A) +
                       (double)d.Fc * (d.Fc + A) + (double)d.NC * d.Fc;
-  if (wr_loop_eligible(a)) {
-    AVC_TRY(wr_loop_run(ctx, a, s, macs));
+  bool per_step = !wr_loop_eligible(a);
+  if (!per_step) {
+    bool gave_up = false;
+    const int rc = wr_loop_run(ctx, a, s, macs, stamps, &gave_up);
+    if (rc != AVC_OK && !gave_up) return rc;
+    if (gave_up) {
+      // The loop needs all rnn_dims / 2 workgroups resident at once; with CUs held elsewhere it gave
+      // up (persist_guard has reset the counter regions).  The per-step graph path forms the same
+      // sums in the same order (bit-identical samples), so the call is re-run there from a fresh state.
+      ++g_wr_fallbacks;
+      wr_init_state_kernel<<<ew(2 * R * (long)H), 256, 0, s>>>((int)R, d.H, d.Fc, a.step, a.done, x_prev, h1, h2);
+      AVC_LAUNCH_CHECK();
+      per_step = true;
+    }
+  }
+  if (!per_step) {
   } else if (chunks > 1) {
     AVC_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
     int rc = AVC_OK;
@@ -1532,6 +1557,8 @@ int avc_debug_wavernn_stamps(void* buf, int steps) {
   avc::g_wr_nstamp = steps;
   return AVC_OK;
 }
+
+int avc_wavernn_fallbacks(void) { return avc::g_wr_fallbacks; }
 
 int avc_wavernn_persist_eligible(int rows, int rnn_dims, int fc_dims) {
   avc::WrStep a{};

@@ -222,6 +222,15 @@ int avc_clip_adam_ema(avc_context* ctx, size_t n, float* param, float* grad, flo
                       float* exp_avg_sq, float* ema, float lr, float beta1, float beta2,
                       float eps, float weight_decay, int step, float max_norm, double ema_decay,
                       float* norm_out, void* stream);
+/* The same update with the count of skipped updates kept on the device: `calls` counts every
+ * update requested so far (this one included); *skips (device word, zero-initialised by the
+ * caller) counts those skipped for a non-finite norm and is raised by this call when it skips.
+ * Adam's bias correction uses calls - *skips (host-computed values for up to 7 skips), so the
+ * caller never waits for the norm to know the step count.  Needs the norm (max_norm > 0 or norm_out). */
+int avc_clip_adam_ema_dev(avc_context* ctx, size_t n, float* param, float* grad, float* exp_avg,
+                          float* exp_avg_sq, float* ema, float lr, float beta1, float beta2,
+                          float eps, float weight_decay, int calls, float max_norm, double ema_decay,
+                          float* norm_out, unsigned* skips, void* stream);
 
 /* ---- whole Generator forward (inference / convert(), model.py:68-146) ---------------------
  * One call runs the full encoder -> upsample -> decoder -> postnet chain on device, with the
@@ -470,17 +479,21 @@ int avc_wavernn_generate(avc_context* ctx, const int* dims, int T, const float* 
  * rnn_dims / 2 workgroups with in-launch hand-offs where eligible
  * (avc_wavernn_persist_eligible: <= 96 fold rows, 2 * ceil(fc_dims / 8) + rows <= rnn_dims / 2,
  * every workgroup resident); 0 = five graph-captured launches per sample step.  Same arithmetic,
- * bit-identical samples, logits and waveform.  A loop launch that abandons a bounded wait writes
- * its remaining samples as NaN and the call fails with AVC_ERR_DEVICE. */
+ * bit-identical samples, logits and waveform.  A loop launch that abandons a bounded wait (its
+ * workgroups could not all be resident, e.g. CUs held by another process) is re-run by the same
+ * call on the per-step graph path from a fresh state (same bits); avc_wavernn_fallbacks() counts
+ * such re-runs. */
 int avc_wavernn_persist(int on);
+int avc_wavernn_fallbacks(void);
 /* Tuning hook: 1 (default) = generate()'s input projection of every sample position (pI) as an
  * LDS-tiled kernel; 0 = one thread per output.  Same bits. */
 int avc_wavernn_proj_tiled(int on);
 int avc_wavernn_persist_eligible(int rows, int rnn_dims, int fc_dims);
 /* Test hook: the next `launches` loop launches give up at their first unmet wait. */
 int avc_debug_wavernn_inject(int launches);
-/* Diagnostics: the next loop launch stamps its first `steps` steps (s_memrealtime, 100 MHz) into
- * buf [rnn_dims / 2][steps][24] (u64; per op of the loop: start, wait done, end). */
+/* Diagnostics: the next avc_wavernn_generate call (if its loop runs as one launch) stamps its first
+ * `steps` steps (s_memrealtime, 100 MHz) into buf [rnn_dims / 2][steps][24] (u64; per op of the
+ * loop: start, wait done, end).  That call consumes the request whichever path it takes. */
 int avc_debug_wavernn_stamps(void* buf, int steps);
 
 #ifdef __cplusplus

@@ -91,6 +91,10 @@ for step in "$@"; do
     abc2) run abc2 700 bash scripts/ab_c2.sh ab/prev_bnstats.so ;;
     dpprod) run dpprod 600 python -u -m pytest tests/test_gpu_dp.py tests/test_gpu_production.py -x -v -s --timeout 400 -p no:cacheprovider ;;
     fragchain) rm -f gpurun_out/abe.log && run fragchain 600 bash scripts/ab_env.sh AUTOVC_FRAG_CHAIN 0 1 ;;
+    r5a) run r5a 900 python -u -m pytest tests/test_gpu_bnfuse.py tests/test_gpu_bnbwd.py tests/test_gpu_wavernn_persist.py tests/test_gpu_persist_safety.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    margin) run margin 900 python -u -m pytest tests/test_gpu_margin.py -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    abr4) run abr4 700 bash scripts/ab_c2.sh ab/prev_r04.so ;;
+    abr4t) run abr4t 700 bash scripts/ab_train.sh ab/prev_r04.so ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -27,7 +27,7 @@ def _t(a, dev):
     return torch.as_tensor(a, dtype=torch.float32).to(dev).contiguous()
 
 
-def _grads(dev, B, T, cin, cout, act, training, res, dscale, mode):
+def _grads(dev, B, T, cin, cout, act, training, res, dscale, mode, mean_dom=0.0):
     g = torch.Generator().manual_seed(B * 1000 + T + cin + cout)
     x = torch.rand(B, cin, T, generator=g)
     W = (torch.rand(cout, cin, 5, generator=g) - 0.5) * 0.1
@@ -38,6 +38,8 @@ def _grads(dev, B, T, cin, cout, act, training, res, dscale, mode):
     rv = torch.rand(cout, generator=g) + 0.5
     resid = torch.randn(B, cout, T, generator=g) if res else None
     dout = torch.randn(B, cout, T, generator=g) * dscale
+    if mean_dom:  # a gradient that is mostly its channel mean: c (1 + mean_dom * noise)
+        dout = dscale * (3.0 + 3.0 * mean_dom * torch.randn(B, cout, T, generator=g))
     fr = x.permute(2, 0, 1).reshape(T * B, cin)
     xg = _t(fr, dev).requires_grad_(True)
     pg = [_t(t, dev).requires_grad_(True) for t in (W, bias, gamma, beta)]
@@ -88,3 +90,21 @@ def test_split_writing_bn_backward_matches_fp32_path(cuda_device, B, T, cin, cou
             assert d_old < 1e-6, name
             assert same > 0.98, name
             assert d_f64 < (2e-5 if name == "dx" else 3e-5), name
+
+
+@pytest.mark.parametrize("mean_dom", [1e-3, 1e-5])
+@pytest.mark.parametrize("B,T,cin,cout,act,training,res", [CASES[2], (16, 64, 512, 512, ops.ACT_NONE, True, False)])
+def test_mean_dominated_gradient_keeps_the_bound_tight(cuda_device, B, T, cin, cout, act, training, res, mean_dom):
+    """dY = g is (dA - k1 - x^ k2) cancels when dA is mostly its channel mean k1.  A bound
+    built from max|dA| + |k1| then sits log2(1 / mean_dom) binades above the true max |dY|, and every
+    element drops that far toward f16's subnormals.  The bound now takes the signed range of dA about
+    k1, so the split-writing path stays bit-identical to the fp32-dY path here as well."""
+    new, ref64 = _grads(cuda_device, B, T, cin, cout, act, training, res, 1.0, 1, mean_dom)
+    old, _ = _grads(cuda_device, B, T, cin, cout, act, training, res, 1.0, 0, mean_dom)
+    for name, a, b, r in zip(["dx", "dW"], new[:2], old[:2], ref64[:2]):
+        scale = float(r.abs().max()) or 1.0
+        d_old = float((a.double() - b.double()).abs().max()) / scale
+        same = float((a == b).double().mean())
+        print(f"mean_dom {mean_dom:g} {name}: |new - fp32-dY path| {d_old:.2e} (rel. to max), bit-identical {100 * same:.2f} %")
+        assert torch.isfinite(a).all(), name
+        assert d_old < 1e-6 and same > 0.98, name

@@ -10,8 +10,8 @@ For each set three distances are reported on mel / mel_post / codes:
   * the fp32 reference itself vs float64.
 The reference's own distance from exact arithmetic is part of every GPU-vs-reference number (the
 train-mode postnet BNs amplify input noise ~60x), so the GPU-vs-float64 column is what
-says how good the HIP arithmetic is.  The test writes gpurun_out/r04_margin.json (copied to
-profiles/r04_margin.json)."""
+says how good the HIP arithmetic is.  The test writes gpurun_out/r05_margin.json (copied to
+profiles/r05_margin.json)."""
 import json
 import os
 
@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 
 TOL_MEL = 1e-4
 B, T = 64, 128
-OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "r04_margin.json")
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "r05_margin.json")
 
 
 def _scaled(sd, f):
@@ -117,6 +117,8 @@ def _margin(dev, results, key, sd, B, T, xseed=1):
 # the batch sizes convert() actually runs (voice_converter.py:171-175: one utterance, B = 1, with
 # cut=False; batch_forward's slices otherwise) and the smoke test's B = 2, T = 64
 SMALL = [(0, 1, 128), (1, 1, 128), (2, 1, 128), (0, 1, 300), (0, 2, 64), (1, 2, 64), (0, 2, 128), (2, 3, 96)]
+# convert(cut=False) runs one utterance at its full length: B = 1 at T = 1024 and 2000
+SMALL += [(s, 1, t) for t in (1024, 2000) for s in (0, 1, 2)]
 
 
 @pytest.mark.parametrize("seed,B,T", SMALL, ids=[f"seed{s}_B{b}_T{t}" for s, b, t in SMALL])
