@@ -154,6 +154,7 @@ namespace avc {
 // zero `bytes` at p (16-B aligned) on stream s with a kernel (elementwise.hip); used instead of
 // hipMemsetAsync everywhere (see there)
 int zero_async(void* p, size_t bytes, hipStream_t s);
+int fill_async(void* p, size_t bytes, unsigned v, hipStream_t s);
 // n (<= 64) device words that read as zero in stream order on s: taken from the context's pool,
 // which is re-zeroed by one launch when it wraps (every earlier use of the pool precedes that
 // launch on the stream).  While s is capturing a graph the words are zeroed by their own node

@@ -1471,24 +1471,27 @@ int frames_from_mel_backward(int T, int B, int cm, int ce, const float* df, int 
 // library: on ROCm 7.2 a memset issued ahead of a persistent (spin-waiting) launch was measured to
 // land out of order with it (stale counters -> wrong recurrence outputs in the first calls of a
 // process; scripts/persist_repeat.py "modes"), while a kernel is ordered like every other launch.
-__global__ void zero_bytes_kernel(unsigned char* __restrict__ p, size_t n) {
+__global__ void zero_bytes_kernel(unsigned char* __restrict__ p, size_t n, unsigned v) {
   const size_t n16 = n / 16;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
-    reinterpret_cast<uint4*>(p)[i] = make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(p)[i] = make_uint4(v, v, v, v);
   const size_t tail = n16 * 16 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tail < n) p[tail] = 0;
+  if (tail < n) p[tail] = (unsigned char)(v >> (8 * (tail & 3)));
 }
 
-int zero_async(void* p, size_t bytes, hipStream_t s) {
+// fill with a repeated 32-bit pattern (zero_async's kernel); p 16-byte aligned
+int fill_async(void* p, size_t bytes, unsigned v, hipStream_t s) {
   if (bytes == 0) return AVC_OK;
-  AVC_CHECK_ARG(p != nullptr && (reinterpret_cast<uintptr_t>(p) & 15) == 0, "zero_async: NULL or unaligned");
+  AVC_CHECK_ARG(p != nullptr && (reinterpret_cast<uintptr_t>(p) & 15) == 0, "fill_async: NULL or unaligned");
   const size_t n16 = bytes / 16;
   const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>((n16 + 255) / 256, 2048));
-  zero_bytes_kernel<<<blocks, 256, 0, s>>>(static_cast<unsigned char*>(p), bytes);
+  zero_bytes_kernel<<<blocks, 256, 0, s>>>(static_cast<unsigned char*>(p), bytes, v);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
+
+int zero_async(void* p, size_t bytes, hipStream_t s) { return fill_async(p, bytes, 0u, s); }
 
 constexpr int kZeroPool = 16384;  // words (64 KiB)
 

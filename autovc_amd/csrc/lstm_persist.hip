@@ -179,6 +179,8 @@ struct PersistArgs {
   unsigned* fail_host;        // pinned host word (avc_context::fail_host): last failure number
   unsigned char* hg;          // GR: granule ring [grp][kGrRing][hg_step] (in the counter region)
   long hg_step, hg_gstride;   // GR: bytes per (group, step) / per group
+  unsigned char* hsn;         // SN: split-h hand-off buffers [layer][2 sets][T][hsz] (in the region)
+  long hsn_set, hsn_layer;    // SN: bytes per set (T * hsz) and per layer (two sets)
   int nwg;                    // workgroups in the grid
   unsigned spin_limit;        // polls before giving up (0 = test injection: give up at once)
   int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
@@ -407,6 +409,30 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
   }
 }
 
+// SN hand-off (lstm_persist_kernel's SN): is every dword of an h chunk (RT row tiles x hi / lo,
+// one b128 per lane each) written?  The sentinel dword 0xFFFFFFFF is two f16 NaNs with every
+// payload bit set; producers never store it (sn_word), so a dword that is not the sentinel holds
+// this launch's data.  Wave-uniform result.
+template <int RT>
+__device__ __forceinline__ bool sn_ready(const f16x8 (&hv)[RT][2]) {
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+      const u32x4 v = __builtin_bit_cast(u32x4, hv[r][hl]);
+      bad = bad | (v[0] == ~0u) | (v[1] == ~0u) | (v[2] == ~0u) | (v[3] == ~0u);
+    }
+  return __builtin_amdgcn_ballot_w64(bad) == 0ull;
+}
+// a stored dword of split h (two f16): an f16 0xFFFF (a NaN h) becomes the canonical NaN 0x7E00,
+// so no producer ever writes the sentinel
+__device__ __forceinline__ unsigned sn_word(unsigned v) {
+  if ((v & 0xffffu) == 0xffffu) v = (v & 0xffff0000u) | 0x7e00u;
+  if ((v >> 16) == 0xffffu) v = (v & 0xffffu) | 0x7e000000u;
+  return v;
+}
+
 // HO = hand-off form on the consumer side: 0 = one agent-scope acquire (L1 invalidate) then plain
 // loads; 1 = no invalidate, EVERY load of handed-off bytes (split h, gx1) an sc1 load
 // (cdna_hip_programming.md Guideline 16, "Valid forms": producer stores sc1 + drained).
@@ -420,10 +446,21 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
 // publish, on counters per (step, half).  A half's hand-off (drain, counter, the consumers' poll
 // and first loads) then runs while every workgroup computes the other half, instead of on the
 // critical path of the whole step.  Same products, same order per row: bit-identical to NH = 1.
-template <int NCH, int RT, int HO, int PD, int QW, int GR = 0, int NH = 1>
+// SN = 1: sentinel hand-off of split h (round 5; sn_ready).  The split-h buffers live in the
+// launch's region as two sets [2][T][hsz] per layer, every byte 0xFF (the sentinel: an f16 pair
+// 0xFFFF 0xFFFF is a NaN no producer writes, see sn_word) except what this launch has written.  A
+// consumer wave loads its h chunks as soon as its step starts and re-loads a chunk until no dword
+// of it is the sentinel; a dword is written by one store, so a dword that is not the sentinel is
+// this launch's data.  No drain, barrier, counter add or poll stands between a producer's epilogue
+// and its consumers' MFMAs, and each wave's chunk waits only for that chunk's two producers (not a
+// quarter's sixteen).  Launch E uses set E & 1; each producer resets its bytes of step t in the
+// other set to the sentinel right after storing them in this one, so launch E + 1 finds it clean.
+// Counters remain for the gx hand-offs and the back-pressure (slot 0 publishes none).
+template <int NCH, int RT, int HO, int PD, int QW, int GR = 0, int NH = 1, int SN = 0>
 __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   static_assert(!GR || (NCH == 4 && RT == 1 && HO == 1 && !QW), "granule hand-off: one-layer form, H = 512, RT = 1");
   static_assert(NH == 1 || (NH == 2 && QW && !GR && HO == 1), "batch halves: two-layer quarter-wait form");
+  static_assert(!SN || (HO == 1 && !GR && NH == 1), "sentinel hand-off: sc1 loads, counter-free h, one half");
   constexpr int NW = 4, NC = 4;
   constexpr int MB = 16 * RT;        // batch rows computed per half (B <= MB * NH)
   constexpr int TW = 16 * NC;        // 64 gate rows
@@ -580,7 +617,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     }
     // ---- wait for this step's operands ----------------------------------------------------
     AVC_PSTAMP(0);
-    if constexpr (QW || GR) {
+    if constexpr (QW || GR || SN) {
       // GR: only the input slot's gx0 is waited on here (h comes with its tags, below).
       // Lane 0 of every wave waits for what THIS wave reads, all in one multi-counter poll: the
       // quarter of the h source its K chunks come from; slot 2: the slot-1 quarter that wrote its
@@ -596,7 +633,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         // 0: the h quarter; 1: the gx operand; 2: back-pressure (wave 1)
         // (NH = 2: h and gx1 per (step, half); the input slot's gx0 and the back-pressure per step,
         // taken at half 0 on the last half's counters -- a workgroup publishes its halves in order)
-        const bool e0 = !GR && ht >= 0;
+        const bool e0 = !GR && !SN && ht >= 0;  // (SN: the h chunks carry their own readiness)
         unsigned* p0 = cnt + qcnt_index(a.nslot, hsl, TT, e0 ? ht * NH + hf : 0, w, rep);
         const bool e1 = L == 2 || (L == 0 && a.in_slot > 0 && (t & 3) == 0 && hf == 0);
         unsigned* p1 = L == 2 ? cnt + qcnt_index(a.nslot, 1, TT, t * NH + hf, cb / (a.ncb / kQuarters), rep)
@@ -607,8 +644,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         flag[4 + w] = wait3(p0, qtarget, e0, p1, t1, e1, p2, target, e2, a, E) ? 1 : 0;
       }
       // the polled values are in (the loop compared them); nothing below moves above this point
-      // (GR: no wait here -- it would drain the previous step's granule and output stores)
-      if constexpr (!GR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (GR / SN: no wait here -- it would drain the previous step's hand-off and output stores)
+      if constexpr (!GR && !SN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       AVC_PSTAMP(1);
       AVC_PRSTAMP(7);
@@ -703,9 +740,15 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     for (int r = 0; r < RT; ++r)
 #pragma unroll
       for (int n = 0; n < NC; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const unsigned char* src = L == 0 ? (t > 0 ? a.hs0 + (long)(t - 1) * a.hsz : nullptr)
-                                      : (L == 1 ? a.hs0 + (long)t * a.hsz
-                                                : (t > 0 ? a.hs1 + (long)((t - 1) & 1) * a.hsz : nullptr));
+    const unsigned char* src;
+    if constexpr (SN) {  // this launch's set of the layer's [T] buffers
+      const unsigned char* cur = a.hsn + (long)(E & 1u) * a.hsn_set;
+      src = L == 0 ? (t > 0 ? cur + (long)(t - 1) * a.hsz : nullptr)
+                   : (L == 1 ? cur + (long)t * a.hsz : (t > 0 ? cur + a.hsn_layer + (long)(t - 1) * a.hsz : nullptr));
+    } else {
+      src = L == 0 ? (t > 0 ? a.hs0 + (long)(t - 1) * a.hsz : nullptr)
+                   : (L == 1 ? a.hs0 + (long)t * a.hsz : (t > 0 ? a.hs1 + (long)((t - 1) & 1) * a.hsz : nullptr));
+    }
     if (GR ? t == 0 : src == nullptr) {  // (GR: h_{t-1} comes from the granule ring, hs0 is unused)
       load_gx();
     } else {
@@ -824,15 +867,31 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
       for (int c = 0; c < PDX && c < NCH; ++c) { AVC_PLD(hb[c], c) }
       if constexpr (NCH <= PDX) load_gx();
+      bool sn_good = true;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         if (c + PDX < NCH) {
           AVC_PLD(hb[(c + PDX) % NB], c + PDX)
           if (c + PDX == NCH - 1) load_gx();
         }
+        if constexpr (SN) {
+          // re-load chunk c until none of its dwords is the sentinel (a wave-uniform decision);
+          // the re-load is the youngest load, so waiting for it also covers the prefetches
+          for (unsigned spins = 0; sn_good && !sn_ready<RT>(hb[c % NB]); ++spins) {
+            if (spin_give_up(spins, a, E, lane)) {
+              sn_good = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            AVC_PLD(hb[c % NB], c)
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
         AVC_PMFMA(hb[c % NB], c)
         __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (SN) {
+        if (!sn_good && lane == 0) flag[4 + w] = 0;  // acted on after the reduction barrier
       }
       }
 #undef AVC_PMFMA
@@ -850,7 +909,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e];
     __syncthreads();
-    if constexpr (QW || GR) {
+    if constexpr (QW || GR || SN) {
       if (flag[4] == 0 || flag[5] == 0 || flag[6] == 0 || flag[7] == 0) break;
     }
     fu hv, ig, fg, gg, og;
@@ -943,14 +1002,31 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         for (int k = 1; k < SUB; ++k)
 #pragma unroll
           for (int u = 0; u < UPT; ++u) q[k * UPT + u] = __shfl_down(hl[u], k);
-        if (live && sub == 0) {
-          const u32x2 hi2 = {(q[0] & 0xffffu) | (q[1] << 16), (q[2] & 0xffffu) | (q[3] << 16)};
-          const u32x2 lo2 = {(q[0] >> 16) | (q[1] & 0xffff0000u), (q[2] >> 16) | (q[3] & 0xffff0000u)};
+        // (SN: padding rows b >= B of the last tile are stored too, as zeros -- their consumers'
+        // chunks must not keep the sentinel; rows past the buffer fall outside its descriptor)
+        if ((live || SN) && sub == 0) {
+          u32x2 hi2 = {(q[0] & 0xffffu) | (q[1] << 16), (q[2] & 0xffffu) | (q[3] << 16)};
+          u32x2 lo2 = {(q[0] >> 16) | (q[1] & 0xffff0000u), (q[2] >> 16) | (q[3] & 0xffff0000u)};
           const long off = ((long)(b >> 4) * nck + (j0 >> 5)) * 2048 + (((b & 15) + 16 * ((j0 & 31) >> 3)) * 8 + (j0 & 7)) * 2;
-          unsigned char* hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
-          const auto ors = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)a.hsz, 0x00020000);
-          __builtin_amdgcn_raw_buffer_store_b64(hi2, ors, (int)off, 0, 16 /*sc1*/);
-          __builtin_amdgcn_raw_buffer_store_b64(lo2, ors, (int)off + 1024, 0, 16 /*sc1*/);
+          if constexpr (SN) {
+            // this launch's set of step t; the same bytes of the other set back to the sentinel
+            // (the next launch's set; nothing reads it during this one)
+            unsigned char* cur = a.hsn + (L == 0 ? 0 : a.hsn_layer) + (long)t * a.hsz;
+            const auto ors = __builtin_amdgcn_make_buffer_rsrc(cur + (long)(E & 1u) * a.hsn_set, 0, (int)a.hsz, 0x00020000);
+            const auto rrs = __builtin_amdgcn_make_buffer_rsrc(cur + (long)((E & 1u) ^ 1u) * a.hsn_set, 0, (int)a.hsz, 0x00020000);
+            hi2 = u32x2{sn_word(hi2[0]), sn_word(hi2[1])};
+            lo2 = u32x2{sn_word(lo2[0]), sn_word(lo2[1])};
+            __builtin_amdgcn_raw_buffer_store_b64(hi2, ors, (int)off, 0, 16 /*sc1*/);
+            __builtin_amdgcn_raw_buffer_store_b64(lo2, ors, (int)off + 1024, 0, 16 /*sc1*/);
+            const u32x2 sen = {~0u, ~0u};
+            __builtin_amdgcn_raw_buffer_store_b64(sen, rrs, (int)off, 0, 16 /*sc1*/);
+            __builtin_amdgcn_raw_buffer_store_b64(sen, rrs, (int)off + 1024, 0, 16 /*sc1*/);
+          } else {
+            unsigned char* hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
+            const auto ors = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)a.hsz, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b64(hi2, ors, (int)off, 0, 16 /*sc1*/);
+            __builtin_amdgcn_raw_buffer_store_b64(lo2, ors, (int)off + 1024, 0, 16 /*sc1*/);
+          }
         }
       }
     }
@@ -967,13 +1043,16 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       continue;
     }
     // ---- publish: every storing wave drains, barrier, the workgroup counts itself in ------
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (SN: slot 0's h needs no counter and nobody waits on slot 0's counters, so it only keeps the
+    // barrier that orders this step's partial reads before the next step's partial writes)
+    const bool publish = !SN || L != 0;
+    if (publish) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     AVC_PSTAMP(5);
     AVC_PRSTAMP(6);
     // lanes 8..15 count in on this workgroup's quarter -- in both wait forms, so every launch adds
     // ncb / 4 to every quarter word and the epoch targets hold whichever form the next launch takes
-    if (tid < 2 * kRep) {
+    if (publish && tid < 2 * kRep) {
       const long ci = tid < kRep ? cnt_index(L, TT, s, tid)
                                  : qcnt_index(a.nslot, L, TT, s, cb / (a.ncb / kQuarters), tid - kRep);
       __hip_atomic_fetch_add((gu32*)(cnt + ci), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1088,6 +1167,16 @@ bool persist_gran(int H, int RT) {
   return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd >= 2 && !(g_persist_qwait & 2);
 }
 
+// avc_lstm_persist_sentinel(): sentinel hand-off of split h (SN), bit 0 = two-layer form, bit 1 =
+// one-layer form
+int g_persist_sn = 0;
+extern int g_persist_halves;
+// Does a launch of this form take the sentinel hand-off under the current tuning?
+bool persist_sn(bool two_layer) {
+  return (g_persist_sn & (two_layer ? 1 : 2)) && g_persist_mode == 2 && g_persist_pd >= 2 && !g_persist_halves &&
+         (two_layer || !g_persist_gran);
+}
+
 int g_persist_halves = 0;  // avc_lstm_persist_halves(): the two-layer form walks two batch halves
                            // (measured slower: C2 lstm2 1062 -> 1335 us, C5 6120 -> 8090 us)
 
@@ -1105,6 +1194,15 @@ const void* persist_fn(int H, int RT, bool two_layer = true) {
   const bool qw = (g_persist_qwait & (two_layer ? 1 : 2)) != 0;
   const int nch = H / 32 / 4;
   if (!two_layer && persist_gran(H, RT)) return (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 1>;
+  if (persist_sn(two_layer)) {
+    if (nch == 8)
+      return RT == 1 ? (const void*)lstm_persist_kernel<8, 1, 1, 2, 0, 0, 1, 1>
+           : RT == 2 ? (const void*)lstm_persist_kernel<8, 2, 1, 2, 0, 0, 1, 1>
+                     : (const void*)lstm_persist_kernel<8, 4, 1, 2, 0, 0, 1, 1>;
+    return RT == 1 ? (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 0, 1, 1>
+         : RT == 2 ? (const void*)lstm_persist_kernel<4, 2, 1, 2, 0, 0, 1, 1>
+                   : (const void*)lstm_persist_kernel<4, 4, 1, 2, 0, 0, 1, 1>;
+  }
   if (persist_nh(RT, two_layer) == 2) {  // RT / 2 tiles per half
     // a half's h chunks are half as large, so depth 3 / 4 keeps the bytes in flight of depth 2
     // at RT rows (avc_lstm_persist_depth; the RT = 1 halves already take every chunk at once)
@@ -1256,7 +1354,7 @@ int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_
 // retired (freed when the context is destroyed: a captured graph may still reference them).
 constexpr int kMaxRegions = 32;
 int persist_region(avc_context* ctx, int kind, int T, int ngrp, int ncb, int nwg, size_t counter_words,
-                   hipStream_t s, unsigned** out) {
+                   hipStream_t s, unsigned** out, size_t sentinel_from = ~size_t(0)) {
   const size_t bytes = (kRegionHeaderWords + counter_words) * sizeof(unsigned);
   for (auto& r : ctx->regions) {
     if (r.kind == kind && r.T == T && r.ngrp == ngrp && r.ncb == ncb && r.nwg == nwg && r.bytes == bytes) {
@@ -1280,6 +1378,10 @@ int persist_region(avc_context* ctx, int kind, int T, int ngrp, int ncb, int nwg
   void* mem = nullptr;
   AVC_HIP(hipMalloc(&mem, bytes));
   AVC_TRY(zero_async(mem, bytes, s));
+  if (sentinel_from < counter_words) {  // (the SN h buffers: every byte 0xFF, see lstm_persist_kernel)
+    const size_t off = (kRegionHeaderWords + sentinel_from) * sizeof(unsigned);
+    AVC_TRY(fill_async(static_cast<unsigned char*>(mem) + off, bytes - off, ~0u, s));
+  }
   avc_persist_region r;
   r.kind = kind; r.T = T; r.ngrp = ngrp; r.ncb = ncb; r.nwg = nwg; r.bytes = bytes; r.mem = mem;
   r.last_use = ++ctx->region_clock;
@@ -1862,16 +1964,19 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   // granule hand-off: a kGrRing-step ring per group behind the counters (zeroed with them; the
   // tags make stale entries harmless, see gr_tag)
   const bool gran = persist_gran(H, RT);
+  const bool sn = !gran && persist_sn(false);
   const long hg_step = (long)RT * (H / 32) * 4096;
   const size_t cwords = ((size_t)ngrp * gstride + 63) & ~size_t(63);
-  const size_t gwords = gran ? (size_t)ngrp * kGrRing * hg_step / sizeof(unsigned) : 0;
+  const size_t gwords = gran ? (size_t)ngrp * kGrRing * hg_step / sizeof(unsigned)
+                             : (sn ? (size_t)2 * T * hsz / sizeof(unsigned) : 0);  // SN: two h sets [2][T][hsz]
   unsigned char* hs0 = nullptr;
-  if (!gran) {
+  if (!gran && !sn) {
     hs0 = sc.template take<unsigned char>((size_t)T * hsz);
     if (hs0 == nullptr) return AVC_ERR_WORKSPACE;
   }
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), cwords + gwords, s, &region));
+  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), cwords + gwords, s, &region,
+                         sn ? cwords : ~size_t(0)));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = nslot; a.cnt_gstride = gstride;
@@ -1880,8 +1985,13 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
     a.hg_step = hg_step;
     a.hg_gstride = kGrRing * hg_step;
   }
+  if (sn) {
+    a.hsn = reinterpret_cast<unsigned char*>(region + kRegionHeaderWords + cwords);
+    a.hsn_set = (long)T * hsz;
+    a.hsn_layer = 0;
+  }
   if (ip) AVC_TRY(attach_inproj(ctx, sc, *ip, T, B, 1, a, s));
-  if (gran) a.in_lead = 1;  // (back-pressure polls slot 0's counters, which a GR launch does not add to)
+  if (gran || sn) a.in_lead = 1;  // (back-pressure polls slot 0's counters, which GR / SN launches do not add to)
   a.W[0] = reinterpret_cast<const unsigned char*>(whh_s);
   a.winv[0] = winv;
   a.gx0 = gx;
@@ -1935,21 +2045,36 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   Scratch sc(ctx);
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2 * 2;  // bytes per split-h step buffer
-  AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
-  AVC_TAKE(hs1, unsigned char, (size_t)2 * hsz, sc);                      // ring of 2
+  const bool sn = persist_sn(true);
+  unsigned char* hs0 = nullptr;
+  unsigned char* hs1 = nullptr;
+  if (!sn) {  // (SN: the h buffers live in the region, two sets per layer)
+    AVC_TAKE(h0b, unsigned char, (size_t)T * hsz, sc);
+    AVC_TAKE(h1b, unsigned char, (size_t)2 * hsz, sc);                    // ring of 2
+    hs0 = h0b;
+    hs1 = h1b;
+  }
   AVC_TAKE(gx1, float, (size_t)kGxRing * (4 * H / 64) * 64 * 64, sc);     // slab ring
   const int nslot = ip ? 4 : 3;
   const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
   const int NH = persist_nh(RT, true);
   // counters [nslot][T * NH][kRep] (one 128-B line each, per time step and batch half) and the
-  // quarter counters in the persistent region of this layout
+  // quarter counters in the persistent region of this layout; SN: then the h sets [2][2][T][hsz]
+  const size_t cwords = ((size_t)cnt_words(nslot, T * NH, true) + 63) & ~size_t(63);
+  const size_t hwords = sn ? (size_t)2 * 2 * T * hsz / sizeof(unsigned) : 0;
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), (size_t)cnt_words(nslot, T * NH, true), s,
-                         &region));
+  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), cwords + hwords, s, &region,
+                         sn ? cwords : ~size_t(0)));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = nslot; a.cnt_gstride = 0;
+  if (sn) {
+    a.hsn = reinterpret_cast<unsigned char*>(region + kRegionHeaderWords + cwords);
+    a.hsn_set = (long)T * hsz;
+    a.hsn_layer = 2L * T * hsz;
+  }
   if (ip) AVC_TRY(attach_inproj(ctx, sc, *ip, T, B, 3, a, s));
+  if (sn) a.in_lead = 1;  // (input-slot back-pressure polls slot 0's counters, which an SN launch does not add to)
   a.W[0] = reinterpret_cast<const unsigned char*>(w0_s);
   a.W[1] = reinterpret_cast<const unsigned char*>(w1i_s);
   a.W[2] = reinterpret_cast<const unsigned char*>(w1h_s);
@@ -2118,6 +2243,16 @@ extern "C" int avc_lstm_persist_qwait(int mask) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_qwait = mask;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_sentinel(int mask) {
+  if (mask < 0 || mask > 3) {
+    avc::set_error("avc_lstm_persist_sentinel: mask must be 0..3");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_sn = mask;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

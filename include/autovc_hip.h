@@ -333,6 +333,13 @@ int avc_lstm_persist_qwait(int mask);
  * hand-off.  Applies when bit 1 of the qwait mask is clear and
  * the default hand-off form and depth are set.  Same arithmetic either way (bit-identical). */
 int avc_lstm_persist_granules(int on);
+/* Tuning hook (round 5): sentinel hand-off of split h in the persistent recurrences, bit 0 = the
+ * two-layer form (decoder.lstm2), bit 1 = the one-layer form (decoder.lstm1).  The split-h buffers
+ * live in the launch's region as two sets (launch epoch parity), every byte 0xFF until written;
+ * consumers re-load an h chunk until none of its dwords is 0xFFFFFFFF (a pair of f16 NaNs no
+ * producer writes) instead of waiting on arrival counters, and each producer resets its bytes in the
+ * other set for the next launch.  Same products in the same order: bit-identical outputs. */
+int avc_lstm_persist_sentinel(int mask);
 /* Tuning hook: 1 = the two-layer persistent form (decoder lstm2, batch > 16) walks its
  * workgroup's rows as two independent batch halves, step t of one half while the other half's
  * hand-off is in flight (counters per step and half); 0 (default, measured faster) = all rows at

@@ -95,6 +95,8 @@ for step in "$@"; do
     margin) run margin 900 python -u -m pytest tests/test_gpu_margin.py -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     abr4) run abr4 700 bash scripts/ab_c2.sh ab/prev_r04.so ;;
     abr4t) run abr4t 700 bash scripts/ab_train.sh ab/prev_r04.so ;;
+    sn) run sn 600 python -u -m pytest tests/test_gpu_sentinel.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    snab) run snab 400 python scripts/persist_cfg_ab.py "avc_lstm_persist_sentinel=0" "avc_lstm_persist_sentinel=3" "avc_lstm_persist_sentinel=1" "avc_lstm_persist_sentinel=2" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
