@@ -444,16 +444,37 @@ __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const 
   const int c = blockIdx.x * 64 + cl;
   double s1 = 0.0, s2 = 0.0;
   float m1 = -INFINITY, m0 = INFINITY, m2 = 0.f;  // max dA, min dA, max |x^|
-  if (c < C)
-    for (int r = grp; r < R; r += 16) {
-      s1 += part[((long)r * 2 + 0) * C + c];
-      s2 += part[((long)r * 2 + 1) * C + c];
-      if (bb.bound) {
-        m1 = fmaxf(m1, bb.mpart[((long)r * 3 + 0) * C + c]);
-        m0 = fminf(m0, bb.mpart[((long)r * 3 + 1) * C + c]);
-        m2 = fmaxf(m2, bb.mpart[((long)r * 3 + 2) * C + c]);
+  if (c < C) {
+    // rows r = grp, grp + 16, ... summed in that order; kB rows' loads in flight per batch (the
+    // sums are a dependent fp64 chain: one load round trip per row took 17 us per C3 call)
+    constexpr int kB = 8;
+    for (int r0 = grp; r0 < R; r0 += 16 * kB) {
+      float a[kB], b[kB];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const int r = r0 + 16 * u;
+        a[u] = r < R ? part[((long)r * 2 + 0) * C + c] : 0.f;
+        b[u] = r < R ? part[((long)r * 2 + 1) * C + c] : 0.f;
       }
+      if (bb.bound) {
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+          const int r = r0 + 16 * u;
+          if (r < R) {
+            m1 = fmaxf(m1, bb.mpart[((long)r * 3 + 0) * C + c]);
+            m0 = fminf(m0, bb.mpart[((long)r * 3 + 1) * C + c]);
+            m2 = fmaxf(m2, bb.mpart[((long)r * 3 + 2) * C + c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kB; ++u)
+        if (r0 + 16 * u < R) {
+          s1 += a[u];
+          s2 += b[u];
+        }
     }
+  }
   red[0][grp][cl] = s1;
   red[1][grp][cl] = s2;
   redm[0][grp][cl] = m1;

@@ -34,9 +34,7 @@ for step in "$@"; do
     pmcw)  run pmcw 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcW -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
     pmcft) run pmcft 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcFT -o train -- python3 bench.py --mode train --steps 2 --warmup 1 --no-cpu --no-timing ;;
     pmcwt) run pmcwt 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcWT -o train -- python3 bench.py --mode train --steps 2 --warmup 1 --no-cpu --no-timing ;;
-    sweep) run sweep 600 python scripts/sweep_lstm.py ;;
     proftrain) run proftrain 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/proftrain -o train -- python3 bench.py --mode train --steps 3 --warmup 1 --no-cpu --no-timing ;;
-    ssplit) run ssplit 400 python scripts/sweep_split.py ;;
     sstamps) run sstamps 300 python scripts/stamps_split.py 0:0 0:4 ;;
     pstamps) run pstamps 300 python scripts/stamps_persist.py 1 ;;
     pstamps2) run pstamps2 300 python scripts/stamps_persist.py 2 ;;
@@ -46,9 +44,6 @@ for step in "$@"; do
     gcfg) run gcfg 300 python scripts/gemm_cfgs.py ;;
     pmodes) run pmodes 300 python scripts/persist_modes.py ;;
     pmodes1) run pmodes1 300 python scripts/persist_modes.py 1 0 1 1 ;;
-    playr) run playr1 100 python scripts/persist_layer_repeat.py && run playr2 100 python scripts/persist_layer_repeat.py conv ;;
-    prep) run prepb 200 python scripts/persist_repeat.py bump && run prepg 200 python scripts/persist_repeat.py graph && run prepe 200 python scripts/persist_repeat.py eager && run prep0 200 python scripts/persist_repeat.py graph 2 0 && run prep1 200 python scripts/persist_repeat.py graph 1 1 ;;
-    palt) run palt2 200 python scripts/persist_alternate.py 2 && run palt1 200 python scripts/persist_alternate.py 1 && run palt0 200 python scripts/persist_alternate.py 0 ;;
     pident) run pident 300 python scripts/persist_identity.py ;;
     pdepth) run pdepth 300 python scripts/persist_modes.py 0 2:1 2:2 2:1 2:2 1:2 ;;
     probe) run probe 200 python scripts/probe_cache.py ;;
@@ -59,7 +54,6 @@ for step in "$@"; do
              for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" "TA_BUSY_avr TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
                n=$(echo $grp | cut -d' ' -f1); run gpmc3_${mode}_$n 120 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/gpmc3/${mode}_$n -o g -- python3 scripts/gemm_micro.py $mode; done; done ;;
     stamps) run stamps 300 python scripts/stamps_lstm.py ;;
-    pgran) run pgran 300 python scripts/persist_gran_ab.py ;;
     audio) run audio 600 python -m pytest tests/test_gpu_audio.py -v -m gpu -s --timeout 200 -p no:cacheprovider ;;
     benchtrain) run benchtrain 400 python bench.py --mode train --steps 5 --warmup 2 --no-cpu ;;
     benchtraincpu) run benchtraincpu 500 python bench.py --mode train --steps 5 --warmup 2 ;;
@@ -81,7 +75,6 @@ for step in "$@"; do
     bnbwd) run bnbwd 400 python -u -m pytest tests/test_gpu_bnbwd.py tests/test_gpu_kernels.py -x -v -s --timeout 200 -p no:cacheprovider ;;
     bnbwdab) run bnbwdab 400 python scripts/train_hook_ab.py avc_bn_bwd_frag 0 1 ;;
     prodcurve) run prodcurve 500 python -u -m pytest tests/test_gpu_production.py tests/test_gpu_curve.py -x -v -s --timeout 300 -p no:cacheprovider ;;
-    bpttc) run bpttc 300 python -u -m pytest tests/test_gpu_bptt_coalesce.py -x -v -s --timeout 200 -p no:cacheprovider && run bpttcab 300 python scripts/bptt_coalesce_ab.py && run bpttctrain 400 python scripts/train_hook_ab.py avc_bptt_coalesce 0 1 ;;
     wrp) run wrp 400 python -u -m pytest tests/test_gpu_wavernn_persist.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider && run wrpab 300 python scripts/vocoder_ab.py 3 ;;
     wrstamps) run wrstamps 300 python scripts/vocoder_stamps.py 128 ;;
     bnstat) run bnstat 600 python -u -m pytest tests/test_gpu_bnfuse.py tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_margin.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
