@@ -90,6 +90,8 @@ for step in "$@"; do
     abr4t) run abr4t 700 bash scripts/ab_train.sh ab/prev_r04.so ;;
     sn) run sn 600 python -u -m pytest tests/test_gpu_sentinel.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     snab) run snab 400 python scripts/persist_cfg_ab.py "avc_lstm_persist_sentinel=0" "avc_lstm_persist_sentinel=3" "avc_lstm_persist_sentinel=1" "avc_lstm_persist_sentinel=2" ;;
+    stamps1) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stamps1c2 200 python scripts/stamps_lstm1.py sentinel=2 && AVC_STAMPS_BT=32,1024 run stamps1c5 300 python scripts/stamps_lstm1.py sentinel=2 ;;
+    stamps2) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stamps2 300 python scripts/stamps_persist.py && run stamps2sn 300 python scripts/stamps_persist.py sn ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -15,7 +15,9 @@ from autovc_amd import _lib  # noqa: E402
 from autovc_amd.auto_encoder import AutoEncoder  # noqa: E402
 from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_dict  # noqa: E402
 
-B, T, NCB = 64, 128, 32
+# AVC_STAMPS_BT="32,1024" for C5's shape (default C2: 64, 128)
+B, T = (int(v) for v in os.environ.get("AVC_STAMPS_BT", "64,128").split(","))
+NCB = 32
 lib = _lib.load()
 _lib.call("avc_lstm_persist_layers", 1)
 lib.avc_debug_stamps_persist.argtypes = [ctypes.c_void_p]
@@ -49,8 +51,8 @@ def measure(label):
 
 
 measure("default")
-# further measurements after each tuning call: "granules=0" -> avc_lstm_persist_granules(0); a
-# bare integer is an avc_lstm_persist_qwait mask
+# further measurements after each tuning call: "granules=0" -> avc_lstm_persist_granules(0),
+# "sentinel=2" -> avc_lstm_persist_sentinel(2); a bare integer is an avc_lstm_persist_qwait mask
 for arg in sys.argv[1:]:
     name, val = arg.split("=") if "=" in arg else ("qwait", arg)
     _lib.call(f"avc_lstm_persist_{name}", int(val))
