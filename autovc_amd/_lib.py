@@ -67,6 +67,7 @@ _SIGS = {
     "avc_lstm_split_tune": [_I, _I, _I],
     "avc_gemm_tune": [_I],
     "avc_gemm_config": [_I],
+    "avc_bn_fuse_band": [_I],
     "avc_bn_fuse": [_I],
     "avc_split_handover": [_I],
     "avc_dead_h_stores": [_I],

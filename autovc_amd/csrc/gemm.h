@@ -29,6 +29,7 @@ struct BnFuse {
   unsigned* fail_host = nullptr;
   unsigned spin_limit = 0;
   int nwg = 0;
+  int band = 1;                    // dispatch order: 1 = XCD-contiguous row bands per column group
 };
 
 // C(m, n) = act( sum_tap sum_k A_tap(m, k) * B_tap(k, n) + bias0[n] + bias1[n] )

@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
     // tile sat in another XCD's L2, +46 % fetched bytes at C2.)  Speed only: any bijection is correct.
     tn = bid / tilesM;
     const int l = bid - tn * tilesM;
-    tm = (tilesM & 7) ? l : (l & 7) * (tilesM >> 3) + (l >> 3);
+    tm = (!d.bnf.band || (tilesM & 7)) ? l : (l & 7) * (tilesM >> 3) + (l >> 3);
     (void)wgid;
   } else {
     tile_of(wgid, tilesM, tilesN, tm, tn);
@@ -1849,6 +1849,7 @@ int guard_scan(avc_context* ctx, const float* src, long rows, long cols, long ld
 
 // ---- fused BatchNorm epilogue: eligibility and launch ------------------------------------
 int g_bnf = 1;  // avc_bn_fuse()
+int g_bnf_band = 1;  // avc_bn_fuse_band(): XCD-contiguous row bands in the fused instance's dispatch order
 int g_bnf_inject = 0;  // avc_debug_bnf_inject(): train-mode fused launches left that give up at once
 
 namespace {
@@ -1881,6 +1882,7 @@ int bnf_capacity(int bm) {
 }
 
 int launch16f_bnf(avc_context* ctx, GemmDesc d, Frag16Args f, const Plan& p, hipStream_t s) {
+  d.bnf.band = g_bnf_band;
   const int bm = p.bm;
   const int KC = bm == 128 ? 4 : 2;
   int kt_per_tap = (f.a_nkc + KC - 1) / KC;
@@ -2114,6 +2116,16 @@ extern "C" int avc_gemm_config(int cfg) {
     return AVC_ERR_INVALID;
   }
   avc::g_gemm_cfg = cfg;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_bn_fuse_band(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_bn_fuse_band: on must be 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_bnf_band = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -298,6 +298,10 @@ int avc_gemm_config(int cfg);
  * tile's row tiles, a contiguous dispatch range -- must be resident at once; eval mode: running
  * statistics); 2 = fused wherever one such group fits the device (grids of several waves);
  * 0 = the GEMM, a statistics launch and a normalise launch.  All give the same bits. */
+/* Tuning hook (round 5): 1 (default) = the fused-BN GEMM deals each XCD a contiguous band of a
+ * column group's row tiles (the conv taps' neighbouring row tiles then share its L2); 0 = round 4's
+ * order (row tile = dispatch index within the group).  Same products: bit-identical. */
+int avc_bn_fuse_band(int on);
 int avc_bn_fuse(int on);
 /* Whole-Generator forward: 1 (default) = the encoder's last conv, decoder lstm1 and decoder lstm2
  * hand their outputs to the next contraction (BiLSTM projection, first decoder conv, Linear) as

@@ -92,6 +92,8 @@ for step in "$@"; do
     snab) run snab 400 python scripts/persist_cfg_ab.py "avc_lstm_persist_sentinel=0" "avc_lstm_persist_sentinel=3" "avc_lstm_persist_sentinel=1" "avc_lstm_persist_sentinel=2" ;;
     stamps1) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stamps1c2 200 python scripts/stamps_lstm1.py sentinel=2 && AVC_STAMPS_BT=32,1024 run stamps1c5 300 python scripts/stamps_lstm1.py sentinel=2 ;;
     stamps2) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stamps2 300 python scripts/stamps_persist.py && run stamps2sn 300 python scripts/stamps_persist.py sn ;;
+    bandab) run bandab 400 python scripts/persist_hook_ab.py avc_bn_fuse_band 0 1 0 1 0 1 ;;
+    pmcband) for g in 0 1; do run pmcbandF$g 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcbandF$g -o fwd -- python3 scripts/fwd_hooks.py avc_bn_fuse_band=$g 4 && run pmcbandW$g 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcbandW$g -o fwd -- python3 scripts/fwd_hooks.py avc_bn_fuse_band=$g 4; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

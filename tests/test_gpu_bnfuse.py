@@ -150,6 +150,23 @@ def test_whole_generator_fused_bn_is_bit_identical(cuda_device, training):
             assert torch.equal(a, b), (rep, i, float((a.double() - b.double()).abs().max()))
 
 
+@pytest.mark.parametrize("training", [True, False])
+def test_fused_bn_dispatch_band_is_bit_identical(cuda_device, training):
+    """avc_bn_fuse_band (round 5): XCD-contiguous row bands per column group vs round 4's order.
+    Only which workgroup computes which tile changes, so the whole Generator forward is identical."""
+    _fuse(1)
+    try:
+        _lib.call("avc_bn_fuse_band", 0)
+        ref = _generator(cuda_device, training, reps=3)
+        _lib.call("avc_bn_fuse_band", 1)
+        got = _generator(cuda_device, training, reps=3)
+    finally:
+        _lib.call("avc_bn_fuse_band", 1)
+    for rep in range(3):
+        for i, (a, b) in enumerate(zip(got[rep], ref[rep])):
+            assert torch.equal(a, b), (rep, i, float((a.double() - b.double()).abs().max()))
+
+
 def _set_handover(on):
     _lib.call("avc_split_handover", int(on))
 
