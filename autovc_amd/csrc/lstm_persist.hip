@@ -864,10 +864,25 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           AVC_PMFMA(hv8, c)
         }
       } else {
+      bool sn_good = true;
+      if constexpr (SN) {
+        // every chunk issued at the step start would come back as the sentinel and cost one more
+        // round trip each (measured: +50 % per lstm2 step): probe chunk 0's first piece (1 KB per
+        // wave) until it is written, then start the pipeline; each chunk is still checked below
+        constexpr int hoff = 0;  // row tile 0, chunk 0, hi
+        u32x4 pr = __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, hoff, 16);
+        for (unsigned spins = 0; __builtin_amdgcn_ballot_w64((pr[0] == ~0u) | (pr[1] == ~0u) | (pr[2] == ~0u) | (pr[3] == ~0u)) != 0ull; ++spins) {
+          if (spin_give_up(spins, a, E, lane)) {
+            sn_good = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          pr = __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, hoff, 16);
+        }
+      }
 #pragma unroll
       for (int c = 0; c < PDX && c < NCH; ++c) { AVC_PLD(hb[c], c) }
       if constexpr (NCH <= PDX) load_gx();
-      bool sn_good = true;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         if (c + PDX < NCH) {
