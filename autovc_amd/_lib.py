@@ -81,6 +81,7 @@ _SIGS = {
     "avc_lstm_persist_inproj": [_I],
     "avc_lstm_persist_qwait": [_I],
     "avc_lstm_persist_sentinel": [_I],
+    "avc_lstm_persist_st16": [_I],
     "avc_lstm_persist_granules": [_I],
     "avc_lstm_persist_halves": [_I],
     "avc_bn_bwd_frag": [_I],

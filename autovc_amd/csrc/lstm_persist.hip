@@ -181,6 +181,7 @@ struct PersistArgs {
   long hg_step, hg_gstride;   // GR: bytes per (group, step) / per group
   unsigned char* hsn;         // SN: split-h hand-off buffers [layer][2 sets][T][hsz] (in the region)
   long hsn_set, hsn_layer;    // SN: bytes per set (T * hsz) and per layer (two sets)
+  int st16;                   // split-h hand-off stores as 16-B pieces (avc_lstm_persist_st16)
   int nwg;                    // workgroups in the grid
   unsigned spin_limit;        // polls before giving up (0 = test injection: give up at once)
   int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
@@ -1017,30 +1018,41 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         for (int k = 1; k < SUB; ++k)
 #pragma unroll
           for (int u = 0; u < UPT; ++u) q[k * UPT + u] = __shfl_down(hl[u], k);
+        u32x2 hi2 = {(q[0] & 0xffffu) | (q[1] << 16), (q[2] & 0xffffu) | (q[3] << 16)};
+        u32x2 lo2 = {(q[0] >> 16) | (q[1] & 0xffff0000u), (q[2] >> 16) | (q[3] & 0xffff0000u)};
+        if constexpr (SN) {
+          hi2 = u32x2{sn_word(hi2[0]), sn_word(hi2[1])};
+          lo2 = u32x2{sn_word(lo2[0]), sn_word(lo2[1])};
+        }
+        // 16-B pieces (avc_lstm_persist_st16, round 5): the pair leads of blocks 2m and 2m + 1 (lanes
+        // tid and tid ^ SUB, same row) hold the two halves of one 8-k fragment piece; the even one
+        // stores the hi piece, the odd one the lo piece (half the store instructions, each 16 B)
+        const bool odd = (blk & 1) != 0;
+        const unsigned x0 = __shfl_xor(odd ? hi2[0] : lo2[0], SUB), x1 = __shfl_xor(odd ? hi2[1] : lo2[1], SUB);
         // (SN: padding rows b >= B of the last tile are stored too, as zeros -- their consumers'
         // chunks must not keep the sentinel; rows past the buffer fall outside its descriptor)
         if ((live || SN) && sub == 0) {
-          u32x2 hi2 = {(q[0] & 0xffffu) | (q[1] << 16), (q[2] & 0xffffu) | (q[3] << 16)};
-          u32x2 lo2 = {(q[0] >> 16) | (q[1] & 0xffff0000u), (q[2] >> 16) | (q[3] & 0xffff0000u)};
           const long off = ((long)(b >> 4) * nck + (j0 >> 5)) * 2048 + (((b & 15) + 16 * ((j0 & 31) >> 3)) * 8 + (j0 & 7)) * 2;
-          if constexpr (SN) {
-            // this launch's set of step t; the same bytes of the other set back to the sentinel
-            // (the next launch's set; nothing reads it during this one)
-            unsigned char* cur = a.hsn + (L == 0 ? 0 : a.hsn_layer) + (long)t * a.hsz;
-            const auto ors = __builtin_amdgcn_make_buffer_rsrc(cur + (long)(E & 1u) * a.hsn_set, 0, (int)a.hsz, 0x00020000);
-            const auto rrs = __builtin_amdgcn_make_buffer_rsrc(cur + (long)((E & 1u) ^ 1u) * a.hsn_set, 0, (int)a.hsz, 0x00020000);
-            hi2 = u32x2{sn_word(hi2[0]), sn_word(hi2[1])};
-            lo2 = u32x2{sn_word(lo2[0]), sn_word(lo2[1])};
+          const u32x4 pc = odd ? u32x4{x0, x1, lo2[0], lo2[1]} : u32x4{hi2[0], hi2[1], x0, x1};
+          const int off16 = (int)off + (odd ? 1024 - 8 : 0);  // the piece starts at the even lead's units
+          unsigned char* hb;
+          if constexpr (SN) hb = a.hsn + (L == 0 ? 0 : a.hsn_layer) + (long)t * a.hsz + (long)(E & 1u) * a.hsn_set;
+          else hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
+          const auto ors = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)a.hsz, 0x00020000);
+          if (a.st16) {
+            __builtin_amdgcn_raw_buffer_store_b128(pc, ors, off16, 0, 16 /*sc1*/);
+          } else {
             __builtin_amdgcn_raw_buffer_store_b64(hi2, ors, (int)off, 0, 16 /*sc1*/);
             __builtin_amdgcn_raw_buffer_store_b64(lo2, ors, (int)off + 1024, 0, 16 /*sc1*/);
+          }
+          if constexpr (SN) {
+            // the same bytes of the other set back to the sentinel (the next launch's set; nothing
+            // reads it during this one)
+            const auto rrs = __builtin_amdgcn_make_buffer_rsrc(hb + (long)(1 - 2 * (int)(E & 1u)) * a.hsn_set, 0,
+                                                               (int)a.hsz, 0x00020000);
             const u32x2 sen = {~0u, ~0u};
             __builtin_amdgcn_raw_buffer_store_b64(sen, rrs, (int)off, 0, 16 /*sc1*/);
             __builtin_amdgcn_raw_buffer_store_b64(sen, rrs, (int)off + 1024, 0, 16 /*sc1*/);
-          } else {
-            unsigned char* hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
-            const auto ors = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)a.hsz, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b64(hi2, ors, (int)off, 0, 16 /*sc1*/);
-            __builtin_amdgcn_raw_buffer_store_b64(lo2, ors, (int)off + 1024, 0, 16 /*sc1*/);
           }
         }
       }
@@ -1263,6 +1275,7 @@ int persist_capacity(int H, int RT, bool two_layer = true) {
 }
 
 int g_persist_coop = 0;          // avc_lstm_persist_coop()
+int g_persist_st16 = 1;          // avc_lstm_persist_st16()
 int g_persist_inject = 0;        // avc_debug_persist_inject(): launches left that give up at once
 unsigned g_spin_limit = kSpinLimit;  // avc_debug_persist_spin_limit()
 
@@ -1359,6 +1372,7 @@ int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_
     --g_persist_inject;
     a.spin_limit = 0;
   }
+  a.st16 = g_persist_st16;
   const void* fn = persist_fn(a.H, RT, a.nslot >= 3);
   void* args[] = {&a};
   return persist_dispatch(ctx, fn, grid, dim3(256), args, persist_lds(a.H, RT), s);
@@ -2258,6 +2272,16 @@ extern "C" int avc_lstm_persist_qwait(int mask) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_qwait = mask;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_st16(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_lstm_persist_st16: 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_st16 = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

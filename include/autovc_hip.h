@@ -344,6 +344,10 @@ int avc_lstm_persist_granules(int on);
  * producer writes) instead of waiting on arrival counters, and each producer resets its bytes in the
  * other set for the next launch.  Same products in the same order: bit-identical outputs. */
 int avc_lstm_persist_sentinel(int mask);
+/* Tuning hook (round 5): 1 (default) = the persistent recurrences hand split h over in 16-B
+ * pieces (the two pair leads sharing a fragment piece exchange halves by a lane shuffle; one
+ * write-through store each); 0 = two 8-B stores per pair lead.  Same bytes. */
+int avc_lstm_persist_st16(int on);
 /* Tuning hook: 1 = the two-layer persistent form (decoder lstm2, batch > 16) walks its
  * workgroup's rows as two independent batch halves, step t of one half while the other half's
  * hand-off is in flight (counters per step and half); 0 (default, measured faster) = all rows at

@@ -157,3 +157,24 @@ def test_sentinel_give_up_is_nan_and_next_call_raises(cuda_device, layers):
     for run in again:
         for a, b in zip(run, ref):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,T,sn", [(64, 128, 0), (32, 200, 0), (3, 50, 0), (64, 64, 3), (256, 32, 0)])
+def test_16_byte_hand_off_stores_are_bit_identical(cuda_device, B, T, sn):
+    """avc_lstm_persist_st16 (round 5): the split-h hand-off as one 16-B write-through piece per
+    pair lead (halves exchanged by a lane shuffle) instead of two 8-B stores; the same bytes land."""
+    ae = _model(cuda_device)
+    x = torch.from_numpy(synthetic_mel(97 + B, B, T)).to(cuda_device)
+    c = torch.from_numpy(synthetic_embedding(98, B)).to(cuda_device)
+    try:
+        _lib.call("avc_lstm_persist_sentinel", sn)
+        _lib.call("avc_lstm_persist_st16", 0)
+        ref = _forwards(ae, x, c, c)
+        _lib.call("avc_lstm_persist_st16", 1)
+        got = _forwards(ae, x, c, c)
+    finally:
+        _lib.call("avc_lstm_persist_st16", 1)
+        _lib.call("avc_lstm_persist_sentinel", DEFAULT)
+    for run in got:
+        for a, b in zip(run, ref[0]):
+            assert torch.equal(a, b)
