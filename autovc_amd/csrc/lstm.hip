@@ -1157,6 +1157,16 @@ size_t lstm_backward_scratch(int T, int B, int din, int H) {
   return s + gs + colsum_scratch((int)TB, 4 * H);
 }
 
+__device__ unsigned g_h_bound_bits = 0x3f800000u;  // 1.0f: the bound of an LSTM's |h|
+const unsigned* h_bound_word() {
+  static const unsigned* p = nullptr;
+  if (!p) {
+    void* q = nullptr;
+    if (hipGetSymbolAddress(&q, HIP_SYMBOL(g_h_bound_bits)) == hipSuccess) p = static_cast<const unsigned*>(q);
+  }
+  return p;  // nullptr: the product scans y itself
+}
+
 int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,
                        const float* x, int ldx, const float* w_ih, const float* w_hh,
                        const float* y, int ldy, const float* saved_gates, const float* saved_c,
@@ -1330,6 +1340,11 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   GemmDesc g2 = g1;
   g2.N = H;
   g2.B = y; g2.ldb = ldy; g2.b_shift0 = reverse ? B : -B;
+  // y is this layer's h = o tanh(c), |h| < 1: its split takes the power of two of that bound
+  // instead of a max scan of the 64-128 MB operand (round 5).  A bound above the max by 2^k moves
+  // every element k binades down inside f16's range, so only elements below ~2^-28 of the bound
+  // could split differently (DESIGN §9i's argument); their share of dW_hh is below 2^-28.
+  g2.amax_b = h_bound_word();
   g2.C = dwhh_dst; g2.ldc = H;
   if (share && gemm_frag_eligible(g2)) {
     g2.a_frag = g1.a_frag_out ? g1.a_frag_out : g1.a_frag;
