@@ -46,6 +46,8 @@ _SIGS = {
     "avc_bilstm_forward": [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P],
     "avc_lstm_backward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P,
                           _P, _P, _P, _I, _I, _P],
+    "avc_lstm_backward_ex": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P,
+                             _P, _P, _P, _I, _I, _I, _P],
     "avc_linear_forward": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
     "avc_linear_backward": [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P],
     "avc_frames_from_mel": [_I, _I, _I, _P, _I, _P, _P, _P],
@@ -82,6 +84,7 @@ _SIGS = {
     "avc_lstm_persist_qwait": [_I],
     "avc_lstm_persist_sentinel": [_I],
     "avc_lstm_persist_st16": [_I],
+    "avc_lstm_persist_chunkwait": [_I],
     "avc_lstm_persist_granules": [_I],
     "avc_lstm_persist_halves": [_I],
     "avc_bn_bwd_frag": [_I],

@@ -410,6 +410,19 @@ int avc_lstm_backward(avc_context* ctx, int T, int B, int din, int H, int revers
                             accumulate_dw, S(stream));
 }
 
+int avc_lstm_backward_ex(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                         const float* x, int ldx, const float* w_ih, const float* w_hh,
+                         const float* y, int ldy, const float* saved_gates, const float* saved_c,
+                         const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh, float* d_b_ih,
+                         float* d_b_hh, int accumulate_dx, int accumulate_dw, int x_unit, void* stream) {
+  AVC_CHECK_ARG(ctx && x && w_ih && w_hh && y && d_y && d_w_ih && d_w_hh && d_b_ih && d_b_hh, "NULL pointer");
+  AVC_CHECK_ARG(x_unit == 0 || x_unit == 1, "avc_lstm_backward_ex: x_unit must be 0 or 1");
+  AVC_TRY(ensure_arena(ctx, lstm_backward_scratch(T, B, din, H)));
+  return lstm_backward_impl(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, y, ldy, saved_gates,
+                            saved_c, d_y, d_x, d_w_ih, d_w_hh, d_b_ih, d_b_hh, accumulate_dx,
+                            accumulate_dw, S(stream), x_unit != 0);
+}
+
 int avc_linear_forward(avc_context* ctx, int M, int din, int dout, const float* x,
                        const float* weight, const float* bias, float* y, void* stream) {
   AVC_CHECK_ARG(ctx && x && weight && y, "NULL pointer");

@@ -23,7 +23,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
                        const float* y, int ldy, const float* saved_gates, const float* saved_c,
                        const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh,
                        float* d_b_ih, float* d_b_hh, int accumulate_dx, int accumulate_dw,
-                       hipStream_t s);
+                       hipStream_t s, bool x_unit = false);
 size_t lstm_backward_scratch(int T, int B, int din, int H);
 // two stacked layers as a wavefront (w0/w1 = {w_ih, w_hh, b_ih, b_hh}); saved buffers optional
 int lstm2_forward_impl(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,

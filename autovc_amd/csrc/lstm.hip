@@ -1172,7 +1172,9 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
                        const float* y, int ldy, const float* saved_gates, const float* saved_c,
                        const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh,
                        float* d_b_ih, float* d_b_hh, int accumulate_dx, int accumulate_dw,
-                       hipStream_t s) {
+                       hipStream_t s, bool x_unit) {
+  // x_unit: every |x| <= 1 (x is the previous stacked layer's h): dW_ih's split of x takes that
+  // bound (as dW_hh's split of y does, below) instead of a max scan
   AVC_CHECK_ARG(T > 0 && B > 0 && din > 0, "lstm_backward: empty problem");
   AVC_CHECK_ARG(H == 32 || (H % 64 == 0), "lstm_backward: H must be 32 or a multiple of 64");
   AVC_CHECK_ARG(saved_gates && saved_c, "lstm_backward: saved gates/cells required");
@@ -1315,6 +1317,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   g1.B = x; g1.ldb = ldx; g1.b_rows = TB;
   g1.C = dwih_dst; g1.ldc = din; g1.accumulate = acc_w;
   g1.prec16 = 1; g1.split_scale = 1; g1.amax_a = amax_dg;
+  if (x_unit) g1.amax_b = h_bound_word();
   // dG^T is split once (the larger operand of both products: TB x 4H against TB x din / H); with
   // the dX product also streaming split dG, one pass writes both images (g_dg_dual)
   const bool share = gemm_frag_eligible(g1);

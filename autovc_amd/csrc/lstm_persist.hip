@@ -106,6 +106,13 @@ __host__ __device__ __forceinline__ long qcnt_index(int nslot, int L, int T, int
 __host__ __device__ __forceinline__ long cnt_words(int nslot, int T, bool quarters) {
   return (long)nslot * T * kRep * kLine * (quarters ? 1 + kQuarters : 1);
 }
+// Chunk counters (round 5, `avc_lstm_persist_chunkwait`, two-layer form): one per (slot, step,
+// 32-deep chunk kc of h), after the quarter counters; the two workgroups that write chunk kc
+// (units 32 kc .. 32 kc + 31, workgroups 2 kc and 2 kc + 1) count in on it, so a consumer wave can
+// start on chunk c of its K quarter once those two are in instead of waiting for all sixteen.
+__host__ __device__ __forceinline__ long ccnt_index(int nslot, int L, int T, int t, int kc, int r, int nck) {
+  return cnt_words(nslot, T, true) + ((((long)L * T + t) * nck + kc) * kRep + r) * kLine;
+}
 // gx1 hand-off: a ring of kGxRing steps of per-column-block slabs [64 rows][64 columns] fp32, so
 // each (step, column block) pair exchanges one contiguous 16 KB; slot 1 re-fills a ring entry
 // only after every slot-2 workgroup has finished the step that read it (back-pressure wait)
@@ -261,14 +268,18 @@ __device__ __forceinline__ bool wait_ge(unsigned* p, unsigned target, const Pers
 // One lane waits until *p_i >= t_i for every enabled i (e_i): each poll loads all of them back to
 // back (one round trip for the lot), then compares; bounded and giving up like wait_ge_ctl.
 __device__ bool wait3(unsigned* p0, unsigned t0, bool e0, unsigned* p1, unsigned t1, bool e1, unsigned* p2,
-                      unsigned t2, bool e2, const PersistArgs& a, unsigned E) {
-  if (!e0 && !e1 && !e2) return true;
+                      unsigned t2, bool e2, const PersistArgs& a, unsigned E, unsigned* p3 = nullptr,
+                      unsigned t3 = 0, bool e3 = false) {
+  if (!e0 && !e1 && !e2 && !e3) return true;
   gu32* gt = (gu32*)(a.tmo);
   for (unsigned spins = 0;; ++spins) {
     const unsigned v0 = e0 ? __hip_atomic_load((gu32*)p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     const unsigned v1 = e1 ? __hip_atomic_load((gu32*)p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     const unsigned v2 = e2 ? __hip_atomic_load((gu32*)p2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    if ((!e0 || (int)(v0 - t0) >= 0) && (!e1 || (int)(v1 - t1) >= 0) && (!e2 || (int)(v2 - t2) >= 0)) return true;
+    const unsigned v3 = e3 ? __hip_atomic_load((gu32*)p3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    if ((!e0 || (int)(v0 - t0) >= 0) && (!e1 || (int)(v1 - t1) >= 0) && (!e2 || (int)(v2 - t2) >= 0) &&
+        (!e3 || (int)(v3 - t3) >= 0))
+      return true;
     if ((spins & 63) == 63 && __hip_atomic_load(gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E)
       return false;
     if (spins >= a.spin_limit) {
@@ -457,8 +468,12 @@ __device__ __forceinline__ unsigned sn_word(unsigned v) {
 // quarter's sixteen).  Launch E uses set E & 1; each producer resets its bytes of step t in the
 // other set to the sentinel right after storing them in this one, so launch E + 1 finds it clean.
 // Counters remain for the gx hand-offs and the back-pressure (slot 0 publishes none).
-template <int NCH, int RT, int HO, int PD, int QW, int GR = 0, int NH = 1, int SN = 0>
+// CW = 1: per-chunk waits (round 5, see ccnt_index): each wave waits for its chunks 0 and 1 at the
+// step start and polls chunk c + 2's counter one chunk ahead of its loads (two-layer form, QW).
+template <int NCH, int RT, int HO, int PD, int QW, int GR = 0, int NH = 1, int SN = 0, int CW = 0>
 __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
+  static_assert(!CW || (QW && !GR && !SN && NH == 1 && PD == 2 && RT >= 2 && NCH >= 3),
+                "chunk waits: two-layer quarter-wait form, PD 2, RT >= 2");
   static_assert(!GR || (NCH == 4 && RT == 1 && HO == 1 && !QW), "granule hand-off: one-layer form, H = 512, RT = 1");
   static_assert(NH == 1 || (NH == 2 && QW && !GR && HO == 1), "batch halves: two-layer quarter-wait form");
   static_assert(!SN || (HO == 1 && !GR && NH == 1), "sentinel hand-off: sc1 loads, counter-free h, one half");
@@ -635,14 +650,20 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         // (NH = 2: h and gx1 per (step, half); the input slot's gx0 and the back-pressure per step,
         // taken at half 0 on the last half's counters -- a workgroup publishes its halves in order)
         const bool e0 = !GR && !SN && ht >= 0;  // (SN: the h chunks carry their own readiness)
-        unsigned* p0 = cnt + qcnt_index(a.nslot, hsl, TT, e0 ? ht * NH + hf : 0, w, rep);
+        // (CW: chunks 0 and 1 of this wave's quarter instead of the whole quarter)
+        unsigned* p0 = CW ? cnt + ccnt_index(a.nslot, hsl, T, e0 ? ht : 0, w * NCH, rep, nck)
+                          : cnt + qcnt_index(a.nslot, hsl, TT, e0 ? ht * NH + hf : 0, w, rep);
         const bool e1 = L == 2 || (L == 0 && a.in_slot > 0 && (t & 3) == 0 && hf == 0);
         unsigned* p1 = L == 2 ? cnt + qcnt_index(a.nslot, 1, TT, t * NH + hf, cb / (a.ncb / kQuarters), rep)
                               : cnt + cnt_index(a.in_slot, TT, min(t + 3, T - 1) * NH + NH - 1, rep);
         const unsigned t1 = L == 2 ? qtarget : target;
         const bool e2 = !GR && w == 1 && hf == 0 && ((L == 0 && t >= kLead && a.nslot >= 3) || (L == 1 && t >= kGxRing));
         unsigned* p2 = cnt + cnt_index(2, TT, e2 ? (t - (L == 0 ? kLead : kGxRing)) * NH + NH - 1 : 0, rep);
-        flag[4 + w] = wait3(p0, qtarget, e0, p1, t1, e1, p2, target, e2, a, E) ? 1 : 0;
+        if constexpr (CW)
+          flag[4 + w] = wait3(p0, 2u * E, e0, p1, t1, e1, p2, target, e2, a, E,
+                              cnt + ccnt_index(a.nslot, hsl, T, e0 ? ht : 0, w * NCH + 1, rep, nck), 2u * E, e0) ? 1 : 0;
+        else
+          flag[4 + w] = wait3(p0, qtarget, e0, p1, t1, e1, p2, target, e2, a, E) ? 1 : 0;
       }
       // the polled values are in (the loop compared them); nothing below moves above this point
       // (GR / SN: no wait here -- it would drain the previous step's hand-off and output stores)
@@ -881,12 +902,42 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           pr = __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, hoff, 16);
         }
       }
+      // CW: chunk c + 2's counter, polled one chunk ahead of its loads (lane 0; wave-uniform below)
+      unsigned* const cw_base = CW ? cnt + ccnt_index(a.nslot, L == 1 ? 0 : L, T, L == 1 ? t : t - 1, kc0, rep, nck) : nullptr;
+      unsigned cw_v = 0u;
+      bool cw_good = true;
+      auto cw_poll = [&](int c) {
+        if (lane == 0)
+          cw_v = __hip_atomic_load((gu32*)(cw_base + (long)c * kRep * kLine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      };
+      if constexpr (CW) {
+        AVC_PLD(hb[0], 0)
+        cw_poll(2);  // (issued before chunk 1's loads: waiting for it never waits for them)
+        AVC_PLD(hb[1], 1)
+      } else {
 #pragma unroll
       for (int c = 0; c < PDX && c < NCH; ++c) { AVC_PLD(hb[c], c) }
+      }
       if constexpr (NCH <= PDX) load_gx();
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         if (c + PDX < NCH) {
+          if constexpr (CW) {
+            // chunk c + 2's two producers: the poll issued one chunk ago has returned by now
+            const unsigned ct = 2u * E;
+            unsigned v = __builtin_amdgcn_readfirstlane(cw_v);
+            for (unsigned spins = 0; cw_good && (int)(v - ct) < 0; ++spins) {
+              if (spin_give_up(spins, a, E, lane)) {
+                cw_good = false;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(1);
+              cw_poll(c + 2);
+              v = __builtin_amdgcn_readfirstlane(cw_v);
+            }
+            if (c + 3 < NCH) cw_poll(c + 3);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering: loads stay below)
+          }
           AVC_PLD(hb[(c + PDX) % NB], c + PDX)
           if (c + PDX == NCH - 1) load_gx();
         }
@@ -908,6 +959,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       }
       if constexpr (SN) {
         if (!sn_good && lane == 0) flag[4 + w] = 0;  // acted on after the reduction barrier
+      }
+      if constexpr (CW) {
+        if (!cw_good && lane == 0) flag[4 + w] = 0;
       }
       }
 #undef AVC_PMFMA
@@ -1079,9 +1133,10 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     AVC_PRSTAMP(6);
     // lanes 8..15 count in on this workgroup's quarter -- in both wait forms, so every launch adds
     // ncb / 4 to every quarter word and the epoch targets hold whichever form the next launch takes
-    if (publish && tid < 2 * kRep) {
-      const long ci = tid < kRep ? cnt_index(L, TT, s, tid)
-                                 : qcnt_index(a.nslot, L, TT, s, cb / (a.ncb / kQuarters), tid - kRep);
+    if (publish && tid < (CW && (L == 0 || L == 2) ? 3 : 2) * kRep) {
+      const long ci = tid < kRep       ? cnt_index(L, TT, s, tid)
+                      : tid < 2 * kRep ? qcnt_index(a.nslot, L, TT, s, cb / (a.ncb / kQuarters), tid - kRep)
+                                       : ccnt_index(a.nslot, L, T, s, cb >> 1, tid - 2 * kRep, nck);  // (CW: h's chunk)
       __hip_atomic_fetch_add((gu32*)(cnt + ci), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // outputs nobody reads inside this launch: stored after publishing (off the hand-off path);
@@ -1216,10 +1271,27 @@ int persist_nh(int RT, bool two_layer) {
              : 1;
 }
 
+// avc_lstm_persist_chunkwait(): per-chunk waits in the two-layer form (CW; ccnt_index)
+int g_persist_cw = 0;
+// Does a launch of (RT 16-row tiles) take the per-chunk waits under the current tuning?  The
+// two-layer form in its quarter-wait hand-off with PD 2 and at least two row tiles (RT 1 requests
+// every chunk at once, so there is nothing to start early).
+bool persist_cw(int RT, bool two_layer) {
+  return g_persist_cw && two_layer && RT >= 2 && (g_persist_qwait & 1) && g_persist_mode == 2 && g_persist_pd == 2 &&
+         !persist_sn(true) && persist_nh(RT, true) == 1;
+}
+
 // The template instance a launch of (H, RT) runs under the current tuning.
 const void* persist_fn(int H, int RT, bool two_layer = true) {
   const bool qw = (g_persist_qwait & (two_layer ? 1 : 2)) != 0;
   const int nch = H / 32 / 4;
+  if (persist_cw(RT, two_layer)) {
+    if (nch == 8)
+      return RT == 2 ? (const void*)lstm_persist_kernel<8, 2, 1, 2, 1, 0, 1, 0, 1>
+                     : (const void*)lstm_persist_kernel<8, 4, 1, 2, 1, 0, 1, 0, 1>;
+    return RT == 2 ? (const void*)lstm_persist_kernel<4, 2, 1, 2, 1, 0, 1, 0, 1>
+                   : (const void*)lstm_persist_kernel<4, 4, 1, 2, 1, 0, 1, 0, 1>;
+  }
   if (!two_layer && persist_gran(H, RT)) return (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 1>;
   if (persist_sn(two_layer)) {
     if (nch == 8)
@@ -2089,7 +2161,9 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   const int NH = persist_nh(RT, true);
   // counters [nslot][T * NH][kRep] (one 128-B line each, per time step and batch half) and the
   // quarter counters in the persistent region of this layout; SN: then the h sets [2][2][T][hsz]
-  const size_t cwords = ((size_t)cnt_words(nslot, T * NH, true) + 63) & ~size_t(63);
+  // (CW: then the chunk counters, [3][T][H / 32][kRep] lines; ccnt_index)
+  const size_t cwords = ((size_t)cnt_words(nslot, T * NH, true) +
+                         (persist_cw(RT, true) ? (size_t)3 * T * (H / 32) * kRep * kLine : 0) + 63) & ~size_t(63);
   const size_t hwords = sn ? (size_t)2 * 2 * T * hsz / sizeof(unsigned) : 0;
   unsigned* region = nullptr;
   AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), cwords + hwords, s, &region,
@@ -2282,6 +2356,16 @@ extern "C" int avc_lstm_persist_st16(int on) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_st16 = on;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_chunkwait(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_lstm_persist_chunkwait: 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_cw = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

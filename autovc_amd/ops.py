@@ -282,7 +282,14 @@ def _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, reverse, save, T, B):
     return gates, cst
 
 
-def _lstm_bwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, gates, cst, d_y, d_x, reverse, acc, T, B, needs):
+def _unit_bounded(x):
+    """Is x an LSTMLayer output (h = o tanh(c), every |x| <= 1), unmodified since?"""
+    rec = getattr(x, "_avc_unit", None)
+    return rec is not None and rec == x._version
+
+
+def _lstm_bwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, gates, cst, d_y, d_x, reverse, acc, T, B, needs,
+              x_unit=False):
     H = w_hh.shape[1]
     din = x.shape[1]
     params = (w_ih, w_hh, b_ih, b_hh)
@@ -295,10 +302,10 @@ def _lstm_bwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, gates, cst, d_y, d_x, reve
     sink = _sink if _sink is not None and _persistent_bptt(T, B, H) else None
     if sink is not None:
         sink.recurrence_begin()
-    call("avc_lstm_backward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
+    call("avc_lstm_backward_ex", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
          ptr(w_hh.contiguous()), y.data_ptr() + col * F32, ldy, ptr(gates), ptr(cst),
          d_y.data_ptr() + col * F32, ptr(d_x), *[ptr(t) for t in scratch], int(acc), int(direct),
-         _stream(x))
+         int(x_unit), _stream(x))
     done = tuple(_param_done(params, (dwi, dwh, dbi, dbh), direct))
     if sink is not None:
         sink.recurrence_end()
@@ -310,10 +317,12 @@ class LSTMLayer(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, T, B, save):
+        ctx.x_unit = _unit_bounded(x)  # (x is the layer below's h: its weight gradient skips a scan)
         x = x.contiguous()
         H = w_hh.shape[1]
         y = _empty((T * B, H), x)
         gates, cst = _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, 0, H, False, save, T, B)
+        y._avc_unit = y._version  # |y| <= 1 (_unit_bounded)
         _use(w_ih, w_hh, b_ih, b_hh)
         if save:
             ctx.save_for_backward(x, w_ih, w_hh, y, gates, cst)
@@ -328,7 +337,7 @@ class LSTMLayer(torch.autograd.Function):
         d_y = d_y.contiguous()
         d_x = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         dwi, dwh, dbi, dbh = _lstm_bwd(x, w_ih, w_hh, *ctx.biases, y, 0, y.shape[1], gates, cst, d_y, d_x, False, 0,
-                                       T, B, ctx.needs_input_grad[1:5])
+                                       T, B, ctx.needs_input_grad[1:5], ctx.x_unit)
         return d_x, dwi, dwh, dbi, dbh, None, None, None
 
 

@@ -156,6 +156,14 @@ int avc_lstm_backward(avc_context* ctx, int T, int B, int din, int H, int revers
                       const float* y, int ldy, const float* saved_gates, const float* saved_c,
                       const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh, float* d_b_ih,
                       float* d_b_hh, int accumulate_dx, int accumulate_dw, void* stream);
+/* As avc_lstm_backward; x_unit = 1 declares every |x| <= 1 (x is the previous stacked layer's h,
+ * o * tanh(c)): the W_ih gradient's split of x then takes that bound instead of a max scan of x
+ * (round 5).  Same products otherwise. */
+int avc_lstm_backward_ex(avc_context* ctx, int T, int B, int din, int H, int reverse,
+                         const float* x, int ldx, const float* w_ih, const float* w_hh,
+                         const float* y, int ldy, const float* saved_gates, const float* saved_c,
+                         const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh, float* d_b_ih,
+                         float* d_b_hh, int accumulate_dx, int accumulate_dw, int x_unit, void* stream);
 
 /* ---- Linear (decoder.linear_projection, decoder.py:56,77; net_layers.py:3-20) ------------ */
 int avc_linear_forward(avc_context* ctx, int M, int din, int dout, const float* x,
@@ -348,6 +356,11 @@ int avc_lstm_persist_sentinel(int mask);
  * pieces (the two pair leads sharing a fragment piece exchange halves by a lane shuffle; one
  * write-through store each); 0 = two 8-B stores per pair lead.  Same bytes. */
 int avc_lstm_persist_st16(int on);
+/* Tuning hook (round 5): 1 = the two-layer persistent form (decoder.lstm2, batch > 16) waits per
+ * 32-deep chunk of h (a counter per chunk that its two producing workgroups count in on, polled one
+ * chunk ahead of the loads) instead of for the whole K quarter a wave reads; 0 (default) = the
+ * quarter counters.  Same products in the same order: bit-identical outputs. */
+int avc_lstm_persist_chunkwait(int on);
 /* Tuning hook: 1 = the two-layer persistent form (decoder lstm2, batch > 16) walks its
  * workgroup's rows as two independent batch halves, step t of one half while the other half's
  * hand-off is in flight (counters per step and half); 0 (default, measured faster) = all rows at

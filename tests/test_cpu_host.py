@@ -122,3 +122,14 @@ def test_grad_sink_counts_uses():
     assert done == [b]
     sink.done(a)
     assert done == [b, a]
+
+
+def test_unit_bound_mark_follows_the_tensor_version():
+    """ops._unit_bounded: an LSTMLayer output carries the |h| <= 1 mark until it is modified."""
+    from autovc_amd import ops
+    t = torch.zeros(4)
+    assert not ops._unit_bounded(t)
+    t._avc_unit = t._version
+    assert ops._unit_bounded(t)
+    t.add_(1.0)  # an in-place change voids the bound
+    assert not ops._unit_bounded(t)

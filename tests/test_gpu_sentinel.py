@@ -178,3 +178,55 @@ def test_16_byte_hand_off_stores_are_bit_identical(cuda_device, B, T, sn):
     for run in got:
         for a, b in zip(run, ref[0]):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,T,training", [(64, 128, True), (32, 1000, False), (48, 40, True), (17, 64, True),
+                                          (256, 32, True)])
+def test_chunk_waits_are_bit_identical(cuda_device, B, T, training):
+    """avc_lstm_persist_chunkwait (round 5): the two-layer form's waves wait per 32-deep h chunk
+    (two producing workgroups) instead of per K quarter; the products and their order are unchanged."""
+    ae = _model(cuda_device, training)
+    x = torch.from_numpy(synthetic_mel(99 + B, B, T)).to(cuda_device)
+    c = torch.from_numpy(synthetic_embedding(100, B)).to(cuda_device)
+    before = _giveups()
+    try:
+        _lib.call("avc_lstm_persist_chunkwait", 0)
+        ref = _forwards(ae, x, c, c)
+        _lib.call("avc_lstm_persist_chunkwait", 1)
+        got = _forwards(ae, x, c, c)
+    finally:
+        _lib.call("avc_lstm_persist_chunkwait", 0)
+    for run in got:
+        for a, b in zip(run, ref[0]):
+            assert torch.equal(a, b), f"max|d| {(a - b).abs().max().item():.3e}"
+    assert _giveups() == before
+
+
+def test_chunk_wait_give_up_is_nan_and_next_call_raises(cuda_device):
+    B, T = 64, 64
+    ae = _model(cuda_device)
+    x = torch.from_numpy(synthetic_mel(101, B, T)).to(cuda_device)
+    c = torch.from_numpy(synthetic_embedding(102, B)).to(cuda_device)
+    _lib.call("avc_graph_mode", 0)
+    _lib.call("avc_lstm_persist_layers", 2)
+    _lib.call("avc_lstm_persist_chunkwait", 1)
+    try:
+        ref = _forwards(ae, x, c, c, reps=1)[0]
+        before = _giveups()
+        _lib.call("avc_debug_persist_inject", 1)
+        with torch.no_grad():
+            bad = [o.clone() for o in ae(x, c, c)]
+        torch.cuda.synchronize()
+        assert _giveups() > before
+        assert torch.isnan(bad[1]).any(), "a forward whose recurrence gave up returned numbers"
+        with pytest.raises(RuntimeError, match="abandoned a bounded wait"):
+            ae.check_health()
+        again = _forwards(ae, x, c, c, reps=2)
+    finally:
+        _lib.call("avc_debug_persist_inject", 0)
+        _lib.call("avc_lstm_persist_chunkwait", 0)
+        _lib.call("avc_lstm_persist_layers", 3)
+        _lib.call("avc_graph_mode", 1)
+    for run in again:
+        for a, b in zip(run, ref):
+            assert torch.equal(a, b)
