@@ -123,20 +123,21 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, int nparts, int
       const double inv_last = 1.0 / (double)(M - (long)(nparts - 1) * part_rows);  // the short last partial
       const float S0 = stats[c];
       float Sv[kB], Qv[kB];
+      // (clamped, unconditional loads: see bn_bwd_final_kernel; partials past nparts are skipped)
 #pragma unroll
       for (int u = 0; u < kB; ++u) {
-        const int p = grp + 4 * u;
-        Sv[u] = p < nparts ? stats[((long)p * 2 + 0) * C + c] : 0.f;
-        Qv[u] = p < nparts ? stats[((long)p * 2 + 1) * C + c] : 0.f;
+        const long p = min(grp + 4 * u, nparts - 1);
+        Sv[u] = stats[(p * 2 + 0) * C + c];
+        Qv[u] = stats[(p * 2 + 1) * C + c];
       }
       const double K = (double)S0 * (nparts == 1 ? inv_last : inv_pr);
       for (int p0 = grp; p0 < nparts; p0 += 4 * kB) {
         float Sn[kB], Qn[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-          const int p = p0 + 4 * kB + 4 * u;
-          Sn[u] = p < nparts ? stats[((long)p * 2 + 0) * C + c] : 0.f;
-          Qn[u] = p < nparts ? stats[((long)p * 2 + 1) * C + c] : 0.f;
+          const long p = min(p0 + 4 * kB + 4 * u, nparts - 1);
+          Sn[u] = stats[(p * 2 + 0) * C + c];
+          Qn[u] = stats[(p * 2 + 1) * C + c];
         }
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
@@ -450,21 +451,28 @@ __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(int R, int C, const 
     constexpr int kB = 8;
     for (int r0 = grp; r0 < R; r0 += 16 * kB) {
       float a[kB], b[kB];
+      // (unconditional loads of a clamped row, masked below: a load under `r < R` compiles to a
+      // branch that waits for it, one round trip per row -- 53 us per C3 call measured)
 #pragma unroll
       for (int u = 0; u < kB; ++u) {
-        const int r = r0 + 16 * u;
-        a[u] = r < R ? part[((long)r * 2 + 0) * C + c] : 0.f;
-        b[u] = r < R ? part[((long)r * 2 + 1) * C + c] : 0.f;
+        const long rc = min(r0 + 16 * u, R - 1);
+        a[u] = part[(rc * 2 + 0) * C + c];
+        b[u] = part[(rc * 2 + 1) * C + c];
       }
       if (bb.bound) {
+        float x1[kB], x0[kB], x2[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-          const int r = r0 + 16 * u;
-          if (r < R) {
-            m1 = fmaxf(m1, bb.mpart[((long)r * 3 + 0) * C + c]);
-            m0 = fminf(m0, bb.mpart[((long)r * 3 + 1) * C + c]);
-            m2 = fmaxf(m2, bb.mpart[((long)r * 3 + 2) * C + c]);
-          }
+          const long rc = min(r0 + 16 * u, R - 1);  // (a repeated row leaves max / min unchanged)
+          x1[u] = bb.mpart[(rc * 3 + 0) * C + c];
+          x0[u] = bb.mpart[(rc * 3 + 1) * C + c];
+          x2[u] = bb.mpart[(rc * 3 + 2) * C + c];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+          m1 = fmaxf(m1, x1[u]);
+          m0 = fminf(m0, x0[u]);
+          m2 = fmaxf(m2, x2[u]);
         }
       }
 #pragma unroll
@@ -1236,9 +1244,16 @@ struct AdamArgs {
   float ss[kAdamTab], bc[kAdamTab];  // the host's values for effective steps step, step - 1, ...
 };
 
+// ema_decay * avg + keep * p with both products rounded (HIP's __fmul_rn is a plain multiply, so
+// without this the compiler may contract the sum into an fma: measured 4-ulp EMA drift vs torch)
+__device__ __forceinline__ float ema_blend(float decay, float avg, float keep, float p) {
+#pragma clang fp contract(off)
+  return decay * avg + keep * p;
+}
+
 // one element of the fused clip + Adam + EMA update (torch.optim.Adam's foreach arithmetic)
 __device__ __forceinline__ void adam_elem(const AdamArgs& a, float& pi, float& gi, float& mi, float& vi,
-                                          float* ei) {
+                                          float& ei, bool has_e) {
   if (a.clip) gi *= a.c;
   float gw = gi;
   if (a.wd != 0.f) gw += a.wd * pi;
@@ -1248,7 +1263,7 @@ __device__ __forceinline__ void adam_elem(const AdamArgs& a, float& pi, float& g
   pi -= a.step_size * (mi / denom);
   // torch: ema_decay * avg + (1 - ema_decay) * flat  (two rounded products, one rounded sum;
   // 1 - ema_decay formed in double on the host like the Python scalar)
-  if (ei) *ei = __fadd_rn(__fmul_rn(a.ema_decay, *ei), __fmul_rn(a.ema_keep, pi));
+  if (has_e) ei = ema_blend(a.ema_decay, ei, a.ema_keep, pi);
 }
 
 // float4 form over the first n4 * 4 elements (all five arrays 16-byte aligned), scalar tail
@@ -1259,20 +1274,28 @@ __global__ __launch_bounds__(256) void adam_ema_kernel(long n, long n4, float* _
   if (a.guard && coef[1] != 0.f) return;  // non-finite gradient norm: parameters, moments, EMA kept
   a.c = a.clip ? coef[0] : 1.f;
   if (a.tabled) {
+    // table entry k by selects: a dynamic index into the by-value arguments put the whole struct
+    // in scratch, and every element's update read its scalars from there (adam 218 -> 297 us at C3)
     const unsigned k = min(__float_as_uint(coef[2]), (unsigned)(kAdamTab - 1));
-    a.step_size = a.ss[k];
-    a.bc2_sqrt = a.bc[k];
+    float ss = a.ss[0], bc = a.bc[0];
+#pragma unroll
+    for (int j = 1; j < kAdamTab; ++j) {
+      ss = k == (unsigned)j ? a.ss[j] : ss;
+      bc = k == (unsigned)j ? a.bc[j] : bc;
+    }
+    a.step_size = ss;
+    a.bc2_sqrt = bc;
   }
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 p4 = reinterpret_cast<float4*>(p)[i], g4 = reinterpret_cast<float4*>(g)[i];
     float4 m4 = reinterpret_cast<float4*>(m)[i], v4 = reinterpret_cast<float4*>(v)[i];
-    float4 e4 = ema ? reinterpret_cast<float4*>(ema)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float* e = ema ? &e4.x : nullptr;
-    adam_elem(a, p4.x, g4.x, m4.x, v4.x, e ? e + 0 : nullptr);
-    adam_elem(a, p4.y, g4.y, m4.y, v4.y, e ? e + 1 : nullptr);
-    adam_elem(a, p4.z, g4.z, m4.z, v4.z, e ? e + 2 : nullptr);
-    adam_elem(a, p4.w, g4.w, m4.w, v4.w, e ? e + 3 : nullptr);
+    const bool he = ema != nullptr;
+    float4 e4 = he ? reinterpret_cast<float4*>(ema)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    adam_elem(a, p4.x, g4.x, m4.x, v4.x, e4.x, he);
+    adam_elem(a, p4.y, g4.y, m4.y, v4.y, e4.y, he);
+    adam_elem(a, p4.z, g4.z, m4.z, v4.z, e4.z, he);
+    adam_elem(a, p4.w, g4.w, m4.w, v4.w, e4.w, he);
     if (a.clip) reinterpret_cast<float4*>(g)[i] = g4;
     reinterpret_cast<float4*>(m)[i] = m4;
     reinterpret_cast<float4*>(v)[i] = v4;
@@ -1280,8 +1303,9 @@ __global__ __launch_bounds__(256) void adam_ema_kernel(long n, long n4, float* _
     if (ema) reinterpret_cast<float4*>(ema)[i] = e4;
   }
   for (long i = 4 * n4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
-    float pi = p[i], gi = g[i], mi = m[i], vi = v[i];
-    adam_elem(a, pi, gi, mi, vi, ema ? ema + i : nullptr);
+    float pi = p[i], gi = g[i], mi = m[i], vi = v[i], ei = ema ? ema[i] : 0.f;
+    adam_elem(a, pi, gi, mi, vi, ei, ema != nullptr);
+    if (ema) ema[i] = ei;
     if (a.clip) g[i] = gi;
     m[i] = mi;
     v[i] = vi;

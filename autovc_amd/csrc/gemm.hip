@@ -869,8 +869,10 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
       // before the current one is combined)
       const double inv_pr = 1.0 / (double)BM;
       const double inv_last = 1.0 / (double)(d.M - (tilesM - 1) * BM);  // the short last partial
+      // (partials past tilesM lie past the descriptor's range and load as zeros: no branch, whose
+      // wait would serialise the batch's loads)
       auto ld = [&](int p, int h) {
-        return p < tilesM ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + h) * d.N + col) * 4, 0, 16)) : 0.f;
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((p * 2 + h) * d.N + col) * 4, 0, 16));
       };
       const float S0 = ld(0, 0);
       float Sv[4], Qv[4];
