@@ -590,7 +590,9 @@ struct L32Dir {
 // s + PF is fetched while step s computes (a register ring of PF steps, the loop unrolled by PF
 // so ring slots are static), and FAST selects hardware exp / reciprocal gate math
 // (sigma(x) = rcp(1 + 2^(-x log2 e)), tanh(x) = 2 sigma(2x) - 1; within ~1e-7 of the libm forms).
-template <int PF, bool FAST>
+// DIAG (timing experiments only, avc_lstm32_tune 2 / 3; results invalid): 1 = no output stores,
+// 2 = no input loads either
+template <int PF, bool FAST, int DIAG = 0>
 __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx, long ldy, L32Dir d0,
                                                         L32Dir d1) {
   const int dir = blockIdx.x >= B ? 1 : 0;
@@ -598,14 +600,14 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx,
   const int b = blockIdx.x - dir * B, lane = threadIdx.x;
   const float* __restrict__ gx = D.gx;
   const int reverse = D.reverse;
-  __shared__ __attribute__((aligned(16))) float hs[32];
+  __shared__ __attribute__((aligned(16))) float hs[64];  // [0, 32) h; [32, 64) lanes 32..63's unused writes
   float w0[32], w1[32];
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     w0[k] = D.whh[lane * 32 + k];
     w1[k] = D.whh[(lane + 64) * 32 + k];
   }
-  if (lane < 32) hs[lane] = 0.f;
+  hs[lane] = 0.f;
   float c = 0.f;
   auto grow = [&](int st) {
     const int sc = st < T ? st : T - 1;
@@ -619,6 +621,88 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx,
     if constexpr (FAST) return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f;
     else return tanhf(x);
   };
+  // Outputs as buffer stores, the same number of them on every path (round 5): lanes 32..63 and
+  // absent outputs (no c / gates outside training: a zero-sized descriptor) store out of range,
+  // which the hardware drops.  Stores under `lane < 32` / `if (D.c)` branches left the compiler's
+  // counted waits unable to count them, and the loop's back edge waited for every store (a write
+  // drain every PF steps).
+  constexpr unsigned kOut = 0x80000000u;
+  const long TB = (long)T * B;
+  const auto yrs = __builtin_amdgcn_make_buffer_rsrc(D.y, 0, (int)std::min<long>(TB * ldy * 4, 0x7fffffffL), 0x00020000);
+  const auto crs = __builtin_amdgcn_make_buffer_rsrc(D.c, 0, D.c ? (int)(TB * 32 * 4) : 0, 0x00020000);
+  const auto grs = __builtin_amdgcn_make_buffer_rsrc(D.gates, 0, D.gates ? (int)(TB * 128 * 4) : 0, 0x00020000);
+  const bool lo = lane < 32;
+  auto step = [&](int s, float z0, float z1) {
+    const int t = reverse ? T - 1 - s : s;
+    const long row = (long)t * B + b;
+    float a0, a1, fg, og;
+    if constexpr (FAST) {
+      // packed FMAs (v_pk_fma_f32: two k per instruction), two chains of 8 per gate row
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      f2 q0[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, q1[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+      for (int k4 = 0; k4 < 8; ++k4) {
+        const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
+        const f2 ha = {h4.x, h4.y}, hb = {h4.z, h4.w};
+        q0[0] = __builtin_elementwise_fma(f2{w0[4 * k4], w0[4 * k4 + 1]}, ha, q0[0]);
+        q0[1] = __builtin_elementwise_fma(f2{w0[4 * k4 + 2], w0[4 * k4 + 3]}, hb, q0[1]);
+        q1[0] = __builtin_elementwise_fma(f2{w1[4 * k4], w1[4 * k4 + 1]}, ha, q1[0]);
+        q1[1] = __builtin_elementwise_fma(f2{w1[4 * k4 + 2], w1[4 * k4 + 3]}, hb, q1[1]);
+      }
+      const f2 s0 = q0[0] + q0[1], s1 = q1[0] + q1[1];
+      z0 += s0.x + s0.y;
+      z1 += s1.x + s1.y;
+      a0 = sig(z0);                      // i (lane<32) or f
+      a1 = lo ? th(z1) : sig(z1);        // g (lane<32) or o
+      // lanes 32..63 -> 0..31 with one VALU swap of the wave halves instead of ds_bpermute
+      fg = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a0), false, false)[1]);
+      og = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(a1), __float_as_uint(a1), false, false)[1]);
+    } else {
+      // four independent FMA chains per gate row (8 deep instead of 32)
+      float p0[4] = {0.f, 0.f, 0.f, 0.f}, p1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k4 = 0; k4 < 8; ++k4) {
+        const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
+        p0[0] = fmaf(w0[4 * k4], h4.x, p0[0]);
+        p0[1] = fmaf(w0[4 * k4 + 1], h4.y, p0[1]);
+        p0[2] = fmaf(w0[4 * k4 + 2], h4.z, p0[2]);
+        p0[3] = fmaf(w0[4 * k4 + 3], h4.w, p0[3]);
+        p1[0] = fmaf(w1[4 * k4], h4.x, p1[0]);
+        p1[1] = fmaf(w1[4 * k4 + 1], h4.y, p1[1]);
+        p1[2] = fmaf(w1[4 * k4 + 2], h4.z, p1[2]);
+        p1[3] = fmaf(w1[4 * k4 + 3], h4.w, p1[3]);
+      }
+      z0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
+      z1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
+      a0 = sig(z0);
+      a1 = lo ? th(z1) : sig(z1);
+      fg = __shfl(a0, (lane + 32) & 63);
+      og = __shfl(a1, (lane + 32) & 63);
+    }
+    // every lane runs the cell update; only lanes 0..31's values are stored or read back.  (An
+    // explicit fma, the form the compiler had chosen here through round 4: left to contraction,
+    // f c + i g fused the other way round in the two-wave kernel.)
+    c = fmaf(a0, a1, fg * c);
+    const float h = og * th(c);
+    hs[lane] = h;
+    const unsigned oy = lo ? (unsigned)((row * ldy + lane) * 4) : kOut;
+    const unsigned oc = lo ? (unsigned)((row * 32 + lane) * 4) : kOut;
+    const unsigned og4 = lo ? (unsigned)((row * 128 + lane) * 4) : kOut;
+    if constexpr (DIAG == 0) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), yrs, oy, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(c), crs, oc, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a0), grs, og4, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fg), grs, lo ? og4 + 128 : kOut, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a1), grs, lo ? og4 + 256 : kOut, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(og), grs, lo ? og4 + 384 : kOut, 0, 0);
+    }
+    // one wave: LDS operations complete in issue order, so the next step's h reads only need
+    // the compiler not to move them above this write.  (__syncthreads() would also wait for
+    // every outstanding global load -- the prefetch ring -- and store on every step.)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
   float r0[PF], r1[PF];
 #pragma unroll
   for (int u = 0; u < PF; ++u) {
@@ -626,101 +710,171 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx,
     r1[u] = gx[grow(u) + lane + 64];
   }
   __syncthreads();
-  for (int s0 = 0; s0 < T; s0 += PF) {
+  int s0 = 0;
+  for (; s0 + PF <= T; s0 += PF) {
+    // the next group's input rows, all requested before this group's steps (round 5): with one
+    // refill per step the last refill sat behind only its own step's stores, and the back edge
+    // (the ring moves into the next iteration's registers) waited for them all.  Requested first,
+    // they are the oldest operations there.  (Unconditional, clamped by grow(): no joins.)
+    float n0[PF], n1[PF];
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
-      const int s = s0 + u;
-      // the ring refill is unconditional (grow() clamps to the last row): a refill under the
-      // s < T guard would make the slot a join of old and new values and wait for the load here
-      float z0 = r0[u], z1 = r1[u];
-      const long rn = grow(s + PF);
-      r0[u] = gx[rn + lane];
-      r1[u] = gx[rn + lane + 64];
-      if (s < T) {
-        const int t = reverse ? T - 1 - s : s;
-        const long row = (long)t * B + b;
-        float a0, a1, fg, og;
-        if constexpr (FAST) {
-          // packed FMAs (v_pk_fma_f32: two k per instruction), two chains of 8 per gate row
-          typedef float f2 __attribute__((ext_vector_type(2)));
-          f2 q0[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, q1[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+      const long rn = grow(s0 + PF + u);
+      n0[u] = DIAG == 2 ? 0.f : gx[rn + lane];
+      n1[u] = DIAG == 2 ? 0.f : gx[rn + lane + 64];
+    }
 #pragma unroll
-          for (int k4 = 0; k4 < 8; ++k4) {
-            const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
-            const f2 ha = {h4.x, h4.y}, hb = {h4.z, h4.w};
-            q0[0] = __builtin_elementwise_fma(f2{w0[4 * k4], w0[4 * k4 + 1]}, ha, q0[0]);
-            q0[1] = __builtin_elementwise_fma(f2{w0[4 * k4 + 2], w0[4 * k4 + 3]}, hb, q0[1]);
-            q1[0] = __builtin_elementwise_fma(f2{w1[4 * k4], w1[4 * k4 + 1]}, ha, q1[0]);
-            q1[1] = __builtin_elementwise_fma(f2{w1[4 * k4 + 2], w1[4 * k4 + 3]}, hb, q1[1]);
-          }
-          const f2 s0 = q0[0] + q0[1], s1 = q1[0] + q1[1];
-          z0 += s0.x + s0.y;
-          z1 += s1.x + s1.y;
-          a0 = sig(z0);                           // i (lane<32) or f
-          a1 = lane < 32 ? th(z1) : sig(z1);      // g (lane<32) or o
-          // lanes 32..63 -> 0..31 with one VALU swap of the wave halves instead of ds_bpermute
-          fg = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a0), false, false)[1]);
-          og = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(a1), __float_as_uint(a1), false, false)[1]);
-        } else {
-          // four independent FMA chains per gate row (8 deep instead of 32)
-          float p0[4] = {0.f, 0.f, 0.f, 0.f}, p1[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < PF; ++u) step(s0 + u, r0[u], r1[u]);
 #pragma unroll
-          for (int k4 = 0; k4 < 8; ++k4) {
-            const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
-            p0[0] = fmaf(w0[4 * k4], h4.x, p0[0]);
-            p0[1] = fmaf(w0[4 * k4 + 1], h4.y, p0[1]);
-            p0[2] = fmaf(w0[4 * k4 + 2], h4.z, p0[2]);
-            p0[3] = fmaf(w0[4 * k4 + 3], h4.w, p0[3]);
-            p1[0] = fmaf(w1[4 * k4], h4.x, p1[0]);
-            p1[1] = fmaf(w1[4 * k4 + 1], h4.y, p1[1]);
-            p1[2] = fmaf(w1[4 * k4 + 2], h4.z, p1[2]);
-            p1[3] = fmaf(w1[4 * k4 + 3], h4.w, p1[3]);
-          }
-          z0 += (p0[0] + p0[1]) + (p0[2] + p0[3]);
-          z1 += (p1[0] + p1[1]) + (p1[2] + p1[3]);
-          a0 = sig(z0);
-          a1 = lane < 32 ? th(z1) : sig(z1);
-          fg = __shfl(a0, (lane + 32) & 63);
-          og = __shfl(a1, (lane + 32) & 63);
+    for (int u = 0; u < PF; ++u) {
+      r0[u] = n0[u];
+      r1[u] = n1[u];
+    }
+  }
+  // the last T % PF steps (their rows are the ring's first slots)
+#pragma unroll
+  for (int u = 0; u < PF - 1; ++u)
+    if (s0 + u < T) step(s0 + u, r0[u], r1[u]);
+}
+
+// Round 5 (avc_lstm32_tune(1), the default): the same step math, with the memory operations taken
+// off the chain.  Wave 0 runs the recurrence touching only LDS and registers: its input rows come
+// from an LDS ring and its outputs go to an LDS ring.  Wave 1 fills the input ring one PF-step
+// group ahead and stores the previous group's outputs; the two meet at one barrier per group.
+// (Priced with avc_lstm32_tune 2 / 3: the one-wave kernel's loads and stores were ~100 of 383 us
+// per C5 layer.)  Same expressions, same order: the same bits as lstm32_fwd_kernel<PF, true>.
+template <int PF>
+__global__ __launch_bounds__(128) void lstm32_fwd2_kernel(int T, int B, long ldgx, long ldy, L32Dir d0,
+                                                          L32Dir d1) {
+  const int dir = blockIdx.x >= B ? 1 : 0;
+  const L32Dir& D = dir ? d1 : d0;
+  const int b = blockIdx.x - dir * B;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int reverse = D.reverse;
+  // one LDS array: hs [64] | input ring [2][PF][128] | output ring [2][PF][8][32]
+  // (output rows: h, c, i, f, g, o, and two rows lanes 32..63's h / c writes land in)
+  __shared__ __attribute__((aligned(16))) float lds[64 + 2 * PF * 128 + 2 * PF * 8 * 32];
+  float* const hs = lds;
+  float* const gxr = lds + 64;
+  float* const outr = gxr + 2 * PF * 128;
+  auto rowof = [&](int st) { return (long)(reverse ? T - 1 - st : st) * B + b; };
+  const int ngroups = (T + PF - 1) / PF;
+  // wave 1: input rows of group g into ring slot g & 1 (loads issued by load_issue, written by load_land)
+  float2 lv[PF];
+  auto load_issue = [&](int g) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int st = min(g * PF + u, T - 1);  // clamped: always issued
+      lv[u] = *reinterpret_cast<const float2*>(D.gx + rowof(st) * ldgx + 2 * lane);
+    }
+  };
+  auto load_land = [&](int g) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      *reinterpret_cast<float2*>(gxr + ((g & 1) * PF + u) * 128 + 2 * lane) = lv[u];
+  };
+  auto store_group = [&](int g) {  // wave 1: group g's outputs out of ring slot g & 1
+    for (int u = 0; u < PF; ++u) {
+      const int st = g * PF + u;
+      if (st >= T) break;
+      const long row = rowof(st);
+      const float* o = outr + ((g & 1) * PF + u) * 256;
+      if (lane < 32) D.y[row * ldy + lane] = o[lane];
+      else if (D.c) D.c[row * 32 + lane - 32] = o[32 + lane - 32];
+      if (D.gates) {
+        // gate k = 2 lane + e: row 2 + k / 32 of the ring, unit k % 32 (i, f, g, o)
+        const int k = 2 * lane;
+        *reinterpret_cast<float2*>(D.gates + row * 128 + k) =
+            make_float2(o[(2 + k / 32) * 32 + k % 32], o[(2 + k / 32) * 32 + k % 32 + 1]);
+      }
+    }
+  };
+  float w0[32], w1[32];
+  if (wv == 0) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      w0[k] = D.whh[lane * 32 + k];
+      w1[k] = D.whh[(lane + 64) * 32 + k];
+    }
+    hs[lane] = 0.f;
+  } else {
+    load_issue(0);
+    load_land(0);
+  }
+  __syncthreads();
+  auto sig = [](float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); };
+  auto th = [](float x) { return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f; };
+  const bool lo = lane < 32;
+  float c = 0.f;
+  for (int g = 0; g < ngroups; ++g) {
+    if (wv == 0) {
+      const float* gin = gxr + (g & 1) * PF * 128;
+      float* gout = outr + (g & 1) * PF * 256;
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        if (g * PF + u >= T) break;
+        float z0 = gin[u * 128 + lane], z1 = gin[u * 128 + 64 + lane];
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 q0[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, q1[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+        for (int k4 = 0; k4 < 8; ++k4) {
+          const float4 h4 = *reinterpret_cast<const float4*>(hs + 4 * k4);
+          const f2 ha = {h4.x, h4.y}, hb = {h4.z, h4.w};
+          q0[0] = __builtin_elementwise_fma(f2{w0[4 * k4], w0[4 * k4 + 1]}, ha, q0[0]);
+          q0[1] = __builtin_elementwise_fma(f2{w0[4 * k4 + 2], w0[4 * k4 + 3]}, hb, q0[1]);
+          q1[0] = __builtin_elementwise_fma(f2{w1[4 * k4], w1[4 * k4 + 1]}, ha, q1[0]);
+          q1[1] = __builtin_elementwise_fma(f2{w1[4 * k4 + 2], w1[4 * k4 + 3]}, hb, q1[1]);
         }
-        if (lane < 32) {
-          c = fg * c + a0 * a1;
-          const float h = og * th(c);
-          hs[lane] = h;
-          D.y[row * ldy + lane] = h;
-          if (D.c) D.c[row * 32 + lane] = c;
-          if (D.gates) {
-            float* g = D.gates + row * 128;
-            g[lane] = a0;
-            g[32 + lane] = fg;
-            g[64 + lane] = a1;
-            g[96 + lane] = og;
-          }
-        }
-        // one wave: LDS operations complete in issue order, so the next step's h reads only need
-        // the compiler not to move them above this write.  (__syncthreads() would also wait for
-        // every outstanding global load -- the prefetch ring -- and store on every step.)
+        const f2 s0 = q0[0] + q0[1], s1 = q1[0] + q1[1];
+        z0 += s0.x + s0.y;
+        z1 += s1.x + s1.y;
+        const float a0 = sig(z0);                 // i (lane<32) or f
+        const float a1 = lo ? th(z1) : sig(z1);   // g (lane<32) or o
+        const float fg = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a0), false, false)[1]);
+        const float og = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(a1), __float_as_uint(a1), false, false)[1]);
+        c = fmaf(a0, a1, fg * c);  // (as lstm32_fwd_kernel; lanes 32..63 carry a value nobody reads)
+        const float h = og * th(c);
+        hs[lane] = h;
+        float* o = gout + u * 256;
+        const int l = lane & 31;
+        o[(lo ? 0 : 6) * 32 + l] = h;
+        o[(lo ? 1 : 7) * 32 + l] = c;
+        o[(lo ? 2 : 3) * 32 + l] = a0;  // i | f
+        o[(lo ? 4 : 5) * 32 + l] = a1;  // g | o
+        // one wave: LDS operations complete in issue order (see lstm32_fwd_kernel)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
+    } else {
+      if (g + 1 < ngroups) load_issue(g + 1);
+      if (g > 0) store_group(g - 1);
+      if (g + 1 < ngroups) load_land(g + 1);
     }
+    // both rings change hands: LDS operations drained, no wait for the helper's global stores
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
+  if (wv == 1) store_group(ngroups - 1);
 }
 
 int g_dg_dual = 1;  // avc_dg_dual_split(): one pass writes both split images of dG (dX and dW products)
-int g_lstm32_mode = 1;  // avc_lstm32_tune(): 0 = libm gate math, 3-step prefetch; 1 = fast math, 8 steps
+int g_lstm32_mode = 1;  // avc_lstm32_tune(): 0 = libm gate math, 3-step prefetch; 1 = fast math with a
+                        // memory wave (lstm32_fwd2_kernel); 4 = fast math, one wave
 
 void launch_lstm32(int nblk, int T, int B, long ldgx, long ldy, const L32Dir& d0, const L32Dir& d1, hipStream_t s) {
   if (g_lstm32_mode == 0) lstm32_fwd_kernel<3, false><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
-  else lstm32_fwd_kernel<8, true><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
+  else if (g_lstm32_mode == 2) lstm32_fwd_kernel<8, true, 1><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
+  else if (g_lstm32_mode == 3) lstm32_fwd_kernel<8, true, 2><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
+  else if (g_lstm32_mode == 4) lstm32_fwd_kernel<8, true><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
+  else lstm32_fwd2_kernel<8><<<nblk, 128, 0, s>>>(T, B, ldgx, ldy, d0, d1);
 }
 
 // BPTT of an H = 32 direction: one single-wave workgroup per utterance walks the steps backwards.
-// Lane j (< 32) owns hidden unit j's cell math; lanes 32..63 add the other half of the
-// dh = W_hh^T dG sum.  The per-step operands (dy, the saved gates, c_t, c_{t-1}) come from a
-// register ring refilled PF steps ahead (loop unrolled by PF: static slots; refills are
-// unconditional and clamped so no join waits on them), and the dG broadcast through LDS needs
+// Lanes j and j + 32 each add one half of unit j's dh = W_hh^T dG sum and, after exchanging
+// them, both run its cell math (lanes 32..63 store nothing).  The per-step operands (dy, the
+// saved gates, c_t, c_{t-1}) come from a register ring whose next group is requested before a
+// group's steps (loop unrolled by PF: static slots; clamped, so no join waits on them), and the dG broadcast through LDS needs
 // no barrier: one wave's LDS operations complete in issue order (see lstm32_fwd_kernel).
 // FAST (round 4, avc_lstm32_tune(1), the default): the 64-term dot product as two packed-FMA
 // chains (v_pk_fma_f32, 16 instructions deep each, instead of one 64-deep scalar chain), and
@@ -753,78 +907,93 @@ __global__ __launch_bounds__(64) void lstm32_bwd_kernel(int T, int B, int revers
     return reverse ? T - s : s - 1;  // may be T or -1 at the ends (then unused)
   };
   float rdy[PF], rg[PF][4], rc[PF], rcp[PF];
-  auto fetch = [&](int k, int u) {
+  auto fetch = [&](int k, float& fdy, float (&fg4)[4], float& fc, float& fcp) {
     const long row = (long)tof(k) * B + b;
     const int tp = tprev(k);
-    rdy[u] = dy[row * lddy + j];
+    fdy = dy[row * lddy + j];
     const float* g = gates + row * 128;
-    rg[u][0] = g[j]; rg[u][1] = g[32 + j]; rg[u][2] = g[64 + j]; rg[u][3] = g[96 + j];
-    rc[u] = cs[row * 32 + j];
+    fg4[0] = g[j]; fg4[1] = g[32 + j]; fg4[2] = g[64 + j]; fg4[3] = g[96 + j];
+    fc = cs[row * 32 + j];
     const int tpc = min(max(tp, 0), T - 1);
-    rcp[u] = cs[((long)tpc * B + b) * 32 + j];
+    fcp = cs[((long)tpc * B + b) * 32 + j];
   };
+  // dG rows as buffer stores, the same number on every path (see lstm32_fwd_kernel): both wave
+  // halves compute the same unit j (the dot product is completed across them), and lanes 32..63
+  // store out of range.  Stores under `lane < 32` left the back edge waiting for all of them.
+  constexpr unsigned kOut = 0x80000000u;
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc(dg, 0, (int)std::min<long>((long)T * B * 128 * 4, 0x7fffffffL),
+                                                     0x00020000);
+  auto step = [&](int k, float dyv, const float (&g4)[4], float c, float cpv) {
+    const float ig = g4[0], fg = g4[1], gg = g4[2], og = g4[3];
+    const int s = T - 1 - k;
+    const int t = reverse ? T - 1 - s : s;
+    const long row = (long)t * B + b;
+    float part = 0.f;
+    if constexpr (FAST) {
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      f2 q[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
-  for (int u = 0; u < PF; ++u) fetch(u, u);
-  for (int k0 = 0; k0 < T; k0 += PF) {
+      for (int q4 = 0; q4 < 16; ++q4) {
+        const float4 gq = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
+        q[0] = __builtin_elementwise_fma(f2{wc[4 * q4], wc[4 * q4 + 1]}, f2{gq.x, gq.y}, q[0]);
+        q[1] = __builtin_elementwise_fma(f2{wc[4 * q4 + 2], wc[4 * q4 + 3]}, f2{gq.z, gq.w}, q[1]);
+      }
+      const f2 sq = q[0] + q[1];
+      part = sq.x + sq.y;
+    } else {
 #pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const int k = k0 + u;
-      const float dyv = rdy[u], ig = rg[u][0], fg = rg[u][1], gg = rg[u][2], og = rg[u][3];
-      const float c = rc[u], cpv = rcp[u];
-      fetch(k + PF, u);  // unconditional (clamped): the slot is never a join of old and new values
-      if (k < T) {
-        const int s = T - 1 - k;
-        const int t = reverse ? T - 1 - s : s;
-        const long row = (long)t * B + b;
-        float part = 0.f;
-        if constexpr (FAST) {
-          typedef float f2 __attribute__((ext_vector_type(2)));
-          f2 q[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
-#pragma unroll
-          for (int q4 = 0; q4 < 16; ++q4) {
-            const float4 g4 = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
-            q[0] = __builtin_elementwise_fma(f2{wc[4 * q4], wc[4 * q4 + 1]}, f2{g4.x, g4.y}, q[0]);
-            q[1] = __builtin_elementwise_fma(f2{wc[4 * q4 + 2], wc[4 * q4 + 3]}, f2{g4.z, g4.w}, q[1]);
-          }
-          const f2 sq = q[0] + q[1];
-          part = sq.x + sq.y;
-        } else {
-#pragma unroll
-          for (int q4 = 0; q4 < 16; ++q4) {
-            const float4 g4 = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
-            part += wc[4 * q4] * g4.x + wc[4 * q4 + 1] * g4.y + wc[4 * q4 + 2] * g4.z + wc[4 * q4 + 3] * g4.w;
-          }
-        }
-        part += __shfl_xor(part, 32);
-        float dzi = 0.f, dzf = 0.f, dzg = 0.f, dzo = 0.f;
-        if (lane < 32) {
-          const float dh = dyv + part;
-          const float cp = s > 0 ? cpv : 0.f;
-          // (FAST: lstm32_fwd_kernel<8, true>'s th(c))
-          const float tc = FAST ? 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * c)) - 1.f : tanhf(c);
-          const float dct = dh * og * (1.f - tc * tc) + dc;
-          dc = dct * fg;
-          dzi = dct * gg * ig * (1.f - ig);
-          dzf = dct * cp * fg * (1.f - fg);
-          dzg = dct * ig * (1.f - gg * gg);
-          dzo = dh * tc * og * (1.f - og);
-          float* o = dg + row * 128;
-          o[j] = dzi;
-          o[32 + j] = dzf;
-          o[64 + j] = dzg;
-          o[96 + j] = dzo;
-          // one wave: these LDS writes land after this step's dgs reads (issue order)
-          dgs[j] = dzi;
-          dgs[32 + j] = dzf;
-          dgs[64 + j] = dzg;
-          dgs[96 + j] = dzo;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int q4 = 0; q4 < 16; ++q4) {
+        const float4 gq = *reinterpret_cast<const float4*>(dgs + half * 64 + 4 * q4);
+        part += wc[4 * q4] * gq.x + wc[4 * q4 + 1] * gq.y + wc[4 * q4 + 2] * gq.z + wc[4 * q4 + 3] * gq.w;
       }
     }
+    // (lanes j and j + 32 add the same two halves: both hold the full sum)
+    part += __shfl_xor(part, 32);
+    const float dh = dyv + part;
+    const float cp = s > 0 ? cpv : 0.f;
+    // (FAST: lstm32_fwd_kernel<8, true>'s th(c))
+    const float tc = FAST ? 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * c)) - 1.f : tanhf(c);
+    const float dct = dh * og * (1.f - tc * tc) + dc;
+    dc = dct * fg;
+    const float dzi = dct * gg * ig * (1.f - ig);
+    const float dzf = dct * cp * fg * (1.f - fg);
+    const float dzg = dct * ig * (1.f - gg * gg);
+    const float dzo = dh * tc * og * (1.f - og);
+    const unsigned o = half ? kOut : (unsigned)((row * 128 + j) * 4);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dzi), drs, o, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dzf), drs, half ? kOut : o + 128, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dzg), drs, half ? kOut : o + 256, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dzo), drs, half ? kOut : o + 384, 0, 0);
+    // one wave: these LDS writes land after this step's dgs reads (issue order); both halves
+    // write the same values
+    dgs[j] = dzi;
+    dgs[32 + j] = dzf;
+    dgs[64 + j] = dzg;
+    dgs[96 + j] = dzo;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) fetch(u, rdy[u], rg[u], rc[u], rcp[u]);
+  int k0 = 0;
+  for (; k0 + PF <= T; k0 += PF) {
+    // the next group's operands requested before this group's steps (see lstm32_fwd_kernel)
+    float ndy[PF], ng[PF][4], nc[PF], ncp[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) fetch(k0 + PF + u, ndy[u], ng[u], nc[u], ncp[u]);  // clamped: no joins
+#pragma unroll
+    for (int u = 0; u < PF; ++u) step(k0 + u, rdy[u], rg[u], rc[u], rcp[u]);
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      rdy[u] = ndy[u]; rc[u] = nc[u]; rcp[u] = ncp[u];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rg[u][q] = ng[u][q];
+    }
   }
+#pragma unroll
+  for (int u = 0; u < PF - 1; ++u)
+    if (k0 + u < T) step(k0 + u, rdy[u], rg[u], rc[u], rcp[u]);
 }
 
 inline int ew_blocks(long n) { return (int)std::min<long>((n + 255) / 256, 8192); }
@@ -1201,8 +1370,9 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
     colpart = cp;
   }
   if (small) {
-    if (g_lstm32_mode == 0) lstm32_bwd_kernel<8, false><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
-    else lstm32_bwd_kernel<8, true><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
+    // (PF 4: a group's 28 operand loads + 16 stores stay inside the 63 counted vector-memory ops)
+    if (g_lstm32_mode == 0) lstm32_bwd_kernel<4, false><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
+    else lstm32_bwd_kernel<4, true><<<B, 64, 0, s>>>(T, B, reverse, w_hh, saved_gates, saved_c, d_y, ldy, dg);
     AVC_LAUNCH_CHECK();
   } else if (gemm_bptt) {
     // W_hh^T permuted ([H][4H]: row j = hidden unit, k = permuted gate row), split once with the
@@ -1432,8 +1602,8 @@ extern "C" int avc_lstm_tune(int rows_per_block, int waves) {
 }
 
 extern "C" int avc_lstm32_tune(int mode) {
-  if (mode < 0 || mode > 1) {
-    avc::set_error("avc_lstm32_tune: mode must be 0 or 1");
+  if (mode < 0 || mode > 4) {
+    avc::set_error("avc_lstm32_tune: mode must be 0, 1 or 4 (2, 3: timing experiments, outputs invalid)");
     return AVC_ERR_INVALID;
   }
   avc::g_lstm32_mode = mode;
