@@ -85,6 +85,7 @@ _SIGS = {
     "avc_lstm_persist_sentinel": [_I],
     "avc_lstm_persist_st16": [_I],
     "avc_lstm_persist_chunkwait": [_I],
+    "avc_gemm_plan_rounds": [_I],
     "avc_lstm_persist_granules": [_I],
     "avc_lstm_persist_halves": [_I],
     "avc_bn_bwd_frag": [_I],

@@ -1455,6 +1455,8 @@ struct Plan {
   int bm, bn, tilesM, tilesN, kt_per_tap, ktotal, nsplit, kps;
 };
 
+int g_plan_rounds = 1;  // avc_gemm_plan_rounds(): round-aware split-K count for long-K products
+
 Plan make_plan(const GemmDesc& d, int force_split) {
   Plan p;
   // long-K products (weight gradients: K = T*B rows) take 128x128 tiles and split K until the
@@ -1476,6 +1478,28 @@ Plan make_plan(const GemmDesc& d, int force_split) {
     ns = std::min(ns, p.ktotal / 16);
     ns = std::min(ns, 32);
     ns = std::max(ns, 1);
+    if (g_plan_rounds) {
+      // round-aware split (round 5, avc_gemm_plan_rounds): the grid runs in rounds of one
+      // workgroup per CU, so a split count whose grid spills a few workgroups into an extra round
+      // pays that whole round (the conv weight gradients: 80 tiles x 13 splits = 1040 workgroups,
+      // 4.06 rounds on 256 CUs).  Among ns / 2 .. 2 ns, take the count that minimises rounds x
+      // K-steps per split, plus each split's slab write + read (~0.75 us per 32-deep K-step,
+      // ~5 TB/s for the slab)
+      const int cus = std::max(1, coresident_cus());
+      const double slab_us = (double)d.M * d.N * d.nz * 8.0 / 5.0e6;
+      double best = 1e30;
+      int pick = ns;
+      for (int n = std::max(1, ns / 2); n <= std::min({2 * ns, 32, std::max(1, p.ktotal / 16)}); ++n) {
+        const long rounds = (blocks * n + cus - 1) / cus;
+        const long kps = (p.ktotal + n - 1) / n;
+        const double cost = (double)rounds * kps * 0.75 + n * slab_us;
+        if (cost < best - 1e-9) {
+          best = cost;
+          pick = n;
+        }
+      }
+      ns = pick;
+    }
   } else if (!d.stats && blocks < 256 && p.ktotal >= 16) {
     ns = (int)((512 + blocks - 1) / blocks);
     ns = std::min(ns, p.ktotal / 8);
@@ -2118,6 +2142,16 @@ extern "C" int avc_gemm_config(int cfg) {
     return AVC_ERR_INVALID;
   }
   avc::g_gemm_cfg = cfg;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_gemm_plan_rounds(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_gemm_plan_rounds: 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_plan_rounds = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -361,6 +361,11 @@ int avc_lstm_persist_st16(int on);
  * chunk ahead of the loads) instead of for the whole K quarter a wave reads; 0 (default) = the
  * quarter counters.  Same products in the same order: bit-identical outputs. */
 int avc_lstm_persist_chunkwait(int on);
+/* Tuning hook (round 5): 1 (default) = long-K products (weight gradients) pick their split-K count
+ * by rounds of one workgroup per CU (a grid that spills a few workgroups into an extra round pays
+ * the whole round); 0 = ~4 workgroups per CU (round 4).  The sums split differently: not
+ * bit-identical, same accuracy. */
+int avc_gemm_plan_rounds(int on);
 /* Tuning hook: 1 = the two-layer persistent form (decoder lstm2, batch > 16) walks its
  * workgroup's rows as two independent batch halves, step t of one half while the other half's
  * hand-off is in flight (counters per step and half); 0 (default, measured faster) = all rows at
