@@ -87,25 +87,31 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
   AVC_CHECK_ARG(training || (running_mean && running_var), "conv: eval mode needs running stats");
   AVC_CHECK_ARG(!training || (long)T * B > 1, "BatchNorm in training mode needs more than 1 value per channel");
   Scratch sc(ctx);
-  bool fresh = true;
-  float* wt = prep_or_scratch<float>(ctx, sc, PREP_CONV_WT, weight, nullptr, 5UL * cin * cout, &fresh);
-  if (!wt) return AVC_ERR_WORKSPACE;
-  if (fresh) {
-    conv_weight_fwd_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wt, cin, cout);
-    AVC_LAUNCH_CHECK();
-  }
-  GemmDesc g = conv_fwd_desc(T, B, cin, cout, x, wt, bias, y_pre);
+  GemmDesc g = conv_fwd_desc(T, B, cin, cout, x, weight, bias, y_pre);
   g.a_frag = x_frag;
   g.a_frag_guard = x_frag ? x_frag_guard : nullptr;  // x_frag split with that guard's scale (frames_frag)
   if (x_amax) g.a_guard = x_amax + 1;
   if (!out && !out_frag) out_amax = nullptr;
-  if (ctx->prep_version >= 0) {  // cache the split-f16 copy of the taps as well
-    bool fb = true;
-    auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_CONV_BFRAG, weight, nullptr, gemm_bfrag_bytes(g), &fb));
-    if (bf) {
-      if (fb) AVC_TRY(gemm_prepare_bfrag(g, bf, s));
-      g.b_frag = bf;
+  if (gemm_frag_eligible(g)) {
+    // the split-f16 taps straight from the PyTorch layout (GemmDesc::b_conv; round 5: no
+    // transposed fp32 copy), cached per weight version inside the whole-Generator forward
+    g.b_conv = 1;
+    if (ctx->prep_version >= 0) {
+      bool fb = true;
+      auto* bf = static_cast<_Float16*>(prep_buffer(ctx, PREP_CONV_BFRAG, weight, nullptr, gemm_bfrag_bytes(g), &fb));
+      if (bf && fb) AVC_TRY(gemm_prepare_bfrag(g, bf, s));
+      if (bf) g.b_frag = bf;
     }
+  } else {  // every other path reads the taps as a transposed fp32 copy
+    g.b_conv = 0;
+    bool fresh = true;
+    float* wt = prep_or_scratch<float>(ctx, sc, PREP_CONV_WT, weight, nullptr, 5UL * cin * cout, &fresh);
+    if (!wt) return AVC_ERR_WORKSPACE;
+    if (fresh) {
+      conv_weight_fwd_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wt, cin, cout);
+      AVC_LAUNCH_CHECK();
+    }
+    g.B = wt;
   }
   float* stats = nullptr;
   int nparts = 0, part_rows = 0;
@@ -226,10 +232,15 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
   gd.A = dy; gd.amax_a = amax_dy;
   gw.A = dy; gw.amax_a = amax_dy;
   if (d_x) {
-    AVC_TAKE(wd, float, 5UL * cin * cout, sc);
-    conv_weight_dgrad_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wd, cin, cout);
-    AVC_LAUNCH_CHECK();
-    gd.B = wd;
+    gd.B = weight;
+    gd.b_conv = 2;  // the split reads the PyTorch layout (GemmDesc::b_conv, round 5)
+    if (!gemm_frag_eligible(gd)) {
+      gd.b_conv = 0;
+      AVC_TAKE(wd, float, 5UL * cin * cout, sc);
+      conv_weight_dgrad_kernel<<<ew_blocks(5L * cin * cout), 256, 0, s>>>(weight, wd, cin, cout);
+      AVC_LAUNCH_CHECK();
+      gd.B = wd;
+    }
     AVC_TRY(gemm_run(ctx, gd, s));
   }
   if (d_weight) AVC_TRY(gemm_run(ctx, gw, s));

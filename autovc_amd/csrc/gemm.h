@@ -48,6 +48,10 @@ struct GemmDesc {
   int a_trans = 0;
   const float* B = nullptr; long ldb = 0; long b_rows = 0; long b_shift0 = 0; long b_zshift = 0;
   long b_tapoff = 0; int b_trans = 0;
+  // B straight from a PyTorch Conv1d weight W[co][ci][5] (split-f16 fragment path only, round 5):
+  // 1 = the forward, element (k = ci, n = co) of tap tau at W[n][k][tau]; 2 = the data gradient,
+  // element (k = co, n = ci) of tap tau at W[k][n][4 - tau].  Replaces the transposed fp32 copies.
+  int b_conv = 0;
   int nz = 1; long a_zoff = 0; long c_zoff = 0;
   float* C = nullptr; long ldc = 0; long ldc_col = 1; int accumulate = 0;
   const float* bias0 = nullptr; const float* bias1 = nullptr; int act = AVC_ACT_NONE;

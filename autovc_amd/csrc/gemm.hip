@@ -1646,7 +1646,22 @@ void absmax_taps(const float* src, int ntaps, long tapoff, long rows, long cols,
   for (int tau = 0; tau < ntaps; ++tau) absmax2d(src + (long)tau * tapoff, rows, cols, ld, out, s);
 }
 
+// where the B split reads element (n, k) of tap tau: p[n * rs + k * ks + tau * tap]
+struct BSrc {
+  const float* p;
+  long rs, ks, tap;
+};
+BSrc b_src(const GemmDesc& d) {
+  if (d.b_conv == 1) return {d.B, 5L * d.Kc, 5, 1};
+  if (d.b_conv == 2) return {d.B + 4, 5, 5L * d.N, -1};
+  return {d.B, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.b_tapoff};
+}
+
 void absmax_b(const GemmDesc& d, unsigned* w, hipStream_t s) {
+  if (d.b_conv) {  // the whole weight, one contiguous scan
+    absmax2d(d.B, 1, 5L * d.N * d.Kc, 5L * d.N * d.Kc, w, s);
+    return;
+  }
   const long b_rows = d.b_rows ? d.b_rows : (d.b_trans ? d.N : d.Kc);
   const long kb = d.b_trans ? d.Kc : std::min<long>(d.Kc, b_rows);
   if (d.b_trans) absmax_taps(d.B, d.ntaps, d.b_tapoff, d.N, kb, d.ldb, w, s);
@@ -1723,9 +1738,10 @@ int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
   unsigned* guard = bfrag_guard_word(d, dst);
   guard_init_kernel<<<1, 64, 0, stream>>>(guard, 1);
   absmax_b(d, guard, stream);
+  const BSrc bsrc = b_src(d);
   split_frag32_kernel<<<dim3((int)std::min<long>((tb + 255) / 256, 8192), d.ntaps), 256, 0, stream>>>(
-      d.B, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N, d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows),
-      (int)b_ntile, nkc, dst, guard, d.b_tapoff, tapstride);
+      bsrc.p, bsrc.rs, bsrc.ks, d.N, d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows),
+      (int)b_ntile, nkc, dst, guard, bsrc.tap, tapstride);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
@@ -1979,6 +1995,8 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
   }
   Frag16Args fa{};
   const bool frag = frag16_eligible(d);
+  AVC_CHECK_ARG(!d.b_conv || (frag && d.ntaps == 5 && !d.b_trans && d.b_rows == d.Kc),
+                "gemm: a Conv1d-layout B operand needs the split-f16 fragment path");
   const bool scaled_product = d.split_scale != 0;
   if (!frag) {  // only the split-f16 path scales its operands
     d.split_scale = 0;
@@ -2021,7 +2039,8 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
       }
       if (!d.amax_b) {
         const long kb = frag16_b_krows(d);
-        if (d.b_trans) absmax_taps(d.B, d.ntaps, d.b_tapoff, d.N, d.Kc, d.ldb, amax + 1, stream);
+        if (d.b_conv) absmax_b(d, amax + 1, stream);
+        else if (d.b_trans) absmax_taps(d.B, d.ntaps, d.b_tapoff, d.N, d.Kc, d.ldb, amax + 1, stream);
         else absmax_taps(d.B, d.ntaps, d.b_tapoff, kb, d.N, d.ldb, amax + 1, stream);
         d.amax_b = amax + 1;
       }
@@ -2049,9 +2068,9 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
       _Float16* tmp = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, (int)b_krows) / 2);
       if (!tmp) return AVC_ERR_WORKSPACE;
       const long tb = b_ntile * 32 * b_nkc * 2;
+      const BSrc bsrc = b_src(d);
       split_frag32_kernel<<<dim3((int)std::min<long>((tb + 255) / 256, 8192), d.ntaps), 256, 0, stream>>>(
-          d.B, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.N, (int)b_krows, (int)b_ntile, b_nkc, tmp,
-          d.amax_b, d.b_tapoff, tapstride);
+          bsrc.p, bsrc.rs, bsrc.ks, d.N, (int)b_krows, (int)b_ntile, b_nkc, tmp, d.amax_b, bsrc.tap, tapstride);
       bs = tmp;
     }
     AVC_LAUNCH_CHECK();
