@@ -47,7 +47,9 @@ _SIGS = {
     "avc_lstm_backward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P,
                           _P, _P, _P, _I, _I, _P],
     "avc_lstm_backward_ex": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P,
-                             _P, _P, _P, _I, _I, _I, _P],
+                             _P, _P, _P, _I, _I, _P, _I, _P],
+    "avc_lstm_forward_ex": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _P],
+    "avc_bilstm_forward_ex": [_P, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _P],
     "avc_linear_forward": [_P, _I, _I, _I, _P, _P, _P, _P, _P],
     "avc_linear_backward": [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P],
     "avc_frames_from_mel": [_I, _I, _I, _P, _I, _P, _P, _P],

@@ -383,6 +383,28 @@ int avc_lstm_forward(avc_context* ctx, int T, int B, int din, int H, int reverse
                            saved_gates, saved_c, S(stream));
 }
 
+int avc_lstm_forward_ex(avc_context* ctx, int T, int B, int din, int H, int reverse, const float* x,
+                        int ldx, const float* w_ih, const float* w_hh, const float* b_ih,
+                        const float* b_hh, float* y, int ldy, float* saved_gates, float* saved_c,
+                        const unsigned* x_amax, int x_unit, void* stream) {
+  AVC_CHECK_ARG(ctx, "NULL pointer");
+  AVC_CHECK_ARG(x_unit == 0 || x_unit == 1, "avc_lstm_forward_ex: x_unit must be 0 or 1");
+  XHintScope hint(ctx, x, x_amax, x_unit);
+  return avc_lstm_forward(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, b_ih, b_hh, y, ldy, saved_gates,
+                          saved_c, stream);
+}
+
+int avc_bilstm_forward_ex(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                          const float* const* w_f, const float* const* w_r, float* y, int ldy,
+                          float* saved_gates_f, float* saved_c_f, float* saved_gates_r, float* saved_c_r,
+                          const unsigned* x_amax, int x_unit, void* stream) {
+  AVC_CHECK_ARG(ctx, "NULL pointer");
+  AVC_CHECK_ARG(x_unit == 0 || x_unit == 1, "avc_bilstm_forward_ex: x_unit must be 0 or 1");
+  XHintScope hint(ctx, x, x_amax, x_unit);
+  return avc_bilstm_forward(ctx, T, B, din, H, x, ldx, w_f, w_r, y, ldy, saved_gates_f, saved_c_f, saved_gates_r,
+                            saved_c_r, stream);
+}
+
 int avc_bilstm_forward(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
                        const float* const* w_f, const float* const* w_r, float* y, int ldy,
                        float* saved_gates_f, float* saved_c_f, float* saved_gates_r,
@@ -414,10 +436,12 @@ int avc_lstm_backward_ex(avc_context* ctx, int T, int B, int din, int H, int rev
                          const float* x, int ldx, const float* w_ih, const float* w_hh,
                          const float* y, int ldy, const float* saved_gates, const float* saved_c,
                          const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh, float* d_b_ih,
-                         float* d_b_hh, int accumulate_dx, int accumulate_dw, int x_unit, void* stream) {
+                         float* d_b_hh, int accumulate_dx, int accumulate_dw, const unsigned* x_amax, int x_unit,
+                         void* stream) {
   AVC_CHECK_ARG(ctx && x && w_ih && w_hh && y && d_y && d_w_ih && d_w_hh && d_b_ih && d_b_hh, "NULL pointer");
   AVC_CHECK_ARG(x_unit == 0 || x_unit == 1, "avc_lstm_backward_ex: x_unit must be 0 or 1");
   AVC_TRY(ensure_arena(ctx, lstm_backward_scratch(T, B, din, H)));
+  XHintScope hint(ctx, x, x_amax, x_unit);
   return lstm_backward_impl(ctx, T, B, din, H, reverse, x, ldx, w_ih, w_hh, y, ldy, saved_gates,
                             saved_c, d_y, d_x, d_w_ih, d_w_hh, d_b_ih, d_b_hh, accumulate_dx,
                             accumulate_dw, S(stream), x_unit != 0);

@@ -124,6 +124,10 @@ struct avc_context {
   // activations whose range a producer already checked (or bounds by construction: an LSTM's h)
   // inside the current whole-Generator forward; their contractions skip the range scan
   bool track_ranges = false;
+  // What the caller of one per-layer LSTM call knows about its input x (XHintScope, round 5):
+  // its producer's max words ([0] max |x|, [1] max(max |x|, 2^14): ConvBNAct's out_amax), or that
+  // |x| <= 1 (x is another LSTM layer's h).  Products and splits that would scan x use them.
+  struct { const void* x; const unsigned* amax; bool unit; } xhint{nullptr, nullptr, false};
   std::vector<const void*> range_ok;
   // inside the whole-Generator forward: fp32 outputs of the persistent recurrences that nothing
   // reads (bit 0: the h whose split image y_frag the next contraction streams instead -- lstm1's,
@@ -175,6 +179,13 @@ struct RangeScope {
   avc_context* ctx;
   explicit RangeScope(avc_context* c) : ctx(c) { ctx->track_ranges = true; ctx->range_ok.clear(); }
   ~RangeScope() { ctx->track_ranges = false; ctx->range_ok.clear(); }
+};
+struct XHintScope {
+  avc_context* ctx;
+  XHintScope(avc_context* c, const void* x, const unsigned* amax, int unit) : ctx(c) {
+    ctx->xhint.x = x; ctx->xhint.amax = amax; ctx->xhint.unit = unit != 0;
+  }
+  ~XHintScope() { ctx->xhint.x = nullptr; ctx->xhint.amax = nullptr; ctx->xhint.unit = false; }
 };
 inline bool range_checked(const avc_context* ctx, const void* p) {
   for (const void* q : ctx->range_ok)

@@ -2010,6 +2010,10 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     float* part = sc.take<float>(kGuardBlocks);
     if (!gw || !part) return AVC_ERR_WORKSPACE;
     d.amax_a = nullptr;
+    if (!d.a_frag && !d.a_guard && d.A && d.A == ctx->xhint.x) {  // (XHintScope: x's producer's words)
+      if (ctx->xhint.amax) d.a_guard = ctx->xhint.amax + 1;
+      else if (ctx->xhint.unit) d.a_bound = 1.f;
+    }
     if (d.a_frag && d.a_frag_guard) {
       d.amax_a = d.a_frag_guard;  // the image's own scale (its producer range-checked A)
     } else if (d.a_guard && !d.a_frag) {

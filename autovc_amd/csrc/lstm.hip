@@ -1488,6 +1488,7 @@ int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int rever
   g1.C = dwih_dst; g1.ldc = din; g1.accumulate = acc_w;
   g1.prec16 = 1; g1.split_scale = 1; g1.amax_a = amax_dg;
   if (x_unit) g1.amax_b = h_bound_word();
+  else if (x == ctx->xhint.x && ctx->xhint.amax) g1.amax_b = ctx->xhint.amax;  // max |x| from its producer
   // dG^T is split once (the larger operand of both products: TB x 4H against TB x din / H); with
   // the dX product also streaming split dG, one pass writes both images (g_dg_dual)
   const bool share = gemm_frag_eligible(g1);

@@ -2009,7 +2009,9 @@ int attach_inproj(avc_context* ctx, Scratch& sc, const InProj& ip, int T, int B,
   const long hszx = (long)ntile * 16 * Kp * 2 * 2;
   AVC_TAKE(xs, unsigned char, (size_t)T * hszx, sc);
   const unsigned* amax = nullptr;
-  if (!range_checked(ctx, ip.x)) {
+  if (ip.x == ctx->xhint.x && (ctx->xhint.amax || ctx->xhint.unit)) {
+    amax = ctx->xhint.amax;  // max |x| from x's producer; |x| <= 1: unscaled (XHintScope)
+  } else if (!range_checked(ctx, ip.x)) {
     AVC_TAKE(am, unsigned, 2, sc);
     AVC_TRY(gemm_absmax(ip.x, (long)T * B, ip.din, ip.ldx, am, s));
     amax = am;

@@ -269,14 +269,15 @@ class ConvBNAct(torch.autograd.Function):
         return dx, dw, db, dg, dbt, None, None, None, None, None, None, d_res, None, None, None
 
 
-def _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, reverse, save, T, B):
+def _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, reverse, save, T, B, x_amax=None, x_unit=False):
     H = w_hh.shape[1]
     din = x.shape[1]
     gates = _empty((T * B, 4 * H), x) if save else None
     cst = _empty((T * B, H), x) if save else None
-    call("avc_lstm_forward", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
+    # x_amax / x_unit: what x's producer knows of its range (no scan of x; avc_lstm_forward_ex)
+    call("avc_lstm_forward_ex", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
          ptr(w_hh.contiguous()), ptr(b_ih), ptr(b_hh), y.data_ptr() + col * F32, ldy, ptr(gates),
-         ptr(cst), _stream(x))
+         ptr(cst), _wptr(x_amax), int(x_unit), _stream(x))
     if save and _sink is not None and _persistent_bptt(T, B, H):
         _sink.recurrences += 1
     return gates, cst
@@ -289,7 +290,7 @@ def _unit_bounded(x):
 
 
 def _lstm_bwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, gates, cst, d_y, d_x, reverse, acc, T, B, needs,
-              x_unit=False):
+              x_unit=False, x_amax=None):
     H = w_hh.shape[1]
     din = x.shape[1]
     params = (w_ih, w_hh, b_ih, b_hh)
@@ -305,7 +306,7 @@ def _lstm_bwd(x, w_ih, w_hh, b_ih, b_hh, y, col, ldy, gates, cst, d_y, d_x, reve
     call("avc_lstm_backward_ex", _ctx(x), T, B, din, H, int(reverse), ptr(x), din, ptr(w_ih.contiguous()),
          ptr(w_hh.contiguous()), y.data_ptr() + col * F32, ldy, ptr(gates), ptr(cst),
          d_y.data_ptr() + col * F32, ptr(d_x), *[ptr(t) for t in scratch], int(acc), int(direct),
-         int(x_unit), _stream(x))
+         _wptr(x_amax), int(x_unit), _stream(x))
     done = tuple(_param_done(params, (dwi, dwh, dbi, dbh), direct))
     if sink is not None:
         sink.recurrence_end()
@@ -317,11 +318,13 @@ class LSTMLayer(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, T, B, save):
-        ctx.x_unit = _unit_bounded(x)  # (x is the layer below's h: its weight gradient skips a scan)
+        # what x's producer knows of its range (a conv's max words, or |h| <= 1 of the layer below):
+        # the input projection, the input slot and the weight gradient skip their scans of x
+        ctx.x_amax, ctx.x_unit = _amax_of(x), _unit_bounded(x)
         x = x.contiguous()
         H = w_hh.shape[1]
         y = _empty((T * B, H), x)
-        gates, cst = _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, 0, H, False, save, T, B)
+        gates, cst = _lstm_fwd(x, w_ih, w_hh, b_ih, b_hh, y, 0, H, False, save, T, B, ctx.x_amax, ctx.x_unit)
         y._avc_unit = y._version  # |y| <= 1 (_unit_bounded)
         _use(w_ih, w_hh, b_ih, b_hh)
         if save:
@@ -337,7 +340,7 @@ class LSTMLayer(torch.autograd.Function):
         d_y = d_y.contiguous()
         d_x = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         dwi, dwh, dbi, dbh = _lstm_bwd(x, w_ih, w_hh, *ctx.biases, y, 0, y.shape[1], gates, cst, d_y, d_x, False, 0,
-                                       T, B, ctx.needs_input_grad[1:5], ctx.x_unit)
+                                       T, B, ctx.needs_input_grad[1:5], ctx.x_unit, ctx.x_amax)
         return d_x, dwi, dwh, dbi, dbh, None, None, None
 
 
@@ -346,6 +349,7 @@ class BiLSTMLayer(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wi_f, wh_f, bi_f, bh_f, wi_r, wh_r, bi_r, bh_r, T, B, save):
+        ctx.x_amax, ctx.x_unit = _amax_of(x), _unit_bounded(x)  # (see LSTMLayer)
         x = x.contiguous()
         H = wh_f.shape[1]
         y = _empty((T * B, 2 * H), x)
@@ -353,8 +357,9 @@ class BiLSTMLayer(torch.autograd.Function):
         (g_f, c_f), (g_r, c_r) = sv
         keep = [[t.contiguous() for t in grp] for grp in ((wi_f, wh_f, bi_f, bh_f), (wi_r, wh_r, bi_r, bh_r))]
         ws = [(ctypes.c_void_p * 4)(*[ptr(t) for t in grp]) for grp in keep]
-        call("avc_bilstm_forward", _ctx(x), T, B, x.shape[1], H, ptr(x), x.shape[1], ws[0], ws[1], ptr(y),
-             2 * H, ptr(g_f), ptr(c_f), ptr(g_r), ptr(c_r), _stream(x))
+        call("avc_bilstm_forward_ex", _ctx(x), T, B, x.shape[1], H, ptr(x), x.shape[1], ws[0], ws[1], ptr(y),
+             2 * H, ptr(g_f), ptr(c_f), ptr(g_r), ptr(c_r), _wptr(ctx.x_amax), int(ctx.x_unit), _stream(x))
+        y._avc_unit = y._version  # |y| <= 1 (_unit_bounded)
         _use(wi_f, wh_f, bi_f, bh_f, wi_r, wh_r, bi_r, bh_r)
         if save:
             ctx.save_for_backward(x, wi_f, wh_f, wi_r, wh_r, y, g_f, c_f, g_r, c_r)
@@ -370,8 +375,10 @@ class BiLSTMLayer(torch.autograd.Function):
         d_y = d_y.contiguous()
         ng = ctx.needs_input_grad
         d_x = torch.empty_like(x) if ng[0] else None
-        gf = _lstm_bwd(x, wi_f, wh_f, bi_f, bh_f, y, 0, 2 * H, g_f, c_f, d_y, d_x, False, 0, T, B, ng[1:5])
-        gr = _lstm_bwd(x, wi_r, wh_r, bi_r, bh_r, y, H, 2 * H, g_r, c_r, d_y, d_x, True, 1, T, B, ng[5:9])
+        gf = _lstm_bwd(x, wi_f, wh_f, bi_f, bh_f, y, 0, 2 * H, g_f, c_f, d_y, d_x, False, 0, T, B, ng[1:5],
+                       ctx.x_unit, ctx.x_amax)
+        gr = _lstm_bwd(x, wi_r, wh_r, bi_r, bh_r, y, H, 2 * H, g_r, c_r, d_y, d_x, True, 1, T, B, ng[5:9],
+                       ctx.x_unit, ctx.x_amax)
         return (d_x,) + gf + gr + (None, None, None)
 
 

@@ -156,14 +156,26 @@ int avc_lstm_backward(avc_context* ctx, int T, int B, int din, int H, int revers
                       const float* y, int ldy, const float* saved_gates, const float* saved_c,
                       const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh, float* d_b_ih,
                       float* d_b_hh, int accumulate_dx, int accumulate_dw, void* stream);
-/* As avc_lstm_backward; x_unit = 1 declares every |x| <= 1 (x is the previous stacked layer's h,
- * o * tanh(c)): the W_ih gradient's split of x then takes that bound instead of a max scan of x
- * (round 5).  Same products otherwise. */
+/* Round 5: the LSTM calls with what the caller knows about x, so no product or split scans it.
+ * x_amax (device, may be NULL): two words from x's producer, [0] = max |x|, [1] = max(max |x|, 2^14)
+ * (avc_conv_bn_act_forward_frag's out_amax); x_unit = 1: every |x| <= 1 (x is another LSTM layer's
+ * h = o tanh(c)).  The input projection's guard, the input slot's split scale and the W_ih
+ * gradient's split of x take them; with x_amax every value is the one the scan would have found
+ * (same bits), with x_unit the bound 1.  Otherwise as the calls without _ex. */
+int avc_lstm_forward_ex(avc_context* ctx, int T, int B, int din, int H, int reverse, const float* x,
+                        int ldx, const float* w_ih, const float* w_hh, const float* b_ih,
+                        const float* b_hh, float* y, int ldy, float* saved_gates, float* saved_c,
+                        const unsigned* x_amax, int x_unit, void* stream);
+int avc_bilstm_forward_ex(avc_context* ctx, int T, int B, int din, int H, const float* x, int ldx,
+                          const float* const* w_f, const float* const* w_r, float* y, int ldy,
+                          float* saved_gates_f, float* saved_c_f, float* saved_gates_r, float* saved_c_r,
+                          const unsigned* x_amax, int x_unit, void* stream);
 int avc_lstm_backward_ex(avc_context* ctx, int T, int B, int din, int H, int reverse,
                          const float* x, int ldx, const float* w_ih, const float* w_hh,
                          const float* y, int ldy, const float* saved_gates, const float* saved_c,
                          const float* d_y, float* d_x, float* d_w_ih, float* d_w_hh, float* d_b_ih,
-                         float* d_b_hh, int accumulate_dx, int accumulate_dw, int x_unit, void* stream);
+                         float* d_b_hh, int accumulate_dx, int accumulate_dw, const unsigned* x_amax,
+                         int x_unit, void* stream);
 
 /* ---- Linear (decoder.linear_projection, decoder.py:56,77; net_layers.py:3-20) ------------ */
 int avc_linear_forward(avc_context* ctx, int M, int din, int dout, const float* x,
