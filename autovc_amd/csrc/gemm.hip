@@ -2024,6 +2024,12 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     }
     if (d.b_frag) {
       d.amax_b = bfrag_guard_word(d, d.b_frag);
+    } else if (d.b_conv || (d.ntaps == 1 && d.b_trans && d.ldb == d.Kc)) {
+      // a contiguous B (a conv weight, or one [N][K] matrix): the one-launch guard scan (round 5;
+      // the same word as guard_init + absmax_b)
+      const long n = d.b_conv ? 5L * d.N * d.Kc : (long)d.N * d.Kc;
+      AVC_TRY(guard_scan(ctx, d.B, 1, n, n, part, gw + 1, stream));
+      d.amax_b = gw + 1;
     } else {
       guard_init_kernel<<<1, 64, 0, stream>>>(gw + 1, 1);
       absmax_b(d, gw + 1, stream);
