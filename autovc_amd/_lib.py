@@ -87,6 +87,8 @@ _SIGS = {
     "avc_lstm_persist_sentinel": [_I],
     "avc_lstm_persist_st16": [_I],
     "avc_lstm_persist_chunkwait": [_I],
+    "avc_lstm_persist_xcd": [_I],
+    "avc_debug_xl_census": [_P],
     "avc_gemm_plan_rounds": [_I],
     "avc_lstm_persist_granules": [_I],
     "avc_lstm_persist_halves": [_I],

@@ -189,11 +189,19 @@ struct PersistArgs {
   unsigned char* hsn;         // SN: split-h hand-off buffers [layer][2 sets][T][hsz] (in the region)
   long hsn_set, hsn_layer;    // SN: bytes per set (T * hsz) and per layer (two sets)
   int st16;                   // split-h hand-off stores as 16-B pieces (avc_lstm_persist_st16)
-  int nwg;                    // workgroups in the grid
+  // XL (round 5, avc_lstm_persist_xcd; one-layer form): a linear grid of 8 x ncb workgroups dealt
+  // so that workgroup bid is (slot residue bid % 8, column block bid / 8): under the round-robin
+  // XCD deal every recurrent group sits on one XCD.  Checked at run time (xl_tab); a group whose
+  // workgroups do share one XCD hands h over with plain stores (the lines stay in that XCD's L2,
+  // which its consumers' sc1 loads read), any other with the write-through stores.
+  int xl, xl_slots;           // xl_slots: residues in use (nslot * ngrp <= 8); the rest exit at once
+  unsigned* xl_tab;           // [8 * ncb] epoch-tagged XCD of each workgroup (in the region)
+  int nwg;                    // workgroups in the grid (XL: the active ones)
   unsigned spin_limit;        // polls before giving up (0 = test injection: give up at once)
   int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
 };
 int g_persist_diag = 0;
+__device__ unsigned g_xl_seen[2];  // (avc_debug_xl_census) recurrent workgroups that found their group local / not
 // avc_lstm_persist_qwait(): per-wave waits on quarter counters, bit 0 = two-layer form (lstm2:
 // 1141 -> 1073 us at C2), bit 1 = one-layer form (lstm1: 384 -> 400 us at C2, so off)
 int g_persist_qwait = 1;
@@ -499,11 +507,21 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
-  const int L = blockIdx.x / a.ncb, cb = blockIdx.x - L * a.ncb;
-  const int B = a.B, H = a.H, T = a.T;
+  int L, cb, grp;
   // batch group: rows [grp * MB, grp * MB + MB).  LSTM batch rows never interact, so in the
   // one-layer form every group is an independent recurrence with counters of its own.
-  const int grp = blockIdx.y;
+  if (a.xl) {  // (see PersistArgs::xl)
+    const int xs = blockIdx.x & 7;
+    if (xs >= a.xl_slots) return;  // an unused residue: no ticket, no counter
+    L = a.nslot == 2 ? (xs & 1) : 0;
+    grp = a.nslot == 2 ? xs >> 1 : xs;
+    cb = blockIdx.x >> 3;
+  } else {
+    L = blockIdx.x / a.ncb;
+    cb = blockIdx.x - L * a.ncb;
+    grp = blockIdx.y;
+  }
+  const int B = a.B, H = a.H, T = a.T;
   unsigned* const cnt = a.cnt + (long)grp * a.cnt_gstride;
   const int nck = H >> 5;            // 32-deep chunks per row
   const long G4 = 4L * H;
@@ -517,6 +535,38 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   __syncthreads();
   const unsigned E = (unsigned)flag[2];
   const unsigned target = E * (unsigned)a.ncb;
+
+  // XL: this group's recurrent workgroups record their XCD, then each checks that all of them share
+  // one (every member reads the same ncb words: the same decision).  Bounded like every wait.
+  bool xl_local = false;
+  if (a.xl && L == 0) {
+    if (tid < 64) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      const int xs = blockIdx.x & 7;
+      if (tid == 0)
+        __hip_atomic_store((gu32*)(a.xl_tab + blockIdx.x), (E << 4) | (xcc & 7u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      bool same = true, done = false;
+      for (unsigned spins = 0; !done; ++spins) {
+        bool all = true;
+        same = true;
+        for (int k = tid; k < a.ncb; k += 64) {
+          const unsigned v = __hip_atomic_load((gu32*)(a.xl_tab + k * 8 + xs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          all &= (v >> 4) == (E & 0x0fffffffu);
+          same &= (v & 7u) == (xcc & 7u);
+        }
+        done = __builtin_amdgcn_ballot_w64(!all) == 0ull;
+        if (!done && spin_give_up(spins, a, E, tid)) break;  // (then: the write-through stores)
+        if (!done) __builtin_amdgcn_s_sleep(2);
+      }
+      const bool ok = done && __builtin_amdgcn_ballot_w64(!same) == 0ull;
+      if (tid == 0) flag[3] = ok ? 1 : 0;
+    }
+    __syncthreads();
+    xl_local = flag[3] != 0;
+    if (tid == 0) atomicAdd(&g_xl_seen[xl_local ? 0 : 1], 1u);
+  }
 
   if (a.in_slot > 0 && L == a.in_slot) {  // layer 0's input projection
     if (a.din == 512) input_slot<RT * NH, 4, NH>(a, cnt, grp, part, flag, E, target, cb);
@@ -570,7 +620,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   float* g_save = L == 0 ? a.g0 : a.g1;
   float* y_out = L == 0 ? a.y0 : a.y1;
   auto gx1_slab = [&](int tt, int c) -> long { return ((long)(tt % kGxRing) * a.ncb + c) * (64 * TW); };
-  const int rep = blockIdx.x & (kRep - 1);
+  const int rep = (a.xl ? blockIdx.x >> 3 : blockIdx.x) & (kRep - 1);
   // outputs nobody reads inside this launch: h, and for training c and the activated gates
   _Float16* const yfrag = L == a.yf_slot ? a.yfrag : nullptr;
   // frag: also this thread's units of y_frag (the give-up NaN fill; normally yfrag_rows writes it)
@@ -678,6 +728,29 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     // slot running far ahead streams gx0 / writes h0 through the Infinity Cache and starves the
     // others: measured as a bistable 10 vs 20 us per step).  Each polling lane then acquires.
     // With slot 3 (nslot == 4) a third lane (wave 2) waits for this step's gx0.
+    // XL-local group (round 5): the previous step's h producers signal through one line of tags in
+    // this XCD's L2 (plain stores, sc1 loads; PersistArgs::xl) instead of the counter, polled by
+    // wave 0 (one load per poll covers all of them)
+    const bool xlf = xl_local && L == 0 && t > 0;
+    if (xlf && tid < 64) {
+      const unsigned want = E * (unsigned)(T + 1) + (unsigned)t;  // step t - 1's tag (see the publish)
+      const auto frs = __builtin_amdgcn_make_buffer_rsrc(a.xl_tab + 8 * a.ncb + grp * 32, 0, 128, 0x00020000);
+      auto ld = [&]() {
+        return lane < a.ncb ? __builtin_amdgcn_raw_buffer_load_b32(frs, lane * 4, 0, 16 /*sc1*/) : want;
+      };
+      bool ok = true;
+      unsigned v = ld();
+      for (unsigned spins = 0; __builtin_amdgcn_ballot_w64((int)(v - want) < 0) != 0ull; ++spins) {
+        if (spin_give_up(spins, a, E, lane)) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v = ld();
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+      if (lane == 0) flag[0] = ok ? 1 : 0;
+    }
     if (tid == 0 || tid == 64 || tid == 128) {
       const bool primary = tid == 0;
       long idx = -1;
@@ -685,7 +758,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       // for 4 steps at once: its workgroups finish steps in order, so all of them counting in on
       // step t + 3 implies steps t .. t + 2 are complete (and drained) as well
       if (tid == 128) idx = L == 0 && a.in_slot > 0 && (t & 3) == 0 ? cnt_index(a.in_slot, TT, min(t + 3, T - 1), rep) : -1;
-      else if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, TT, t - 1, rep) : -1)
+      else if (L == 0) idx = primary ? (t > 0 && !xlf ? cnt_index(0, TT, t - 1, rep) : -1)
                                      : (t >= kLead && a.nslot >= 3 ? cnt_index(2, TT, t - kLead, rep) : -1);
       else if (L == 1) idx = primary ? cnt_index(0, TT, t, rep)
                                      : (t >= kGxRing ? cnt_index(2, TT, t - kGxRing, rep) : -1);
@@ -701,7 +774,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       } else {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
       }
-      flag[tid == 128 ? 3 : (primary ? 0 : 1)] = ok ? 1 : 0;
+      if (!(primary && xlf)) flag[tid == 128 ? 3 : (primary ? 0 : 1)] = ok ? 1 : 0;
     }
     __syncthreads();
     if (flag[0] == 0 || flag[1] == 0 || flag[3] == 0) break;
@@ -1093,7 +1166,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           if constexpr (SN) hb = a.hsn + (L == 0 ? 0 : a.hsn_layer) + (long)t * a.hsz + (long)(E & 1u) * a.hsn_set;
           else hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
           const auto ors = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)a.hsz, 0x00020000);
-          if (a.st16) {
+          if (xl_local) {  // (XL: the group's XCD keeps the lines in its L2; consumers load sc1 from it)
+            __builtin_amdgcn_raw_buffer_store_b128(pc, ors, off16, 0, 0);
+          } else if (a.st16) {
             __builtin_amdgcn_raw_buffer_store_b128(pc, ors, off16, 0, 16 /*sc1*/);
           } else {
             __builtin_amdgcn_raw_buffer_store_b64(hi2, ors, (int)off, 0, 16 /*sc1*/);
@@ -1133,6 +1208,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     AVC_PRSTAMP(6);
     // lanes 8..15 count in on this workgroup's quarter -- in both wait forms, so every launch adds
     // ncb / 4 to every quarter word and the epoch targets hold whichever form the next launch takes
+    if (xl_local && L == 0 && tid == 0)  // (XL: this workgroup's tag for step s, after every wave's drain)
+      __builtin_amdgcn_raw_buffer_store_b32(E * (unsigned)(T + 1) + (unsigned)s + 1u,
+                                            __builtin_amdgcn_make_buffer_rsrc(a.xl_tab + 8 * a.ncb + grp * 32, 0, 128,
+                                                                              0x00020000),
+                                            cb * 4, 0, 0);
     if (publish && tid < (CW && (L == 0 || L == 2) ? 3 : 2) * kRep) {
       const long ci = tid < kRep       ? cnt_index(L, TT, s, tid)
                       : tid < 2 * kRep ? qcnt_index(a.nslot, L, TT, s, cb / (a.ncb / kQuarters), tid - kRep)
@@ -1248,6 +1328,8 @@ size_t persist_lds(int H, int RT) {
 bool persist_gran(int H, int RT) {
   return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd >= 2 && !(g_persist_qwait & 2);
 }
+
+int g_persist_xl = 0;  // avc_lstm_persist_xcd(): XCD-local groups in the one-layer form (PersistArgs::xl)
 
 // avc_lstm_persist_sentinel(): sentinel hand-off of split h (SN), bit 0 = two-layer form, bit 1 =
 // one-layer form
@@ -1433,8 +1515,8 @@ int persist_dispatch(avc_context* ctx, const void* fn, dim3 grid, dim3 block, vo
 
 // Launch: grid (nslot * ncb, ngrp); co-residency was checked by the eligibility test.
 int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_t s) {
-  const dim3 grid(a.nslot * a.ncb, ngrp);
-  a.nwg = (int)(grid.x * grid.y);
+  const dim3 grid = a.xl ? dim3(8 * a.ncb, 1) : dim3(a.nslot * a.ncb, ngrp);
+  a.nwg = a.xl ? a.xl_slots * a.ncb : (int)(grid.x * grid.y);
   for (int L = 0; L < a.nslot; ++L)
     AVC_CHECK_ARG(a.W[L] && a.winv[L], "persistent recurrence: a slot's split weights are missing");
   AVC_CHECK_ARG(a.in_slot == 0 || (a.in_slot == a.nslot - 1 && a.xs && a.b0 && a.gx0 && (a.din == 384 || a.din == 512)),
@@ -2072,14 +2154,18 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   const size_t cwords = ((size_t)ngrp * gstride + 63) & ~size_t(63);
   const size_t gwords = gran ? (size_t)ngrp * kGrRing * hg_step / sizeof(unsigned)
                              : (sn ? (size_t)2 * T * hsz / sizeof(unsigned) : 0);  // SN: two h sets [2][T][hsz]
+  // XL (PersistArgs::xl): the recurrent groups dealt one per XCD, the XCD table behind the rest
+  const int ncb = 4 * H / 64;
+  const bool xl = g_persist_xl && !gran && !sn && ncb == 32 && ngrp * nslot <= 8 && device_cus() == 256;
+  const size_t xwords = xl ? (size_t)8 * ncb + 8 * 32 : 0;  // the XCD table, then a tag line per group
   unsigned char* hs0 = nullptr;
   if (!gran && !sn) {
     hs0 = sc.template take<unsigned char>((size_t)T * hsz);
     if (hs0 == nullptr) return AVC_ERR_WORKSPACE;
   }
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), cwords + gwords, s, &region,
-                         sn ? cwords : ~size_t(0)));
+  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), cwords + gwords + xwords, s,
+                         &region, sn ? cwords : ~size_t(0)));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = nslot; a.cnt_gstride = gstride;
@@ -2092,6 +2178,11 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
     a.hsn = reinterpret_cast<unsigned char*>(region + kRegionHeaderWords + cwords);
     a.hsn_set = (long)T * hsz;
     a.hsn_layer = 0;
+  }
+  if (xl) {
+    a.xl = 1;
+    a.xl_slots = ngrp * nslot;
+    a.xl_tab = region + kRegionHeaderWords + cwords + gwords;
   }
   if (ip) AVC_TRY(attach_inproj(ctx, sc, *ip, T, B, 1, a, s));
   if (gran || sn) a.in_lead = 1;  // (back-pressure polls slot 0's counters, which GR / SN launches do not add to)
@@ -2358,6 +2449,26 @@ extern "C" int avc_lstm_persist_st16(int on) {
     return AVC_ERR_INVALID;
   }
   avc::g_persist_st16 = on;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_debug_xl_census(unsigned* local_nonlocal) {
+  // (test hook) copies and clears the XL census: recurrent workgroups that found their group local
+  // / not local since the last call
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(avc::g_xl_seen)) != hipSuccess) return AVC_ERR_HIP;
+  if (hipMemcpy(local_nonlocal, p, 2 * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return AVC_ERR_HIP;
+  if (hipMemset(p, 0, 2 * sizeof(unsigned)) != hipSuccess) return AVC_ERR_HIP;
+  return AVC_OK;
+}
+
+extern "C" int avc_lstm_persist_xcd(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_lstm_persist_xcd: 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_persist_xl = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

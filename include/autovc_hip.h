@@ -373,6 +373,15 @@ int avc_lstm_persist_st16(int on);
  * chunk ahead of the loads) instead of for the whole K quarter a wave reads; 0 (default) = the
  * quarter counters.  Same products in the same order: bit-identical outputs. */
 int avc_lstm_persist_chunkwait(int on);
+/* Tuning hook (round 5): 1 = the one-layer persistent form (decoder.lstm1, H = 512, at most 8
+ * recurrent + input-slot groups) deals each batch group's workgroups to one XCD and, where a run-
+ * time check confirms they share one, hands h over with plain stores that stay in that XCD's L2
+ * (the consumers' sc1 loads read it there); any other group keeps the write-through stores.  Same
+ * arithmetic (bit-identical). */
+int avc_lstm_persist_xcd(int on);
+/* Test hook: recurrent workgroups of XCD-local launches that found their group on one XCD / not,
+ * since the last call (two words, then cleared). */
+int avc_debug_xl_census(unsigned* local_nonlocal);
 /* Tuning hook (round 5): 1 (default) = long-K products (weight gradients) pick their split-K count
  * by rounds of one workgroup per CU (a grid that spills a few workgroups into an extra round pays
  * the whole round); 0 = ~4 workgroups per CU (round 4).  The sums split differently: not

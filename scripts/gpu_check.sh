@@ -98,6 +98,8 @@ for step in "$@"; do
     fix5) run fix5 600 python -u -m pytest tests/test_gpu_bnfuse.py tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_bnbwd.py tests/test_gpu_production.py tests/test_gpu_curve.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     l32diag) run l32test 200 python -u -m pytest tests/test_gpu_lstm32.py -v -x --timeout 100 --timeout-method thread -p no:cacheprovider && run l32diag 200 python scripts/lstm32_diag.py ;;
     dualw) run dualw 300 python -u -m pytest tests/test_gpu_dgsplit.py -v -x --timeout 100 --timeout-method thread -p no:cacheprovider && run dualwab 400 python scripts/train_hook_ab.py avc_dg_dual_wide 0 1 ;;
+    xl) run xl 400 python -u -m pytest tests/test_gpu_xcd_local.py -v -x -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    xlab) run xlab 400 python scripts/persist_hook_ab.py avc_lstm_persist_xcd 0 1 0 1 0 1 ;;
     abtree) run abtree 1000 bash scripts/ab_r04_tree.sh ;;
     roundsab) run roundsab 500 python scripts/train_hook_ab.py avc_gemm_plan_rounds 0 1 ;;
     cwab) run cwab 400 python scripts/persist_hook_ab.py avc_lstm_persist_chunkwait 0 1 0 1 0 1 ;;
