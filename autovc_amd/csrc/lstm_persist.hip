@@ -1329,7 +1329,7 @@ bool persist_gran(int H, int RT) {
   return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd >= 2 && !(g_persist_qwait & 2);
 }
 
-int g_persist_xl = 0;  // avc_lstm_persist_xcd(): XCD-local groups in the one-layer form (PersistArgs::xl)
+int g_persist_xl = 1;  // avc_lstm_persist_xcd() (default on): XCD-local groups in the one-layer form (PersistArgs::xl)
 
 // avc_lstm_persist_sentinel(): sentinel hand-off of split h (SN), bit 0 = two-layer form, bit 1 =
 // one-layer form
