@@ -97,6 +97,7 @@ _SIGS = {
     "avc_dg_dual_split": [_I],
     "avc_lstm32_tune": [_I],
     "avc_bptt_persist": [_I],
+    "avc_bptt_xcd": [_I],
     "avc_debug_bptt_diag": [_I],
     "avc_debug_persist_inject": [_I],
     "avc_persist_notify": [_P, _P],

@@ -231,18 +231,22 @@ __host__ __device__ __forceinline__ unsigned gr_tag(unsigned E, int t) { return 
 
 // One wave, every lane: leave a spin?  The give-up word is read every 64 passes; past the limit
 // the launch gives up (the first wave to do so reports it, as wait_ge_ctl).  spins is uniform.
-__device__ bool spin_give_up(unsigned spins, const PersistArgs& a, unsigned E, int lane) {
-  if ((spins & 63) == 63 && __hip_atomic_load((gu32*)a.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E)
+__device__ bool spin_give_up_ctl(unsigned spins, unsigned* tmo, unsigned* fail_host, unsigned spin_limit, unsigned E,
+                                 int lane) {
+  if ((spins & 63) == 63 && __hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == E)
     return true;
-  if (spins < a.spin_limit) return false;
+  if (spins < spin_limit) return false;
   if (lane == 0) {
-    const unsigned old = __hip_atomic_fetch_max((gu32*)a.tmo, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_max((gu32*)tmo, E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old != E) {
       const unsigned nf = atomicAdd(&g_persist_giveups, 1u) + 1u;
-      if (a.fail_host) __hip_atomic_store(a.fail_host, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (fail_host) __hip_atomic_store(fail_host, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   return true;
+}
+__device__ bool spin_give_up(unsigned spins, const PersistArgs& a, unsigned E, int lane) {
+  return spin_give_up_ctl(spins, a.tmo, a.fail_host, a.spin_limit, E, lane);
 }
 
 // One lane waits until *p reaches target (wrap-safe; relaxed agent-scope polls).  false = gave
@@ -1605,6 +1609,13 @@ void set_region_args(PersistArgs& a, avc_context* ctx, unsigned* region) {
 // Write-after-read safety: slab[sp] rows of tile rt are rewritten at step k+1 only after all of
 // the tile's phase-B readers of step k counted in (cntB), and a split dG block is rewritten at
 // step k+1 only after every phase-A reader of step k+1's tile counted in (cntA).
+// a rounded sum that is never contracted with the product that formed v (the column sums of dG
+// must not depend on the compiler's contraction choices in each BPTT kernel)
+__device__ __forceinline__ float add_rounded(float s, float v) {
+#pragma clang fp contract(off)
+  return s + v;
+}
+
 __device__ __forceinline__ float pow2_scale(float m) {  // max |x| -> [2^14, 2^15) (split_scale_of)
   if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
   int e;
@@ -1856,13 +1867,16 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           mx = fmaxf(mx, fabsf(d[e]));
-          if constexpr (!CS_LDS) csum[e] += d[e];
+          if constexpr (!CS_LDS) csum[e] = add_rounded(csum[e], d[e]);
         }
         if constexpr (CS_LDS) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             f32x4* p4 = reinterpret_cast<f32x4*>(csl) + tid * 4 + g;
-            *p4 += f32x4{d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]};
+            f32x4 cs4 = *p4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cs4[j] = add_rounded(cs4[j], d[4 * g + j]);
+            *p4 = cs4;
           }
         }
         dmax = fmaxf(dmax, mx);
@@ -1959,6 +1973,310 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<f32x4*>(cp + 4 * g) = f32x4{cs[4 * g], cs[4 * g + 1], cs[4 * g + 2], cs[4 * g + 3]};
     }
+    }
+    for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o));
+    if (lane == 0) atomicMax(a.amax_dg, __float_as_uint(dmax));
+  }
+  // gave up at step k: this workgroup's dG slices of the remaining steps are NaN (never plausible)
+  if (!ok && b_task) {
+    for (int kk = k; kk < T; ++kk) {
+      const int st = T - 1 - kk;
+      const int t = a.reverse ? T - 1 - st : st;
+      float* go = a.dg + ((long)t * B + b_row) * G4 + kq;
+      for (int e = 0; e < 16; ++e) go[e] = __builtin_nanf("");
+    }
+  }
+}
+
+// ---- XCD-local BPTT of an H = 512 layer (decoder.lstm1; round 5, avc_bptt_xcd) ---------------
+//
+// bptt_persist_kernel's 128-row tiles make every step two all-to-all hand-offs across the chip (the
+// split dG rows to the product owners, the partials back to the epilogue owners), each a
+// write-through drain, a counter and a poll.  At H = 512 the split W_hh^T is 4 MB: one XCD's 32
+// CUs hold all of it in LDS (128 KB each), so a group of 32 batch rows can run its whole BPTT on
+// one XCD, and the batch (rows never interact) splits into up to 8 such groups.  Workgroup bid is
+// (group g = bid % 8, K-slice q = bid / 8): under the round-robin deal each group lands on one XCD
+// (checked at run time, as PersistArgs::xl).  Workgroup q of group g
+//   phase A: (dG_{t+1} . W_hh)[32 rows, all 512 units] over K-slice q (64 permuted gate columns =
+//            4 chunks of 16) -> the fp32 partial slab[q] (8 waves x 64 units);
+//   phase B: rows x units 16q .. 16q + 15: sums the 32 partials (fixed order), gate derivatives,
+//            dc (kept in registers), dG_t out, and splits dG_t over exactly K-slice q -- the operand
+//            of its OWN next phase A, so the split goes to LDS and that hand-off disappears.
+// One hand-off per step (partials, phase A -> phase B), inside one XCD: plain stores that stay in
+// its L2, a per-group line of tags (one word per workgroup, written after the drain; polled by one
+// wave, one load for all 32), sc1 loads.  A group that is not on one XCD uses sc1 stores and an
+// agent-scope counter per (step, group) instead -- the forward kernels' protocol.  The products
+// (same chunks, same MFMA order), the per-(row, K-slice) split scales, the partial order and the
+// epilogue are bptt_persist_kernel<4, 32, 32, true>'s, so dG, the column sums and max |dG| are
+// the same bits.
+struct BpttXArgs {
+  int B, T, reverse, ngrp;
+  const _Float16* whhT_s;   // W_hh^T permuted, fragment-major split ([512] rows x [2048] k)
+  const unsigned* amax_w;
+  float* slab;              // [2][32][B][512] partials (step parity, K-slice)
+  const float* dy; long lddy;
+  const float* gates;       // [T][B][2048] saved activated gates (permuted)
+  const float* c;           // [T][B][512] saved cell states
+  float* dg;                // [T][B][2048] output dG (permuted)
+  float* colpart;           // [B/32][2048] per-group column sums of dG (bias gradients)
+  unsigned* amax_dg;        // max |dG| over all steps (float bits; zeroed before the launch)
+  unsigned* tags;           // [8 groups][32] tag lines (local groups)
+  unsigned* xl_tab;         // [256] epoch-tagged XCD of each workgroup
+  unsigned* cnt;            // [T][8] counter lines (groups that are not on one XCD)
+  unsigned* tmo;
+  unsigned long long* tickets;
+  unsigned* fail_host;
+  unsigned spin_limit;
+};
+
+constexpr int kBxNch = 4;  // 16-deep chunks per K-slice (2048 gates / 32 slices / 16)
+size_t bptt_xl_lds() { return (size_t)16 * kBxNch * 2048 + kBxNch * 2048 + 32 * 4 * 2 + 8 * 4; }
+
+__global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
+  constexpr int H = 512, G4 = 2048, nkc = G4 / 16, NCH = kBxNch, UG = 4, KS = 64, RB = 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_x[];
+  unsigned char* wl = lds_x;                                 // [16 unit tiles][NCH][hi, lo] 1 KiB blocks
+  unsigned char* dgl = lds_x + 16 * NCH * 2048;              // [NCH][hi, lo] 1 KiB: this slice's split dG
+  float* rsl = reinterpret_cast<float*>(dgl + NCH * 2048);   // [32] the rows' split scales
+  unsigned* rmax = reinterpret_cast<unsigned*>(rsl + 32);    // [32] row max |dG| (float bits)
+  int* flag = reinterpret_cast<int*>(rmax + 32);             // [8]
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int B = a.B, T = a.T;
+  const int g = blockIdx.x & 7, q = blockIdx.x >> 3;
+  if (tid == 0) {  // every workgroup takes a ticket (the epoch counts the whole grid)
+    const unsigned long long tk = __hip_atomic_fetch_add(a.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[2] = (int)(unsigned)(tk / 256ull + 1ull);
+  }
+  __syncthreads();
+  const unsigned E = (unsigned)flag[2];
+  if (g >= a.ngrp) return;
+
+  // the group's 32 workgroups record their XCD and check that they share one (bounded)
+  if (tid < 64) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (tid == 0)
+      __hip_atomic_store((gu32*)(a.xl_tab + blockIdx.x), (E << 4) | (xcc & 7u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool same = true, done = false;
+    for (unsigned spins = 0; !done; ++spins) {
+      bool all = true;
+      same = true;
+      if (lane < 32) {
+        const unsigned v = __hip_atomic_load((gu32*)(a.xl_tab + lane * 8 + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        all = (v >> 4) == (E & 0x0fffffffu);
+        same = (v & 7u) == (xcc & 7u);
+      }
+      done = __builtin_amdgcn_ballot_w64(!all) == 0ull;
+      if (!done && spin_give_up_ctl(spins, a.tmo, a.fail_host, a.spin_limit, E, lane)) break;
+      if (!done) __builtin_amdgcn_s_sleep(2);
+    }
+    const bool loc = done && __builtin_amdgcn_ballot_w64(!same) == 0ull;
+    if (tid == 0) {
+      flag[3] = loc ? 1 : 0;
+      flag[4] = done ? 1 : 0;
+    }
+  }
+  // stationary W_hh^T slice: every unit tile, chunks q * NCH .. q * NCH + NCH - 1
+  for (int blk = w; blk < 16 * NCH * 2; blk += 8) {
+    const int hl = blk & 1, c = (blk >> 1) % NCH, ut = (blk >> 1) / NCH;
+    const long src = (((long)ut * nkc + q * NCH + c) * 2 + hl) * 512;  // halves
+    const f16x8 v = *reinterpret_cast<const f16x8*>(a.whhT_s + src + lane * 8);
+    *reinterpret_cast<f16x8*>(wl + ((ut * NCH + c) * 2 + hl) * 1024 + lane * 16) = v;
+  }
+  __syncthreads();
+  const bool loc = flag[3] != 0;
+  bool ok = flag[4] != 0;
+  if (tid == 0) atomicAdd(&g_xl_seen[loc ? 0 : 1], 1u);
+  const float sw_inv = 1.f / pow2_scale(__uint_as_float(*a.amax_w));
+  const auto trs = __builtin_amdgcn_make_buffer_rsrc(a.tags + g * 32, 0, 128, 0x00020000);
+
+  // phase B task: row br of the group, 4-unit group bg of the slice (tid < 128)
+  const bool b_task = tid < RB * UG;
+  const int br = tid / UG, bg = tid % UG;
+  const int b_row = g * RB + br;
+  const int j0 = q * 16 + bg * 4;  // first hidden unit of the task
+  const int kq = q * KS + bg * 16;  // first (permuted) gate column of the task
+  float csum[16], dmax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) csum[e] = 0.f;
+  f32x4 dcv = {0.f, 0.f, 0.f, 0.f};  // the carried cell-state gradient of the task's 4 units
+
+  int k = 0;
+  for (; k < T && ok; ++k) {
+    const int st = T - 1 - k;
+    const int t = a.reverse ? T - 1 - st : st;
+    const int tp = a.reverse ? t + 1 : t - 1;
+    const int par = k & 1;
+    // ---------------- phase A: slab[q] = (dG_{t+1} . W_hh)[group rows, all units] over slice q ----
+    if (k > 0) {
+      f32x16 part[2], crs[2];
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) part[jn][e] = crs[jn][e] = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(dgl + (c * 2 + 0) * 1024 + lane * 16);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(dgl + (c * 2 + 1) * 1024 + lane * 16);
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) {
+          const unsigned char* pb = wl + (((w * 2 + jn) * NCH + c) * 2) * 1024 + lane * 16;
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(pb);
+          const f16x8 bl = *reinterpret_cast<const f16x8*>(pb + 1024);
+          part[jn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, part[jn], 0, 0, 0);
+          crs[jn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, crs[jn], 0, 0, 0);
+          crs[jn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, crs[jn], 0, 0, 0);
+        }
+      }
+      // unscale row by row: 1 / (scale of this row's split over slice q * scale of W)
+      const float rsv = lane < 32 ? rsl[lane] : 1.f;
+      const float inv = sw_inv / rsv;
+      const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.slab + ((long)par * 32 + q) * B * H + (long)g * RB * H, 0,
+                                                         RB * H * 4, 0x00020000);
+      // (the cache policy is an immediate: plain for a local group, sc1 otherwise)
+#define AVC_BX_STORE(POL)                                                                         \
+  _Pragma("unroll") for (int e = 0; e < 16; ++e) {                                                \
+    const int r = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);                                       \
+    const float ie = __shfl(inv, r);                                                              \
+    _Pragma("unroll") for (int jn = 0; jn < 2; ++jn) {                                            \
+      const int col = (w * 2 + jn) * 32 + (lane & 31);                                            \
+      const float v = (part[jn][e] + crs[jn][e] * (1.f / 2048.f)) * ie;                           \
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), srs, (r * H + col) * 4, 0, POL); \
+    }                                                                                             \
+  }
+      if (loc) {
+        AVC_BX_STORE(0)
+      } else {
+        AVC_BX_STORE(16)
+      }
+#undef AVC_BX_STORE
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        if (loc)  // this workgroup's tag for step k, after every wave's drain
+          __builtin_amdgcn_raw_buffer_store_b32(E * (unsigned)(T + 1) + (unsigned)k, trs, q * 4, 0, 0);
+        else
+          __hip_atomic_fetch_add((gu32*)(a.cnt + ((long)k * 8 + g) * 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // ---------------- phase B: dG_t for the group's rows, slice q ----------------------------------
+    const long tb = (long)t * B + b_row;
+    f32x4 dyv = {}, ig = {}, fg = {}, gg = {}, og = {}, cc = {}, cpv = {};
+    if (b_task) {
+      dyv = *reinterpret_cast<const f32x4*>(a.dy + (long)t * B * a.lddy + (long)b_row * a.lddy + j0);
+      const float* gp = a.gates + tb * G4 + kq;
+      ig = *reinterpret_cast<const f32x4*>(gp);
+      fg = *reinterpret_cast<const f32x4*>(gp + 4);
+      gg = *reinterpret_cast<const f32x4*>(gp + 8);
+      og = *reinterpret_cast<const f32x4*>(gp + 12);
+      cc = *reinterpret_cast<const f32x4*>(a.c + tb * H + j0);
+      if (st > 0) cpv = *reinterpret_cast<const f32x4*>(a.c + ((long)tp * B + b_row) * H + j0);
+    }
+    if (tid < 32) rmax[tid] = 0u;
+    if (k > 0) {
+      if (tid < 64) {  // wave 0: every phase A of the group at step k
+        bool good = true;
+        if (loc) {
+          const unsigned want = E * (unsigned)(T + 1) + (unsigned)k;
+          auto ld = [&]() { return lane < 32 ? __builtin_amdgcn_raw_buffer_load_b32(trs, lane * 4, 0, 16 /*sc1*/) : want; };
+          unsigned v = ld();
+          for (unsigned spins = 0; __builtin_amdgcn_ballot_w64((int)(v - want) < 0) != 0ull; ++spins) {
+            if (spin_give_up_ctl(spins, a.tmo, a.fail_host, a.spin_limit, E, lane)) {
+              good = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            v = ld();
+          }
+        } else if (lane == 0) {
+          good = wait_ge_ctl(a.cnt + ((long)k * 8 + g) * 32, E * 32u, a.tmo, a.fail_host, a.spin_limit, E);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
+        if (lane == 0) flag[1] = good ? 1 : 0;
+      }
+      __syncthreads();
+      if (!flag[1]) { ok = false; break; }
+    } else {
+      __syncthreads();
+    }
+    float d[16];
+    float mx = 0.f;
+    if (b_task) {
+      f32x4 rec = {0.f, 0.f, 0.f, 0.f};
+      if (k > 0) {
+        const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)par * 32 * B * H, 0, 32 * B * H * 4, 0x00020000);
+#pragma unroll
+        for (int s0 = 0; s0 < 32; s0 += 16) {
+          f32x4 pv[16];
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2)
+            pv[s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   srs, (int)((((long)(s0 + s2) * B + b_row) * H + j0) * 4), 0, 16));
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) rec += pv[s2];  // fixed slice order
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float dh = dyv[u] + rec[u];
+        const float tc = gate_tanh(cc[u]);  // as the forward epilogue formed it
+        const float dct = dh * og[u] * (1.f - tc * tc) + dcv[u];
+        dcv[u] = dct * fg[u];
+        d[u] = dct * gg[u] * ig[u] * (1.f - ig[u]);
+        d[4 + u] = dct * cpv[u] * fg[u] * (1.f - fg[u]);
+        d[8 + u] = dct * ig[u] * (1.f - gg[u] * gg[u]);
+        d[12 + u] = dh * tc * og[u] * (1.f - og[u]);
+      }
+      float* go = a.dg + tb * G4 + kq;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq)
+        *reinterpret_cast<f32x4*>(go + 4 * gq) = f32x4{d[4 * gq], d[4 * gq + 1], d[4 * gq + 2], d[4 * gq + 3]};
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        mx = fmaxf(mx, fabsf(d[e]));
+        csum[e] = add_rounded(csum[e], d[e]);
+      }
+      dmax = fmaxf(dmax, mx);
+      atomicMax(rmax + br, __float_as_uint(mx));
+    }
+    __syncthreads();
+    if (st > 0) {  // the split for this workgroup's next phase A (none after the last step)
+      if (b_task) {
+        const float sb = pow2_scale(__uint_as_float(rmax[br]));
+        // chunk bg of the slice: lanes (row) and (row + 32) hold k 0-7 and 8-15
+        f16x8 hi0, lo0, hi1, lo1;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v0 = d[e] * sb, v1 = d[8 + e] * sb;
+          const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+          hi0[e] = h0; lo0[e] = (_Float16)((v0 - (float)h0) * 2048.0f);
+          hi1[e] = h1; lo1[e] = (_Float16)((v1 - (float)h1) * 2048.0f);
+        }
+        *reinterpret_cast<f16x8*>(dgl + (bg * 2 + 0) * 1024 + br * 16) = hi0;
+        *reinterpret_cast<f16x8*>(dgl + (bg * 2 + 0) * 1024 + (br + 32) * 16) = hi1;
+        *reinterpret_cast<f16x8*>(dgl + (bg * 2 + 1) * 1024 + br * 16) = lo0;
+        *reinterpret_cast<f16x8*>(dgl + (bg * 2 + 1) * 1024 + (br + 32) * 16) = lo1;
+        if (bg == 0) rsl[br] = sb;
+      }
+      __syncthreads();
+    }
+  }
+  // the bias gradients' column sums over the group's rows (row order, through LDS: the W slice is
+  // free now) and max |dG| for the weight-gradient products' operand scale
+  if (ok) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(wl);  // [128 tasks][16]
+    if (b_task) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) red[tid * 16 + e] = csum[e];
+    }
+    __syncthreads();
+    if (tid < UG * 16) {
+      const int g4 = tid / 16, e = tid % 16;
+      float v = 0.f;
+      for (int r = 0; r < RB; ++r) v += red[(r * UG + g4) * 16 + e];
+      a.colpart[(long)g * G4 + q * KS + g4 * 16 + e] = v;
     }
     for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o));
     if (lane == 0) atomicMax(a.amax_dg, __float_as_uint(dmax));
@@ -2300,9 +2618,13 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
 int g_bptt_persist = 1;  // avc_bptt_persist(): the persistent BPTT where eligible
 int g_bptt_diag = 0;     // avc_debug_bptt_diag(): timing experiments (results invalid when set)
 
+bool bptt_xl_eligible(int B, int H);
+
 bool bptt_persist_eligible(int T, int B, int H) {
   int nrt, ntn, ns, nch;
-  if (!g_bptt_persist || T < 2 || !bptt_plan(B, H, nrt, ntn, ns, nch)) return false;
+  if (!g_bptt_persist || T < 2) return false;
+  if (bptt_xl_eligible(B, H)) return true;  // (any batch of whole 32-row groups, up to 8 of them)
+  if (!bptt_plan(B, H, nrt, ntn, ns, nch)) return false;
   struct Entry { const void* fn; int dev; int cap; };
   static std::vector<Entry> cache;
   const void* fn = bptt_fn(nch, ns);
@@ -2326,14 +2648,77 @@ bool bptt_persist_eligible(int T, int B, int H) {
 
 int bptt_colpart_rows(int B, int H) {
   int nrt, ntn, ns, nch;
+  if (bptt_xl_eligible(B, H)) return B / 32;
   return bptt_plan(B, H, nrt, ntn, ns, nch) ? B / bptt_rb(ns) : 0;
 }
 
 size_t bptt_persist_scratch(int B, int H) {
   int nrt, ntn, ns, nch;
+  if (bptt_xl_eligible(B, H)) return al((size_t)2 * 32 * B * H * sizeof(float)) + 4096;
   if (!bptt_plan(B, H, nrt, ntn, ns, nch)) return 0;
   return al((size_t)2 * ns * B * H * sizeof(float)) + al((size_t)2 * ns * B * sizeof(float)) +
          al((size_t)2 * (B / 32) * (4 * H / 16) * 2048) + al((size_t)B * H * sizeof(float)) + 4096;
+}
+
+int g_bptt_xl = 1;  // avc_bptt_xcd(): the XCD-local form for H = 512 (bptt_xl_kernel)
+
+// The XCD-local form takes an H = 512 layer whose batch splits into at most 8 groups of 32 rows,
+// on a 256-CU device that holds the grid (one 512-thread, 136 KB-LDS workgroup per CU).
+bool bptt_xl_eligible(int B, int H) {
+  if (!g_bptt_xl || H != 512 || B % 32 || B > 256 || device_cus() != 256) return false;
+  static int cap = -1;  // (one instance; the device count is checked above)
+  if (cap < 0) {
+    const void* fn = reinterpret_cast<const void*>(&bptt_xl_kernel);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bptt_xl_lds());
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 512, bptt_xl_lds()) != hipSuccess) {
+      (void)hipGetLastError();
+      per_cu = 0;
+    }
+    cap = per_cu * device_cus();
+  }
+  return cap >= 256;
+}
+
+int bptt_xl_run(avc_context* ctx, int T, int B, int reverse, const _Float16* whhT_s, const unsigned* amax_w,
+                const float* d_y, long ldy, const float* gates, const float* c, float* dg, float* colpart,
+                unsigned* amax_dg, hipStream_t s) {
+  constexpr int H = 512;
+  Scratch sc(ctx);
+  AVC_TAKE(slab, float, (size_t)2 * 32 * B * H, sc);
+  unsigned* region = nullptr;
+  // tag lines [8][32], the XCD table [256], counter lines [T][8][32]
+  const size_t words = 8 * 32 + 256 + (size_t)T * 8 * 32;
+  AVC_TRY(persist_region(ctx, 4, T, 8, 32, 256, words, s, &region));
+  BpttXArgs a{};
+  a.B = B; a.T = T; a.reverse = reverse; a.ngrp = B / 32;
+  a.whhT_s = whhT_s; a.amax_w = amax_w; a.slab = slab;
+  a.dy = d_y; a.lddy = ldy; a.gates = gates; a.c = c; a.dg = dg;
+  a.colpart = colpart; a.amax_dg = amax_dg;
+  AVC_TRY(zero_async(amax_dg, sizeof(unsigned), s));
+  a.tickets = reinterpret_cast<unsigned long long*>(region);
+  a.tmo = region + 32;
+  a.tags = region + kRegionHeaderWords;
+  a.xl_tab = a.tags + 8 * 32;
+  a.cnt = a.xl_tab + 256;
+  a.fail_host = ctx->fail_host;
+  a.spin_limit = g_spin_limit;
+  if (g_persist_inject > 0) {
+    --g_persist_inject;
+    a.spin_limit = 0;
+  }
+  void* args[] = {&a};
+  hipEvent_t ev = timing_begin(TC_LSTM_STEP_BWD, s);
+  AVC_TRY(persist_dispatch(ctx, reinterpret_cast<const void*>(&bptt_xl_kernel), dim3(256), dim3(512), args,
+                           bptt_xl_lds(), s));
+  if (ev) {
+    // the recurrent products of T - 1 steps; algorithmic bytes: the partials written and read per
+    // step (the split dG stays in LDS), the epilogue operands, dG written
+    const double flops = (double)(T - 1) * 2.0 * B * H * 4.0 * H;
+    const double bytes = (double)(T - 1) * 2.0 * 4.0 * 32 * B * H + (double)T * 4.0 * B * H * 12.0;
+    timing_end(TC_LSTM_STEP_BWD, ev, s, flops, bytes);
+  }
+  return AVC_OK;
 }
 
 // BPTT of one LSTM layer direction over all T steps as one launch (see bptt_persist_kernel).
@@ -2345,9 +2730,11 @@ int bptt_persist_run(avc_context* ctx, int T, int B, int H, int reverse, const _
                      const unsigned* amax_w, const float* d_y, long ldy, const float* gates, const float* c,
                      float* dg, float* colpart, unsigned* amax_dg, hipStream_t s) {
   int nrt, ntn, ns, nch;
-  AVC_CHECK_ARG(bptt_persist_eligible(T, B, H) && bptt_plan(B, H, nrt, ntn, ns, nch),
-                "persistent BPTT: not eligible for this shape");
+  AVC_CHECK_ARG(bptt_persist_eligible(T, B, H), "persistent BPTT: not eligible for this shape");
   AVC_TRY(persist_guard(ctx));
+  if (bptt_xl_eligible(B, H))
+    return bptt_xl_run(ctx, T, B, reverse, whhT_s, amax_w, d_y, ldy, gates, c, dg, colpart, amax_dg, s);
+  AVC_CHECK_ARG(bptt_plan(B, H, nrt, ntn, ns, nch), "persistent BPTT: not eligible for this shape");
   Scratch sc(ctx);
   AVC_TAKE(slab, float, (size_t)2 * ns * B * H, sc);
   AVC_TAKE(rowscale, float, (size_t)2 * ns * B, sc);
@@ -2530,6 +2917,16 @@ extern "C" int avc_debug_bptt_diag(int bits) {
 
 extern "C" int avc_bptt_persist(int on) {
   avc::g_bptt_persist = on ? 1 : 0;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_bptt_xcd(int on) {
+  if (on != 0 && on != 1) {
+    avc::set_error("avc_bptt_xcd: 0 or 1");
+    return AVC_ERR_INVALID;
+  }
+  avc::g_bptt_xl = on;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

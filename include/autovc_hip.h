@@ -436,6 +436,10 @@ int avc_lstm32_tune(int mode);
 /* Tuning hook: the BPTT of LSTM layers with B = 128 / 256 and H a multiple of 128 as one
  * persistent launch (1, default; lstm_persist.hip: bptt_persist_kernel) or launch per step (0). */
 int avc_bptt_persist(int on);
+/* Tuning hook (round 5): 1 (default) = the persistent BPTT of an H = 512 layer (decoder.lstm1)
+ * runs XCD-local: groups of 32 batch rows, each on one XCD's 32 CUs with all of W_hh^T in their
+ * LDS, one in-XCD hand-off per step (bptt_xl_kernel); 0 = the 128-row-tile form.  Same bits. */
+int avc_bptt_xcd(int on);
 /* Diagnostic hook (timing experiments only; results are NOT valid while set): bit 0 skips the
  * persistent BPTT's dG operand loads, bit 1 its partial loads, bit 2 its waits. */
 int avc_debug_bptt_diag(int bits);

@@ -100,6 +100,9 @@ for step in "$@"; do
     dualw) run dualw 300 python -u -m pytest tests/test_gpu_dgsplit.py -v -x --timeout 100 --timeout-method thread -p no:cacheprovider && run dualwab 400 python scripts/train_hook_ab.py avc_dg_dual_wide 0 1 ;;
     xl) run xl 400 python -u -m pytest tests/test_gpu_xcd_local.py -v -x -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     xlab) run xlab 400 python scripts/persist_hook_ab.py avc_lstm_persist_xcd 0 1 0 1 0 1 ;;
+    bxl) run bxl 400 python -u -m pytest tests/test_gpu_bptt_xl.py -v -x -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    bxlsuite) run bxlsuite 700 python -u -m pytest tests/test_gpu_bptt_coalesce.py tests/test_gpu_persist_safety.py tests/test_gpu_production.py tests/test_gpu_curve.py tests/test_gpu_dp.py tests/test_gpu_model.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    bxlab) run bxlab 500 python scripts/train_hook_ab.py avc_bptt_xcd 0 1 ;;
     abtree) run abtree 1000 bash scripts/ab_r04_tree.sh ;;
     roundsab) run roundsab 500 python scripts/train_hook_ab.py avc_gemm_plan_rounds 0 1 ;;
     cwab) run cwab 400 python scripts/persist_hook_ab.py avc_lstm_persist_chunkwait 0 1 0 1 0 1 ;;
