@@ -1616,6 +1616,29 @@ __device__ __forceinline__ float add_rounded(float s, float v) {
   return s + v;
 }
 
+// One element of the LSTM cell's backward (decoder.py's nn.LSTM under autograd): from dh (the
+// output gradient plus the recurrent product), the carried dc and the saved activated gates i, f,
+// g, o, tanh(c_t) and c_{t-1}: the next carried dc and the four gate-preactivation gradients.  Every
+// product and sum rounded as written (no contraction), so every BPTT kernel that uses it forms the
+// same bits whatever its surrounding code lets the compiler fuse.
+__device__ __forceinline__ void lstm_cell_grad(float dh, float dcv, float ig, float fg, float gg, float og, float tc,
+                                               float cpv, float& dc_next, float& di, float& df, float& dgg, float& dout) {
+#pragma clang fp contract(off)
+  const float dct = dh * og * (1.f - tc * tc) + dcv;
+  dc_next = dct * fg;
+  di = dct * gg * ig * (1.f - ig);
+  df = dct * cpv * fg * (1.f - fg);
+  dgg = dct * ig * (1.f - gg * gg);
+  dout = dh * tc * og * (1.f - og);
+}
+
+// A phase-A partial of the BPTT product: (hi.hi + (hi.lo + lo.hi) / 2048) * unscale, rounded as
+// written (the same bits in every BPTT kernel)
+__device__ __forceinline__ float bptt_unscale(float part, float crs, float ie) {
+#pragma clang fp contract(off)
+  return (part + crs * (1.f / 2048.f)) * ie;
+}
+
 __device__ __forceinline__ float pow2_scale(float m) {  // max |x| -> [2^14, 2^15) (split_scale_of)
   if (!(m > 0.f) || !(m < 3.0e38f)) return 1.f;
   int e;
@@ -1786,7 +1809,7 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
 #pragma unroll
         for (int jn = 0; jn < 2; ++jn) {
           const int col = ct * 128 + wn * 64 + jn * 32 + (lane & 31);
-          const float v = (part[jn][e] + crs[jn][e] * (1.f / 2048.f)) * ie;
+          const float v = bptt_unscale(part[jn][e], crs[jn][e], ie);
           if (!(a.diag & 8))
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), srs, ((row0 + r) * H + col) * 4, 0,
                                                   16 /*sc1*/);
@@ -1848,12 +1871,9 @@ __global__ __launch_bounds__(512, 1) void bptt_persist_kernel(BpttPArgs a) {
         for (int u = 0; u < 4; ++u) {
           const float dh = dyv[u] + rec[u];
           const float tc = gate_tanh(cc[u]);  // as the forward epilogue formed it
-          const float dct = dh * og[u] * (1.f - tc * tc) + dcv[u];
-          dcv[u] = dct * fg[u];
-          d[u] = dct * gg[u] * ig[u] * (1.f - ig[u]);
-          d[4 + u] = dct * cpv[u] * fg[u] * (1.f - fg[u]);
-          d[8 + u] = dct * ig[u] * (1.f - gg[u] * gg[u]);
-          d[12 + u] = dh * tc * og[u] * (1.f - og[u]);
+          float dn;
+          lstm_cell_grad(dh, dcv[u], ig[u], fg[u], gg[u], og[u], tc, cpv[u], dn, d[u], d[4 + u], d[8 + u], d[12 + u]);
+          dcv[u] = dn;
         }
         float* go = a.dg + tb * G4 + kq;
         if (!(a.diag & 16)) {  // (stores issued after the hand-off measured slower: 15.8 -> 16.7 us
@@ -2030,7 +2050,19 @@ struct BpttXArgs {
 };
 
 constexpr int kBxNch = 4;  // 16-deep chunks per K-slice (2048 gates / 32 slices / 16)
-size_t bptt_xl_lds() { return (size_t)16 * kBxNch * 2048 + kBxNch * 2048 + 32 * 4 * 2 + 8 * 4; }
+#ifdef AVC_STAMPS
+#define AVC_BXSTAMP(slot)                                                                         \
+  do {                                                                                            \
+    unsigned long long _t;                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (g_pstamps && tid == 0) g_pstamps[((long)blockIdx.x * T + k) * 8 + (slot)] = _t;           \
+  } while (0)
+#else
+#define AVC_BXSTAMP(slot) do { } while (0)
+#endif
+size_t bptt_xl_lds() { return (size_t)16 * kBxNch * 2048 + kBxNch * 2048 + 32 * 4 + 8 * 4; }
 
 __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
   constexpr int H = 512, G4 = 2048, nkc = G4 / 16, NCH = kBxNch, UG = 4, KS = 64, RB = 32;
@@ -2038,8 +2070,7 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
   unsigned char* wl = lds_x;                                 // [16 unit tiles][NCH][hi, lo] 1 KiB blocks
   unsigned char* dgl = lds_x + 16 * NCH * 2048;              // [NCH][hi, lo] 1 KiB: this slice's split dG
   float* rsl = reinterpret_cast<float*>(dgl + NCH * 2048);   // [32] the rows' split scales
-  unsigned* rmax = reinterpret_cast<unsigned*>(rsl + 32);    // [32] row max |dG| (float bits)
-  int* flag = reinterpret_cast<int*>(rmax + 32);             // [8]
+  int* flag = reinterpret_cast<int*>(rsl + 32);              // [8]
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int B = a.B, T = a.T;
@@ -2091,16 +2122,14 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
   const float sw_inv = 1.f / pow2_scale(__uint_as_float(*a.amax_w));
   const auto trs = __builtin_amdgcn_make_buffer_rsrc(a.tags + g * 32, 0, 128, 0x00020000);
 
-  // phase B task: row br of the group, 4-unit group bg of the slice (tid < 128)
-  const bool b_task = tid < RB * UG;
-  const int br = tid / UG, bg = tid % UG;
+  // phase B task: row br of the group, hidden unit uu of the slice (every thread: 32 x 16); the
+  // unit's four gate columns i, f, g, o sit at bg * 16 + {u, 4 + u, 8 + u, 12 + u} of the slice
+  const int br = tid >> 4, uu = tid & 15, bg = uu >> 2, u = uu & 3;
   const int b_row = g * RB + br;
-  const int j0 = q * 16 + bg * 4;  // first hidden unit of the task
-  const int kq = q * KS + bg * 16;  // first (permuted) gate column of the task
-  float csum[16], dmax = 0.f;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) csum[e] = 0.f;
-  f32x4 dcv = {0.f, 0.f, 0.f, 0.f};  // the carried cell-state gradient of the task's 4 units
+  const int j = q * 16 + uu;        // the task's hidden unit
+  const int kq = q * KS + bg * 16;  // the task's 16-column chunk of (permuted) gate columns
+  float csum[4] = {0.f, 0.f, 0.f, 0.f}, dmax = 0.f;
+  float dcv = 0.f;  // the carried cell-state gradient of the task's unit
 
   int k = 0;
   for (; k < T && ok; ++k) {
@@ -2108,6 +2137,7 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
     const int t = a.reverse ? T - 1 - st : st;
     const int tp = a.reverse ? t + 1 : t - 1;
     const int par = k & 1;
+    AVC_BXSTAMP(0);
     // ---------------- phase A: slab[q] = (dG_{t+1} . W_hh)[group rows, all units] over slice q ----
     if (k > 0) {
       f32x16 part[2], crs[2];
@@ -2129,6 +2159,7 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
           crs[jn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, crs[jn], 0, 0, 0);
         }
       }
+      AVC_BXSTAMP(1);
       // unscale row by row: 1 / (scale of this row's split over slice q * scale of W)
       const float rsv = lane < 32 ? rsl[lane] : 1.f;
       const float inv = sw_inv / rsv;
@@ -2141,7 +2172,7 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
     const float ie = __shfl(inv, r);                                                              \
     _Pragma("unroll") for (int jn = 0; jn < 2; ++jn) {                                            \
       const int col = (w * 2 + jn) * 32 + (lane & 31);                                            \
-      const float v = (part[jn][e] + crs[jn][e] * (1.f / 2048.f)) * ie;                           \
+      const float v = bptt_unscale(part[jn][e], crs[jn][e], ie);                                  \
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), srs, (r * H + col) * 4, 0, POL); \
     }                                                                                             \
   }
@@ -2153,6 +2184,7 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
 #undef AVC_BX_STORE
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      AVC_BXSTAMP(2);
       if (tid == 0) {
         if (loc)  // this workgroup's tag for step k, after every wave's drain
           __builtin_amdgcn_raw_buffer_store_b32(E * (unsigned)(T + 1) + (unsigned)k, trs, q * 4, 0, 0);
@@ -2161,19 +2193,13 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
       }
     }
     // ---------------- phase B: dG_t for the group's rows, slice q ----------------------------------
+    // (one element per thread: each sums its 32 partials in slice order with one round of loads)
     const long tb = (long)t * B + b_row;
-    f32x4 dyv = {}, ig = {}, fg = {}, gg = {}, og = {}, cc = {}, cpv = {};
-    if (b_task) {
-      dyv = *reinterpret_cast<const f32x4*>(a.dy + (long)t * B * a.lddy + (long)b_row * a.lddy + j0);
-      const float* gp = a.gates + tb * G4 + kq;
-      ig = *reinterpret_cast<const f32x4*>(gp);
-      fg = *reinterpret_cast<const f32x4*>(gp + 4);
-      gg = *reinterpret_cast<const f32x4*>(gp + 8);
-      og = *reinterpret_cast<const f32x4*>(gp + 12);
-      cc = *reinterpret_cast<const f32x4*>(a.c + tb * H + j0);
-      if (st > 0) cpv = *reinterpret_cast<const f32x4*>(a.c + ((long)tp * B + b_row) * H + j0);
-    }
-    if (tid < 32) rmax[tid] = 0u;
+    const float* gp = a.gates + tb * G4 + kq + u;
+    const float dyv = a.dy[(long)t * B * a.lddy + (long)b_row * a.lddy + j];
+    const float ig = gp[0], fg = gp[4], gg = gp[8], og = gp[12];
+    const float cc = a.c[tb * H + j];
+    const float cpv = st > 0 ? a.c[((long)tp * B + b_row) * H + j] : 0.f;
     if (k > 0) {
       if (tid < 64) {  // wave 0: every phase A of the group at step k
         bool good = true;
@@ -2200,94 +2226,81 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
     } else {
       __syncthreads();
     }
-    float d[16];
-    float mx = 0.f;
-    if (b_task) {
-      f32x4 rec = {0.f, 0.f, 0.f, 0.f};
-      if (k > 0) {
-        const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)par * 32 * B * H, 0, 32 * B * H * 4, 0x00020000);
+    AVC_BXSTAMP(3);
+    float rec = 0.f;
+    if (k > 0) {
+      const auto srs = __builtin_amdgcn_make_buffer_rsrc(a.slab + (long)par * 32 * B * H, 0, 32 * B * H * 4, 0x00020000);
+      float pv[32];
 #pragma unroll
-        for (int s0 = 0; s0 < 32; s0 += 16) {
-          f32x4 pv[16];
+      for (int s2 = 0; s2 < 32; ++s2)
+        pv[s2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                               srs, (int)((((long)s2 * B + b_row) * H + j) * 4), 0, 16 /*sc1*/));
 #pragma unroll
-          for (int s2 = 0; s2 < 16; ++s2)
-            pv[s2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   srs, (int)((((long)(s0 + s2) * B + b_row) * H + j0) * 4), 0, 16));
-#pragma unroll
-          for (int s2 = 0; s2 < 16; ++s2) rec += pv[s2];  // fixed slice order
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float dh = dyv[u] + rec[u];
-        const float tc = gate_tanh(cc[u]);  // as the forward epilogue formed it
-        const float dct = dh * og[u] * (1.f - tc * tc) + dcv[u];
-        dcv[u] = dct * fg[u];
-        d[u] = dct * gg[u] * ig[u] * (1.f - ig[u]);
-        d[4 + u] = dct * cpv[u] * fg[u] * (1.f - fg[u]);
-        d[8 + u] = dct * ig[u] * (1.f - gg[u] * gg[u]);
-        d[12 + u] = dh * tc * og[u] * (1.f - og[u]);
-      }
-      float* go = a.dg + tb * G4 + kq;
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq)
-        *reinterpret_cast<f32x4*>(go + 4 * gq) = f32x4{d[4 * gq], d[4 * gq + 1], d[4 * gq + 2], d[4 * gq + 3]};
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        mx = fmaxf(mx, fabsf(d[e]));
-        csum[e] = add_rounded(csum[e], d[e]);
-      }
-      dmax = fmaxf(dmax, mx);
-      atomicMax(rmax + br, __float_as_uint(mx));
+      for (int s2 = 0; s2 < 32; ++s2) rec += pv[s2];  // fixed slice order
     }
-    __syncthreads();
-    if (st > 0) {  // the split for this workgroup's next phase A (none after the last step)
-      if (b_task) {
-        const float sb = pow2_scale(__uint_as_float(rmax[br]));
-        // chunk bg of the slice: lanes (row) and (row + 32) hold k 0-7 and 8-15
-        f16x8 hi0, lo0, hi1, lo1;
+    AVC_BXSTAMP(4);
+    const float dh = dyv + rec;
+    const float tc = gate_tanh(cc);  // as the forward epilogue formed it
+    float d[4], dn;
+    lstm_cell_grad(dh, dcv, ig, fg, gg, og, tc, cpv, dn, d[0], d[1], d[2], d[3]);
+    dcv = dn;
+    float* go = a.dg + tb * G4 + kq + u;
+    float mx = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v0 = d[e] * sb, v1 = d[8 + e] * sb;
-          const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
-          hi0[e] = h0; lo0[e] = (_Float16)((v0 - (float)h0) * 2048.0f);
-          hi1[e] = h1; lo1[e] = (_Float16)((v1 - (float)h1) * 2048.0f);
-        }
-        *reinterpret_cast<f16x8*>(dgl + (bg * 2 + 0) * 1024 + br * 16) = hi0;
-        *reinterpret_cast<f16x8*>(dgl + (bg * 2 + 0) * 1024 + (br + 32) * 16) = hi1;
-        *reinterpret_cast<f16x8*>(dgl + (bg * 2 + 1) * 1024 + br * 16) = lo0;
-        *reinterpret_cast<f16x8*>(dgl + (bg * 2 + 1) * 1024 + (br + 32) * 16) = lo1;
-        if (bg == 0) rsl[br] = sb;
+    for (int gi = 0; gi < 4; ++gi) {
+      go[4 * gi] = d[gi];
+      mx = fmaxf(mx, fabsf(d[gi]));
+      csum[gi] = add_rounded(csum[gi], d[gi]);
+    }
+    dmax = fmaxf(dmax, mx);
+    AVC_BXSTAMP(5);
+    // the row's max over its 16 units: the 16 lanes of this row in this wave (float bits compare
+    // as the magnitudes do)
+    unsigned mxu = __float_as_uint(mx);
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) mxu = max(mxu, (unsigned)__shfl_xor((int)mxu, o));
+    AVC_BXSTAMP(6);
+    if (st > 0) {  // the split for this workgroup's next phase A (none after the last step)
+      const float sb = pow2_scale(__uint_as_float(mxu));
+      // chunk bg of the slice: lane (row) holds k 0-7 (i, f of the chunk's 4 units), lane (row + 32)
+      // k 8-15 (g, o): this unit's i / f at elements u / 4 + u of the first, g / o of the second
+#pragma unroll
+      for (int gi = 0; gi < 4; ++gi) {
+        const float v = d[gi] * sb;
+        const _Float16 hv = (_Float16)v;
+        const _Float16 lv = (_Float16)((v - (float)hv) * 2048.0f);
+        const int off = (br + 32 * (gi >> 1)) * 16 + ((gi & 1) * 4 + u) * 2;
+        *reinterpret_cast<_Float16*>(dgl + (bg * 2 + 0) * 1024 + off) = hv;
+        *reinterpret_cast<_Float16*>(dgl + (bg * 2 + 1) * 1024 + off) = lv;
       }
+      if (uu == 0) rsl[br] = sb;
       __syncthreads();
     }
+    AVC_BXSTAMP(7);
   }
   // the bias gradients' column sums over the group's rows (row order, through LDS: the W slice is
   // free now) and max |dG| for the weight-gradient products' operand scale
   if (ok) {
     __syncthreads();
-    float* red = reinterpret_cast<float*>(wl);  // [128 tasks][16]
-    if (b_task) {
+    float* red = reinterpret_cast<float*>(wl);  // [32 rows][64 columns of the slice]
 #pragma unroll
-      for (int e = 0; e < 16; ++e) red[tid * 16 + e] = csum[e];
-    }
+    for (int gi = 0; gi < 4; ++gi) red[br * KS + bg * 16 + gi * 4 + u] = csum[gi];
     __syncthreads();
-    if (tid < UG * 16) {
-      const int g4 = tid / 16, e = tid % 16;
+    if (tid < KS) {
       float v = 0.f;
-      for (int r = 0; r < RB; ++r) v += red[(r * UG + g4) * 16 + e];
-      a.colpart[(long)g * G4 + q * KS + g4 * 16 + e] = v;
+      for (int r = 0; r < RB; ++r) v += red[r * KS + tid];
+      a.colpart[(long)g * G4 + q * KS + tid] = v;
     }
     for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o));
     if (lane == 0) atomicMax(a.amax_dg, __float_as_uint(dmax));
   }
-  // gave up at step k: this workgroup's dG slices of the remaining steps are NaN (never plausible)
-  if (!ok && b_task) {
+  // gave up at step k: this workgroup's dG columns of the remaining steps are NaN (never plausible)
+  if (!ok) {
     for (int kk = k; kk < T; ++kk) {
       const int st = T - 1 - kk;
       const int t = a.reverse ? T - 1 - st : st;
-      float* go = a.dg + ((long)t * B + b_row) * G4 + kq;
-      for (int e = 0; e < 16; ++e) go[e] = __builtin_nanf("");
+      float* go = a.dg + ((long)t * B + b_row) * G4 + kq + u;
+      for (int gi = 0; gi < 4; ++gi) go[4 * gi] = __builtin_nanf("");
     }
   }
 }

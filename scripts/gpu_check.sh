@@ -102,6 +102,8 @@ for step in "$@"; do
     xlab) run xlab 400 python scripts/persist_hook_ab.py avc_lstm_persist_xcd 0 1 0 1 0 1 ;;
     bxl) run bxl 400 python -u -m pytest tests/test_gpu_bptt_xl.py -v -x -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     bxlsuite) run bxlsuite 700 python -u -m pytest tests/test_gpu_bptt_coalesce.py tests/test_gpu_persist_safety.py tests/test_gpu_production.py tests/test_gpu_curve.py tests/test_gpu_dp.py tests/test_gpu_model.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    bxstamps) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run bxstamps 200 python scripts/stamps_bptt_xl.py ;;
+    bxtime) run bxtime 300 python scripts/bptt_xl_ab.py 0 1 ;;
     bxlab) run bxlab 500 python scripts/train_hook_ab.py avc_bptt_xcd 0 1 ;;
     abtree) run abtree 1000 bash scripts/ab_r04_tree.sh ;;
     roundsab) run roundsab 500 python scripts/train_hook_ab.py avc_gemm_plan_rounds 0 1 ;;
