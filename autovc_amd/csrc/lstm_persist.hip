@@ -2632,11 +2632,14 @@ int g_bptt_persist = 1;  // avc_bptt_persist(): the persistent BPTT where eligib
 int g_bptt_diag = 0;     // avc_debug_bptt_diag(): timing experiments (results invalid when set)
 
 bool bptt_xl_eligible(int B, int H);
+int g_bptt_xl = 1;  // avc_bptt_xcd(): the XCD-local form for H = 512 (bptt_xl_kernel); 2 = also other batches
 
 bool bptt_persist_eligible(int T, int B, int H) {
   int nrt, ntn, ns, nch;
   if (!g_bptt_persist || T < 2) return false;
-  if (bptt_xl_eligible(B, H)) return true;  // (any batch of whole 32-row groups, up to 8 of them)
+  // (avc_bptt_xcd(2): any batch of whole 32-row groups, up to 8 of them; by default only the
+  // batches the 128-row form takes, whose results it reproduces bit for bit)
+  if (g_bptt_xl == 2 && bptt_xl_eligible(B, H)) return true;
   if (!bptt_plan(B, H, nrt, ntn, ns, nch)) return false;
   struct Entry { const void* fn; int dev; int cap; };
   static std::vector<Entry> cache;
@@ -2673,7 +2676,6 @@ size_t bptt_persist_scratch(int B, int H) {
          al((size_t)2 * (B / 32) * (4 * H / 16) * 2048) + al((size_t)B * H * sizeof(float)) + 4096;
 }
 
-int g_bptt_xl = 1;  // avc_bptt_xcd(): the XCD-local form for H = 512 (bptt_xl_kernel)
 
 // The XCD-local form takes an H = 512 layer whose batch splits into at most 8 groups of 32 rows,
 // on a 256-CU device that holds the grid (one 512-thread, 136 KB-LDS workgroup per CU).
@@ -2935,8 +2937,8 @@ extern "C" int avc_bptt_persist(int on) {
 }
 
 extern "C" int avc_bptt_xcd(int on) {
-  if (on != 0 && on != 1) {
-    avc::set_error("avc_bptt_xcd: 0 or 1");
+  if (on < 0 || on > 2) {
+    avc::set_error("avc_bptt_xcd: 0, 1 or 2");
     return AVC_ERR_INVALID;
   }
   avc::g_bptt_xl = on;

@@ -438,7 +438,10 @@ int avc_lstm32_tune(int mode);
 int avc_bptt_persist(int on);
 /* Tuning hook (round 5): 1 (default) = the persistent BPTT of an H = 512 layer (decoder.lstm1)
  * runs XCD-local: groups of 32 batch rows, each on one XCD's 32 CUs with all of W_hh^T in their
- * LDS, one in-XCD hand-off per step (bptt_xl_kernel); 0 = the 128-row-tile form.  Same bits. */
+ * LDS, one in-XCD hand-off per step (bptt_xl_kernel), for the batches the 128-row-tile form takes
+ * (B = 256; same bits); 2 = also every other batch of whole 32-row groups up to 256, which
+ * otherwise run the launch-per-step BPTT (within 2e-5 of it, not the same bits); 0 = the
+ * 128-row-tile form. */
 int avc_bptt_xcd(int on);
 /* Diagnostic hook (timing experiments only; results are NOT valid while set): bit 0 skips the
  * persistent BPTT's dG operand loads, bit 1 its partial loads, bit 2 its waits. */

@@ -104,6 +104,7 @@ for step in "$@"; do
     bxlsuite) run bxlsuite 700 python -u -m pytest tests/test_gpu_bptt_coalesce.py tests/test_gpu_persist_safety.py tests/test_gpu_production.py tests/test_gpu_curve.py tests/test_gpu_dp.py tests/test_gpu_model.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     bxstamps) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run bxstamps 200 python scripts/stamps_bptt_xl.py ;;
     bxtime) run bxtime 300 python scripts/bptt_xl_ab.py 0 1 ;;
+    stampsxl) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stampsxl2 200 python scripts/stamps_lstm1.py && AVC_STAMPS_BT=32,1024 run stampsxl5 300 python scripts/stamps_lstm1.py ;;
     bxlab) run bxlab 500 python scripts/train_hook_ab.py avc_bptt_xcd 0 1 ;;
     abtree) run abtree 1000 bash scripts/ab_r04_tree.sh ;;
     roundsab) run roundsab 500 python scripts/train_hook_ab.py avc_gemm_plan_rounds 0 1 ;;

@@ -17,7 +17,7 @@ from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_d
 
 # AVC_STAMPS_BT="32,1024" for C5's shape (default C2: 64, 128)
 B, T = (int(v) for v in os.environ.get("AVC_STAMPS_BT", "64,128").split(","))
-NCB = 32
+NWG = 256  # (the XCD-local grid is linear: 8 x ncb workgroups, bid = residue + 8 x column block)
 lib = _lib.load()
 _lib.call("avc_lstm_persist_layers", 1)
 lib.avc_debug_stamps_persist.argtypes = [ctypes.c_void_p]
@@ -30,7 +30,7 @@ c = torch.from_numpy(synthetic_embedding(101, B)).to(dev)
 with torch.no_grad():
     ae(x, c, c)
 torch.cuda.synchronize()
-buf = torch.zeros(NCB * T * 8, dtype=torch.int64, device=dev)
+buf = torch.zeros(NWG * T * 8, dtype=torch.int64, device=dev)
 names = ["poll wait", "acquire+barrier (GR: granule wait)", "mfma loop", "lds reduce", "epilogue+drain"]
 
 
@@ -41,7 +41,8 @@ def measure(label):
         ae(x, c, c)
     torch.cuda.synchronize()
     lib.avc_debug_stamps_persist(ctypes.c_void_p(0))
-    st = buf.view(NCB, T, 8).cpu().numpy().astype(np.int64)
+    st = buf.view(NWG, T, 8).cpu().numpy().astype(np.int64)
+    st = st[(st[:, 4:T - 4, :6] != 0).all(axis=(1, 2))]  # the recurrent workgroups (every stamp written)
     s = st[:, 4:T - 4, :]
     ph = [np.median(s[:, :, i + 1] - s[:, :, i]) for i in range(5)]
     step = np.median(np.diff(st[:, 4:T - 4, 5], axis=1))

@@ -66,14 +66,15 @@ def test_xcd_local_bptt_is_bit_identical(cuda_device, B, T, din):
 
 @pytest.mark.parametrize("B,T", [(32, 64), (64, 48), (128, 40), (96, 5)])
 def test_xcd_local_bptt_other_batches(cuda_device, B, T):
-    """Batches the 128-row form does not take (they ran the launch-per-step BPTT before): the XCD-
-    local form against that path (fp32 MFMA products) within the products' rounding."""
+    """Batches the 128-row form does not take (avc_bptt_xcd(2); by default they keep the launch-per-
+    step BPTT): the XCD-local form against that path (fp32 MFMA products) within the products'
+    rounding."""
     H, din = 512, 320
     _lib.call("avc_debug_xl_census", (ctypes.c_uint * 2)())  # (clear)
-    new, n1 = _bwd(cuda_device, B, T, din, H, 1, seed=B + T)
+    new, n1 = _bwd(cuda_device, B, T, din, H, 2, seed=B + T)
     seen = (ctypes.c_uint * 2)()
     _lib.call("avc_debug_xl_census", seen)
-    old, n0 = _bwd(cuda_device, B, T, din, H, 0, seed=B + T)
+    old, n0 = _bwd(cuda_device, B, T, din, H, 1, seed=B + T)  # (the default: the step kernels)
     assert n1 == n0 + 1  # the XCD-local BPTT is the one extra persistent launch
     print(f"B={B} T={T}: BPTT workgroups on a local group {seen[0]}, not local {seen[1]}")
     for name, a, b in zip(["dx", "dW_ih", "dW_hh", "db_ih", "db_hh"], new, old):
