@@ -25,7 +25,7 @@ CLASSES = {
     # lstm2 (H = 1024) instantiates NCH = 8, decoder lstm1 (H = 512) NCH = 4
     "lstm2_persist": lambda n: "lstm_persist_kernel<8," in n,
     "lstm1_persist": lambda n: "lstm_persist_kernel<4," in n,
-    "bptt_persist": lambda n: "bptt_persist_kernel<" in n,
+    "bptt_persist": lambda n: "bptt_persist_kernel<" in n or "bptt_xl_kernel" in n,
 }
 
 
