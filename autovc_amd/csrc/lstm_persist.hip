@@ -482,13 +482,16 @@ __device__ __forceinline__ unsigned sn_word(unsigned v) {
 // Counters remain for the gx hand-offs and the back-pressure (slot 0 publishes none).
 // CW = 1: per-chunk waits (round 5, see ccnt_index): each wave waits for its chunks 0 and 1 at the
 // step start and polls chunk c + 2's counter one chunk ahead of its loads (two-layer form, QW).
-template <int NCH, int RT, int HO, int PD, int QW, int GR = 0, int NH = 1, int SN = 0, int CW = 0>
+template <int NCH, int RT, int HO, int PD, int QW, int GR = 0, int NH = 1, int SN = 0, int CW = 0, int XL = 0>
 __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   static_assert(!CW || (QW && !GR && !SN && NH == 1 && PD == 2 && RT >= 2 && NCH >= 3),
                 "chunk waits: two-layer quarter-wait form, PD 2, RT >= 2");
   static_assert(!GR || (NCH == 4 && RT == 1 && HO == 1 && !QW), "granule hand-off: one-layer form, H = 512, RT = 1");
   static_assert(NH == 1 || (NH == 2 && QW && !GR && HO == 1), "batch halves: two-layer quarter-wait form");
   static_assert(!SN || (HO == 1 && !GR && NH == 1), "sentinel hand-off: sc1 loads, counter-free h, one half");
+  static_assert(!XL || (NCH == 4 && HO == 1 && PD == 2 && !QW && !GR && NH == 1 && !SN && !CW),
+                "XCD-local groups: the one-layer form's default hand-off (its own instances, so the other forms "
+                "compile without the XL code)");
   constexpr int NW = 4, NC = 4;
   constexpr int MB = 16 * RT;        // batch rows computed per half (B <= MB * NH)
   constexpr int TW = 16 * NC;        // 64 gate rows
@@ -514,7 +517,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   int L, cb, grp;
   // batch group: rows [grp * MB, grp * MB + MB).  LSTM batch rows never interact, so in the
   // one-layer form every group is an independent recurrence with counters of its own.
-  if (a.xl) {  // (see PersistArgs::xl)
+  if (XL && a.xl) {  // (see PersistArgs::xl)
     const int xs = blockIdx.x & 7;
     if (xs >= a.xl_slots) return;  // an unused residue: no ticket, no counter
     L = a.nslot == 2 ? (xs & 1) : 0;
@@ -543,7 +546,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   // XL: this group's recurrent workgroups record their XCD, then each checks that all of them share
   // one (every member reads the same ncb words: the same decision).  Bounded like every wait.
   bool xl_local = false;
-  if (a.xl && L == 0) {
+  if (XL && a.xl && L == 0) {
     if (tid < 64) {
       unsigned xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -624,7 +627,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   float* g_save = L == 0 ? a.g0 : a.g1;
   float* y_out = L == 0 ? a.y0 : a.y1;
   auto gx1_slab = [&](int tt, int c) -> long { return ((long)(tt % kGxRing) * a.ncb + c) * (64 * TW); };
-  const int rep = (a.xl ? blockIdx.x >> 3 : blockIdx.x) & (kRep - 1);
+  const int rep = (XL && a.xl ? blockIdx.x >> 3 : blockIdx.x) & (kRep - 1);
   // outputs nobody reads inside this launch: h, and for training c and the activated gates
   _Float16* const yfrag = L == a.yf_slot ? a.yfrag : nullptr;
   // frag: also this thread's units of y_frag (the give-up NaN fill; normally yfrag_rows writes it)
@@ -1333,7 +1336,9 @@ bool persist_gran(int H, int RT) {
   return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd >= 2 && !(g_persist_qwait & 2);
 }
 
-int g_persist_xl = 1;  // avc_lstm_persist_xcd() (default on): XCD-local groups in the one-layer form (PersistArgs::xl)
+// avc_lstm_persist_xcd(): XCD-local groups in the one-layer form (PersistArgs::xl), off by default:
+// against the build without them (same box) lstm1 was 1 % faster at C2 and 3 % slower at C5
+int g_persist_xl = 0;
 
 // avc_lstm_persist_sentinel(): sentinel hand-off of split h (SN), bit 0 = two-layer form, bit 1 =
 // one-layer form
@@ -1368,9 +1373,13 @@ bool persist_cw(int RT, bool two_layer) {
 }
 
 // The template instance a launch of (H, RT) runs under the current tuning.
-const void* persist_fn(int H, int RT, bool two_layer = true) {
+const void* persist_fn(int H, int RT, bool two_layer = true, bool xl = false) {
   const bool qw = (g_persist_qwait & (two_layer ? 1 : 2)) != 0;
   const int nch = H / 32 / 4;
+  if (xl)  // (persist_xl_ok: the one-layer form's default hand-off at H = 512)
+    return RT == 1 ? (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 0, 1, 0, 0, 1>
+         : RT == 2 ? (const void*)lstm_persist_kernel<4, 2, 1, 2, 0, 0, 1, 0, 0, 1>
+                   : (const void*)lstm_persist_kernel<4, 4, 1, 2, 0, 0, 1, 0, 0, 1>;
   if (persist_cw(RT, two_layer)) {
     if (nch == 8)
       return RT == 2 ? (const void*)lstm_persist_kernel<8, 2, 1, 2, 1, 0, 1, 0, 1>
@@ -1414,10 +1423,10 @@ const void* persist_fn(int H, int RT, bool two_layer = true) {
 
 // Workgroups of instance (H, RT) the device can hold at once: the occupancy API's resident
 // workgroups per CU (LDS, VGPRs, waves) x CUs.  Cached per instance.
-int persist_capacity(int H, int RT, bool two_layer = true) {
+int persist_capacity(int H, int RT, bool two_layer = true, bool xl = false) {
   struct Entry { const void* fn; int dev; int cap; };
   static std::vector<Entry> cache;
-  const void* fn = persist_fn(H, RT, two_layer);
+  const void* fn = persist_fn(H, RT, two_layer, xl);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   for (const auto& e : cache)
@@ -1531,7 +1540,7 @@ int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_
     a.spin_limit = 0;
   }
   a.st16 = g_persist_st16;
-  const void* fn = persist_fn(a.H, RT, a.nslot >= 3);
+  const void* fn = persist_fn(a.H, RT, a.nslot >= 3, a.xl != 0);
   void* args[] = {&a};
   return persist_dispatch(ctx, fn, grid, dim3(256), args, persist_lds(a.H, RT), s);
 }
@@ -2487,7 +2496,9 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
                              : (sn ? (size_t)2 * T * hsz / sizeof(unsigned) : 0);  // SN: two h sets [2][T][hsz]
   // XL (PersistArgs::xl): the recurrent groups dealt one per XCD, the XCD table behind the rest
   const int ncb = 4 * H / 64;
-  const bool xl = g_persist_xl && !gran && !sn && ncb == 32 && ngrp * nslot <= 8 && device_cus() == 256;
+  const bool xl = g_persist_xl && !gran && !sn && ncb == 32 && ngrp * nslot <= 8 && device_cus() == 256 &&
+                  g_persist_mode == 2 && g_persist_pd == 2 && !(g_persist_qwait & 2) &&
+                  persist_capacity(H, RT, false, true) >= 8 * ncb;  // (the linear grid: 8 x ncb resident)
   const size_t xwords = xl ? (size_t)8 * ncb + 8 * 32 : 0;  // the XCD table, then a tag line per group
   unsigned char* hs0 = nullptr;
   if (!gran && !sn) {

@@ -373,12 +373,12 @@ int avc_lstm_persist_st16(int on);
  * chunk ahead of the loads) instead of for the whole K quarter a wave reads; 0 (default) = the
  * quarter counters.  Same products in the same order: bit-identical outputs. */
 int avc_lstm_persist_chunkwait(int on);
-/* Tuning hook (round 5): 1 (default) = the one-layer persistent form (decoder.lstm1, H = 512, at
- * most 8 recurrent + input-slot groups) deals each batch group's workgroups to one XCD and, where a
+/* Tuning hook (round 5): 1 = the one-layer persistent form (decoder.lstm1, H = 512, at most 8
+ * recurrent + input-slot groups) deals each batch group's workgroups to one XCD and, where a
  * run-time check confirms they share one, hands h over with plain stores that stay in that XCD's L2
  * and signals each step through a line of per-workgroup tags there (the consumers' sc1 loads read
  * both); any other group keeps the write-through stores and counters.  Same arithmetic
- * (bit-identical); 0 = the round-4 grid. */
+ * (bit-identical); 0 (default: measured no faster) = the round-4 grid. */
 int avc_lstm_persist_xcd(int on);
 /* Test hook: recurrent workgroups of XCD-local launches that found their group on one XCD / not,
  * since the last call (two words, then cleared). */

@@ -105,6 +105,9 @@ for step in "$@"; do
     bxstamps) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run bxstamps 200 python scripts/stamps_bptt_xl.py ;;
     bxtime) run bxtime 300 python scripts/bptt_xl_ab.py 0 1 ;;
     stampsxl) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stampsxl2 200 python scripts/stamps_lstm1.py && AVC_STAMPS_BT=32,1024 run stampsxl5 300 python scripts/stamps_lstm1.py ;;
+    longxl) run longxl 400 python scripts/long_hook_ab.py avc_lstm_persist_xcd 0 1 ;;
+    abpre) rm -f gpurun_out/abpre_*.log && run abpre 900 bash scripts/ab_prexl.sh ;;
+    xltrain) run xltrain 500 python scripts/train_hook_ab.py avc_lstm_persist_xcd 0 1 ;;
     bxlab) run bxlab 500 python scripts/train_hook_ab.py avc_bptt_xcd 0 1 ;;
     abtree) run abtree 1000 bash scripts/ab_r04_tree.sh ;;
     roundsab) run roundsab 500 python scripts/train_hook_ab.py avc_gemm_plan_rounds 0 1 ;;

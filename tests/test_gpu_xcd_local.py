@@ -52,7 +52,7 @@ def test_xcd_local_forward_is_bit_identical(cuda_device, B, T, training):
         _lib.call("avc_lstm_persist_xcd", 1)
         got = _forwards(ae, x, co, ct, 6)
     finally:
-        _lib.call("avc_lstm_persist_xcd", 1)  # (the default)
+        _lib.call("avc_lstm_persist_xcd", 0)  # (the default)
     for run in got:
         for name, a, b in zip(("mel", "mel_post", "codes"), run, ref[0]):
             assert torch.equal(a, b), f"{name}: max|d| {(a - b).abs().max().item():.3e}"
@@ -76,7 +76,7 @@ def test_xcd_local_training_step_is_bit_identical(cuda_device):
                 loss, norm = ae.train_step(X, c)
             torch.cuda.synchronize()
         finally:
-            _lib.call("avc_lstm_persist_xcd", 1)  # (the default)
+            _lib.call("avc_lstm_persist_xcd", 0)  # (the default)
         res.append((loss.item(), norm.item(), ae._flat_param.detach().clone()))
     for r in res[1:]:
         assert r[0] == res[0][0] and r[1] == res[0][1]
