@@ -2074,7 +2074,7 @@ constexpr int kBxNch = 4;  // 16-deep chunks per K-slice (2048 gates / 32 slices
 size_t bptt_xl_lds() { return (size_t)16 * kBxNch * 2048 + kBxNch * 2048 + 32 * 4 + 8 * 4; }
 
 __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
-  constexpr int H = 512, G4 = 2048, nkc = G4 / 16, NCH = kBxNch, UG = 4, KS = 64, RB = 32;
+  constexpr int H = 512, G4 = 2048, nkc = G4 / 16, NCH = kBxNch, KS = 64, RB = 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_x[];
   unsigned char* wl = lds_x;                                 // [16 unit tiles][NCH][hi, lo] 1 KiB blocks
   unsigned char* dgl = lds_x + 16 * NCH * 2048;              // [NCH][hi, lo] 1 KiB: this slice's split dG
