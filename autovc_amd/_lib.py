@@ -89,6 +89,7 @@ _SIGS = {
     "avc_lstm_persist_chunkwait": [_I],
     "avc_lstm_persist_xcd": [_I],
     "avc_debug_xl_census": [_P],
+    "avc_debug_xl_force_remote": [_I],
     "avc_gemm_plan_rounds": [_I],
     "avc_lstm_persist_granules": [_I],
     "avc_lstm_persist_halves": [_I],

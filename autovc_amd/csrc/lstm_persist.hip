@@ -199,6 +199,7 @@ struct PersistArgs {
   int nwg;                    // workgroups in the grid (XL: the active ones)
   unsigned spin_limit;        // polls before giving up (0 = test injection: give up at once)
   int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
+  int xl_remote;              // (avc_debug_xl_force_remote) treat every XL group as not local
 };
 int g_persist_diag = 0;
 __device__ unsigned g_xl_seen[2];  // (avc_debug_xl_census) recurrent workgroups that found their group local / not
@@ -571,7 +572,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       if (tid == 0) flag[3] = ok ? 1 : 0;
     }
     __syncthreads();
-    xl_local = flag[3] != 0;
+    xl_local = flag[3] != 0 && !a.xl_remote;
     if (tid == 0) atomicAdd(&g_xl_seen[xl_local ? 0 : 1], 1u);
   }
 
@@ -1339,6 +1340,7 @@ bool persist_gran(int H, int RT) {
 // avc_lstm_persist_xcd(): XCD-local groups in the one-layer form (PersistArgs::xl), off by default:
 // against the build without them (same box) lstm1 was 1 % faster at C2 and 3 % slower at C5
 int g_persist_xl = 0;
+int g_xl_remote = 0;  // avc_debug_xl_force_remote(): test the not-local fallback of the XCD-local forms
 
 // avc_lstm_persist_sentinel(): sentinel hand-off of split h (SN), bit 0 = two-layer form, bit 1 =
 // one-layer form
@@ -2056,6 +2058,7 @@ struct BpttXArgs {
   unsigned long long* tickets;
   unsigned* fail_host;
   unsigned spin_limit;
+  int xl_remote;            // (avc_debug_xl_force_remote) treat every group as not local
 };
 
 constexpr int kBxNch = 4;  // 16-deep chunks per K-slice (2048 gates / 32 slices / 16)
@@ -2125,7 +2128,7 @@ __global__ __launch_bounds__(512, 1) void bptt_xl_kernel(BpttXArgs a) {
     *reinterpret_cast<f16x8*>(wl + ((ut * NCH + c) * 2 + hl) * 1024 + lane * 16) = v;
   }
   __syncthreads();
-  const bool loc = flag[3] != 0;
+  const bool loc = flag[3] != 0 && !a.xl_remote;
   bool ok = flag[4] != 0;
   if (tid == 0) atomicAdd(&g_xl_seen[loc ? 0 : 1], 1u);
   const float sw_inv = 1.f / pow2_scale(__uint_as_float(*a.amax_w));
@@ -2523,6 +2526,7 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   }
   if (xl) {
     a.xl = 1;
+    a.xl_remote = g_xl_remote;
     a.xl_slots = ngrp * nslot;
     a.xl_tab = region + kRegionHeaderWords + cwords + gwords;
   }
@@ -2729,6 +2733,7 @@ int bptt_xl_run(avc_context* ctx, int T, int B, int reverse, const _Float16* whh
   a.cnt = a.xl_tab + 256;
   a.fail_host = ctx->fail_host;
   a.spin_limit = g_spin_limit;
+  a.xl_remote = g_xl_remote;
   if (g_persist_inject > 0) {
     --g_persist_inject;
     a.spin_limit = 0;
@@ -2953,6 +2958,12 @@ extern "C" int avc_bptt_xcd(int on) {
     return AVC_ERR_INVALID;
   }
   avc::g_bptt_xl = on;
+  ++avc::g_config_epoch;
+  return AVC_OK;
+}
+
+extern "C" int avc_debug_xl_force_remote(int on) {
+  avc::g_xl_remote = on ? 1 : 0;
   ++avc::g_config_epoch;
   return AVC_OK;
 }

@@ -383,6 +383,10 @@ int avc_lstm_persist_xcd(int on);
 /* Test hook: recurrent workgroups of XCD-local launches that found their group on one XCD / not,
  * since the last call (two words, then cleared). */
 int avc_debug_xl_census(unsigned* local_nonlocal);
+/* Test hook: 1 = the XCD-local forms (avc_lstm_persist_xcd, avc_bptt_xcd) treat every group as not
+ * local and run their fallback (write-through stores, counters) -- the path a box whose workgroup
+ * deal differs takes.  Same bits. */
+int avc_debug_xl_force_remote(int on);
 /* Tuning hook (round 5): 1 (default) = long-K products (weight gradients) pick their split-K count
  * by rounds of one workgroup per CU (a grid that spills a few workgroups into an extra round pays
  * the whole round); 0 = ~4 workgroups per CU (round 4).  The sums split differently: not

@@ -110,6 +110,7 @@ for step in "$@"; do
     xltrain) run xltrain 500 python scripts/train_hook_ab.py avc_lstm_persist_xcd 0 1 ;;
     abheadt) run abheadt 600 bash scripts/ab_lib_train.sh ab/prev_head.so ;;
     bptts) run bptts 400 python -u -m pytest tests/test_gpu_bptt_coalesce.py tests/test_gpu_bptt_xl.py tests/test_gpu_persist_safety.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    xlfb) run xlfb 400 python -u -m pytest tests/test_gpu_bptt_xl.py tests/test_gpu_xcd_local.py -v -x -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     bxlab) run bxlab 500 python scripts/train_hook_ab.py avc_bptt_xcd 0 1 ;;
     abtree) run abtree 1000 bash scripts/ab_r04_tree.sh ;;
     roundsab) run roundsab 500 python scripts/train_hook_ab.py avc_gemm_plan_rounds 0 1 ;;

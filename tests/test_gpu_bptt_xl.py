@@ -114,3 +114,21 @@ def test_xcd_local_bptt_timeout_is_nan_and_next_call_raises(cuda_device):
     y.backward(dy)
     torch.cuda.synchronize()
     assert all(torch.isfinite(w.grad).all() for w in ws) and torch.isfinite(x.grad).all()
+
+
+def test_xcd_local_bptt_fallback_is_bit_identical(cuda_device):
+    """Groups found not to share one XCD (forced here: avc_debug_xl_force_remote) hand the partials
+    over with write-through stores and a counter per (step, group) instead -- the same bits."""
+    B, T, din, H = 256, 40, 320, 512
+    ref, _ = _bwd(cuda_device, B, T, din, H, 0, seed=7)
+    _lib.call("avc_debug_xl_census", (ctypes.c_uint * 2)())  # (clear)
+    _lib.call("avc_debug_xl_force_remote", 1)
+    try:
+        got, _ = _bwd(cuda_device, B, T, din, H, 1, seed=7)
+    finally:
+        _lib.call("avc_debug_xl_force_remote", 0)
+    seen = (ctypes.c_uint * 2)()
+    _lib.call("avc_debug_xl_census", seen)
+    assert seen[1] >= 256 and seen[0] == 0, (seen[0], seen[1])  # every BPTT workgroup took the fallback
+    for name, a, b in zip(["dx", "dW_ih", "dW_hh", "db_ih", "db_hh"], got, ref):
+        assert torch.equal(a, b), name

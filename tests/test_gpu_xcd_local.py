@@ -81,3 +81,28 @@ def test_xcd_local_training_step_is_bit_identical(cuda_device):
     for r in res[1:]:
         assert r[0] == res[0][0] and r[1] == res[0][1]
         assert torch.equal(r[2], res[0][2])
+
+
+@pytest.mark.parametrize("B,T", [(64, 128), (32, 300)])
+def test_xcd_local_fallback_is_bit_identical(cuda_device, B, T):
+    """XL groups found not local (forced: avc_debug_xl_force_remote) keep the write-through stores
+    and counters on the linear grid -- the same bits as the round-4 grid."""
+    ae = _model(cuda_device, True)
+    x = torch.from_numpy(synthetic_mel(300 + B, B, T)).to(cuda_device)
+    co = torch.from_numpy(synthetic_embedding(301, B)).to(cuda_device)
+    ct = torch.from_numpy(synthetic_embedding(302, B)).to(cuda_device)
+    ref = _forwards(ae, x, co, ct, 2)
+    _lib.call("avc_debug_xl_census", (ctypes.c_uint * 2)())  # (clear)
+    try:
+        _lib.call("avc_lstm_persist_xcd", 1)
+        _lib.call("avc_debug_xl_force_remote", 1)
+        got = _forwards(ae, x, co, ct, 4)
+    finally:
+        _lib.call("avc_debug_xl_force_remote", 0)
+        _lib.call("avc_lstm_persist_xcd", 0)  # (the default)
+    seen = (ctypes.c_uint * 2)()
+    _lib.call("avc_debug_xl_census", seen)
+    assert seen[0] == 0 and seen[1] > 0, (seen[0], seen[1])
+    for run in got:
+        for a, b in zip(run, ref[0]):
+            assert torch.equal(a, b)
