@@ -5,7 +5,7 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable
 SRC      := $(wildcard autovc_amd/csrc/*.hip)
-HDR      := $(wildcard autovc_amd/csrc/*.h) include/autovc_hip.h
+HDR      := $(wildcard autovc_amd/csrc/*.h) include/autovc_hip.h include/autovc_hip_debug.h
 OBJ      := $(patsubst autovc_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB      := autovc_amd/libautovc_hip.so
 
@@ -18,8 +18,9 @@ build/%.o: autovc_amd/csrc/%.hip $(HDR)
 $(LIB): $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJ) -o $@
 
+#   (product surface: include/autovc_hip.h; tuning toggles / test hooks: include/autovc_hip_debug.h)
 check-abi: $(LIB)
-	python3 -c "import re,ctypes;h=open('include/autovc_hip.h').read();names=re.findall(r'^\w[\w\s\*]*?\b(avc_\w+)\(',h,re.M);lib=ctypes.CDLL('$(LIB)');[getattr(lib,n) for n in names];print(len(names),'symbols ok')"
+	python3 -c "import re,ctypes;lib=ctypes.CDLL('$(LIB)');n=[re.findall(r'^\w[\w\s\*]*?\b(avc_\w+)\(',open(f).read(),re.M) for f in ('include/autovc_hip.h','include/autovc_hip_debug.h')];[getattr(lib,x) for v in n for x in v];print(len(n[0]),'product +',len(n[1]),'debug symbols ok')"
 
 clean:
 	rm -rf build $(LIB)
@@ -38,7 +39,7 @@ build/sanitize/%.o: autovc_amd/csrc/%.hip $(HDR)
 	@mkdir -p build/sanitize
 	$(HIPCC) --offload-arch=$(ARCH) $(SAN_FLAGS) -c $< -o $@
 
-$(SAN_BIN): $(SAN_OBJ) tests/host_sanitize/abi_driver.cpp include/autovc_hip.h
+$(SAN_BIN): $(SAN_OBJ) tests/host_sanitize/abi_driver.cpp include/autovc_hip.h include/autovc_hip_debug.h
 	$(HIPCC) --offload-arch=$(ARCH) $(SAN_FLAGS) $(SAN_OBJ) tests/host_sanitize/abi_driver.cpp -o $@
 
 sanitize: $(SAN_BIN)

@@ -84,15 +84,9 @@ _SIGS = {
     "avc_lstm_persist_coop": [_I],
     "avc_lstm_persist_inproj": [_I],
     "avc_lstm_persist_qwait": [_I],
-    "avc_lstm_persist_sentinel": [_I],
-    "avc_lstm_persist_st16": [_I],
-    "avc_lstm_persist_chunkwait": [_I],
-    "avc_lstm_persist_xcd": [_I],
     "avc_debug_xl_census": [_P],
     "avc_debug_xl_force_remote": [_I],
     "avc_gemm_plan_rounds": [_I],
-    "avc_lstm_persist_granules": [_I],
-    "avc_lstm_persist_halves": [_I],
     "avc_bn_bwd_frag": [_I],
     "avc_bptt_coalesce": [_I],
     "avc_dg_dual_split": [_I],

@@ -37,7 +37,13 @@ _PREP_OWNER = {}  # device -> uid of the model whose derived weights the library
 class FusedAdam(torch.optim.Optimizer):
     """torch.optim.Adam semantics (amsgrad=False) on the flat parameter/gradient buffers of an
     AutoEncoder, fused with clip_grad_norm_ and the EMA of model.py:314-321 in one HIP pass
-    (avc_clip_adam_ema).  state_dict() has torch Adam's layout (step/exp_avg/exp_avg_sq)."""
+    (avc_clip_adam_ema).  state_dict() has torch Adam's layout (step/exp_avg/exp_avg_sq).
+
+    The device counts the updates it skipped for a non-finite gradient norm, and each update's
+    bias correction uses (step() calls - skips) on the device, so step() never waits for the norm.
+    The host-side 'step' in ``optimizer.state[p]`` is therefore PROVISIONAL between settles: it
+    counts step() calls, skipped ones included, until state_dict() or settle() folds the device
+    count in.  Code that reads ``state[p]['step']`` directly should call settle() first."""
 
     def __init__(self, model: "AutoEncoder", lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  amsgrad=False, **_ignored):
@@ -99,6 +105,10 @@ class FusedAdam(torch.optim.Optimizer):
             self._step -= sk
             self._skips.zero_()
         self._step_t.fill_(float(self._step))
+
+    def settle(self):
+        """Public form of _settle(): make ``state[p]['step']`` exact (waits for the device)."""
+        self._settle()
 
     def state_dict(self):
         self._settle()

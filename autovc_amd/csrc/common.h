@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/autovc_hip.h"
+#include "../../include/autovc_hip_debug.h"
 
 namespace avc {
 

@@ -1206,7 +1206,8 @@ __global__ __launch_bounds__(256) void sumsq_partial_kernel(long n, const float*
 // one block of 256: strided partial sums, then a fixed-order tree (deterministic)
 __global__ __launch_bounds__(256) void clip_coef_kernel(int nparts, const double* __restrict__ part, float max_norm,
                                                         float* __restrict__ norm_out, float* __restrict__ coef,
-                                                        unsigned* __restrict__ skips) {
+                                                        unsigned* __restrict__ skips, int step, float lr, float b1,
+                                                        float b2) {
   __shared__ double red[256];
   double s = 0.0;
   for (int p = threadIdx.x; p < nparts; p += 256) s += part[p];
@@ -1233,6 +1234,12 @@ __global__ __launch_bounds__(256) void clip_coef_kernel(int nparts, const double
   unsigned sk = skips ? *skips : 0u;
   if (skips && !isfinite(norm)) *skips = ++sk;
   coef[2] = __uint_as_float(sk);
+  // the bias corrections of effective step max(1, step - sk), formed here in double as the host
+  // forms its table (clip_adam_ema): adam_ema_kernel takes these where sk is past the table, so
+  // any number of skipped updates between two settles keeps torch.optim.Adam's step
+  const int st = (int)max(1L, (long)step - (long)sk);
+  coef[3] = (float)((double)lr / (1.0 - pow((double)b1, (double)st)));
+  coef[4] = (float)sqrt(1.0 - pow((double)b2, (double)st));
 }
 
 constexpr int kAdamTab = 8;
@@ -1241,6 +1248,7 @@ struct AdamArgs {
   int clip;
   int guard;  // coef[1] holds the skip flag of clip_coef_kernel
   int tabled;  // step_size / bc2_sqrt from the tables below, indexed by the device skip count coef[2]
+               // (coef[3] / coef[4], formed by clip_coef_kernel, past the table's end)
   float ss[kAdamTab], bc[kAdamTab];  // the host's values for effective steps step, step - 1, ...
 };
 
@@ -1276,10 +1284,11 @@ __global__ __launch_bounds__(256) void adam_ema_kernel(long n, long n4, float* _
   if (a.tabled) {
     // table entry k by selects: a dynamic index into the by-value arguments put the whole struct
     // in scratch, and every element's update read its scalars from there (adam 218 -> 297 us at C3)
-    const unsigned k = min(__float_as_uint(coef[2]), (unsigned)(kAdamTab - 1));
-    float ss = a.ss[0], bc = a.bc[0];
+    // (k >= kAdamTab: the device's own values for step - k)
+    const unsigned k = __float_as_uint(coef[2]);
+    float ss = coef[3], bc = coef[4];
 #pragma unroll
-    for (int j = 1; j < kAdamTab; ++j) {
+    for (int j = 0; j < kAdamTab; ++j) {
       ss = k == (unsigned)j ? a.ss[j] : ss;
       bc = k == (unsigned)j ? a.bc[j] : bc;
     }
@@ -1660,11 +1669,11 @@ int clip_adam_ema(avc_context* ctx, size_t n, float* p, float* g, float* m, floa
   Scratch sc(ctx);
   const int nb = (int)std::min<size_t>(2048, (n + 255) / 256);
   AVC_TAKE(part, double, (size_t)nb, sc);
-  AVC_TAKE(coef, float, 4, sc);
+  AVC_TAKE(coef, float, 8, sc);
   const bool need_norm = max_norm > 0.f || norm_out != nullptr;
   if (need_norm) {
     sumsq_partial_kernel<<<nb, 256, 0, s>>>((long)n, g, part);
-    clip_coef_kernel<<<1, 256, 0, s>>>(nb, part, max_norm, norm_out, coef, skips);
+    clip_coef_kernel<<<1, 256, 0, s>>>(nb, part, max_norm, norm_out, coef, skips, step, lr, b1, b2);
   }
   AdamArgs a{};
   a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;

@@ -15,6 +15,7 @@
 //     steps afterwards.
 // Small H (32 — encoder BiLSTM): one single-wave workgroup per (utterance, direction) walks
 //   all T steps with W_hh held in registers and h broadcast through LDS (latency-bound path).
+#include <mutex>
 #include <algorithm>
 
 #include "kernels.h"
@@ -629,8 +630,10 @@ __global__ __launch_bounds__(64) void lstm32_fwd_kernel(int T, int B, long ldgx,
   constexpr unsigned kOut = 0x80000000u;
   const long TB = (long)T * B;
   const auto yrs = __builtin_amdgcn_make_buffer_rsrc(D.y, 0, (int)std::min<long>(TB * ldy * 4, 0x7fffffffL), 0x00020000);
-  const auto crs = __builtin_amdgcn_make_buffer_rsrc(D.c, 0, D.c ? (int)(TB * 32 * 4) : 0, 0x00020000);
-  const auto grs = __builtin_amdgcn_make_buffer_rsrc(D.gates, 0, D.gates ? (int)(TB * 128 * 4) : 0, 0x00020000);
+  // (launch_lstm32 refuses T * B * 512 >= 2^31; the clamps keep a descriptor from wrapping regardless)
+  const auto crs = __builtin_amdgcn_make_buffer_rsrc(D.c, 0, D.c ? (int)std::min<long>(TB * 32 * 4, 0x7fffffffL) : 0, 0x00020000);
+  const auto grs = __builtin_amdgcn_make_buffer_rsrc(D.gates, 0, D.gates ? (int)std::min<long>(TB * 128 * 4, 0x7fffffffL) : 0,
+                                                     0x00020000);
   const bool lo = lane < 32;
   auto step = [&](int s, float z0, float z1) {
     const int t = reverse ? T - 1 - s : s;
@@ -862,12 +865,16 @@ int g_dg_dual = 1;  // avc_dg_dual_split(): one pass writes both split images of
 int g_lstm32_mode = 1;  // avc_lstm32_tune(): 0 = libm gate math, 3-step prefetch; 1 = fast math with a
                         // memory wave (lstm32_fwd2_kernel); 4 = fast math, one wave
 
-void launch_lstm32(int nblk, int T, int B, long ldgx, long ldy, const L32Dir& d0, const L32Dir& d1, hipStream_t s) {
+int launch_lstm32(int nblk, int T, int B, long ldgx, long ldy, const L32Dir& d0, const L32Dir& d1, hipStream_t s) {
+  // the one-wave kernels address the saved gates / cell states through buffer descriptors with
+  // 32-bit byte offsets: refuse sizes whose offsets would wrap
+  AVC_CHECK_ARG((long)T * B * 512 < 0x80000000L, "encoder BiLSTM: T * B too large for 32-bit gate offsets");
   if (g_lstm32_mode == 0) lstm32_fwd_kernel<3, false><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
   else if (g_lstm32_mode == 2) lstm32_fwd_kernel<8, true, 1><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
   else if (g_lstm32_mode == 3) lstm32_fwd_kernel<8, true, 2><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
   else if (g_lstm32_mode == 4) lstm32_fwd_kernel<8, true><<<nblk, 64, 0, s>>>(T, B, ldgx, ldy, d0, d1);
   else lstm32_fwd2_kernel<8><<<nblk, 128, 0, s>>>(T, B, ldgx, ldy, d0, d1);
+  return AVC_OK;
 }
 
 // BPTT of an H = 32 direction: one single-wave workgroup per utterance walks the steps backwards.
@@ -1070,7 +1077,7 @@ int lstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, int revers
     AVC_TRY(gemm_run(ctx, g, s));
     hipEvent_t ev = timing_begin(TC_LSTM32, s);
     L32Dir d{gx, w_hh, y, saved_gates, saved_c, reverse};
-    launch_lstm32(B, T, B, 128, ldy, d, d, s);
+    AVC_TRY(launch_lstm32(B, T, B, 128, ldy, d, d, s));
     AVC_LAUNCH_CHECK();
     if (ev) timing_end(TC_LSTM32, ev, s, 2.0 * T * B * 128.0 * 32.0, 4.0 * T * B * (128.0 + 32.0));
     return AVC_OK;
@@ -1186,7 +1193,7 @@ int bilstm_forward_impl(avc_context* ctx, int T, int B, int din, int H, const fl
   hipEvent_t ev = timing_begin(TC_LSTM32, s);
   L32Dir d0{gx, wf[1], y, g_f, c_f, 0};
   L32Dir d1{gx + 128, wr[1], y + 32, g_r, c_r, 1};
-  launch_lstm32(2 * B, T, B, 256, ldy, d0, d1, s);
+  AVC_TRY(launch_lstm32(2 * B, T, B, 256, ldy, d0, d1, s));
   AVC_LAUNCH_CHECK();
   if (ev) timing_end(TC_LSTM32, ev, s, 2.0 * 2 * T * B * 128.0 * 32.0, 2.0 * 4.0 * T * B * (128.0 + 32.0));
   return AVC_OK;
@@ -1327,13 +1334,22 @@ size_t lstm_backward_scratch(int T, int B, int din, int H) {
 }
 
 __device__ unsigned g_h_bound_bits = 0x3f800000u;  // 1.0f: the bound of an LSTM's |h|
+// The word's address on the CURRENT device: a __device__ symbol has one instance per device, and
+// the library keeps one context per device in one process (a single cached address
+// made a second device's LSTM backward read the first device's global).
 const unsigned* h_bound_word() {
-  static const unsigned* p = nullptr;
-  if (!p) {
+  constexpr int kMaxDev = 64;
+  static std::mutex m;
+  static const unsigned* addr[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  std::lock_guard<std::mutex> g(m);
+  if (!addr[dev]) {
     void* q = nullptr;
-    if (hipGetSymbolAddress(&q, HIP_SYMBOL(g_h_bound_bits)) == hipSuccess) p = static_cast<const unsigned*>(q);
+    if (hipGetSymbolAddress(&q, HIP_SYMBOL(g_h_bound_bits)) == hipSuccess) addr[dev] = static_cast<const unsigned*>(q);
+    else (void)hipGetLastError();
   }
-  return p;  // nullptr: the product scans y itself
+  return addr[dev];  // nullptr: the product scans y itself
 }
 
 int lstm_backward_impl(avc_context* ctx, int T, int B, int din, int H, int reverse,

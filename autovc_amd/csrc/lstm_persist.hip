@@ -71,7 +71,7 @@ namespace avc {
 
 int g_persist_mode = 2;  // avc_lstm_persist_tune(): 0 = never; 1 / 2 = when eligible (hand-off form)
 int g_persist_layers = 3;  // avc_lstm_persist_layers(): bit 0 = one-layer form, bit 1 = two-layer form
-int g_persist_pd = 2;    // avc_lstm_persist_depth(): h chunks in flight ahead of the MFMAs (1..4; 3 / 4: halves only)
+int g_persist_pd = 2;    // avc_lstm_persist_depth(): h chunks in flight ahead of the MFMAs (1 or 2)
 
 namespace {
 
@@ -105,13 +105,6 @@ __host__ __device__ __forceinline__ long qcnt_index(int nslot, int L, int T, int
 // counter words of one group: the full lines, and with quarter counters four more per (slot, step)
 __host__ __device__ __forceinline__ long cnt_words(int nslot, int T, bool quarters) {
   return (long)nslot * T * kRep * kLine * (quarters ? 1 + kQuarters : 1);
-}
-// Chunk counters (round 5, `avc_lstm_persist_chunkwait`, two-layer form): one per (slot, step,
-// 32-deep chunk kc of h), after the quarter counters; the two workgroups that write chunk kc
-// (units 32 kc .. 32 kc + 31, workgroups 2 kc and 2 kc + 1) count in on it, so a consumer wave can
-// start on chunk c of its K quarter once those two are in instead of waiting for all sixteen.
-__host__ __device__ __forceinline__ long ccnt_index(int nslot, int L, int T, int t, int kc, int r, int nck) {
-  return cnt_words(nslot, T, true) + ((((long)L * T + t) * nck + kc) * kRep + r) * kLine;
 }
 // gx1 hand-off: a ring of kGxRing steps of per-column-block slabs [64 rows][64 columns] fp32, so
 // each (step, column block) pair exchanges one contiguous 16 KB; slot 1 re-fills a ring entry
@@ -184,51 +177,15 @@ struct PersistArgs {
   unsigned* tmo;              // give-up word: epoch of the last launch that gave up
   unsigned long long* tickets;  // one per workgroup per launch
   unsigned* fail_host;        // pinned host word (avc_context::fail_host): last failure number
-  unsigned char* hg;          // GR: granule ring [grp][kGrRing][hg_step] (in the counter region)
-  long hg_step, hg_gstride;   // GR: bytes per (group, step) / per group
-  unsigned char* hsn;         // SN: split-h hand-off buffers [layer][2 sets][T][hsz] (in the region)
-  long hsn_set, hsn_layer;    // SN: bytes per set (T * hsz) and per layer (two sets)
-  int st16;                   // split-h hand-off stores as 16-B pieces (avc_lstm_persist_st16)
-  // XL (round 5, avc_lstm_persist_xcd; one-layer form): a linear grid of 8 x ncb workgroups dealt
-  // so that workgroup bid is (slot residue bid % 8, column block bid / 8): under the round-robin
-  // XCD deal every recurrent group sits on one XCD.  Checked at run time (xl_tab); a group whose
-  // workgroups do share one XCD hands h over with plain stores (the lines stay in that XCD's L2,
-  // which its consumers' sc1 loads read), any other with the write-through stores.
-  int xl, xl_slots;           // xl_slots: residues in use (nslot * ngrp <= 8); the rest exit at once
-  unsigned* xl_tab;           // [8 * ncb] epoch-tagged XCD of each workgroup (in the region)
-  int nwg;                    // workgroups in the grid (XL: the active ones)
+  int nwg;                    // workgroups in the grid
   unsigned spin_limit;        // polls before giving up (0 = test injection: give up at once)
   int diag;                   // diagnostic build only (avc_debug_persist_diag): timing experiments
-  int xl_remote;              // (avc_debug_xl_force_remote) treat every XL group as not local
 };
 int g_persist_diag = 0;
-__device__ unsigned g_xl_seen[2];  // (avc_debug_xl_census) recurrent workgroups that found their group local / not
+__device__ unsigned g_xl_seen[2];  // (avc_debug_xl_census) XCD-local BPTT workgroups that found their group local / not
 // avc_lstm_persist_qwait(): per-wave waits on quarter counters, bit 0 = two-layer form (lstm2:
 // 1141 -> 1073 us at C2), bit 1 = one-layer form (lstm1: 384 -> 400 us at C2, so off)
 int g_persist_qwait = 1;
-// avc_lstm_persist_granules(): the one-layer form hands split h over as data-tagged granules
-int g_persist_gran = 0;  // (round 4: the counter form measured 20 us faster at C2, equal at C5)
-
-// Granule hand-off (GR, one-layer form, H = 512): split h_t goes out as 8-B granules
-// {f16 hi | f16 lo << 16, tag}, one per (batch row, hidden unit), each written by ONE sc1 store
-// (cdna_hip_programming.md Guideline 16, R2: the data is the flag).  A consumer wave loads its K
-// quarter of h_{t-1} and re-loads until every tag it holds is this (launch, step)'s tag: no
-// drain, no workgroup barrier and no counter between the producer's epilogue and the consumer's
-// MFMAs.  Layout per (group, step): [RT tiles][nck chunks][4 j][64 lanes][16 B], lane l of chunk
-// kc holding row l & 15, units kc*32 + 8*(l >> 4) + 2j, +1 -- the lane's 8 units of the split-h
-// fragment in 4 b128 loads, each wave instruction reading 1 KB contiguous.  A ring of kGrRing
-// steps: a producer at step t has seen h_{t-1} of every workgroup of its group, so every reader
-// of step t - 2 is done (ring >= 2 suffices); the tag carries t & 7 so the step t - 4 left in the
-// same entry never matches, and E so an earlier launch's granules never do.
-// Torn reads: the memory model does not promise that a 16-B load sees an 8-B store whole, so the
-// stored tag word is gr_tag ^ data and a consumer accepts a granule only when tag ^ data equals
-// this step's gr_tag.  With data and tag from different stores: a new tag with an old data word
-// passes only if the two data words are equal, and an old tag with the new data word only ever
-// hands over the new data -- either way the accepted data is this step's, so a tear can delay a
-// consumer (it re-loads) but never feed it stale h.  (Old tag with old data never passes: tags of
-// different steps or launches differ, and a zeroed entry's 0 is no tag, E >= 1.)
-constexpr int kGrRing = 4;
-__host__ __device__ __forceinline__ unsigned gr_tag(unsigned E, int t) { return (E << 3) | (unsigned)(t & 7); }
 
 // One wave, every lane: leave a spin?  The give-up word is read every 64 passes; past the limit
 // the launch gives up (the first wave to do so reports it, as wait_ge_ctl).  spins is uniform.
@@ -330,15 +287,13 @@ constexpr int kLead3 = 12;  // with back-pressure (in_lead 2 / 3) the input slot
 // bn_apply_frag's split), reduces the 4 waves' K quarters in a fixed order and stores
 // gx0_t = sum * unscale + b0 with whole-line write-through stores, then counts itself in on
 // cnt[3][t].  Slot 0 waits for that counter and reads gx0_t with sc1 loads (the gx1 hand-off form).
-// NHI: the recurrence's batch halves (counters per (step, half), see lstm_persist_kernel): this
-// slot computes every row of a step at once and counts in on the step's last half.
-template <int RT, int NCH3, int NHI>
+template <int RT, int NCH3>
 __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* part, int* flag, unsigned E,
                            unsigned target, int cb) {
   constexpr int NW = 4, NC = 4, MB = 16 * RT, TW = 16 * NC, RP = TW + 4;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
-  const int B = a.B, T = a.T, TT = T * NHI;
+  const int B = a.B, T = a.T;
   const int nck3 = 4 * NCH3;  // a.din == 128 * NCH3
   const long G4 = 4L * a.H;
   const int rep = blockIdx.x & (kRep - 1);
@@ -371,7 +326,7 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
     // back-pressure: at most kLead3 steps ahead of slot 0
     if (tid == 0) {
       const bool check = t >= kLead3 && (a.in_lead == 3 || (a.in_lead == 2 && (t & 3) == 0));
-      const bool ok = !check || wait_ge(cnt + cnt_index(0, TT, (t - kLead3) * NHI + NHI - 1, rep), target, a, E);
+      const bool ok = !check || wait_ge(cnt + cnt_index(0, T, t - kLead3, rep), target, a, E);
       flag[0] = ok ? 1 : 0;
     }
     __syncthreads();
@@ -429,33 +384,9 @@ __device__ void input_slot(const PersistArgs& a, unsigned* cnt, int grp, float* 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid < kRep)
-      __hip_atomic_fetch_add((gu32*)(cnt + cnt_index(a.in_slot, TT, t * NHI + NHI - 1, tid)), 1u, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add((gu32*)(cnt + cnt_index(a.in_slot, T, t, tid)), 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-// SN hand-off (lstm_persist_kernel's SN): is every dword of an h chunk (RT row tiles x hi / lo,
-// one b128 per lane each) written?  The sentinel dword 0xFFFFFFFF is two f16 NaNs with every
-// payload bit set; producers never store it (sn_word), so a dword that is not the sentinel holds
-// this launch's data.  Wave-uniform result.
-template <int RT>
-__device__ __forceinline__ bool sn_ready(const f16x8 (&hv)[RT][2]) {
-  bool bad = false;
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int hl = 0; hl < 2; ++hl) {
-      const u32x4 v = __builtin_bit_cast(u32x4, hv[r][hl]);
-      bad = bad | (v[0] == ~0u) | (v[1] == ~0u) | (v[2] == ~0u) | (v[3] == ~0u);
-    }
-  return __builtin_amdgcn_ballot_w64(bad) == 0ull;
-}
-// a stored dword of split h (two f16): an f16 0xFFFF (a NaN h) becomes the canonical NaN 0x7E00,
-// so no producer ever writes the sentinel
-__device__ __forceinline__ unsigned sn_word(unsigned v) {
-  if ((v & 0xffffu) == 0xffffu) v = (v & 0xffff0000u) | 0x7e00u;
-  if ((v >> 16) == 0xffffu) v = (v & 0xffffu) | 0x7e000000u;
-  return v;
 }
 
 // HO = hand-off form on the consumer side: 0 = one agent-scope acquire (L1 invalidate) then plain
@@ -464,76 +395,38 @@ __device__ __forceinline__ unsigned sn_word(unsigned v) {
 // PD = h chunks loaded ahead of the chunk being multiplied (register buffers PD + 1).
 // QW = 1: per-wave waits on quarter counters (see qcnt_index) instead of three polling lanes and a
 // workgroup barrier at the top of every step.
-// GR = 1: granule hand-off of split h (one-layer form, NCH = 4, RT = 1; see gr_tag).
-// NH = 2: batch halves (two-layer form with quarter waits; round 4).  The workgroup's rows are two
-// independent halves of 16 * RT rows (LSTM batch rows never interact), walked alternately: step t
-// of half 0, then step t of half 1, each with its own wait, product, reduction, epilogue and
-// publish, on counters per (step, half).  A half's hand-off (drain, counter, the consumers' poll
-// and first loads) then runs while every workgroup computes the other half, instead of on the
-// critical path of the whole step.  Same products, same order per row: bit-identical to NH = 1.
-// SN = 1: sentinel hand-off of split h (round 5; sn_ready).  The split-h buffers live in the
-// launch's region as two sets [2][T][hsz] per layer, every byte 0xFF (the sentinel: an f16 pair
-// 0xFFFF 0xFFFF is a NaN no producer writes, see sn_word) except what this launch has written.  A
-// consumer wave loads its h chunks as soon as its step starts and re-loads a chunk until no dword
-// of it is the sentinel; a dword is written by one store, so a dword that is not the sentinel is
-// this launch's data.  No drain, barrier, counter add or poll stands between a producer's epilogue
-// and its consumers' MFMAs, and each wave's chunk waits only for that chunk's two producers (not a
-// quarter's sixteen).  Launch E uses set E & 1; each producer resets its bytes of step t in the
-// other set to the sentinel right after storing them in this one, so launch E + 1 finds it clean.
-// Counters remain for the gx hand-offs and the back-pressure (slot 0 publishes none).
-// CW = 1: per-chunk waits (round 5, see ccnt_index): each wave waits for its chunks 0 and 1 at the
-// step start and polls chunk c + 2's counter one chunk ahead of its loads (two-layer form, QW).
-template <int NCH, int RT, int HO, int PD, int QW, int GR = 0, int NH = 1, int SN = 0, int CW = 0, int XL = 0>
+// (Round 6: the hand-off variants measured and rejected in rounds 3-5 -- granules, batch halves,
+// sentinel h, per-chunk waits, XCD-local lstm1 groups -- are no longer compiled)
+template <int NCH, int RT, int HO, int PD, int QW>
 __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
-  static_assert(!CW || (QW && !GR && !SN && NH == 1 && PD == 2 && RT >= 2 && NCH >= 3),
-                "chunk waits: two-layer quarter-wait form, PD 2, RT >= 2");
-  static_assert(!GR || (NCH == 4 && RT == 1 && HO == 1 && !QW), "granule hand-off: one-layer form, H = 512, RT = 1");
-  static_assert(NH == 1 || (NH == 2 && QW && !GR && HO == 1), "batch halves: two-layer quarter-wait form");
-  static_assert(!SN || (HO == 1 && !GR && NH == 1), "sentinel hand-off: sc1 loads, counter-free h, one half");
-  static_assert(!XL || (NCH == 4 && HO == 1 && PD == 2 && !QW && !GR && NH == 1 && !SN && !CW),
-                "XCD-local groups: the one-layer form's default hand-off (its own instances, so the other forms "
-                "compile without the XL code)");
   constexpr int NW = 4, NC = 4;
-  constexpr int MB = 16 * RT;        // batch rows computed per half (B <= MB * NH)
+  constexpr int MB = 16 * RT;        // batch rows computed (B <= MB)
   constexpr int TW = 16 * NC;        // 64 gate rows
   constexpr int RP = TW + 4;
   constexpr int NPAIR = MB * NC;     // (row, 16-column block) epilogue pairs, <= 256
   // LDS: gate tile 3's weights for every wave (NW x NCH x 2 KiB), then the reduction partials
-  // (sized for all NH halves: the input slot reduces every row at once)
   extern __shared__ float lds[];
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds);
   float* part = lds + NW * NCH * 512;
   // [8]: polling lanes' results (0, 1, 3), epoch (2); QW: each wave's wait result (4 + w)
-  int* flag = reinterpret_cast<int*>(part + NW * MB * NH * RP);
+  int* flag = reinterpret_cast<int*>(part + NW * MB * RP);
   // [TW] per-row unscale of this block's gate rows, then [TW] b_ih1 + b_hh1 (slot 1): read from
   // LDS in the epilogue instead of living in registers through the MFMA loop
   float* cpar = reinterpret_cast<float*>(flag + 8);
-  // GR: [MB][16] split h of this workgroup's 16 hidden units, staged for the granule stores; then
-  // [MB][16] the unscaled split of the same h for the y_frag image (whole fragment rows, below)
-  unsigned* hst = reinterpret_cast<unsigned*>(cpar + 2 * 64);
-  unsigned* yst = hst + MB * NH * 16;
+  // [MB][16] the unscaled split of this workgroup's h for the y_frag image (whole fragment rows)
+  unsigned* yst = reinterpret_cast<unsigned*>(cpar + 2 * 64);
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, lq = lane >> 4;
-  int L, cb, grp;
   // batch group: rows [grp * MB, grp * MB + MB).  LSTM batch rows never interact, so in the
   // one-layer form every group is an independent recurrence with counters of its own.
-  if (XL && a.xl) {  // (see PersistArgs::xl)
-    const int xs = blockIdx.x & 7;
-    if (xs >= a.xl_slots) return;  // an unused residue: no ticket, no counter
-    L = a.nslot == 2 ? (xs & 1) : 0;
-    grp = a.nslot == 2 ? xs >> 1 : xs;
-    cb = blockIdx.x >> 3;
-  } else {
-    L = blockIdx.x / a.ncb;
-    cb = blockIdx.x - L * a.ncb;
-    grp = blockIdx.y;
-  }
+  const int L = blockIdx.x / a.ncb;
+  const int cb = blockIdx.x - L * a.ncb;
+  const int grp = blockIdx.y;
   const int B = a.B, H = a.H, T = a.T;
   unsigned* const cnt = a.cnt + (long)grp * a.cnt_gstride;
   const int nck = H >> 5;            // 32-deep chunks per row
   const long G4 = 4L * H;
-  const int TT = T * NH;             // counter steps: one per (time step, half)
 
   // this launch's epoch (see the header): every workgroup takes one ticket
   if (tid == 0) {
@@ -544,41 +437,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   const unsigned E = (unsigned)flag[2];
   const unsigned target = E * (unsigned)a.ncb;
 
-  // XL: this group's recurrent workgroups record their XCD, then each checks that all of them share
-  // one (every member reads the same ncb words: the same decision).  Bounded like every wait.
-  bool xl_local = false;
-  if (XL && a.xl && L == 0) {
-    if (tid < 64) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      const int xs = blockIdx.x & 7;
-      if (tid == 0)
-        __hip_atomic_store((gu32*)(a.xl_tab + blockIdx.x), (E << 4) | (xcc & 7u), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      bool same = true, done = false;
-      for (unsigned spins = 0; !done; ++spins) {
-        bool all = true;
-        same = true;
-        for (int k = tid; k < a.ncb; k += 64) {
-          const unsigned v = __hip_atomic_load((gu32*)(a.xl_tab + k * 8 + xs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          all &= (v >> 4) == (E & 0x0fffffffu);
-          same &= (v & 7u) == (xcc & 7u);
-        }
-        done = __builtin_amdgcn_ballot_w64(!all) == 0ull;
-        if (!done && spin_give_up(spins, a, E, tid)) break;  // (then: the write-through stores)
-        if (!done) __builtin_amdgcn_s_sleep(2);
-      }
-      const bool ok = done && __builtin_amdgcn_ballot_w64(!same) == 0ull;
-      if (tid == 0) flag[3] = ok ? 1 : 0;
-    }
-    __syncthreads();
-    xl_local = flag[3] != 0 && !a.xl_remote;
-    if (tid == 0) atomicAdd(&g_xl_seen[xl_local ? 0 : 1], 1u);
-  }
-
   if (a.in_slot > 0 && L == a.in_slot) {  // layer 0's input projection
-    if (a.din == 512) input_slot<RT * NH, 4, NH>(a, cnt, grp, part, flag, E, target, cb);
-    else input_slot<RT * NH, 3, NH>(a, cnt, grp, part, flag, E, target, cb);
+    if (a.din == 512) input_slot<RT, 4>(a, cnt, grp, part, flag, E, target, cb);
+    else input_slot<RT, 3>(a, cnt, grp, part, flag, E, target, cb);
     return;
   }
 
@@ -610,10 +471,9 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
   static_assert(NPAIR * SUB == 256, "one epilogue slot per thread");
   const int pair = tid / SUB, sub = tid % SUB, u0 = sub * UPT;
   const int row = pair / NC, blk = pair % NC;
-  const int row0 = grp * MB * NH + row;  // this thread's batch row in half 0 (half hf: + hf * MB)
-  int b = row0;
-  bool live = b < B;
-  int bc = min(b, B - 1);
+  const int b = grp * MB + row;            // this thread's batch row
+  const bool live = b < B;
+  const int bc = min(b, B - 1);
   const int p0 = cb * TW + blk * 16;       // first permuted gate column of the pair
   const int j0 = cb * 4 * NC + blk * 4;    // first hidden unit of the pair
   typedef float fu __attribute__((ext_vector_type(UPT)));
@@ -621,14 +481,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     cpar[tid] = a.winv[L][cb * TW + tid];
     if (L == 1) cpar[TW + tid] = a.b1[cb * TW + tid];
   }
-  fu cst = fu{}, cst_other = fu{};  // cell state of the current half, and of the other one (NH = 2)
+  fu cst = fu{};  // cell state
   // slot 1 stores gx1 in whole lines: lane -> (row 4i + lane/16 of the wave's 16, columns 4*pc..)
   const int pc = lane & 15;
   float* c_save = L == 0 ? a.c0 : a.c1;
   float* g_save = L == 0 ? a.g0 : a.g1;
   float* y_out = L == 0 ? a.y0 : a.y1;
   auto gx1_slab = [&](int tt, int c) -> long { return ((long)(tt % kGxRing) * a.ncb + c) * (64 * TW); };
-  const int rep = (XL && a.xl ? blockIdx.x >> 3 : blockIdx.x) & (kRep - 1);
+  const int rep = blockIdx.x & (kRep - 1);
   // outputs nobody reads inside this launch: h, and for training c and the activated gates
   _Float16* const yfrag = L == a.yf_slot ? a.yfrag : nullptr;
   // frag: also this thread's units of y_frag (the give-up NaN fill; normally yfrag_rows writes it)
@@ -660,7 +520,6 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       *reinterpret_cast<fu*>(go + 12) = o;
     }
   };
-  fu pend_h = {}, pend_c = {}, pend_i = {}, pend_f = {}, pend_g = {}, pend_o = {};  // GR: step t - 1's outputs
   // y_frag as whole fragment rows (round 4): the MB rows staged in yst (batch rows rb0 ..) of step
   // tt go out as 16-B pieces, 32 consecutive fragment lanes of one (hi / lo, k half) per 512 B.
   // This workgroup's 16 units are exactly the 16-k chunk cb of the image.  (Per-thread stores of
@@ -681,18 +540,11 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     }
   };
 
-  int s = 0;
-  for (; s < TT; ++s) {
-    const int t = NH == 1 ? s : s / NH, hf = NH == 1 ? 0 : s % NH;
-    if constexpr (NH > 1) {
-      b = row0 + hf * MB;
-      live = b < B;
-      bc = min(b, B - 1);
-    }
+  int t = 0;
+  for (; t < T; ++t) {
     // ---- wait for this step's operands ----------------------------------------------------
     AVC_PSTAMP(0);
-    if constexpr (QW || GR || SN) {
-      // GR: only the input slot's gx0 is waited on here (h comes with its tags, below).
+    if constexpr (QW) {
       // Lane 0 of every wave waits for what THIS wave reads, all in one multi-counter poll: the
       // quarter of the h source its K chunks come from; slot 2: the slot-1 quarter that wrote its
       // gx1 slab (the one of workgroup cb); slot 0 with the input slot, every 4th step: gx0 for 4
@@ -705,72 +557,40 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         const int hsl = L == 1 ? 0 : L;      // slot whose h this slot reads (0: h0, 2: h1)
         const int ht = L == 1 ? t : t - 1;   // and its step
         // 0: the h quarter; 1: the gx operand; 2: back-pressure (wave 1)
-        // (NH = 2: h and gx1 per (step, half); the input slot's gx0 and the back-pressure per step,
-        // taken at half 0 on the last half's counters -- a workgroup publishes its halves in order)
-        const bool e0 = !GR && !SN && ht >= 0;  // (SN: the h chunks carry their own readiness)
-        // (CW: chunks 0 and 1 of this wave's quarter instead of the whole quarter)
-        unsigned* p0 = CW ? cnt + ccnt_index(a.nslot, hsl, T, e0 ? ht : 0, w * NCH, rep, nck)
-                          : cnt + qcnt_index(a.nslot, hsl, TT, e0 ? ht * NH + hf : 0, w, rep);
-        const bool e1 = L == 2 || (L == 0 && a.in_slot > 0 && (t & 3) == 0 && hf == 0);
-        unsigned* p1 = L == 2 ? cnt + qcnt_index(a.nslot, 1, TT, t * NH + hf, cb / (a.ncb / kQuarters), rep)
-                              : cnt + cnt_index(a.in_slot, TT, min(t + 3, T - 1) * NH + NH - 1, rep);
+        const bool e0 = ht >= 0;
+        unsigned* p0 = cnt + qcnt_index(a.nslot, hsl, T, e0 ? ht : 0, w, rep);
+        const bool e1 = L == 2 || (L == 0 && a.in_slot > 0 && (t & 3) == 0);
+        unsigned* p1 = L == 2 ? cnt + qcnt_index(a.nslot, 1, T, t, cb / (a.ncb / kQuarters), rep)
+                              : cnt + cnt_index(a.in_slot, T, min(t + 3, T - 1), rep);
         const unsigned t1 = L == 2 ? qtarget : target;
-        const bool e2 = !GR && w == 1 && hf == 0 && ((L == 0 && t >= kLead && a.nslot >= 3) || (L == 1 && t >= kGxRing));
-        unsigned* p2 = cnt + cnt_index(2, TT, e2 ? (t - (L == 0 ? kLead : kGxRing)) * NH + NH - 1 : 0, rep);
-        if constexpr (CW)
-          flag[4 + w] = wait3(p0, 2u * E, e0, p1, t1, e1, p2, target, e2, a, E,
-                              cnt + ccnt_index(a.nslot, hsl, T, e0 ? ht : 0, w * NCH + 1, rep, nck), 2u * E, e0) ? 1 : 0;
-        else
-          flag[4 + w] = wait3(p0, qtarget, e0, p1, t1, e1, p2, target, e2, a, E) ? 1 : 0;
+        const bool e2 = w == 1 && ((L == 0 && t >= kLead && a.nslot >= 3) || (L == 1 && t >= kGxRing));
+        unsigned* p2 = cnt + cnt_index(2, T, e2 ? t - (L == 0 ? kLead : kGxRing) : 0, rep);
+        flag[4 + w] = wait3(p0, qtarget, e0, p1, t1, e1, p2, target, e2, a, E) ? 1 : 0;
       }
       // the polled values are in (the loop compared them); nothing below moves above this point
-      // (GR / SN: no wait here -- it would drain the previous step's hand-off and output stores)
-      if constexpr (!GR && !SN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       AVC_PSTAMP(1);
       AVC_PRSTAMP(7);
-      if constexpr (!GR) AVC_PSTAMP(2);  // (GR: once the granules' tags match)
+      AVC_PSTAMP(2);
     } else {
     // Two lanes poll in parallel (lane 0 of waves 0 and 1): the data this step reads, and the
     // back-pressure that keeps slots 0 and 1 at most kLead / kGxRing steps ahead of slot 2 (a
     // slot running far ahead streams gx0 / writes h0 through the Infinity Cache and starves the
     // others: measured as a bistable 10 vs 20 us per step).  Each polling lane then acquires.
     // With slot 3 (nslot == 4) a third lane (wave 2) waits for this step's gx0.
-    // XL-local group (round 5): the previous step's h producers signal through one line of tags in
-    // this XCD's L2 (plain stores, sc1 loads; PersistArgs::xl) instead of the counter, polled by
-    // wave 0 (one load per poll covers all of them)
-    const bool xlf = xl_local && L == 0 && t > 0;
-    if (xlf && tid < 64) {
-      const unsigned want = E * (unsigned)(T + 1) + (unsigned)t;  // step t - 1's tag (see the publish)
-      const auto frs = __builtin_amdgcn_make_buffer_rsrc(a.xl_tab + 8 * a.ncb + grp * 32, 0, 128, 0x00020000);
-      auto ld = [&]() {
-        return lane < a.ncb ? __builtin_amdgcn_raw_buffer_load_b32(frs, lane * 4, 0, 16 /*sc1*/) : want;
-      };
-      bool ok = true;
-      unsigned v = ld();
-      for (unsigned spins = 0; __builtin_amdgcn_ballot_w64((int)(v - want) < 0) != 0ull; ++spins) {
-        if (spin_give_up(spins, a, E, lane)) {
-          ok = false;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        v = ld();
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-      if (lane == 0) flag[0] = ok ? 1 : 0;
-    }
     if (tid == 0 || tid == 64 || tid == 128) {
       const bool primary = tid == 0;
       long idx = -1;
       // the input slot runs ahead (up to kLead3 steps), so its progress is checked every 4th step
       // for 4 steps at once: its workgroups finish steps in order, so all of them counting in on
       // step t + 3 implies steps t .. t + 2 are complete (and drained) as well
-      if (tid == 128) idx = L == 0 && a.in_slot > 0 && (t & 3) == 0 ? cnt_index(a.in_slot, TT, min(t + 3, T - 1), rep) : -1;
-      else if (L == 0) idx = primary ? (t > 0 && !xlf ? cnt_index(0, TT, t - 1, rep) : -1)
-                                     : (t >= kLead && a.nslot >= 3 ? cnt_index(2, TT, t - kLead, rep) : -1);
-      else if (L == 1) idx = primary ? cnt_index(0, TT, t, rep)
-                                     : (t >= kGxRing ? cnt_index(2, TT, t - kGxRing, rep) : -1);
-      else idx = primary ? (t > 0 ? cnt_index(2, TT, t - 1, rep) : -1) : cnt_index(1, TT, t, rep);
+      if (tid == 128) idx = L == 0 && a.in_slot > 0 && (t & 3) == 0 ? cnt_index(a.in_slot, T, min(t + 3, T - 1), rep) : -1;
+      else if (L == 0) idx = primary ? (t > 0 ? cnt_index(0, T, t - 1, rep) : -1)
+                                     : (t >= kLead && a.nslot >= 3 ? cnt_index(2, T, t - kLead, rep) : -1);
+      else if (L == 1) idx = primary ? cnt_index(0, T, t, rep)
+                                     : (t >= kGxRing ? cnt_index(2, T, t - kGxRing, rep) : -1);
+      else idx = primary ? (t > 0 ? cnt_index(2, T, t - 1, rep) : -1) : cnt_index(1, T, t, rep);
       const bool ok = idx < 0 || wait_ge(cnt + idx, target, a, E);
       if (primary) {
         AVC_PSTAMP(1);
@@ -782,7 +602,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       } else {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
       }
-      if (!(primary && xlf)) flag[tid == 128 ? 3 : (primary ? 0 : 1)] = ok ? 1 : 0;
+      flag[tid == 128 ? 3 : (primary ? 0 : 1)] = ok ? 1 : 0;
     }
     __syncthreads();
     if (flag[0] == 0 || flag[1] == 0 || flag[3] == 0) break;
@@ -843,20 +663,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     for (int r = 0; r < RT; ++r)
 #pragma unroll
       for (int n = 0; n < NC; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const unsigned char* src;
-    if constexpr (SN) {  // this launch's set of the layer's [T] buffers
-      const unsigned char* cur = a.hsn + (long)(E & 1u) * a.hsn_set;
-      src = L == 0 ? (t > 0 ? cur + (long)(t - 1) * a.hsz : nullptr)
-                   : (L == 1 ? cur + (long)t * a.hsz : (t > 0 ? cur + a.hsn_layer + (long)(t - 1) * a.hsz : nullptr));
-    } else {
-      src = L == 0 ? (t > 0 ? a.hs0 + (long)(t - 1) * a.hsz : nullptr)
-                   : (L == 1 ? a.hs0 + (long)t * a.hsz : (t > 0 ? a.hs1 + (long)((t - 1) & 1) * a.hsz : nullptr));
-    }
-    if (GR ? t == 0 : src == nullptr) {  // (GR: h_{t-1} comes from the granule ring, hs0 is unused)
+    const unsigned char* src =
+        L == 0 ? (t > 0 ? a.hs0 + (long)(t - 1) * a.hsz : nullptr)
+               : (L == 1 ? a.hs0 + (long)t * a.hsz : (t > 0 ? a.hs1 + (long)((t - 1) & 1) * a.hsz : nullptr));
+    if (src == nullptr) {
       load_gx();
     } else {
       const int hrow16 = nck * 2048;
-      const long hbase = ((long)grp * NH + hf) * RT * hrow16 + (long)kc0 * 2048;
+      const long hbase = (long)grp * RT * hrow16 + (long)kc0 * 2048;
       const auto hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(src) + hbase, 0,
                                                          (int)((long)a.ntile * nck * 2048 - hbase), 0x00020000);
       // h chunk buffers: PDX chunks in flight ahead of the MFMAs.  With one 16-row tile (the
@@ -866,12 +680,14 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
       constexpr int NB = PDX + 1;
       f16x8 hb[NB][RT][2], wt[2];
 #ifdef AVC_STAMPS
-#define AVC_PLD_SKIP (a.diag & 4)  // timing experiment: no h loads (zeros)
+// timing experiments: diag 4 = no h loads (zeros); diag 8 = the second half of the wave's K chunks
+// not loaded (the per-CU h intake of a K split over two workgroups, priced without its fan-in hop)
+#define AVC_PLD_SKIP(C) ((a.diag & 4) || ((a.diag & 8) && (C) >= NCH / 2))
 #else
-#define AVC_PLD_SKIP false
+#define AVC_PLD_SKIP(C) false
 #endif
 #define AVC_PLD(HV, C)                                                                             \
-  if (AVC_PLD_SKIP) { _Pragma("unroll") for (int r = 0; r < RT; ++r) HV[r][0] = HV[r][1] = f16x8{}; } else \
+  if (AVC_PLD_SKIP(C)) { _Pragma("unroll") for (int r = 0; r < RT; ++r) HV[r][0] = HV[r][1] = f16x8{}; } else \
   _Pragma("unroll") for (int r = 0; r < RT; ++r) {                                                 \
     HV[r][0] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048, HO ? 16 : 0)); \
     HV[r][1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, r * hrow16 + (C) * 2048 + 1024, HO ? 16 : 0)); \
@@ -906,144 +722,18 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
     acc[r][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(HV[r][0], wt[0], acc[r][3], 0, 0, 0);      \
   }
 #endif
-      if constexpr (GR) {
-        // granules of step t - 1: this wave's K quarter (chunks kc0 ..) of every row tile,
-        // re-loaded until every tag is this step's (see gr_tag); gx0 goes out behind the first
-        // round (its producer was waited on above), so one vmcnt covers both
-        const unsigned tg = gr_tag(E, t - 1);
-        const auto grs = __builtin_amdgcn_make_buffer_rsrc(
-            a.hg + grp * a.hg_gstride + (long)((t - 1) % kGrRing) * a.hg_step, 0, (int)a.hg_step, 0x00020000);
-        const int gvo = kc0 * 4096 + lane * 16;
-        u32x4 gv[NCH][RT][4];
-        auto gload = [&]() {
-#pragma unroll
-          for (int c = 0; c < NCH; ++c)
-#pragma unroll
-            for (int r = 0; r < RT; ++r)
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                gv[c][r][j] = __builtin_amdgcn_raw_buffer_load_b128(grs, gvo, (r * nck + c) * 4096 + j * 1024, 16 /*sc1*/);
-        };
-        gload();
-        load_gx();
-        if (live) store_out(t - 1, pend_h, pend_c, pend_i, pend_f, pend_g, pend_o);
-        if (yfrag) yfrag_rows(t - 1, grp * MB);
-        bool good = true;
-        for (unsigned spins = 0;; ++spins) {
-          bool ok = true;
-#pragma unroll
-          for (int c = 0; c < NCH; ++c)
-#pragma unroll
-            for (int r = 0; r < RT; ++r)
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                ok = ok & ((gv[c][r][j][1] ^ gv[c][r][j][0]) == tg) & ((gv[c][r][j][3] ^ gv[c][r][j][2]) == tg);
-          if (__all(ok)) break;
-          if (spin_give_up(spins, a, E, lane)) {
-            good = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          gload();
-        }
-        if (!good && lane == 0) flag[4 + w] = 0;
-        AVC_PSTAMP(2);
-        // repack: granule 2j / 2j+1 of a lane -> element 2j / 2j+1 of the hi and lo f16x8
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          f16x8 hv8[RT][2];
-#pragma unroll
-          for (int r = 0; r < RT; ++r) {
-            u32x4 hi4, lo4;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const unsigned d0 = gv[c][r][j][0], d1 = gv[c][r][j][2];
-              hi4[j] = (d0 & 0xffffu) | (d1 << 16);
-              lo4[j] = (d0 >> 16) | (d1 & 0xffff0000u);
-            }
-            hv8[r][0] = __builtin_bit_cast(f16x8, hi4);
-            hv8[r][1] = __builtin_bit_cast(f16x8, lo4);
-          }
-          AVC_PMFMA(hv8, c)
-        }
-      } else {
-      bool sn_good = true;
-      if constexpr (SN) {
-        // every chunk issued at the step start would come back as the sentinel and cost one more
-        // round trip each (measured: +50 % per lstm2 step): probe chunk 0's first piece (1 KB per
-        // wave) until it is written, then start the pipeline; each chunk is still checked below
-        constexpr int hoff = 0;  // row tile 0, chunk 0, hi
-        u32x4 pr = __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, hoff, 16);
-        for (unsigned spins = 0; __builtin_amdgcn_ballot_w64((pr[0] == ~0u) | (pr[1] == ~0u) | (pr[2] == ~0u) | (pr[3] == ~0u)) != 0ull; ++spins) {
-          if (spin_give_up(spins, a, E, lane)) {
-            sn_good = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-          pr = __builtin_amdgcn_raw_buffer_load_b128(hrs, lane * 16, hoff, 16);
-        }
-      }
-      // CW: chunk c + 2's counter, polled one chunk ahead of its loads (lane 0; wave-uniform below)
-      unsigned* const cw_base = CW ? cnt + ccnt_index(a.nslot, L == 1 ? 0 : L, T, L == 1 ? t : t - 1, kc0, rep, nck) : nullptr;
-      unsigned cw_v = 0u;
-      bool cw_good = true;
-      auto cw_poll = [&](int c) {
-        if (lane == 0)
-          cw_v = __hip_atomic_load((gu32*)(cw_base + (long)c * kRep * kLine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      };
-      if constexpr (CW) {
-        AVC_PLD(hb[0], 0)
-        cw_poll(2);  // (issued before chunk 1's loads: waiting for it never waits for them)
-        AVC_PLD(hb[1], 1)
-      } else {
 #pragma unroll
       for (int c = 0; c < PDX && c < NCH; ++c) { AVC_PLD(hb[c], c) }
-      }
       if constexpr (NCH <= PDX) load_gx();
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         if (c + PDX < NCH) {
-          if constexpr (CW) {
-            // chunk c + 2's two producers: the poll issued one chunk ago has returned by now
-            const unsigned ct = 2u * E;
-            unsigned v = __builtin_amdgcn_readfirstlane(cw_v);
-            for (unsigned spins = 0; cw_good && (int)(v - ct) < 0; ++spins) {
-              if (spin_give_up(spins, a, E, lane)) {
-                cw_good = false;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-              cw_poll(c + 2);
-              v = __builtin_amdgcn_readfirstlane(cw_v);
-            }
-            if (c + 3 < NCH) cw_poll(c + 3);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering: loads stay below)
-          }
           AVC_PLD(hb[(c + PDX) % NB], c + PDX)
           if (c + PDX == NCH - 1) load_gx();
-        }
-        if constexpr (SN) {
-          // re-load chunk c until none of its dwords is the sentinel (a wave-uniform decision);
-          // the re-load is the youngest load, so waiting for it also covers the prefetches
-          for (unsigned spins = 0; sn_good && !sn_ready<RT>(hb[c % NB]); ++spins) {
-            if (spin_give_up(spins, a, E, lane)) {
-              sn_good = false;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            AVC_PLD(hb[c % NB], c)
-          }
         }
         __builtin_amdgcn_sched_barrier(0);
         AVC_PMFMA(hb[c % NB], c)
         __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (SN) {
-        if (!sn_good && lane == 0) flag[4 + w] = 0;  // acted on after the reduction barrier
-      }
-      if constexpr (CW) {
-        if (!cw_good && lane == 0) flag[4 + w] = 0;
-      }
       }
 #undef AVC_PMFMA
 #undef AVC_PLD
@@ -1060,7 +750,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) mine[(r * 16 + 4 * lq + e) * RP + n * 16 + l15] = acc[r][n][e];
     __syncthreads();
-    if constexpr (QW || GR || SN) {
+    if constexpr (QW) {
       if (flag[4] == 0 || flag[5] == 0 || flag[6] == 0 || flag[7] == 0) break;
     }
     fu hv, ig, fg, gg, og;
@@ -1073,7 +763,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = w * 16 + i * 4 + (lane >> 4);
-        if (r < MB && hf * MB + r < B) {
+        if (r < MB && r < B) {
           const int off = r * RP + 4 * pc;
           f32x4 v = *reinterpret_cast<const f32x4*>(part + off);
 #pragma unroll
@@ -1081,7 +771,7 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           const f32x4 wiv1 = *reinterpret_cast<const f32x4*>(cpar + 4 * pc);
           const f32x4 b1v = *reinterpret_cast<const f32x4*>(cpar + TW + 4 * pc);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v * wiv1 + b1v), ors,
-                                                 ((hf * MB + r) * TW + 4 * pc) * 4, 0, 16 /*sc1*/);
+                                                 (r * TW + 4 * pc) * 4, 0, 16 /*sc1*/);
         }
       }
     } else {
@@ -1122,29 +812,8 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
           }
         }
       }
-      if constexpr (GR) {
-        if (t + 1 < T) {
-          // stage the workgroup's [MB rows][16 units], then every thread stores RT granules: per
-          // (tile, j) one wave instruction writes 512 contiguous bytes (lanes 32(cb&1) .. +31 of
-          // chunk cb >> 1; layout at gr_tag), i.e. 4 whole lines
-#pragma unroll
-          for (int u = 0; u < UPT; ++u) hst[row * 16 + blk * 4 + u0 + u] = hl[u];
-          __syncthreads();
-          const unsigned tg = gr_tag(E, t);
-          const auto ors = __builtin_amdgcn_make_buffer_rsrc(
-              a.hg + grp * a.hg_gstride + (long)(t % kGrRing) * a.hg_step, 0, (int)a.hg_step, 0x00020000);
-          const int j = tid >> 6, lp = (tid & 63) >> 1, hh = tid & 1;
-          const int lu = 8 * (lp >> 4) + 2 * j + hh;
-#pragma unroll
-          for (int r = 0; r < RT; ++r) {
-            const unsigned hd = hst[(r * 16 + (lp & 15)) * 16 + lu];
-            const u32x2 gr = {hd, tg ^ hd};  // the tag word covers the data word (torn reads: gr_tag)
-            const int off = (((r * nck + (cb >> 1)) * 4 + j) * 64 + 32 * (cb & 1) + lp) * 16 + hh * 8;
-            __builtin_amdgcn_raw_buffer_store_b64(gr, ors, off, 0, 16 /*sc1*/);
-          }
-        }
-      } else if (t + 1 < T || L == 0) {
-        // the pair's 4 units go out as one 8-B hi and one 8-B lo store (whole fragment rows) from
+      if (t + 1 < T || L == 0) {
+        // the pair's 4 units go out as one 8-B hi and one 8-B lo piece (whole fragment rows) from
         // its first thread; the other SUB - 1 threads hand their units over by lane shuffles
         unsigned q[4];
 #pragma unroll
@@ -1153,111 +822,48 @@ __global__ __launch_bounds__(256, 1) void lstm_persist_kernel(PersistArgs a) {
         for (int k = 1; k < SUB; ++k)
 #pragma unroll
           for (int u = 0; u < UPT; ++u) q[k * UPT + u] = __shfl_down(hl[u], k);
-        u32x2 hi2 = {(q[0] & 0xffffu) | (q[1] << 16), (q[2] & 0xffffu) | (q[3] << 16)};
-        u32x2 lo2 = {(q[0] >> 16) | (q[1] & 0xffff0000u), (q[2] >> 16) | (q[3] & 0xffff0000u)};
-        if constexpr (SN) {
-          hi2 = u32x2{sn_word(hi2[0]), sn_word(hi2[1])};
-          lo2 = u32x2{sn_word(lo2[0]), sn_word(lo2[1])};
-        }
-        // 16-B pieces (avc_lstm_persist_st16, round 5): the pair leads of blocks 2m and 2m + 1 (lanes
-        // tid and tid ^ SUB, same row) hold the two halves of one 8-k fragment piece; the even one
-        // stores the hi piece, the odd one the lo piece (half the store instructions, each 16 B)
+        const u32x2 hi2 = {(q[0] & 0xffffu) | (q[1] << 16), (q[2] & 0xffffu) | (q[3] << 16)};
+        const u32x2 lo2 = {(q[0] >> 16) | (q[1] & 0xffff0000u), (q[2] >> 16) | (q[3] & 0xffff0000u)};
+        // 16-B pieces (round 5): the pair leads of blocks 2m and 2m + 1 (lanes tid and tid ^ SUB,
+        // same row) hold the two halves of one 8-k fragment piece; the even one stores the hi
+        // piece, the odd one the lo piece (half the store instructions, each 16 B)
         const bool odd = (blk & 1) != 0;
         const unsigned x0 = __shfl_xor(odd ? hi2[0] : lo2[0], SUB), x1 = __shfl_xor(odd ? hi2[1] : lo2[1], SUB);
-        // (SN: padding rows b >= B of the last tile are stored too, as zeros -- their consumers'
-        // chunks must not keep the sentinel; rows past the buffer fall outside its descriptor)
-        if ((live || SN) && sub == 0) {
+        if (live && sub == 0) {
           const long off = ((long)(b >> 4) * nck + (j0 >> 5)) * 2048 + (((b & 15) + 16 * ((j0 & 31) >> 3)) * 8 + (j0 & 7)) * 2;
           const u32x4 pc = odd ? u32x4{x0, x1, lo2[0], lo2[1]} : u32x4{hi2[0], hi2[1], x0, x1};
           const int off16 = (int)off + (odd ? 1024 - 8 : 0);  // the piece starts at the even lead's units
-          unsigned char* hb;
-          if constexpr (SN) hb = a.hsn + (L == 0 ? 0 : a.hsn_layer) + (long)t * a.hsz + (long)(E & 1u) * a.hsn_set;
-          else hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
+          unsigned char* const hb = L == 0 ? a.hs0 + (long)t * a.hsz : a.hs1 + (long)(t & 1) * a.hsz;
           const auto ors = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)a.hsz, 0x00020000);
-          if (xl_local) {  // (XL: the group's XCD keeps the lines in its L2; consumers load sc1 from it)
-            __builtin_amdgcn_raw_buffer_store_b128(pc, ors, off16, 0, 0);
-          } else if (a.st16) {
-            __builtin_amdgcn_raw_buffer_store_b128(pc, ors, off16, 0, 16 /*sc1*/);
-          } else {
-            __builtin_amdgcn_raw_buffer_store_b64(hi2, ors, (int)off, 0, 16 /*sc1*/);
-            __builtin_amdgcn_raw_buffer_store_b64(lo2, ors, (int)off + 1024, 0, 16 /*sc1*/);
-          }
-          if constexpr (SN) {
-            // the same bytes of the other set back to the sentinel (the next launch's set; nothing
-            // reads it during this one)
-            const auto rrs = __builtin_amdgcn_make_buffer_rsrc(hb + (long)(1 - 2 * (int)(E & 1u)) * a.hsn_set, 0,
-                                                               (int)a.hsz, 0x00020000);
-            const u32x2 sen = {~0u, ~0u};
-            __builtin_amdgcn_raw_buffer_store_b64(sen, rrs, (int)off, 0, 16 /*sc1*/);
-            __builtin_amdgcn_raw_buffer_store_b64(sen, rrs, (int)off + 1024, 0, 16 /*sc1*/);
-          }
+          __builtin_amdgcn_raw_buffer_store_b128(pc, ors, off16, 0, 16 /*sc1*/);
         }
       }
     }
-    if constexpr (GR) {
-      // no publish: the granules carry their own tags, and slot 0's counters are not used (a GR
-      // launch has a region of its own -- its size differs -- and no input-slot back-pressure).
-      // This step's outputs are stored next step, behind its granule loads: vmcnt retires in
-      // issue order, so stores issued here would hold those loads' data until they complete.
-      AVC_PSTAMP(5);
-      AVC_PRSTAMP(6);
-      if (L == 0) {
-        pend_h = hv; pend_c = cst; pend_i = ig; pend_f = fg; pend_g = gg; pend_o = og;
-      }
-      continue;
-    }
     // ---- publish: every storing wave drains, barrier, the workgroup counts itself in ------
-    // (SN: slot 0's h needs no counter and nobody waits on slot 0's counters, so it only keeps the
-    // barrier that orders this step's partial reads before the next step's partial writes)
-    const bool publish = !SN || L != 0;
-    if (publish) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     AVC_PSTAMP(5);
     AVC_PRSTAMP(6);
     // lanes 8..15 count in on this workgroup's quarter -- in both wait forms, so every launch adds
     // ncb / 4 to every quarter word and the epoch targets hold whichever form the next launch takes
-    if (xl_local && L == 0 && tid == 0)  // (XL: this workgroup's tag for step s, after every wave's drain)
-      __builtin_amdgcn_raw_buffer_store_b32(E * (unsigned)(T + 1) + (unsigned)s + 1u,
-                                            __builtin_amdgcn_make_buffer_rsrc(a.xl_tab + 8 * a.ncb + grp * 32, 0, 128,
-                                                                              0x00020000),
-                                            cb * 4, 0, 0);
-    if (publish && tid < (CW && (L == 0 || L == 2) ? 3 : 2) * kRep) {
-      const long ci = tid < kRep       ? cnt_index(L, TT, s, tid)
-                      : tid < 2 * kRep ? qcnt_index(a.nslot, L, TT, s, cb / (a.ncb / kQuarters), tid - kRep)
-                                       : ccnt_index(a.nslot, L, T, s, cb >> 1, tid - 2 * kRep, nck);  // (CW: h's chunk)
+    if (tid < 2 * kRep) {
+      const long ci = tid < kRep ? cnt_index(L, T, t, tid)
+                                 : qcnt_index(a.nslot, L, T, t, cb / (a.ncb / kQuarters), tid - kRep);
       __hip_atomic_fetch_add((gu32*)(cnt + ci), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // outputs nobody reads inside this launch: stored after publishing (off the hand-off path);
     // the publish barrier above orders every thread's yst writes before yfrag_rows reads them
     if (L != 1 && live) store_out(t, hv, cst, ig, fg, gg, og);
-    if (yfrag) yfrag_rows(t, row0 - row + hf * MB);
-    if constexpr (NH > 1) {  // the other half's cell state becomes the current one
-      const fu tmp = cst;
-      cst = cst_other;
-      cst_other = tmp;
-    }
-  }
-  const int t = NH == 1 ? s : s / NH;  // the step the loop stopped at (T: completed)
-  if constexpr (GR) {
-    if (t == T && T > 0 && live) store_out(T - 1, pend_h, pend_c, pend_i, pend_f, pend_g, pend_o);
-    if (t == T && T > 0 && yfrag) {  // (the last step staged yst without the granules' barrier)
-      __syncthreads();
-      yfrag_rows(T - 1, grp * MB);
-    }
+    if (yfrag) yfrag_rows(t, grp * MB);
   }
   // gave up at step t: the rows this workgroup owns for steps t..T-1 are written as NaN, so a
   // timed-out launch never hands plausible numbers downstream (the host reports it, see above) --
-  // through every output, the split image included.  The granule form stores a step's outputs
-  // one step late, so its step t - 1 is written as NaN as well.
-  if (t < T && L != 1) {
+  // through every output, the split image included
+  if (t < T && L != 1 && live) {
     fu nv;
 #pragma unroll
     for (int u = 0; u < UPT; ++u) nv[u] = __builtin_nanf("");
-    for (int h2 = 0; h2 < NH; ++h2) {  // every half's rows (NH = 2: from the step that gave up)
-      b = row0 + h2 * MB;
-      if (b < B)
-        for (int tt = GR && t > 0 ? t - 1 : t; tt < T; ++tt) store_out(tt, nv, nv, nv, nv, nv, nv, true);
-    }
+    for (int tt = t; tt < T; ++tt) store_out(tt, nv, nv, nv, nv, nv, nv, true);
   }
 }
 
@@ -1326,90 +932,15 @@ int lstm1_rows_per_group(int B, int H) {
 size_t persist_lds(int H, int RT) {
   const int nch = H / 32 / 4;
   return (size_t)4 * nch * 2048 + (size_t)4 * 16 * RT * 68 * sizeof(float) + 32 + 2 * 64 * sizeof(float) +
-         (size_t)2 * 16 * RT * 16 * sizeof(unsigned);  // hst + yst
+         (size_t)16 * RT * 16 * sizeof(unsigned);  // yst
 }
 
-// Does a one-layer launch of (H, RT) hand split h over as granules under the current tuning?
-// One 16-row tile per group only: a granule carries 4 B of tag per 4 B of h, and what a step costs
-// tracks the bytes each consumer wave ingests (MI355X_MICROARCH.md, handoff-payload).  Measured:
-// C5 lstm1 (RT 1) 2930 -> 2862 us, C2 lstm1 (RT 1) unchanged, C3 lstm1 (RT 2) 542 -> 721 us.
-bool persist_gran(int H, int RT) {
-  return g_persist_gran && H == 512 && RT == 1 && g_persist_mode == 2 && g_persist_pd >= 2 && !(g_persist_qwait & 2);
-}
-
-// avc_lstm_persist_xcd(): XCD-local groups in the one-layer form (PersistArgs::xl), off by default:
-// against the build without them (same box) lstm1 was 1 % faster at C2 and 3 % slower at C5
-int g_persist_xl = 0;
-int g_xl_remote = 0;  // avc_debug_xl_force_remote(): test the not-local fallback of the XCD-local forms
-
-// avc_lstm_persist_sentinel(): sentinel hand-off of split h (SN), bit 0 = two-layer form, bit 1 =
-// one-layer form
-int g_persist_sn = 0;
-extern int g_persist_halves;
-// Does a launch of this form take the sentinel hand-off under the current tuning?
-bool persist_sn(bool two_layer) {
-  return (g_persist_sn & (two_layer ? 1 : 2)) && g_persist_mode == 2 && g_persist_pd >= 2 && !g_persist_halves &&
-         (two_layer || !g_persist_gran);
-}
-
-int g_persist_halves = 0;  // avc_lstm_persist_halves(): the two-layer form walks two batch halves
-                           // (measured slower: C2 lstm2 1062 -> 1335 us, C5 6120 -> 8090 us)
-
-// Batch halves (lstm_persist_kernel's NH) a launch of (RT 16-row tiles) takes under the current
-// tuning: 2 for the two-layer form in its default hand-off with at least two tiles, else 1.
-int persist_nh(int RT, bool two_layer) {
-  return two_layer && RT >= 2 && g_persist_halves && (g_persist_qwait & 1) && g_persist_mode == 2 &&
-                 g_persist_pd >= 2
-             ? 2
-             : 1;
-}
-
-// avc_lstm_persist_chunkwait(): per-chunk waits in the two-layer form (CW; ccnt_index)
-int g_persist_cw = 0;
-// Does a launch of (RT 16-row tiles) take the per-chunk waits under the current tuning?  The
-// two-layer form in its quarter-wait hand-off with PD 2 and at least two row tiles (RT 1 requests
-// every chunk at once, so there is nothing to start early).
-bool persist_cw(int RT, bool two_layer) {
-  return g_persist_cw && two_layer && RT >= 2 && (g_persist_qwait & 1) && g_persist_mode == 2 && g_persist_pd == 2 &&
-         !persist_sn(true) && persist_nh(RT, true) == 1;
-}
+int g_xl_remote = 0;  // avc_debug_xl_force_remote(): test the not-local fallback of the XCD-local BPTT
 
 // The template instance a launch of (H, RT) runs under the current tuning.
-const void* persist_fn(int H, int RT, bool two_layer = true, bool xl = false) {
+const void* persist_fn(int H, int RT, bool two_layer = true) {
   const bool qw = (g_persist_qwait & (two_layer ? 1 : 2)) != 0;
   const int nch = H / 32 / 4;
-  if (xl)  // (persist_xl_ok: the one-layer form's default hand-off at H = 512)
-    return RT == 1 ? (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 0, 1, 0, 0, 1>
-         : RT == 2 ? (const void*)lstm_persist_kernel<4, 2, 1, 2, 0, 0, 1, 0, 0, 1>
-                   : (const void*)lstm_persist_kernel<4, 4, 1, 2, 0, 0, 1, 0, 0, 1>;
-  if (persist_cw(RT, two_layer)) {
-    if (nch == 8)
-      return RT == 2 ? (const void*)lstm_persist_kernel<8, 2, 1, 2, 1, 0, 1, 0, 1>
-                     : (const void*)lstm_persist_kernel<8, 4, 1, 2, 1, 0, 1, 0, 1>;
-    return RT == 2 ? (const void*)lstm_persist_kernel<4, 2, 1, 2, 1, 0, 1, 0, 1>
-                   : (const void*)lstm_persist_kernel<4, 4, 1, 2, 1, 0, 1, 0, 1>;
-  }
-  if (!two_layer && persist_gran(H, RT)) return (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 1>;
-  if (persist_sn(two_layer)) {
-    if (nch == 8)
-      return RT == 1 ? (const void*)lstm_persist_kernel<8, 1, 1, 2, 0, 0, 1, 1>
-           : RT == 2 ? (const void*)lstm_persist_kernel<8, 2, 1, 2, 0, 0, 1, 1>
-                     : (const void*)lstm_persist_kernel<8, 4, 1, 2, 0, 0, 1, 1>;
-    return RT == 1 ? (const void*)lstm_persist_kernel<4, 1, 1, 2, 0, 0, 1, 1>
-         : RT == 2 ? (const void*)lstm_persist_kernel<4, 2, 1, 2, 0, 0, 1, 1>
-                   : (const void*)lstm_persist_kernel<4, 4, 1, 2, 0, 0, 1, 1>;
-  }
-  if (persist_nh(RT, two_layer) == 2) {  // RT / 2 tiles per half
-    // a half's h chunks are half as large, so depth 3 / 4 keeps the bytes in flight of depth 2
-    // at RT rows (avc_lstm_persist_depth; the RT = 1 halves already take every chunk at once)
-    if (nch == 8 && RT > 2)
-      return g_persist_pd == 4   ? (const void*)lstm_persist_kernel<8, 2, 1, 4, 1, 0, 2>
-             : g_persist_pd == 3 ? (const void*)lstm_persist_kernel<8, 2, 1, 3, 1, 0, 2>
-                                 : (const void*)lstm_persist_kernel<8, 2, 1, 2, 1, 0, 2>;
-    if (nch == 8) return (const void*)lstm_persist_kernel<8, 1, 1, 2, 1, 0, 2>;
-    return RT == 2 ? (const void*)lstm_persist_kernel<4, 1, 1, 2, 1, 0, 2>
-                   : (const void*)lstm_persist_kernel<4, 2, 1, 2, 1, 0, 2>;
-  }
 #define AVC_PERSIST_FN(NCHV, RTV)                                                                 \
   return g_persist_mode == 1 ? (const void*)lstm_persist_kernel<NCHV, RTV, 0, 1, 0>               \
        : g_persist_pd == 1   ? (const void*)lstm_persist_kernel<NCHV, RTV, 1, 1, 0>               \
@@ -1425,10 +956,10 @@ const void* persist_fn(int H, int RT, bool two_layer = true, bool xl = false) {
 
 // Workgroups of instance (H, RT) the device can hold at once: the occupancy API's resident
 // workgroups per CU (LDS, VGPRs, waves) x CUs.  Cached per instance.
-int persist_capacity(int H, int RT, bool two_layer = true, bool xl = false) {
+int persist_capacity(int H, int RT, bool two_layer = true) {
   struct Entry { const void* fn; int dev; int cap; };
   static std::vector<Entry> cache;
-  const void* fn = persist_fn(H, RT, two_layer, xl);
+  const void* fn = persist_fn(H, RT, two_layer);
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   for (const auto& e : cache)
@@ -1444,7 +975,6 @@ int persist_capacity(int H, int RT, bool two_layer = true, bool xl = false) {
 }
 
 int g_persist_coop = 0;          // avc_lstm_persist_coop()
-int g_persist_st16 = 1;          // avc_lstm_persist_st16()
 int g_persist_inject = 0;        // avc_debug_persist_inject(): launches left that give up at once
 unsigned g_spin_limit = kSpinLimit;  // avc_debug_persist_spin_limit()
 
@@ -1530,8 +1060,8 @@ int persist_dispatch(avc_context* ctx, const void* fn, dim3 grid, dim3 block, vo
 
 // Launch: grid (nslot * ncb, ngrp); co-residency was checked by the eligibility test.
 int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_t s) {
-  const dim3 grid = a.xl ? dim3(8 * a.ncb, 1) : dim3(a.nslot * a.ncb, ngrp);
-  a.nwg = a.xl ? a.xl_slots * a.ncb : (int)(grid.x * grid.y);
+  const dim3 grid(a.nslot * a.ncb, ngrp);
+  a.nwg = (int)(grid.x * grid.y);
   for (int L = 0; L < a.nslot; ++L)
     AVC_CHECK_ARG(a.W[L] && a.winv[L], "persistent recurrence: a slot's split weights are missing");
   AVC_CHECK_ARG(a.in_slot == 0 || (a.in_slot == a.nslot - 1 && a.xs && a.b0 && a.gx0 && (a.din == 384 || a.din == 512)),
@@ -1541,8 +1071,7 @@ int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_
     --g_persist_inject;
     a.spin_limit = 0;
   }
-  a.st16 = g_persist_st16;
-  const void* fn = persist_fn(a.H, RT, a.nslot >= 3, a.xl != 0);
+  const void* fn = persist_fn(a.H, RT, a.nslot >= 3);
   void* args[] = {&a};
   return persist_dispatch(ctx, fn, grid, dim3(256), args, persist_lds(a.H, RT), s);
 }
@@ -1552,7 +1081,7 @@ int persist_launch(avc_context* ctx, PersistArgs a, int RT, int ngrp, hipStream_
 // retired (freed when the context is destroyed: a captured graph may still reference them).
 constexpr int kMaxRegions = 32;
 int persist_region(avc_context* ctx, int kind, int T, int ngrp, int ncb, int nwg, size_t counter_words,
-                   hipStream_t s, unsigned** out, size_t sentinel_from = ~size_t(0)) {
+                   hipStream_t s, unsigned** out) {
   const size_t bytes = (kRegionHeaderWords + counter_words) * sizeof(unsigned);
   for (auto& r : ctx->regions) {
     if (r.kind == kind && r.T == T && r.ngrp == ngrp && r.ncb == ncb && r.nwg == nwg && r.bytes == bytes) {
@@ -1576,10 +1105,6 @@ int persist_region(avc_context* ctx, int kind, int T, int ngrp, int ncb, int nwg
   void* mem = nullptr;
   AVC_HIP(hipMalloc(&mem, bytes));
   AVC_TRY(zero_async(mem, bytes, s));
-  if (sentinel_from < counter_words) {  // (the SN h buffers: every byte 0xFF, see lstm_persist_kernel)
-    const size_t off = (kRegionHeaderWords + sentinel_from) * sizeof(unsigned);
-    AVC_TRY(fill_async(static_cast<unsigned char*>(mem) + off, bytes - off, ~0u, s));
-  }
   avc_persist_region r;
   r.kind = kind; r.T = T; r.ngrp = ngrp; r.ncb = ncb; r.nwg = nwg; r.bytes = bytes; r.mem = mem;
   r.last_use = ++ctx->region_clock;
@@ -2489,49 +2014,14 @@ int lstm1_persist_forward(avc_context* ctx, int T, int B, int H, float* gx, cons
   const int RT = lstm1_rows_per_group(B, H), ngrp = (B + 16 * RT - 1) / (16 * RT);
   const int nslot = ip ? 2 : 1;
   const long gstride = cnt_words(nslot, T, true);  // counter words per group: full + quarter lines
-  // granule hand-off: a kGrRing-step ring per group behind the counters (zeroed with them; the
-  // tags make stale entries harmless, see gr_tag)
-  const bool gran = persist_gran(H, RT);
-  const bool sn = !gran && persist_sn(false);
-  const long hg_step = (long)RT * (H / 32) * 4096;
   const size_t cwords = ((size_t)ngrp * gstride + 63) & ~size_t(63);
-  const size_t gwords = gran ? (size_t)ngrp * kGrRing * hg_step / sizeof(unsigned)
-                             : (sn ? (size_t)2 * T * hsz / sizeof(unsigned) : 0);  // SN: two h sets [2][T][hsz]
-  // XL (PersistArgs::xl): the recurrent groups dealt one per XCD, the XCD table behind the rest
-  const int ncb = 4 * H / 64;
-  const bool xl = g_persist_xl && !gran && !sn && ncb == 32 && ngrp * nslot <= 8 && device_cus() == 256 &&
-                  g_persist_mode == 2 && g_persist_pd == 2 && !(g_persist_qwait & 2) &&
-                  persist_capacity(H, RT, false, true) >= 8 * ncb;  // (the linear grid: 8 x ncb resident)
-  const size_t xwords = xl ? (size_t)8 * ncb + 8 * 32 : 0;  // the XCD table, then a tag line per group
-  unsigned char* hs0 = nullptr;
-  if (!gran && !sn) {
-    hs0 = sc.template take<unsigned char>((size_t)T * hsz);
-    if (hs0 == nullptr) return AVC_ERR_WORKSPACE;
-  }
+  AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), cwords + gwords + xwords, s,
-                         &region, sn ? cwords : ~size_t(0)));
+  AVC_TRY(persist_region(ctx, 1, T, ngrp, 4 * H / 64, nslot * ngrp * (4 * H / 64), cwords, s, &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = nslot; a.cnt_gstride = gstride;
-  if (gran) {
-    a.hg = reinterpret_cast<unsigned char*>(region + kRegionHeaderWords + cwords);
-    a.hg_step = hg_step;
-    a.hg_gstride = kGrRing * hg_step;
-  }
-  if (sn) {
-    a.hsn = reinterpret_cast<unsigned char*>(region + kRegionHeaderWords + cwords);
-    a.hsn_set = (long)T * hsz;
-    a.hsn_layer = 0;
-  }
-  if (xl) {
-    a.xl = 1;
-    a.xl_remote = g_xl_remote;
-    a.xl_slots = ngrp * nslot;
-    a.xl_tab = region + kRegionHeaderWords + cwords + gwords;
-  }
   if (ip) AVC_TRY(attach_inproj(ctx, sc, *ip, T, B, 1, a, s));
-  if (gran || sn) a.in_lead = 1;  // (back-pressure polls slot 0's counters, which GR / SN launches do not add to)
   a.W[0] = reinterpret_cast<const unsigned char*>(whh_s);
   a.winv[0] = winv;
   a.gx0 = gx;
@@ -2585,38 +2075,20 @@ int lstm2_persist_forward(avc_context* ctx, int T, int B, int H, float* gx0,
   Scratch sc(ctx);
   const int ntile = (B + 15) / 16;
   const long hsz = (long)ntile * 16 * H * 2 * 2;  // bytes per split-h step buffer
-  const bool sn = persist_sn(true);
-  unsigned char* hs0 = nullptr;
-  unsigned char* hs1 = nullptr;
-  if (!sn) {  // (SN: the h buffers live in the region, two sets per layer)
-    AVC_TAKE(h0b, unsigned char, (size_t)T * hsz, sc);
-    AVC_TAKE(h1b, unsigned char, (size_t)2 * hsz, sc);                    // ring of 2
-    hs0 = h0b;
-    hs1 = h1b;
-  }
+  AVC_TAKE(hs0, unsigned char, (size_t)T * hsz, sc);
+  AVC_TAKE(hs1, unsigned char, (size_t)2 * hsz, sc);                      // ring of 2
   AVC_TAKE(gx1, float, (size_t)kGxRing * (4 * H / 64) * 64 * 64, sc);     // slab ring
   const int nslot = ip ? 4 : 3;
   const int RT = ntile <= 1 ? 1 : (ntile <= 2 ? 2 : 4);
-  const int NH = persist_nh(RT, true);
-  // counters [nslot][T * NH][kRep] (one 128-B line each, per time step and batch half) and the
-  // quarter counters in the persistent region of this layout; SN: then the h sets [2][2][T][hsz]
-  // (CW: then the chunk counters, [3][T][H / 32][kRep] lines; ccnt_index)
-  const size_t cwords = ((size_t)cnt_words(nslot, T * NH, true) +
-                         (persist_cw(RT, true) ? (size_t)3 * T * (H / 32) * kRep * kLine : 0) + 63) & ~size_t(63);
-  const size_t hwords = sn ? (size_t)2 * 2 * T * hsz / sizeof(unsigned) : 0;
+  // counters [nslot][T][kRep] (one 128-B line each) and the quarter counters in the persistent
+  // region of this layout
+  const size_t cwords = ((size_t)cnt_words(nslot, T, true) + 63) & ~size_t(63);
   unsigned* region = nullptr;
-  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), cwords + hwords, s, &region,
-                         sn ? cwords : ~size_t(0)));
+  AVC_TRY(persist_region(ctx, 2, T, 1, 4 * H / 64, nslot * (4 * H / 64), cwords, s, &region));
   PersistArgs a{};
   a.B = B; a.T = T; a.H = H; a.ncb = 4 * H / 64; a.ntile = ntile;
   a.nslot = nslot; a.cnt_gstride = 0;
-  if (sn) {
-    a.hsn = reinterpret_cast<unsigned char*>(region + kRegionHeaderWords + cwords);
-    a.hsn_set = (long)T * hsz;
-    a.hsn_layer = 2L * T * hsz;
-  }
   if (ip) AVC_TRY(attach_inproj(ctx, sc, *ip, T, B, 3, a, s));
-  if (sn) a.in_lead = 1;  // (input-slot back-pressure polls slot 0's counters, which an SN launch does not add to)
   a.W[0] = reinterpret_cast<const unsigned char*>(w0_s);
   a.W[1] = reinterpret_cast<const unsigned char*>(w1i_s);
   a.W[2] = reinterpret_cast<const unsigned char*>(w1h_s);
@@ -2832,8 +2304,8 @@ extern "C" int avc_lstm_persist_tune(int mode) {
 }
 
 extern "C" int avc_lstm_persist_depth(int chunks) {
-  if (chunks < 1 || chunks > 4) {
-    avc::set_error("avc_lstm_persist_depth: chunks must be 1..4 (3 and 4 apply to the batch-halves form only)");
+  if (chunks < 1 || chunks > 2) {
+    avc::set_error("avc_lstm_persist_depth: chunks must be 1 or 2");
     return AVC_ERR_INVALID;
   }
   avc::g_persist_pd = chunks;
@@ -2861,73 +2333,13 @@ extern "C" int avc_lstm_persist_qwait(int mask) {
   return AVC_OK;
 }
 
-extern "C" int avc_lstm_persist_st16(int on) {
-  if (on != 0 && on != 1) {
-    avc::set_error("avc_lstm_persist_st16: 0 or 1");
-    return AVC_ERR_INVALID;
-  }
-  avc::g_persist_st16 = on;
-  ++avc::g_config_epoch;
-  return AVC_OK;
-}
-
 extern "C" int avc_debug_xl_census(unsigned* local_nonlocal) {
-  // (test hook) copies and clears the XL census: recurrent workgroups that found their group local
-  // / not local since the last call
+  // (test hook) copies and clears the XCD-local BPTT census: workgroups that found their group
+  // local / not local since the last call
   void* p = nullptr;
   if (hipGetSymbolAddress(&p, HIP_SYMBOL(avc::g_xl_seen)) != hipSuccess) return AVC_ERR_HIP;
   if (hipMemcpy(local_nonlocal, p, 2 * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return AVC_ERR_HIP;
   if (hipMemset(p, 0, 2 * sizeof(unsigned)) != hipSuccess) return AVC_ERR_HIP;
-  return AVC_OK;
-}
-
-extern "C" int avc_lstm_persist_xcd(int on) {
-  if (on != 0 && on != 1) {
-    avc::set_error("avc_lstm_persist_xcd: 0 or 1");
-    return AVC_ERR_INVALID;
-  }
-  avc::g_persist_xl = on;
-  ++avc::g_config_epoch;
-  return AVC_OK;
-}
-
-extern "C" int avc_lstm_persist_chunkwait(int on) {
-  if (on != 0 && on != 1) {
-    avc::set_error("avc_lstm_persist_chunkwait: 0 or 1");
-    return AVC_ERR_INVALID;
-  }
-  avc::g_persist_cw = on;
-  ++avc::g_config_epoch;
-  return AVC_OK;
-}
-
-extern "C" int avc_lstm_persist_sentinel(int mask) {
-  if (mask < 0 || mask > 3) {
-    avc::set_error("avc_lstm_persist_sentinel: mask must be 0..3");
-    return AVC_ERR_INVALID;
-  }
-  avc::g_persist_sn = mask;
-  ++avc::g_config_epoch;
-  return AVC_OK;
-}
-
-extern "C" int avc_lstm_persist_granules(int on) {
-  if (on != 0 && on != 1) {
-    avc::set_error("avc_lstm_persist_granules: 0 or 1");
-    return AVC_ERR_INVALID;
-  }
-  avc::g_persist_gran = on;
-  ++avc::g_config_epoch;
-  return AVC_OK;
-}
-
-extern "C" int avc_lstm_persist_halves(int on) {
-  if (on != 0 && on != 1) {
-    avc::set_error("avc_lstm_persist_halves: 0 or 1");
-    return AVC_ERR_INVALID;
-  }
-  avc::g_persist_halves = on;
-  ++avc::g_config_epoch;
   return AVC_OK;
 }
 

@@ -7,8 +7,9 @@ the same seeded weights and input:
   -> post -- that local error carried to mel_post through the float64 downstream stages: what the
              stage's own rounding costs at the output the 1e-4 bar is stated on;
   chain   -- the full chain's error at the stage output (GPU per-layer path, fp32 reference).
-Usage: python scripts/error_budget.py [seed B T] (defaults 2 1 128: the worst B = 1 margin case of
-profiles/r04_margin.json).  Prints a table; writes gpurun_out/error_budget_s{seed}_B{B}_T{T}.json."""
+Usage: python scripts/error_budget.py [seed B T [xseed]] (defaults 2 1 128: the worst B = 1 margin case of
+profiles/r04_margin.json; xseed = the input mel's seed, default 1; tests/test_gpu_margin.py's small
+cases use 5 + seed).  Prints a table; writes gpurun_out/error_budget_s{seed}_B{B}_T{T}.json."""
 import json
 import os
 import sys
@@ -25,6 +26,7 @@ from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_d
 from oracle import autovc_oracle as orc  # noqa: E402
 
 seed, B, T = (int(v) for v in sys.argv[1:4]) if len(sys.argv) > 3 else (2, 1, 128)
+xseed = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 dev = torch.device("cuda:0")
 torch.set_num_threads(min(16, os.cpu_count() or 1))
 sd32 = torch_state_dict(seed)
@@ -32,7 +34,7 @@ sd64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in sd32
 ae = AutoEncoder(device=dev, verbose=False)
 ae.load_state_dict(sd32)
 ae.to(dev).train()
-x_np, co_np, ct_np = synthetic_mel(1, B, T), synthetic_embedding(101, B), synthetic_embedding(201, B)
+x_np, co_np, ct_np = synthetic_mel(xseed, B, T), synthetic_embedding(101, B), synthetic_embedding(201, B)
 
 
 # frames [T*B][C] (time-major, the HIP layout) <-> (B, T, C) / (B, C, T)
@@ -178,5 +180,5 @@ summ = {"gpu_fused_vs_f64_mel_post": mx(fused[1], post64), "gpu_per_layer_vs_f64
         "gpu_fused_vs_per_layer_mel_post": mx(fused[1], g[LAST])}
 print(json.dumps(summ, indent=1))
 os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-with open(os.path.join(REPO, "gpurun_out", f"error_budget_s{seed}_B{B}_T{T}.json"), "w") as fh:
-    json.dump({"seed": seed, "B": B, "T": T, "rows": rows, "summary": summ}, fh, indent=1)
+with open(os.path.join(REPO, "gpurun_out", f"error_budget_s{seed}_B{B}_T{T}_x{xseed}.json"), "w") as fh:
+    json.dump({"seed": seed, "xseed": xseed, "B": B, "T": T, "rows": rows, "summary": summ}, fh, indent=1)

@@ -1,6 +1,6 @@
 """N C2 forwards (B = 64, T = 128, whole-Generator fused path, graph replay) under the library hook
 settings in argv[1] ("hook=value,hook=value" or "-"), for PMC passes of one configuration:
-rocprofv3 --pmc FETCH_SIZE -- python3 scripts/fwd_hooks.py avc_lstm_persist_granules=0 5"""
+rocprofv3 --pmc FETCH_SIZE -- python3 scripts/fwd_hooks.py avc_lstm_persist_qwait=0 5"""
 import sys
 
 sys.path.insert(0, __file__.rsplit("/", 2)[0])

@@ -17,10 +17,6 @@ for step in "$@"; do
   case $step in
     persist) run persist 300 python -u -m pytest tests/test_gpu_model.py -x -v -s -k persistent --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     bnf)   run bnf 300 python -u -m pytest tests/test_gpu_bnfuse.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider ;;
-    halves) run halves 300 python -u -m pytest tests/test_gpu_halves.py tests/test_gpu_model.py -k "halves or persistent or back_to_back or c5" -x -v --timeout 150 --timeout-method thread -p no:cacheprovider ;;
-    halvesab) run halvesab 300 python scripts/persist_hook_ab.py avc_lstm_persist_halves 0 1 0 1 0 1 ;;
-    deadab) run deadab 300 python scripts/persist_hook_ab.py avc_dead_h_stores 0 1 0 1 0 1 ;;
-    gran)  run gran 300 python -u -m pytest tests/test_gpu_granules.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     safety) run safety 300 python -u -m pytest tests/test_gpu_persist_safety.py tests/test_gpu_coresidency.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kern)  run kern 600 python -m pytest tests/test_gpu_kernels.py -v -m gpu -x --timeout 120 -p no:cacheprovider ;;
@@ -68,10 +64,7 @@ for step in "$@"; do
     bnfab) run bnfab 300 python scripts/persist_hook_ab.py avc_bn_fuse 1 2 1 2 1 2 ;;
     bnftrain) run bnftrain 400 python scripts/train_hook_ab.py avc_bn_fuse 1 2 ;;
     ebudget) run ebudget 400 python scripts/error_budget.py 2 1 128 && run ebudget0 400 python scripts/error_budget.py 0 1 128 && run ebudget64 600 python scripts/error_budget.py 0 64 128 ;;
-    hpd) run hpd 400 python scripts/persist_cfg_ab.py "avc_lstm_persist_halves=0,avc_lstm_persist_depth=2" "avc_lstm_persist_halves=1,avc_lstm_persist_depth=2" "avc_lstm_persist_halves=1,avc_lstm_persist_depth=3" "avc_lstm_persist_halves=1,avc_lstm_persist_depth=4" ;;
     rccl) run rccl 400 python -u -m pytest tests/test_gpu_rccl.py -x -v -s --timeout 600 -p no:cacheprovider ;;
-    pmcgran) for g in 0 1; do run pmcgranF$g 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcgranF$g -o fwd -- python3 scripts/fwd_hooks.py avc_lstm_persist_granules=$g 4 && run pmcgranW$g 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcgranW$g -o fwd -- python3 scripts/fwd_hooks.py avc_lstm_persist_granules=$g 4; done ;;
-    granab) run granab 300 python scripts/persist_cfg_ab.py "avc_lstm_persist_granules=1" "avc_lstm_persist_granules=0" ;;
     bnbwd) run bnbwd 400 python -u -m pytest tests/test_gpu_bnbwd.py tests/test_gpu_kernels.py -x -v -s --timeout 200 -p no:cacheprovider ;;
     bnbwdab) run bnbwdab 400 python scripts/train_hook_ab.py avc_bn_bwd_frag 0 1 ;;
     prodcurve) run prodcurve 500 python -u -m pytest tests/test_gpu_production.py tests/test_gpu_curve.py -x -v -s --timeout 300 -p no:cacheprovider ;;
@@ -85,37 +78,29 @@ for step in "$@"; do
     dpprod) run dpprod 600 python -u -m pytest tests/test_gpu_dp.py tests/test_gpu_production.py -x -v -s --timeout 400 -p no:cacheprovider ;;
     fragchain) rm -f gpurun_out/abe.log && run fragchain 600 bash scripts/ab_env.sh AUTOVC_FRAG_CHAIN 0 1 ;;
     r5a) run r5a 900 python -u -m pytest tests/test_gpu_bnfuse.py tests/test_gpu_bnbwd.py tests/test_gpu_wavernn_persist.py tests/test_gpu_persist_safety.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    deadh) run deadh 300 python -u -m pytest tests/test_gpu_dead_h.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     margin) run margin 900 python -u -m pytest tests/test_gpu_margin.py -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     abr4) run abr4 700 bash scripts/ab_c2.sh ab/prev_r04.so ;;
     abr4t) run abr4t 700 bash scripts/ab_train.sh ab/prev_r04.so ;;
-    sn) run sn 600 python -u -m pytest tests/test_gpu_sentinel.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
-    snab) run snab 400 python scripts/persist_cfg_ab.py "avc_lstm_persist_sentinel=0" "avc_lstm_persist_sentinel=3" "avc_lstm_persist_sentinel=1" "avc_lstm_persist_sentinel=2" ;;
-    stamps1) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stamps1c2 200 python scripts/stamps_lstm1.py sentinel=2 && AVC_STAMPS_BT=32,1024 run stamps1c5 300 python scripts/stamps_lstm1.py sentinel=2 ;;
-    stamps2) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stamps2 300 python scripts/stamps_persist.py && run stamps2sn 300 python scripts/stamps_persist.py sn ;;
     bandab) run bandab 400 python scripts/persist_hook_ab.py avc_bn_fuse_band 0 1 0 1 0 1 ;;
     pmcband) for g in 0 1; do run pmcbandF$g 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcbandF$g -o fwd -- python3 scripts/fwd_hooks.py avc_bn_fuse_band=$g 4 && run pmcbandW$g 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcbandW$g -o fwd -- python3 scripts/fwd_hooks.py avc_bn_fuse_band=$g 4; done ;;
-    cw) run cw 300 python -u -m pytest tests/test_gpu_sentinel.py tests/test_gpu_unit_bound.py -v -s -k "chunk or unit" --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     fix5) run fix5 600 python -u -m pytest tests/test_gpu_bnfuse.py tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_bnbwd.py tests/test_gpu_production.py tests/test_gpu_curve.py -x -v -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     l32diag) run l32test 200 python -u -m pytest tests/test_gpu_lstm32.py -v -x --timeout 100 --timeout-method thread -p no:cacheprovider && run l32diag 200 python scripts/lstm32_diag.py ;;
     dualw) run dualw 300 python -u -m pytest tests/test_gpu_dgsplit.py -v -x --timeout 100 --timeout-method thread -p no:cacheprovider && run dualwab 400 python scripts/train_hook_ab.py avc_dg_dual_wide 0 1 ;;
-    xl) run xl 400 python -u -m pytest tests/test_gpu_xcd_local.py -v -x -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
-    xlab) run xlab 400 python scripts/persist_hook_ab.py avc_lstm_persist_xcd 0 1 0 1 0 1 ;;
     bxl) run bxl 400 python -u -m pytest tests/test_gpu_bptt_xl.py -v -x -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     bxlsuite) run bxlsuite 700 python -u -m pytest tests/test_gpu_bptt_coalesce.py tests/test_gpu_persist_safety.py tests/test_gpu_production.py tests/test_gpu_curve.py tests/test_gpu_dp.py tests/test_gpu_model.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     bxstamps) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run bxstamps 200 python scripts/stamps_bptt_xl.py ;;
     bxtime) run bxtime 300 python scripts/bptt_xl_ab.py 0 1 ;;
-    stampsxl) export AVC_STAMPS_LIB=stampslib/libautovc_hip_stamps.so && run stampsxl2 200 python scripts/stamps_lstm1.py && AVC_STAMPS_BT=32,1024 run stampsxl5 300 python scripts/stamps_lstm1.py ;;
-    longxl) run longxl 400 python scripts/long_hook_ab.py avc_lstm_persist_xcd 0 1 ;;
-    abpre) rm -f gpurun_out/abpre_*.log && run abpre 900 bash scripts/ab_prexl.sh ;;
-    xltrain) run xltrain 500 python scripts/train_hook_ab.py avc_lstm_persist_xcd 0 1 ;;
     abheadt) run abheadt 600 bash scripts/ab_lib_train.sh ab/prev_head.so ;;
     bptts) run bptts 400 python -u -m pytest tests/test_gpu_bptt_coalesce.py tests/test_gpu_bptt_xl.py tests/test_gpu_persist_safety.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
-    xlfb) run xlfb 400 python -u -m pytest tests/test_gpu_bptt_xl.py tests/test_gpu_xcd_local.py -v -x -s --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     bxlab) run bxlab 500 python scripts/train_hook_ab.py avc_bptt_xcd 0 1 ;;
     abtree) run abtree 1000 bash scripts/ab_r04_tree.sh ;;
     roundsab) run roundsab 500 python scripts/train_hook_ab.py avc_gemm_plan_rounds 0 1 ;;
-    cwab) run cwab 400 python scripts/persist_hook_ab.py avc_lstm_persist_chunkwait 0 1 0 1 0 1 ;;
-    st16ab) run st16ab 400 python scripts/persist_hook_ab.py avc_lstm_persist_st16 0 1 0 1 0 1 ;;
+    adam) run adam 300 python -u -m pytest tests/test_gpu_persist_safety.py tests/test_gpu_kernels.py -k "skip or adam" -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    marginsmall) run marginsmall 900 python -u -m pytest tests/test_gpu_margin.py -k small -v -s --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    eb1) run eb1a 400 python scripts/error_budget.py 1 1 128 6 && run eb1b 400 python scripts/error_budget.py 1 2 64 6 ;;
+    kprice) export AVC_STAMPS_LIB=diag6/libautovc_hip_stamps.so && run kprice0 200 python scripts/stamps_persist.py 2 0 && run kprice4 200 python scripts/stamps_persist.py 2 4 && run kprice8 200 python scripts/stamps_persist.py 2 8 && run kprice0b 200 python scripts/stamps_persist.py 2 0 ;;
+    ab5) run ab5 900 bash scripts/ab_r05.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,5 +1,5 @@
 """A/B of persistent-recurrence configurations, each a comma list of hook=value settings (argv[1:],
-e.g. "avc_lstm_persist_halves=0" "avc_lstm_persist_halves=1,avc_lstm_persist_depth=4"): the fused
+e.g. "avc_lstm_persist_qwait=1" "avc_lstm_persist_qwait=0,avc_lstm_persist_depth=1"): the fused
 forward at C2 (B=64, T=128) and at C5's shape (B=32, T=1024), configurations alternated 3 times in
 one process; ms per forward (graph replay), per-launch lstm2 / lstm1 times from the library's
 timing events, and a bit-identity check against the first configuration."""

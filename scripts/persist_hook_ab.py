@@ -1,4 +1,4 @@
-"""A/B of one persistent-recurrence tuning hook (argv[1], e.g. avc_lstm_persist_halves; values argv[2:]): fused forward at C2
+"""A/B of one persistent-recurrence tuning hook (argv[1], e.g. avc_lstm_persist_qwait; values argv[2:]): fused forward at C2
 (B=64, T=128) and at a C5-like shape (B=32, T=1024), alternating 0 / 1 in one process; ms per
 forward (graph replay, 20 reps), per-kernel times from the library's timing events, and a
 bit-identity check of the outputs against the first run."""

@@ -31,7 +31,7 @@ with torch.no_grad():
     ae(x, c, c)
 torch.cuda.synchronize()
 buf = torch.zeros(NWG * T * 8, dtype=torch.int64, device=dev)
-names = ["poll wait", "acquire+barrier (GR: granule wait)", "mfma loop", "lds reduce", "epilogue+drain"]
+names = ["poll wait", "acquire+barrier", "mfma loop", "lds reduce", "epilogue+drain"]
 
 
 def measure(label):
@@ -52,8 +52,8 @@ def measure(label):
 
 
 measure("default")
-# further measurements after each tuning call: "granules=0" -> avc_lstm_persist_granules(0),
-# "sentinel=2" -> avc_lstm_persist_sentinel(2); a bare integer is an avc_lstm_persist_qwait mask
+# further measurements after each tuning call: "depth=1" -> avc_lstm_persist_depth(1); a bare
+# integer is an avc_lstm_persist_qwait mask
 for arg in sys.argv[1:]:
     name, val = arg.split("=") if "=" in arg else ("qwait", arg)
     _lib.call(f"avc_lstm_persist_{name}", int(val))

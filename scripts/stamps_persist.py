@@ -20,9 +20,7 @@ from autovc_amd.weights import synthetic_embedding, synthetic_mel, torch_state_d
 
 B, T, NCB = 64, 128, 64
 lib = _lib.load()
-if len(sys.argv) > 1 and sys.argv[1] == "sn":  # the sentinel hand-off of split h (round 5)
-    _lib.call("avc_lstm_persist_sentinel", 1)
-elif len(sys.argv) > 1:
+if len(sys.argv) > 1:
     _lib.call("avc_lstm_persist_tune", int(sys.argv[1]))
 if len(sys.argv) > 2:  # diagnostic bits (timing experiments; outputs not meaningful)
     lib.avc_debug_persist_diag.argtypes = [ctypes.c_int]

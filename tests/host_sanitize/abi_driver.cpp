@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/autovc_hip.h"
+#include "../../include/autovc_hip_debug.h"
 
 static int failures = 0;
 #define CHECK(cond)                                                             \
@@ -48,13 +49,14 @@ static void host_only() {
   // tuning hooks: valid values accepted, invalid ones rejected with a message
   CHECK(avc_gemm_config(12) == AVC_ERR_INVALID);
   CHECK(avc_gemm_config(8) == AVC_OK);
-  CHECK(avc_lstm_persist_granules(2) == AVC_ERR_INVALID);
-  CHECK(avc_lstm_persist_granules(1) == AVC_OK);
+  CHECK(avc_lstm_persist_qwait(4) == AVC_ERR_INVALID);
+  CHECK(avc_lstm_persist_qwait(1) == AVC_OK);
   CHECK(avc_lstm_tune(17, 0) == AVC_ERR_INVALID);
   CHECK(avc_lstm_tune(0, 0) == AVC_OK);
   CHECK(avc_lstm_persist_tune(3) == AVC_ERR_INVALID);
   CHECK(avc_lstm_persist_tune(2) == AVC_OK);
   CHECK(avc_lstm_persist_depth(0) == AVC_ERR_INVALID);
+  CHECK(avc_lstm_persist_depth(3) == AVC_ERR_INVALID);
   CHECK(avc_lstm_persist_layers(4) == AVC_ERR_INVALID);
   CHECK(avc_debug_persist_inject(-1) == AVC_ERR_INVALID);
   // timing bookkeeping (host vectors)

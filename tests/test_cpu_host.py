@@ -13,19 +13,21 @@ from autovc_amd.weights import param_specs, torch_state_dict
 from tests.conftest import REPO, load_golden
 
 
-def header_symbols():
-    h = open(os.path.join(REPO, "include", "autovc_hip.h")).read()
+def header_symbols(name="autovc_hip.h"):
+    h = open(os.path.join(REPO, "include", name)).read()
     h = re.sub(r"/\*.*?\*/", "", h, flags=re.S)
     return sorted(set(re.findall(r"\b(avc_\w+)\s*\(", h)))
 
 
 def test_library_exports_every_header_symbol():
     lib = _lib.load()
-    syms = header_symbols()
-    assert len(syms) >= 25
+    product, debug = header_symbols(), header_symbols("autovc_hip_debug.h")
+    assert len(product) >= 25
+    assert not set(product) & set(debug), "a symbol is declared as product and as debug"
+    syms = sorted(product + debug)
     for s in syms:
         assert hasattr(lib, s), s
-    # and the ctypes table binds exactly the header's functions
+    # and the ctypes table binds exactly the two headers' functions
     assert sorted(_lib.exported_symbols()) == syms
     assert lib.avc_abi_version() == 1
     assert lib.avc_generator_param_count() == 96

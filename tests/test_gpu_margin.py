@@ -10,8 +10,8 @@ For each set three distances are reported on mel / mel_post / codes:
   * the fp32 reference itself vs float64.
 The reference's own distance from exact arithmetic is part of every GPU-vs-reference number (the
 train-mode postnet BNs amplify input noise ~60x), so the GPU-vs-float64 column is what
-says how good the HIP arithmetic is.  The test writes gpurun_out/r05_margin.json (copied to
-profiles/r05_margin.json)."""
+says how good the HIP arithmetic is.  The test writes gpurun_out/r06_margin.json (copied to
+profiles/r06_margin.json)."""
 import json
 import os
 
@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 
 TOL_MEL = 1e-4
 B, T = 64, 128
-OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "r05_margin.json")
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "r06_margin.json")
 
 
 def _scaled(sd, f):
@@ -68,8 +68,10 @@ def _weights(dev, name):
     return _trained(dev)
 
 
-def _margin(dev, results, key, sd, B, T, xseed=1):
-    """GPU forward vs the oracle in fp32 and float64 (see the module docstring); records and checks."""
+def _margin(dev, results, key, sd, B, T, xseed=1, strict=False):
+    """GPU forward vs the oracle in fp32 and float64 (see the module docstring); records and checks.
+    strict: the 1e-4 bar is asserted whatever the reference's own distance from float64 (the
+    batches convert() runs, VERDICT r5 weak #1)."""
     from oracle import autovc_oracle as orc
     torch.set_num_threads(min(16, torch.get_num_threads()))
     x = synthetic_mel(xseed, B, T)
@@ -109,7 +111,7 @@ def _margin(dev, results, key, sd, B, T, xseed=1):
         # the bar is NOT met (GPU - ref 2.5e-3 / 1.6e-4), and only the line above is checked: the GPU
         # is closer to float64 than the reference there, so the distance is the reference's own
         # rounding, which an implementation with a different summation order cannot reproduce.
-        if r["ref_vs_f64"] < TOL_MEL / 2:
+        if strict or r["ref_vs_f64"] < TOL_MEL / 2:
             assert r["gpu_vs_ref"] <= TOL_MEL, (k, r)
     return rec
 
@@ -123,7 +125,7 @@ SMALL += [(s, 1, t) for t in (1024, 2000) for s in (0, 1, 2)]
 
 @pytest.mark.parametrize("seed,B,T", SMALL, ids=[f"seed{s}_B{b}_T{t}" for s, b, t in SMALL])
 def test_small_batch_margin(cuda_device, results, seed, B, T):
-    _margin(cuda_device, results, f"seed{seed}_B{B}_T{T}", torch_state_dict(seed), B, T, xseed=5 + seed)
+    _margin(cuda_device, results, f"seed{seed}_B{B}_T{T}", torch_state_dict(seed), B, T, xseed=5 + seed, strict=True)
 
 
 @pytest.mark.parametrize("name", WEIGHT_SETS)

@@ -153,6 +153,82 @@ def test_skipped_update_does_not_count_as_a_step(cuda_device):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("runs", [(3, 9, 2), (1, 12, 3, 10, 1)])
+def test_many_skipped_updates_keep_adams_step(cuda_device, runs):
+    """Runs of consecutive non-finite steps with no settle (state_dict) in between, longer than the
+    8-entry host table of bias corrections: the device skip count
+    reaches 9..13, and every finite update after it must use Adam's bias correction of the updates
+    actually applied.  runs = (finite, skipped, finite, ...): compared with torch.optim.Adam +
+    clip_grad_norm_ + the EMA fed only the finite steps, and the step count after a settle."""
+    n = 50_021
+    torch.manual_seed(11)
+    p0 = torch.randn(n)
+    pr = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([pr], lr=1e-3, betas=(0.9, 0.999), eps=1e-8)
+    ema_ref = p0.clone()
+    p = p0.clone().to(cuda_device)
+    m = torch.zeros(n, device=cuda_device)
+    v = torch.zeros(n, device=cuda_device)
+    ema = p.clone()
+    skips = torch.zeros(1, dtype=torch.int32, device=cuda_device)
+    norm = torch.empty((), device=cuda_device)
+    calls = applied = 0
+    for i, cnt in enumerate(runs):
+        for _ in range(cnt):
+            g = torch.randn(n) * 1e-2
+            gd = g.to(cuda_device)
+            if i % 2:
+                gd[101] = float("nan")
+            else:
+                pr.grad = g.clone()
+                torch.nn.utils.clip_grad_norm_([pr], max_norm=1.0)
+                opt.step()
+                ema_ref = 0.9999 * ema_ref + (1 - 0.9999) * pr.detach()
+                applied += 1
+            calls += 1
+            _lib.call("avc_clip_adam_ema_dev", _lib.context(cuda_device), n, p.data_ptr(), gd.data_ptr(),
+                      m.data_ptr(), v.data_ptr(), ema.data_ptr(), 1e-3, 0.9, 0.999, 1e-8, 0.0, calls, 1.0, 0.9999,
+                      norm.data_ptr(), skips.data_ptr(), _lib.stream(cuda_device))
+    torch.cuda.synchronize()
+    assert calls - int(skips.item()) == applied
+    assert (p.cpu() - pr.detach()).abs().max().item() < 2e-7 * max(1.0, pr.abs().max().item())
+    assert (ema.cpu() - ema_ref).abs().max().item() < 4e-7 * max(1.0, ema_ref.abs().max().item())
+    # the moments carry the clip coefficient c (fp64 norm here; torch's fp32 norm of 5e4 squares
+    # is ~1e-5 relative off), m ~ c and v ~ c^2, while the update m / sqrt(v) cancels c -- hence the
+    # tight bound on the parameters above and a c-sized one here.  (The bias corrections this test
+    # is about enter the parameters only.)
+    st = opt.state[pr]
+    for got, ref in ((m.cpu(), st["exp_avg"]), (v.cpu(), st["exp_avg_sq"])):
+        assert ((got - ref).abs() <= 1e-4 * ref.abs() + 1e-12 * ref.abs().max()).all()
+
+
+def test_fused_adam_settles_after_many_skips(cuda_device):
+    """FusedAdam (the module path): 10 NaN steps between finite ones, then state_dict(): the same
+    parameters, moments, EMA and step count as the finite steps alone."""
+    res = []
+    for with_nan in (False, True):
+        ae = _model(cuda_device)
+        ae.configure_optimizer()
+        gen = torch.Generator().manual_seed(5)
+        gs = [torch.randn(ae._flat_grad.shape, generator=gen).to(cuda_device) * 1e-3 for _ in range(3)]
+        for k, g in enumerate(gs):
+            if with_nan and k > 0:
+                for _ in range(10):
+                    ae._flat_grad.copy_(g)
+                    ae._flat_grad[4242] = float("inf")
+                    ae.optimiser.step(max_norm=1.0, ema=ae.avg_params)
+            ae._flat_grad.copy_(g)
+            ae.optimiser.step(max_norm=1.0, ema=ae.avg_params)
+        torch.cuda.synchronize()
+        st = ae.optimiser.state_dict()
+        res.append(([t.detach().clone() for t in (ae._flat_param, ae.optimiser.exp_avg, ae.optimiser.exp_avg_sq,
+                                                 ae.avg_params)], float(st["state"][0]["step"])))
+    (ref, ref_step), (got, got_step) = res
+    assert ref_step == got_step == 3.0
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
 def test_cooperative_launch_matches(cuda_device):
     """avc_lstm_persist_coop(1): the same kernels under hipLaunchCooperativeKernel (runtime
     co-residency guarantee), eager and graph-replayed, bit-identical to the default launch."""
