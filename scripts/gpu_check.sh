@@ -101,6 +101,10 @@ for step in "$@"; do
     eb1) run eb1a 400 python scripts/error_budget.py 1 1 128 6 && run eb1b 400 python scripts/error_budget.py 1 2 64 6 ;;
     kprice) export AVC_STAMPS_LIB=diag6/libautovc_hip_stamps.so && run kprice0 200 python scripts/stamps_persist.py 2 0 && run kprice4 200 python scripts/stamps_persist.py 2 4 && run kprice8 200 python scripts/stamps_persist.py 2 8 && run kprice0b 200 python scripts/stamps_persist.py 2 0 ;;
     ab5) run ab5 900 bash scripts/ab_r05.sh ;;
+    hostgpu) run hostgpu 200 python scripts/host_vs_gpu.py ;;
+    ab6at) run ab6at 600 bash scripts/ab_lib_train.sh ab/r06a.so ;;
+    psafe) run psafe 600 python -u -m pytest tests/test_gpu_persist_safety.py tests/test_gpu_model.py tests/test_gpu_bptt_xl.py tests/test_gpu_bptt_coalesce.py tests/test_gpu_coresidency.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
+    ab6a) run ab6a 900 bash scripts/ab_r05.sh ab/r06a.so ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -199,7 +199,7 @@ def test_many_skipped_updates_keep_adams_step(cuda_device, runs):
     # is about enter the parameters only.)
     st = opt.state[pr]
     for got, ref in ((m.cpu(), st["exp_avg"]), (v.cpu(), st["exp_avg_sq"])):
-        assert ((got - ref).abs() <= 1e-4 * ref.abs() + 1e-12 * ref.abs().max()).all()
+        assert ((got - ref).abs() <= 1e-4 * ref.abs() + 1e-5 * ref.abs().max()).all()
 
 
 def test_fused_adam_settles_after_many_skips(cuda_device):
