@@ -27,6 +27,9 @@ constexpr int BK = 32;
 #ifndef AVC_GEMM_DIAG_NOBAR
 #define AVC_GEMM_DIAG_NOBAR 0  // diagnostic (wrong results): gemm16f skips its per-K-tile barrier
 #endif
+#ifndef AVC_GEMM_DIAG_NOMFMA
+#define AVC_GEMM_DIAG_NOMFMA 0  // diagnostic (wrong results): gemm16f skips its MFMAs (loads, reads, barriers kept)
+#endif
 #ifndef AVC_GEMM_DIAG_NOKAHAN
 #define AVC_GEMM_DIAG_NOKAHAN 0  // diagnostic: gemm16f folds 128-k partials with a plain add
 #endif
@@ -1236,6 +1239,13 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
       // MFMAs and every pass waits on lgkmcnt(0) again
       __builtin_amdgcn_sched_barrier(0);
       const int cb = s & 1;
+      if (AVC_GEMM_DIAG_NOMFMA) {  // (diagnostic: the fragments stay live, no MFMA)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            crs[i][j][0] += (float)fah[cb][i][0] + (float)fal[cb][i][1] + (float)fbh[cb][j][2] + (float)fbl[cb][j][3];
+      } else {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1252,6 +1262,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[cb][i], fbh[cb][j], crs[i][j], 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
 #undef AVC16F_FRAGS
@@ -1344,6 +1355,363 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   }
   if (d.stats)
     bn_tile_stats<BM, BN, WM, WTN, TM, TN, BM == 256 ? 2 : 1, false, false>(
+        d, acc, biasv, reinterpret_cast<float*>(lds), tm, tn, wm, wn, lane, tid, NT, row_base, col_base);
+}
+
+// ---- warp-specialized split-f16 GEMM ("gemm16w", round 6; avc_gemm_config 12) ---------------
+// gemm16f<128, 128, 4, 2, 2, 4> with its LDS-DMA taken off the computing waves.  Measured on the
+// default kernel (`scripts/gemm_diag_ab.sh`): the C2 conv takes 83 us, 54 us without
+// its LDS-DMA and 59 us without its MFMAs -- the loads and the MFMAs overlap by only half, because
+// every wave both issues its K-tile's DMA and multiplies, one barrier per K-tile and one K-tile in
+// flight (two 64 KB stages fill the LDS).  Here a workgroup of 12 waves splits the roles:
+//  * waves 0-7 (consumers) own exactly gemm16f's 4 x 2 layout of 32 x 64 output tiles and run its
+//    MFMA sequence (per 16-deep chunk hi.hi, hi.lo, lo.hi; the hi.hi partials folded into the sum
+//    after every 128 k, at the same K-tile boundaries): the same bits as configuration 8;
+//  * waves 8-11 (loaders) stream the operands by LDS-DMA into a ring of NS slots, each half a
+//    64-deep K-tile (32 KB: 16 A + 16 B pieces of 1 KiB), up to three slots ahead of the consumers.
+// Hand-shake through LDS words (MI355X_MICROARCH.md, ring-gemm): a loader publishes FULL[slot][l]
+// = use + 1 once its own 8 pieces of that slot have landed (counted vmcnt), a consumer reads a slot
+// once all four FULL words are there and returns it with FREE[slot][w] = use + 1 as soon as its
+// fragments are in registers; a loader refills a slot only when all eight FREE words are.  The
+// consumers never wait on a DMA they issued, the loaders never wait on an MFMA: no barrier in the
+// K loop.  The loaders end after the K loop (a terminated wave no longer takes part in s_barrier);
+// the consumers run gemm16f's epilogues (bias / act / stats, split-K slabs, fused BatchNorm) as
+// threads 0..511.
+// Every ring wait is bounded (kRingSpins polls, ~0.1 s: a healthy wait is microseconds), so a
+// protocol fault can only produce wrong numbers, never a workgroup that does not finish.
+constexpr unsigned kRingSpins = 1u << 21;
+// The loader waves' own LDS accesses (the FREE polls, the FULL stores) are inline asm: hipcc
+// orders every compiler-visible LDS access of a wave behind that wave's pending LDS-DMA with an
+// s_waitcnt vmcnt(0), which would drain the loader's ring at every hand-shake (cdna_hip_programming.md
+// §5.7, "LDS-DMA issued beside the loader's own LDS accesses").  The words are plain LDS words;
+// ds ops of one wave complete in order, and the load's wait is inside its statement.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ unsigned lds_load_now(unsigned a) {
+  unsigned v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_store_asm(unsigned a, unsigned v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+template <int BNF>
+__global__ __launch_bounds__(768, 3) void gemm16w_kernel(GemmDesc d, Frag16Args f, int tilesM, int tilesN,
+                                                        int kt_per_tap, int kps, int nsplit,
+                                                        float* __restrict__ slab) {
+  constexpr int BM = 128, BN = 128, WM = 4, WN = 2, KC = 4;  // KC: 16-deep chunks per K-tile (the plan's unit)
+  constexpr int NT = 64 * WM * WN, NWAVE = WM * WN;          // consumers
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+  constexpr int HKC = KC / 2;                                // chunks per ring slot (half a K-tile)
+  constexpr int ABLK = (BM / 32) * HKC * 2, BBLK = (BN / 32) * HKC * 2, NBLK = ABLK + BBLK;
+  constexpr int SLOT = NBLK * 1024;
+  constexpr int NS = 4;                                      // ring slots
+  constexpr int NL = 4, DPL = NBLK / NL;                     // loader waves, pieces per loader per slot
+  static_assert(DPL * NL == NBLK && ABLK % DPL == 0, "a loader's pieces are all A or all B");
+  static_assert(!BNF || 18432 + BM * (BN + 4) * 4 <= NS * SLOT, "fused BN: the tile does not fit the ring's LDS");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned* full = reinterpret_cast<unsigned*>(lds + NS * SLOT);  // [NS][NL]
+  unsigned* freew = full + NS * NL;                                // [NS][NWAVE]
+
+  unsigned long long bnf_ticket = 0;
+  if constexpr (BNF) {
+    if (d.bnf.training && threadIdx.x == 0)
+      bnf_ticket = __hip_atomic_fetch_add(d.bnf.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwg = tilesM * tilesN;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+  int tm, tn;
+  if constexpr (BNF) {  // (gemm16f_kernel: the column-tile barrier group and the XCD row bands)
+    tn = bid / tilesM;
+    const int l = bid - tn * tilesM;
+    tm = (!d.bnf.band || (tilesM & 7)) ? l : (l & 7) * (tilesM >> 3) + (l >> 3);
+    (void)wgid;
+  } else {
+    tile_of(wgid, tilesM, tilesN, tm, tn);
+  }
+  const int split = blockIdx.y % nsplit, z = blockIdx.y / nsplit;
+  const int ktotal = d.ntaps * kt_per_tap;
+  const int kt0 = split * kps;
+  const int kt1 = min(ktotal, kt0 + kps);
+  const int nh = 2 * max(0, kt1 - kt0);  // ring slots' worth of work: half K-tiles
+
+  if (tid < NS * (NL + NWAVE)) full[tid] = 0u;  // (FULL and FREE words are contiguous)
+  __syncthreads();
+
+  if (w >= NWAVE) {
+    // ================================ loader wave ================================
+    const int l = w - NWAVE;
+    const auto ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.As), 0,
+                                                       f.a_ntile * f.a_nkc * 2048, 0x00020000);
+    const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.Bs), 0,
+                                                       (int)(d.ntaps * f.b_tapstride * 2), 0x00020000);
+    constexpr unsigned kOut = 0x7FFFFF00u;  // past num_records: the DMA lands zeros
+    const int a_ntile = f.a_ntile, a_nkc = f.a_nkc, b_ntile = f.b_ntile, b_nkc = f.b_nkc;
+    const long a_shift0 = f.a_shift0, a_tapshift = f.a_tapshift, b_tapstride = f.b_tapstride;
+    const int bzs = f.b_shift0_c + z * f.b_zshift_c;
+    const bool is_a = l * DPL < ABLK;
+    // per tap: each piece's VGPR offset without its chunk (the chunk goes in the SGPR offset;
+    // gemm16f's fast issue), re-formed when the tap changes
+    unsigned voff[DPL];
+    int vtau = -1;
+    auto set_tap = [&](int tau) {
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) {
+        const int b = l * DPL + i;
+        if (is_a) {
+          const int rt = b / (2 * HKC), kc = (b >> 1) % HKC, hl = b & 1;
+          const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)tau * a_tapshift) / 32;
+          voff[i] = src_tile >= 0 && src_tile < a_ntile
+                        ? (unsigned)(((src_tile * a_nkc + kc) * 2 + hl) * 1024) + lane * 16 : kOut;
+        } else {
+          const int bb = b - ABLK;
+          const int ct = bb / (2 * HKC), kc = (bb >> 1) % HKC, hl = bb & 1;
+          const int src_tile = tn * (BN / 32) + ct;
+          voff[i] = src_tile < b_ntile
+                        ? (unsigned)(tau * b_tapstride * 2 + ((long)(src_tile * b_nkc + kc) * 2 + hl) * 1024) + lane * 16
+                        : kOut;
+        }
+      }
+      vtau = tau;
+    };
+    auto issue = [&](int h) {
+      const int KT = kt0 + (h >> 1);
+      const int tau = KT / kt_per_tap;
+      const int kc0 = (KT - tau * kt_per_tap) * KC + (h & 1) * HKC;  // first 16-deep chunk of the slot
+      unsigned char* const base = lds + (h % NS) * SLOT;
+      const bool inside = is_a ? kc0 + HKC <= a_nkc : (kc0 + bzs >= 0 && kc0 + HKC + bzs <= b_nkc);
+      if (inside) {
+        if (tau != vtau) set_tap(tau);
+        const int so = (is_a ? kc0 : kc0 + bzs) * 2048;
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) {
+          unsigned char* dst = base + (l * DPL + i) * 1024;
+          const unsigned vo = voff[i];
+          if (AVC_GEMM_NOLOAD) {
+          } else if (is_a)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)dst, 16, vo, so, 0, 0);
+          else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16, vo, so, 0, 0);
+        }
+      } else {  // a slot that runs past K (padding chunks): per-piece range checks
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) {
+          const int b = l * DPL + i;
+          unsigned char* dst = base + b * 1024;
+          if (is_a) {
+            const int rt = b / (2 * HKC), kc = (b >> 1) % HKC, hl = b & 1;
+            const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)tau * a_tapshift) / 32;
+            const bool ok = src_tile >= 0 && src_tile < a_ntile && kc0 + kc < a_nkc;
+            const unsigned off = ok ? (unsigned)(((src_tile * a_nkc + kc0 + kc) * 2 + hl) * 1024) : kOut;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)dst, 16,
+                                                     off + lane * 16, 0, 0, 0);
+          } else {
+            const int bb = b - ABLK;
+            const int ct = bb / (2 * HKC), kc = (bb >> 1) % HKC, hl = bb & 1;
+            const int src_tile = tn * (BN / 32) + ct;
+            const int bkc = kc0 + kc + bzs;
+            const bool ok = src_tile < b_ntile && bkc >= 0 && bkc < b_nkc;
+            const unsigned off = ok ? (unsigned)(tau * b_tapstride * 2 + ((long)(src_tile * b_nkc + bkc) * 2 + hl) * 1024)
+                                    : kOut;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16,
+                                                     off + lane * 16, 0, 0, 0);
+          }
+        }
+      }
+    };
+    const unsigned full_l = lds_addr(full + l);
+    auto publish = [&](int h) {  // this loader's pieces of slot h have landed (the caller waited)
+      if (lane == 0) lds_store_asm(full_l + (h % NS) * NL * 4, (unsigned)(h / NS + 1));
+    };
+    for (int h = 0; h < nh; ++h) {
+      if (h >= NS) {  // the slot's previous use: every consumer has its fragments in registers
+        const unsigned want = (unsigned)(h / NS);
+        // lanes 0..7 each watch one consumer's FREE word of the slot
+        const unsigned fa = lds_addr(freew + (h % NS) * NWAVE + (lane & 7));
+        for (unsigned spins = 0;; ++spins) {
+          const bool done = __builtin_amdgcn_ballot_w64(lane < NWAVE && lds_load_now(fa) < want) == 0ull;
+          if (done || spins >= kRingSpins) break;  // (bounded: a healthy wait is microseconds)
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      issue(h);
+      if (h >= 2) {  // two slots stay in flight: the one issued two iterations ago has landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPL) : "memory");
+        publish(h - 2);
+      }
+    }
+    if (nh >= 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPL) : "memory");
+      publish(nh - 2);
+    }
+    if (nh >= 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      publish(nh - 1);
+    }
+    return;
+  }
+
+  // ================================ consumer waves ================================
+  const int wm = w / WN, wn = w % WN;
+  f32x16 zero16;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) zero16[e] = 0.f;
+  f32x16 acc[TM][TN], part[TM][TN], crs[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = part[i][j] = crs[i][j] = zero16;
+  f16x8 fah[2][TM], fal[2][TM], fbh[2][TN], fbl[2][TN];
+  for (int h = 0; h < nh; ++h) {
+    const int st = h % NS;
+    {  // every loader's pieces of this slot have landed
+      const unsigned want = (unsigned)(h / NS + 1);
+      const unsigned* fl = full + st * NL;
+      for (unsigned spins = 0;; ++spins) {
+        bool done = true;
+#pragma unroll
+        for (int c = 0; c < NL; ++c)
+          done &= __hip_atomic_load(fl + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want;
+        if (done || spins >= kRingSpins) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const unsigned char* Ai = lds + st * SLOT;
+    const unsigned char* Bi = Ai + ABLK * 1024;
+#define AVC16W_FRAGS(S, BUF)                                                                      \
+    _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                              \
+      const unsigned char* p = Ai + (((wm * TM + i) * HKC + (S)) * 2) * 1024 + lane * 16;         \
+      fah[BUF][i] = *reinterpret_cast<const f16x8*>(p);                                           \
+      fal[BUF][i] = *reinterpret_cast<const f16x8*>(p + 1024);                                    \
+    }                                                                                             \
+    _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                              \
+      const unsigned char* p = Bi + (((wn * TN + j) * HKC + (S)) * 2) * 1024 + lane * 16;         \
+      fbh[BUF][j] = *reinterpret_cast<const f16x8*>(p);                                           \
+      fbl[BUF][j] = *reinterpret_cast<const f16x8*>(p + 1024);                                    \
+    }
+    AVC16W_FRAGS(0, 0)
+#pragma unroll
+    for (int s = 0; s < HKC; ++s) {
+      if (s + 1 < HKC) { AVC16W_FRAGS(s + 1, (s + 1) & 1) }
+      if (s + 1 == HKC) {  // every fragment of the slot is in registers: hand the slot back
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store(freew + st * NWAVE + w, (unsigned)(h / NS + 1), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const int cb = s & 1;
+      if (AVC_GEMM_DIAG_NOMFMA) {  // (diagnostic: the fragments stay live, no MFMA)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            crs[i][j][0] += (float)fah[cb][i][0] + (float)fal[cb][i][1] + (float)fbh[cb][j][2] + (float)fbl[cb][j][3];
+        __builtin_amdgcn_sched_barrier(0);
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbh[cb][j], part[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbl[cb][j], crs[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[cb][i], fbh[cb][j], crs[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#undef AVC16W_FRAGS
+    // the 128-k partial folds at gemm16f's K-tile boundaries (every second 64-deep K-tile, and
+    // the last): after the odd half of K-tiles kt0 + 1, kt0 + 3, ...
+    if ((h & 3) == 3 || h + 1 == nh) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] += part[i][j][e];
+          part[i][j] = zero16;
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = acc[i][j][e] + crs[i][j][e] * (1.0f / 2048.0f);
+  if (d.split_scale && nsplit == 1) {
+    const float us = split_unscale(d.amax_a, d.amax_b);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] *= us;
+  }
+
+  // ---- epilogues: gemm16f_kernel's, by the consumer threads (tid < NT) --------------------
+  const int row_base = tm * BM + wm * WTM + 4 * (lane >> 5);
+  const int col_base = tn * BN + wn * WTN + (lane & 31);
+  if (nsplit > 1) {
+    float* out = slab + ((long)split * d.nz + z) * d.M * d.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col_base + 32 * j;
+        if (col >= d.N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+          if (row < d.M) out[(long)row * d.N + col] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+  if constexpr (BNF) {
+    bnf_epilogue<BM, BN, WM, WTN, TM, TN, NT>(d, acc, lds, tm, tn, tilesM, wm, lane, tid, row_base, col_base,
+                                              bnf_ticket);
+    return;
+  }
+  float* __restrict__ C = d.C + (long)z * d.c_zoff;
+  float biasv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col_base + 32 * j;
+    const bool colok = col < d.N;
+    float bias = 0.f;
+    if (colok) {
+      if (d.bias0) bias += d.bias0[col];
+      if (d.bias1) bias += d.bias1[col];
+    }
+    biasv[j] = bias;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
+        if (!colok || row >= d.M) continue;
+        const float v = act_apply(acc[i][j][e] + bias, d.act);
+        float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
+        if (d.accumulate) *p += v; else *p = v;
+      }
+  }
+  if (d.stats)
+    bn_tile_stats<BM, BN, WM, WTN, TM, TN, 1, false, false>(
         d, acc, biasv, reinterpret_cast<float*>(lds), tm, tn, wm, wn, lane, tid, NT, row_base, col_base);
 }
 
@@ -1573,6 +1941,25 @@ void launch16f_cfg(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
                                                                         kps, p.nsplit, slab);
 }
 
+constexpr size_t kLds16w = 4 * 32 * 1024 + 4 * (4 + 8) * sizeof(unsigned);  // the ring + FULL / FREE words
+
+// configuration 12: gemm16w_kernel (same plan, tiles, K-tiles and split-K as configuration 8)
+void launch16w(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16w_kernel<0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds16w);
+    attr = true;
+  }
+  constexpr int KC = 4;
+  const int kt_per_tap = (f.a_nkc + KC - 1) / KC;
+  const int ktotal = d.ntaps * kt_per_tap;
+  const int kps = (ktotal + p.nsplit - 1) / p.nsplit;
+  const int tilesM = (d.M + 127) / 128, tilesN = (d.N + 127) / 128;
+  dim3 grid(tilesM * tilesN, d.nz * p.nsplit);
+  gemm16w_kernel<0><<<grid, 768, kLds16w, s>>>(d, f, tilesM, tilesN, kt_per_tap, kps, p.nsplit, slab);
+}
+
 void launch16f_128(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
   switch (g_gemm_cfg) {
     case 1: launch16f_cfg<128, 128, 4, 2, 2, 4>(d, f, p, slab, s); break;
@@ -1586,6 +1973,7 @@ void launch16f_128(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
     case 9: launch16f_cfg<256, 128, 4, 2, 3, 2, 1, 0>(d, f, p, slab, s); break;  // 256-row tiles
     case 10: launch16f_cfg<256, 128, 4, 2, 3, 2, 1, 2>(d, f, p, slab, s); break;  // ... hi.hi into one chain
     case 11: launch16f_cfg<128, 128, 4, 2, 2, 4, 1, 2>(d, f, p, slab, s); break;  // 8 with hi.hi into one chain
+    case 12: launch16w(d, f, p, slab, s); break;  // 8's arithmetic, warp-specialized (gemm16w_kernel)
     default: launch16f_cfg<128, 128, 4, 2, 4, 2>(d, f, p, slab, s); break;
   }
 }
@@ -1896,22 +2284,24 @@ int g_bnf_inject = 0;  // avc_debug_bnf_inject(): train-mode fused launches left
 
 namespace {
 // the two gemm16f instances the plans pick (128 x 128: avc_gemm_config 8; 64 x 64), BNF = 1
+// (configuration 12: the warp-specialized 128 x 128 instance, gemm16w_kernel)
 const void* bnf_fn(int bm) {
+  if (bm == 128 && g_gemm_cfg == 12) return reinterpret_cast<const void*>(&gemm16w_kernel<1>);
   if (bm == 128) return reinterpret_cast<const void*>(&gemm16f_kernel<128, 128, 4, 2, 2, 4, 1, 0, 1>);
   return reinterpret_cast<const void*>(&gemm16f_kernel<64, 64, 2, 2, 4, 2, 1, 1, 1>);
 }
-size_t bnf_lds(int bm) { return bm == 128 ? 2 * 64 * 1024 : 4 * 16 * 1024; }
-int bnf_threads(int bm) { return bm == 128 ? 512 : 256; }
+size_t bnf_lds(int bm) { return bm == 128 ? (g_gemm_cfg == 12 ? kLds16w : 2 * 64 * 1024) : 4 * 16 * 1024; }
+int bnf_threads(int bm) { return bm == 128 ? (g_gemm_cfg == 12 ? 768 : 512) : 256; }
 
 // workgroups of the instance the device holds at once (occupancy API x CUs), per device
 int bnf_capacity(int bm) {
-  struct Entry { int bm, dev, cap; };
+  struct Entry { const void* fn; int dev, cap; };
   static std::vector<Entry> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  for (const auto& e : cache)
-    if (e.bm == bm && e.dev == dev) return e.cap;
   const void* fn = bnf_fn(bm);
+  for (const auto& e : cache)
+    if (e.fn == fn && e.dev == dev) return e.cap;
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bnf_lds(bm));
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, bnf_threads(bm), bnf_lds(bm)) != hipSuccess) {
@@ -1919,7 +2309,7 @@ int bnf_capacity(int bm) {
     per_cu = 0;
   }
   const int cap = per_cu * coresident_cus();
-  cache.push_back({bm, dev, cap});
+  cache.push_back({fn, dev, cap});
   return cap;
 }
 
@@ -1964,7 +2354,7 @@ bool gemm_bnf_ok(const GemmDesc& d, bool training) {
   Plan p = make_plan(d, 0);
   if (training) p.nsplit = 1;  // a stats product never splits K (gemm_run)
   if (p.nsplit != 1 || p.bm != p.bn) return false;
-  if (p.bm == 128 && g_gemm_cfg != 8) return false;  // the fused instance is configuration 8's
+  if (p.bm == 128 && g_gemm_cfg != 8 && g_gemm_cfg != 12) return false;  // the fused instances: configurations 8, 12
   // The invariant the barrier needs: one column tile's tilesM workgroups (a contiguous dispatch
   // range) resident at once.  avc_bn_fuse(1) also keeps the fused form to grids that are one
   // co-resident wave; 2 takes it wherever a single group fits (multi-wave grids, e.g. C3's 1024).
@@ -2106,7 +2496,7 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     d.amax_b = gw + 1;
     d.split_scale = 1;
   }
-  AVC_CHECK_ARG(!d.bnf.on || (frag && p.nsplit == 1 && p.bm == p.bn && (p.bm == 64 || g_gemm_cfg == 8) &&
+  AVC_CHECK_ARG(!d.bnf.on || (frag && p.nsplit == 1 && p.bm == p.bn && (p.bm == 64 || g_gemm_cfg == 8 || g_gemm_cfg == 12) &&
                               (d.stats != nullptr) == (d.bnf.training != 0)),
                 "gemm: fused BatchNorm requested for a product that cannot take it (gemm_bnf_ok)");
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
@@ -2166,8 +2556,8 @@ extern "C" int avc_gemm_tune(int mode) {
 }
 
 extern "C" int avc_gemm_config(int cfg) {
-  if (cfg < 0 || cfg > 11) {
-    avc::set_error("avc_gemm_config: cfg must be 0..11");
+  if (cfg < 0 || cfg > 12) {
+    avc::set_error("avc_gemm_config: cfg must be 0..12");
     return AVC_ERR_INVALID;
   }
   avc::g_gemm_cfg = cfg;

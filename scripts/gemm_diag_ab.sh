@@ -3,7 +3,7 @@
 #   bash scripts/gemm_diag_ab.sh         # on the GPU box: scripts/gemm_cfg_ab.py against each build
 set -e
 if [ "$1" = build ]; then
-  for v in NOLOAD:nl DIAG_NOREAD:nr DIAG_NOBAR:nb; do
+  for v in ${GEMM_DIAGS:-NOLOAD:nl DIAG_NOREAD:nr DIAG_NOBAR:nb DIAG_NOMFMA:nm}; do
     d=abd_${v##*:}; mkdir -p $d
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -Wno-unused-variable \
       -DAVC_GEMM_${v%%:*}=1 -c autovc_amd/csrc/gemm.hip -o $d/gemm.o
@@ -14,7 +14,7 @@ if [ "$1" = build ]; then
   exit 0
 fi
 for r in 1 2; do
-  for d in "" abd_nl abd_nr abd_nb; do
+  for d in "" ${GEMM_DIAG_DIRS:-abd_nl abd_nr abd_nb abd_nm}; do
     if [ -n "$d" ]; then export AUTOVC_HIP_LIB=$PWD/$d/libautovc_hip.so; else unset AUTOVC_HIP_LIB; fi
     echo "== lib ${d:-default}"
     timeout -k 10 120 python -u scripts/gemm_cfg_ab.py 8 8 2>&1 | grep cfg | tail -1
