@@ -8,6 +8,7 @@
 // current one (one barrier per K-step).  The row-shift in the A/B addressing implements the
 // Conv1d taps implicitly (no im2col buffer): in time-major frame rows a shift of one frame is
 // a shift of B rows, and rows outside the sequence read as the zero padding.
+#include <type_traits>
 #include <vector>
 
 #include "gemm.h"
@@ -30,6 +31,13 @@ constexpr int BK = 32;
 #ifndef AVC_GEMM_DIAG_NOMFMA
 #define AVC_GEMM_DIAG_NOMFMA 0  // diagnostic (wrong results): gemm16f skips its MFMAs (loads, reads, barriers kept)
 #endif
+#ifndef AVC_GEMM_DIAG_NOEPI
+#define AVC_GEMM_DIAG_NOEPI 0  // diagnostic (wrong results): gemm16f returns right after its K loop
+#endif
+#ifndef AVC_GEMM_DIAG_EPI
+#define AVC_GEMM_DIAG_EPI 0  // diagnostic (wrong results): bnf_epilogue pieces skipped, bit 1 the column-tile
+                             // wait, bit 2 the partials' combine, bit 4 the tile staging, bit 8 the outputs
+#endif
 #ifndef AVC_GEMM_DIAG_NOKAHAN
 #define AVC_GEMM_DIAG_NOKAHAN 0  // diagnostic: gemm16f folds 128-k partials with a plain add
 #endif
@@ -41,7 +49,11 @@ __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
   return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
 }
 
+#ifndef AVC_GEMM_DIAG_NOACT
+#define AVC_GEMM_DIAG_NOACT 0  // diagnostic (wrong results for act != none): act_apply is the identity
+#endif
 __device__ __forceinline__ float act_apply(float v, int act) {
+  if (AVC_GEMM_DIAG_NOACT) return v;
   if (act == AVC_ACT_RELU) return v < 0.f ? 0.f : v;  // NaN propagates, as torch.relu
   if (act == AVC_ACT_TANH) return tanhf(v);
   if (act == AVC_ACT_DBNORM) {
@@ -49,6 +61,27 @@ __device__ __forceinline__ float act_apply(float v, int act) {
     return fminf(fmaxf((db + 100.f) / 100.f, 0.f), 1.f);
   }
   return v;
+}
+
+#ifdef AVC_GEMM_EPI_STAMPS
+// diagnostic build only: s_memtime per (workgroup, phase) of the fused-BN epilogue, thread 0,
+// launches of 256 workgroups (the 512-column convs at B = 64, T = 128; the last one wins)
+__device__ unsigned long long g_epi_st[1024][10];
+#define AVC_EPI_STAMP(k)                                                                          \
+  do {                                                                                            \
+    unsigned long long _t;                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    if (threadIdx.x == 0 && gridDim.x == 256) g_epi_st[blockIdx.x][k] = _t;                     \
+  } while (0)
+#else
+#define AVC_EPI_STAMP(k) do { } while (0)
+#endif
+
+// rows of ld floats starting at p are 16-B aligned pieces (store_tile_rows' float4 form)
+__device__ __forceinline__ bool g_tile_rows_ok(const float* p, long ld, int unit) {
+  return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && (ld & 3) == 0 && unit == 1;
 }
 
 // ---- fused BatchNorm epilogue (BnFuse): the column-tile barrier ------------------------------
@@ -393,13 +426,19 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col_base + 32 * j;
-    const bool colok = col < d.N;
     float bias = 0.f;
-    if (colok) {
+    if (col < d.N) {
       if (d.bias0) bias += d.bias0[col];
       if (d.bias1) bias += d.bias1[col];
     }
     biasv[j] = bias;
+  }
+  {  // (the fallback kernels keep the per-element stores)
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col_base + 32 * j;
+    const bool colok = col < d.N;
+    const float bias = biasv[j];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -410,6 +449,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(GemmDesc d, int tile
         float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
         if (d.accumulate) *p += v; else *p = v;
       }
+  }
   }
 
   if (d.stats)  // (the LDS operand tiles are dead now: the column reduction reuses them)
@@ -634,13 +674,19 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col_base + 32 * j;
-    const bool colok = col < d.N;
     float bias = 0.f;
-    if (colok) {
+    if (col < d.N) {
       if (d.bias0) bias += d.bias0[col];
       if (d.bias1) bias += d.bias1[col];
     }
     biasv[j] = bias;
+  }
+  {  // (the fallback kernels keep the per-element stores)
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col_base + 32 * j;
+    const bool colok = col < d.N;
+    const float bias = biasv[j];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -652,9 +698,69 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm16_kernel(GemmDesc d, int ti
         if (d.accumulate) *p += v; else *p = v;
       }
   }
+  }
   if (d.stats)
     bn_tile_stats<BM, BN, WM, WTN, TM, TN, 1, false, false>(d, acc, biasv, reinterpret_cast<float*>(lds), tm, tn, wm,
                                                             wn, lane, tid, NT, row_base, col_base);
+}
+
+// ---- output tile through LDS (round 6) ------------------------------------------------------
+// The per-element epilogue (one 4-B store per accumulator element, the activation picked by a
+// runtime switch per element, 64-bit address arithmetic per element) took about as long as the K
+// loop itself: the C2 forward's GEMM class measured 66 -> 36 us per launch with every epilogue
+// skipped.  Here the tile's values -- act(acc + bias), the same expression -- go to
+// LDS once (the operand ring is dead by then), and the tile leaves as whole rows of 16-B pieces
+// (one wave instruction writes 1 KiB: two 128-column rows); an accumulating product reads the old
+// row pieces and adds in the same order.  Same values, same bits.  Requires a row-major C
+// (ldc_col = 1) with 16-B aligned rows; other layouts keep the per-element form.
+template <int ACT>
+__device__ __forceinline__ float act_k(float v) { return act_apply(v, ACT); }
+
+template <int BM, int BN, int TM, int TN, int NT, int ACT>
+__device__ __forceinline__ void tile_to_lds(float* tile, const f32x16 (&acc)[TM][TN], const float (&bias)[TN], int rl0,
+                                            int cl0) {
+  constexpr int TP = BN + 4;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        tile[(rl0 + 32 * i + (e & 3) + 8 * (e >> 2)) * TP + cl0 + 32 * j] = act_k<ACT>(acc[i][j][e] + bias[j]);
+}
+
+template <int BM, int BN, int TM, int TN, int NT>
+__device__ __forceinline__ void store_tile_rows(float* __restrict__ C, long ldc, int M, int N, int row0, int col0,
+                                                const f32x16 (&acc)[TM][TN], const float (&bias)[TN], int act,
+                                                bool accumulate, unsigned char* lds, int rl0, int cl0, int tid) {
+  constexpr int TP = BN + 4, C4 = BN / 4;
+  float* tile = reinterpret_cast<float*>(lds);
+  __syncthreads();  // (every wave is done with the LDS operand ring)
+  switch (act) {  // once, not per element
+    case AVC_ACT_RELU: tile_to_lds<BM, BN, TM, TN, NT, AVC_ACT_RELU>(tile, acc, bias, rl0, cl0); break;
+    case AVC_ACT_TANH: tile_to_lds<BM, BN, TM, TN, NT, AVC_ACT_TANH>(tile, acc, bias, rl0, cl0); break;
+    case AVC_ACT_DBNORM: tile_to_lds<BM, BN, TM, TN, NT, AVC_ACT_DBNORM>(tile, acc, bias, rl0, cl0); break;
+    default: tile_to_lds<BM, BN, TM, TN, NT, AVC_ACT_NONE>(tile, acc, bias, rl0, cl0); break;
+  }
+  __syncthreads();
+  for (int it = tid; it < BM * C4; it += NT) {
+    const int rl = it / C4, c4 = it - rl * C4;
+    const int row = row0 + rl, col = col0 + 4 * c4;
+    if (row >= M || col >= N) continue;
+    const float4 v = *reinterpret_cast<const float4*>(tile + rl * TP + 4 * c4);
+    float* p = C + (long)row * ldc + col;
+    if (col + 4 <= N) {
+      float4 o = v;
+      if (accumulate) {
+        const float4 q = *reinterpret_cast<const float4*>(p);
+        o = make_float4(q.x + v.x, q.y + v.y, q.z + v.z, q.w + v.w);
+      }
+      *reinterpret_cast<float4*>(p) = o;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int e = 0; e < N - col; ++e) p[e] = accumulate ? p[e] + vv[e] : vv[e];
+    }
+  }
 }
 
 // ---- split-f16 GEMM on pre-split fragment-major operands ("gemm16f") ---------------------
@@ -801,6 +907,34 @@ inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* 
   }
 }
 
+// gemm16f's per-column epilogue operands, loaded at kernel start so their latency hides behind
+// the main loop: this lane's bias per column block (biasv, summed as every epilogue sums it) and,
+// with the fused BatchNorm (bn), for threads tid < BN column tid's gamma, beta, running mean and
+// running var (par).
+template <int BN, int TN>
+__device__ __forceinline__ void bnf_prefetch(const GemmDesc& d, int tn, int tid, int col_base, float (&biasv)[TN],
+                                             float (&par)[4], bool bn) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col_base + 32 * j;
+    float bias = 0.f;
+    if (col < d.N) {
+      if (d.bias0) bias += d.bias0[col];
+      if (d.bias1) bias += d.bias1[col];
+    }
+    biasv[j] = bias;
+  }
+  const BnFuse& bf = d.bnf;
+  const int col = tn * BN + tid;
+  par[0] = par[1] = par[2] = par[3] = 0.f;
+  if (bn && tid < BN && col < d.N) {
+    par[0] = bf.gamma[col];
+    par[1] = bf.beta[col];
+    if (bf.rmean) par[2] = bf.rmean[col];
+    if (bf.rvar) par[3] = bf.rvar[col];
+  }
+}
+
 // Fused BatchNorm epilogue of gemm16f (GemmDesc::bnf, see gemm.h).  Every expression that forms a
 // value is the one the unfused chain uses (this kernel's epilogue for y and the column partials,
 // bn_finalize_kernel for mean / invstd and the running statistics, bn_apply(_frag) for the
@@ -810,7 +944,8 @@ inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* 
 template <int BM, int BN, int WM, int WTN, int TM, int TN, int NT>
 __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM][TN], unsigned char* lds, int tm,
                                              int tn, int tilesM, int wm, int lane, int tid, int row_base,
-                                             int col_base, unsigned long long ticket) {
+                                             int col_base, unsigned long long ticket, const float (&biasv)[TN],
+                                             const float (&par)[4]) {
   static_assert(NT == 4 * BN, "the finalize step takes 4 threads per column (bn_finalize_kernel)");
   const BnFuse& bf = d.bnf;
   float* red = reinterpret_cast<float*>(lds);
@@ -821,23 +956,20 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
   float* tile = reinterpret_cast<float*>(lds + 22528);
   constexpr int TP = BN + 4;
   const int wn = (col_base - tn * BN - (lane & 31)) / WTN;
-  // (1) y = A.B + bias, kept in registers (stored only where the caller keeps y_pre)
+  AVC_EPI_STAMP(1);
+  // (1) y = A.B + bias (biasv: bnf_prefetch; d.act is none, gemm_bnf_ok), kept in registers
+  // (stored only where the caller keeps y_pre)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col_base + 32 * j;
     const bool colok = col < d.N;
-    float bias = 0.f;
-    if (colok) {
-      if (d.bias0) bias += d.bias0[col];
-      if (d.bias1) bias += d.bias1[col];
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
         if (!colok || row >= d.M) continue;
-        const float v = act_apply(acc[i][j][e] + bias, d.act);
+        const float v = acc[i][j][e] + biasv[j];
         acc[i][j][e] = v;
         if (d.C) d.C[(long)row * d.ldc + col] = v;
       }
@@ -848,16 +980,20 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
     // stored write-through, drained, then this workgroup counts itself in on its column tile
     const float nob[TN] = {};
     const int wm_ = wm, wn_ = wn;
+    AVC_EPI_STAMP(2);
     bn_tile_stats<BM, BN, WM, WTN, TM, TN, 1, true, true>(d, acc, nob, red, tm, tn, wm_, wn_, lane, tid, NT, row_base,
                                                           col_base);
+    AVC_EPI_STAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    AVC_EPI_STAMP(4);
     if (tid == 0) {
       const unsigned E = (unsigned)(ticket / (unsigned long long)bf.nwg) + 1u;
       __hip_atomic_fetch_add((bnf_gu32*)(bf.cnt + tn * 32), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = bnf_wait(bf.cnt + tn * 32, E * (unsigned)tilesM, bf, E) ? 1 : 0;
+      flag[0] = (AVC_GEMM_DIAG_EPI & 1) ? 1 : (bnf_wait(bf.cnt + tn * 32, E * (unsigned)tilesM, bf, E) ? 1 : 0);
     }
     __syncthreads();
+    AVC_EPI_STAMP(5);
     ok = flag[0] != 0;
     // (3) this workgroup's columns' partials over every tile, combined in bn_finalize_kernel's
     // order (4 thread groups over the partial rows p = grp, grp + 4, ..., then the 4 group sums
@@ -867,7 +1003,7 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
     // (4 rows of loads in flight per thread: a variant that requested all 16 rows of a thread
     // before its first add measured 0.08 ms slower per C2 forward)
     double s = 0.0, a1 = 0.0, a2 = 0.0;
-    if (col < d.N) {
+    if (col < d.N && !(AVC_GEMM_DIAG_EPI & 2)) {
       // (bn_finalize_kernel's order and loads: K with the first batch, the next batch's loads issued
       // before the current one is combined)
       const double inv_pr = 1.0 / (double)BM;
@@ -911,8 +1047,10 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
     dred[(1 * 4 + grp) * BN + cl] = a1;
     dred[(2 * 4 + grp) * BN + cl] = a2;
     __syncthreads();
+    AVC_EPI_STAMP(6);
   }
-  // (4) per-column scale and shift (bn_finalize_kernel, then bn_apply's sc / sh)
+  // (4) per-column scale and shift (bn_finalize_kernel, then bn_apply's sc / sh); par = gamma,
+  // beta, running mean, running var of column tid (bnf_prefetch)
   if (tid < BN) {
     const int col = tn * BN + tid;
     if (col < d.N) {
@@ -931,87 +1069,109 @@ __device__ __forceinline__ void bnf_epilogue(const GemmDesc& d, f32x16 (&acc)[TM
         if (tm == 0 && ok) {
           if (bf.mean) bf.mean[col] = mf;
           if (bf.invstd) bf.invstd[col] = isf;
-          if (bf.rmean) bf.rmean[col] = (float)((1.0 - bf.momentum) * bf.rmean[col] + bf.momentum * mean);
+          if (bf.rmean) bf.rmean[col] = (float)((1.0 - bf.momentum) * par[2] + bf.momentum * mean);
           if (bf.rvar) {
             const double unb = bf.count > 1.0 ? var * bf.count / (bf.count - 1.0) : var;
-            bf.rvar[col] = (float)((1.0 - bf.momentum) * bf.rvar[col] + bf.momentum * unb);
+            bf.rvar[col] = (float)((1.0 - bf.momentum) * par[3] + bf.momentum * unb);
           }
         }
       } else {
-        mf = bf.rmean[col];
-        isf = (float)(1.0 / sqrt((double)bf.rvar[col] + (double)bf.eps));
+        mf = par[2];
+        isf = (float)(1.0 / sqrt((double)par[3] + (double)bf.eps));
         if (tm == 0) {
           if (bf.mean) bf.mean[col] = mf;
           if (bf.invstd) bf.invstd[col] = isf;
         }
       }
-      const float sc = isf * bf.gamma[col];
+      const float sc = isf * par[0];
       s_sc[tid] = sc;
-      s_sh[tid] = bf.beta[col] - mf * sc;
+      s_sh[tid] = par[1] - mf * sc;
     }
   }
   // (5) the pre-BN tile into LDS, so each output item is one row's 8 consecutive columns
+  AVC_EPI_STAMP(7);
   const int rl0 = row_base - tm * BM, cl0 = col_base - tn * BN;
+  if (!(AVC_GEMM_DIAG_EPI & 4)) {
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) tile[(rl0 + 32 * i + (e & 3) + 8 * (e >> 2)) * TP + cl0 + 32 * j] = acc[i][j][e];
+  }
   __syncthreads();
+  AVC_EPI_STAMP(8);
+  if (AVC_GEMM_DIAG_EPI & 8) return;
   // (6) BN + act (+ residual) per item (32-row block, 16-deep chunk, lane): a wave's fragment
   // stores cover whole 1 KiB blocks.  Items past N inside the image's K padding are zeros, as
   // bn_apply_frag writes them.
   constexpr int NCH16 = BN / 16, ITEMS = (BM / 32) * NCH16 * 64;
   const long fr_rows = ((long)d.M + 31) / 32 * 32;
   const int kpad = bf.nkc_out * 16;
-  bool over = false;
-  for (int it = tid; it < ITEMS; it += NT) {
-    const int l = it & 63, blk = it >> 6;
-    const int c16 = blk % NCH16, rb = blk / NCH16;
-    const int rl = rb * 32 + (l & 31), cl8 = c16 * 16 + 8 * (l >> 5);
-    const long row = (long)tm * BM + rl;
-    const int col = tn * BN + cl8;
-    float o[8];
-    if (row < d.M && col < d.N) {
-      const float4 a = *reinterpret_cast<const float4*>(tile + rl * TP + cl8);
-      const float4 b = *reinterpret_cast<const float4*>(tile + rl * TP + cl8 + 4);
-      o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
-      o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = act_apply(o[e] * s_sc[cl8 + e] + s_sh[cl8 + e], bf.act);
-      if (bf.residual) {
-        const float4* rq = reinterpret_cast<const float4*>(bf.residual + row * d.N + col);
-        const float4 ra = rq[0], rb4 = rq[1];
-        o[0] += ra.x; o[1] += ra.y; o[2] += ra.z; o[3] += ra.w;
-        o[4] += rb4.x; o[5] += rb4.y; o[6] += rb4.z; o[7] += rb4.w;
+  // (the act switch taken once, outside the item loop)
+  auto items = [&](auto actc) {
+    constexpr int ACT = decltype(actc)::value;
+    bool over = false;
+    for (int it = tid; it < ITEMS; it += NT) {
+      const int l = it & 63, blk = it >> 6;
+      const int c16 = blk % NCH16, rb = blk / NCH16;
+      const int rl = rb * 32 + (l & 31), cl8 = c16 * 16 + 8 * (l >> 5);
+      const long row = (long)tm * BM + rl;
+      const int col = tn * BN + cl8;
+      float o[8];
+      if (row < d.M && col < d.N) {
+        const float4 a = *reinterpret_cast<const float4*>(tile + rl * TP + cl8);
+        const float4 b = *reinterpret_cast<const float4*>(tile + rl * TP + cl8 + 4);
+        o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+        o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = act_k<ACT>(o[e] * s_sc[cl8 + e] + s_sh[cl8 + e]);
+        if (bf.residual) {
+          const float4* rq = reinterpret_cast<const float4*>(bf.residual + row * d.N + col);
+          const float4 ra = rq[0], rb4 = rq[1];
+          o[0] += ra.x; o[1] += ra.y; o[2] += ra.z; o[3] += ra.w;
+          o[4] += rb4.x; o[5] += rb4.y; o[6] += rb4.z; o[7] += rb4.w;
+        }
+        if (bf.out) {
+          float4* oq = reinterpret_cast<float4*>(bf.out + row * d.N + col);
+          oq[0] = make_float4(o[0], o[1], o[2], o[3]);
+          oq[1] = make_float4(o[4], o[5], o[6], o[7]);
+        }
+      } else {
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = 0.f;
       }
-      if (bf.out) {
-        float4* oq = reinterpret_cast<float4*>(bf.out + row * d.N + col);
-        oq[0] = make_float4(o[0], o[1], o[2], o[3]);
-        oq[1] = make_float4(o[4], o[5], o[6], o[7]);
+  #pragma unroll
+      for (int e = 0; e < 8; ++e) over |= fabsf(o[e]) >= 65504.f && fabsf(o[e]) < __builtin_inff();
+      if (bf.frag && row < fr_rows && col < kpad) {
+        f16x8 hi, lo;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const _Float16 h = (_Float16)o[e];
+          hi[e] = h;
+          lo[e] = (_Float16)((o[e] - (float)h) * 2048.0f);
+        }
+        const long fb = ((row >> 5) * bf.nkc_out + (col >> 4)) * 2;
+        const int fl = (int)(row & 31) + 32 * ((col >> 3) & 1);
+        *reinterpret_cast<f16x8*>(bf.frag + fb * 512 + fl * 8) = hi;
+        *reinterpret_cast<f16x8*>(bf.frag + (fb + 1) * 512 + fl * 8) = lo;
       }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = 0.f;
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) over |= fabsf(o[e]) >= 65504.f && fabsf(o[e]) < __builtin_inff();
-    if (bf.frag && row < fr_rows && col < kpad) {
-      f16x8 hi, lo;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const _Float16 h = (_Float16)o[e];
-        hi[e] = h;
-        lo[e] = (_Float16)((o[e] - (float)h) * 2048.0f);
-      }
-      const long fb = ((row >> 5) * bf.nkc_out + (col >> 4)) * 2;
-      const int fl = (int)(row & 31) + 32 * ((col >> 3) & 1);
-      *reinterpret_cast<f16x8*>(bf.frag + fb * 512 + fl * 8) = hi;
-      *reinterpret_cast<f16x8*>(bf.frag + (fb + 1) * 512 + fl * 8) = lo;
-    }
+    return over;
+  };
+  bool over;
+  switch (bf.act) {
+    case AVC_ACT_RELU: over = items(std::integral_constant<int, AVC_ACT_RELU>{}); break;
+    case AVC_ACT_TANH: over = items(std::integral_constant<int, AVC_ACT_TANH>{}); break;
+    case AVC_ACT_DBNORM: over = items(std::integral_constant<int, AVC_ACT_DBNORM>{}); break;
+    default: over = items(std::integral_constant<int, AVC_ACT_NONE>{}); break;
   }
   if (over && bf.range_flag) __hip_atomic_store(bf.range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#ifdef AVC_GEMM_EPI_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#endif
+  AVC_EPI_STAMP(9);
 }
 
 struct Frag16Args {
@@ -1047,6 +1207,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   constexpr int DPW = NBLK / NWAVE;  // LDS-DMA instructions per wave per K-tile
   constexpr int STAGE = NBLK * 1024;
   static_assert(!BNF || 18432 + BM * (BN + 4) * 4 <= NS * STAGE, "fused BN: the tile does not fit the ring's LDS");
+  constexpr bool kTileFits = BM * (BN + 4) * 4 <= NS * STAGE;  // (store_tile_rows stages the tile in the ring)
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];  // NS stages
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1078,6 +1239,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   const int ktotal = d.ntaps * kt_per_tap;
   const int kt0 = split * kps;
   const int kt1 = min(ktotal, kt0 + kps);
+  if constexpr (BNF) AVC_EPI_STAMP(0);
+  // the epilogue's per-column operands, loaded now so their latency hides behind the main loop
+  float bnf_bias[TN], bnf_par[4];
+  bnf_prefetch<BN, TN>(d, tn, tid, tn * BN + wn * WTN + (lane & 31), bnf_bias, bnf_par, BNF != 0);
 
   const auto ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.As), 0,
                                                      f.a_ntile * f.a_nkc * 2048, 0x00020000);
@@ -1296,6 +1461,17 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
 #undef AVC16F_ISSUE
 #undef AVC16F_SETTAP
 #undef AVC16F_FAST_ISSUE
+  if (AVC_GEMM_DIAG_NOEPI) {  // (diagnostic: keep every sum live, skip every epilogue)
+    float keep = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) keep += acc[i][j][e];
+    if (keep == 1.2345f && threadIdx.x == 9999) d.C[0] = keep;
+    return;
+  }
   if (d.split_scale && nsplit == 1) {  // split-K partials stay scaled; splitk_reduce_kernel unscales
     const float us = split_unscale(d.amax_a, d.amax_b);
 #pragma unroll
@@ -1311,6 +1487,12 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   const int col_base = tn * BN + wn * WTN + (lane & 31);
   if (nsplit > 1) {
     float* out = slab + ((long)split * d.nz + z) * d.M * d.N;
+    if (kTileFits && g_tile_rows_ok(out, d.N, 1)) {  // (round 6: through LDS, whole rows; same values)
+      const float zb[TN] = {};
+      store_tile_rows<BM, BN, TM, TN, NT>(out, d.N, d.M, d.N, tm * BM, tn * BN, acc, zb, AVC_ACT_NONE, false, lds,
+                                          row_base - tm * BM, col_base - tn * BN, tid);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1327,21 +1509,20 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
   }
   if constexpr (BNF) {
     bnf_epilogue<BM, BN, WM, WTN, TM, TN, NT>(d, acc, lds, tm, tn, tilesM, wm, lane, tid, row_base, col_base,
-                                              bnf_ticket);
+                                              bnf_ticket, bnf_bias, bnf_par);
     return;
   }
   float* __restrict__ C = d.C + (long)z * d.c_zoff;
-  float biasv[TN];
+  const float (&biasv)[TN] = bnf_bias;
+  if (kTileFits && d.ldc_col == 1 && g_tile_rows_ok(C, d.ldc, 1)) {  // (round 6: through LDS, whole rows; same values)
+    store_tile_rows<BM, BN, TM, TN, NT>(C, d.ldc, d.M, d.N, tm * BM, tn * BN, acc, biasv, d.act, d.accumulate != 0,
+                                        lds, row_base - tm * BM, col_base - tn * BN, tid);
+  } else {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col_base + 32 * j;
     const bool colok = col < d.N;
-    float bias = 0.f;
-    if (colok) {
-      if (d.bias0) bias += d.bias0[col];
-      if (d.bias1) bias += d.bias1[col];
-    }
-    biasv[j] = bias;
+    const float bias = biasv[j];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1352,366 +1533,10 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
         float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
         if (d.accumulate) *p += v; else *p = v;
       }
+  }
   }
   if (d.stats)
     bn_tile_stats<BM, BN, WM, WTN, TM, TN, BM == 256 ? 2 : 1, false, false>(
-        d, acc, biasv, reinterpret_cast<float*>(lds), tm, tn, wm, wn, lane, tid, NT, row_base, col_base);
-}
-
-// ---- warp-specialized split-f16 GEMM ("gemm16w", round 6; avc_gemm_config 12) ---------------
-// gemm16f<128, 128, 4, 2, 2, 4> with its LDS-DMA taken off the computing waves.  Measured on the
-// default kernel (`scripts/gemm_diag_ab.sh`): the C2 conv takes 83 us, 54 us without
-// its LDS-DMA and 59 us without its MFMAs -- the loads and the MFMAs overlap by only half, because
-// every wave both issues its K-tile's DMA and multiplies, one barrier per K-tile and one K-tile in
-// flight (two 64 KB stages fill the LDS).  Here a workgroup of 12 waves splits the roles:
-//  * waves 0-7 (consumers) own exactly gemm16f's 4 x 2 layout of 32 x 64 output tiles and run its
-//    MFMA sequence (per 16-deep chunk hi.hi, hi.lo, lo.hi; the hi.hi partials folded into the sum
-//    after every 128 k, at the same K-tile boundaries): the same bits as configuration 8;
-//  * waves 8-11 (loaders) stream the operands by LDS-DMA into a ring of NS slots, each half a
-//    64-deep K-tile (32 KB: 16 A + 16 B pieces of 1 KiB), up to three slots ahead of the consumers.
-// Hand-shake through LDS words (MI355X_MICROARCH.md, ring-gemm): a loader publishes FULL[slot][l]
-// = use + 1 once its own 8 pieces of that slot have landed (counted vmcnt), a consumer reads a slot
-// once all four FULL words are there and returns it with FREE[slot][w] = use + 1 as soon as its
-// fragments are in registers; a loader refills a slot only when all eight FREE words are.  The
-// consumers never wait on a DMA they issued, the loaders never wait on an MFMA: no barrier in the
-// K loop.  The loaders end after the K loop (a terminated wave no longer takes part in s_barrier);
-// the consumers run gemm16f's epilogues (bias / act / stats, split-K slabs, fused BatchNorm) as
-// threads 0..511.
-// Every ring wait is bounded (kRingSpins polls, ~0.1 s: a healthy wait is microseconds), so a
-// protocol fault can only produce wrong numbers, never a workgroup that does not finish.
-constexpr unsigned kRingSpins = 1u << 21;
-// The loader waves' own LDS accesses (the FREE polls, the FULL stores) are inline asm: hipcc
-// orders every compiler-visible LDS access of a wave behind that wave's pending LDS-DMA with an
-// s_waitcnt vmcnt(0), which would drain the loader's ring at every hand-shake (cdna_hip_programming.md
-// §5.7, "LDS-DMA issued beside the loader's own LDS accesses").  The words are plain LDS words;
-// ds ops of one wave complete in order, and the load's wait is inside its statement.
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ unsigned lds_load_now(unsigned a) {
-  unsigned v;
-  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(a) : "memory");
-  return v;
-}
-__device__ __forceinline__ void lds_store_asm(unsigned a, unsigned v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-template <int BNF>
-__global__ __launch_bounds__(768, 3) void gemm16w_kernel(GemmDesc d, Frag16Args f, int tilesM, int tilesN,
-                                                        int kt_per_tap, int kps, int nsplit,
-                                                        float* __restrict__ slab) {
-  constexpr int BM = 128, BN = 128, WM = 4, WN = 2, KC = 4;  // KC: 16-deep chunks per K-tile (the plan's unit)
-  constexpr int NT = 64 * WM * WN, NWAVE = WM * WN;          // consumers
-  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
-  constexpr int HKC = KC / 2;                                // chunks per ring slot (half a K-tile)
-  constexpr int ABLK = (BM / 32) * HKC * 2, BBLK = (BN / 32) * HKC * 2, NBLK = ABLK + BBLK;
-  constexpr int SLOT = NBLK * 1024;
-  constexpr int NS = 4;                                      // ring slots
-  constexpr int NL = 4, DPL = NBLK / NL;                     // loader waves, pieces per loader per slot
-  static_assert(DPL * NL == NBLK && ABLK % DPL == 0, "a loader's pieces are all A or all B");
-  static_assert(!BNF || 18432 + BM * (BN + 4) * 4 <= NS * SLOT, "fused BN: the tile does not fit the ring's LDS");
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  unsigned* full = reinterpret_cast<unsigned*>(lds + NS * SLOT);  // [NS][NL]
-  unsigned* freew = full + NS * NL;                                // [NS][NWAVE]
-
-  unsigned long long bnf_ticket = 0;
-  if constexpr (BNF) {
-    if (d.bnf.training && threadIdx.x == 0)
-      bnf_ticket = __hip_atomic_fetch_add(d.bnf.tickets, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nwg = tilesM * tilesN;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
-  int tm, tn;
-  if constexpr (BNF) {  // (gemm16f_kernel: the column-tile barrier group and the XCD row bands)
-    tn = bid / tilesM;
-    const int l = bid - tn * tilesM;
-    tm = (!d.bnf.band || (tilesM & 7)) ? l : (l & 7) * (tilesM >> 3) + (l >> 3);
-    (void)wgid;
-  } else {
-    tile_of(wgid, tilesM, tilesN, tm, tn);
-  }
-  const int split = blockIdx.y % nsplit, z = blockIdx.y / nsplit;
-  const int ktotal = d.ntaps * kt_per_tap;
-  const int kt0 = split * kps;
-  const int kt1 = min(ktotal, kt0 + kps);
-  const int nh = 2 * max(0, kt1 - kt0);  // ring slots' worth of work: half K-tiles
-
-  if (tid < NS * (NL + NWAVE)) full[tid] = 0u;  // (FULL and FREE words are contiguous)
-  __syncthreads();
-
-  if (w >= NWAVE) {
-    // ================================ loader wave ================================
-    const int l = w - NWAVE;
-    const auto ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.As), 0,
-                                                       f.a_ntile * f.a_nkc * 2048, 0x00020000);
-    const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.Bs), 0,
-                                                       (int)(d.ntaps * f.b_tapstride * 2), 0x00020000);
-    constexpr unsigned kOut = 0x7FFFFF00u;  // past num_records: the DMA lands zeros
-    const int a_ntile = f.a_ntile, a_nkc = f.a_nkc, b_ntile = f.b_ntile, b_nkc = f.b_nkc;
-    const long a_shift0 = f.a_shift0, a_tapshift = f.a_tapshift, b_tapstride = f.b_tapstride;
-    const int bzs = f.b_shift0_c + z * f.b_zshift_c;
-    const bool is_a = l * DPL < ABLK;
-    // per tap: each piece's VGPR offset without its chunk (the chunk goes in the SGPR offset;
-    // gemm16f's fast issue), re-formed when the tap changes
-    unsigned voff[DPL];
-    int vtau = -1;
-    auto set_tap = [&](int tau) {
-#pragma unroll
-      for (int i = 0; i < DPL; ++i) {
-        const int b = l * DPL + i;
-        if (is_a) {
-          const int rt = b / (2 * HKC), kc = (b >> 1) % HKC, hl = b & 1;
-          const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)tau * a_tapshift) / 32;
-          voff[i] = src_tile >= 0 && src_tile < a_ntile
-                        ? (unsigned)(((src_tile * a_nkc + kc) * 2 + hl) * 1024) + lane * 16 : kOut;
-        } else {
-          const int bb = b - ABLK;
-          const int ct = bb / (2 * HKC), kc = (bb >> 1) % HKC, hl = bb & 1;
-          const int src_tile = tn * (BN / 32) + ct;
-          voff[i] = src_tile < b_ntile
-                        ? (unsigned)(tau * b_tapstride * 2 + ((long)(src_tile * b_nkc + kc) * 2 + hl) * 1024) + lane * 16
-                        : kOut;
-        }
-      }
-      vtau = tau;
-    };
-    auto issue = [&](int h) {
-      const int KT = kt0 + (h >> 1);
-      const int tau = KT / kt_per_tap;
-      const int kc0 = (KT - tau * kt_per_tap) * KC + (h & 1) * HKC;  // first 16-deep chunk of the slot
-      unsigned char* const base = lds + (h % NS) * SLOT;
-      const bool inside = is_a ? kc0 + HKC <= a_nkc : (kc0 + bzs >= 0 && kc0 + HKC + bzs <= b_nkc);
-      if (inside) {
-        if (tau != vtau) set_tap(tau);
-        const int so = (is_a ? kc0 : kc0 + bzs) * 2048;
-#pragma unroll
-        for (int i = 0; i < DPL; ++i) {
-          unsigned char* dst = base + (l * DPL + i) * 1024;
-          const unsigned vo = voff[i];
-          if (AVC_GEMM_NOLOAD) {
-          } else if (is_a)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)dst, 16, vo, so, 0, 0);
-          else
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16, vo, so, 0, 0);
-        }
-      } else {  // a slot that runs past K (padding chunks): per-piece range checks
-#pragma unroll
-        for (int i = 0; i < DPL; ++i) {
-          const int b = l * DPL + i;
-          unsigned char* dst = base + b * 1024;
-          if (is_a) {
-            const int rt = b / (2 * HKC), kc = (b >> 1) % HKC, hl = b & 1;
-            const long src_tile = (long)tm * (BM / 32) + rt + (a_shift0 + (long)tau * a_tapshift) / 32;
-            const bool ok = src_tile >= 0 && src_tile < a_ntile && kc0 + kc < a_nkc;
-            const unsigned off = ok ? (unsigned)(((src_tile * a_nkc + kc0 + kc) * 2 + hl) * 1024) : kOut;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)dst, 16,
-                                                     off + lane * 16, 0, 0, 0);
-          } else {
-            const int bb = b - ABLK;
-            const int ct = bb / (2 * HKC), kc = (bb >> 1) % HKC, hl = bb & 1;
-            const int src_tile = tn * (BN / 32) + ct;
-            const int bkc = kc0 + kc + bzs;
-            const bool ok = src_tile < b_ntile && bkc >= 0 && bkc < b_nkc;
-            const unsigned off = ok ? (unsigned)(tau * b_tapstride * 2 + ((long)(src_tile * b_nkc + bkc) * 2 + hl) * 1024)
-                                    : kOut;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16,
-                                                     off + lane * 16, 0, 0, 0);
-          }
-        }
-      }
-    };
-    const unsigned full_l = lds_addr(full + l);
-    auto publish = [&](int h) {  // this loader's pieces of slot h have landed (the caller waited)
-      if (lane == 0) lds_store_asm(full_l + (h % NS) * NL * 4, (unsigned)(h / NS + 1));
-    };
-    for (int h = 0; h < nh; ++h) {
-      if (h >= NS) {  // the slot's previous use: every consumer has its fragments in registers
-        const unsigned want = (unsigned)(h / NS);
-        // lanes 0..7 each watch one consumer's FREE word of the slot
-        const unsigned fa = lds_addr(freew + (h % NS) * NWAVE + (lane & 7));
-        for (unsigned spins = 0;; ++spins) {
-          const bool done = __builtin_amdgcn_ballot_w64(lane < NWAVE && lds_load_now(fa) < want) == 0ull;
-          if (done || spins >= kRingSpins) break;  // (bounded: a healthy wait is microseconds)
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      issue(h);
-      if (h >= 2) {  // two slots stay in flight: the one issued two iterations ago has landed
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DPL) : "memory");
-        publish(h - 2);
-      }
-    }
-    if (nh >= 2) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPL) : "memory");
-      publish(nh - 2);
-    }
-    if (nh >= 1) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      publish(nh - 1);
-    }
-    return;
-  }
-
-  // ================================ consumer waves ================================
-  const int wm = w / WN, wn = w % WN;
-  f32x16 zero16;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) zero16[e] = 0.f;
-  f32x16 acc[TM][TN], part[TM][TN], crs[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = part[i][j] = crs[i][j] = zero16;
-  f16x8 fah[2][TM], fal[2][TM], fbh[2][TN], fbl[2][TN];
-  for (int h = 0; h < nh; ++h) {
-    const int st = h % NS;
-    {  // every loader's pieces of this slot have landed
-      const unsigned want = (unsigned)(h / NS + 1);
-      const unsigned* fl = full + st * NL;
-      for (unsigned spins = 0;; ++spins) {
-        bool done = true;
-#pragma unroll
-        for (int c = 0; c < NL; ++c)
-          done &= __hip_atomic_load(fl + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want;
-        if (done || spins >= kRingSpins) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const unsigned char* Ai = lds + st * SLOT;
-    const unsigned char* Bi = Ai + ABLK * 1024;
-#define AVC16W_FRAGS(S, BUF)                                                                      \
-    _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                              \
-      const unsigned char* p = Ai + (((wm * TM + i) * HKC + (S)) * 2) * 1024 + lane * 16;         \
-      fah[BUF][i] = *reinterpret_cast<const f16x8*>(p);                                           \
-      fal[BUF][i] = *reinterpret_cast<const f16x8*>(p + 1024);                                    \
-    }                                                                                             \
-    _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                              \
-      const unsigned char* p = Bi + (((wn * TN + j) * HKC + (S)) * 2) * 1024 + lane * 16;         \
-      fbh[BUF][j] = *reinterpret_cast<const f16x8*>(p);                                           \
-      fbl[BUF][j] = *reinterpret_cast<const f16x8*>(p + 1024);                                    \
-    }
-    AVC16W_FRAGS(0, 0)
-#pragma unroll
-    for (int s = 0; s < HKC; ++s) {
-      if (s + 1 < HKC) { AVC16W_FRAGS(s + 1, (s + 1) & 1) }
-      if (s + 1 == HKC) {  // every fragment of the slot is in registers: hand the slot back
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_store(freew + st * NWAVE + w, (unsigned)(h / NS + 1), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const int cb = s & 1;
-      if (AVC_GEMM_DIAG_NOMFMA) {  // (diagnostic: the fragments stay live, no MFMA)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            crs[i][j][0] += (float)fah[cb][i][0] + (float)fal[cb][i][1] + (float)fbh[cb][j][2] + (float)fbl[cb][j][3];
-        __builtin_amdgcn_sched_barrier(0);
-        continue;
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          part[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbh[cb][j], part[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fah[cb][i], fbl[cb][j], crs[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          crs[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[cb][i], fbh[cb][j], crs[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#undef AVC16W_FRAGS
-    // the 128-k partial folds at gemm16f's K-tile boundaries (every second 64-deep K-tile, and
-    // the last): after the odd half of K-tiles kt0 + 1, kt0 + 3, ...
-    if ((h & 3) == 3 || h + 1 == nh) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][j][e] += part[i][j][e];
-          part[i][j] = zero16;
-        }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = acc[i][j][e] + crs[i][j][e] * (1.0f / 2048.0f);
-  if (d.split_scale && nsplit == 1) {
-    const float us = split_unscale(d.amax_a, d.amax_b);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] *= us;
-  }
-
-  // ---- epilogues: gemm16f_kernel's, by the consumer threads (tid < NT) --------------------
-  const int row_base = tm * BM + wm * WTM + 4 * (lane >> 5);
-  const int col_base = tn * BN + wn * WTN + (lane & 31);
-  if (nsplit > 1) {
-    float* out = slab + ((long)split * d.nz + z) * d.M * d.N;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = col_base + 32 * j;
-        if (col >= d.N) continue;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
-          if (row < d.M) out[(long)row * d.N + col] = acc[i][j][e];
-        }
-      }
-    return;
-  }
-  if constexpr (BNF) {
-    bnf_epilogue<BM, BN, WM, WTN, TM, TN, NT>(d, acc, lds, tm, tn, tilesM, wm, lane, tid, row_base, col_base,
-                                              bnf_ticket);
-    return;
-  }
-  float* __restrict__ C = d.C + (long)z * d.c_zoff;
-  float biasv[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = col_base + 32 * j;
-    const bool colok = col < d.N;
-    float bias = 0.f;
-    if (colok) {
-      if (d.bias0) bias += d.bias0[col];
-      if (d.bias1) bias += d.bias1[col];
-    }
-    biasv[j] = bias;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = row_base + 32 * i + (e & 3) + 8 * (e >> 2);
-        if (!colok || row >= d.M) continue;
-        const float v = act_apply(acc[i][j][e] + bias, d.act);
-        float* p = C + (long)row * d.ldc + (long)col * d.ldc_col;
-        if (d.accumulate) *p += v; else *p = v;
-      }
-  }
-  if (d.stats)
-    bn_tile_stats<BM, BN, WM, WTN, TM, TN, 1, false, false>(
         d, acc, biasv, reinterpret_cast<float*>(lds), tm, tn, wm, wn, lane, tid, NT, row_base, col_base);
 }
 
@@ -1941,25 +1766,6 @@ void launch16f_cfg(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
                                                                         kps, p.nsplit, slab);
 }
 
-constexpr size_t kLds16w = 4 * 32 * 1024 + 4 * (4 + 8) * sizeof(unsigned);  // the ring + FULL / FREE words
-
-// configuration 12: gemm16w_kernel (same plan, tiles, K-tiles and split-K as configuration 8)
-void launch16w(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm16w_kernel<0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLds16w);
-    attr = true;
-  }
-  constexpr int KC = 4;
-  const int kt_per_tap = (f.a_nkc + KC - 1) / KC;
-  const int ktotal = d.ntaps * kt_per_tap;
-  const int kps = (ktotal + p.nsplit - 1) / p.nsplit;
-  const int tilesM = (d.M + 127) / 128, tilesN = (d.N + 127) / 128;
-  dim3 grid(tilesM * tilesN, d.nz * p.nsplit);
-  gemm16w_kernel<0><<<grid, 768, kLds16w, s>>>(d, f, tilesM, tilesN, kt_per_tap, kps, p.nsplit, slab);
-}
-
 void launch16f_128(const GemmDesc& d, const Frag16Args& f, const Plan& p, float* slab, hipStream_t s) {
   switch (g_gemm_cfg) {
     case 1: launch16f_cfg<128, 128, 4, 2, 2, 4>(d, f, p, slab, s); break;
@@ -1973,7 +1779,6 @@ void launch16f_128(const GemmDesc& d, const Frag16Args& f, const Plan& p, float*
     case 9: launch16f_cfg<256, 128, 4, 2, 3, 2, 1, 0>(d, f, p, slab, s); break;  // 256-row tiles
     case 10: launch16f_cfg<256, 128, 4, 2, 3, 2, 1, 2>(d, f, p, slab, s); break;  // ... hi.hi into one chain
     case 11: launch16f_cfg<128, 128, 4, 2, 2, 4, 1, 2>(d, f, p, slab, s); break;  // 8 with hi.hi into one chain
-    case 12: launch16w(d, f, p, slab, s); break;  // 8's arithmetic, warp-specialized (gemm16w_kernel)
     default: launch16f_cfg<128, 128, 4, 2, 4, 2>(d, f, p, slab, s); break;
   }
 }
@@ -2284,14 +2089,12 @@ int g_bnf_inject = 0;  // avc_debug_bnf_inject(): train-mode fused launches left
 
 namespace {
 // the two gemm16f instances the plans pick (128 x 128: avc_gemm_config 8; 64 x 64), BNF = 1
-// (configuration 12: the warp-specialized 128 x 128 instance, gemm16w_kernel)
 const void* bnf_fn(int bm) {
-  if (bm == 128 && g_gemm_cfg == 12) return reinterpret_cast<const void*>(&gemm16w_kernel<1>);
   if (bm == 128) return reinterpret_cast<const void*>(&gemm16f_kernel<128, 128, 4, 2, 2, 4, 1, 0, 1>);
   return reinterpret_cast<const void*>(&gemm16f_kernel<64, 64, 2, 2, 4, 2, 1, 1, 1>);
 }
-size_t bnf_lds(int bm) { return bm == 128 ? (g_gemm_cfg == 12 ? kLds16w : 2 * 64 * 1024) : 4 * 16 * 1024; }
-int bnf_threads(int bm) { return bm == 128 ? (g_gemm_cfg == 12 ? 768 : 512) : 256; }
+size_t bnf_lds(int bm) { return bm == 128 ? 2 * 64 * 1024 : 4 * 16 * 1024; }
+int bnf_threads(int bm) { return bm == 128 ? 512 : 256; }
 
 // workgroups of the instance the device holds at once (occupancy API x CUs), per device
 int bnf_capacity(int bm) {
@@ -2354,7 +2157,7 @@ bool gemm_bnf_ok(const GemmDesc& d, bool training) {
   Plan p = make_plan(d, 0);
   if (training) p.nsplit = 1;  // a stats product never splits K (gemm_run)
   if (p.nsplit != 1 || p.bm != p.bn) return false;
-  if (p.bm == 128 && g_gemm_cfg != 8 && g_gemm_cfg != 12) return false;  // the fused instances: configurations 8, 12
+  if (p.bm == 128 && g_gemm_cfg != 8) return false;  // the fused 128 x 128 instance: configuration 8
   // The invariant the barrier needs: one column tile's tilesM workgroups (a contiguous dispatch
   // range) resident at once.  avc_bn_fuse(1) also keeps the fused form to grids that are one
   // co-resident wave; 2 takes it wherever a single group fits (multi-wave grids, e.g. C3's 1024).
@@ -2496,7 +2299,7 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
     d.amax_b = gw + 1;
     d.split_scale = 1;
   }
-  AVC_CHECK_ARG(!d.bnf.on || (frag && p.nsplit == 1 && p.bm == p.bn && (p.bm == 64 || g_gemm_cfg == 8 || g_gemm_cfg == 12) &&
+  AVC_CHECK_ARG(!d.bnf.on || (frag && p.nsplit == 1 && p.bm == p.bn && (p.bm == 64 || g_gemm_cfg == 8) &&
                               (d.stats != nullptr) == (d.bnf.training != 0)),
                 "gemm: fused BatchNorm requested for a product that cannot take it (gemm_bnf_ok)");
   hipEvent_t ev = timing_begin(TC_GEMM, stream);
@@ -2556,8 +2359,8 @@ extern "C" int avc_gemm_tune(int mode) {
 }
 
 extern "C" int avc_gemm_config(int cfg) {
-  if (cfg < 0 || cfg > 12) {
-    avc::set_error("avc_gemm_config: cfg must be 0..12");
+  if (cfg < 0 || cfg > 11) {
+    avc::set_error("avc_gemm_config: cfg must be 0..11");
     return AVC_ERR_INVALID;
   }
   avc::g_gemm_cfg = cfg;
@@ -2594,6 +2397,13 @@ extern "C" int avc_bn_fuse(int on) {
   ++avc::g_config_epoch;
   return AVC_OK;
 }
+
+#ifdef AVC_GEMM_EPI_STAMPS
+extern "C" int avc_debug_epi_stamps(unsigned long long* host) {  // (diagnostic build) [1024][10]
+  AVC_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(avc::g_epi_st), sizeof(avc::g_epi_st), 0, hipMemcpyDeviceToHost));
+  return AVC_OK;
+}
+#endif
 
 extern "C" int avc_debug_bnf_inject(int launches) {
   if (launches < 0) {

@@ -102,6 +102,8 @@ for step in "$@"; do
     kprice) export AVC_STAMPS_LIB=diag6/libautovc_hip_stamps.so && run kprice0 200 python scripts/stamps_persist.py 2 0 && run kprice4 200 python scripts/stamps_persist.py 2 4 && run kprice8 200 python scripts/stamps_persist.py 2 8 && run kprice0b 200 python scripts/stamps_persist.py 2 0 ;;
     ab5) run ab5 900 bash scripts/ab_r05.sh ;;
     hostgpu) run hostgpu 200 python scripts/host_vs_gpu.py ;;
+    cmp6a) run cmp6a 900 bash scripts/compare_libs.sh ab/r06a.so ;;
+    epist) AUTOVC_HIP_LIB=$PWD/abd_stamps/libautovc_hip.so run epist 200 python scripts/stamps_bnf.py ;;
     ab6at) run ab6at 600 bash scripts/ab_lib_train.sh ab/r06a.so ;;
     psafe) run psafe 600 python -u -m pytest tests/test_gpu_persist_safety.py tests/test_gpu_model.py tests/test_gpu_bptt_xl.py tests/test_gpu_bptt_coalesce.py tests/test_gpu_coresidency.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     ab6a) run ab6a 900 bash scripts/ab_r05.sh ab/r06a.so ;;
