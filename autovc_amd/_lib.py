@@ -40,6 +40,11 @@ _SIGS = {
                                     _P, _P, _P, _P, _I, _P, _P],
     "avc_conv_bn_act_forward_frag": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _I,
                                      _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "avc_conv_bn_act_forward_wg": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _I,
+                                   _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "avc_conv_bn_act_backward_wg": [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P,
+                                    _P, _P, _P, _P, _I, _P, _P, _P],
+    "avc_conv_wgrad_image_bytes": [_I, _I, _I, _I],
     "avc_conv_frag_chain_ok": [_I, _I, _I, _I],
     "avc_act_frag_bytes": [ctypes.c_long, _I],
     "avc_lstm_forward": [_P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P],
@@ -128,7 +133,7 @@ _SIGS = {
     "avc_wavernn_fold_shape": [ctypes.c_long, _I, _I, _I, ctypes.POINTER(ctypes.c_long),
                                ctypes.POINTER(ctypes.c_long)],
 }
-_RESTYPES = {"avc_last_error": ctypes.c_char_p, "avc_act_frag_bytes": _Z}
+_RESTYPES = {"avc_last_error": ctypes.c_char_p, "avc_act_frag_bytes": _Z, "avc_conv_wgrad_image_bytes": _Z}
 
 _lib = None
 _lock = threading.RLock()

@@ -338,6 +338,37 @@ int avc_conv_bn_act_forward_frag(avc_context* ctx, int T, int B, int cin, int co
                                   static_cast<_Float16*>(out_frag), x_amax, out_amax);
 }
 
+int avc_conv_bn_act_forward_wg(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                               const void* x_frag, const float* weight, const float* bias, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var, int training,
+                               float momentum, float eps, int act, const float* residual, float* y_pre, float* out,
+                               void* out_frag, float* mean, float* invstd, const unsigned* x_amax,
+                               unsigned* out_amax, void* x_wimg, void* stream) {
+  AVC_CHECK_ARG(aligned16(x_wimg), "split images must be 16-byte aligned");
+  AVC_CHECK_ARG(!x_wimg || (x_amax && !x_frag && T > 0 && B > 0 && cin > 0 && cout > 0 &&
+                            conv_wgrad_image_ok(T, B, cin, cout)),
+                "conv forward: x_wimg needs x_amax, no x_frag and avc_conv_wgrad_image_bytes(T, B, cin, cout) > 0");
+  if (!x_wimg)
+    return avc_conv_bn_act_forward_frag(ctx, T, B, cin, cout, x, x_frag, weight, bias, gamma, beta, running_mean,
+                                        running_var, training, momentum, eps, act, residual, y_pre, out, out_frag,
+                                        mean, invstd, x_amax, out_amax, stream);
+  AVC_CHECK_ARG(ctx && x && weight && gamma && beta && y_pre && out && mean && invstd, "NULL pointer");
+  AVC_CHECK_ARG(aligned16(x) && aligned16(x_amax) && aligned16(out_amax) && aligned16(out_frag),
+                "x, amax words and split images must be 16-byte aligned");
+  AVC_CHECK_ARG(!out_frag || cout % 8 == 0, "conv forward: a split output needs cout % 8 == 0");
+  AVC_TRY(ensure_arena(ctx, conv_bn_forward_scratch(T, B, cin, cout)));
+  return conv_bn_act_forward_impl(ctx, T, B, cin, cout, x, weight, bias, gamma, beta, running_mean,
+                                  running_var, training, momentum, eps, act, residual, y_pre, out,
+                                  mean, invstd, S(stream), nullptr, static_cast<_Float16*>(out_frag), x_amax,
+                                  out_amax, nullptr, static_cast<_Float16*>(x_wimg));
+}
+
+size_t avc_conv_wgrad_image_bytes(int T, int B, int cin, int cout) {
+  return T > 0 && B > 0 && cin > 0 && cout > 0 && conv_wgrad_image_ok(T, B, cin, cout)
+             ? conv_wgrad_image_bytes(T, B, cin)
+             : 0;
+}
+
 int avc_conv_frag_chain_ok(int T, int B, int cin, int cout) {
   return T > 0 && B > 0 && cin > 0 && cout > 0 && conv_frag_chain_ok(T, B, cin, cout) ? 1 : 0;
 }
@@ -357,6 +388,22 @@ int avc_conv_bn_act_backward_ex(avc_context* ctx, int T, int B, int cin, int cou
   return conv_bn_act_backward_impl(ctx, T, B, cin, cout, x, weight, gamma, beta, y_pre, mean, invstd,
                                    training, act, d_out, d_x, d_weight, d_bias, d_gamma, d_beta,
                                    accumulate, S(stream), x_amax);
+}
+
+int avc_conv_bn_act_backward_wg(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                                const float* weight, const float* gamma, const float* beta,
+                                const float* y_pre, const float* mean, const float* invstd,
+                                int training, int act, const float* d_out, float* d_x,
+                                float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
+                                int accumulate, const unsigned* x_amax, const void* x_wimg, void* stream) {
+  AVC_CHECK_ARG(ctx && x && weight && gamma && beta && y_pre && mean && invstd && d_out, "NULL pointer");
+  AVC_CHECK_ARG(aligned16(x_wimg), "split images must be 16-byte aligned");
+  AVC_CHECK_ARG(!x_wimg || (x_amax && T > 0 && B > 0 && cin > 0 && cout > 0 && conv_wgrad_image_ok(T, B, cin, cout)),
+                "conv backward: x_wimg needs x_amax and avc_conv_wgrad_image_bytes(T, B, cin, cout) > 0");
+  AVC_TRY(ensure_arena(ctx, conv_bn_backward_scratch(T, B, cin, cout)));
+  return conv_bn_act_backward_impl(ctx, T, B, cin, cout, x, weight, gamma, beta, y_pre, mean, invstd,
+                                   training, act, d_out, d_x, d_weight, d_bias, d_gamma, d_beta,
+                                   accumulate, S(stream), x_amax, static_cast<const _Float16*>(x_wimg));
 }
 
 int avc_conv_bn_act_backward(avc_context* ctx, int T, int B, int cin, int cout, const float* x,

@@ -56,7 +56,32 @@ GemmDesc conv_fwd_desc(int T, int B, int cin, int cout, const float* x, const fl
   return g;
 }
 
+// dW[co][ci][tau] = sum_r dY[r][co] * x[r + (tau-2)B][ci]: the weight gradient's product (its A,
+// dY^T, and C are set by the caller)
+GemmDesc conv_wgrad_desc(int T, int B, int cin, int cout, const float* x, const unsigned* x_amax) {
+  const long TB = (long)T * B;
+  GemmDesc gw;
+  gw.M = cout; gw.N = cin; gw.Kc = (int)TB;
+  gw.a_trans = 1; gw.lda = cout;
+  gw.B = x; gw.ldb = cin; gw.b_rows = TB; gw.b_shift0 = -2L * B; gw.b_zshift = B;
+  gw.nz = 5; gw.c_zoff = 1;
+  gw.ldc = 5L * cin; gw.ldc_col = 5;
+  gw.prec16 = 1; gw.split_scale = 1;
+  gw.amax_b = x_amax;
+  return gw;
+}
+
 }  // namespace
+
+bool conv_wgrad_image_ok(int T, int B, int cin, int cout) {
+  const long TB = (long)T * B;
+  if (TB > 0x7fffffffL || !gemm_split_dual_ok(TB, cin, cin)) return false;
+  const GemmDesc g = conv_fwd_desc(T, B, cin, cout, nullptr, nullptr, nullptr, nullptr);
+  const GemmDesc gw = conv_wgrad_desc(T, B, cin, cout, nullptr, nullptr);
+  return gemm_frag_eligible(g) && gemm_frag_eligible(gw);
+}
+
+size_t conv_wgrad_image_bytes(int T, int B, int cin) { return gemm_afrag_bytes((long)T * B, cin); }
 
 bool conv_frag_chain_ok(int T, int B, int cin, int cout) {
   const GemmDesc g = conv_fwd_desc(T, B, cin, cout, nullptr, nullptr, nullptr, nullptr);
@@ -77,7 +102,7 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
                              const float* residual, float* y_pre, float* out, float* mean,
                              float* invstd, hipStream_t s, const _Float16* x_frag,
                              _Float16* out_frag, const unsigned* x_amax, unsigned* out_amax,
-                             const unsigned* x_frag_guard) {
+                             const unsigned* x_frag_guard, _Float16* x_wimg) {
   // x_frag: x already split (the previous layer's bn_apply wrote it); out_frag: also emit the
   // output split for the next layer (out may then be NULL: the fp32 output is not stored).
   // x_amax: x's max words from its producer (see bn_apply's amax_out): the range scan of x is
@@ -112,6 +137,19 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
       AVC_LAUNCH_CHECK();
     }
     g.B = wt;
+  }
+  if (x_wimg) {
+    // round 6: the weight gradient's split of x (its B operand, K = frames, scaled by the power of
+    // two of max |x|, as that product's own split would be) written by the same pass that splits
+    // x for this product (A, K = cin, guard-scaled): the backward reads x_wimg instead of
+    // splitting x again (conv_bn_act_backward_impl; same bits)
+    AVC_CHECK_ARG(x_amax && !x_frag && conv_wgrad_image_ok(T, B, cin, cout) && g.b_conv == 1 &&
+                      (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+                  "conv forward: a weight-gradient image needs x_amax, no x_frag and avc_conv_wgrad_image_bytes > 0");
+    AVC_TAKE(ximg, _Float16, gemm_afrag_bytes((long)T * B, cin) / 2, sc);
+    AVC_TRY(gemm_split_dual2(x, cin, (long)T * B, cin, x_amax + 1, x_amax, ximg, x_wimg, s));
+    g.a_frag = ximg;
+    g.a_frag_guard = x_amax + 1;
   }
   float* stats = nullptr;
   int nparts = 0, part_rows = 0;
@@ -174,7 +212,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
                               const float* y_pre, const float* mean, const float* invstd,
                               int training, int act, const float* d_out, float* d_x,
                               float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
-                              int accumulate, hipStream_t s, const unsigned* x_amax) {
+                              int accumulate, hipStream_t s, const unsigned* x_amax, const _Float16* x_wimg) {
   // x_amax: max |x| recorded by x's producer (bn_apply's amax_out): the weight gradient's scan
   // of x is skipped
   AVC_CHECK_ARG(T > 0 && B > 0, "conv_backward: empty input");
@@ -192,15 +230,14 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
   gd.ldb = cin; gd.b_rows = cout; gd.b_tapoff = (long)cout * cin;
   gd.C = d_x; gd.ldc = cin; gd.accumulate = acc_x;
   gd.prec16 = 1; gd.split_scale = 1;
-  // dW[co][ci][tau] = sum_r dY[r][co] * x[r + (tau-2)B][ci]
-  GemmDesc gw;
-  gw.M = cout; gw.N = cin; gw.Kc = (int)TB;
-  gw.a_trans = 1; gw.lda = cout;
-  gw.B = x; gw.ldb = cin; gw.b_rows = TB; gw.b_shift0 = -2L * B; gw.b_zshift = B;
-  gw.nz = 5; gw.c_zoff = 1;
-  gw.C = d_weight; gw.ldc = 5L * cin; gw.ldc_col = 5; gw.accumulate = acc_p;
-  gw.prec16 = 1; gw.split_scale = 1;
-  gw.amax_b = x_amax;
+  GemmDesc gw = conv_wgrad_desc(T, B, cin, cout, x, x_amax);
+  gw.C = d_weight; gw.accumulate = acc_p;
+  if (x_wimg) {  // x split by its forward (conv_bn_act_forward_impl's x_wimg)
+    AVC_CHECK_ARG(x_amax && conv_wgrad_image_ok(T, B, cin, cout),
+                  "conv backward: a weight-gradient image needs x_amax and avc_conv_wgrad_image_bytes > 0");
+    gw.b_frag = x_wimg;
+    gw.b_frag_scaled = 1;
+  }
   // round 4 (avc_bn_bwd_frag): the BN backward writes dY already split for both
   // products -- dY and dY^T fragment images scaled by a proven bound on max |dY| -- so neither the
   // fp32 dY nor its max scan and two split passes exist

@@ -76,6 +76,9 @@ struct GemmDesc {
                                    // scratch; a_trans: gemm_afrag_bytes(M, Kc) bytes) ...
   int a_frag_scaled = 0;    // ... and a later product with the same A and amax_a passes it back as
                             // a_frag with a_frag_scaled = 1 (gradient products sharing dY^T / dG^T)
+  int b_frag_scaled = 0;    // scaled (gradient) products: b_frag was split scaled by the power of two
+                            // of *amax_b, as gemm_run's own split would be (a conv's x image written
+                            // by its forward, gemm_split_dual2), and is streamed as is
   const unsigned* a_frag_guard = nullptr;  // forward products: a_frag was split scaled by the power of
                                            // two of this range-guard word (max(|A|, 2^14); frames_frag)
   float* stats = nullptr;   // [ceil(M/BM)][2][N] column (sum, sumsq) partials of the output
@@ -114,6 +117,9 @@ int gemm_split_frag(const float* src, long rs, int R, int K, const unsigned* ama
 bool gemm_split_dual_ok(long R, long C, long ld);
 int gemm_split_dual(const float* src, long ld, long R, int C, const unsigned* amax, _Float16* dst_a, _Float16* dst_t,
                     hipStream_t s);
+// ... with its own scale for each image: dst_a scaled by *amax_a, dst_t by *amax_t (NULL: unscaled)
+int gemm_split_dual2(const float* src, long ld, long R, int C, const unsigned* amax_a, const unsigned* amax_t,
+                     _Float16* dst_a, _Float16* dst_t, hipStream_t s);
 // max |x| of a rows x cols region (row stride ld) into *out (float bits), for GemmDesc::amax_a
 int gemm_absmax(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t stream);
 

@@ -836,6 +836,61 @@ __global__ __launch_bounds__(256) void split_frag32_kernel(const float* __restri
   }
 }
 
+// A Conv1d weight's five tap images in one pass (GemmDesc::b_conv; split_frag32_kernel's layout,
+// scale and split8, so the same bits): one wave per 1 KiB block pair (32 rows x 16 k), lane
+// l -> row 32t + (l & 31), k = 16c + 8(l >> 5) .. +7, every tap of those 8 k read at once and each
+// tap's hi / lo written as whole 1 KiB blocks.  MODE 1 (forward, N = cout, K = cin): element
+// (n, k, tau) = W[n][k][tau], a lane's 40 floats contiguous; MODE 2 (dgrad, N = cin, K = cout):
+// W[k][n][4 - tau], 32 lanes reading 640 contiguous bytes per k.  (split_frag32_kernel walked
+// the weight with the row as the fast index: each lane strided 10 KB from its neighbour, 8 us per
+// 512 x 512 weight.)
+template <int MODE>
+__global__ __launch_bounds__(64) void split_convw_kernel(const float* __restrict__ W, int N, int K, int ntile, int nkc,
+                                                         _Float16* __restrict__ dst, long tapstride,
+                                                         const unsigned* __restrict__ amax) {
+  const int l = threadIdx.x;
+  const int t = blockIdx.x / nkc, c = blockIdx.x - (blockIdx.x / nkc) * nkc;
+  const int n = 32 * t + (l & 31), k0 = 16 * c + 8 * (l >> 5);
+  const float sc = split_scale_of(amax);
+  float f[8][5];
+  if (MODE == 1 && n < N && k0 + 8 <= K && (K & 3) == 0 && (reinterpret_cast<uintptr_t>(W) & 15) == 0) {
+    const float4* q = reinterpret_cast<const float4*>(W + ((long)n * K + k0) * 5);
+    float4 r[10];
+#pragma unroll
+    for (int u = 0; u < 10; ++u) r[u] = q[u];
+    const float* rf = reinterpret_cast<const float*>(r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int tau = 0; tau < 5; ++tau) f[e][tau] = rf[e * 5 + tau];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = k0 + e;
+      const bool ok = n < N && k < K;
+#pragma unroll
+      for (int tau = 0; tau < 5; ++tau)
+        f[e][tau] = !ok ? 0.f : (MODE == 1 ? W[((long)n * K + k) * 5 + tau] : W[((long)k * N + n) * 5 + 4 - tau]);
+    }
+  }
+  const long blk = ((long)t * nkc + c) * 2;
+#pragma unroll
+  for (int tau = 0; tau < 5; ++tau) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = f[e][tau];
+    if (amax) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= sc;
+    }
+    f16x8 hi, lo;
+    split8(v, hi, lo);
+    _Float16* o = dst + tau * tapstride + blk * 512 + l * 8;
+    *reinterpret_cast<f16x8*>(o) = hi;
+    *reinterpret_cast<f16x8*>(o + 512) = lo;
+  }
+}
+
 // max |x| over a rows x cols region (row stride ld) into *out (float bits; out pre-zeroed).
 // Contiguous regions stream as float4; strided ones walk rows per block (no 64-bit division).
 __global__ __launch_bounds__(256) void absmax_vec_kernel(const float4* __restrict__ src, long n4,
@@ -843,15 +898,15 @@ __global__ __launch_bounds__(256) void absmax_vec_kernel(const float4* __restric
                                                          unsigned* __restrict__ out) {
   __shared__ float red[4];
   float m = 0.f;
-  // four independent loads in flight per thread per iteration
+  // eight independent loads in flight per thread per iteration
   const long stride = (long)gridDim.x * 256;
   long i = blockIdx.x * 256L + threadIdx.x;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    float4 v[4];
+  for (; i + 7 * stride < n4; i += 8 * stride) {
+    float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = src[i + u * stride];
+    for (int u = 0; u < 8; ++u) v[u] = src[i + u * stride];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 8; ++u)
       m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
   }
   for (; i < n4; i += stride) {
@@ -895,10 +950,14 @@ __global__ __launch_bounds__(256) void absmax_rows_kernel(const float* __restric
 // (2048 workgroups made a 64 MB scan take ~37 us, mostly serialised atomics); the loop keeps four
 // loads in flight per thread instead.
 constexpr long kMaxScanBlocks = 256;
+// ... and a small scan takes at least 4096 float4 per workgroup (16 per thread, two batches of
+// eight loads): each workgroup's atomic costs ~35 ns serialised on the one word, so a 5 MB weight
+// spread over 256 workgroups spent most of its 9-13 us in atomics (round 6)
+inline long scan_blocks(long n4) { return std::max<long>(1, std::min<long>((n4 + 4095) / 4096, kMaxScanBlocks)); }
 inline void absmax2d(const float* src, long rows, long cols, long ld, unsigned* out, hipStream_t s) {
   if (ld == cols && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
     const long n = rows * cols, n4 = n / 4;
-    absmax_vec_kernel<<<(int)std::max<long>(1, std::min<long>((n4 + 1023) / 1024, kMaxScanBlocks)), 256, 0, s>>>(
+    absmax_vec_kernel<<<(int)scan_blocks(n4), 256, 0, s>>>(
         reinterpret_cast<const float4*>(src), n4, src + 4 * n4, (int)(n - 4 * n4), out);
   } else {
     const long blocks = (cols % 4 == 0 && ld % 4 == 0) ? (rows * (cols / 4) + 1023) / 1024 : rows;
@@ -1850,6 +1909,24 @@ BSrc b_src(const GemmDesc& d) {
   return {d.B, d.b_trans ? d.ldb : 1, d.b_trans ? 1 : d.ldb, d.b_tapoff};
 }
 
+// the B operand's split into its tap images: a Conv1d weight through split_convw_kernel (one
+// pass, whole-block stores), any other through split_frag32_kernel
+void split_b(const GemmDesc& d, int K, long ntile, int nkc, _Float16* dst, long tapstride, const unsigned* amax,
+             hipStream_t s) {
+  if (d.b_conv && d.ntaps == 5) {
+    const unsigned blocks = (unsigned)(ntile * nkc);
+    if (d.b_conv == 1)
+      split_convw_kernel<1><<<blocks, 64, 0, s>>>(d.B, d.N, K, (int)ntile, nkc, dst, tapstride, amax);
+    else
+      split_convw_kernel<2><<<blocks, 64, 0, s>>>(d.B, d.N, K, (int)ntile, nkc, dst, tapstride, amax);
+    return;
+  }
+  const long tb = ntile * 32 * nkc * 2;
+  const BSrc bsrc = b_src(d);
+  split_frag32_kernel<<<dim3((int)std::min<long>((tb + 255) / 256, 8192), d.ntaps), 256, 0, s>>>(
+      bsrc.p, bsrc.rs, bsrc.ks, d.N, K, (int)ntile, nkc, dst, amax, bsrc.tap, tapstride);
+}
+
 void absmax_b(const GemmDesc& d, unsigned* w, hipStream_t s) {
   if (d.b_conv) {  // the whole weight, one contiguous scan
     absmax2d(d.B, 1, 5L * d.N * d.Kc, 5L * d.N * d.Kc, w, s);
@@ -1885,12 +1962,12 @@ __global__ __launch_bounds__(256) void guard_scan_kernel(const float* __restrict
     const float4* s4 = reinterpret_cast<const float4*>(src);
     const long stride = (long)gridDim.x * 256;
     long i = blockIdx.x * 256L + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {  // four loads in flight
-      float4 v[4];
+    for (; i + 7 * stride < n4; i += 8 * stride) {  // eight loads in flight
+      float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = s4[i + u * stride];
+      for (int u = 0; u < 8; ++u) v[u] = s4[i + u * stride];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
         m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
     }
     for (; i < n4; i += stride) {
@@ -1926,15 +2003,11 @@ int gemm_prepare_bfrag(const GemmDesc& d, _Float16* dst, hipStream_t stream) {
   const long b_ntile = frag_ntile(d.N);
   const int nkc = frag_nkc(d.Kc);
   const long tapstride = b_ntile * nkc * 1024;  // halves
-  const long tb = b_ntile * 32 * nkc * 2;
   const long b_rows = d.b_rows ? d.b_rows : (d.b_trans ? d.N : d.Kc);
   unsigned* guard = bfrag_guard_word(d, dst);
   guard_init_kernel<<<1, 64, 0, stream>>>(guard, 1);
   absmax_b(d, guard, stream);
-  const BSrc bsrc = b_src(d);
-  split_frag32_kernel<<<dim3((int)std::min<long>((tb + 255) / 256, 8192), d.ntaps), 256, 0, stream>>>(
-      bsrc.p, bsrc.rs, bsrc.ks, d.N, d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows),
-      (int)b_ntile, nkc, dst, guard, bsrc.tap, tapstride);
+  split_b(d, d.b_trans ? d.Kc : (int)std::min<long>(d.Kc, b_rows), b_ntile, nkc, dst, tapstride, guard, stream);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
@@ -1984,12 +2057,15 @@ int gemm_frag_partials(int M, int N, int K, const _Float16* As, const _Float16* 
 __global__ __launch_bounds__(256) void split_frag32_dual_kernel(const float* __restrict__ src, long ld, int R, int C,
                                                                 const unsigned* __restrict__ amax,
                                                                 _Float16* __restrict__ dst_a,
-                                                                _Float16* __restrict__ dst_t) {
+                                                                _Float16* __restrict__ dst_t,
+                                                                const unsigned* __restrict__ amax_t) {
+  // (amax_t: the A^T image's own scale; the tile holds the unscaled values, each image multiplies
+  // by its scale once, as split_frag32_kernel does)
   __shared__ float tile[32][65];
   const int tid = threadIdx.x;
   const long bt = blockIdx.x;        // 32-row block
   const int bc = (int)blockIdx.y;    // 64-column block
-  const float sc = split_scale_of(amax);
+  const float sc = split_scale_of(amax), sct = split_scale_of(amax_t);
   const int nkc_a = C / 16, nkc_t = R / 16;
   {  // A image: thread = (row rr, 8-column group g)
     const int rr = tid >> 3, g = tid & 7;
@@ -1997,12 +2073,12 @@ __global__ __launch_bounds__(256) void split_frag32_dual_kernel(const float* __r
     const float4* q = reinterpret_cast<const float4*>(src + r * ld + (long)bc * 64 + 8 * g);
     const float4 a = q[0], b = q[1];
     float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[rr][8 * g + e] = v[e];
     if (amax) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= sc;
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) tile[rr][8 * g + e] = v[e];
     f16x8 hi, lo;
     split8(v, hi, lo);
     const int g8 = bc * 8 + g;
@@ -2017,6 +2093,10 @@ __global__ __launch_bounds__(256) void split_frag32_dual_kernel(const float* __r
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = tile[8 * q + e][c];
+    if (amax_t) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= sct;
+    }
     f16x8 hi, lo;
     split8(v, hi, lo);
     const long r = (long)bc * 64 + c;
@@ -2032,14 +2112,19 @@ bool gemm_split_dual_ok(long R, long C, long ld) {
   return R > 0 && C > 0 && R % 32 == 0 && C % 64 == 0 && ld % 4 == 0 && R / 32 < 0x7fffffffL && C / 64 <= 65535;
 }
 
-int gemm_split_dual(const float* src, long ld, long R, int C, const unsigned* amax, _Float16* dst_a, _Float16* dst_t,
-                    hipStream_t s) {
+int gemm_split_dual2(const float* src, long ld, long R, int C, const unsigned* amax_a, const unsigned* amax_t,
+                     _Float16* dst_a, _Float16* dst_t, hipStream_t s) {
   AVC_CHECK_ARG(gemm_split_dual_ok(R, C, ld) && (reinterpret_cast<uintptr_t>(src) & 15) == 0,
                 "gemm_split_dual: needs rows % 32 == 0, columns % 64 == 0 and 16-byte aligned rows");
-  split_frag32_dual_kernel<<<dim3((unsigned)(R / 32), (unsigned)(C / 64)), 256, 0, s>>>(src, ld, (int)R, C, amax,
-                                                                                       dst_a, dst_t);
+  split_frag32_dual_kernel<<<dim3((unsigned)(R / 32), (unsigned)(C / 64)), 256, 0, s>>>(src, ld, (int)R, C, amax_a,
+                                                                                       dst_a, dst_t, amax_t);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
+}
+
+int gemm_split_dual(const float* src, long ld, long R, int C, const unsigned* amax, _Float16* dst_a, _Float16* dst_t,
+                    hipStream_t s) {
+  return gemm_split_dual2(src, ld, R, C, amax, amax, dst_a, dst_t, s);
 }
 
 int gemm_split_frag(const float* src, long rs, int R, int K, const unsigned* amax, _Float16* dst, hipStream_t s) {
@@ -2075,7 +2160,7 @@ int guard_scan(avc_context* ctx, const float* src, long rows, long cols, long ld
     AVC_HIP(hipStreamSynchronize(s));
   }
   const long n4 = rows * cols / 4;
-  const int blocks = (int)std::max<long>(1, std::min<long>((n4 + 1023) / 1024, kGuardBlocks));
+  const int blocks = (int)std::min<long>(scan_blocks(n4), kGuardBlocks);
   guard_scan_kernel<<<blocks, 256, 0, s>>>(src, rows, (int)cols, ld, part, ctx->guard_ticket, out);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
@@ -2266,14 +2351,11 @@ int gemm_run(avc_context* ctx, GemmDesc d, hipStream_t stream, int force_split) 
       as = at;
     }
     const long tapstride = b_ntile * b_nkc * 1024;  // halves
-    const _Float16* bs = scaled_product ? nullptr : d.b_frag;
+    const _Float16* bs = (scaled_product && !(d.b_frag_scaled && d.amax_b)) ? nullptr : d.b_frag;
     if (!bs) {
       _Float16* tmp = sc.take<_Float16>((size_t)d.ntaps * frag_bytes(d.N, (int)b_krows) / 2);
       if (!tmp) return AVC_ERR_WORKSPACE;
-      const long tb = b_ntile * 32 * b_nkc * 2;
-      const BSrc bsrc = b_src(d);
-      split_frag32_kernel<<<dim3((int)std::min<long>((tb + 255) / 256, 8192), d.ntaps), 256, 0, stream>>>(
-          bsrc.p, bsrc.rs, bsrc.ks, d.N, (int)b_krows, (int)b_ntile, b_nkc, tmp, d.amax_b, bsrc.tap, tapstride);
+      split_b(d, (int)b_krows, b_ntile, b_nkc, tmp, tapstride, d.amax_b, stream);
       bs = tmp;
     }
     AVC_LAUNCH_CHECK();

@@ -98,16 +98,22 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
                              const float* residual, float* y_pre, float* out, float* mean,
                              float* invstd, hipStream_t s, const _Float16* x_frag = nullptr,
                              _Float16* out_frag = nullptr, const unsigned* x_amax = nullptr,
-                             unsigned* out_amax = nullptr, const unsigned* x_frag_guard = nullptr);
+                             unsigned* out_amax = nullptr, const unsigned* x_frag_guard = nullptr,
+                             _Float16* x_wimg = nullptr);
 size_t conv_bn_forward_scratch(int T, int B, int cin, int cout);
 // true when a conv with cin input channels takes its input as split fragments (x_frag honoured)
 bool conv_frag_chain_ok(int T, int B, int cin, int cout);
+// true when a conv's forward can hand its weight gradient the split of x (x_wimg: T*B % 32 == 0,
+// cin % 64 == 0); conv_wgrad_image_bytes = the image's size
+bool conv_wgrad_image_ok(int T, int B, int cin, int cout);
+size_t conv_wgrad_image_bytes(int T, int B, int cin);
 int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
                               const float* weight, const float* gamma, const float* beta,
                               const float* y_pre, const float* mean, const float* invstd,
                               int training, int act, const float* d_out, float* d_x,
                               float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
-                              int accumulate, hipStream_t s, const unsigned* x_amax = nullptr);
+                              int accumulate, hipStream_t s, const unsigned* x_amax = nullptr,
+                              const _Float16* x_wimg = nullptr);
 size_t conv_bn_backward_scratch(int T, int B, int cin, int cout);
 
 // arena growth (only legal when no scratch is outstanding)

@@ -200,6 +200,23 @@ def frag_chain_ok(T, B, cin):
     return ok and _FRAG_CHAIN
 
 
+# AUTOVC_WGRAD_IMAGE=0: the per-layer path's conv forwards stop handing their weight gradients the
+# split of x (avc_conv_bn_act_forward_wg / _backward_wg; bit-identical either way, round 6)
+_WGRAD_IMAGE = os.environ.get("AUTOVC_WGRAD_IMAGE", "1") != "0"
+_wimg_cache = {}
+
+
+def wgrad_image_bytes(T, B, cin, cout):
+    """Bytes of x's weight-gradient split image for this conv shape (0: not available)."""
+    if not _WGRAD_IMAGE:
+        return 0
+    key = (T, B, cin, cout)
+    n = _wimg_cache.get(key)
+    if n is None:
+        n = _wimg_cache[key] = int(_lib.load().avc_conv_wgrad_image_bytes(T, B, cin, cout))
+    return n
+
+
 def _take_frag(x):
     """The split image a ConvBNAct forward emitted for x (its output), if x is that very tensor and
     unmodified since; the record is dropped once taken (one consumer per activation)."""
@@ -237,11 +254,22 @@ class ConvBNAct(torch.autograd.Function):
         if emit_frag and frag_chain_ok(T, B, cout):
             out_frag = torch.empty(int(_lib.load().avc_act_frag_bytes(T * B, cout)), dtype=torch.uint8,
                                    device=x.device)
-        call("avc_conv_bn_act_forward_frag", _ctx(x), T, B, cin, cout, ptr(x), _wptr(x_frag),
-             ptr(weight.contiguous()), ptr(_c(bias)), ptr(gamma), ptr(beta), ptr(running_mean),
-             ptr(running_var), int(training), float(momentum), float(eps), act, ptr(_c(residual)),
-             ptr(y_pre), ptr(out), _wptr(out_frag), ptr(mean), ptr(invstd), _wptr(x_amax),
-             _wptr(out_amax), _stream(x))
+        # the weight gradient's split of x, written by the pass that splits x for this product
+        # (x's max words set its scale); the backward then skips its own split of x
+        x_wimg = None
+        if ctx.needs_input_grad[1] and x_amax is not None and x_frag is None:
+            nb = wgrad_image_bytes(T, B, cin, cout)
+            if nb:
+                x_wimg = torch.empty(nb, dtype=torch.uint8, device=x.device)
+        args = (_ctx(x), T, B, cin, cout, ptr(x), _wptr(x_frag), ptr(weight.contiguous()), ptr(_c(bias)),
+                ptr(gamma), ptr(beta), ptr(running_mean), ptr(running_var), int(training), float(momentum),
+                float(eps), act, ptr(_c(residual)), ptr(y_pre), ptr(out), _wptr(out_frag), ptr(mean), ptr(invstd),
+                _wptr(x_amax), _wptr(out_amax))
+        if x_wimg is not None:
+            call("avc_conv_bn_act_forward_wg", *args, _wptr(x_wimg), _stream(x))
+        else:
+            call("avc_conv_bn_act_forward_frag", *args, _stream(x))
+        ctx.x_wimg = x_wimg
         out._avc_amax = (out_amax, out._version)
         if out_frag is not None:
             out._avc_frag = (out_frag, out._version)
@@ -261,9 +289,13 @@ class ConvBNAct(torch.autograd.Function):
         dx = _empty(x.shape, x) if ng[0] else None
         params = (weight, ctx.bias if has_bias else None, gamma, beta)
         (dw, db, dg, dbt), direct = _param_grads(params, ng[1:5])
-        call("avc_conv_bn_act_backward_ex", _ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()),
-             ptr(gamma), ptr(beta), ptr(y_pre), ptr(mean), ptr(invstd), training, act, ptr(d_out),
-             ptr(dx), ptr(dw), ptr(db), ptr(dg), ptr(dbt), 2 if direct else 0, _wptr(ctx.x_amax), _stream(x))
+        args = (_ctx(x), T, B, cin, cout, ptr(x), ptr(weight.contiguous()), ptr(gamma), ptr(beta), ptr(y_pre),
+                ptr(mean), ptr(invstd), training, act, ptr(d_out), ptr(dx), ptr(dw), ptr(db), ptr(dg), ptr(dbt),
+                2 if direct else 0, _wptr(ctx.x_amax))
+        if ctx.x_wimg is not None and ng[1]:
+            call("avc_conv_bn_act_backward_wg", *args, _wptr(ctx.x_wimg), _stream(x))
+        else:
+            call("avc_conv_bn_act_backward_ex", *args, _stream(x))
         d_res = d_out if (has_res and ng[11]) else None
         dw, db, dg, dbt = _param_done(params, (dw, db, dg, dbt), direct)
         return dx, dw, db, dg, dbt, None, None, None, None, None, None, d_res, None, None, None

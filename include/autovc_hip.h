@@ -120,6 +120,26 @@ int avc_conv_bn_act_forward_frag(avc_context* ctx, int T, int B, int cin, int co
                                  float momentum, float eps, int act, const float* residual, float* y_pre,
                                  float* out, void* out_frag, float* mean, float* invstd, const unsigned* x_amax,
                                  unsigned* out_amax, void* stream);
+/* Round 6: the forward of _frag ALSO writing x's split image for the layer's weight gradient
+ * (x_wimg: avc_conv_wgrad_image_bytes(T, B, cin, cout) bytes, 16-byte aligned, NULL = _frag), in
+ * the pass that splits x for this product; the backward _wg reads it instead of splitting x
+ * again (training path, encoder.py:69-70, decoder.py:69-70, postnet.py:54-61 / model.py:312-313).
+ * Needs x_amax (its max word sets the image's scale) and no x_frag.  Results are bit-identical to
+ * _frag / _ex; x_wimg must describe exactly the x the backward is given. */
+int avc_conv_bn_act_forward_wg(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                               const void* x_frag, const float* weight, const float* bias, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var, int training,
+                               float momentum, float eps, int act, const float* residual, float* y_pre, float* out,
+                               void* out_frag, float* mean, float* invstd, const unsigned* x_amax,
+                               unsigned* out_amax, void* x_wimg, void* stream);
+int avc_conv_bn_act_backward_wg(avc_context* ctx, int T, int B, int cin, int cout, const float* x,
+                                const float* weight, const float* gamma, const float* beta,
+                                const float* y_pre, const float* mean, const float* invstd,
+                                int training, int act, const float* d_out, float* d_x,
+                                float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
+                                int accumulate, const unsigned* x_amax, const void* x_wimg, void* stream);
+/* bytes of that image; 0 when this shape cannot take one (T*B % 32 != 0 or cin % 64 != 0) */
+size_t avc_conv_wgrad_image_bytes(int T, int B, int cin, int cout);
 /* 1 if a conv of this shape can take its input as a split image (B % 32 == 0, cin % 8 == 0) */
 int avc_conv_frag_chain_ok(int T, int B, int cin, int cout);
 /* bytes of the split image of a [rows][channels] activation (0 for an empty one) */

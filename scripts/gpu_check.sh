@@ -30,6 +30,7 @@ for step in "$@"; do
     pmcw)  run pmcw 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcW -o fwd -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-timing ;;
     pmcft) run pmcft 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcFT -o train -- python3 bench.py --mode train --steps 2 --warmup 1 --no-cpu --no-timing ;;
     pmcwt) run pmcwt 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcWT -o train -- python3 bench.py --mode train --steps 2 --warmup 1 --no-cpu --no-timing ;;
+    ktrain) run ktrain 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ktrain -o train -- python3 bench.py --mode train --steps 1 --warmup 1 --no-cpu --no-timing ;;
     proftrain) run proftrain 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/proftrain -o train -- python3 bench.py --mode train --steps 3 --warmup 1 --no-cpu --no-timing ;;
     sstamps) run sstamps 300 python scripts/stamps_split.py 0:0 0:4 ;;
     pstamps) run pstamps 300 python scripts/stamps_persist.py 1 ;;
@@ -103,10 +104,14 @@ for step in "$@"; do
     ab5) run ab5 900 bash scripts/ab_r05.sh ;;
     hostgpu) run hostgpu 200 python scripts/host_vs_gpu.py ;;
     cmp6a) run cmp6a 900 bash scripts/compare_libs.sh ab/r06a.so ;;
+    wgimg) run wgimg 300 python -u -m pytest tests/test_gpu_wgrad_image.py tests/test_gpu_bnfuse.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    cmp6b) run cmp6b 900 bash scripts/compare_libs.sh ab/r06b.so ;;
+    ab6bt) run ab6bt 600 bash scripts/ab_lib_train.sh ab/r06b.so ;;
     epist) AUTOVC_HIP_LIB=$PWD/abd_stamps/libautovc_hip.so run epist 200 python scripts/stamps_bnf.py ;;
     ab6at) run ab6at 600 bash scripts/ab_lib_train.sh ab/r06a.so ;;
     psafe) run psafe 600 python -u -m pytest tests/test_gpu_persist_safety.py tests/test_gpu_model.py tests/test_gpu_bptt_xl.py tests/test_gpu_bptt_coalesce.py tests/test_gpu_coresidency.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
     ab6a) run ab6a 900 bash scripts/ab_r05.sh ab/r06a.so ;;
+    ab6b) run ab6b 900 bash scripts/ab_r05.sh ab/r06b.so ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
