@@ -73,12 +73,11 @@ GemmDesc conv_wgrad_desc(int T, int B, int cin, int cout, const float* x, const 
 
 }  // namespace
 
+// (shape only: whether the products then stream split images depends on the process-wide GEMM
+// toggles, which may change between a forward and its backward; both sides check them themselves)
 bool conv_wgrad_image_ok(int T, int B, int cin, int cout) {
   const long TB = (long)T * B;
-  if (TB > 0x7fffffffL || !gemm_split_dual_ok(TB, cin, cin)) return false;
-  const GemmDesc g = conv_fwd_desc(T, B, cin, cout, nullptr, nullptr, nullptr, nullptr);
-  const GemmDesc gw = conv_wgrad_desc(T, B, cin, cout, nullptr, nullptr);
-  return gemm_frag_eligible(g) && gemm_frag_eligible(gw);
+  return cout > 0 && B % 16 == 0 && TB <= 0x7fffffffL && gemm_split_dual_ok(TB, cin, cin);
 }
 
 size_t conv_wgrad_image_bytes(int T, int B, int cin) { return gemm_afrag_bytes((long)T * B, cin); }
@@ -143,13 +142,16 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
     // two of max |x|, as that product's own split would be) written by the same pass that splits
     // x for this product (A, K = cin, guard-scaled): the backward reads x_wimg instead of
     // splitting x again (conv_bn_act_backward_impl; same bits)
-    AVC_CHECK_ARG(x_amax && !x_frag && conv_wgrad_image_ok(T, B, cin, cout) && g.b_conv == 1 &&
-                      (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+    AVC_CHECK_ARG(x_amax && !x_frag && conv_wgrad_image_ok(T, B, cin, cout) && (reinterpret_cast<uintptr_t>(x) & 15) == 0,
                   "conv forward: a weight-gradient image needs x_amax, no x_frag and avc_conv_wgrad_image_bytes > 0");
-    AVC_TAKE(ximg, _Float16, gemm_afrag_bytes((long)T * B, cin) / 2, sc);
-    AVC_TRY(gemm_split_dual2(x, cin, (long)T * B, cin, x_amax + 1, x_amax, ximg, x_wimg, s));
-    g.a_frag = ximg;
-    g.a_frag_guard = x_amax + 1;
+    if (g.b_conv == 1) {  // this product streams split fragments: one pass writes both images
+      AVC_TAKE(ximg, _Float16, gemm_afrag_bytes((long)T * B, cin) / 2, sc);
+      AVC_TRY(gemm_split_dual2(x, cin, (long)T * B, cin, x_amax + 1, x_amax, ximg, x_wimg, s));
+      g.a_frag = ximg;
+      g.a_frag_guard = x_amax + 1;
+    } else {  // (a GEMM toggle moved this product off the split path: the image alone)
+      AVC_TRY(gemm_split_frag_t(x, cin, (long)T * B, cin, x_amax, x_wimg, s));
+    }
   }
   float* stats = nullptr;
   int nparts = 0, part_rows = 0;
@@ -232,7 +234,7 @@ int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout,
   gd.prec16 = 1; gd.split_scale = 1;
   GemmDesc gw = conv_wgrad_desc(T, B, cin, cout, x, x_amax);
   gw.C = d_weight; gw.accumulate = acc_p;
-  if (x_wimg) {  // x split by its forward (conv_bn_act_forward_impl's x_wimg)
+  if (x_wimg && gemm_frag_eligible(gw)) {  // x split by its forward (conv_bn_act_forward_impl's x_wimg)
     AVC_CHECK_ARG(x_amax && conv_wgrad_image_ok(T, B, cin, cout),
                   "conv backward: a weight-gradient image needs x_amax and avc_conv_wgrad_image_bytes > 0");
     gw.b_frag = x_wimg;

@@ -117,6 +117,8 @@ int gemm_split_frag(const float* src, long rs, int R, int K, const unsigned* ama
 bool gemm_split_dual_ok(long R, long C, long ld);
 int gemm_split_dual(const float* src, long ld, long R, int C, const unsigned* amax, _Float16* dst_a, _Float16* dst_t,
                     hipStream_t s);
+// the A^T image of row-major [R][C] src alone (rows C, K = R): gemm_split_dual's dst_t, one pass
+int gemm_split_frag_t(const float* src, long ld, long R, int C, const unsigned* amax, _Float16* dst, hipStream_t s);
 // ... with its own scale for each image: dst_a scaled by *amax_a, dst_t by *amax_t (NULL: unscaled)
 int gemm_split_dual2(const float* src, long ld, long R, int C, const unsigned* amax_a, const unsigned* amax_t,
                      _Float16* dst_a, _Float16* dst_t, hipStream_t s);

@@ -2136,6 +2136,16 @@ int gemm_split_frag(const float* src, long rs, int R, int K, const unsigned* ama
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
+int gemm_split_frag_t(const float* src, long ld, long R, int C, const unsigned* amax, _Float16* dst, hipStream_t s) {
+  AVC_CHECK_ARG(R > 0 && C > 0 && R < 0x7fffffffL, "gemm_split_frag_t: bad shape");
+  const long ntile = frag_ntile(C);
+  const int nkc = frag_nkc((int)R);
+  const long total = ntile * 32 * nkc * 2;
+  split_frag32_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(src, 1, ld, C, (int)R, (int)ntile,
+                                                                                   nkc, dst, amax);
+  AVC_LAUNCH_CHECK();
+  return AVC_OK;
+}
 bool gemm_frag_eligible(const GemmDesc& d) { return frag16_eligible(d); }
 
 size_t gemm_scratch_bytes(const GemmDesc& d) {

@@ -103,8 +103,8 @@ int conv_bn_act_forward_impl(avc_context* ctx, int T, int B, int cin, int cout, 
 size_t conv_bn_forward_scratch(int T, int B, int cin, int cout);
 // true when a conv with cin input channels takes its input as split fragments (x_frag honoured)
 bool conv_frag_chain_ok(int T, int B, int cin, int cout);
-// true when a conv's forward can hand its weight gradient the split of x (x_wimg: T*B % 32 == 0,
-// cin % 64 == 0); conv_wgrad_image_bytes = the image's size
+// true when a conv's forward can hand its weight gradient the split of x (x_wimg; a shape rule:
+// B % 16 == 0, T*B % 32 == 0, cin % 64 == 0); conv_wgrad_image_bytes = the image's size
 bool conv_wgrad_image_ok(int T, int B, int cin, int cout);
 size_t conv_wgrad_image_bytes(int T, int B, int cin);
 int conv_bn_act_backward_impl(avc_context* ctx, int T, int B, int cin, int cout, const float* x,

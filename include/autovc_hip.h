@@ -138,7 +138,7 @@ int avc_conv_bn_act_backward_wg(avc_context* ctx, int T, int B, int cin, int cou
                                 int training, int act, const float* d_out, float* d_x,
                                 float* d_weight, float* d_bias, float* d_gamma, float* d_beta,
                                 int accumulate, const unsigned* x_amax, const void* x_wimg, void* stream);
-/* bytes of that image; 0 when this shape cannot take one (T*B % 32 != 0 or cin % 64 != 0) */
+/* bytes of that image; 0 when this shape cannot take one (B % 16, T*B % 32 or cin % 64 != 0) */
 size_t avc_conv_wgrad_image_bytes(int T, int B, int cin, int cout);
 /* 1 if a conv of this shape can take its input as a split image (B % 32 == 0, cin % 8 == 0) */
 int avc_conv_frag_chain_ok(int T, int B, int cin, int cout);
