@@ -23,6 +23,7 @@ for step in "$@"; do
     model) run model 600 python -m pytest tests/test_gpu_model.py -v -m gpu -s --timeout 200 -p no:cacheprovider ;;
     gpu)   run gpu 900 python -m pytest tests -v -m gpu --timeout 300 -p no:cacheprovider ;;
     bench) run bench 400 python bench.py --steps 10 --warmup 2 ;;
+    benchdef) run benchdef 400 python bench.py ;;
     benchnt) run benchnt 400 python bench.py --steps 20 --warmup 3 --no-timing --no-cpu ;;
     perf)  run perf 400 python scripts/perf_layers.py 1 6 7 ;;
     prof)  run prof 500 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof -o fwd -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-timing ;;
