@@ -108,6 +108,7 @@ for step in "$@"; do
     wgimg) run wgimg 300 python -u -m pytest tests/test_gpu_wgrad_image.py tests/test_gpu_bnfuse.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     cmp6b) run cmp6b 900 bash scripts/compare_libs.sh ab/r06b.so ;;
     ab6bt) run ab6bt 600 bash scripts/ab_lib_train.sh ab/r06b.so ;;
+    ab5t) run ab5t 600 bash scripts/ab_lib_train.sh ab/r05.so ;;
     epist) AUTOVC_HIP_LIB=$PWD/abd_stamps/libautovc_hip.so run epist 200 python scripts/stamps_bnf.py ;;
     ab6at) run ab6at 600 bash scripts/ab_lib_train.sh ab/r06a.so ;;
     psafe) run psafe 600 python -u -m pytest tests/test_gpu_persist_safety.py tests/test_gpu_model.py tests/test_gpu_bptt_xl.py tests/test_gpu_bptt_coalesce.py tests/test_gpu_coresidency.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider ;;
