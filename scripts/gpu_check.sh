@@ -106,6 +106,9 @@ for step in "$@"; do
     hostgpu) run hostgpu 200 python scripts/host_vs_gpu.py ;;
     cmp6a) run cmp6a 900 bash scripts/compare_libs.sh ab/r06a.so ;;
     wgimg) run wgimg 300 python -u -m pytest tests/test_gpu_wgrad_image.py tests/test_gpu_bnfuse.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    cmpl2) run cmpl2 900 bash scripts/compare_libs.sh abd_l2/libautovc_hip.so ;;
+    abl2) run abl2 900 bash scripts/ab_r05.sh abd_l2/libautovc_hip.so ;;
+    bnfl2) AUTOVC_HIP_LIB=$PWD/abd_l2/libautovc_hip.so run bnfl2 300 python -u -m pytest tests/test_gpu_bnfuse.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     cmp6b) run cmp6b 900 bash scripts/compare_libs.sh ab/r06b.so ;;
     ab6bt) run ab6bt 600 bash scripts/ab_lib_train.sh ab/r06b.so ;;
     ab5t) run ab5t 600 bash scripts/ab_lib_train.sh ab/r05.so ;;
