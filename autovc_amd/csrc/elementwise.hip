@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long M, int C, const floa
   }
   // kRows rows per pass, all loads issued before any store (out may alias y: every element is
   // read and written by the same thread, so loading ahead is safe), so the loads overlap
-  constexpr int kRows = 4;
+  constexpr int kRows = 8;
   for (long rb = r0; rb < M; rb += kRows * rows_per_pass) {
     float4 v[kRows], rr[kRows];
 #pragma unroll
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce4_kernel(int M, int C, const
     BnQuad k;
     bn_quad_load(k, 4 * q, mean, invstd, gamma, beta);
     const int m0 = blockIdx.y * rows_per, m1 = min(M, m0 + rows_per);
-#pragma unroll 4
+#pragma unroll 8
     for (int m = m0 + ph; m < m1; m += P) {
       const long i4 = (long)m * Q + q;
       const float4 yv = reinterpret_cast<const float4*>(y)[i4];
