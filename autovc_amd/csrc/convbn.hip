@@ -80,7 +80,7 @@ bool conv_wgrad_image_ok(int T, int B, int cin, int cout) {
   return cout > 0 && B % 16 == 0 && TB <= 0x7fffffffL && gemm_split_dual_ok(TB, cin, cin);
 }
 
-size_t conv_wgrad_image_bytes(int T, int B, int cin) { return gemm_afrag_bytes((long)T * B, cin); }
+size_t conv_wgrad_image_bytes(int T, int B, int cin) { return gemm_afrag_bytes(cin, T * B); }  // rows cin, K = T*B
 
 bool conv_frag_chain_ok(int T, int B, int cin, int cout) {
   const GemmDesc g = conv_fwd_desc(T, B, cin, cout, nullptr, nullptr, nullptr, nullptr);
