@@ -1,5 +1,6 @@
 """CPU-side checks: the C-ABI library loads and exports every symbol include/autovc_hip.h
 declares; the drop-in module mirrors the reference's state_dict and call surface."""
+import ctypes
 import inspect
 import os
 import re
@@ -135,3 +136,19 @@ def test_unit_bound_mark_follows_the_tensor_version():
     assert ops._unit_bounded(t)
     t.add_(1.0)  # an in-place change voids the bound
     assert not ops._unit_bounded(t)
+
+
+def test_wgrad_image_shape_rule():
+    """avc_conv_wgrad_image_bytes (host logic, no device call): the conv forward can hand its weight
+    gradient x's split image when B % 16 == 0, T*B % 32 == 0 and cin % 64 == 0, sized rows = cin by
+    K = T*B in 2 KiB fragment blocks; 0 otherwise (ops.wgrad_image_bytes then takes the _frag path)."""
+    lib = _lib.load()
+    f = lib.avc_conv_wgrad_image_bytes
+    f.restype = ctypes.c_size_t
+    assert f(128, 64, 512, 512) == 512 * 128 * 64 * 4
+    assert f(128, 256, 512, 512) == 512 * 128 * 256 * 4
+    assert f(64, 32, 256, 128) == 256 * 64 * 32 * 4
+    assert f(20, 8, 512, 512) == 0       # B % 16 != 0
+    assert f(128, 64, 336, 512) == 0     # the first encoder conv (80 + 256 channels)
+    assert f(128, 64, 80, 512) == 0      # postnet's first conv
+    assert f(0, 64, 512, 512) == 0 and f(128, 64, 512, 0) == 0
