@@ -11,9 +11,13 @@ LIB      := autovc_amd/libautovc_hip.so
 
 all: $(LIB)
 
-build/%.o: autovc_amd/csrc/%.hip $(HDR)
+# per-file machine-scheduler strategy (round 6, same-box A/B in DESIGN §9p): the persistent
+# recurrences schedule for instruction-level parallelism
+SCHED_lstm_persist := -mllvm -amdgpu-sched-strategy=max-ilp
+
+build/%.o: autovc_amd/csrc/%.hip $(HDR) Makefile
 	@mkdir -p build
-	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -c $< -o $@
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) $(SCHED_$*) -c $< -o $@
 
 $(LIB): $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJ) -o $@

@@ -5,11 +5,11 @@ lib=${1:-ab/r05.so}; tag=$(basename $lib .so)
 mkdir -p gpurun_out
 rm -f gpurun_out/ab5_*.log
 for i in 1 2 3; do
-  AUTOVC_WGRAD_IMAGE=0 AUTOVC_HIP_LIB=$lib timeout -k 10 150 python bench.py --steps 30 --warmup 3 --no-cpu >> gpurun_out/ab5_c2_$tag.log 2>&1
+  AUTOVC_WGRAD_IMAGE=${REF_WGRAD:-0} AUTOVC_HIP_LIB=$lib timeout -k 10 150 python bench.py --steps 30 --warmup 3 --no-cpu >> gpurun_out/ab5_c2_$tag.log 2>&1
   timeout -k 10 150 python bench.py --steps 30 --warmup 3 --no-cpu >> gpurun_out/ab5_c2_new.log 2>&1
 done
 for i in 1 2 3; do
-  AUTOVC_WGRAD_IMAGE=0 AUTOVC_HIP_LIB=$lib timeout -k 10 150 python bench.py --mode long --steps 8 --warmup 2 --no-cpu >> gpurun_out/ab5_c5_$tag.log 2>&1
+  AUTOVC_WGRAD_IMAGE=${REF_WGRAD:-0} AUTOVC_HIP_LIB=$lib timeout -k 10 150 python bench.py --mode long --steps 8 --warmup 2 --no-cpu >> gpurun_out/ab5_c5_$tag.log 2>&1
   timeout -k 10 150 python bench.py --mode long --steps 8 --warmup 2 --no-cpu >> gpurun_out/ab5_c5_new.log 2>&1
 done
 for f in c2_$tag c2_new c5_$tag c5_new; do
