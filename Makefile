@@ -14,6 +14,7 @@ all: $(LIB)
 # per-file machine-scheduler strategy (round 6, same-box A/B in DESIGN §9p): the persistent
 # recurrences schedule for instruction-level parallelism
 SCHED_lstm_persist := -mllvm -amdgpu-sched-strategy=max-ilp
+SCHED_lstm := -mllvm -amdgpu-sched-strategy=max-ilp
 
 build/%.o: autovc_amd/csrc/%.hip $(HDR) Makefile
 	@mkdir -p build
