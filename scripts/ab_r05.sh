@@ -16,5 +16,5 @@ for f in c2_$tag c2_new c5_$tag c5_new; do
   python -c "
 import json,sys
 L=[json.loads(x) for x in open(sys.argv[2]) if x.startswith('{')]
-print(sys.argv[1], 'ms/step', [d['ms_per_step'] for d in L], 'lstm2 us', [round(d.get('kernels',{}).get('lstm2_persist',{}).get('avg_us',0),1) for d in L], 'lstm1 us', [round(d.get('kernels',{}).get('lstm1_persist',{}).get('avg_us',0),1) for d in L])" $f gpurun_out/ab5_$f.log
+print(sys.argv[1], 'ms/step', [d['ms_per_step'] for d in L], 'lstm2 us', [round(d.get('kernels',{}).get('lstm2_persist',{}).get('avg_us',0),1) for d in L], 'lstm1 us', [round(d.get('kernels',{}).get('lstm1_persist',{}).get('avg_us',0),1) for d in L], 'gemm us', [round(d.get('kernels',{}).get('gemm',{}).get('avg_us',0),1) for d in L])" $f gpurun_out/ab5_$f.log
 done
