@@ -41,7 +41,8 @@ constexpr int BK = 32;
 #ifndef AVC_GEMM_DMA_SPREAD
 // gemm16f issues the next K-tile's LDS-DMA over the first AVC_GEMM_DMA_SPREAD chunks of the current
 // one, between their fragment reads and MFMAs, instead of all DPW pieces right after the barrier
-// (round 6: 2 measured -2.4 % on the C2 conv, -2.5 % at C5; 4 less; same bytes, same bits)
+// (round 6: 2 measured -2.4 % on the C2 conv, -2.5 % at C5; 4 less; the pieces after the chunk's
+// MFMAs, or interleaved with them by sched_group_barrier, no better; same bytes, same bits)
 #define AVC_GEMM_DMA_SPREAD 2
 #endif
 #ifndef AVC_GEMM_DIAG_NOKAHAN
