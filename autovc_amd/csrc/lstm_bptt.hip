@@ -6,7 +6,7 @@
 #include <algorithm>
 #include <vector>
 
-#define AVC_GIVEUP_TAG 0x40000000u
+#define AVC_GIVEUP_TAG 0x20000000u  // (the vocoder tags 0x40000000, the fused BN 0x80000000)
 #include "kernels.h"
 #include "persist_internal.h"
 #include "timing.h"
