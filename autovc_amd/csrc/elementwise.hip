@@ -890,8 +890,29 @@ __global__ __launch_bounds__(256) void frames_guard_kernel(const float* __restri
   __shared__ float red[4];
   __shared__ bool last;
   float m = 0.f;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < nx + ne; i += (long)gridDim.x * 256)
-    m = fmaxf(m, fabsf(i < nx ? x[i] : emb[i - nx]));
+  const long stride = (long)gridDim.x * 256, gid = blockIdx.x * 256L + threadIdx.x;
+  if ((nx & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    // (round 6) the mel as float4 with four loads in flight, then the embedding: the scalar walk
+    // below went one dependent round trip per element (10.6 us for a C2 batch)
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const long n4 = nx >> 2;
+    long i = gid;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = x4[i + u * stride];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
+    }
+    for (; i < n4; i += stride) {
+      const float4 v = x4[i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (long j = gid; j < ne; j += stride) m = fmaxf(m, fabsf(emb[j]));
+  } else {
+    for (long i = gid; i < nx + ne; i += stride) m = fmaxf(m, fabsf(i < nx ? x[i] : emb[i - nx]));
+  }
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
@@ -948,6 +969,47 @@ __global__ __launch_bounds__(256) void frames_frag_kernel(int T, int B, int cm, 
     const int lane = rr + 32 * (g8 & 1);
     *reinterpret_cast<h16x8*>(frag + blk * 512 + lane * 8) = hi;
     *reinterpret_cast<h16x8*>(frag + (blk + 1) * 512 + lane * 8) = lo;
+  }
+}
+
+// frames_frag_kernel for T % 4 == 0 (round 6): a thread takes 4 consecutive frames t of one batch
+// row b and 8-channel group, reading each channel's 4 frames as one float4 (the mel is [B][cm][T]:
+// the scalar form read 4 B from each of 8 lines per item), and writes the 4 rows' fragments; lanes
+// take consecutive b, so a wave still writes whole 512-B runs of a fragment block.  Same values,
+// same split: the same image.
+__global__ __launch_bounds__(256) void frames_frag4_kernel(int T, int B, int cm, const float* __restrict__ x, int ce,
+                                                           const float* __restrict__ emb, int nkc,
+                                                           const unsigned* __restrict__ guard,
+                                                           _Float16* __restrict__ frag) {
+  const int C = cm + ce, G8 = nkc * 2, T4 = T >> 2;
+  const float sc = pow2_of_bound(guard);
+  const long total = (long)T4 * G8 * B;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int b = (int)(idx % B);
+    const long rest = idx / B;
+    const int g8 = (int)(rest % G8), t4 = (int)(rest / G8);
+    float v[4][8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = 8 * g8 + e;
+      if (c < cm) {
+        const float4 q = *reinterpret_cast<const float4*>(x + ((long)b * cm + c) * T + 4 * t4);
+        v[0][e] = q.x * sc; v[1][e] = q.y * sc; v[2][e] = q.z * sc; v[3][e] = q.w * sc;
+      } else {
+        const float ev = (c < C ? emb[(long)b * ce + (c - cm)] : 0.f) * sc;
+        v[0][e] = v[1][e] = v[2][e] = v[3][e] = ev;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long r = (long)(4 * t4 + u) * B + b;
+      h16x8 hi, lo;
+      bwd_split8(v[u], hi, lo);
+      const long blk = ((r >> 5) * nkc + (g8 >> 1)) * 2;
+      const int lane = (int)(r & 31) + 32 * (g8 & 1);
+      *reinterpret_cast<h16x8*>(frag + blk * 512 + lane * 8) = hi;
+      *reinterpret_cast<h16x8*>(frag + (blk + 1) * 512 + lane * 8) = lo;
+    }
   }
 }
 
@@ -1506,8 +1568,15 @@ int frames_from_mel_frag(avc_context* ctx, int T, int B, int cm, const float* x,
       x, nx, emb, ne, part, ctx->guard_ticket, guard);
   const int nkc = (cm + ce + 31) / 32 * 2;
   const long ntile = ((long)T * B + 31) / 32, total = ntile * 32 * nkc * 2;
-  frames_frag_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(T, B, cm, x, ce, emb, nkc, ntile,
-                                                                                   guard + 1, frag);
+  if (T % 4 == 0 && B % 32 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    // (every row tile is whole: T * B % 32 == 0, so no padding rows to zero)
+    const long total4 = (long)(T / 4) * nkc * 2 * B;
+    frames_frag4_kernel<<<(int)std::min<long>((total4 + 255) / 256, 8192), 256, 0, s>>>(T, B, cm, x, ce, emb, nkc,
+                                                                                      guard + 1, frag);
+  } else {
+    frames_frag_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(T, B, cm, x, ce, emb, nkc, ntile,
+                                                                                     guard + 1, frag);
+  }
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }
