@@ -972,19 +972,25 @@ __global__ __launch_bounds__(256) void frames_frag_kernel(int T, int B, int cm, 
   }
 }
 
-// frames_frag_kernel for T % 4 == 0 (round 6): a thread takes 4 consecutive frames t of one batch
-// row b and 8-channel group, reading each channel's 4 frames as one float4 (the mel is [B][cm][T]:
-// the scalar form read 4 B from each of 8 lines per item), and writes the 4 rows' fragments; lanes
-// take consecutive b, so a wave still writes whole 512-B runs of a fragment block.  Same values,
-// same split: the same image.
-__global__ __launch_bounds__(256) void frames_frag4_kernel(int T, int B, int cm, const float* __restrict__ x, int ce,
-                                                           const float* __restrict__ emb, int nkc,
-                                                           const unsigned* __restrict__ guard,
-                                                           _Float16* __restrict__ frag) {
+// frames_guard_kernel and frames_frag_kernel in ONE launch for T % 4 == 0, B % 32 == 0 (round 6):
+// a thread takes 4 consecutive frames of one batch row and 8-channel group (one float4 per channel;
+// lanes take consecutive b, so a wave writes whole 512-B runs of a block).  The image is written with
+// scale 1 -- what the guard gives whenever max |x| < 2^15, i.e. for every mel in [0, 1] and unit-norm
+// embedding -- while each workgroup also takes the max of the values it split; the last workgroup
+// to take a ticket forms the guard words and, only if the guard's scale is not 1, re-writes the
+// whole image with that scale itself (correct, slow, never taken for normalised inputs).  Every
+// other workgroup's stores precede its ticket (fence), so the re-write lands last.  Same words,
+// same image as the two kernels; one launch and one pass fewer.
+__global__ __launch_bounds__(256) void frames_frag_guard_kernel(int T, int B, int cm, const float* __restrict__ x,
+                                                                int ce, const float* __restrict__ emb, int nkc,
+                                                                float* __restrict__ partial,
+                                                                unsigned* __restrict__ ticket, unsigned* __restrict__ w,
+                                                                _Float16* __restrict__ frag) {
+  __shared__ float red[4];
+  __shared__ bool last;
   const int C = cm + ce, G8 = nkc * 2, T4 = T >> 2;
-  const float sc = pow2_of_bound(guard);
   const long total = (long)T4 * G8 * B;
-  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+  auto item = [&](long idx, float sc, float& m) {
     const int b = (int)(idx % B);
     const long rest = idx / B;
     const int g8 = (int)(rest % G8), t4 = (int)(rest / G8);
@@ -994,10 +1000,12 @@ __global__ __launch_bounds__(256) void frames_frag4_kernel(int T, int B, int cm,
       const int c = 8 * g8 + e;
       if (c < cm) {
         const float4 q = *reinterpret_cast<const float4*>(x + ((long)b * cm + c) * T + 4 * t4);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
         v[0][e] = q.x * sc; v[1][e] = q.y * sc; v[2][e] = q.z * sc; v[3][e] = q.w * sc;
       } else {
-        const float ev = (c < C ? emb[(long)b * ce + (c - cm)] : 0.f) * sc;
-        v[0][e] = v[1][e] = v[2][e] = v[3][e] = ev;
+        const float ev = c < C ? emb[(long)b * ce + (c - cm)] : 0.f;
+        m = fmaxf(m, fabsf(ev));
+        v[0][e] = v[1][e] = v[2][e] = v[3][e] = ev * sc;
       }
     }
 #pragma unroll
@@ -1010,6 +1018,38 @@ __global__ __launch_bounds__(256) void frames_frag4_kernel(int T, int B, int cm,
       *reinterpret_cast<h16x8*>(frag + blk * 512 + lane * 8) = hi;
       *reinterpret_cast<h16x8*>(frag + (blk + 1) * 512 + lane * 8) = lo;
     }
+  };
+  float m = 0.f;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) item(idx, 1.f, m);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(partial + blockIdx.x, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    last = atomicInc(ticket, gridDim.x - 1) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  float v = 0.f;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += 256)
+    v = fmaxf(v, __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const unsigned w1 = __float_as_uint(fmaxf(v, 16384.f));
+  if (threadIdx.x == 0) {
+    w[0] = __float_as_uint(v);
+    w[1] = w1;
+  }
+  const float sc = pow2_of_bound(&w1);
+  if (sc != 1.f) {  // out of the split's range: the whole image again, with the guard's scale
+    float unused = 0.f;
+    for (long idx = threadIdx.x; idx < total; idx += 256) item(idx, sc, unused);
   }
 }
 
@@ -1562,21 +1602,23 @@ int frames_from_mel_frag(avc_context* ctx, int T, int B, int cm, const float* x,
     AVC_HIP(hipStreamSynchronize(s));
   }
   Scratch sc(ctx);
+  const int nkc0 = (cm + ce + 31) / 32 * 2;
+  if (T % 4 == 0 && B % 32 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const long total4 = (long)(T / 4) * nkc0 * 2 * B;
+    const int blocks = (int)std::min<long>((total4 + 255) / 256, 8192);
+    AVC_TAKE(partm, float, blocks, sc);
+    frames_frag_guard_kernel<<<blocks, 256, 0, s>>>(T, B, cm, x, ce, emb, nkc0, partm, ctx->guard_ticket, guard, frag);
+    AVC_LAUNCH_CHECK();
+    return AVC_OK;
+  }
   AVC_TAKE(part, float, 256, sc);
   const long nx = (long)B * cm * T, ne = (long)B * ce;
   frames_guard_kernel<<<(int)std::max<long>(1, std::min<long>((nx + ne + 1023) / 1024, 256)), 256, 0, s>>>(
       x, nx, emb, ne, part, ctx->guard_ticket, guard);
   const int nkc = (cm + ce + 31) / 32 * 2;
   const long ntile = ((long)T * B + 31) / 32, total = ntile * 32 * nkc * 2;
-  if (T % 4 == 0 && B % 32 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-    // (every row tile is whole: T * B % 32 == 0, so no padding rows to zero)
-    const long total4 = (long)(T / 4) * nkc * 2 * B;
-    frames_frag4_kernel<<<(int)std::min<long>((total4 + 255) / 256, 8192), 256, 0, s>>>(T, B, cm, x, ce, emb, nkc,
-                                                                                      guard + 1, frag);
-  } else {
-    frames_frag_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(T, B, cm, x, ce, emb, nkc, ntile,
-                                                                                     guard + 1, frag);
-  }
+  frames_frag_kernel<<<(int)std::min<long>((total + 255) / 256, 8192), 256, 0, s>>>(T, B, cm, x, ce, emb, nkc, ntile,
+                                                                                   guard + 1, frag);
   AVC_LAUNCH_CHECK();
   return AVC_OK;
 }

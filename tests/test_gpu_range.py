@@ -91,3 +91,27 @@ def test_fused_handover_beyond_range_raises(cuda_device):
         rel = float((o.detach().cpu() - r).abs().max()) / max(float(r.abs().max()), 1e-30)
         print(f"layers, gamma x1e6: {name} max|d|/max|ref| {rel:.2e}")
         assert rel <= 1e-4, name
+
+
+def test_out_of_range_frames_into_the_first_conv(cuda_device):
+    """B = 32, T = 64: the fused forward writes the frames straight into the first conv's split
+    image with its range guard in one launch (frames_frag_guard_kernel), splitting with scale 1
+    first.  Mels x 1e5 put the guard's scale below 1, so the launch's last workgroup re-writes the
+    image with that scale; the outputs must still match the oracle (relative bar as above)."""
+    sd = torch_state_dict(0)
+    x, co, ct = _case(B=32)
+    ref = _oracle(sd, x, co, ct)
+    ae = AutoEncoder(device=cuda_device, verbose=False)
+    ae.load_state_dict(sd)
+    ae.to(cuda_device).train()
+    xs = [torch.from_numpy(a).to(cuda_device) for a in (x, co, ct)]
+    with torch.no_grad():
+        outs = ae(*xs)
+    torch.cuda.synchronize()
+    for name, o, r in zip(("mel", "mel_post", "codes"), outs, ref):
+        o = o.cpu()
+        assert torch.isfinite(o).all(), name
+        rel = float((o - r).abs().max()) / float(r.abs().max())
+        print(f"frames x1e5, B=32: {name} max|d|/max|ref| {rel:.2e}")
+        assert rel <= 1e-4, name
+    ae.check_health()
