@@ -174,13 +174,14 @@ int generator_forward(avc_context* ctx, int T, int B, const float* const* P, con
   mark_range_checked(ctx, e1);  // an LSTM's h: |h| < 1
   AVC_TRY(bilstm_forward_impl(ctx, T, B, 64, 32, e1, 64, P + EL + 8, P + EL + 12, e2, 64, nullptr, nullptr,
                               nullptr, nullptr, s));
-  AVC_TRY(codes_from_encoder(T, B, e2, codes, s));
+  AVC_CHECK_ARG(T >= 32, "content codes need T >= 32 frames (model.py:99 cat of an empty list)");
 
-  // Upsample + decoder (model.py:115-127, decoder.py:58-79)
+  // Upsample + decoder (model.py:115-127, decoder.py:58-79); the content codes (model.py:94-99)
+  // are written by the same pass
   {  // the decoder input's embedding part is range-checked on the way (codes are LSTM outputs)
     unsigned* flags = host_flags(ctx);
     if (!flags) return AVC_ERR_HIP;
-    AVC_TRY(decoder_input(T, B, e2, 256, c_trg, din, s, flags + 1));
+    AVC_TRY(decoder_input(T, B, e2, 256, c_trg, din, s, flags + 1, codes));
     mark_range_checked(ctx, din);
   }
   const int D1 = P_DEC_LSTM1;

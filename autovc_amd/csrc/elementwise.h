@@ -52,8 +52,9 @@ int mel_from_frames(int T, int B, int cm, const float* fr, float* mel, hipStream
 int codes_from_encoder(int T, int B, const float* enc, float* codes, hipStream_t s);
 int codes_from_encoder_backward(int T, int B, const float* dcodes, float* denc, int accumulate,
                                 hipStream_t s);
+// codes (optional): also the content codes (codes_from_encoder's output), in the same pass
 int decoder_input(int T, int B, const float* enc, int ce, const float* ctrg, float* out,
-                  hipStream_t s, unsigned* range_flag = nullptr);
+                  hipStream_t s, unsigned* range_flag = nullptr, float* codes = nullptr);
 int decoder_input_backward(int T, int B, int ce, const float* dd, float* denc, int accumulate,
                            hipStream_t s);
 int overlap_average(int M, int C, int N, int step, const float* fr, float* out, hipStream_t s);

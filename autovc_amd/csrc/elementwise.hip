@@ -1152,6 +1152,45 @@ __global__ void decoder_input_kernel(int T, int B, const float* __restrict__ enc
   }
 }
 
+// decoder_input_kernel four channels per thread (C % 4 == 0), also writing the content codes where
+// `codes` is given (round 6: the whole-Generator forward's codes_kernel folded in -- each code
+// element is the decoder input's value at frame 32 i + 31 (forward stream) or 32 i (backward
+// stream), written by the one thread that reads it).  Same values as decoder_input_kernel and
+// codes_kernel.
+__global__ void decoder_input4_kernel(int T, int B, const float* __restrict__ enc, int ce,
+                                      const float* __restrict__ ctrg, float* __restrict__ out,
+                                      unsigned* __restrict__ range_flag, float* __restrict__ codes) {
+  const int C = 64 + ce, C4 = C >> 2, nA = T / 32, L = 32 * (nA + (T + 31) / 32);
+  const long total = (long)T * B * C4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C4;
+    const int c0 = 4 * (int)(i - r * C4), t = (int)(r / B), b = (int)(r - (long)t * B);
+    float4 v;
+    if (c0 < 32) {
+      const int blk = min(t / 32, nA - 1);
+      v = *reinterpret_cast<const float4*>(enc + ((long)(32 * blk + 31) * B + b) * 64 + c0);
+      if (codes && (t & 31) == 31 && t / 32 < nA)
+        *reinterpret_cast<float4*>(codes + (long)b * L + (t / 32) * 32 + c0) = v;
+    } else if (c0 < 64) {
+      v = *reinterpret_cast<const float4*>(enc + ((long)(32 * (t / 32)) * B + b) * 64 + c0);
+      if (codes && (t & 31) == 0)
+        *reinterpret_cast<float4*>(codes + (long)b * L + (nA + t / 32) * 32 + (c0 - 32)) = v;
+    } else {
+      v = *reinterpret_cast<const float4*>(ctrg + (long)b * ce + (c0 - 64));
+      if (range_flag) {  // (see decoder_input_kernel)
+        bool over = false;
+        over |= fabsf(v.x) >= 65504.f && fabsf(v.x) < __builtin_inff();
+        over |= fabsf(v.y) >= 65504.f && fabsf(v.y) < __builtin_inff();
+        over |= fabsf(v.z) >= 65504.f && fabsf(v.z) < __builtin_inff();
+        over |= fabsf(v.w) >= 65504.f && fabsf(v.w) < __builtin_inff();
+        if (over) __hip_atomic_store(range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    *reinterpret_cast<float4*>(out + r * C + c0) = v;
+  }
+}
+
 // one thread per (b, stream s in {fwd,bwd}, code index i, dim d)
 __global__ void decoder_input_bwd_kernel(int T, int B, int ce, const float* __restrict__ dd,
                                          float* __restrict__ denc) {
@@ -1712,8 +1751,16 @@ int codes_from_encoder_backward(int T, int B, const float* dcodes, float* denc, 
 }
 
 int decoder_input(int T, int B, const float* enc, int ce, const float* ctrg, float* out,
-                  hipStream_t s, unsigned* range_flag) {
+                  hipStream_t s, unsigned* range_flag, float* codes) {
   AVC_CHECK_ARG(T >= 32, "decoder input needs T >= 32 frames (model.py:115-119)");
+  const auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (ce % 4 == 0 && a16(enc) && a16(ctrg) && a16(out) && (!codes || a16(codes))) {
+    decoder_input4_kernel<<<ew_blocks((long)T * B * ((64 + ce) / 4)), 256, 0, s>>>(T, B, enc, ce, ctrg, out,
+                                                                                   range_flag, codes);
+    AVC_LAUNCH_CHECK();
+    return AVC_OK;
+  }
+  if (codes) AVC_TRY(codes_from_encoder(T, B, enc, codes, s));
   decoder_input_kernel<<<ew_blocks((long)T * B * (64 + ce)), 256, 0, s>>>(T, B, enc, ce, ctrg, out, range_flag);
   AVC_LAUNCH_CHECK();
   return AVC_OK;

@@ -1,4 +1,4 @@
-# frames split + range guard in one launch (frames_frag_guard_kernel, in-tree) against ab/r06f.so:
+# (round 6, last changes: the frames kernel, then codes folded into the decoder input) in-tree against ab/r06f.so:
 # range tests, GPU suite, bit-identity, C2 / C5 A/B
 export REF_WGRAD=1
 timeout -k 10 300 python -u -m pytest tests/test_gpu_range.py -q -s --timeout 120 --timeout-method thread -p no:cacheprovider 2>&1 | grep -E "x1e5|passed|failed"
