@@ -42,7 +42,8 @@ constexpr int BK = 32;
 // gemm16f issues the next K-tile's LDS-DMA over the first AVC_GEMM_DMA_SPREAD chunks of the current
 // one, between their fragment reads and MFMAs, instead of all DPW pieces right after the barrier
 // (round 6: 2 measured -2.4 % on the C2 conv, -2.5 % at C5; 4 less; the pieces after the chunk's
-// MFMAs, or interleaved with them by sched_group_barrier, no better; same bytes, same bits)
+// MFMAs, interleaved with them by sched_group_barrier, or starting at chunk 1, no better; same
+// bytes, same bits)
 #define AVC_GEMM_DMA_SPREAD 2
 #endif
 #ifndef AVC_GEMM_DIAG_NOKAHAN
@@ -1449,7 +1450,9 @@ __global__ __launch_bounds__(64 * WM * WN, OCC * WM * WN / 4) void gemm16f_kerne
     else                                                                                          \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)dst, 16, vo, sp_so, 0, 0); \
   }
-  constexpr int SPR = AVC_GEMM_DMA_SPREAD > 0 && AVC_GEMM_DMA_SPREAD <= KC && DPW % (AVC_GEMM_DMA_SPREAD > 0 ? AVC_GEMM_DMA_SPREAD : 1) == 0
+  // (every piece must be issued inside this K-tile's chunk loop: SPREAD <= KC, or the burst)
+  constexpr int SPR = AVC_GEMM_DMA_SPREAD > 0 && AVC_GEMM_DMA_SPREAD <= KC &&
+                              DPW % (AVC_GEMM_DMA_SPREAD > 0 ? AVC_GEMM_DMA_SPREAD : 1) == 0
                           ? AVC_GEMM_DMA_SPREAD : 0;
   bool sp_inside = false;
   unsigned char* sp_base = lds;
